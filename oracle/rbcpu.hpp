@@ -1,0 +1,120 @@
+// rbcpu — CPU ORACLE for the Roaring set-algebra hot path.
+//
+// TEST INFRASTRUCTURE ONLY.  This is a C++17 restatement of the Java reference
+// (luvk1412/RoaringBitmap @ 2025-02-27, read at /root/reference) used as the
+// parity checker.  Only tests/, __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg may load it.  The product engine (roaringbitmap_amd/) never
+// links, loads or calls anything in oracle/.
+//
+// Path prefixes used in citations:
+//   RB/  = RoaringBitmap/src/main/java/org/roaringbitmap/
+//
+// The Java reference cannot be compiled or run in this image (no JDK, see
+// DESIGN.md §Oracle).  Parity of this restatement is pinned by the reference's
+// own fixtures: the golden serialized files (testdata/bitmapwith{,out}runs.bin,
+// crashproneinput1..7.bin), the realdata known-answer constants
+// (jmh/src/test/.../realdata/*Test.java) and the container-type assertions of
+// RBT/TestContainer.java / TestRunContainer.java.  See tests/test_oracle_*.py.
+//
+// Every container operation restates the Java control flow of the cited
+// method, because the *result container type* (array / bitmap / run) and the
+// run layout are part of the serialized bytes and therefore of parity.
+#pragma once
+#include <cstdint>
+#include <cstddef>
+#include <string>
+#include <vector>
+
+namespace rbcpu {
+
+enum Kind : uint8_t { ARRAY = 0, BITMAP = 1, RUN = 2 };
+
+constexpr int kArrayMax = 4096;          // RB/ArrayContainer.java:27 DEFAULT_MAX_SIZE
+constexpr int kArrayLazyLowerBound = 1024;  // RB/ArrayContainer.java:25
+constexpr int kWords = 1024;             // RB/BitmapContainer.java:28 (1<<16)/64
+constexpr int kMaxCapacity = 1 << 16;    // RB/BitmapContainer.java:24
+constexpr int kRunVsArrayThreshold = 32; // RB/RunContainer.java:576,2412 "arbitrary_threshold"
+
+// One container.  A: `vals` sorted u16, `card` = size.  B: `words` (1024 u64),
+// `card` cached cardinality, -1 = lazy (RB/BitmapContainer.java:648-676).
+// R: `vals` interleaved (start, length-1) pairs (RB/RunContainer.java:92-99).
+struct Ctr {
+  Kind kind = ARRAY;
+  int card = 0;
+  std::vector<uint16_t> vals;
+  std::vector<uint64_t> words;
+
+  int nruns() const { return (int)(vals.size() / 2); }
+  int cardinality() const;                 // R: RB/RunContainer.java:1003-1009
+  bool empty() const;
+  bool full() const;                       // RB/RunContainer.java:1659-1661, BitmapContainer isFull
+  int array_size_bytes() const;            // getArraySizeInBytes (payload bytes)
+};
+
+// ---- container constructors / conversions ---------------------------------
+Ctr make_array(std::vector<uint16_t> v);
+Ctr make_bitmap_zero();
+Ctr run_full();                                      // RB/RunContainer.java:1663
+Ctr to_bitmap(const Ctr& c);                         // toBitmapContainer()
+Ctr bitmap_to_array(const Ctr& b);                   // BitmapContainer.toArrayContainer
+Ctr to_efficient(const Ctr& r);                      // RB/RunContainer.java:2326-2335
+Ctr to_bitmap_or_array(const Ctr& r, int card);      // RB/RunContainer.java:2300-2323
+Ctr repair_after_lazy(const Ctr& c);                 // A: this, B: :1205-1215, R: EFF
+Ctr run_optimize(const Ctr& c);                      // A :1085-1099, B :1218-1237, R :2083
+int number_of_runs(const Ctr& c);                    // exact run count of the set
+
+// ---- pairwise container ops (Container.and/or/xor/andNot dispatch) --------
+Ctr c_and(const Ctr& a, const Ctr& b);               // RB/Container.java:81-88
+Ctr c_or(const Ctr& a, const Ctr& b);                // RB/Container.java:822-829
+Ctr c_xor(const Ctr& a, const Ctr& b);               // RB/Container.java:964-971
+Ctr c_andnot(const Ctr& a, const Ctr& b);            // RB/Container.java:164-171
+int c_and_card(const Ctr& a, const Ctr& b);          // RB/Container.java:113-126
+bool c_intersects(const Ctr& a, const Ctr& b);
+// in-place variants used by the FastAggregation chains
+Ctr c_iand(const Ctr& a, const Ctr& b);              // RB/Container.java:459-466
+Ctr c_ixor(const Ctr& a, const Ctr& b);              // RB/Container.java:688-695
+Ctr b_ilazyor(const Ctr& lazy_bitmap, const Ctr& x); // RB/BitmapContainer.java:648-676
+Ctr b_lazy_iand(const Ctr& lazy_bitmap, const Ctr& x); // RB/BitmapContainer.java:523-599 lazy branches
+
+// ---- bitmaps ---------------------------------------------------------------
+struct Bitmap {
+  std::vector<uint16_t> keys;
+  std::vector<Ctr> ctrs;
+  size_t size() const { return keys.size(); }
+  int64_t long_card() const;
+  int32_t card() const { return (int32_t)(uint32_t)(uint64_t)long_card(); }
+};
+
+Bitmap bitmap_of(const uint32_t* vals, size_t n);    // RoaringBitmap.bitmapOf via addN (BY_CARD)
+void bitmap_run_optimize(Bitmap& b);                 // RB/RoaringBitmap.java:2764-2774
+std::vector<uint32_t> bitmap_values(const Bitmap& b);
+
+// static pairwise ops, RB/RoaringBitmap.java
+Bitmap op_and(const Bitmap& x1, const Bitmap& x2);        // :377-401
+Bitmap op_or(const Bitmap& x1, const Bitmap& x2);         // :860-902
+Bitmap op_xor(const Bitmap& x1, const Bitmap& x2);        // :1071-1118
+Bitmap op_andnot(const Bitmap& x1, const Bitmap& x2);     // :444-473
+int32_t op_and_card(const Bitmap& x1, const Bitmap& x2);  // :413-434
+int32_t op_or_card(const Bitmap& x1, const Bitmap& x2);   // :916-920
+int32_t op_xor_card(const Bitmap& x1, const Bitmap& x2);  // :931-933
+int32_t op_andnot_card(const Bitmap& x1, const Bitmap& x2); // :944-985
+bool op_intersects(const Bitmap& x1, const Bitmap& x2);   // :698-720
+
+// FastAggregation, RB/FastAggregation.java.  `ids` carries Java object
+// identity (naive_and skips `bitmaps[k] != smallest` by reference, :341):
+// two inputs with equal id are the same object.  nullptr = all distinct.
+Bitmap fa_or(const std::vector<const Bitmap*>& bms);                        // :653-666 -> naive_or :603-610
+Bitmap fa_and(const std::vector<const Bitmap*>& bms, const int* ids);       // :37-42
+Bitmap fa_and_iter(const std::vector<const Bitmap*>& bms);                  // :26-28 -> naive_and(Iterator) :304-313
+Bitmap fa_xor(const std::vector<const Bitmap*>& bms);                       // :823-836 -> naive_xor :621-644
+Bitmap fa_naive_and(const std::vector<const Bitmap*>& bms, const int* ids); // :328-346
+Bitmap fa_workshy_and(const std::vector<const Bitmap*>& bms);               // :356-414
+int32_t fa_and_card(const std::vector<const Bitmap*>& bms);                 // :71-82
+int32_t fa_or_card(const std::vector<const Bitmap*>& bms);                  // :90-101
+
+// ---- portable format, RB/RoaringArray.java ---------------------------------
+enum Status : int { OK = 0, ERR_FORMAT = -1, ERR_TRUNCATED = -2, ERR_ARG = -3 };
+std::vector<uint8_t> serialize(const Bitmap& b);                            // :896-940
+int deserialize(const uint8_t* p, size_t n, Bitmap* out, size_t* consumed); // :547-629
+
+}  // namespace rbcpu

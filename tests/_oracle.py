@@ -1,0 +1,168 @@
+"""ctypes binding to the CPU ORACLE (oracle/build/librbcpu.so) — test infrastructure.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "build", "librbcpu.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+        L = ctypes.CDLL(LIB_PATH)
+        u8p = ctypes.POINTER(ctypes.c_uint8)
+        L.rbo_free.argtypes = [ctypes.c_void_p]
+        L.rbo_pairwise.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                   ctypes.c_size_t, ctypes.POINTER(u8p),
+                                   ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_pairwise_card.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                        ctypes.c_char_p, ctypes.c_size_t,
+                                        ctypes.POINTER(ctypes.c_int32)]
+        L.rbo_wide.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                               ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
+                               ctypes.POINTER(ctypes.c_int), ctypes.POINTER(u8p),
+                               ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_wide_card.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_int32)]
+        L.rbo_from_values.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t, ctypes.c_int,
+                                      ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_run_optimize.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(u8p),
+                                       ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_to_values.argtypes = [ctypes.c_char_p, ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)),
+                                    ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_roundtrip.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(u8p),
+                                    ctypes.POINTER(ctypes.c_size_t),
+                                    ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_stats.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64)]
+        L.rbo_time_pairwise.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                                        ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+        L.rbo_time_pairwise.restype = ctypes.c_double
+        L.rbo_time_wide.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_int]
+        L.rbo_time_wide.restype = ctypes.c_double
+        _lib = L
+    return _lib
+
+
+class OracleError(Exception):
+    def __init__(self, status):
+        super().__init__(f"oracle status {status}")
+        self.status = status
+
+
+def _take(p, n):
+    out = ctypes.string_at(p, n.value)
+    lib().rbo_free(p)
+    return out
+
+
+def _check(st):
+    if st != 0:
+        raise OracleError(st)
+
+
+OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3}
+CARD_OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
+WIDE_OPS = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5}
+
+
+def pairwise(op, a: bytes, b: bytes) -> bytes:
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_pairwise(OPS[op], a, len(a), b, len(b), ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
+
+
+def pairwise_card(op, a: bytes, b: bytes) -> int:
+    out = ctypes.c_int32()
+    _check(lib().rbo_pairwise_card(CARD_OPS[op], a, len(a), b, len(b), ctypes.byref(out)))
+    return out.value
+
+
+def _bufs(bufs):
+    arr = (ctypes.c_char_p * max(len(bufs), 1))(*bufs)
+    lens = (ctypes.c_size_t * max(len(bufs), 1))(*[len(b) for b in bufs])
+    return arr, lens
+
+
+def wide(op, bufs, ids=None) -> bytes:
+    arr, lens = _bufs(bufs)
+    idp = None
+    if ids is not None:
+        idp = (ctypes.c_int * len(ids))(*ids)
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_wide(WIDE_OPS[op], arr, lens, len(bufs), idp, ctypes.byref(p),
+                          ctypes.byref(n)))
+    return _take(p, n)
+
+
+def wide_card(op, bufs) -> int:
+    arr, lens = _bufs(bufs)
+    out = ctypes.c_int32()
+    _check(lib().rbo_wide_card({"and": 0, "or": 1}[op], arr, lens, len(bufs), ctypes.byref(out)))
+    return out.value
+
+
+def from_values(values, run_optimize=False) -> bytes:
+    v = np.ascontiguousarray(np.asarray(values, dtype=np.uint32))
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_from_values(v.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), v.size,
+                                 int(run_optimize), ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
+
+
+def run_optimize(buf: bytes) -> bytes:
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_run_optimize(buf, len(buf), ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
+
+
+def to_values(buf: bytes) -> np.ndarray:
+    p = ctypes.POINTER(ctypes.c_uint32)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_to_values(buf, len(buf), ctypes.byref(p), ctypes.byref(n)))
+    out = np.ctypeslib.as_array(p, shape=(n.value,)).copy() if n.value else np.zeros(0, np.uint32)
+    lib().rbo_free(p)
+    return out
+
+
+def roundtrip(buf: bytes):
+    """Returns (status, bytes, consumed)."""
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    used = ctypes.c_size_t()
+    st = lib().rbo_roundtrip(buf, len(buf), ctypes.byref(p), ctypes.byref(n), ctypes.byref(used))
+    if st != 0:
+        return st, None, 0
+    return 0, _take(p, n), used.value
+
+
+def stats(buf: bytes):
+    s = (ctypes.c_int64 * 5)()
+    _check(lib().rbo_stats(buf, len(buf), s))
+    return {"array": s[0], "bitmap": s[1], "run": s[2], "card": s[3], "payload": s[4]}
+
+
+def time_pairwise(op, a, b, reps):
+    code = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "and_card": 4}[op]
+    return lib().rbo_time_pairwise(code, a, len(a), b, len(b), reps)
+
+
+def time_wide(op, bufs, reps):
+    arr, lens = _bufs(bufs)
+    return lib().rbo_time_wide({"and": 0, "or": 1, "xor": 2}[op], arr, lens, len(bufs), reps)
