@@ -1,0 +1,183 @@
+/*
+ * roaring_mi355x.h — C ABI of the MI355X Roaring set-algebra engine.
+ *
+ * Drop-in boundary for the reference's data-parallel hot path
+ * (luvk1412/RoaringBitmap, Java; RB/ = RoaringBitmap/src/main/java/org/roaringbitmap/).
+ * The reference has no native boundary, so each entry point below is what a
+ * JNI shim for the cited static Java method binds.
+ *
+ * Data contract
+ *   - Bitmaps cross the boundary in the portable serialized format
+ *     (RB/RoaringArray.java:896-940 serialize, :547-629 deserialize), exactly the
+ *     bytes of RoaringBitmap.serialize(ByteBuffer) or an ImmutableRoaringBitmap's
+ *     mapped buffer.  Outputs are the bytes RoaringBitmap.serialize would write
+ *     for the reference's result object, including its array/bitmap/run
+ *     container choice, so RoaringBitmap.deserialize(out) == reference result.
+ *   - Inputs are borrowed, read-only, caller-owned, valid for the call.
+ *   - Outputs (rbg_buffer) are allocated by the library; release with rbg_free.
+ *   - All calls are reentrant.  Concurrent calls from different threads each use
+ *     their own HIP stream and workspace (thread-local device context).
+ *   - Every compute entry point runs on the GPU.  If no HIP device is usable the
+ *     call returns RBG_ERR_DEVICE; there is no CPU fallback.
+ *
+ * Status codes map 1:1 to the reference's exceptions.
+ */
+#ifndef ROARING_MI355X_H
+#define ROARING_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RBG_OK 0
+/* InvalidRoaringFormat -> IOException: bad cookie or size > 65536
+ * (RB/RoaringArray.java:279-288,553-566; RB/RoaringBitmap.java:1779-1811).
+ * Also returned for a negative container count (Java NegativeArraySizeException)
+ * and for keys that are not strictly increasing (the reference does not check
+ * this; such input is outside the format spec). */
+#define RBG_ERR_INVALID_FORMAT (-1)
+/* EOFException / BufferUnderflowException on truncated input
+ * (RBT/TestAdversarialInputs.java:50-55). */
+#define RBG_ERR_TRUNCATED (-2)
+/* IllegalArgumentException (e.g. aggregation buffer < 1024 longs,
+ * RB/FastAggregation.java:52-54) or a bad op code / null pointer. */
+#define RBG_ERR_ILLEGAL_ARGUMENT (-3)
+/* HIP runtime failure or no usable gfx950 device. */
+#define RBG_ERR_DEVICE (-4)
+#define RBG_ERR_OUT_OF_MEMORY (-5)
+
+typedef struct rbg_buffer {
+  uint8_t* data;
+  size_t len;
+} rbg_buffer;
+
+/* pairwise ops: RB/RoaringBitmap.java and :377, or :860, xor :1071, andNot :444 */
+enum { RBG_AND = 0, RBG_OR = 1, RBG_XOR = 2, RBG_ANDNOT = 3 };
+/* cardinality ops: andCardinality :413, orCardinality :916, xorCardinality :931,
+ * andNotCardinality :944 (all Java int, wrapping mod 2^32), intersects :698 (0/1) */
+enum { RBG_CARD_AND = 0, RBG_CARD_OR = 1, RBG_CARD_XOR = 2, RBG_CARD_ANDNOT = 3, RBG_INTERSECTS = 4 };
+/* wide ops, RB/FastAggregation.java:
+ *   RBG_WIDE_AND      and(RoaringBitmap...)  :37-42  (N>10 workShyAnd, else naive_and)
+ *   RBG_WIDE_OR       or(RoaringBitmap...)   :664-666 (naive_or); also RoaringBitmap.or(...) :844
+ *   RBG_WIDE_XOR      xor(RoaringBitmap...)  :834-836 (naive_xor)
+ *   RBG_WIDE_AND_ITER and(Iterator)          :26-28  (naive_and over an iterator)
+ *   RBG_WIDE_NAIVE_AND   naive_and(RoaringBitmap...) :328-346 for any N
+ *   RBG_WIDE_WORKSHY_AND workShyAnd(long[], RoaringBitmap...) :356-414 for any N >= 1 */
+enum { RBG_WIDE_AND = 0, RBG_WIDE_OR = 1, RBG_WIDE_XOR = 2, RBG_WIDE_AND_ITER = 3, RBG_WIDE_NAIVE_AND = 4,
+       RBG_WIDE_WORKSHY_AND = 5 };
+/* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
+enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
+
+/* static RoaringBitmap.and/or/xor/andNot(RoaringBitmap, RoaringBitmap) -> RoaringBitmap */
+int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len,
+                 rbg_buffer* out);
+
+/* static RoaringBitmap.{and,or,xor,andNot}Cardinality / intersects -> int */
+int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len,
+                      int32_t* out);
+
+/* FastAggregation.and/or/xor.  `ids` (may be NULL) carries Java object identity:
+ * inputs with equal id are the same RoaringBitmap object (naive_and skips
+ * `bitmaps[k] != smallest` by reference, RB/FastAggregation.java:341).
+ * n == 0 yields the empty bitmap (:329-331). */
+int rbg_wide(int op, const uint8_t* const* bufs, const size_t* lens, const int32_t* ids, size_t n,
+             rbg_buffer* out);
+
+/* FastAggregation.andCardinality / orCardinality(RoaringBitmap...) -> int */
+int rbg_wide_card(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out);
+
+/* Batched andCardinality: out[i] = RoaringBitmap.andCardinality(a_i, b_i).  No reference
+ * signature; defined as a loop of RB/RoaringBitmap.java:413-434 (config C4). */
+int rbg_batch_and_card(size_t n_pairs, const uint8_t* const* a_bufs, const size_t* a_lens,
+                       const uint8_t* const* b_bufs, const size_t* b_lens, int32_t* out);
+
+void rbg_free(rbg_buffer* buf);
+
+/* Select the HIP devices the one-shot calls may use (bit i = device i).  Returns the
+ * number of usable devices selected, or RBG_ERR_DEVICE. */
+int rbg_set_devices(uint64_t mask);
+
+/* Human-readable message for the last error on this thread. */
+const char* rbg_last_error(void);
+int rbg_version(void);
+
+/* ---- host-side format utilities (construction, not the hot path) ----------------
+ * RoaringBitmap.bitmapOf(int...) (RB/RoaringBitmap.java:566-570) optionally followed
+ * by runOptimize() (:2764-2774); values need not be sorted or distinct. */
+int rbg_from_values(const uint32_t* values, size_t n, int run_optimize, rbg_buffer* out);
+/* RoaringBitmap.runOptimize() on a serialized bitmap. */
+int rbg_run_optimize(const uint8_t* buf, size_t len, rbg_buffer* out);
+/* RoaringBitmap.toArray(): ascending values (unsigned); out->data holds n*4 bytes. */
+int rbg_to_values(const uint8_t* buf, size_t len, rbg_buffer* out);
+/* Validate a serialized bitmap; returns bytes consumed, long cardinality and the
+ * container mix (stats[0..2] = #array, #bitmap, #run). */
+int rbg_inspect(const uint8_t* buf, size_t len, size_t* consumed, int64_t* cardinality,
+                int64_t* stats3);
+
+/* ---- device-resident session API (bench.py, torch integration) ------------------
+ * A context owns one HIP stream and a workspace on one device.  Batches are
+ * device-resident sets of bitmaps in the engine's key-major arena layout
+ * (DESIGN.md §Data layout).  Ops on a context are enqueued asynchronously on its
+ * stream; rbg_ctx_sync waits. */
+typedef struct rbg_ctx rbg_ctx;
+int rbg_ctx_create(int device, rbg_ctx** out);
+void rbg_ctx_destroy(rbg_ctx* ctx);
+/* hipStream_t of the context, for HIP-event timing by the caller */
+void* rbg_ctx_stream(rbg_ctx* ctx);
+int rbg_ctx_sync(rbg_ctx* ctx);
+
+/* Parse + upload n serialized bitmaps as one batch; returns a batch id >= 0. */
+int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n,
+                 int32_t* batch);
+/* Synthetic batches generated on the device (bench configs).
+ *   kind 0: C2 operand: one bitmap, all 65536 keys, per key A/B/R with p=1/3 (seed)
+ *   kind 1: C3 uniform: n bitmaps x keys [key_lo,key_hi), ~15.26 values per (bitmap,key)
+ *   kind 2: C3 clustered: n bitmaps, 16 dense bitmap keys each, restricted to [key_lo,key_hi)
+ *   kind 3: C4 pairs: n bitmaps (2 per pair), 1-4 array keys in [0,64) each */
+int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi,
+                  int32_t* batch);
+int rbg_ctx_release(rbg_ctx* ctx, int32_t batch);
+/* Batch facts: stats[0..7] = bitmaps, containers, #array, #bitmap, #run, payload bytes,
+ * long cardinality, serialized bytes. (synchronous) */
+int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* stats8);
+/* Download bitmap i of a batch as serialized bytes (synchronous). */
+int rbg_ctx_batch_fetch(rbg_ctx* ctx, int32_t batch, size_t i, rbg_buffer* out);
+
+/* Enqueue a pairwise op between bitmap ia of batch a and bitmap ib of batch b; the
+ * serialized result stays in the context's result buffer on the device. */
+int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
+/* Enqueue a cardinality op; the int32 lands in device memory, read by rbg_ctx_card. */
+int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
+/* Enqueue a wide op over every bitmap of a batch, restricted to keys [key_lo, key_hi)
+ * (key-range sharding; use 0, 65536 for the whole universe).  The chain-order
+ * decisions of FastAggregation (smallest input, identity skips) use `ids` as in
+ * rbg_wide (may be NULL). */
+int rbg_ctx_wide(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, const int32_t* ids);
+int rbg_ctx_wide_card(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi);
+/* Enqueue batched andCardinality over pairs (2i, 2i+1) of a batch; results stay on device. */
+int rbg_ctx_batch_and_card(rbg_ctx* ctx, int32_t batch);
+
+/* Result access (synchronous). */
+int rbg_ctx_card(rbg_ctx* ctx, int32_t* out);
+int rbg_ctx_cards(rbg_ctx* ctx, int32_t* out, size_t n);
+/* stats[0..3] = containers, payload bytes, has_run, long cardinality of the last
+ * result (before header).  Used for the cross-shard allgather. */
+int rbg_ctx_result_stats(rbg_ctx* ctx, int64_t* stats4);
+/* Serialized bytes of the last result (a standalone portable bitmap). */
+int rbg_ctx_fetch(rbg_ctx* ctx, rbg_buffer* out);
+/* Key-range shard assembly: write this shard's descriptors / offsets / payloads into
+ * a global serialized bitmap whose header is described by (total containers,
+ * has_run, this shard's first container index, this shard's payload byte offset
+ * within the global payload region).  Returns this shard's byte slices:
+ * out_desc (descriptors), out_offsets (offset table, may be empty), out_payload. */
+int rbg_ctx_fetch_shard(rbg_ctx* ctx, int64_t total_containers, int has_run,
+                        int64_t first_container, int64_t payload_base, rbg_buffer* out_desc,
+                        rbg_buffer* out_offsets, rbg_buffer* out_payload);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ROARING_MI355X_H */

@@ -1,0 +1,14 @@
+"""MI355X-native engine for the Roaring bitmap set-algebra hot path.
+
+Drop-in for luvk1412/RoaringBitmap's pairwise static ops and FastAggregation's
+wide or/and/xor.  Bitmaps travel in the portable serialized
+format; every op runs in hand-written gfx950 HIP kernels behind the C ABI of
+include/roaring_mi355x.h.
+"""
+from ._lib import (DeviceError, IllegalArgumentException, InvalidRoaringFormat, RoaringError,  # noqa: F401
+                   TruncatedInput)
+from .engine import Engine  # noqa: F401
+from .roaring import FastAggregation, RoaringBitmap, batch_and_cardinality  # noqa: F401
+
+__all__ = ["RoaringBitmap", "FastAggregation", "Engine", "batch_and_cardinality", "InvalidRoaringFormat",
+           "TruncatedInput", "IllegalArgumentException", "DeviceError", "RoaringError"]

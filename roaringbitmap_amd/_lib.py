@@ -1,0 +1,140 @@
+"""ctypes binding of libroaring_mi355x.so (include/roaring_mi355x.h).
+
+The library is built in-tree (roaringbitmap_amd/_build.py).  There is no CPU
+fallback: if the shared object is missing this module raises at import time,
+and every compute call returns RBG_ERR_DEVICE when no gfx950 device is present.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libroaring_mi355x.so")
+
+RBG_OK = 0
+RBG_ERR_INVALID_FORMAT = -1
+RBG_ERR_TRUNCATED = -2
+RBG_ERR_ILLEGAL_ARGUMENT = -3
+RBG_ERR_DEVICE = -4
+RBG_ERR_OUT_OF_MEMORY = -5
+
+OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3}
+CARD_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
+WIDE_OP = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5}
+WIDE_CARD_OP = {"and": 0, "or": 1}
+
+
+class rbg_buffer(ctypes.Structure):
+    _fields_ = [("data", ctypes.POINTER(ctypes.c_uint8)), ("len", ctypes.c_size_t)]
+
+
+EXPORTED = [
+    "rbg_pairwise", "rbg_pairwise_card", "rbg_wide", "rbg_wide_card", "rbg_batch_and_card", "rbg_free",
+    "rbg_set_devices", "rbg_last_error", "rbg_version", "rbg_from_values", "rbg_run_optimize",
+    "rbg_to_values", "rbg_inspect", "rbg_ctx_create", "rbg_ctx_destroy", "rbg_ctx_stream", "rbg_ctx_sync",
+    "rbg_ctx_load", "rbg_ctx_synth", "rbg_ctx_release", "rbg_ctx_batch_stats", "rbg_ctx_batch_fetch",
+    "rbg_ctx_pairwise", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
+    "rbg_ctx_batch_and_card", "rbg_ctx_card", "rbg_ctx_cards", "rbg_ctx_result_stats", "rbg_ctx_fetch",
+    "rbg_ctx_fetch_shard",
+]
+
+_lib = None
+
+
+def _declare(L):
+    P = ctypes.POINTER
+    u8p = ctypes.c_char_p
+    sz = ctypes.c_size_t
+    buf = P(rbg_buffer)
+    i32 = ctypes.c_int32
+    vp = ctypes.c_void_p
+    L.rbg_pairwise.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, buf]
+    L.rbg_pairwise_card.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, P(i32)]
+    L.rbg_wide.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), P(i32), sz, buf]
+    L.rbg_wide_card.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), sz, P(i32)]
+    L.rbg_batch_and_card.argtypes = [sz, P(ctypes.c_char_p), P(sz), P(ctypes.c_char_p), P(sz), P(i32)]
+    L.rbg_free.argtypes = [buf]
+    L.rbg_free.restype = None
+    L.rbg_set_devices.argtypes = [ctypes.c_uint64]
+    L.rbg_last_error.restype = ctypes.c_char_p
+    L.rbg_from_values.argtypes = [P(ctypes.c_uint32), sz, ctypes.c_int, buf]
+    L.rbg_run_optimize.argtypes = [u8p, sz, buf]
+    L.rbg_to_values.argtypes = [u8p, sz, buf]
+    L.rbg_inspect.argtypes = [u8p, sz, P(sz), P(ctypes.c_int64), P(ctypes.c_int64)]
+    L.rbg_ctx_create.argtypes = [ctypes.c_int, P(vp)]
+    L.rbg_ctx_destroy.argtypes = [vp]
+    L.rbg_ctx_destroy.restype = None
+    L.rbg_ctx_stream.argtypes = [vp]
+    L.rbg_ctx_stream.restype = vp
+    L.rbg_ctx_sync.argtypes = [vp]
+    L.rbg_ctx_load.argtypes = [vp, P(ctypes.c_char_p), P(sz), sz, P(i32)]
+    L.rbg_ctx_synth.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, sz, ctypes.c_int, ctypes.c_int, P(i32)]
+    L.rbg_ctx_release.argtypes = [vp, i32]
+    L.rbg_ctx_batch_stats.argtypes = [vp, i32, P(ctypes.c_int64)]
+    L.rbg_ctx_batch_fetch.argtypes = [vp, i32, sz, buf]
+    L.rbg_ctx_pairwise.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz]
+    L.rbg_ctx_pairwise_card.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz]
+    L.rbg_ctx_wide.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int, P(i32)]
+    L.rbg_ctx_wide_card.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int]
+    L.rbg_ctx_batch_and_card.argtypes = [vp, i32]
+    L.rbg_ctx_card.argtypes = [vp, P(i32)]
+    L.rbg_ctx_cards.argtypes = [vp, P(i32), sz]
+    L.rbg_ctx_result_stats.argtypes = [vp, P(ctypes.c_int64)]
+    L.rbg_ctx_fetch.argtypes = [vp, buf]
+    L.rbg_ctx_fetch_shard.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, buf, buf,
+                                      buf]
+
+
+def lib():
+    """Load the engine library; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(the engine has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+class RoaringError(Exception):
+    pass
+
+
+class InvalidRoaringFormat(RoaringError, OSError):
+    """RB/InvalidRoaringFormat.java surfaced as IOException (RB/RoaringBitmap.java:1779-1811)."""
+
+
+class TruncatedInput(RoaringError, OSError):
+    """EOFException / BufferUnderflowException on a truncated buffer."""
+
+
+class IllegalArgumentException(RoaringError, ValueError):
+    pass
+
+
+class DeviceError(RoaringError, RuntimeError):
+    pass
+
+
+def check(status):
+    if status >= 0:
+        return status
+    msg = lib().rbg_last_error().decode(errors="replace")
+    cls = {RBG_ERR_INVALID_FORMAT: InvalidRoaringFormat, RBG_ERR_TRUNCATED: TruncatedInput,
+           RBG_ERR_ILLEGAL_ARGUMENT: IllegalArgumentException}.get(status, DeviceError)
+    raise cls(f"status {status}: {msg}")
+
+
+def take(b: rbg_buffer) -> bytes:
+    out = ctypes.string_at(b.data, b.len) if b.len else b""
+    lib().rbg_free(ctypes.byref(b))
+    return out
+
+
+def buf_array(bufs):
+    n = len(bufs)
+    arr = (ctypes.c_char_p * max(n, 1))(*bufs)
+    lens = (ctypes.c_size_t * max(n, 1))(*[len(b) for b in bufs])
+    return arr, lens

@@ -1,0 +1,433 @@
+// Device-side building blocks shared by every engine kernel (gfx950, wave64).
+//
+// A workgroup of NT = 256 threads (4 waves) owns one 65536-bit container at a
+// time.  Thread t holds four u64 words of it in registers:
+//     w0 = word 2t, w1 = word 2t+1        (first half, bytes [16t, 16t+16))
+//     w2 = word 512+2t, w3 = word 513+2t  (second half, bytes [4096+16t, ...))
+// so a bitmap container streams from HBM as two perfectly coalesced 16-byte
+// loads per lane (1 KiB per wave instruction), and LDS copies of it are read
+// conflict-free with ds_read_b128.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace rbg {
+
+constexpr int NT = 256;
+constexpr int kSlotBytes = 8208;  // max serialized payload (8194) rounded to 16
+
+enum DKind : uint8_t { DK_A = 0, DK_B = 1, DK_R = 2 };
+
+// Input container descriptor (16 B).  Slot layout in the payload arena:
+//   A: u16 values at +0 | B: 1024 u64 words at +0 | R: [u16 pad][u16 nruns][u32 pairs]
+// The portable-format payload bytes of a container start at slot + (R ? 2 : 0).
+struct __align__(16) CDesc {
+  uint64_t slot;
+  uint32_t card;  // 1..65536 (header cardinality)
+  uint16_t key;
+  uint8_t kind;
+  uint8_t flags;
+};
+
+// Output container descriptor (32 B) produced by an op, consumed by the emitter.
+struct __align__(16) ODesc {
+  uint64_t src;      // device address of the serialized payload bytes
+  uint32_t ser_len;  // serialized payload length
+  uint32_t card;
+  uint16_t key;
+  uint8_t kind;
+  uint8_t keep;
+  uint32_t pad0;
+  uint64_t pad1;
+};
+
+struct Task {
+  uint32_t key;
+  int32_t a;  // pairwise: container index in operand A (-1 absent); wide: segment start
+  int32_t b;  // pairwise: container index in operand B (-1 absent); wide: segment length
+  int32_t aux;
+};
+
+struct ResultInfo {
+  uint32_t n_out;
+  uint32_t has_run;
+  uint64_t header;    // header bytes
+  uint64_t payload;   // payload bytes
+  uint64_t total;     // header + payload
+  int64_t long_card;  // sum of result cardinalities (64-bit)
+  uint32_t card32;    // Java int (mod 2^32)
+  uint32_t any;       // nonzero iff some task had a non-empty result
+};
+
+__device__ __forceinline__ int popc64(uint64_t x) { return __popcll(x); }
+
+__device__ __forceinline__ int by_card(int c) { return c <= 4096 ? DK_A : DK_B; }
+// RunContainer.toEfficientContainer (RB/RunContainer.java:2326-2335)
+__device__ __forceinline__ int eff(int c, int r) {
+  const int run_sz = 2 + 4 * r;
+  const int arr_sz = 2 + 2 * c;
+  return run_sz <= min(8192, arr_sz) ? DK_R : by_card(c);
+}
+
+// ---------------------------------------------------------------------------
+// wave / block reductions and scans
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// Sum of (a, b) over the workgroup; `sh` needs 8 ints.  Ends with a barrier.
+__device__ __forceinline__ void block_sum2(int& a, int& b, int* sh) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sh[w] = a;
+    sh[4 + w] = b;
+  }
+  __syncthreads();
+  a = sh[0] + sh[1] + sh[2] + sh[3];
+  b = sh[4] + sh[5] + sh[6] + sh[7];
+  __syncthreads();
+}
+
+// Exclusive scan in word order (first halves of threads 0..255, then second
+// halves).  v0 counts for words {2t, 2t+1}, v1 for {512+2t, 513+2t}.
+__device__ __forceinline__ void block_scan_halves(int v0, int v1, int& p0, int& p1, int& total,
+                                                  int* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int s0 = wave_incl_scan(v0), s1 = wave_incl_scan(v1);
+  if (lane == 63) {
+    sh[w] = s0;
+    sh[4 + w] = s1;
+  }
+  __syncthreads();
+  int o0 = 0, o1 = 0, t0 = 0, t1 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int x = sh[i], y = sh[4 + i];
+    if (i < w) {
+      o0 += x;
+      o1 += y;
+    }
+    t0 += x;
+    t1 += y;
+  }
+  p0 = o0 + s0 - v0;
+  p1 = t0 + o1 + s1 - v1;
+  total = t0 + t1;
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// 8 KiB LDS bitmaps (u32 words) and register-resident containers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lds_clear(uint32_t* lds) {
+  uint4* p = reinterpret_cast<uint4*>(lds);
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  p[threadIdx.x] = z;
+  p[threadIdx.x + NT] = z;
+}
+
+__device__ __forceinline__ void lds_fill_ones(uint32_t* lds) {
+  uint4* p = reinterpret_cast<uint4*>(lds);
+  const uint4 o = make_uint4(~0u, ~0u, ~0u, ~0u);
+  p[threadIdx.x] = o;
+  p[threadIdx.x + NT] = o;
+}
+
+__device__ __forceinline__ void u4_to_words(const uint4 v, uint64_t& lo, uint64_t& hi) {
+  lo = (uint64_t)v.x | ((uint64_t)v.y << 32);
+  hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+}
+__device__ __forceinline__ uint4 words_to_u4(uint64_t lo, uint64_t hi) {
+  return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+// owned words from an LDS bitmap
+__device__ __forceinline__ void lds_read_owned(const uint32_t* lds, uint64_t r[4]) {
+  const uint4* p = reinterpret_cast<const uint4*>(lds);
+  u4_to_words(p[threadIdx.x], r[0], r[1]);
+  u4_to_words(p[threadIdx.x + NT], r[2], r[3]);
+}
+__device__ __forceinline__ void lds_write_owned(uint32_t* lds, const uint64_t r[4]) {
+  uint4* p = reinterpret_cast<uint4*>(lds);
+  p[threadIdx.x] = words_to_u4(r[0], r[1]);
+  p[threadIdx.x + NT] = words_to_u4(r[2], r[3]);
+}
+// owned words of a bitmap container in global memory (two 16 B loads per lane)
+__device__ __forceinline__ void load_bitmap_owned(const uint8_t* words, uint64_t r[4]) {
+  const uint4* p = reinterpret_cast<const uint4*>(words);
+  u4_to_words(p[threadIdx.x], r[0], r[1]);
+  u4_to_words(p[threadIdx.x + NT], r[2], r[3]);
+}
+__device__ __forceinline__ void store_bitmap_owned(uint8_t* words, const uint64_t r[4]) {
+  uint4* p = reinterpret_cast<uint4*>(words);
+  p[threadIdx.x] = words_to_u4(r[0], r[1]);
+  p[threadIdx.x + NT] = words_to_u4(r[2], r[3]);
+}
+
+// OR the sorted u16 values of an array container into an LDS bitmap
+// (cooperative over the workgroup; vals is 16 B aligned, reads stay in the slot).
+template <int MODE = 0>  // 0: or, 1: xor
+__device__ __forceinline__ void lds_scatter_array(uint32_t* lds, const uint16_t* vals, int card) {
+  const int nvec = (card + 7) >> 3;
+  const uint4* v4 = reinterpret_cast<const uint4*>(vals);
+  for (int i = threadIdx.x; i < nvec; i += NT) {
+    const uint4 v = v4[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const int base = i * 8;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (base + j < card) {
+        const uint32_t x = (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFF;
+        if (MODE == 0) atomicOr(&lds[x >> 5], 1u << (x & 31));
+        else atomicXor(&lds[x >> 5], 1u << (x & 31));
+      }
+    }
+  }
+}
+
+// OR one run [s, e] (inclusive) into LDS words, single thread.
+__device__ __forceinline__ void lds_or_run_serial(uint32_t* lds, int s, int e) {
+  const int ws = s >> 5, we = e >> 5;
+  const uint32_t first = ~0u << (s & 31);
+  const uint32_t last = ~0u >> (31 - (e & 31));
+  if (ws == we) {
+    atomicOr(&lds[ws], first & last);
+    return;
+  }
+  atomicOr(&lds[ws], first);
+  for (int w = ws + 1; w < we; w++) lds[w] = ~0u;  // no other run of this pass owns w
+  atomicOr(&lds[we], last);
+}
+
+// OR the runs of a run container into an LDS bitmap.  Short runs are filled by
+// one thread each; runs longer than 8 words are queued and filled by the whole
+// workgroup so a single long run does not serialise one lane.  `q` needs 257
+// ints of LDS.  Must be called by all threads; ends with a barrier.
+__device__ __forceinline__ void lds_or_runs(uint32_t* lds, const uint32_t* pairs, int nruns, int* q) {
+  if (threadIdx.x == 0) q[256] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < nruns; i += NT) {
+    const uint32_t p = pairs[i];
+    const int s = (int)(p & 0xFFFF);
+    const int e = s + (int)(p >> 16);
+    if ((e >> 5) - (s >> 5) <= 8) {
+      lds_or_run_serial(lds, s, e);
+    } else {
+      const int slot = atomicAdd(&q[256], 1);
+      if (slot < 256) q[slot] = i;
+      else lds_or_run_serial(lds, s, e);  // queue full: fall back to the serial fill
+    }
+  }
+  __syncthreads();
+  const int nq = min(q[256], 256);
+  for (int k = 0; k < nq; k++) {
+    const uint32_t p = pairs[q[k]];
+    const int s = (int)(p & 0xFFFF);
+    const int e = s + (int)(p >> 16);
+    const int ws = s >> 5, we = e >> 5;
+    for (int w = ws + threadIdx.x; w <= we; w += NT) {
+      uint32_t m = ~0u;
+      if (w == ws) m &= ~0u << (s & 31);
+      if (w == we) m &= ~0u >> (31 - (e & 31));
+      if (m == ~0u) lds[w] = ~0u;
+      else atomicOr(&lds[w], m);
+    }
+  }
+  __syncthreads();
+}
+
+// Materialise any container into the caller's owned registers.  `lds` is an
+// 8 KiB scratch bitmap, `q` 257 ints.  All threads must call; contains barriers.
+__device__ __forceinline__ void materialize(const CDesc& d, const uint8_t* payload, uint32_t* lds,
+                                            int* q, uint64_t r[4]) {
+  const uint8_t* slot = payload + d.slot;
+  if (d.kind == DK_B) {
+    load_bitmap_owned(slot, r);
+    return;
+  }
+  __syncthreads();  // previous readers of lds are done
+  lds_clear(lds);
+  __syncthreads();
+  if (d.kind == DK_A) {
+    lds_scatter_array(lds, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
+    __syncthreads();
+  } else {
+    const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
+    lds_or_runs(lds, reinterpret_cast<const uint32_t*>(slot + 4), nr, q);
+  }
+  lds_read_owned(lds, r);
+}
+
+// Count runs of the owned words; `lds` receives the words (used to fetch the
+// neighbours' edge bits).  Returns per-thread start bits in s[4] and end bits
+// in e[4].  Contains barriers.
+__device__ __forceinline__ void run_edges(const uint64_t r[4], uint32_t* lds, uint64_t s[4],
+                                          uint64_t e[4]) {
+  __syncthreads();
+  lds_write_owned(lds, r);
+  __syncthreads();
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(lds);
+  const int t = threadIdx.x;
+  const uint64_t prev0 = (t == 0) ? 0 : (w[2 * t - 1] >> 63);
+  const uint64_t prev2 = w[511 + 2 * t] >> 63;  // t == 0 reads word 511
+  const uint64_t next1 = w[2 * t + 2] & 1;      // t == 255 reads word 512
+  const uint64_t next3 = (t == NT - 1) ? 0 : (w[514 + 2 * t] & 1);
+  s[0] = r[0] & ~((r[0] << 1) | prev0);
+  s[1] = r[1] & ~((r[1] << 1) | (r[0] >> 63));
+  s[2] = r[2] & ~((r[2] << 1) | prev2);
+  s[3] = r[3] & ~((r[3] << 1) | (r[2] >> 63));
+  e[0] = r[0] & ~((r[0] >> 1) | ((r[1] & 1) << 63));
+  e[1] = r[1] & ~((r[1] >> 1) | (next1 << 63));
+  e[2] = r[2] & ~((r[2] >> 1) | ((r[3] & 1) << 63));
+  e[3] = r[3] & ~((r[3] >> 1) | (next3 << 63));
+}
+
+// ---------------------------------------------------------------------------
+// emission of a computed container into a 16 B-aligned slot (slot layout above)
+// ---------------------------------------------------------------------------
+// Array: compact the set bits into sorted u16 values via LDS staging.
+__device__ __forceinline__ void emit_array(const uint64_t r[4], int card, uint8_t* slot, uint32_t* stage,
+                                           int* sh) {
+  const int c0 = popc64(r[0]) + popc64(r[1]);
+  const int c1 = popc64(r[2]) + popc64(r[3]);
+  int p0, p1, tot;
+  block_scan_halves(c0, c1, p0, p1, tot, sh);
+  uint16_t* st = reinterpret_cast<uint16_t*>(stage);
+  const int t = threadIdx.x;
+  const int bases[4] = {(2 * t) * 64, (2 * t + 1) * 64, (512 + 2 * t) * 64, (513 + 2 * t) * 64};
+  int pos[4] = {p0, p0 + popc64(r[0]), p1, p1 + popc64(r[2])};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint64_t x = r[k];
+    int p = pos[k];
+    while (x) {
+      st[p++] = (uint16_t)(bases[k] + __builtin_ctzll(x));
+      x &= x - 1;
+    }
+  }
+  __syncthreads();
+  const int nvec = (2 * card + 15) >> 4;
+  for (int i = t; i < nvec; i += NT) reinterpret_cast<uint4*>(slot)[i] = reinterpret_cast<const uint4*>(stage)[i];
+  __syncthreads();
+}
+
+// Run container: (start, length-1) pairs from the edge bits.  Returns nruns.
+__device__ __forceinline__ int emit_runs(const uint64_t r[4], uint8_t* slot, uint32_t* lds, uint32_t* stage,
+                                         int* sh) {
+  uint64_t s[4], e[4];
+  run_edges(r, lds, s, e);
+  int ps0, ps1, nr, pe0, pe1, ne;
+  block_scan_halves(popc64(s[0]) + popc64(s[1]), popc64(s[2]) + popc64(s[3]), ps0, ps1, nr, sh);
+  block_scan_halves(popc64(e[0]) + popc64(e[1]), popc64(e[2]) + popc64(e[3]), pe0, pe1, ne, sh);
+  uint16_t* rs = reinterpret_cast<uint16_t*>(stage);
+  uint16_t* re = rs + 2048;
+  const int t = threadIdx.x;
+  const int bases[4] = {(2 * t) * 64, (2 * t + 1) * 64, (512 + 2 * t) * 64, (513 + 2 * t) * 64};
+  int sp[4] = {ps0, ps0 + popc64(s[0]), ps1, ps1 + popc64(s[2])};
+  int ep[4] = {pe0, pe0 + popc64(e[0]), pe1, pe1 + popc64(e[2])};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint64_t x = s[k];
+    int p = sp[k];
+    while (x) {
+      if (p < 2048) rs[p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
+      p++;
+      x &= x - 1;
+    }
+    x = e[k];
+    p = ep[k];
+    while (x) {
+      if (p < 2048) re[p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
+      p++;
+      x &= x - 1;
+    }
+  }
+  __syncthreads();
+  if (t == 0) reinterpret_cast<uint16_t*>(slot)[1] = (uint16_t)nr;
+  uint32_t* pairs = reinterpret_cast<uint32_t*>(slot + 4);
+  for (int i = t; i < nr && i < 2048; i += NT) pairs[i] = (uint32_t)rs[i] | ((uint32_t)(re[i] - rs[i]) << 16);
+  __syncthreads();
+  return nr;
+}
+
+// Number of runs of the owned container (block-wide).  Contains barriers.
+__device__ __forceinline__ int count_runs(const uint64_t r[4], uint32_t* lds, int* sh) {
+  uint64_t s[4], e[4];
+  run_edges(r, lds, s, e);
+  int a = popc64(s[0]) + popc64(s[1]) + popc64(s[2]) + popc64(s[3]);
+  int b = 0;
+  block_sum2(a, b, sh);
+  return a;
+}
+
+// Emit the owned container as `kind` into `slot`; fills the output descriptor
+// fields (serialized source address and length).  Contains barriers.
+__device__ __forceinline__ void emit_container(int kind, const uint64_t r[4], int card, uint8_t* slot,
+                                               uint32_t* lds, uint32_t* stage, int* sh, uint64_t* src,
+                                               uint32_t* ser_len) {
+  if (kind == DK_B) {
+    store_bitmap_owned(slot, r);
+    *src = reinterpret_cast<uint64_t>(slot);
+    *ser_len = 8192;
+  } else if (kind == DK_A) {
+    emit_array(r, card, slot, stage, sh);
+    *src = reinterpret_cast<uint64_t>(slot);
+    *ser_len = 2u * (uint32_t)card;
+  } else {
+    const int nr = emit_runs(r, slot, lds, stage, sh);
+    *src = reinterpret_cast<uint64_t>(slot + 2);
+    *ser_len = 2u + 4u * (uint32_t)nr;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// byte copy with arbitrary source / destination alignment (group-cooperative).
+// Reads up to 16 bytes past the end of `src`; every source buffer carries slack.
+// ---------------------------------------------------------------------------
+template <int G>
+__device__ __forceinline__ void group_copy(uint8_t* dst, const uint8_t* src, uint32_t n, int lane) {
+  const uintptr_t d = reinterpret_cast<uintptr_t>(dst);
+  uint32_t head = (uint32_t)((16 - (d & 15)) & 15);
+  if (head > n) head = n;
+  for (uint32_t i = lane; i < head; i += G) dst[i] = src[i];
+  uint8_t* db = dst + head;
+  const uint8_t* sb = src + head;
+  const uint32_t rem = n - head;
+  const uint32_t nvec = rem >> 4;
+  const uintptr_t s = reinterpret_cast<uintptr_t>(sb);
+  uint4* dv = reinterpret_cast<uint4*>(db);
+  if ((s & 15) == 0) {
+    const uint4* sv = reinterpret_cast<const uint4*>(sb);
+    for (uint32_t i = lane; i < nvec; i += G) dv[i] = sv[i];
+  } else if ((s & 3) == 0) {
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(sb);
+    for (uint32_t i = lane; i < nvec; i += G) dv[i] = make_uint4(sw[4 * i], sw[4 * i + 1], sw[4 * i + 2], sw[4 * i + 3]);
+  } else {
+    const uint32_t sh = (uint32_t)(s & 3);
+    const uint32_t* sw = reinterpret_cast<const uint32_t*>(s & ~(uintptr_t)3);
+    for (uint32_t i = lane; i < nvec; i += G) {
+      const uint32_t* q = sw + 4 * i;
+      const uint32_t a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3], a4 = q[4];
+      dv[i] = make_uint4(__builtin_amdgcn_alignbyte(a1, a0, sh), __builtin_amdgcn_alignbyte(a2, a1, sh),
+                         __builtin_amdgcn_alignbyte(a3, a2, sh), __builtin_amdgcn_alignbyte(a4, a3, sh));
+    }
+  }
+  const uint32_t done = nvec << 4;
+  for (uint32_t i = done + lane; i < rem; i += G) db[i] = sb[i];
+}
+
+}  // namespace rbg

@@ -1,0 +1,1090 @@
+// Host side of the MI355X Roaring engine: device contexts, batch upload
+// (parse -> raw H2D -> GPU ingest into the slotted arena), op pipelines and
+// the exported C ABI of include/roaring_mi355x.h.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/roaring_mi355x.h"
+#include "format.hpp"
+#include "kernels.hpp"
+
+namespace rbg {
+
+static thread_local std::string g_err;
+static void set_err(const std::string& s) { g_err = s; }
+
+#define HIPCHK(x)                                                            \
+  do {                                                                       \
+    hipError_t e_ = (x);                                                     \
+    if (e_ != hipSuccess) {                                                  \
+      set_err(std::string(#x) + " failed: " + hipGetErrorString(e_));        \
+      return e_ == hipErrorOutOfMemory ? RBG_ERR_OUT_OF_MEMORY : RBG_ERR_DEVICE; \
+    }                                                                        \
+  } while (0)
+
+#define CHK(x)              \
+  do {                      \
+    int st_ = (x);          \
+    if (st_ != RBG_OK) return st_; \
+  } while (0)
+
+constexpr size_t kSlack = 256;  // every device buffer carries read slack (group_copy)
+constexpr int kMaxKeys = 65536;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  int ensure(size_t bytes) {
+    if (cap >= bytes && p) return RBG_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, bytes + kSlack);
+    if (e != hipSuccess) {
+      p = nullptr;
+      set_err(std::string("hipMalloc(") + std::to_string(bytes) + ") failed: " + hipGetErrorString(e));
+      return e == hipErrorOutOfMemory ? RBG_ERR_OUT_OF_MEMORY : RBG_ERR_DEVICE;
+    }
+    cap = bytes;
+    return RBG_OK;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+struct Batch {
+  bool live = false;
+  bool key_major = false;  // containers sorted by (key, input); else by (input, key)
+  size_t n_bm = 0, n_ctr = 0;
+  DevBuf keys, desc, bm, key_off, bm_off, payload;
+  size_t payload_bytes = 0;
+  std::vector<uint32_t> h_bm_off;   // bitmap-major container ranges (n_bm + 1), or counts prefix
+  std::vector<uint32_t> h_bm_nctr;  // containers per input bitmap
+  std::vector<int64_t> h_bm_card;   // long cardinality per input bitmap
+  int64_t n_kind[3] = {0, 0, 0};
+  int64_t ser_bytes = 0;
+  int64_t long_card = 0;
+};
+
+struct Ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::vector<std::unique_ptr<Batch>> batches;
+  DevBuf by_key, flag, tasks, ntasks, out, out_idx, out_off, info, task_card, scratch, result, cards, skip, raw, items;
+  size_t result_cap = 0;
+  size_t n_cards = 0;
+  int last = 0;  // 0 none, 1 serialized result, 2 cardinality, 3 batch cardinalities
+  void* pinned = nullptr;
+  size_t pinned_cap = 0;
+  ~Ctx() {
+    if (pinned) (void)hipHostFree(pinned);
+    batches.clear();
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+static int ctx_init(Ctx* c, int device) {
+  int n = 0;
+  HIPCHK(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) {
+    set_err("no HIP device " + std::to_string(device));
+    return RBG_ERR_DEVICE;
+  }
+  HIPCHK(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_err(std::string("engine is built for gfx950, device is ") + prop.gcnArchName);
+    return RBG_ERR_DEVICE;
+  }
+  c->device = device;
+  HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  CHK(c->by_key.ensure(sizeof(Task) * kMaxKeys));
+  CHK(c->flag.ensure(kMaxKeys));
+  CHK(c->tasks.ensure(sizeof(Task) * kMaxKeys));
+  CHK(c->ntasks.ensure(64));
+  CHK(c->out.ensure(sizeof(ODesc) * kMaxKeys));
+  CHK(c->out_idx.ensure(4 * kMaxKeys));
+  CHK(c->out_off.ensure(8 * kMaxKeys));
+  CHK(c->info.ensure(sizeof(ResultInfo)));
+  CHK(c->task_card.ensure(4 * kMaxKeys));
+  return RBG_OK;
+}
+
+static int pinned_ensure(Ctx* c, size_t bytes) {
+  if (c->pinned_cap >= bytes) return RBG_OK;
+  if (c->pinned) (void)hipHostFree(c->pinned);
+  c->pinned = nullptr;
+  c->pinned_cap = 0;
+  HIPCHK(hipHostMalloc(&c->pinned, bytes, hipHostMallocDefault));
+  c->pinned_cap = bytes;
+  return RBG_OK;
+}
+
+static inline uint64_t round16(uint64_t x) { return (x + 15) & ~15ULL; }
+static inline uint64_t slot_bytes(uint8_t kind, uint32_t ser_len) {
+  return kind == KR ? round16(ser_len + 2) : round16(ser_len);
+}
+
+static int get_batch(Ctx* c, int32_t id, Batch** out) {
+  if (id < 0 || (size_t)id >= c->batches.size() || !c->batches[id] || !c->batches[id]->live) {
+    set_err("invalid batch id " + std::to_string(id));
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  *out = c->batches[id].get();
+  return RBG_OK;
+}
+
+static int32_t new_batch(Ctx* c) {
+  for (size_t i = 0; i < c->batches.size(); i++)
+    if (!c->batches[i]) {
+      c->batches[i].reset(new Batch());
+      return (int32_t)i;
+    }
+  c->batches.emplace_back(new Batch());
+  return (int32_t)(c->batches.size() - 1);
+}
+
+// ---------------------------------------------------------------------------
+// upload: parse headers on the host, H2D the raw bytes once, GPU ingest
+// ---------------------------------------------------------------------------
+static int ctx_load(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out_id) {
+  if (n && (!bufs || !lens)) return RBG_ERR_ILLEGAL_ARGUMENT;
+  std::vector<HostBitmap> hb(n);
+  for (size_t i = 0; i < n; i++) {
+    std::string err;
+    int st = parse(bufs[i], lens[i], &hb[i], &err);
+    if (st) {
+      set_err("input " + std::to_string(i) + ": " + err);
+      return st;
+    }
+  }
+  const int32_t id = new_batch(c);
+  Batch& b = *c->batches[id];
+  b.n_bm = n;
+  b.key_major = true;  // one bitmap is trivially key-major; several are sorted by key
+  size_t C = 0;
+  b.h_bm_nctr.resize(n);
+  b.h_bm_card.resize(n);
+  b.h_bm_off.assign(n + 1, 0);
+  for (size_t i = 0; i < n; i++) {
+    b.h_bm_nctr[i] = (uint32_t)hb[i].ctrs.size();
+    b.h_bm_card[i] = hb[i].card;
+    b.h_bm_off[i + 1] = b.h_bm_off[i] + (uint32_t)hb[i].ctrs.size();
+    C += hb[i].ctrs.size();
+    b.long_card += hb[i].card;
+    b.ser_bytes += (int64_t)hb[i].consumed;
+  }
+  b.n_ctr = C;
+  // key-major order: stable counting sort by key (input order kept within a key)
+  std::vector<uint32_t> key_off(kMaxKeys + 1, 0);
+  for (size_t i = 0; i < n; i++)
+    for (const HostCtr& hc : hb[i].ctrs) key_off[hc.key + 1]++;
+  for (int k = 0; k < kMaxKeys; k++) key_off[k + 1] += key_off[k];
+  std::vector<uint32_t> cursor(key_off.begin(), key_off.end() - 1);
+  std::vector<uint16_t> h_keys(C);
+  std::vector<CDesc> h_desc(C);
+  std::vector<uint32_t> h_bm(C);
+  std::vector<IngestItem> items(C);
+  // raw layout: concatenated inputs
+  std::vector<uint64_t> raw_base(n + 1, 0);
+  for (size_t i = 0; i < n; i++) raw_base[i + 1] = raw_base[i] + hb[i].consumed;
+  std::vector<uint32_t> pos_of(C);  // position of (input i, container j) in key-major order
+  for (size_t i = 0; i < n; i++) {
+    for (size_t j = 0; j < hb[i].ctrs.size(); j++) {
+      const HostCtr& hc = hb[i].ctrs[j];
+      pos_of[b.h_bm_off[i] + j] = cursor[hc.key]++;
+    }
+  }
+  // slot offsets follow key-major order so a key's fan-in is contiguous
+  std::vector<uint64_t> slot_size(C);
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = 0; j < hb[i].ctrs.size(); j++) {
+      const HostCtr& hc = hb[i].ctrs[j];
+      slot_size[pos_of[b.h_bm_off[i] + j]] = slot_bytes(hc.kind, hc.ser_len);
+    }
+  std::vector<uint64_t> slot_off(C + 1, 0);
+  for (size_t p = 0; p < C; p++) slot_off[p + 1] = slot_off[p] + slot_size[p];
+  for (size_t i = 0; i < n; i++) {
+    for (size_t j = 0; j < hb[i].ctrs.size(); j++) {
+      const HostCtr& hc = hb[i].ctrs[j];
+      const uint32_t p = pos_of[b.h_bm_off[i] + j];
+      h_keys[p] = hc.key;
+      h_bm[p] = (uint32_t)i;
+      CDesc d;
+      d.slot = slot_off[p];
+      d.card = hc.card;
+      d.key = hc.key;
+      d.kind = hc.kind;
+      d.flags = 0;
+      h_desc[p] = d;
+      items[p] = IngestItem{raw_base[i] + hc.ser_off, slot_off[p], hc.ser_len, hc.kind};
+      b.n_kind[hc.kind]++;
+    }
+  }
+  b.payload_bytes = slot_off[C];
+  // device allocations
+  CHK(b.keys.ensure(2 * C + 16));
+  CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
+  CHK(b.bm.ensure(4 * C + 16));
+  CHK(b.key_off.ensure(4 * (kMaxKeys + 1)));
+  CHK(b.bm_off.ensure(4 * (n + 1)));
+  CHK(b.payload.ensure(b.payload_bytes + 64));
+  const size_t raw_bytes = raw_base[n];
+  CHK(c->raw.ensure(raw_bytes + 64));
+  CHK(c->items.ensure(sizeof(IngestItem) * C + 16));
+  // stage raw bytes in pinned memory (parallel memcpy for large uploads)
+  CHK(pinned_ensure(c, raw_bytes + 64));
+  uint8_t* pin = reinterpret_cast<uint8_t*>(c->pinned);
+  const int nthr = raw_bytes > (64u << 20) ? (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  if (nthr == 1) {
+    for (size_t i = 0; i < n; i++) std::memcpy(pin + raw_base[i], bufs[i], hb[i].consumed);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthr; t++)
+      th.emplace_back([&, t]() {
+        for (size_t i = t; i < n; i += nthr) std::memcpy(pin + raw_base[i], bufs[i], hb[i].consumed);
+      });
+    for (auto& x : th) x.join();
+  }
+  hipStream_t s = c->stream;
+  HIPCHK(hipMemcpyAsync(c->raw.p, pin, raw_bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->items.p, items.data(), sizeof(IngestItem) * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.keys.p, h_keys.data(), 2 * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.desc.p, h_desc.data(), sizeof(CDesc) * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.bm.p, h_bm.data(), 4 * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.key_off.p, key_off.data(), 4 * (kMaxKeys + 1), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
+  launch_ingest(s, c->raw.as<uint8_t>(), c->items.as<IngestItem>(), C, b.payload.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  b.live = true;
+  *out_id = id;
+  return RBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// op pipelines
+// ---------------------------------------------------------------------------
+static int ensure_outputs(Ctx* c, size_t max_tasks, size_t max_payload) {
+  CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1)));
+  const size_t cap = 16 + 9 * max_tasks + (max_tasks + 7) / 8 + max_payload + 64;
+  CHK(c->result.ensure(cap));
+  c->result_cap = cap;
+  return RBG_OK;
+}
+
+static int grid_for(size_t tasks, size_t cap = 4096) {
+  size_t g = std::min(tasks, cap);
+  return (int)std::max<size_t>(g, 1);
+}
+
+// operand range of bitmap i of a batch (must be contiguous: one-bitmap batch)
+static int operand(Batch* b, size_t i, const uint16_t** keys, const CDesc** desc, int* n) {
+  if (i >= b->n_bm) {
+    set_err("bitmap index out of range");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  if (b->n_bm != 1) {
+    set_err("pairwise operands must be single-bitmap batches");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  *keys = b->keys.as<uint16_t>();
+  *desc = b->desc.as<CDesc>();
+  *n = (int)b->n_ctr;
+  return RBG_OK;
+}
+
+static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only) {
+  if (op < 0 || op > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Batch *A, *B;
+  CHK(get_batch(c, ia, &A));
+  CHK(get_batch(c, ib, &B));
+  const uint16_t *ka, *kb;
+  const CDesc *da, *db;
+  int na, nb;
+  CHK(operand(A, ma, &ka, &da, &na));
+  CHK(operand(B, mb, &kb, &db, &nb));
+  hipStream_t s = c->stream;
+  const int plan_op = card_only ? OP_AND : op;
+  size_t ub;
+  switch (plan_op) {
+    case OP_AND: ub = std::min(na, nb); break;
+    case OP_ANDNOT: ub = na; break;
+    default: ub = std::min<size_t>((size_t)na + nb, kMaxKeys); break;
+  }
+  if (!card_only) CHK(ensure_outputs(c, ub, A->payload_bytes + B->payload_bytes + (size_t)kSlotBytes * ub));
+  launch_plan_pairwise(s, plan_op, ka, na, kb, nb, c->by_key.as<Task>(), c->flag.as<uint8_t>());
+  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->tasks.as<Task>(), c->ntasks.as<uint32_t>());
+  launch_pairwise(s, op, card_only ? 1 : 0, grid_for(ub), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), da,
+                  A->payload.as<uint8_t>(), db, B->payload.as<uint8_t>(), c->out.as<ODesc>(), c->scratch.as<uint8_t>(),
+                  c->task_card.as<uint32_t>());
+  if (card_only) {
+    launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
+    c->last = 2;
+  } else {
+    launch_finalize(s, c->out.as<ODesc>(), c->ntasks.as<uint32_t>(), c->out_idx.as<uint32_t>(),
+                    c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
+    launch_emit(s, grid_for(ub), c->out.as<ODesc>(), c->ntasks.as<uint32_t>(), c->out_idx.as<uint32_t>(),
+                c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
+    c->last = 1;
+  }
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
+
+// FastAggregation dispatch (RB/FastAggregation.java:26-101,653-666,823-836)
+static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const int32_t* ids, bool card_only,
+                    int* host_card_out, bool* host_card_valid) {
+  Batch* B;
+  CHK(get_batch(c, id, &B));
+  if (!B->key_major) {
+    set_err("wide ops need a key-major batch");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  key_lo = std::max(0, key_lo);
+  key_hi = std::min(kMaxKeys, key_hi);
+  hipStream_t s = c->stream;
+  const size_t N = B->n_bm;
+  *host_card_valid = false;
+  int mode = WIDE_OR, plan_mode = 0;
+  uint32_t start_bm = 0;
+  std::vector<uint8_t> skip;
+  if (card_only) {
+    // andCardinality: 0 -> 0, 1 -> card, >= 2 -> per-key AND sum (== andCardinality / workShyAndCardinality)
+    // orCardinality : 0 -> 0, 1 -> card, >= 2 -> per-key OR sum (== orCardinality / horizontalOrCardinality)
+    if (op != RBG_WIDE_CARD_AND && op != RBG_WIDE_CARD_OR) return RBG_ERR_ILLEGAL_ARGUMENT;
+    const bool full_range = key_lo == 0 && key_hi == kMaxKeys;
+    if (N == 0 || (N == 1 && full_range)) {
+      const int64_t cc = N ? B->h_bm_card[0] : 0;
+      *host_card_out = (int32_t)(uint32_t)(uint64_t)cc;
+      *host_card_valid = true;
+      c->last = 2;
+      return RBG_OK;
+    }
+    if (op == RBG_WIDE_CARD_AND && N >= 2) {
+      mode = WIDE_AND_SHY_CARD;
+      plan_mode = 1;
+    } else {
+      mode = WIDE_OR_CARD;  // also a single input restricted to a key range
+    }
+  } else {
+    switch (op) {
+      case RBG_WIDE_OR: mode = WIDE_OR; break;
+      case RBG_WIDE_XOR: mode = WIDE_XOR; break;
+      case RBG_WIDE_AND:
+      case RBG_WIDE_AND_ITER:
+      case RBG_WIDE_NAIVE_AND:
+      case RBG_WIDE_WORKSHY_AND:
+        plan_mode = 1;
+        if (op == RBG_WIDE_WORKSHY_AND && N == 0) {
+          set_err("workShyAnd needs at least one bitmap");  // bitmaps[0] on an empty array
+          return RBG_ERR_ILLEGAL_ARGUMENT;
+        }
+        if ((op == RBG_WIDE_AND && N > 10) || op == RBG_WIDE_WORKSHY_AND) {
+          mode = WIDE_AND_SHY;
+        } else {
+          mode = WIDE_AND_NAIVE;
+          skip.assign(std::max<size_t>(N, 1), 0);
+          if (op != RBG_WIDE_AND_ITER) {
+            // the input with the fewest containers, first on ties (:333-339)
+            for (size_t i = 1; i < N; i++)
+              if (B->h_bm_nctr[i] < B->h_bm_nctr[start_bm]) start_bm = (uint32_t)i;
+            for (size_t i = 0; i < N; i++)
+              skip[i] = (i == start_bm) || (ids && ids[i] == ids[start_bm]);  // :341 identity skip
+          } else {
+            start_bm = 0;  // naive_and(Iterator): clone of the first input, :309-313
+            skip[0] = 1;
+          }
+        }
+        break;
+      default: return RBG_ERR_ILLEGAL_ARGUMENT;
+    }
+  }
+  if (N == 0) {
+    // empty aggregate: empty bitmap (:329-331 for and; naive_or/xor of nothing)
+    plan_mode = 2;
+  }
+  {
+    CHK(ensure_outputs(c, kMaxKeys, (size_t)kSlotBytes * kMaxKeys + B->payload_bytes));
+    if (!skip.empty()) {
+      CHK(c->skip.ensure(skip.size()));
+      HIPCHK(hipMemcpyAsync(c->skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
+    }
+    const uint32_t n_req = plan_mode == 2 ? 0xFFFFFFFFu : (uint32_t)N;
+    launch_plan_wide(s, plan_mode == 0 ? 0 : 1, B->key_off.as<uint32_t>(), n_req, key_lo, key_hi,
+                     c->by_key.as<Task>(), c->flag.as<uint8_t>());
+    launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->tasks.as<Task>(), c->ntasks.as<uint32_t>());
+    WideArgs wa;
+    wa.desc = B->desc.as<CDesc>();
+    wa.bm = B->bm.as<uint32_t>();
+    wa.payload = B->payload.as<uint8_t>();
+    wa.skip = skip.empty() ? nullptr : c->skip.as<uint8_t>();
+    wa.start_bm = start_bm;
+    launch_wide(s, mode, 4096, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, c->out.as<ODesc>(),
+                c->scratch.as<uint8_t>(), c->task_card.as<uint32_t>());
+    if (card_only) {
+      launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
+      c->last = 2;
+    } else {
+      launch_finalize(s, c->out.as<ODesc>(), c->ntasks.as<uint32_t>(), c->out_idx.as<uint32_t>(),
+                      c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
+      launch_emit(s, 4096, c->out.as<ODesc>(), c->ntasks.as<uint32_t>(), c->out_idx.as<uint32_t>(),
+                  c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
+      c->last = 1;
+    }
+    HIPCHK(hipGetLastError());
+  }
+  return RBG_OK;
+}
+
+static int ctx_info(Ctx* c, ResultInfo* ri) {
+  HIPCHK(hipMemcpyAsync(ri, c->info.p, sizeof(ResultInfo), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return RBG_OK;
+}
+
+static int ctx_fetch(Ctx* c, rbg_buffer* out) {
+  if (c->last != 1) {
+    set_err("no serialized result pending");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  ResultInfo ri;
+  CHK(ctx_info(c, &ri));
+  uint8_t* p = (uint8_t*)std::malloc(ri.total ? ri.total : 1);
+  if (!p) return RBG_ERR_OUT_OF_MEMORY;
+  HIPCHK(hipMemcpyAsync(p, c->result.p, ri.total, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  out->data = p;
+  out->len = ri.total;
+  return RBG_OK;
+}
+
+// ---------------------------------------------------------------------------
+// thread-local one-shot contexts
+// ---------------------------------------------------------------------------
+static std::mutex g_dev_mu;
+static uint64_t g_dev_mask = 1;
+
+struct TLCtx {
+  std::unique_ptr<Ctx> ctx;
+  int device = -1;
+};
+static thread_local TLCtx tl;
+
+static int tl_ctx(Ctx** out) {
+  int dev;
+  {
+    std::lock_guard<std::mutex> g(g_dev_mu);
+    uint64_t m = g_dev_mask;
+    dev = m ? __builtin_ctzll(m) : 0;
+  }
+  if (!tl.ctx || tl.device != dev) {
+    std::unique_ptr<Ctx> c(new Ctx());
+    CHK(ctx_init(c.get(), dev));
+    tl.ctx = std::move(c);
+    tl.device = dev;
+  }
+  HIPCHK(hipSetDevice(tl.device));
+  *out = tl.ctx.get();
+  return RBG_OK;
+}
+
+struct BatchGuard {
+  Ctx* c;
+  std::vector<int32_t> ids;
+  ~BatchGuard() {
+    for (int32_t id : ids)
+      if (id >= 0 && (size_t)id < c->batches.size()) c->batches[id].reset();
+  }
+};
+
+}  // namespace rbg
+
+using namespace rbg;
+
+struct rbg_ctx {
+  Ctx c;
+};
+
+extern "C" {
+
+int rbg_version(void) { return 1; }
+const char* rbg_last_error(void) { return g_err.c_str(); }
+
+void rbg_free(rbg_buffer* buf) {
+  if (!buf) return;
+  std::free(buf->data);
+  buf->data = nullptr;
+  buf->len = 0;
+}
+
+int rbg_set_devices(uint64_t mask) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
+    set_err("no HIP device");
+    return RBG_ERR_DEVICE;
+  }
+  uint64_t usable = mask & ((n >= 64) ? ~0ULL : ((1ULL << n) - 1));
+  if (!usable) {
+    set_err("device mask selects no present device");
+    return RBG_ERR_DEVICE;
+  }
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  g_dev_mask = usable;
+  return __builtin_popcountll(usable);
+}
+
+int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, rbg_buffer* out) {
+  if (!out || op < 0 || op > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t ia, ib;
+  CHK(ctx_load(c, &a, &a_len, 1, &ia));
+  g.ids.push_back(ia);
+  CHK(ctx_load(c, &b, &b_len, 1, &ib));
+  g.ids.push_back(ib);
+  CHK(ctx_pairwise(c, op, ia, 0, ib, 0, false));
+  return ctx_fetch(c, out);
+}
+
+int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int32_t* out) {
+  if (!out || op < 0 || op > 4) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t ia, ib;
+  CHK(ctx_load(c, &a, &a_len, 1, &ia));
+  g.ids.push_back(ia);
+  CHK(ctx_load(c, &b, &b_len, 1, &ib));
+  g.ids.push_back(ib);
+  CHK(ctx_pairwise(c, OP_AND, ia, 0, ib, 0, true));
+  ResultInfo ri;
+  CHK(ctx_info(c, &ri));
+  const uint32_t ac = ri.card32;
+  const uint32_t ca = (uint32_t)(uint64_t)c->batches[ia]->long_card;  // RoaringBitmap.getCardinality (int)
+  const uint32_t cb = (uint32_t)(uint64_t)c->batches[ib]->long_card;
+  switch (op) {
+    case RBG_CARD_AND: *out = (int32_t)ac; break;
+    case RBG_CARD_OR: *out = (int32_t)(ca + cb - ac); break;         // RB/RoaringBitmap.java:916-920
+    case RBG_CARD_XOR: *out = (int32_t)(ca + cb - 2u * ac); break;   // :931-933
+    case RBG_CARD_ANDNOT: *out = (int32_t)(ca - ac); break;          // :944-985 (both branches, mod 2^32)
+    default: *out = ri.any ? 1 : 0; break;                           // intersects :698-720
+  }
+  return RBG_OK;
+}
+
+int rbg_wide(int op, const uint8_t* const* bufs, const size_t* lens, const int32_t* ids, size_t n, rbg_buffer* out) {
+  if (!out || op < 0 || op > 5) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(ctx_load(c, bufs, lens, n, &id));
+  g.ids.push_back(id);
+  int hc;
+  bool hv;
+  CHK(ctx_wide(c, op, id, 0, 65536, ids, false, &hc, &hv));
+  return ctx_fetch(c, out);
+}
+
+int rbg_wide_card(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out) {
+  if (!out || op < 0 || op > 1) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(ctx_load(c, bufs, lens, n, &id));
+  g.ids.push_back(id);
+  int hc = 0;
+  bool hv = false;
+  CHK(ctx_wide(c, op, id, 0, 65536, nullptr, true, &hc, &hv));
+  if (hv) {
+    *out = hc;
+    return RBG_OK;
+  }
+  ResultInfo ri;
+  CHK(ctx_info(c, &ri));
+  *out = (int32_t)ri.card32;
+  return RBG_OK;
+}
+
+static int ctx_batch_card(Ctx* c, int32_t id) {
+  Batch* B;
+  CHK(get_batch(c, id, &B));
+  if (B->n_bm % 2 != 0) {
+    set_err("batched andCardinality needs an even number of bitmaps");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  const size_t np = B->n_bm / 2;
+  CHK(c->cards.ensure(4 * std::max<size_t>(np, 1)));
+  if (B->key_major && B->n_bm > 1) {
+    // pairs need bitmap-major ranges: permuted view of a key-major batch is not supported
+    set_err("batched andCardinality needs a bitmap-major batch");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  launch_batch_and_card(c->stream, np, B->bm_off.as<uint32_t>(), B->desc.as<CDesc>(), B->payload.as<uint8_t>(),
+                        c->cards.as<int32_t>());
+  HIPCHK(hipGetLastError());
+  c->n_cards = np;
+  c->last = 3;
+  return RBG_OK;
+}
+
+// bitmap-major upload used by batched andCardinality (pairs kept adjacent)
+static int ctx_load_bitmap_major(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out_id) {
+  std::vector<HostBitmap> hb(n);
+  for (size_t i = 0; i < n; i++) {
+    std::string err;
+    int st = parse(bufs[i], lens[i], &hb[i], &err);
+    if (st) {
+      set_err("input " + std::to_string(i) + ": " + err);
+      return st;
+    }
+  }
+  const int32_t id = new_batch(c);
+  Batch& b = *c->batches[id];
+  b.n_bm = n;
+  b.key_major = n <= 1;
+  b.h_bm_off.assign(n + 1, 0);
+  b.h_bm_nctr.resize(n);
+  b.h_bm_card.resize(n);
+  std::vector<uint64_t> raw_base(n + 1, 0);
+  for (size_t i = 0; i < n; i++) {
+    b.h_bm_off[i + 1] = b.h_bm_off[i] + (uint32_t)hb[i].ctrs.size();
+    b.h_bm_nctr[i] = (uint32_t)hb[i].ctrs.size();
+    b.h_bm_card[i] = hb[i].card;
+    b.long_card += hb[i].card;
+    b.ser_bytes += (int64_t)hb[i].consumed;
+    raw_base[i + 1] = raw_base[i] + hb[i].consumed;
+  }
+  const size_t C = b.h_bm_off[n];
+  b.n_ctr = C;
+  std::vector<uint16_t> h_keys(C);
+  std::vector<CDesc> h_desc(C);
+  std::vector<uint32_t> h_bm(C);
+  std::vector<IngestItem> items(C);
+  uint64_t off = 0;
+  for (size_t i = 0; i < n; i++)
+    for (size_t j = 0; j < hb[i].ctrs.size(); j++) {
+      const HostCtr& hc = hb[i].ctrs[j];
+      const size_t p = b.h_bm_off[i] + j;
+      h_keys[p] = hc.key;
+      h_bm[p] = (uint32_t)i;
+      h_desc[p] = CDesc{off, hc.card, hc.key, hc.kind, 0};
+      items[p] = IngestItem{raw_base[i] + hc.ser_off, off, hc.ser_len, hc.kind};
+      off += slot_bytes(hc.kind, hc.ser_len);
+      b.n_kind[hc.kind]++;
+    }
+  b.payload_bytes = off;
+  CHK(b.keys.ensure(2 * C + 16));
+  CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
+  CHK(b.bm.ensure(4 * C + 16));
+  CHK(b.bm_off.ensure(4 * (n + 1)));
+  CHK(b.payload.ensure(off + 64));
+  const size_t raw_bytes = raw_base[n];
+  CHK(c->raw.ensure(raw_bytes + 64));
+  CHK(c->items.ensure(sizeof(IngestItem) * C + 16));
+  CHK(pinned_ensure(c, raw_bytes + 64));
+  uint8_t* pin = reinterpret_cast<uint8_t*>(c->pinned);
+  for (size_t i = 0; i < n; i++) std::memcpy(pin + raw_base[i], bufs[i], hb[i].consumed);
+  hipStream_t s = c->stream;
+  HIPCHK(hipMemcpyAsync(c->raw.p, pin, raw_bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(c->items.p, items.data(), sizeof(IngestItem) * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.keys.p, h_keys.data(), 2 * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.desc.p, h_desc.data(), sizeof(CDesc) * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.bm.p, h_bm.data(), 4 * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
+  launch_ingest(s, c->raw.as<uint8_t>(), c->items.as<IngestItem>(), C, b.payload.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  b.live = true;
+  *out_id = id;
+  return RBG_OK;
+}
+
+int rbg_batch_and_card(size_t n_pairs, const uint8_t* const* a_bufs, const size_t* a_lens,
+                       const uint8_t* const* b_bufs, const size_t* b_lens, int32_t* out) {
+  if (n_pairs && (!a_bufs || !a_lens || !b_bufs || !b_lens || !out)) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (n_pairs == 0) return RBG_OK;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  std::vector<const uint8_t*> bufs(2 * n_pairs);
+  std::vector<size_t> lens(2 * n_pairs);
+  for (size_t i = 0; i < n_pairs; i++) {
+    bufs[2 * i] = a_bufs[i];
+    lens[2 * i] = a_lens[i];
+    bufs[2 * i + 1] = b_bufs[i];
+    lens[2 * i + 1] = b_lens[i];
+  }
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(ctx_load_bitmap_major(c, bufs.data(), lens.data(), 2 * n_pairs, &id));
+  g.ids.push_back(id);
+  CHK(ctx_batch_card(c, id));
+  HIPCHK(hipMemcpyAsync(out, c->cards.p, 4 * n_pairs, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return RBG_OK;
+}
+
+// ---- host-side format utilities ----
+static int emit_host(const std::vector<uint8_t>& v, rbg_buffer* out) {
+  uint8_t* p = (uint8_t*)std::malloc(v.size() ? v.size() : 1);
+  if (!p) return RBG_ERR_OUT_OF_MEMORY;
+  if (!v.empty()) std::memcpy(p, v.data(), v.size());
+  out->data = p;
+  out->len = v.size();
+  return RBG_OK;
+}
+
+int rbg_from_values(const uint32_t* values, size_t n, int run_optimize, rbg_buffer* out) {
+  if (!out || (n && !values)) return RBG_ERR_ILLEGAL_ARGUMENT;
+  return emit_host(build_from_values(values, n, run_optimize != 0), out);
+}
+
+int rbg_run_optimize(const uint8_t* buf, size_t len, rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  std::vector<uint8_t> v;
+  std::string err;
+  int st = run_optimize_serialized(buf, len, &v, &err);
+  if (st) {
+    set_err(err);
+    return st;
+  }
+  return emit_host(v, out);
+}
+
+int rbg_to_values(const uint8_t* buf, size_t len, rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  std::vector<uint32_t> v;
+  std::string err;
+  int st = values_of_serialized(buf, len, &v, &err);
+  if (st) {
+    set_err(err);
+    return st;
+  }
+  uint8_t* p = (uint8_t*)std::malloc(v.size() * 4 + 4);
+  if (!p) return RBG_ERR_OUT_OF_MEMORY;
+  std::memcpy(p, v.data(), v.size() * 4);
+  out->data = p;
+  out->len = v.size() * 4;
+  return RBG_OK;
+}
+
+int rbg_inspect(const uint8_t* buf, size_t len, size_t* consumed, int64_t* cardinality, int64_t* stats3) {
+  HostBitmap hb;
+  std::string err;
+  int st = parse(buf, len, &hb, &err);
+  if (st) {
+    set_err(err);
+    return st;
+  }
+  if (consumed) *consumed = hb.consumed;
+  if (cardinality) *cardinality = hb.card;
+  if (stats3) {
+    stats3[0] = stats3[1] = stats3[2] = 0;
+    for (const HostCtr& c : hb.ctrs) stats3[c.kind]++;
+  }
+  return RBG_OK;
+}
+
+// ---- session API ----
+int rbg_ctx_create(int device, rbg_ctx** out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  std::unique_ptr<rbg_ctx> c(new rbg_ctx());
+  CHK(ctx_init(&c->c, device));
+  *out = c.release();
+  return RBG_OK;
+}
+void rbg_ctx_destroy(rbg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->c.device);
+  delete ctx;
+}
+void* rbg_ctx_stream(rbg_ctx* ctx) { return ctx ? (void*)ctx->c.stream : nullptr; }
+int rbg_ctx_sync(rbg_ctx* ctx) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  HIPCHK(hipStreamSynchronize(ctx->c.stream));
+  return RBG_OK;
+}
+int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* batch) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_load(&ctx->c, bufs, lens, n, batch);
+}
+int rbg_ctx_release(rbg_ctx* ctx, int32_t batch) {
+  Batch* b;
+  CHK(get_batch(&ctx->c, batch, &b));
+  HIPCHK(hipSetDevice(ctx->c.device));
+  HIPCHK(hipStreamSynchronize(ctx->c.stream));
+  ctx->c.batches[batch].reset();
+  return RBG_OK;
+}
+int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* st) {
+  Batch* b;
+  CHK(get_batch(&ctx->c, batch, &b));
+  st[0] = (int64_t)b->n_bm;
+  st[1] = (int64_t)b->n_ctr;
+  st[2] = b->n_kind[0];
+  st[3] = b->n_kind[1];
+  st[4] = b->n_kind[2];
+  st[5] = 0;  // payload bytes (serialized form)
+  st[6] = b->long_card;
+  st[7] = b->ser_bytes;
+  if (b->n_ctr) {
+    std::vector<CDesc> d(b->n_ctr);
+    HIPCHK(hipSetDevice(ctx->c.device));
+    HIPCHK(hipMemcpy(d.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
+    int64_t pay = 0;
+    for (const CDesc& x : d) {
+      if (x.kind == KA) pay += 2 * (int64_t)x.card;
+      else if (x.kind == KB) pay += 8192;
+      else {
+        uint16_t nr = 0;
+        HIPCHK(hipMemcpy(&nr, b->payload.as<uint8_t>() + x.slot + 2, 2, hipMemcpyDeviceToHost));
+        pay += 2 + 4 * (int64_t)nr;
+      }
+    }
+    st[5] = pay;
+  }
+  return RBG_OK;
+}
+int rbg_ctx_batch_fetch(rbg_ctx* ctx, int32_t batch, size_t i, rbg_buffer* out) {
+  Batch* b;
+  CHK(get_batch(&ctx->c, batch, &b));
+  if (i >= b->n_bm || !out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipSetDevice(ctx->c.device));
+  HIPCHK(hipStreamSynchronize(ctx->c.stream));
+  std::vector<CDesc> all(b->n_ctr);
+  if (b->n_ctr) HIPCHK(hipMemcpy(all.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
+  std::vector<CDesc> mine;
+  if (b->n_bm == 1 || !b->key_major) {
+    for (uint32_t p = b->h_bm_off[i]; p < b->h_bm_off[i + 1]; p++) mine.push_back(all[p]);
+  } else {
+    std::vector<uint32_t> bm(b->n_ctr);
+    HIPCHK(hipMemcpy(bm.data(), b->bm.p, 4 * b->n_ctr, hipMemcpyDeviceToHost));
+    for (size_t p = 0; p < b->n_ctr; p++)
+      if (bm[p] == i) mine.push_back(all[p]);
+  }
+  uint64_t lo = ~0ULL, hi = 0;
+  for (const CDesc& d : mine) {
+    lo = std::min<uint64_t>(lo, d.slot);
+    hi = std::max<uint64_t>(hi, d.slot + kSlotBytes);
+  }
+  hi = std::min<uint64_t>(hi, b->payload_bytes + 64);
+  std::vector<uint8_t> pay(mine.empty() ? 0 : hi - lo);
+  if (!pay.empty()) HIPCHK(hipMemcpy(pay.data(), b->payload.as<uint8_t>() + lo, hi - lo, hipMemcpyDeviceToHost));
+  const size_t n = mine.size();
+  bool has_run = false;
+  for (const CDesc& d : mine) has_run |= d.kind == KR;
+  std::vector<uint8_t> o;
+  auto put16 = [&](uint32_t v) { o.push_back((uint8_t)v); o.push_back((uint8_t)(v >> 8)); };
+  auto put32 = [&](uint32_t v) { for (int k = 0; k < 4; k++) o.push_back((uint8_t)(v >> (8 * k))); };
+  std::vector<uint32_t> lens(n);
+  for (size_t k = 0; k < n; k++) {
+    const CDesc& d = mine[k];
+    if (d.kind == KA) lens[k] = 2 * d.card;
+    else if (d.kind == KB) lens[k] = 8192;
+    else {
+      const uint8_t* q = pay.data() + (d.slot - lo) + 2;
+      lens[k] = 2 + 4 * (uint32_t)(q[0] | (q[1] << 8));
+    }
+  }
+  if (has_run) {
+    put32(12347u | (uint32_t)((n - 1) << 16));
+    std::vector<uint8_t> fl((n + 7) / 8, 0);
+    for (size_t k = 0; k < n; k++)
+      if (mine[k].kind == KR) fl[k / 8] |= (uint8_t)(1u << (k % 8));
+    o.insert(o.end(), fl.begin(), fl.end());
+  } else {
+    put32(12346u);
+    put32((uint32_t)n);
+  }
+  for (const CDesc& d : mine) {
+    put16(d.key);
+    put16(d.card - 1);
+  }
+  if (!has_run || n >= 4) {
+    uint32_t start = (uint32_t)header_size(n, has_run);
+    for (size_t k = 0; k < n; k++) {
+      put32(start);
+      start += lens[k];
+    }
+  }
+  for (size_t k = 0; k < n; k++) {
+    const uint8_t* q = pay.data() + (mine[k].slot - lo) + (mine[k].kind == KR ? 2 : 0);
+    o.insert(o.end(), q, q + lens[k]);
+  }
+  return emit_host(o, out);
+}
+int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_pairwise(&ctx->c, op, a, ia, b, ib, false);
+}
+int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  if (op != RBG_CARD_AND) {
+    set_err("the session API computes andCardinality; derive the others from the input cardinalities");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  return ctx_pairwise(&ctx->c, OP_AND, a, ia, b, ib, true);
+}
+int rbg_ctx_wide(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, const int32_t* ids) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  int hc;
+  bool hv;
+  return ctx_wide(&ctx->c, op, batch, key_lo, key_hi, ids, false, &hc, &hv);
+}
+int rbg_ctx_wide_card(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  int hc;
+  bool hv;
+  CHK(ctx_wide(&ctx->c, op, batch, key_lo, key_hi, nullptr, true, &hc, &hv));
+  if (hv) {
+    ResultInfo ri = {};
+    ri.card32 = (uint32_t)hc;
+    ri.long_card = hc;
+    HIPCHK(hipMemcpyAsync(ctx->c.info.p, &ri, sizeof(ri), hipMemcpyHostToDevice, ctx->c.stream));
+    HIPCHK(hipStreamSynchronize(ctx->c.stream));
+  }
+  return RBG_OK;
+}
+int rbg_ctx_batch_and_card(rbg_ctx* ctx, int32_t batch) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_batch_card(&ctx->c, batch);
+}
+int rbg_ctx_card(rbg_ctx* ctx, int32_t* out) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  ResultInfo ri;
+  CHK(ctx_info(&ctx->c, &ri));
+  *out = (int32_t)ri.card32;
+  return RBG_OK;
+}
+int rbg_ctx_cards(rbg_ctx* ctx, int32_t* out, size_t n) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  if (n > ctx->c.n_cards) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipMemcpyAsync(out, ctx->c.cards.p, 4 * n, hipMemcpyDeviceToHost, ctx->c.stream));
+  HIPCHK(hipStreamSynchronize(ctx->c.stream));
+  return RBG_OK;
+}
+int rbg_ctx_result_stats(rbg_ctx* ctx, int64_t* st) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  ResultInfo ri;
+  CHK(ctx_info(&ctx->c, &ri));
+  st[0] = ri.n_out;
+  st[1] = (int64_t)ri.payload;
+  st[2] = ri.has_run;
+  st[3] = ri.long_card;
+  return RBG_OK;
+}
+int rbg_ctx_fetch(rbg_ctx* ctx, rbg_buffer* out) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_fetch(&ctx->c, out);
+}
+int rbg_ctx_fetch_shard(rbg_ctx* ctx, int64_t total_containers, int has_run, int64_t first_container,
+                        int64_t payload_base, rbg_buffer* out_desc, rbg_buffer* out_offsets, rbg_buffer* out_payload) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  rbg_buffer local = {nullptr, 0};
+  CHK(ctx_fetch(&ctx->c, &local));
+  std::unique_ptr<uint8_t, void (*)(void*)> hold(local.data, std::free);
+  ResultInfo ri;
+  CHK(ctx_info(&ctx->c, &ri));
+  const size_t n = ri.n_out;
+  const size_t desc_base = ri.has_run ? 4 + (n + 7) / 8 : 8;
+  std::vector<uint8_t> desc(local.data + desc_base, local.data + desc_base + 4 * n);
+  std::vector<uint8_t> payload(local.data + ri.header, local.data + ri.total);
+  // global offsets: header(total, has_run) + payload_base + local payload offset
+  std::vector<uint8_t> offs;
+  const bool global_offsets = !has_run || total_containers >= 4;
+  if (global_offsets && n) {
+    const uint64_t gh = header_size((size_t)total_containers, has_run != 0);
+    // local payload offsets from the descriptors: recompute sizes by walking payloads
+    uint64_t pos = 0;
+    const uint8_t* flags = ri.has_run ? local.data + 4 : nullptr;
+    for (size_t i = 0; i < n; i++) {
+      const uint32_t o = (uint32_t)(gh + payload_base + pos);
+      for (int k = 0; k < 4; k++) offs.push_back((uint8_t)(o >> (8 * k)));
+      const uint16_t card1 = (uint16_t)(desc[4 * i + 2] | (desc[4 * i + 3] << 8));
+      const bool is_run = flags && (flags[i / 8] & (1 << (i % 8)));
+      if (is_run) {
+        const uint8_t* q = local.data + ri.header + pos;
+        pos += 2 + 4 * (uint64_t)(q[0] | (q[1] << 8));
+      } else if ((uint32_t)card1 + 1 > 4096) {
+        pos += 8192;
+      } else {
+        pos += 2 * ((uint64_t)card1 + 1);
+      }
+    }
+  }
+  (void)first_container;
+  CHK(emit_host(desc, out_desc));
+  CHK(emit_host(offs, out_offsets));
+  return emit_host(payload, out_payload);
+}
+
+int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi, int32_t* batch) {
+  Ctx* c = &ctx->c;
+  HIPCHK(hipSetDevice(c->device));
+  (void)n;
+  (void)key_lo;
+  (void)key_hi;
+  if (kind != 0) {
+    set_err("synthetic kind not available");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  const int32_t id = new_batch(c);
+  Batch& b = *c->batches[id];
+  const size_t C = kMaxKeys;
+  b.n_bm = 1;
+  b.n_ctr = C;
+  b.key_major = true;
+  b.payload_bytes = (size_t)kSlotBytes * C;
+  CHK(b.keys.ensure(2 * C + 16));
+  CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
+  CHK(b.bm.ensure(4 * C + 16));
+  CHK(b.key_off.ensure(4 * (kMaxKeys + 1)));
+  CHK(b.bm_off.ensure(8));
+  CHK(b.payload.ensure(b.payload_bytes + 64));
+  std::vector<uint32_t> key_off(kMaxKeys + 1);
+  for (int k = 0; k <= kMaxKeys; k++) key_off[k] = (uint32_t)k;
+  b.h_bm_off = {0u, (uint32_t)C};
+  b.h_bm_nctr = {(uint32_t)C};
+  hipStream_t s = c->stream;
+  HIPCHK(hipMemsetAsync(b.bm.p, 0, 4 * C, s));
+  HIPCHK(hipMemcpyAsync(b.key_off.p, key_off.data(), 4 * (kMaxKeys + 1), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 8, hipMemcpyHostToDevice, s));
+  launch_synth_c2(s, seed, b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.payload.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  std::vector<CDesc> d(C);
+  HIPCHK(hipMemcpyAsync(d.data(), b.desc.p, sizeof(CDesc) * C, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  int64_t card = 0, ser = 0;
+  bool has_run = false;
+  for (const CDesc& x : d) {
+    b.n_kind[x.kind]++;
+    card += x.card;
+    has_run |= x.kind == KR;
+  }
+  b.long_card = card;
+  b.h_bm_card = {card};
+  (void)ser;
+  b.ser_bytes = 0;
+  b.live = true;
+  *batch = id;
+  return RBG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// Kernel launch interface of the engine (host side <-> kernels.hip / wide.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device.hpp"
+
+namespace rbg {
+
+enum OpCode : int { OP_AND = 0, OP_OR = 1, OP_XOR = 2, OP_ANDNOT = 3 };
+
+struct IngestItem {  // one container copy raw -> arena slot
+  uint64_t src;  // byte offset in the raw upload
+  uint64_t dst;  // slot byte offset in the payload arena
+  uint32_t len;  // serialized payload length
+  uint32_t kind;
+};
+
+// wide-op flavours (wide.hip)
+enum WideMode : int {
+  WIDE_OR = 0,         // FastAggregation.naive_or
+  WIDE_OR_CARD = 1,    // horizontalOrCardinality
+  WIDE_XOR = 2,        // naive_xor
+  WIDE_AND_SHY = 3,    // workShyAnd
+  WIDE_AND_SHY_CARD = 4,  // workShyAndCardinality
+  WIDE_AND_NAIVE = 5,  // naive_and chain
+};
+
+struct WideArgs {
+  const CDesc* desc;      // key-major container table
+  const uint32_t* bm;     // input bitmap index per container
+  const uint8_t* payload; // arena
+  const uint8_t* skip;    // naive_and: per input bitmap, 1 = skip (identity with the start)
+  uint32_t start_bm;      // naive_and: input bitmap the chain starts from
+};
+
+void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const uint16_t* kb, int nb, Task* by_key,
+                          uint8_t* flag);
+void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,
+                      Task* by_key, uint8_t* flag);
+void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, Task* tasks, uint32_t* n_tasks);
+void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* tasks, const uint32_t* nt, const CDesc* da,
+                     const uint8_t* pa, const CDesc* db, const uint8_t* pb, ODesc* out, uint8_t* scratch,
+                     uint32_t* task_card);
+void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, ODesc* out,
+                 uint8_t* scratch, uint32_t* task_card);
+void launch_finalize(hipStream_t s, const ODesc* out, const uint32_t* nt, uint32_t* out_idx, uint64_t* out_off,
+                     ResultInfo* info, uint8_t* buf);
+void launch_emit(hipStream_t s, int grid, const ODesc* out, const uint32_t* nt, const uint32_t* out_idx,
+                 const uint64_t* out_off, const ResultInfo* info, uint8_t* buf);
+void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info);
+void launch_ingest(hipStream_t s, const uint8_t* raw, const IngestItem* items, uint64_t n, uint8_t* payload);
+
+// batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch
+void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const CDesc* desc,
+                           const uint8_t* payload, int32_t* out);
+
+// synthetic generators (synth.hip)
+void launch_synth_c2(hipStream_t s, uint64_t seed, CDesc* desc, uint16_t* keys, uint8_t* payload);
+
+}  // namespace rbg

@@ -1,0 +1,540 @@
+// Wide (FastAggregation) kernels, batched andCardinality and synthetic
+// generators.  RB/ = reference RoaringBitmap/src/main/java/org/roaringbitmap/.
+//
+// Wide ops read a key-major batch: the containers of key k from every input sit
+// contiguously (ascending input index) in [key_off[k], key_off[k+1]), and so do
+// their payload slots, so one workgroup streams one key's whole fan-in.
+#include "kernels.hpp"
+
+namespace rbg {
+
+__device__ __forceinline__ void passthrough_w(const CDesc& d, const uint8_t* payload, ODesc* o) {
+  ODesc r;
+  r.src = reinterpret_cast<uint64_t>(payload + d.slot + (d.kind == DK_R ? 2 : 0));
+  r.card = d.card;
+  r.key = d.key;
+  r.kind = d.kind;
+  r.keep = 1;
+  if (d.kind == DK_A) r.ser_len = 2 * d.card;
+  else if (d.kind == DK_B) r.ser_len = 8192;
+  else r.ser_len = 2 + 4 * (uint32_t)(*reinterpret_cast<const uint16_t*>(payload + d.slot + 2));
+  r.pad0 = 0;
+  r.pad1 = 0;
+  *o = r;
+}
+
+__device__ __forceinline__ void write_out(ODesc* o, uint64_t src, uint32_t len, int card, uint32_t key, int kind) {
+  ODesc r;
+  r.src = src;
+  r.ser_len = len;
+  r.card = (uint32_t)card;
+  r.key = (uint16_t)key;
+  r.kind = (uint8_t)kind;
+  r.keep = 1;
+  r.pad0 = 0;
+  r.pad1 = 0;
+  *o = r;
+}
+__device__ __forceinline__ void drop_out(ODesc* o) {
+  ODesc r = {};
+  *o = r;
+}
+
+// Thread-serial OR/XOR of a small array container into LDS (16 B vector loads).
+template <int MODE>
+__device__ __forceinline__ void thread_scatter_array(uint32_t* lds, const uint16_t* vals, int card) {
+  const uint4* v4 = reinterpret_cast<const uint4*>(vals);
+  for (int base = 0; base < card; base += 8) {
+    const uint4 v = v4[base >> 3];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (base + j < card) {
+        const uint32_t x = (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFF;
+        if (MODE == 0) atomicOr(&lds[x >> 5], 1u << (x & 31));
+        else atomicXor(&lds[x >> 5], 1u << (x & 31));
+      }
+    }
+  }
+}
+
+constexpr int kSmallArray = 64;  // arrays up to this size are scattered by one lane
+
+// Accumulate (OR or XOR, no run containers for XOR) every container of a key
+// segment: small arrays lane-serial, large arrays / runs cooperatively into LDS,
+// bitmaps into registers.
+template <int MODE>
+__device__ __forceinline__ void accumulate_segment(const CDesc* desc, const uint8_t* payload, uint32_t s, uint32_t n,
+                                                   uint32_t* acc, int* q, int* big, int* nbig, uint64_t r[4]) {
+  for (uint32_t base = 0; base < n; base += NT) {
+    __syncthreads();
+    if (threadIdx.x == 0) *nbig = 0;
+    __syncthreads();
+    const uint32_t j = base + threadIdx.x;
+    if (j < n) {
+      const CDesc d = desc[s + j];
+      if (d.kind == DK_A && d.card <= (uint32_t)kSmallArray) {
+        thread_scatter_array<MODE>(acc, reinterpret_cast<const uint16_t*>(payload + d.slot), (int)d.card);
+      } else {
+        big[atomicAdd(nbig, 1)] = (int)(s + j);
+      }
+    }
+    __syncthreads();
+    const int nb = *nbig;
+    for (int k = 0; k < nb; k++) {
+      const CDesc d = desc[big[k]];
+      const uint8_t* slot = payload + d.slot;
+      if (d.kind == DK_B) {
+        uint64_t x[4];
+        load_bitmap_owned(slot, x);
+#pragma unroll
+        for (int i = 0; i < 4; i++) r[i] = MODE == 0 ? (r[i] | x[i]) : (r[i] ^ x[i]);
+      } else if (d.kind == DK_A) {
+        lds_scatter_array<MODE>(acc, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
+      } else {
+        const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
+        lds_or_runs(acc, reinterpret_cast<const uint32_t*>(slot + 4), nr, q);
+      }
+    }
+  }
+  __syncthreads();
+  uint64_t x[4];
+  lds_read_owned(acc, x);
+#pragma unroll
+  for (int i = 0; i < 4; i++) r[i] = MODE == 0 ? (r[i] | x[i]) : (r[i] ^ x[i]);
+}
+
+__device__ __forceinline__ int block_card(const uint64_t r[4], int* sh) {
+  int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
+  int u = 0;
+  block_sum2(c, u, sh);
+  return c;
+}
+
+// FastAggregation result types (DESIGN.md §Type contract):
+//   naive_or  (RB/FastAggregation.java:603-610): n == 1 -> clone + repairAfterLazy
+//             (A, B unchanged; R -> toEfficientContainer); n >= 2 -> lazy bitmap
+//             repaired: BY_CARD, 65536 -> R.full (RB/BitmapContainer.java:1205-1215)
+//   workShyAnd (:356-414): 0 dropped, <= 4096 A, 65536 R.full, else B
+//   naive_and (:328-346): iand chain from the smallest input (RB/RoaringBitmap.java:1272-1296)
+//   naive_xor (:637-644): ixor chain with restart after an empty result
+//             (RB/RoaringBitmap.java:3296-3348)
+template <int MODE>
+__global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                              WideArgs A, ODesc* __restrict__ out, uint8_t* __restrict__ scratch,
+                                              uint32_t* __restrict__ task_card) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int q[257];
+  __shared__ int big[NT];
+  __shared__ int nbig;
+  __shared__ int sh[8];
+  const uint32_t nt = *n_tasks;
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const Task tk = tasks[t];
+    const uint32_t s = (uint32_t)tk.a, n = (uint32_t)tk.b;
+    uint8_t* slot = scratch + (size_t)t * kSlotBytes;
+    uint64_t r[4];
+    int kind = DK_A, c = 0;
+
+    if (MODE == WIDE_OR || MODE == WIDE_OR_CARD) {
+      if (n == 1) {
+        const CDesc d = A.desc[s];
+        if (MODE == WIDE_OR_CARD) {
+          if (threadIdx.x == 0) task_card[t] = d.card;
+          continue;
+        }
+        if (d.kind != DK_R) {
+          if (threadIdx.x == 0) passthrough_w(d, A.payload, out + t);
+          continue;
+        }
+        const int nr = *reinterpret_cast<const uint16_t*>(A.payload + d.slot + 2);
+        if (eff((int)d.card, nr) == DK_R) {
+          if (threadIdx.x == 0) passthrough_w(d, A.payload, out + t);
+          continue;
+        }
+        materialize(d, A.payload, tmp, q, r);  // toBitmapOrArrayContainer
+        c = (int)d.card;
+        kind = by_card(c);
+      } else {
+        __syncthreads();
+        lds_clear(acc);
+#pragma unroll
+        for (int i = 0; i < 4; i++) r[i] = 0;
+        accumulate_segment<0>(A.desc, A.payload, s, n, acc, q, big, &nbig, r);
+        c = block_card(r, sh);
+        if (MODE == WIDE_OR_CARD) {
+          if (threadIdx.x == 0) task_card[t] = (uint32_t)c;
+          continue;
+        }
+        kind = c == 65536 ? DK_R : by_card(c);
+      }
+    } else if (MODE == WIDE_XOR) {
+      // does a run container take part in this key's chain?
+      int has_r = 0;
+      for (uint32_t j = threadIdx.x; j < n; j += NT) has_r |= A.desc[s + j].kind == DK_R;
+      has_r = __syncthreads_or(has_r);
+      if (!has_r) {
+        // Without run containers every chain step is BY_CARD, so the type is
+        // BY_CARD of the final set and the empty-restart does not change the set.
+        __syncthreads();
+        lds_clear(acc);
+#pragma unroll
+        for (int i = 0; i < 4; i++) r[i] = 0;
+        accumulate_segment<1>(A.desc, A.payload, s, n, acc, q, big, &nbig, r);
+        c = block_card(r, sh);
+        if (c == 0) {
+          if (threadIdx.x == 0) drop_out(out + t);
+          continue;
+        }
+        kind = by_card(c);
+      } else {
+        // exact replay of the in-place xor chain
+        bool present = false;
+        int clone = -1, st_kind = DK_A, st_card = 0;
+        for (uint32_t j = 0; j < n; j++) {
+          const CDesc d = A.desc[s + j];
+          uint64_t x[4];
+          materialize(d, A.payload, tmp, q, x);
+          if (!present) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) r[i] = x[i];
+            present = true;
+            clone = (int)(s + j);
+            st_kind = d.kind;
+            st_card = (int)d.card;
+            continue;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; i++) r[i] ^= x[i];
+          const int cc = block_card(r, sh);
+          if (cc == 0) {
+            present = false;
+            continue;
+          }
+          const bool need_r = (st_kind == DK_R && d.kind == DK_R) ||
+                              (st_kind == DK_R && d.kind == DK_A && d.card < 32) ||
+                              (st_kind == DK_A && d.kind == DK_R && st_card < 32);
+          st_kind = need_r ? eff(cc, count_runs(r, acc, sh)) : by_card(cc);
+          st_card = cc;
+          clone = -1;
+        }
+        if (!present) {
+          if (threadIdx.x == 0) drop_out(out + t);
+          continue;
+        }
+        if (clone >= 0) {
+          if (threadIdx.x == 0) passthrough_w(A.desc[clone], A.payload, out + t);
+          continue;
+        }
+        c = st_card;
+        kind = st_kind;
+      }
+    } else if (MODE == WIDE_AND_SHY || MODE == WIDE_AND_SHY_CARD) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) r[i] = ~0ULL;
+      for (uint32_t j = 0; j < n; j++) {
+        uint64_t x[4];
+        materialize(A.desc[s + j], A.payload, tmp, q, x);
+#pragma unroll
+        for (int i = 0; i < 4; i++) r[i] &= x[i];
+        if ((j & 3) == 3) {  // an empty intersection stays empty: stop reading inputs
+          const int nz = (r[0] | r[1] | r[2] | r[3]) != 0;
+          if (!__syncthreads_or(nz)) break;
+        }
+      }
+      c = block_card(r, sh);
+      if (MODE == WIDE_AND_SHY_CARD) {
+        if (threadIdx.x == 0) task_card[t] = (uint32_t)c;
+        continue;
+      }
+      if (c == 0) {
+        if (threadIdx.x == 0) drop_out(out + t);
+        continue;
+      }
+      kind = c == 65536 ? DK_R : by_card(c);
+    } else {  // WIDE_AND_NAIVE
+      // start container: the one from input start_bm (segments are sorted by input index)
+      int start = -1;
+      for (uint32_t j = threadIdx.x; j < n; j += NT)
+        if (A.bm[s + j] == A.start_bm) start = (int)(s + j);
+      // reduce: at most one lane found it
+      int st = start;
+      for (int o = 32; o > 0; o >>= 1) st = max(st, __shfl_xor(st, o, 64));
+      if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = st;
+      __syncthreads();
+      start = max(max(sh[0], sh[1]), max(sh[2], sh[3]));
+      __syncthreads();
+      const CDesc d0 = A.desc[start];
+      materialize(d0, A.payload, tmp, q, r);
+      int st_kind = d0.kind, steps = 0;
+      bool empty = false;
+      for (uint32_t j = 0; j < n; j++) {
+        const uint32_t b = A.bm[s + j];
+        if (A.skip[b]) continue;
+        const CDesc d = A.desc[s + j];
+        uint64_t x[4];
+        materialize(d, A.payload, tmp, q, x);
+#pragma unroll
+        for (int i = 0; i < 4; i++) r[i] &= x[i];
+        const int cc = block_card(r, sh);
+        steps++;
+        if (cc == 0) {
+          empty = true;
+          break;
+        }
+        const bool need_r = st_kind == DK_R && d.kind == DK_R;  // R.iand(R) = R.and(R) -> EFF
+        st_kind = need_r ? eff(cc, count_runs(r, acc, sh)) : by_card(cc);
+        c = cc;
+      }
+      if (empty) {
+        if (threadIdx.x == 0) drop_out(out + t);
+        continue;
+      }
+      if (steps == 0) {  // the clone of the smallest input is the answer
+        if (threadIdx.x == 0) passthrough_w(d0, A.payload, out + t);
+        continue;
+      }
+      kind = st_kind;
+    }
+
+    uint64_t src;
+    uint32_t len;
+    emit_container(kind, r, c, slot, acc, tmp, sh, &src, &len);
+    if (threadIdx.x == 0) write_out(out + t, src, len, c, tk.key, kind);
+  }
+}
+
+void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, ODesc* out,
+                 uint8_t* scratch, uint32_t* task_card) {
+  switch (mode) {
+    case WIDE_OR:
+      hipLaunchKernelGGL((k_wide<WIDE_OR>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch, task_card);
+      break;
+    case WIDE_OR_CARD:
+      hipLaunchKernelGGL((k_wide<WIDE_OR_CARD>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch, task_card);
+      break;
+    case WIDE_XOR:
+      hipLaunchKernelGGL((k_wide<WIDE_XOR>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch, task_card);
+      break;
+    case WIDE_AND_SHY:
+      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch, task_card);
+      break;
+    case WIDE_AND_SHY_CARD:
+      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY_CARD>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch,
+                         task_card);
+      break;
+    default:
+      hipLaunchKernelGGL((k_wide<WIDE_AND_NAIVE>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch,
+                         task_card);
+      break;
+  }
+}
+
+// ===========================================================================
+// batched andCardinality (config C4): one wave per pair
+// ===========================================================================
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lds_range_card(const uint32_t* lds, int s, int e) {  // [s, e] inclusive
+  const int ws = s >> 5, we = e >> 5;
+  uint32_t c = 0;
+  for (int w = ws; w <= we; w++) {
+    uint32_t m = ~0u;
+    if (w == ws) m &= ~0u << (s & 31);
+    if (w == we) m &= ~0u >> (31 - (e & 31));
+    c += __popc(lds[w] & m);
+  }
+  return c;
+}
+
+// |x & y| for one matched key, computed by one wave (RB/Container.java:113-126).
+__device__ __forceinline__ uint32_t wave_and_card(const CDesc& x, const CDesc& y, const uint8_t* payload,
+                                                  uint32_t* lds, int lane) {
+  const uint8_t* px = payload + x.slot;
+  const uint8_t* py = payload + y.slot;
+  uint32_t c = 0;
+  if (x.kind == DK_B && y.kind == DK_B) {
+    const uint4* a = reinterpret_cast<const uint4*>(px);
+    const uint4* b = reinterpret_cast<const uint4*>(py);
+    for (int i = lane; i < 512; i += 64) {
+      const uint4 u = a[i], v = b[i];
+      c += __popc(u.x & v.x) + __popc(u.y & v.y) + __popc(u.z & v.z) + __popc(u.w & v.w);
+    }
+  } else {
+    // map = a bitmap operand if any, else the larger one; probe with the other
+    const bool x_is_map = (x.kind == DK_B) || (y.kind != DK_B && x.card >= y.card);
+    const CDesc& m = x_is_map ? x : y;
+    const CDesc& p = x_is_map ? y : x;
+    const uint8_t* pm = x_is_map ? px : py;
+    const uint8_t* pp = x_is_map ? py : px;
+    uint4* l4 = reinterpret_cast<uint4*>(lds);
+    if (m.kind == DK_B) {
+      const uint4* b = reinterpret_cast<const uint4*>(pm);
+      for (int i = lane; i < 512; i += 64) l4[i] = b[i];
+    } else {
+      for (int i = lane; i < 512; i += 64) l4[i] = make_uint4(0, 0, 0, 0);
+      wave_sync();
+      if (m.kind == DK_A) {
+        const uint16_t* v = reinterpret_cast<const uint16_t*>(pm);
+        for (uint32_t i = lane; i < m.card; i += 64) atomicOr(&lds[v[i] >> 5], 1u << (v[i] & 31));
+      } else {
+        const int nr = *reinterpret_cast<const uint16_t*>(pm + 2);
+        const uint32_t* pr = reinterpret_cast<const uint32_t*>(pm + 4);
+        for (int i = lane; i < nr; i += 64) {
+          const uint32_t pq = pr[i];
+          lds_or_run_serial(lds, (int)(pq & 0xFFFF), (int)(pq & 0xFFFF) + (int)(pq >> 16));
+        }
+      }
+    }
+    wave_sync();
+    if (p.kind == DK_A) {
+      const uint16_t* v = reinterpret_cast<const uint16_t*>(pp);
+      for (uint32_t i = lane; i < p.card; i += 64) c += (lds[v[i] >> 5] >> (v[i] & 31)) & 1;
+    } else if (p.kind == DK_R) {
+      const int nr = *reinterpret_cast<const uint16_t*>(pp + 2);
+      const uint32_t* pr = reinterpret_cast<const uint32_t*>(pp + 4);
+      for (int i = lane; i < nr; i += 64) {
+        const uint32_t pq = pr[i];
+        c += lds_range_card(lds, (int)(pq & 0xFFFF), (int)(pq & 0xFFFF) + (int)(pq >> 16));
+      }
+    } else {  // p is a bitmap and m is not (cannot happen: a bitmap is always the map)
+      const uint4* b = reinterpret_cast<const uint4*>(pp);
+      for (int i = lane; i < 512; i += 64) {
+        const uint4 u = l4[i], v = b[i];
+        c += __popc(u.x & v.x) + __popc(u.y & v.y) + __popc(u.z & v.z) + __popc(u.w & v.w);
+      }
+    }
+    wave_sync();
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  return c;
+}
+
+__global__ __launch_bounds__(256) void k_batch_and_card(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
+                                                        const CDesc* __restrict__ desc, const uint8_t* __restrict__ payload,
+                                                        int32_t* __restrict__ out) {
+  __shared__ __align__(16) uint32_t lds[4][2048];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (uint64_t p = (uint64_t)blockIdx.x * 4 + w; p < n_pairs; p += (uint64_t)gridDim.x * 4) {
+    uint32_t ia = bm_off[2 * p], a1 = bm_off[2 * p + 1];
+    uint32_t ib = a1, b1 = bm_off[2 * p + 2];
+    uint32_t sum = 0;  // Java int accumulation (wraps), RB/RoaringBitmap.java:414
+    while (ia < a1 && ib < b1) {
+      const CDesc da = desc[ia], db = desc[ib];
+      if (da.key == db.key) {
+        sum += wave_and_card(da, db, payload, lds[w], lane);
+        ia++;
+        ib++;
+      } else if (da.key < db.key) {
+        ia++;
+      } else {
+        ib++;
+      }
+    }
+    if (lane == 0) out[p] = (int32_t)sum;
+  }
+}
+
+void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const CDesc* desc,
+                           const uint8_t* payload, int32_t* out) {
+  uint64_t g = (n_pairs + 3) / 4;
+  if (g > 16384) g = 16384;
+  if (g == 0) return;
+  hipLaunchKernelGGL(k_batch_and_card, dim3((unsigned)g), dim3(256), 0, s, n_pairs, bm_off, desc, payload, out);
+}
+
+// ===========================================================================
+// synthetic C2 operand: one workgroup per key, written straight into 8208 B slots
+// ===========================================================================
+__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+// 64 Bernoulli(p = thr / 2^32) bits
+__device__ __forceinline__ uint64_t bernoulli_word(uint64_t seed, uint32_t thr) {
+  uint64_t w = 0;
+#pragma unroll 8
+  for (int i = 0; i < 64; i += 2) {
+    const uint64_t h = splitmix(seed + (uint64_t)i);
+    w |= (uint64_t)((uint32_t)h < thr) << i;
+    w |= (uint64_t)((uint32_t)(h >> 32) < thr) << (i + 1);
+  }
+  return w;
+}
+
+__global__ __launch_bounds__(256) void k_synth_c2(uint64_t seed, CDesc* __restrict__ desc, uint16_t* __restrict__ keys,
+                                                  uint8_t* __restrict__ payload) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int q[257];
+  __shared__ int sh[8];
+  for (uint32_t k = blockIdx.x; k < 65536; k += gridDim.x) {
+    const uint64_t hk = splitmix(seed ^ ((uint64_t)k << 20));
+    const int kind_pick = (int)(hk % 3);
+    uint64_t r[4];
+    const uint32_t t = threadIdx.x;
+    const uint32_t widx[4] = {2 * t, 2 * t + 1, 512 + 2 * t, 513 + 2 * t};
+    if (kind_pick != DK_R) {
+      // A: target card U[1,4096]; B: U[4097,65535]; realised by Bernoulli bits
+      const uint32_t target = kind_pick == DK_A ? 1 + (uint32_t)((hk >> 8) % 4096) : 4097 + (uint32_t)((hk >> 8) % 61439);
+      const uint32_t thr = (uint32_t)(((uint64_t)target << 32) / 65536);
+#pragma unroll
+      for (int i = 0; i < 4; i++) r[i] = bernoulli_word(splitmix(hk ^ ((uint64_t)widx[i] * 0x100000001B3ULL)), thr);
+    } else {
+      // R: nr in U[1,2047] runs, one per equal segment, each followed by a gap
+      const int nr = 1 + (int)((hk >> 8) % 2047);
+      const int seg = 65536 / nr;
+      __syncthreads();
+      lds_clear(acc);
+      __syncthreads();
+      for (int i = t; i < nr; i += NT) {
+        const uint64_t h = splitmix(hk + 0x51ULL * (uint64_t)(i + 1));
+        const int half = max(seg / 2, 1);
+        const int start = i * seg + (int)(h % (uint64_t)half);
+        const int maxlen = (i + 1) * seg - 1 - start;  // keeps a gap before the next segment
+        const int len = maxlen > 0 ? 1 + (int)((h >> 32) % (uint64_t)maxlen) : 1;
+        lds_or_run_serial(acc, start, start + len - 1);
+      }
+      __syncthreads();
+      lds_read_owned(acc, r);
+    }
+    int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
+    int u = 0;
+    block_sum2(c, u, sh);
+    if (c == 0) {  // never emit an empty container
+      if (t == 0) r[0] |= 1ULL << (k & 63);
+      c = 1;
+    }
+    int kind;
+    if (kind_pick == DK_R) kind = eff(c, count_runs(r, acc, sh));  // runOptimize of a run container
+    else kind = by_card(c);
+    uint8_t* slot = payload + (size_t)k * kSlotBytes;
+    uint64_t src;
+    uint32_t len;
+    emit_container(kind, r, c, slot, acc, tmp, sh, &src, &len);
+    if (t == 0) {
+      CDesc d;
+      d.slot = (uint64_t)k * kSlotBytes;
+      d.card = (uint32_t)c;
+      d.key = (uint16_t)k;
+      d.kind = (uint8_t)kind;
+      d.flags = 0;
+      desc[k] = d;
+      keys[k] = (uint16_t)k;
+    }
+  }
+}
+
+void launch_synth_c2(hipStream_t s, uint64_t seed, CDesc* desc, uint16_t* keys, uint8_t* payload) {
+  hipLaunchKernelGGL(k_synth_c2, dim3(4096), dim3(256), 0, s, seed, desc, keys, payload);
+}
+
+}  // namespace rbg

@@ -1,0 +1,113 @@
+"""Device-resident session API (rbg_ctx_*): one HIP stream + workspace per context.
+
+Used by bench.py (HIP-event timing on `stream_ptr`) and by multi-GPU sharding
+(`fetch_shard`).  All op calls enqueue asynchronously; `sync()` waits.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, take
+from .roaring import RoaringBitmap
+
+SYNTH_C2, SYNTH_C3_UNIFORM, SYNTH_C3_CLUSTERED, SYNTH_C4_PAIRS = 0, 1, 2, 3
+
+
+class Engine:
+    def __init__(self, device=0):
+        self._ctx = ctypes.c_void_p()
+        check(lib().rbg_ctx_create(int(device), ctypes.byref(self._ctx)))
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            lib().rbg_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream_ptr(self) -> int:
+        return lib().rbg_ctx_stream(self._ctx)
+
+    def sync(self):
+        check(lib().rbg_ctx_sync(self._ctx))
+
+    # ---- batches ------------------------------------------------------------
+    def load(self, bitmaps) -> int:
+        bufs = [b.serialize() if isinstance(b, RoaringBitmap) else bytes(b) for b in bitmaps]
+        arr, lens = _lib.buf_array(bufs)
+        out = ctypes.c_int32()
+        check(lib().rbg_ctx_load(self._ctx, arr, lens, len(bufs), ctypes.byref(out)))
+        return out.value
+
+    def synth(self, kind, seed, n=0, key_lo=0, key_hi=65536) -> int:
+        out = ctypes.c_int32()
+        check(lib().rbg_ctx_synth(self._ctx, int(kind), int(seed), int(n), int(key_lo), int(key_hi),
+                                  ctypes.byref(out)))
+        return out.value
+
+    def release(self, batch):
+        check(lib().rbg_ctx_release(self._ctx, int(batch)))
+
+    def batch_stats(self, batch) -> dict:
+        s = (ctypes.c_int64 * 8)()
+        check(lib().rbg_ctx_batch_stats(self._ctx, int(batch), s))
+        keys = ["bitmaps", "containers", "array", "bitmap", "run", "payload_bytes", "cardinality", "serialized_bytes"]
+        return dict(zip(keys, list(s)))
+
+    def batch_fetch(self, batch, i=0) -> RoaringBitmap:
+        b = _lib.rbg_buffer()
+        check(lib().rbg_ctx_batch_fetch(self._ctx, int(batch), int(i), ctypes.byref(b)))
+        return RoaringBitmap(take(b))
+
+    # ---- ops (asynchronous) -------------------------------------------------------
+    def pairwise(self, op, a, b, ia=0, ib=0):
+        check(lib().rbg_ctx_pairwise(self._ctx, _lib.OP[op], int(a), int(ia), int(b), int(ib)))
+
+    def and_cardinality(self, a, b, ia=0, ib=0):
+        check(lib().rbg_ctx_pairwise_card(self._ctx, 0, int(a), int(ia), int(b), int(ib)))
+
+    def wide(self, op, batch, key_lo=0, key_hi=65536, ids=None):
+        idp = None
+        if ids is not None:
+            idp = (ctypes.c_int32 * len(ids))(*ids)
+        check(lib().rbg_ctx_wide(self._ctx, _lib.WIDE_OP[op], int(batch), int(key_lo), int(key_hi), idp))
+
+    def wide_card(self, op, batch, key_lo=0, key_hi=65536):
+        check(lib().rbg_ctx_wide_card(self._ctx, _lib.WIDE_CARD_OP[op], int(batch), int(key_lo), int(key_hi)))
+
+    def batch_and_card(self, batch):
+        check(lib().rbg_ctx_batch_and_card(self._ctx, int(batch)))
+
+    # ---- results (synchronous) -------------------------------------------------
+    def card(self) -> int:
+        out = ctypes.c_int32()
+        check(lib().rbg_ctx_card(self._ctx, ctypes.byref(out)))
+        return out.value
+
+    def cards(self, n) -> np.ndarray:
+        out = np.zeros(n, dtype=np.int32)
+        check(lib().rbg_ctx_cards(self._ctx, out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), n))
+        return out
+
+    def result_stats(self) -> dict:
+        s = (ctypes.c_int64 * 4)()
+        check(lib().rbg_ctx_result_stats(self._ctx, s))
+        return {"containers": s[0], "payload_bytes": s[1], "has_run": s[2], "cardinality": s[3]}
+
+    def fetch(self) -> RoaringBitmap:
+        b = _lib.rbg_buffer()
+        check(lib().rbg_ctx_fetch(self._ctx, ctypes.byref(b)))
+        return RoaringBitmap(take(b))
+
+    def fetch_shard(self, total_containers, has_run, first_container, payload_base):
+        d, o, p = _lib.rbg_buffer(), _lib.rbg_buffer(), _lib.rbg_buffer()
+        check(lib().rbg_ctx_fetch_shard(self._ctx, int(total_containers), int(has_run), int(first_container),
+                                        int(payload_base), ctypes.byref(d), ctypes.byref(o), ctypes.byref(p)))
+        return take(d), take(o), take(p)

@@ -1,0 +1,309 @@
+"""Host-side mirror of the reference's static-op interface for the hot path.
+
+Mirrors (RB/ = RoaringBitmap/src/main/java/org/roaringbitmap/):
+  * RoaringBitmap static ops and/or/xor/andNot, and/or/xor/andNotCardinality,
+    intersects, or(RoaringBitmap...)        RB/RoaringBitmap.java:377-473,698-720,844,860-1118
+  * FastAggregation and/or/xor (+ Iterator and long[] buffer overloads),
+    andCardinality/orCardinality, naive_and/naive_or/naive_xor, workShyAnd
+                                            RB/FastAggregation.java:26-101,304-414,586-666,823-836
+A RoaringBitmap here is an immutable value holding its portable serialized bytes
+(RB/RoaringArray.java:896-940); every op runs on the MI355X through the C ABI of
+include/roaring_mi355x.h and returns the bytes the reference would serialize.
+Java names that are Python keywords are exposed with a trailing underscore and
+also registered under the Java name (getattr(RoaringBitmap, "and")).
+"""
+import ctypes
+import itertools
+from collections.abc import Iterator
+
+import numpy as np
+
+from . import _lib
+from ._lib import IllegalArgumentException, check, lib, take
+
+EMPTY = bytes.fromhex("3a30000000000000")
+
+
+def _int32(x):
+    return int(np.int64(x).astype(np.int32)) if -(1 << 63) <= x < (1 << 63) else int(x)
+
+
+class RoaringBitmap:
+    __slots__ = ("_buf", "_lcard")
+
+    def __init__(self, serialized: bytes = None):
+        self._buf = EMPTY if serialized is None else bytes(serialized)
+        self._lcard = None
+
+    # ---- construction -----------------------------------------------------
+    @classmethod
+    def bitmapOf(cls, *values):
+        """RoaringBitmap.bitmapOf(int...) (RB/RoaringBitmap.java:566-570); ints taken as unsigned 32-bit."""
+        if len(values) == 1 and not isinstance(values[0], (int, np.integer)):
+            values = values[0]
+        return cls.from_values(values)
+
+    @classmethod
+    def from_values(cls, values, run_optimize=False):
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64).astype(np.uint32))
+        b = _lib.rbg_buffer()
+        check(lib().rbg_from_values(v.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), v.size, int(run_optimize),
+                                    ctypes.byref(b)))
+        return cls(take(b))
+
+    @classmethod
+    def deserialize(cls, data: bytes):
+        """RoaringBitmap.deserialize: raises InvalidRoaringFormat / TruncatedInput (both OSError)."""
+        consumed = ctypes.c_size_t()
+        card = ctypes.c_int64()
+        stats = (ctypes.c_int64 * 3)()
+        data = bytes(data)
+        check(lib().rbg_inspect(data, len(data), ctypes.byref(consumed), ctypes.byref(card), stats))
+        out = cls(data[:consumed.value])
+        out._lcard = card.value
+        return out
+
+    def runOptimize(self) -> bool:
+        """In-place runOptimize (RB/RoaringBitmap.java:2764-2774); True if a run container results."""
+        b = _lib.rbg_buffer()
+        check(lib().rbg_run_optimize(self._buf, len(self._buf), ctypes.byref(b)))
+        self._buf = take(b)
+        return self.container_stats()[2] > 0
+
+    def clone(self):
+        return RoaringBitmap(self._buf)
+
+    # ---- inspection ---------------------------------------------------------
+    def serialize(self) -> bytes:
+        return self._buf
+
+    def serializedSizeInBytes(self) -> int:
+        return len(self._buf)
+
+    def getLongCardinality(self) -> int:
+        if self._lcard is None:
+            card = ctypes.c_int64()
+            check(lib().rbg_inspect(self._buf, len(self._buf), None, ctypes.byref(card), None))
+            self._lcard = card.value
+        return self._lcard
+
+    def getCardinality(self) -> int:
+        """Java int cast of the long cardinality (RB/RoaringBitmap.java:1966-1968)."""
+        return _int32(self.getLongCardinality())
+
+    def isEmpty(self) -> bool:
+        return self.getLongCardinality() == 0
+
+    def container_stats(self):
+        """(#array, #bitmap, #run) containers, as RB/insights/BitmapAnalyser reports."""
+        stats = (ctypes.c_int64 * 3)()
+        check(lib().rbg_inspect(self._buf, len(self._buf), None, None, stats))
+        return tuple(stats)
+
+    def toArray(self) -> np.ndarray:
+        b = _lib.rbg_buffer()
+        check(lib().rbg_to_values(self._buf, len(self._buf), ctypes.byref(b)))
+        raw = take(b)
+        return np.frombuffer(raw, dtype=np.uint32).copy()
+
+    def __len__(self):
+        return self.getLongCardinality()
+
+    def __eq__(self, other):
+        return isinstance(other, RoaringBitmap) and self._buf == other._buf
+
+    def __hash__(self):
+        return hash(self._buf)
+
+    def __repr__(self):
+        a, b, r = self.container_stats()
+        return f"RoaringBitmap(card={self.getLongCardinality()}, containers=A{a}/B{b}/R{r}, bytes={len(self._buf)})"
+
+    # ---- static pairwise ops (RB/RoaringBitmap.java) --------------------------
+    @staticmethod
+    def _pair(op, x1, x2):
+        b = _lib.rbg_buffer()
+        check(lib().rbg_pairwise(_lib.OP[op], x1._buf, len(x1._buf), x2._buf, len(x2._buf), ctypes.byref(b)))
+        return RoaringBitmap(take(b))
+
+    @staticmethod
+    def _card(op, x1, x2):
+        out = ctypes.c_int32()
+        check(lib().rbg_pairwise_card(_lib.CARD_OP[op], x1._buf, len(x1._buf), x2._buf, len(x2._buf),
+                                      ctypes.byref(out)))
+        return out.value
+
+    @staticmethod
+    def and_(x1, x2):
+        """static and(x1, x2), RB/RoaringBitmap.java:377-401"""
+        return RoaringBitmap._pair("and", x1, x2)
+
+    @staticmethod
+    def or_(*bitmaps):
+        """static or(x1, x2) (:860-902); any other arity is or(RoaringBitmap...) (:844) = FastAggregation.or"""
+        if len(bitmaps) == 2:
+            return RoaringBitmap._pair("or", bitmaps[0], bitmaps[1])
+        return FastAggregation.or_(*bitmaps)
+
+    @staticmethod
+    def xor(x1, x2):
+        """static xor(x1, x2), :1071-1118"""
+        return RoaringBitmap._pair("xor", x1, x2)
+
+    @staticmethod
+    def andNot(x1, x2):
+        """static andNot(x1, x2), :444-473"""
+        return RoaringBitmap._pair("andnot", x1, x2)
+
+    @staticmethod
+    def andCardinality(x1, x2) -> int:
+        """:413-434 (Java int, wraps)"""
+        return RoaringBitmap._card("and", x1, x2)
+
+    @staticmethod
+    def orCardinality(x1, x2) -> int:
+        """:916-920"""
+        return RoaringBitmap._card("or", x1, x2)
+
+    @staticmethod
+    def xorCardinality(x1, x2) -> int:
+        """:931-933"""
+        return RoaringBitmap._card("xor", x1, x2)
+
+    @staticmethod
+    def andNotCardinality(x1, x2) -> int:
+        """:944-985"""
+        return RoaringBitmap._card("andnot", x1, x2)
+
+    @staticmethod
+    def intersects(x1, x2) -> bool:
+        """:698-720"""
+        return RoaringBitmap._card("intersects", x1, x2) != 0
+
+
+setattr(RoaringBitmap, "and", RoaringBitmap.and_)
+setattr(RoaringBitmap, "or", RoaringBitmap.or_)
+
+
+def _identity_ids(bitmaps):
+    seen = {}
+    return [seen.setdefault(id(b), len(seen)) for b in bitmaps]
+
+
+def _wide(op, bitmaps, ids=None):
+    bufs = [b._buf for b in bitmaps]
+    arr, lens = _lib.buf_array(bufs)
+    idp = None
+    if ids is not None and bitmaps:
+        idp = (ctypes.c_int32 * len(ids))(*ids)
+    b = _lib.rbg_buffer()
+    check(lib().rbg_wide(_lib.WIDE_OP[op], arr, lens, idp, len(bufs), ctypes.byref(b)))
+    return RoaringBitmap(take(b))
+
+
+def _wide_card(op, bitmaps):
+    bufs = [b._buf for b in bitmaps]
+    arr, lens = _lib.buf_array(bufs)
+    out = ctypes.c_int32()
+    check(lib().rbg_wide_card(_lib.WIDE_CARD_OP[op], arr, lens, len(bufs), ctypes.byref(out)))
+    return out.value
+
+
+def _split_args(args):
+    """Java overloads: (Iterator) vs (RoaringBitmap...) vs (long[] buffer, RoaringBitmap...)."""
+    if len(args) == 1 and isinstance(args[0], Iterator):
+        return "iter", None, list(args[0])
+    if args and isinstance(args[0], np.ndarray):
+        return "buffer", args[0], list(args[1:])
+    if len(args) == 1 and isinstance(args[0], (list, tuple)):
+        return "varargs", None, list(args[0])
+    return "varargs", None, list(args)
+
+
+class FastAggregation:
+    """RB/FastAggregation.java static methods."""
+
+    @staticmethod
+    def and_(*args):
+        """and(RoaringBitmap...) :37-42, and(long[], RoaringBitmap...) :51-63, and(Iterator) :26-28"""
+        kind, buf, bms = _split_args(args)
+        if kind == "iter":
+            return _wide("and_iter", bms)
+        if kind == "buffer" and len(bms) > 10:
+            if buf.size < 1024:
+                raise IllegalArgumentException("buffer should have at least 1024 elements.")
+            try:
+                return _wide("and", bms, _identity_ids(bms))
+            finally:
+                buf[...] = 0  # Arrays.fill(aggregationBuffer, 0L)
+        return _wide("and", bms, _identity_ids(bms))
+
+    @staticmethod
+    def or_(*args):
+        """or(RoaringBitmap...) :664-666 and or(Iterator) :653-655 -> naive_or"""
+        _, _, bms = _split_args(args)
+        return _wide("or", bms)
+
+    @staticmethod
+    def xor(*args):
+        """xor(RoaringBitmap...) :834-836 and xor(Iterator) :823-825 -> naive_xor"""
+        _, _, bms = _split_args(args)
+        return _wide("xor", bms)
+
+    @staticmethod
+    def naive_or(*args):
+        _, _, bms = _split_args(args)
+        return _wide("or", bms)
+
+    @staticmethod
+    def naive_xor(*args):
+        _, _, bms = _split_args(args)
+        return _wide("xor", bms)
+
+    @staticmethod
+    def naive_and(*args):
+        """naive_and(RoaringBitmap...) :328-346 for any N, naive_and(Iterator) :304-313"""
+        kind, _, bms = _split_args(args)
+        if kind == "iter":
+            return _wide("and_iter", bms)
+        return _wide("naive_and", bms, _identity_ids(bms))
+
+    @staticmethod
+    def workShyAnd(buffer, *bitmaps):
+        """workShyAnd(long[] buffer, RoaringBitmap...) :356-414"""
+        bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
+        return _wide("workshy_and", bms)
+
+    @staticmethod
+    def andCardinality(*args) -> int:
+        """:71-82"""
+        _, _, bms = _split_args(args)
+        return _wide_card("and", bms)
+
+    @staticmethod
+    def orCardinality(*args) -> int:
+        """:90-101"""
+        _, _, bms = _split_args(args)
+        return _wide_card("or", bms)
+
+
+setattr(FastAggregation, "and", FastAggregation.and_)
+setattr(FastAggregation, "or", FastAggregation.or_)
+
+
+def batch_and_cardinality(pairs):
+    """out[i] = RoaringBitmap.andCardinality(a_i, b_i) for (a_i, b_i) in pairs (config C4)."""
+    pairs = list(pairs)
+    n = len(pairs)
+    if n == 0:
+        return np.zeros(0, dtype=np.int32)
+    a_arr, a_lens = _lib.buf_array([p[0]._buf for p in pairs])
+    b_arr, b_lens = _lib.buf_array([p[1]._buf for p in pairs])
+    out = np.zeros(n, dtype=np.int32)
+    check(lib().rbg_batch_and_card(n, a_arr, a_lens, b_arr, b_lens,
+                                   out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))))
+    return out
+
+
+def _chain(*its):
+    return itertools.chain(*its)

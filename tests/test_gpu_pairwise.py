@@ -1,0 +1,142 @@
+"""Pairwise static ops on the MI355X vs the CPU oracle: byte-identical output.
+
+RB/RoaringBitmap.java and :377, or :860, xor :1071, andNot :444, andCardinality :413,
+or/xor/andNotCardinality :916-985, intersects :698.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import _gen
+import _oracle as O
+from _fmt import decode, encode, R
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+OPS = ["and", "or", "xor", "andnot"]
+CARDS = ["and", "or", "xor", "andnot", "intersects"]
+
+
+def _rb():
+    import roaringbitmap_amd as rb
+    return rb
+
+
+def gpu_pair(op, a, b):
+    rb = _rb()
+    return rb.RoaringBitmap._pair(op, rb.RoaringBitmap(a), rb.RoaringBitmap(b)).serialize()
+
+
+def gpu_card(op, a, b):
+    rb = _rb()
+    return rb.RoaringBitmap._card(op, rb.RoaringBitmap(a), rb.RoaringBitmap(b))
+
+
+def check_all(a, b, label=""):
+    for op in OPS:
+        exp = O.pairwise(op, a, b)
+        got = gpu_pair(op, a, b)
+        if got != exp:
+            de, dg = decode(exp), decode(got)
+            diff = [(x[0], x[1], x[2], y[1], y[2]) for x, y in zip(de, dg) if x[:3] != y[:3]]
+            raise AssertionError(f"{label} {op}: {len(de)} vs {len(dg)} containers; first (key, kind, card) "
+                                 f"diffs exp/got: {diff[:5]}")
+    for op in CARDS:
+        assert gpu_card(op, a, b) == O.pairwise_card(op, a, b), (label, op)
+
+
+def test_every_container_mode_pair(gpu):
+    """All 18x18 container-mode combinations on one key (type thresholds)."""
+    rng = np.random.default_rng(7)
+    for m1 in _gen.MODES:
+        for m2 in _gen.MODES:
+            k1, v1 = _gen.container(rng, m1)
+            k2, v2 = _gen.container(rng, m2)
+            check_all(encode([(3, k1, v1)]), encode([(3, k2, v2)]), f"{m1}x{m2}")
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_bitmaps(gpu, seed):
+    rng = np.random.default_rng(seed)
+    keys = np.sort(rng.choice(64, size=int(rng.integers(1, 40)), replace=False))
+    check_all(_gen.bitmap(rng, keys), _gen.bitmap(rng, keys), f"seed{seed}")
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_perturbed_pairs(gpu, seed):
+    rng = np.random.default_rng(100 + seed)
+    keys = np.sort(rng.choice(1 << 16, size=30, replace=False))
+    a, b = _gen.perturbed_pair(rng, keys)
+    check_all(a, b, f"pert{seed}")
+    check_all(b, a, f"pert{seed}r")
+
+
+def test_empty_and_disjoint(gpu):
+    empty = encode([])
+    rng = np.random.default_rng(5)
+    x = _gen.bitmap(rng, np.arange(10))
+    y = _gen.bitmap(rng, np.arange(100, 110))
+    check_all(empty, empty, "empty")
+    check_all(empty, x, "empty-x")
+    check_all(x, empty, "x-empty")
+    check_all(x, y, "disjoint")
+    check_all(x, x, "self")
+
+
+def test_golden_files(gpu):
+    a = open(os.path.join(GOLD, "testdata", "bitmapwithruns.bin"), "rb").read()
+    b = open(os.path.join(GOLD, "testdata", "bitmapwithoutruns.bin"), "rb").read()
+    check_all(a, b, "golden")
+    check_all(b, a, "golden-r")
+
+
+def test_header_variants(gpu):
+    """size < 4 with runs omits the offset table (RB/RoaringArray.java:927-933)."""
+    full = np.arange(65536, dtype=np.uint16)
+    for n in range(1, 6):
+        a = encode([(k, R, full[: 100 + k]) for k in range(n)])
+        b = encode([(k, R, full[50 + k: 300]) for k in range(n)])
+        check_all(a, b, f"runs{n}")
+
+
+def _realdata(ds):
+    z = np.load(os.path.join(GOLD, "realdata", ds + ".npz"))
+    v, o = z["values"], z["offsets"]
+    return [v[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+
+
+@pytest.mark.parametrize("ds", ["census1881", "census1881_srt", "wikileaks-noquotes", "uscensus2000"])
+@pytest.mark.parametrize("run_opt", [False, True])
+def test_realdata_known_answers(gpu, ds, run_opt):
+    rb = _rb()
+    known = json.load(open(os.path.join(GOLD, "known_answers.json")))["values"][ds]
+    bms = [rb.RoaringBitmap.from_values(s, run_opt) for s in _realdata(ds)]
+    sums = {op: 0 for op in OPS}
+    for k in range(len(bms) - 1):
+        for op in OPS:
+            got = rb.RoaringBitmap._pair(op, bms[k], bms[k + 1])
+            sums[op] += got.getLongCardinality()
+            if k % 20 == 0:
+                assert got.serialize() == O.pairwise(op, bms[k].serialize(), bms[k + 1].serialize())
+        assert rb.RoaringBitmap.andCardinality(bms[k], bms[k + 1]) == O.pairwise_card(
+            "and", bms[k].serialize(), bms[k + 1].serialize())
+    for op in OPS:
+        assert sums[op] == known[op], op
+
+
+def test_java_int_wrap(gpu):
+    full = encode([(k, R, np.arange(65536, dtype=np.uint16)) for k in range(32768)])
+    assert gpu_card("and", full, full) == -(1 << 31)
+    assert gpu_card("or", full, full) == -(1 << 31)
+    assert gpu_card("intersects", full, full) == 1
+
+
+@pytest.mark.parametrize("i", range(1, 8))
+def test_bad_inputs_raise_ioerror(gpu, i):
+    rb = _rb()
+    bad = open(os.path.join(GOLD, "testdata", f"crashproneinput{i}.bin"), "rb").read()
+    good = encode([])
+    with pytest.raises(OSError):
+        rb.RoaringBitmap._pair("and", rb.RoaringBitmap(bad), rb.RoaringBitmap(good))

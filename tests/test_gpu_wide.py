@@ -1,0 +1,101 @@
+"""FastAggregation wide ops on the MI355X vs the CPU oracle (byte-identical).
+
+RB/FastAggregation.java: and :37-42 (workShyAnd :356-414 for N>10, naive_and
+:328-346 otherwise), and(Iterator) :26-28, or :664-666 (naive_or :603-610),
+xor :834-836 (naive_xor :637-644), andCardinality :71-82, orCardinality :90-101.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import _gen
+import _oracle as O
+from _fmt import decode
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _rb():
+    import roaringbitmap_amd as rb
+    return rb
+
+
+def gpu_wide(op, bufs, ids=None):
+    rb = _rb()
+    from roaringbitmap_amd.roaring import _wide
+    return _wide(op, [rb.RoaringBitmap(b) for b in bufs], ids).serialize()
+
+
+def gpu_wide_card(op, bufs):
+    rb = _rb()
+    from roaringbitmap_amd.roaring import _wide_card
+    return _wide_card(op, [rb.RoaringBitmap(b) for b in bufs])
+
+
+def _cmp(op, bufs, ids=None):
+    exp = O.wide(op, bufs, ids)
+    got = gpu_wide(op, bufs, ids)
+    if got != exp:
+        de, dg = decode(exp), decode(got)
+        diff = [(x[0], x[1], x[2], y[1], y[2]) for x, y in zip(de, dg) if x[:3] != y[:3]]
+        raise AssertionError(f"{op} N={len(bufs)}: {len(de)} vs {len(dg)} containers; diffs {diff[:5]}")
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 10, 11, 16])
+def test_wide_random(gpu, n):
+    rng = np.random.default_rng(50 + n)
+    keys = np.arange(10)
+    bufs = [_gen.bitmap(rng, keys, p_present=0.9) for _ in range(n)]
+    for op in ["or", "xor", "and", "and_iter", "naive_and"]:
+        _cmp(op, bufs, list(range(n)))
+    if n:
+        _cmp("workshy_and", bufs)
+    for op in ["and", "or"]:
+        assert gpu_wide_card(op, bufs) == O.wide_card(op, bufs), op
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_wide_dense_overlap(gpu, seed):
+    """inputs restricted to modes whose intersections stay non-empty"""
+    rng = np.random.default_rng(900 + seed)
+    modes = ["b_dense", "full_b", "full_r", "r_dense", "r_few", "b_mid"]
+    n = [2, 4, 7, 10, 12, 20][seed]
+    bufs = [_gen.bitmap(rng, np.arange(6), modes=modes, p_present=1.0) for _ in range(n)]
+    for op in ["or", "xor", "and", "and_iter", "naive_and", "workshy_and"]:
+        _cmp(op, bufs, list(range(n)))
+    assert gpu_wide_card("and", bufs) == O.wide_card("and", bufs)
+    assert gpu_wide_card("or", bufs) == O.wide_card("or", bufs)
+
+
+def test_wide_identity_skip(gpu):
+    """naive_and skips inputs that are the smallest object (RB/FastAggregation.java:341)"""
+    rng = np.random.default_rng(3)
+    small = _gen.bitmap(rng, np.arange(3), modes=["r_few", "r_tie", "r_many"], p_present=1.0)
+    big = _gen.bitmap(rng, np.arange(8), modes=["r_dense", "full_r"], p_present=1.0)
+    bufs = [big, small, big, small]
+    _cmp("and", bufs, [0, 1, 0, 1])
+    _cmp("and", bufs, [0, 1, 2, 3])
+
+
+def _realdata(ds):
+    z = np.load(os.path.join(GOLD, "realdata", ds + ".npz"))
+    v, o = z["values"], z["offsets"]
+    return [v[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+
+
+@pytest.mark.parametrize("run_opt", [False, True])
+def test_wide_realdata(gpu, run_opt):
+    import json
+    known = json.load(open(os.path.join(GOLD, "known_answers.json")))["values"]
+    for ds in ["census1881", "census1881_srt", "wikileaks-noquotes_srt"]:
+        bufs = [O.from_values(s, run_opt) for s in _realdata(ds)]
+        _cmp("or", bufs)
+        _cmp("and", bufs)
+        _cmp("xor", bufs)
+        rb = _rb()
+        got = rb.FastAggregation.or_(*[rb.RoaringBitmap(b) for b in bufs])
+        assert got.getLongCardinality() == known[ds]["wide_or"]
+        got = rb.FastAggregation.and_(iter([rb.RoaringBitmap(b) for b in bufs]))
+        assert got.getLongCardinality() == known[ds]["wide_and"]
