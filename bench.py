@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Benchmark: pairwise AND of two full 2^32-universe bitmaps (BASELINE.json configs[1], "C2").
+
+One step = RoaringBitmap.and(x1, x2) over a device-resident C2 pair (65,536 mixed
+array/bitmap/run containers each, generated on the GPU), producing the
+device-resident portable-format result.  Key plan, container kernel and result
+assembly are all inside the step.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per
+GPU; each rank owns an independent C2 pair (weak scaling, no data-path collective);
+barrier + synchronize bracket the timed loop and the max time over ranks is used.
+
+Prints ONE JSON line (rank 0).  Extra fields:
+  roofline     - dominant kernel (container compute) achieved algorithmic GB/s vs
+                 the 8 TB/s HBM peak, timed with HIP events on the engine's stream
+  cpu_baseline - the CPU oracle (C++ restatement, 1 thread) on the same pair
+  extra        - per-phase times, container mix, result size
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "wide-OR/pairwise-AND input GB/s + % of HBM peak at 1/2/4/8 MI355X"
+
+
+def _pmc_traffic():
+    """Per-launch HBM bytes of the compute kernel from a committed rocprofv3 --pmc pass."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        with open(p) as f:
+            return json.load(f).get("k_pairwise_and", {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from roaringbitmap_amd import Engine
+
+    eng = Engine(local)
+    a = eng.synth(0, 0xC2A0 + 0x10000 * rank)
+    b = eng.synth(0, 0xC2B0 + 0x10000 * rank)
+    sa, sb = eng.batch_stats(a), eng.batch_stats(b)
+    # algorithmic bytes: AND reads the descriptors of both operands and the
+    # payload of matched pairs (every key matches here); writes the result payload + 4 B/container
+    in_bytes = sa["payload_bytes"] + sb["payload_bytes"] + 4 * (sa["containers"] + sb["containers"])
+    eng.pairwise("and", a, b)
+    rs = eng.result_stats()
+    out_bytes = rs["payload_bytes"] + 4 * rs["containers"]
+
+    stream = torch.cuda.ExternalStream(eng.stream_ptr)
+    for _ in range(args.warmup):
+        eng.pairwise("and", a, b)
+    eng.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        eng.pairwise("and", a, b)
+    ev1.record(stream)
+    eng.sync()
+    barrier()
+    wall = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+
+    # per-phase device time of the same op (separate pass: events between phases)
+    eng.profile(args.steps)
+    for _ in range(args.steps):
+        eng.pairwise("and", a, b)
+    n_ops, ph = eng.profile_read()
+    eng.profile(0)
+    ph_avg = [x / max(n_ops, 1) for x in ph]
+
+    t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum[1:], op=dist.ReduceOp.SUM)
+        wall_max, total_in = float(tmax[0]), float(tsum[1])
+    else:
+        wall_max, total_in = wall, float(in_bytes)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O  # CPU baseline leg only
+        xa = eng.batch_fetch(a).serialize()
+        xb = eng.batch_fetch(b).serialize()
+        t1 = O.time_pairwise("and", xa, xb, 1)
+        reps = max(1, int(math.ceil(args.cpu_seconds / max(t1, 1e-3))))
+        tc = O.time_pairwise("and", xa, xb, reps)
+        cpu = {"value": round(in_bytes * reps / tc / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+               "sample": f"full C2 pair (same bytes as the GPU step), {reps} x RoaringBitmap.and on the C++ "
+                         f"restatement oracle/rbcpu (JVM reference not runnable: no JDK), {tc:.1f} s"}
+
+    if rank == 0:
+        step_s = wall_max / args.steps
+        compute_s = ph_avg[1] / 1e3
+        achieved = (in_bytes + out_bytes) / compute_s / 1e9 if compute_s > 0 else 0.0
+        line = {
+            "metric": METRIC,
+            "value": round(total_in / (wall_max / args.steps) / 1e9, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_s * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": "C2: RoaringBitmap.and(x1, x2), two full 2^32-universe bitmaps of 65536 "
+                                   "mixed array/bitmap/run containers each (configs[1])",
+                       "per_rank": "one independent C2 pair per GPU", "parallelism": f"dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(),
+                         "kernel": "k_pairwise<AND> (container compute)",
+                         "bytes_per_launch": int(in_bytes + out_bytes)},
+            "cpu_baseline": cpu,
+            "extra": {
+                "input_bytes_per_step": int(in_bytes), "output_bytes_per_step": int(out_bytes),
+                "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
+                "phase_ms": {"plan": round(ph_avg[0], 4), "compute": round(ph_avg[1], 4),
+                             "assemble": round(ph_avg[2], 4)},
+                "elements_per_s": round((sa["cardinality"] + sb["cardinality"]) * world / step_s, 1),
+                "operand_mix": {k: [sa[k], sb[k]] for k in ["array", "bitmap", "run"]},
+                "result": rs,
+                "input_frac_of_peak": round(total_in / step_s / 1e9 / world / HBM_PEAK_GBS, 4),
+            },
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

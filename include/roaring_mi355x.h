@@ -128,6 +128,12 @@ void rbg_ctx_destroy(rbg_ctx* ctx);
 /* hipStream_t of the context, for HIP-event timing by the caller */
 void* rbg_ctx_stream(rbg_ctx* ctx);
 int rbg_ctx_sync(rbg_ctx* ctx);
+/* HIP-event phase timing on the context stream: enable for up to max_ops ops (0 disables).
+ * rbg_ctx_profile_read returns the summed device time of the recorded ops in three phases:
+ * ms3[0] = key plan + compaction, ms3[1] = container compute kernel, ms3[2] = result
+ * assembly (finalize + emit / reduction), and resets the record. */
+int rbg_ctx_profile(rbg_ctx* ctx, int max_ops);
+int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops);
 
 /* Parse + upload n serialized bitmaps as one batch; returns a batch id >= 0. */
 int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n,

@@ -34,7 +34,7 @@ EXPORTED = [
     "rbg_ctx_load", "rbg_ctx_synth", "rbg_ctx_release", "rbg_ctx_batch_stats", "rbg_ctx_batch_fetch",
     "rbg_ctx_pairwise", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
     "rbg_ctx_batch_and_card", "rbg_ctx_card", "rbg_ctx_cards", "rbg_ctx_result_stats", "rbg_ctx_fetch",
-    "rbg_ctx_fetch_shard",
+    "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read",
 ]
 
 _lib = None
@@ -80,6 +80,8 @@ def _declare(L):
     L.rbg_ctx_cards.argtypes = [vp, P(i32), sz]
     L.rbg_ctx_result_stats.argtypes = [vp, P(ctypes.c_int64)]
     L.rbg_ctx_fetch.argtypes = [vp, buf]
+    L.rbg_ctx_profile.argtypes = [vp, ctypes.c_int]
+    L.rbg_ctx_profile_read.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_int)]
     L.rbg_ctx_fetch_shard.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, buf, buf,
                                       buf]
 

@@ -89,7 +89,21 @@ struct Ctx {
   int last = 0;  // 0 none, 1 serialized result, 2 cardinality, 3 batch cardinalities
   void* pinned = nullptr;
   size_t pinned_cap = 0;
+  // HIP-event phase timing: 4 events per op (start, after plan+compact, after
+  // compute, after finalize+emit); read back without per-op host syncs.
+  std::vector<hipEvent_t> prof_ev;
+  size_t prof_cap = 0, prof_n = 0;
+  void prof_free() {
+    for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
+    prof_ev.clear();
+    prof_cap = prof_n = 0;
+  }
+  void mark(int phase) {
+    if (prof_n < prof_cap) (void)hipEventRecord(prof_ev[4 * prof_n + phase], stream);
+    if (phase == 3 && prof_n < prof_cap) prof_n++;
+  }
   ~Ctx() {
+    prof_free();
     if (pinned) (void)hipHostFree(pinned);
     batches.clear();
     if (stream) (void)hipStreamDestroy(stream);
@@ -327,11 +341,14 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     default: ub = std::min<size_t>((size_t)na + nb, kMaxKeys); break;
   }
   if (!card_only) CHK(ensure_outputs(c, ub, A->payload_bytes + B->payload_bytes + (size_t)kSlotBytes * ub));
+  c->mark(0);
   launch_plan_pairwise(s, plan_op, ka, na, kb, nb, c->by_key.as<Task>(), c->flag.as<uint8_t>());
   launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->tasks.as<Task>(), c->ntasks.as<uint32_t>());
+  c->mark(1);
   launch_pairwise(s, op, card_only ? 1 : 0, grid_for(ub), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), da,
                   A->payload.as<uint8_t>(), db, B->payload.as<uint8_t>(), c->out.as<ODesc>(), c->scratch.as<uint8_t>(),
                   c->task_card.as<uint32_t>());
+  c->mark(2);
   if (card_only) {
     launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
     c->last = 2;
@@ -342,6 +359,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
                 c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
     c->last = 1;
   }
+  c->mark(3);
   HIPCHK(hipGetLastError());
   return RBG_OK;
 }
@@ -425,6 +443,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
       HIPCHK(hipMemcpyAsync(c->skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
     }
     const uint32_t n_req = plan_mode == 2 ? 0xFFFFFFFFu : (uint32_t)N;
+    c->mark(0);
     launch_plan_wide(s, plan_mode == 0 ? 0 : 1, B->key_off.as<uint32_t>(), n_req, key_lo, key_hi,
                      c->by_key.as<Task>(), c->flag.as<uint8_t>());
     launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->tasks.as<Task>(), c->ntasks.as<uint32_t>());
@@ -434,8 +453,10 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.payload = B->payload.as<uint8_t>();
     wa.skip = skip.empty() ? nullptr : c->skip.as<uint8_t>();
     wa.start_bm = start_bm;
+    c->mark(1);
     launch_wide(s, mode, 4096, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, c->out.as<ODesc>(),
                 c->scratch.as<uint8_t>(), c->task_card.as<uint32_t>());
+    c->mark(2);
     if (card_only) {
       launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
       c->last = 2;
@@ -446,6 +467,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
                   c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
       c->last = 1;
     }
+    c->mark(3);
     HIPCHK(hipGetLastError());
   }
   return RBG_OK;
@@ -637,8 +659,12 @@ static int ctx_batch_card(Ctx* c, int32_t id) {
     set_err("batched andCardinality needs a bitmap-major batch");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
+  c->mark(0);
+  c->mark(1);
   launch_batch_and_card(c->stream, np, B->bm_off.as<uint32_t>(), B->desc.as<CDesc>(), B->payload.as<uint8_t>(),
                         c->cards.as<int32_t>());
+  c->mark(2);
+  c->mark(3);
   HIPCHK(hipGetLastError());
   c->n_cards = np;
   c->last = 3;
@@ -816,6 +842,33 @@ void rbg_ctx_destroy(rbg_ctx* ctx) {
   delete ctx;
 }
 void* rbg_ctx_stream(rbg_ctx* ctx) { return ctx ? (void*)ctx->c.stream : nullptr; }
+int rbg_ctx_profile(rbg_ctx* ctx, int max_ops) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  HIPCHK(hipStreamSynchronize(ctx->c.stream));
+  ctx->c.prof_free();
+  if (max_ops <= 0) return RBG_OK;
+  ctx->c.prof_ev.resize(4 * (size_t)max_ops);
+  for (hipEvent_t& e : ctx->c.prof_ev) HIPCHK(hipEventCreate(&e));
+  ctx->c.prof_cap = (size_t)max_ops;
+  ctx->c.prof_n = 0;
+  return RBG_OK;
+}
+int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops) {
+  Ctx& c = ctx->c;
+  HIPCHK(hipSetDevice(c.device));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  ms3[0] = ms3[1] = ms3[2] = 0.0;
+  for (size_t i = 0; i < c.prof_n; i++) {
+    for (int ph = 0; ph < 3; ph++) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, c.prof_ev[4 * i + ph], c.prof_ev[4 * i + ph + 1]));
+      ms3[ph] += ms;
+    }
+  }
+  *n_ops = (int)c.prof_n;
+  c.prof_n = 0;
+  return RBG_OK;
+}
 int rbg_ctx_sync(rbg_ctx* ctx) {
   HIPCHK(hipSetDevice(ctx->c.device));
   HIPCHK(hipStreamSynchronize(ctx->c.stream));

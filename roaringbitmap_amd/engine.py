@@ -38,6 +38,17 @@ class Engine:
     def sync(self):
         check(lib().rbg_ctx_sync(self._ctx))
 
+    def profile(self, max_ops):
+        """Enable HIP-event phase timing for the next `max_ops` ops (0 disables)."""
+        check(lib().rbg_ctx_profile(self._ctx, int(max_ops)))
+
+    def profile_read(self):
+        """-> (n_ops, [plan_ms, compute_ms, assemble_ms]) summed over the recorded ops."""
+        ms = (ctypes.c_double * 3)()
+        n = ctypes.c_int()
+        check(lib().rbg_ctx_profile_read(self._ctx, ms, ctypes.byref(n)))
+        return n.value, list(ms)
+
     # ---- batches ------------------------------------------------------------
     def load(self, bitmaps) -> int:
         bufs = [b.serialize() if isinstance(b, RoaringBitmap) else bytes(b) for b in bitmaps]
