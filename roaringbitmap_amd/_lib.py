@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libroaring_mi355x.so")
+LIB_PATH = os.environ.get("RBG_LIB") or os.path.join(HERE, "lib", "libroaring_mi355x.so")
 
 RBG_OK = 0
 RBG_ERR_INVALID_FORMAT = -1

@@ -57,6 +57,36 @@ struct ResultInfo {
   int64_t long_card;  // sum of result cardinalities (64-bit)
   uint32_t card32;    // Java int (mod 2^32)
   uint32_t any;       // nonzero iff some task had a non-empty result
+  uint64_t start;     // byte offset of the serialized result inside the result buffer
+  uint32_t err;       // nonzero if a look-back spin timed out (result invalid)
+  uint32_t pad;
+};
+
+// per-task output record, consumed by the header kernels
+struct __align__(16) ORec {
+  uint64_t off;  // payload offset within the payload region
+  uint32_t idx;  // output container index (valid if keep)
+  uint32_t card;
+  uint32_t ser_len;
+  uint16_t key;
+  uint8_t kind;
+  uint8_t keep;
+};
+
+// where an op writes its result: payload region at out + payload_base, header in
+// front of it; look-back state (ticket, error word, per-task status) and records
+struct OutCtx {
+  uint8_t* out;
+  uint64_t payload_base;
+  uint64_t* status;
+  uint32_t* ticket;
+  uint32_t* err;
+  ORec* recs;
+};
+
+struct OperandView {
+  const CDesc* desc;
+  const uint8_t* payload;
 };
 
 __device__ __forceinline__ int popc64(uint64_t x) { return __popcll(x); }
@@ -299,9 +329,10 @@ __device__ __forceinline__ void run_edges(const uint64_t r[4], uint32_t* lds, ui
 // ---------------------------------------------------------------------------
 // emission of a computed container into a 16 B-aligned slot (slot layout above)
 // ---------------------------------------------------------------------------
-// Array: compact the set bits into sorted u16 values via LDS staging.
-__device__ __forceinline__ void emit_array(const uint64_t r[4], int card, uint8_t* slot, uint32_t* stage,
-                                           int* sh) {
+// Stage the owned container's serialized payload in LDS `stage` (8 KiB):
+// A: u16 values; B: 1024 u64 words; R: u16 nruns + (start, length-1) pairs.
+// Returns the serialized length.  `lds` is scratch for the run-edge exchange.
+__device__ __forceinline__ uint32_t stage_array(const uint64_t r[4], int card, uint32_t* stage, int* sh) {
   const int c0 = popc64(r[0]) + popc64(r[1]);
   const int c1 = popc64(r[2]) + popc64(r[3]);
   int p0, p1, tot;
@@ -320,48 +351,44 @@ __device__ __forceinline__ void emit_array(const uint64_t r[4], int card, uint8_
     }
   }
   __syncthreads();
-  const int nvec = (2 * card + 15) >> 4;
-  for (int i = t; i < nvec; i += NT) reinterpret_cast<uint4*>(slot)[i] = reinterpret_cast<const uint4*>(stage)[i];
-  __syncthreads();
+  return 2u * (uint32_t)card;
 }
 
-// Run container: (start, length-1) pairs from the edge bits.  Returns nruns.
-__device__ __forceinline__ int emit_runs(const uint64_t r[4], uint8_t* slot, uint32_t* lds, uint32_t* stage,
-                                         int* sh) {
+__device__ __forceinline__ uint32_t stage_runs(const uint64_t r[4], uint32_t* lds, uint32_t* stage, int* sh) {
   uint64_t s[4], e[4];
   run_edges(r, lds, s, e);
   int ps0, ps1, nr, pe0, pe1, ne;
   block_scan_halves(popc64(s[0]) + popc64(s[1]), popc64(s[2]) + popc64(s[3]), ps0, ps1, nr, sh);
   block_scan_halves(popc64(e[0]) + popc64(e[1]), popc64(e[2]) + popc64(e[3]), pe0, pe1, ne, sh);
-  uint16_t* rs = reinterpret_cast<uint16_t*>(stage);
-  uint16_t* re = rs + 2048;
+  uint16_t* st = reinterpret_cast<uint16_t*>(stage);
   const int t = threadIdx.x;
   const int bases[4] = {(2 * t) * 64, (2 * t + 1) * 64, (512 + 2 * t) * 64, (513 + 2 * t) * 64};
   int sp[4] = {ps0, ps0 + popc64(s[0]), ps1, ps1 + popc64(s[2])};
-  int ep[4] = {pe0, pe0 + popc64(e[0]), pe1, pe1 + popc64(e[2])};
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     uint64_t x = s[k];
     int p = sp[k];
     while (x) {
-      if (p < 2048) rs[p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
-      p++;
-      x &= x - 1;
-    }
-    x = e[k];
-    p = ep[k];
-    while (x) {
-      if (p < 2048) re[p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
+      if (p < 2047) st[1 + 2 * p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
       p++;
       x &= x - 1;
     }
   }
   __syncthreads();
-  if (t == 0) reinterpret_cast<uint16_t*>(slot)[1] = (uint16_t)nr;
-  uint32_t* pairs = reinterpret_cast<uint32_t*>(slot + 4);
-  for (int i = t; i < nr && i < 2048; i += NT) pairs[i] = (uint32_t)rs[i] | ((uint32_t)(re[i] - rs[i]) << 16);
+  int ep[4] = {pe0, pe0 + popc64(e[0]), pe1, pe1 + popc64(e[2])};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint64_t x = e[k];
+    int p = ep[k];
+    while (x) {
+      if (p < 2047) st[2 + 2 * p] = (uint16_t)(bases[k] + __builtin_ctzll(x) - st[1 + 2 * p]);
+      p++;
+      x &= x - 1;
+    }
+  }
+  if (t == 0) st[0] = (uint16_t)nr;
   __syncthreads();
-  return nr;
+  return 2u + 4u * (uint32_t)nr;
 }
 
 // Number of runs of the owned container (block-wide).  Contains barriers.
@@ -374,24 +401,16 @@ __device__ __forceinline__ int count_runs(const uint64_t r[4], uint32_t* lds, in
   return a;
 }
 
-// Emit the owned container as `kind` into `slot`; fills the output descriptor
-// fields (serialized source address and length).  Contains barriers.
-__device__ __forceinline__ void emit_container(int kind, const uint64_t r[4], int card, uint8_t* slot,
-                                               uint32_t* lds, uint32_t* stage, int* sh, uint64_t* src,
-                                               uint32_t* ser_len) {
+__device__ __forceinline__ uint32_t stage_container(int kind, const uint64_t r[4], int card, uint32_t* lds,
+                                                    uint32_t* stage, int* sh) {
   if (kind == DK_B) {
-    store_bitmap_owned(slot, r);
-    *src = reinterpret_cast<uint64_t>(slot);
-    *ser_len = 8192;
-  } else if (kind == DK_A) {
-    emit_array(r, card, slot, stage, sh);
-    *src = reinterpret_cast<uint64_t>(slot);
-    *ser_len = 2u * (uint32_t)card;
-  } else {
-    const int nr = emit_runs(r, slot, lds, stage, sh);
-    *src = reinterpret_cast<uint64_t>(slot + 2);
-    *ser_len = 2u + 4u * (uint32_t)nr;
+    __syncthreads();
+    lds_write_owned(stage, r);
+    __syncthreads();
+    return 8192;
   }
+  if (kind == DK_A) return stage_array(r, card, stage, sh);
+  return stage_runs(r, lds, stage, sh);
 }
 
 // ---------------------------------------------------------------------------

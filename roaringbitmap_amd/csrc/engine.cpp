@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -38,6 +39,23 @@ static void set_err(const std::string& s) { g_err = s; }
 
 constexpr size_t kSlack = 256;  // every device buffer carries read slack (group_copy)
 constexpr int kMaxKeys = 65536;
+constexpr size_t kLbHeader = 256;
+
+// RBG_DEBUG_SYNC=1: synchronise and report after every pipeline stage (debugging aid)
+static bool debug_sync() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("RBG_DEBUG_SYNC");
+    v = (e && e[0] == '1') ? 1 : 0;
+  }
+  return v == 1;
+}
+static void dbg(hipStream_t s, const char* what) {
+  if (!debug_sync()) return;
+  hipError_t e = hipStreamSynchronize(s);
+  std::fprintf(stderr, "[rbg] %s done: %s\n", what, hipGetErrorString(e));
+  std::fflush(stderr);
+}  // look-back state: ticket @0, error word @64, statuses @256
 
 struct DevBuf {
   void* p = nullptr;
@@ -83,7 +101,8 @@ struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Batch>> batches;
-  DevBuf by_key, flag, tasks, ntasks, out, out_idx, out_off, info, task_card, scratch, result, cards, skip, raw, items;
+  DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw, items,
+      scalar;
   size_t result_cap = 0;
   size_t n_cards = 0;
   int last = 0;  // 0 none, 1 serialized result, 2 cardinality, 3 batch cardinalities
@@ -130,9 +149,11 @@ static int ctx_init(Ctx* c, int device) {
   CHK(c->flag.ensure(kMaxKeys));
   CHK(c->tasks.ensure(sizeof(Task) * kMaxKeys));
   CHK(c->ntasks.ensure(64));
-  CHK(c->out.ensure(sizeof(ODesc) * kMaxKeys));
-  CHK(c->out_idx.ensure(4 * kMaxKeys));
-  CHK(c->out_off.ensure(8 * kMaxKeys));
+  CHK(c->wg_count.ensure(4 * 256));
+  CHK(c->lb.ensure(kLbHeader + 8 * kMaxKeys));
+  CHK(c->recs.ensure(sizeof(ORec) * kMaxKeys));
+  CHK(c->kind_by_out.ensure(kMaxKeys));
+  CHK(c->scalar.ensure(64));
   CHK(c->info.ensure(sizeof(ResultInfo)));
   CHK(c->task_card.ensure(4 * kMaxKeys));
   return RBG_OK;
@@ -293,11 +314,25 @@ static int ctx_load(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size
 // ---------------------------------------------------------------------------
 // op pipelines
 // ---------------------------------------------------------------------------
-static int ensure_outputs(Ctx* c, size_t max_tasks, size_t max_payload) {
-  CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1)));
-  const size_t cap = 16 + 9 * max_tasks + (max_tasks + 7) / 8 + max_payload + 64;
-  CHK(c->result.ensure(cap));
-  c->result_cap = cap;
+// Result buffer: [header reserve P0][payload region].  The header (whose size
+// depends on the final container count and run flag) is written right in front
+// of the payload, so the serialized bitmap starts at P0 - header.
+static uint64_t header_reserve(size_t max_tasks) {
+  return round16(8 + (max_tasks + 7) / 8 + 8 * (uint64_t)max_tasks + 16);
+}
+
+static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc) {
+  const uint64_t P0 = header_reserve(max_tasks);
+  CHK(c->result.ensure(P0 + max_payload + 64));
+  c->result_cap = P0 + max_payload;
+  HIPCHK(hipMemsetAsync(c->lb.p, 0, kLbHeader + 8 * std::max<size_t>(max_tasks, 1), c->stream));
+  uint8_t* lb = c->lb.as<uint8_t>();
+  oc->out = c->result.as<uint8_t>();
+  oc->payload_base = P0;
+  oc->ticket = reinterpret_cast<uint32_t*>(lb);
+  oc->err = reinterpret_cast<uint32_t*>(lb + 64);
+  oc->status = reinterpret_cast<uint64_t*>(lb + kLbHeader);
+  oc->recs = c->recs.as<ORec>();
   return RBG_OK;
 }
 
@@ -340,23 +375,30 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     case OP_ANDNOT: ub = na; break;
     default: ub = std::min<size_t>((size_t)na + nb, kMaxKeys); break;
   }
-  if (!card_only) CHK(ensure_outputs(c, ub, A->payload_bytes + B->payload_bytes + (size_t)kSlotBytes * ub));
+  OutCtx oc;
+  CHK(prepare_output(c, ub, card_only ? 0 : A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc));
   c->mark(0);
-  launch_plan_pairwise(s, plan_op, ka, na, kb, nb, c->by_key.as<Task>(), c->flag.as<uint8_t>());
-  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->tasks.as<Task>(), c->ntasks.as<uint32_t>());
+  dbg(s, "memset");
+  launch_plan_pairwise(s, plan_op, ka, na, kb, nb, c->by_key.as<Task>(), c->flag.as<uint8_t>(),
+                       c->wg_count.as<uint32_t>());
+  dbg(s, "plan");
+  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
+                 c->ntasks.as<uint32_t>());
+  dbg(s, "compact");
   c->mark(1);
-  launch_pairwise(s, op, card_only ? 1 : 0, grid_for(ub), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), da,
-                  A->payload.as<uint8_t>(), db, B->payload.as<uint8_t>(), c->out.as<ODesc>(), c->scratch.as<uint8_t>(),
+  const int grid = grid_for((ub + 3) / 4, 1024);  // 4 waves (tasks) per workgroup
+  launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(),
+                  OperandView{da, A->payload.as<uint8_t>()}, OperandView{db, B->payload.as<uint8_t>()}, oc,
                   c->task_card.as<uint32_t>());
+  dbg(s, "pairwise");
   c->mark(2);
   if (card_only) {
     launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
     c->last = 2;
   } else {
-    launch_finalize(s, c->out.as<ODesc>(), c->ntasks.as<uint32_t>(), c->out_idx.as<uint32_t>(),
-                    c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
-    launch_emit(s, grid_for(ub), c->out.as<ODesc>(), c->ntasks.as<uint32_t>(), c->out_idx.as<uint32_t>(),
-                c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
+    launch_header(s, grid_for((ub + 255) / 256, 256), c->ntasks.as<uint32_t>(), oc, c->kind_by_out.as<uint8_t>(),
+                  c->info.as<ResultInfo>());
+    dbg(s, "header");
     c->last = 1;
   }
   c->mark(3);
@@ -437,7 +479,9 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     plan_mode = 2;
   }
   {
-    CHK(ensure_outputs(c, kMaxKeys, (size_t)kSlotBytes * kMaxKeys + B->payload_bytes));
+    const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
+    OutCtx oc;
+    CHK(prepare_output(c, ub, card_only ? 0 : (size_t)8194 * ub + B->payload_bytes, &oc));
     if (!skip.empty()) {
       CHK(c->skip.ensure(skip.size()));
       HIPCHK(hipMemcpyAsync(c->skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
@@ -445,8 +489,9 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     const uint32_t n_req = plan_mode == 2 ? 0xFFFFFFFFu : (uint32_t)N;
     c->mark(0);
     launch_plan_wide(s, plan_mode == 0 ? 0 : 1, B->key_off.as<uint32_t>(), n_req, key_lo, key_hi,
-                     c->by_key.as<Task>(), c->flag.as<uint8_t>());
-    launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->tasks.as<Task>(), c->ntasks.as<uint32_t>());
+                     c->by_key.as<Task>(), c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>());
+    launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
+                   c->ntasks.as<uint32_t>());
     WideArgs wa;
     wa.desc = B->desc.as<CDesc>();
     wa.bm = B->bm.as<uint32_t>();
@@ -454,17 +499,15 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.skip = skip.empty() ? nullptr : c->skip.as<uint8_t>();
     wa.start_bm = start_bm;
     c->mark(1);
-    launch_wide(s, mode, 4096, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, c->out.as<ODesc>(),
-                c->scratch.as<uint8_t>(), c->task_card.as<uint32_t>());
+    launch_wide(s, mode, grid_for(ub, 2048), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
+                c->task_card.as<uint32_t>());
     c->mark(2);
     if (card_only) {
       launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
       c->last = 2;
     } else {
-      launch_finalize(s, c->out.as<ODesc>(), c->ntasks.as<uint32_t>(), c->out_idx.as<uint32_t>(),
-                      c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
-      launch_emit(s, 4096, c->out.as<ODesc>(), c->ntasks.as<uint32_t>(), c->out_idx.as<uint32_t>(),
-                  c->out_off.as<uint64_t>(), c->info.as<ResultInfo>(), c->result.as<uint8_t>());
+      launch_header(s, grid_for((ub + 255) / 256, 256), c->ntasks.as<uint32_t>(), oc, c->kind_by_out.as<uint8_t>(),
+                    c->info.as<ResultInfo>());
       c->last = 1;
     }
     c->mark(3);
@@ -486,9 +529,13 @@ static int ctx_fetch(Ctx* c, rbg_buffer* out) {
   }
   ResultInfo ri;
   CHK(ctx_info(c, &ri));
+  if (ri.err) {
+    set_err("look-back placement timed out");
+    return RBG_ERR_DEVICE;
+  }
   uint8_t* p = (uint8_t*)std::malloc(ri.total ? ri.total : 1);
   if (!p) return RBG_ERR_OUT_OF_MEMORY;
-  HIPCHK(hipMemcpyAsync(p, c->result.p, ri.total, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(p, c->result.as<uint8_t>() + ri.start, ri.total, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   out->data = p;
   out->len = ri.total;
@@ -898,20 +945,15 @@ int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* st) {
   st[6] = b->long_card;
   st[7] = b->ser_bytes;
   if (b->n_ctr) {
-    std::vector<CDesc> d(b->n_ctr);
     HIPCHK(hipSetDevice(ctx->c.device));
-    HIPCHK(hipMemcpy(d.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
-    int64_t pay = 0;
-    for (const CDesc& x : d) {
-      if (x.kind == KA) pay += 2 * (int64_t)x.card;
-      else if (x.kind == KB) pay += 8192;
-      else {
-        uint16_t nr = 0;
-        HIPCHK(hipMemcpy(&nr, b->payload.as<uint8_t>() + x.slot + 2, 2, hipMemcpyDeviceToHost));
-        pay += 2 + 4 * (int64_t)nr;
-      }
-    }
-    st[5] = pay;
+    hipStream_t s = ctx->c.stream;
+    HIPCHK(hipMemsetAsync(ctx->c.scalar.p, 0, 8, s));
+    launch_batch_bytes(s, b->desc.as<CDesc>(), b->n_ctr, b->payload.as<uint8_t>(),
+                       ctx->c.scalar.as<unsigned long long>());
+    unsigned long long pay = 0;
+    HIPCHK(hipMemcpyAsync(&pay, ctx->c.scalar.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    st[5] = (int64_t)pay;
   }
   return RBG_OK;
 }

@@ -1,15 +1,17 @@
 // HIP kernels of the MI355X Roaring engine (gfx950).  RB/ = reference
 // RoaringBitmap/src/main/java/org/roaringbitmap/.
 //
-// Every op runs as one pipeline on the context stream, with no host sync:
-//   plan    : per-key (65536 threads) decide whether key k produces a task
-//   compact : one workgroup scans the per-key flags into a dense task list
-//   compute : one 256-thread workgroup per task computes the result container
-//             in registers/LDS and writes it to a fixed 8208 B scratch slot
-//   finalize: one workgroup scans the kept outputs, writes the header prefix
-//   emit    : descriptors, offset table and payload copies into the
-//             portable-format output buffer
+// Every op is one pipeline on the context stream with no host sync:
+//   plan    : per-key (65536 threads) "does key k produce a task", per-WG counts
+//   compact : 256 workgroups place the flagged keys into a dense task list
+//   compute : one wavefront per task (tickets in task order) computes the result
+//             container in registers, places it with a decoupled look-back scan
+//             over (containers, payload bytes) and writes its serialized payload
+//             straight into the output buffer (no scratch copy)
+//   header  : descriptors, offset table, run flags and cookie, written in front of
+//             the payload region once the totals are known
 #include "kernels.hpp"
+#include "wave.hpp"
 
 namespace rbg {
 
@@ -26,13 +28,21 @@ __device__ __forceinline__ int lower_bound_u16(const uint16_t* keys, int n, uint
   return lo;
 }
 
-// Key alignment of two sorted key arrays (RoaringArray.advanceUntil walk of
+__device__ __forceinline__ void plan_count(int f, uint32_t* wg_count) {
+  __shared__ int wc[4];
+  const uint64_t m = __ballot(f);
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) wg_count[blockIdx.x] = (uint32_t)(wc[0] + wc[1] + wc[2] + wc[3]);
+}
+
+// Key alignment of two sorted key arrays (the advanceUntil walks of
 // RB/RoaringBitmap.java:382-400, :864-896, :1076-1113, :449-471), one thread per key.
 __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint16_t* __restrict__ ka, int na,
                                                        const uint16_t* __restrict__ kb, int nb,
-                                                       Task* __restrict__ by_key, uint8_t* __restrict__ flag) {
+                                                       Task* __restrict__ by_key, uint8_t* __restrict__ flag,
+                                                       uint32_t* __restrict__ wg_count) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= 65536) return;
   const int pa = lower_bound_u16(ka, na, k);
   const int pb = lower_bound_u16(kb, nb, k);
   const int ia = (pa < na && ka[pa] == k) ? pa : -1;
@@ -46,55 +56,56 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint16_t* _
   }
   flag[k] = (uint8_t)f;
   by_key[k] = Task{k, ia, ib, 0};
+  plan_count(f, wg_count);
 }
 
 // Wide plan from the key-major CSR: n_k = key_off[k+1] - key_off[k].
 // mode 0: n_k > 0 (or / xor / orCardinality); mode 1: n_k == n_req (and).
-__global__ __launch_bounds__(256) void k_plan_wide(int mode, const uint32_t* __restrict__ key_off,
-                                                   uint32_t n_req, int key_lo, int key_hi,
-                                                   Task* __restrict__ by_key, uint8_t* __restrict__ flag) {
+__global__ __launch_bounds__(256) void k_plan_wide(int mode, const uint32_t* __restrict__ key_off, uint32_t n_req,
+                                                   int key_lo, int key_hi, Task* __restrict__ by_key,
+                                                   uint8_t* __restrict__ flag, uint32_t* __restrict__ wg_count) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= 65536) return;
   const uint32_t s = key_off[k], n = key_off[k + 1] - s;
   int f = (mode == 0) ? (n > 0) : (n == n_req && n > 0);
   if ((int)k < key_lo || (int)k >= key_hi) f = 0;
   flag[k] = (uint8_t)f;
   by_key[k] = Task{k, (int32_t)s, (int32_t)n, 0};
+  plan_count(f, wg_count);
 }
 
-// One 1024-thread workgroup compacts 65536 flags (64 per thread, in key order).
-__global__ __launch_bounds__(1024) void k_compact(const uint8_t* __restrict__ flag, const Task* __restrict__ by_key,
-                                                  Task* __restrict__ tasks, uint32_t* __restrict__ n_tasks) {
-  __shared__ int wsum[16];
+// 256 workgroups x 256 keys: each sums the counts of the workgroups before it.
+__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ flag, const Task* __restrict__ by_key,
+                                                 const uint32_t* __restrict__ wg_count, Task* __restrict__ tasks,
+                                                 uint32_t* __restrict__ n_tasks) {
+  __shared__ int wsum[4];
+  __shared__ uint32_t base_sh;
   const int t = threadIdx.x;
-  const uint4* f4 = reinterpret_cast<const uint4*>(flag + 64 * t);
-  uint4 f[4] = {f4[0], f4[1], f4[2], f4[3]};
-  const uint8_t* fb = reinterpret_cast<const uint8_t*>(f);
-  int cnt = 0;
-#pragma unroll
-  for (int i = 0; i < 64; i++) cnt += fb[i];
-  // block exclusive scan of cnt
-  const int lane = t & 63, w = t >> 6;
-  const int inc = wave_incl_scan(cnt);
-  if (lane == 63) wsum[w] = inc;
+  // prefix over previous workgroups (256 counts, one per thread)
+  uint32_t c = (t < (int)blockIdx.x) ? wg_count[t] : 0;
+  int v = wave_sum_i((int)c);
+  if ((t & 63) == 0) wsum[t >> 6] = v;
   __syncthreads();
-  int off = 0, tot = 0;
-  for (int i = 0; i < 16; i++) {
-    if (i < w) off += wsum[i];
-    tot += wsum[i];
-  }
-  int p = off + inc - cnt;
-  for (int i = 0; i < 64; i++)
-    if (fb[i]) tasks[p++] = by_key[64 * t + i];
-  if (t == 0) *n_tasks = (uint32_t)tot;
+  if (t == 0) base_sh = (uint32_t)(wsum[0] + wsum[1] + wsum[2] + wsum[3]);
+  __syncthreads();
+  const uint32_t k = blockIdx.x * 256 + t;
+  const int f = flag[k];
+  int tot;
+  const int lane_pre = wave_excl(f, &tot);
+  __shared__ int wt[4];
+  if ((t & 63) == 0) wt[t >> 6] = tot;
+  __syncthreads();
+  int wpre = 0;
+  for (int i = 0; i < (t >> 6); i++) wpre += wt[i];
+  if (f) tasks[base_sh + wpre + lane_pre] = by_key[k];
+  if (blockIdx.x == gridDim.x - 1 && t == 0) *n_tasks = base_sh + wt[0] + wt[1] + wt[2] + wt[3];
 }
 
 // ===========================================================================
-// pairwise compute
+// pairwise compute, one wavefront per matched key
 // ===========================================================================
-// Result container type of the static pairwise ops, as a function of the
-// operand kinds and the result's cardinality c and run count r (DESIGN.md
-// §Type contract; derived from RB/{Array,Bitmap,Run}Container.java):
+// Result container type of the static pairwise ops as a function of the operand
+// kinds and the result's cardinality c and run count r (DESIGN.md §Type contract,
+// derived from RB/{Array,Bitmap,Run}Container.java):
 //   AND   : R&R -> EFF(c,r) (RB/RunContainer.java:381-456); else BY_CARD(c)
 //   OR    : A|R, R|A, R|R -> EFF(c,r) (:1926-1986); A|A -> BY_CARD(c)
 //           (RB/ArrayContainer.java:949-963); B|x, x|B -> c==65536 ? R.full : B
@@ -127,218 +138,197 @@ __device__ __forceinline__ uint64_t apply_op(uint64_t x, uint64_t y) {
   return x & ~y;
 }
 
-struct OperandView {
-  const CDesc* desc;
-  const uint8_t* payload;
-};
-
-__device__ __forceinline__ void passthrough(const CDesc& d, const uint8_t* payload, ODesc* o) {
-  ODesc r;
-  r.src = reinterpret_cast<uint64_t>(payload + d.slot + (d.kind == DK_R ? 2 : 0));
-  r.card = d.card;
-  r.key = d.key;
-  r.kind = d.kind;
-  r.keep = 1;
-  if (d.kind == DK_A) r.ser_len = 2 * d.card;
-  else if (d.kind == DK_B) r.ser_len = 8192;
-  else r.ser_len = 2 + 4 * (uint32_t)(*reinterpret_cast<const uint16_t*>(payload + d.slot + 2));
-  r.pad0 = 0;
-  r.pad1 = 0;
-  *o = r;
+__device__ __forceinline__ uint32_t ser_len_of(const CDesc& d, const uint8_t* payload) {
+  if (d.kind == DK_A) return 2 * d.card;
+  if (d.kind == DK_B) return 8192;
+  return 2 + 4 * (uint32_t)(*reinterpret_cast<const uint16_t*>(payload + d.slot + 2));
 }
 
-// MODE 0: materialise results.  MODE 1: cardinality only (task_card[t]).
+constexpr int kWaves = 4;  // waves per workgroup in the wave-per-task kernels
+constexpr int kQcap = 64;  // long-run queue per wave
+
+// Emits one task's output: look-back placement + payload write + record.
+// `staged` = payload is in the wave's LDS; otherwise copied from `src` (global).
+__device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
+                                        uint32_t len, uint32_t card, uint32_t key, int kind, OutCtx oc) {
+  const int l = lane_id();
+  const Prefix p = lookback(oc.status, t, keep ? 1u : 0u, keep ? len : 0u, (keep && kind == DK_R) ? 1u : 0u, oc.err);
+  const uint32_t idx = p.idx;
+  const uint64_t off = p.off;
+  if (keep) {
+    uint8_t* dst = oc.out + oc.payload_base + off;
+    if (staged) copy_lds_to_global<64>(dst, lds, len, l);
+    else group_copy<64>(dst, src, len, l);
+  }
+  if (l == 0) {
+    ORec r;
+    r.off = off;
+    r.idx = idx;
+    r.card = card;
+    r.ser_len = len;
+    r.key = (uint16_t)key;
+    r.kind = (uint8_t)kind;
+    r.keep = keep ? 1 : 0;
+    oc.recs[t] = r;
+  }
+}
+
+// One task, processed by one wave.  Every branch below is wave-uniform (scalar).
 template <int OP, int MODE>
-__global__ __launch_bounds__(256) void k_pairwise(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
-                                                  OperandView A, OperandView B, ODesc* __restrict__ out,
-                                                  uint8_t* __restrict__ scratch, uint32_t* __restrict__ task_card) {
-  __shared__ __align__(16) uint32_t lds_a[2048];
-  __shared__ __align__(16) uint32_t lds_b[2048];
-  __shared__ int q[257];
-  __shared__ int sh[8];
-  const uint32_t nt = *n_tasks;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    const Task tk = tasks[t];
-    if (tk.a < 0 || tk.b < 0) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
-      if (MODE == 0 && threadIdx.x == 0) {
-        if (tk.a >= 0) passthrough(A.desc[tk.a], A.payload, out + t);
-        else passthrough(B.desc[tk.b], B.payload, out + t);
-      }
-      continue;
+__device__ __forceinline__ void pair_task(uint32_t t, const Task& tk, const OperandView& A, const OperandView& B,
+                                          const OutCtx& oc, uint32_t* task_card, uint32_t* lds, int* q) {
+  const int l = lane_id();
+  if (tk.a < 0 || tk.b < 0) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
+    if (MODE == 0) {
+      const bool from_a = tk.a >= 0;
+      const CDesc d = from_a ? A.desc[tk.a] : B.desc[tk.b];
+      const uint8_t* pl = from_a ? A.payload : B.payload;
+      w_place(t, true, pl + d.slot + (d.kind == DK_R ? 2 : 0), false, lds, ser_len_of(d, pl), d.card, d.key, d.kind,
+              oc);
     }
+  } else {
     const CDesc da = A.desc[tk.a];
     const CDesc db = B.desc[tk.b];
-    uint64_t x[4], y[4];
-    materialize(da, A.payload, lds_a, q, x);
-    materialize(db, B.payload, lds_b, q, y);
-    uint64_t r[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) r[i] = apply_op<OP>(x[i], y[i]);
-    int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
-    int unused = 0;
-    block_sum2(c, unused, sh);
+    WCtr x;
+    w_materialize(da, A.payload, lds, q, kQcap, x);
+    w_combine<OP>(db, B.payload, lds, q, kQcap, x);
+    const int c = w_card(x);
     if (MODE == 1) {
-      if (threadIdx.x == 0) task_card[t] = (uint32_t)c;
-      continue;
-    }
-    if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389,456,1084)
-      if (threadIdx.x == 0) {
-        ODesc o = {};
-        o.keep = 0;
-        out[t] = o;
-      }
-      continue;
-    }
-    const bool use_eff = pairwise_needs_runs(OP, da.kind, (int)da.card, db.kind, (int)db.card);
-    const int nr = use_eff ? count_runs(r, lds_a, sh) : 0;
-    const int kind = pairwise_kind(OP, da.kind, db.kind, use_eff, c, nr);
-    uint8_t* slot = scratch + (size_t)t * kSlotBytes;
-    uint64_t src;
-    uint32_t len;
-    emit_container(kind, r, c, slot, lds_a, lds_b, sh, &src, &len);
-    if (threadIdx.x == 0) {
-      ODesc o;
-      o.src = src;
-      o.ser_len = len;
-      o.card = (uint32_t)c;
-      o.key = (uint16_t)tk.key;
-      o.kind = (uint8_t)kind;
-      o.keep = 1;
-      o.pad0 = 0;
-      o.pad1 = 0;
-      out[t] = o;
+      if (l == 0) task_card[t] = (uint32_t)c;
+    } else if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389,456,1084)
+      w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
+    } else {
+      const bool use_eff = pairwise_needs_runs(OP, da.kind, (int)da.card, db.kind, (int)db.card);
+      const int nr = use_eff ? w_runs(x) : 0;
+      const int kind = pairwise_kind(OP, da.kind, db.kind, use_eff, c, nr);
+      const uint32_t len = w_stage(kind, x, c, lds);
+      w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, oc);
     }
   }
 }
 
-// ===========================================================================
-// finalize / emit (portable format, RB/RoaringArray.java:896-940)
-// ===========================================================================
-__global__ __launch_bounds__(1024) void k_finalize(const ODesc* __restrict__ out, const uint32_t* __restrict__ n_tasks,
-                                                   uint32_t* __restrict__ out_idx, uint64_t* __restrict__ out_off,
-                                                   ResultInfo* __restrict__ info, uint8_t* __restrict__ buf) {
-  __shared__ uint32_t runflags[2048];  // 65536 bits
-  __shared__ int wsum[16];
-  __shared__ unsigned long long wbytes[16];
-  __shared__ int wrun[16];
-  __shared__ unsigned long long wcard[16];
-  const int t = threadIdx.x;
-  const uint32_t nt = *n_tasks;
-  for (int i = t; i < 2048; i += 1024) runflags[i] = 0;
-  // each thread handles 64 consecutive tasks
-  const uint32_t t0 = 64u * t;
-  int cnt = 0, run = 0;
-  unsigned long long bytes = 0, card = 0;
-  for (uint32_t i = t0; i < t0 + 64 && i < nt; i++) {
-    const ODesc o = out[i];
-    if (o.keep) {
-      cnt++;
-      bytes += o.ser_len;
-      card += o.card;
-      run |= (o.kind == DK_R);
-    }
-  }
-  const int lane = t & 63, w = t >> 6;
-  const int inc = wave_incl_scan(cnt);
-  // 64-bit byte scan inside the wave
-  unsigned long long binc = bytes;
-  for (int o = 1; o < 64; o <<= 1) {
-    unsigned long long u = __shfl_up(binc, o, 64);
-    if (lane >= o) binc += u;
-  }
-  unsigned long long csum = card;
-  for (int o = 32; o > 0; o >>= 1) csum += __shfl_xor(csum, o, 64);
-  int rany = __any(run) ? 1 : 0;
-  if (lane == 63) {
-    wsum[w] = inc;
-    wbytes[w] = binc;
-  }
-  if (lane == 0) {
-    wrun[w] = rany;
-    wcard[w] = csum;
-  }
-  __syncthreads();
-  int off = 0, tot = 0, has_run = 0;
-  unsigned long long boff = 0, btot = 0, ctot = 0;
-  for (int i = 0; i < 16; i++) {
-    if (i < w) {
-      off += wsum[i];
-      boff += wbytes[i];
-    }
-    tot += wsum[i];
-    btot += wbytes[i];
-    has_run |= wrun[i];
-    ctot += wcard[i];
-  }
-  int p = off + inc - cnt;
-  unsigned long long bp = boff + binc - bytes;
-  for (uint32_t i = t0; i < t0 + 64 && i < nt; i++) {
-    const ODesc o = out[i];
-    if (o.keep) {
-      out_idx[i] = (uint32_t)p;
-      out_off[i] = bp;
-      if (o.kind == DK_R) atomicOr(&runflags[p >> 5], 1u << (p & 31));
-      p++;
-      bp += o.ser_len;
-    } else {
-      out_idx[i] = 0xFFFFFFFFu;
-    }
-  }
-  __syncthreads();
-  const uint32_t size = (uint32_t)tot;
-  uint64_t header;
-  if (has_run) header = (size < 4) ? 4 + (size + 7) / 8 + 4 * (uint64_t)size : 4 + (size + 7) / 8 + 8 * (uint64_t)size;
-  else header = 8 + 8 * (uint64_t)size;
-  if (t == 0) {
-    ResultInfo r;
-    r.n_out = size;
-    r.has_run = (uint32_t)has_run;
-    r.header = header;
-    r.payload = btot;
-    r.total = header + btot;
-    r.long_card = (int64_t)ctot;
-    r.card32 = (uint32_t)ctot;
-    r.any = size > 0;
-    *info = r;
-    // cookie (+ size)
-    uint32_t* b32 = reinterpret_cast<uint32_t*>(buf);
-    if (has_run) {
-      b32[0] = 12347u | ((size - 1) << 16);
-    } else {
-      b32[0] = 12346u;
-      b32[1] = size;
-    }
-  }
-  if (has_run) {
-    const uint32_t nflag = (size + 7) / 8;
-    const uint8_t* rf = reinterpret_cast<const uint8_t*>(runflags);
-    for (uint32_t i = t; i < nflag; i += 1024) buf[4 + i] = rf[i];
+// MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
+template <int OP, int MODE>
+__global__ __launch_bounds__(256) void k_pair_wave(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                   OperandView A, OperandView B, OutCtx oc,
+                                                   uint32_t* __restrict__ task_card) {
+  __shared__ __align__(16) uint32_t lds_all[kWaves][2048];
+  __shared__ int q_all[kWaves][kQcap];
+  const int w = threadIdx.x >> 6, l = lane_id();
+  uint32_t* lds = lds_all[w];
+  int* q = q_all[w];
+  const uint32_t nt = uni(*n_tasks);
+  for (;;) {
+    // every lane runs the atomic (lane 0 adds 1, the others 0): the ticket is
+    // provably wave-uniform, so all control flow below stays scalar.  (A
+    // lane-0-only atomic + shuffle made the compiler treat the task as divergent
+    // and the resulting kernel hung on gfx950.)
+    const uint32_t t = uni(atomicAdd(oc.ticket, l == 0 ? 1u : 0u));
+    if (t >= nt) break;
+    Task tk = tasks[t];
+    tk.a = (int32_t)uni((uint32_t)tk.a);
+    tk.b = (int32_t)uni((uint32_t)tk.b);
+    tk.key = uni(tk.key);
+    pair_task<OP, MODE>(t, tk, A, B, oc, task_card, lds, q);
   }
 }
 
-// Writes descriptors, offsets and payloads; one workgroup per task (grid-stride).
-__global__ __launch_bounds__(256) void k_emit(const ODesc* __restrict__ out, const uint32_t* __restrict__ n_tasks,
-                                              const uint32_t* __restrict__ out_idx, const uint64_t* __restrict__ out_off,
-                                              const ResultInfo* __restrict__ info, uint8_t* __restrict__ buf) {
+// ===========================================================================
+// header (RB/RoaringArray.java:896-940): descriptors, offsets, run flags, cookie
+// ===========================================================================
+__device__ __forceinline__ void totals(const OutCtx& oc, uint32_t nt, uint32_t* n_out, uint32_t* has_run,
+                                       uint64_t* payload) {
+  if (nt == 0) {
+    *n_out = 0;
+    *has_run = 0;
+    *payload = 0;
+    return;
+  }
+  const uint64_t s = __hip_atomic_load(oc.status + nt - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  *has_run = (uint32_t)((s >> 61) & 1);
+  *n_out = (uint32_t)((s >> 44) & 0x1FFFF);
+  *payload = s & ((1ULL << 44) - 1);
+}
+
+__device__ __forceinline__ uint64_t header_bytes(uint32_t size, uint32_t has_run) {
+  if (has_run) return (size < 4) ? 4 + (size + 7) / 8 + 4ull * size : 4 + (size + 7) / 8 + 8ull * size;
+  return 8 + 8ull * size;
+}
+
+__global__ __launch_bounds__(256) void k_header(const uint32_t* __restrict__ n_tasks, OutCtx oc,
+                                                uint8_t* __restrict__ kind_by_out, ResultInfo* __restrict__ info) {
   const uint32_t nt = *n_tasks;
-  const ResultInfo ri = *info;
-  const uint32_t size = ri.n_out;
-  const uint64_t desc_base = ri.has_run ? 4 + (size + 7) / 8 : 8;
-  const bool offsets = !ri.has_run || size >= 4;
+  uint32_t size, has_run;
+  uint64_t payload;
+  totals(oc, nt, &size, &has_run, &payload);
+  const uint64_t H = header_bytes(size, has_run);
+  uint8_t* base = oc.out + oc.payload_base - H;
+  const uint64_t desc_base = has_run ? 4 + (size + 7) / 8 : 8;
+  const bool offsets = !has_run || size >= 4;
   const uint64_t off_base = desc_base + 4ull * size;
-  for (uint32_t i = blockIdx.x; i < nt; i += gridDim.x) {
-    const uint32_t idx = out_idx[i];
-    if (idx == 0xFFFFFFFFu) continue;
-    const ODesc o = out[i];
-    const uint64_t poff = ri.header + out_off[i];
-    if (threadIdx.x < 4) {
-      const uint32_t d = (uint32_t)o.key | ((o.card - 1) << 16);
-      buf[desc_base + 4ull * idx + threadIdx.x] = (uint8_t)(d >> (8 * threadIdx.x));
-    } else if (offsets && threadIdx.x < 8) {
-      const int b = threadIdx.x - 4;
-      buf[off_base + 4ull * idx + b] = (uint8_t)((uint32_t)poff >> (8 * b));
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    const ORec r = oc.recs[t];
+    if (!r.keep) continue;
+    const uint32_t d = (uint32_t)r.key | ((r.card - 1) << 16);
+    uint8_t* pd = base + desc_base + 4ull * r.idx;
+    pd[0] = (uint8_t)d;
+    pd[1] = (uint8_t)(d >> 8);
+    pd[2] = (uint8_t)(d >> 16);
+    pd[3] = (uint8_t)(d >> 24);
+    if (offsets) {
+      const uint32_t o = (uint32_t)(H + r.off);
+      uint8_t* po = base + off_base + 4ull * r.idx;
+      po[0] = (uint8_t)o;
+      po[1] = (uint8_t)(o >> 8);
+      po[2] = (uint8_t)(o >> 16);
+      po[3] = (uint8_t)(o >> 24);
     }
-    group_copy<NT>(buf + poff, reinterpret_cast<const uint8_t*>(o.src), o.ser_len, threadIdx.x);
+    kind_by_out[r.idx] = r.kind;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t cookie[2];
+    int nb;
+    if (has_run) {
+      cookie[0] = 12347u | ((size - 1) << 16);
+      nb = 4;
+    } else {
+      cookie[0] = 12346u;
+      cookie[1] = size;
+      nb = 8;
+    }
+    const uint8_t* cb = reinterpret_cast<const uint8_t*>(cookie);
+    for (int i = 0; i < nb; i++) base[i] = cb[i];
+    ResultInfo ri;
+    ri.n_out = size;
+    ri.has_run = has_run;
+    ri.header = H;
+    ri.payload = payload;
+    ri.total = H + payload;
+    ri.long_card = 0;
+    ri.card32 = 0;
+    ri.any = size > 0;
+    ri.start = oc.payload_base - H;
+    ri.err = *oc.err;
+    *info = ri;
+  }
+}
+
+// run-flag bytes: bit i%8 of byte i/8 set iff output container i is a run container
+__global__ __launch_bounds__(256) void k_runflags(const uint32_t* __restrict__ n_tasks, OutCtx oc,
+                                                  const uint8_t* __restrict__ kind_by_out) {
+  uint32_t size, has_run;
+  uint64_t payload;
+  totals(oc, *n_tasks, &size, &has_run, &payload);
+  if (!has_run) return;
+  uint8_t* base = oc.out + oc.payload_base - header_bytes(size, has_run);
+  const uint32_t nbytes = (size + 7) / 8;
+  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nbytes; b += gridDim.x * blockDim.x) {
+    uint8_t v = 0;
+    for (int k = 0; k < 8; k++) {
+      const uint32_t i = 8 * b + k;
+      if (i < size && kind_by_out[i] == DK_R) v |= (uint8_t)(1u << k);
+    }
+    base[4 + b] = v;
   }
 }
 
@@ -392,50 +382,56 @@ __global__ __launch_bounds__(256) void k_ingest(const uint8_t* __restrict__ raw,
   }
 }
 
+// serialized payload bytes of a batch (for statistics)
+__global__ __launch_bounds__(256) void k_batch_bytes(const CDesc* __restrict__ desc, uint64_t n,
+                                                     const uint8_t* __restrict__ payload,
+                                                     unsigned long long* __restrict__ out) {
+  unsigned long long s = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    s += ser_len_of(desc[i], payload);
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, s);
+}
+
 // ===========================================================================
 // host launchers
 // ===========================================================================
 void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const uint16_t* kb, int nb, Task* by_key,
-                          uint8_t* flag) {
-  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, ka, na, kb, nb, by_key, flag);
+                          uint8_t* flag, uint32_t* wg_count) {
+  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, ka, na, kb, nb, by_key, flag, wg_count);
 }
 void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,
-                      Task* by_key, uint8_t* flag) {
-  hipLaunchKernelGGL(k_plan_wide, dim3(256), dim3(256), 0, s, mode, key_off, n_req, key_lo, key_hi, by_key, flag);
+                      Task* by_key, uint8_t* flag, uint32_t* wg_count) {
+  hipLaunchKernelGGL(k_plan_wide, dim3(256), dim3(256), 0, s, mode, key_off, n_req, key_lo, key_hi, by_key, flag,
+                     wg_count);
 }
-void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, Task* tasks, uint32_t* n_tasks) {
-  hipLaunchKernelGGL(k_compact, dim3(1), dim3(1024), 0, s, flag, by_key, tasks, n_tasks);
+void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
+                    uint32_t* n_tasks) {
+  hipLaunchKernelGGL(k_compact, dim3(256), dim3(256), 0, s, flag, by_key, wg_count, tasks, n_tasks);
 }
 
 template <int OP>
-static void launch_pw(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, const CDesc* da,
-                      const uint8_t* pa, const CDesc* db, const uint8_t* pb, ODesc* out, uint8_t* scratch,
-                      uint32_t* task_card) {
-  OperandView A{da, pa}, B{db, pb};
+static void launch_pw(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, OperandView A,
+                      OperandView B, OutCtx oc, uint32_t* task_card) {
   if (mode == 0)
-    hipLaunchKernelGGL((k_pairwise<OP, 0>), dim3(grid), dim3(256), 0, s, tasks, nt, A, B, out, scratch, task_card);
+    hipLaunchKernelGGL((k_pair_wave<OP, 0>), dim3(grid), dim3(256), 0, s, tasks, nt, A, B, oc, task_card);
   else
-    hipLaunchKernelGGL((k_pairwise<OP, 1>), dim3(grid), dim3(256), 0, s, tasks, nt, A, B, out, scratch, task_card);
+    hipLaunchKernelGGL((k_pair_wave<OP, 1>), dim3(grid), dim3(256), 0, s, tasks, nt, A, B, oc, task_card);
 }
 
-void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* tasks, const uint32_t* nt, const CDesc* da,
-                     const uint8_t* pa, const CDesc* db, const uint8_t* pb, ODesc* out, uint8_t* scratch,
-                     uint32_t* task_card) {
+void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* tasks, const uint32_t* nt, OperandView A,
+                     OperandView B, OutCtx oc, uint32_t* task_card) {
   switch (op) {
-    case OP_AND: launch_pw<OP_AND>(s, mode, grid, tasks, nt, da, pa, db, pb, out, scratch, task_card); break;
-    case OP_OR: launch_pw<OP_OR>(s, mode, grid, tasks, nt, da, pa, db, pb, out, scratch, task_card); break;
-    case OP_XOR: launch_pw<OP_XOR>(s, mode, grid, tasks, nt, da, pa, db, pb, out, scratch, task_card); break;
-    default: launch_pw<OP_ANDNOT>(s, mode, grid, tasks, nt, da, pa, db, pb, out, scratch, task_card); break;
+    case OP_AND: launch_pw<OP_AND>(s, mode, grid, tasks, nt, A, B, oc, task_card); break;
+    case OP_OR: launch_pw<OP_OR>(s, mode, grid, tasks, nt, A, B, oc, task_card); break;
+    case OP_XOR: launch_pw<OP_XOR>(s, mode, grid, tasks, nt, A, B, oc, task_card); break;
+    default: launch_pw<OP_ANDNOT>(s, mode, grid, tasks, nt, A, B, oc, task_card); break;
   }
 }
 
-void launch_finalize(hipStream_t s, const ODesc* out, const uint32_t* nt, uint32_t* out_idx, uint64_t* out_off,
-                     ResultInfo* info, uint8_t* buf) {
-  hipLaunchKernelGGL(k_finalize, dim3(1), dim3(1024), 0, s, out, nt, out_idx, out_off, info, buf);
-}
-void launch_emit(hipStream_t s, int grid, const ODesc* out, const uint32_t* nt, const uint32_t* out_idx,
-                 const uint64_t* out_off, const ResultInfo* info, uint8_t* buf) {
-  hipLaunchKernelGGL(k_emit, dim3(grid), dim3(256), 0, s, out, nt, out_idx, out_off, info, buf);
+void launch_header(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out, ResultInfo* info) {
+  hipLaunchKernelGGL(k_header, dim3(grid), dim3(256), 0, s, nt, oc, kind_by_out, info);
+  hipLaunchKernelGGL(k_runflags, dim3(32), dim3(256), 0, s, nt, oc, (const uint8_t*)kind_by_out);
 }
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info) {
   hipLaunchKernelGGL(k_reduce_card, dim3(1), dim3(1024), 0, s, task_card, nt, info);
@@ -445,6 +441,13 @@ void launch_ingest(hipStream_t s, const uint8_t* raw, const IngestItem* items, u
   if (g > 8192) g = 8192;
   if (g == 0) return;
   hipLaunchKernelGGL(k_ingest, dim3((unsigned)g), dim3(256), 0, s, raw, items, n, payload);
+}
+void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload,
+                        unsigned long long* out) {
+  uint64_t g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g == 0) return;
+  hipLaunchKernelGGL(k_batch_bytes, dim3((unsigned)g), dim3(256), 0, s, desc, n, payload, out);
 }
 
 }  // namespace rbg

@@ -34,21 +34,19 @@ struct WideArgs {
 };
 
 void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const uint16_t* kb, int nb, Task* by_key,
-                          uint8_t* flag);
+                          uint8_t* flag, uint32_t* wg_count);
 void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,
-                      Task* by_key, uint8_t* flag);
-void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, Task* tasks, uint32_t* n_tasks);
-void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* tasks, const uint32_t* nt, const CDesc* da,
-                     const uint8_t* pa, const CDesc* db, const uint8_t* pb, ODesc* out, uint8_t* scratch,
-                     uint32_t* task_card);
-void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, ODesc* out,
-                 uint8_t* scratch, uint32_t* task_card);
-void launch_finalize(hipStream_t s, const ODesc* out, const uint32_t* nt, uint32_t* out_idx, uint64_t* out_off,
-                     ResultInfo* info, uint8_t* buf);
-void launch_emit(hipStream_t s, int grid, const ODesc* out, const uint32_t* nt, const uint32_t* out_idx,
-                 const uint64_t* out_off, const ResultInfo* info, uint8_t* buf);
+                      Task* by_key, uint8_t* flag, uint32_t* wg_count);
+void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
+                    uint32_t* n_tasks);
+void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* tasks, const uint32_t* nt, OperandView A,
+                     OperandView B, OutCtx oc, uint32_t* task_card);
+void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
+                 uint32_t* task_card);
+void launch_header(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out, ResultInfo* info);
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info);
 void launch_ingest(hipStream_t s, const uint8_t* raw, const IngestItem* items, uint64_t n, uint8_t* payload);
+void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload, unsigned long long* out);
 
 // batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch
 void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const CDesc* desc,

@@ -5,39 +5,46 @@
 // contiguously (ascending input index) in [key_off[k], key_off[k+1]), and so do
 // their payload slots, so one workgroup streams one key's whole fan-in.
 #include "kernels.hpp"
+#include "wave.hpp"
 
 namespace rbg {
 
-__device__ __forceinline__ void passthrough_w(const CDesc& d, const uint8_t* payload, ODesc* o) {
-  ODesc r;
-  r.src = reinterpret_cast<uint64_t>(payload + d.slot + (d.kind == DK_R ? 2 : 0));
-  r.card = d.card;
-  r.key = d.key;
-  r.kind = d.kind;
-  r.keep = 1;
-  if (d.kind == DK_A) r.ser_len = 2 * d.card;
-  else if (d.kind == DK_B) r.ser_len = 8192;
-  else r.ser_len = 2 + 4 * (uint32_t)(*reinterpret_cast<const uint16_t*>(payload + d.slot + 2));
-  r.pad0 = 0;
-  r.pad1 = 0;
-  *o = r;
+// Workgroup-level output placement: look-back (thread 0), payload copy, record.
+__device__ __forceinline__ void wg_place(uint32_t t, bool keep, const uint8_t* src, bool staged,
+                                         const uint32_t* stage, uint32_t len, uint32_t card, uint32_t key, int kind,
+                                         const OutCtx& oc, Prefix* shp) {
+  if (threadIdx.x < 64) {  // wave 0 runs the (wave-uniform) look-back
+    const Prefix pw = lookback(oc.status, t, keep ? 1u : 0u, keep ? len : 0u, (keep && kind == DK_R) ? 1u : 0u, oc.err);
+    if (threadIdx.x == 0) *shp = pw;
+  }
+  __syncthreads();
+  const Prefix p = *shp;
+  if (keep) {
+    uint8_t* dst = oc.out + oc.payload_base + p.off;
+    if (staged) copy_lds_to_global<NT>(dst, stage, len, threadIdx.x);
+    else group_copy<NT>(dst, src, len, threadIdx.x);
+  }
+  if (threadIdx.x == 0) {
+    ORec r;
+    r.off = p.off;
+    r.idx = p.idx;
+    r.card = card;
+    r.ser_len = len;
+    r.key = (uint16_t)key;
+    r.kind = (uint8_t)kind;
+    r.keep = keep ? 1 : 0;
+    oc.recs[t] = r;
+  }
+  __syncthreads();
 }
 
-__device__ __forceinline__ void write_out(ODesc* o, uint64_t src, uint32_t len, int card, uint32_t key, int kind) {
-  ODesc r;
-  r.src = src;
-  r.ser_len = len;
-  r.card = (uint32_t)card;
-  r.key = (uint16_t)key;
-  r.kind = (uint8_t)kind;
-  r.keep = 1;
-  r.pad0 = 0;
-  r.pad1 = 0;
-  *o = r;
-}
-__device__ __forceinline__ void drop_out(ODesc* o) {
-  ODesc r = {};
-  *o = r;
+__device__ __forceinline__ void wg_passthrough(uint32_t t, const CDesc& d, const uint8_t* payload, const OutCtx& oc,
+                                               Prefix* shp) {
+  uint32_t len;
+  if (d.kind == DK_A) len = 2 * d.card;
+  else if (d.kind == DK_B) len = 8192;
+  else len = 2 + 4 * (uint32_t)(*reinterpret_cast<const uint16_t*>(payload + d.slot + 2));
+  wg_place(t, true, payload + d.slot + (d.kind == DK_R ? 2 : 0), false, nullptr, len, d.card, d.key, d.kind, oc, shp);
 }
 
 // Thread-serial OR/XOR of a small array container into LDS (16 B vector loads).
@@ -108,7 +115,7 @@ __device__ __forceinline__ int block_card(const uint64_t r[4], int* sh) {
   int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
   int u = 0;
   block_sum2(c, u, sh);
-  return c;
+  return (int)uni((uint32_t)c);
 }
 
 // FastAggregation result types (DESIGN.md §Type contract):
@@ -121,19 +128,24 @@ __device__ __forceinline__ int block_card(const uint64_t r[4], int* sh) {
 //             (RB/RoaringBitmap.java:3296-3348)
 template <int MODE>
 __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
-                                              WideArgs A, ODesc* __restrict__ out, uint8_t* __restrict__ scratch,
-                                              uint32_t* __restrict__ task_card) {
+                                              WideArgs A, OutCtx oc, uint32_t* __restrict__ task_card) {
   __shared__ __align__(16) uint32_t acc[2048];
   __shared__ __align__(16) uint32_t tmp[2048];
   __shared__ int q[257];
   __shared__ int big[NT];
   __shared__ int nbig;
   __shared__ int sh[8];
+  __shared__ Prefix shp;
+  __shared__ uint32_t tsh;
   const uint32_t nt = *n_tasks;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+  while (true) {
+    __syncthreads();
+    if (threadIdx.x == 0) tsh = atomicAdd(oc.ticket, 1u);
+    __syncthreads();
+    const uint32_t t = uni(tsh);
+    if (t >= nt) break;
     const Task tk = tasks[t];
-    const uint32_t s = (uint32_t)tk.a, n = (uint32_t)tk.b;
-    uint8_t* slot = scratch + (size_t)t * kSlotBytes;
+    const uint32_t s = uni((uint32_t)tk.a), n = uni((uint32_t)tk.b);
     uint64_t r[4];
     int kind = DK_A, c = 0;
 
@@ -145,12 +157,12 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
           continue;
         }
         if (d.kind != DK_R) {
-          if (threadIdx.x == 0) passthrough_w(d, A.payload, out + t);
+          wg_passthrough(t, d, A.payload, oc, &shp);
           continue;
         }
         const int nr = *reinterpret_cast<const uint16_t*>(A.payload + d.slot + 2);
         if (eff((int)d.card, nr) == DK_R) {
-          if (threadIdx.x == 0) passthrough_w(d, A.payload, out + t);
+          wg_passthrough(t, d, A.payload, oc, &shp);
           continue;
         }
         materialize(d, A.payload, tmp, q, r);  // toBitmapOrArrayContainer
@@ -184,7 +196,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         accumulate_segment<1>(A.desc, A.payload, s, n, acc, q, big, &nbig, r);
         c = block_card(r, sh);
         if (c == 0) {
-          if (threadIdx.x == 0) drop_out(out + t);
+          wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
           continue;
         }
         kind = by_card(c);
@@ -220,11 +232,11 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
           clone = -1;
         }
         if (!present) {
-          if (threadIdx.x == 0) drop_out(out + t);
+          wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
           continue;
         }
         if (clone >= 0) {
-          if (threadIdx.x == 0) passthrough_w(A.desc[clone], A.payload, out + t);
+          wg_passthrough(t, A.desc[clone], A.payload, oc, &shp);
           continue;
         }
         c = st_card;
@@ -249,7 +261,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         continue;
       }
       if (c == 0) {
-        if (threadIdx.x == 0) drop_out(out + t);
+        wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
         continue;
       }
       kind = c == 65536 ? DK_R : by_card(c);
@@ -288,45 +300,41 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         c = cc;
       }
       if (empty) {
-        if (threadIdx.x == 0) drop_out(out + t);
+        wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
         continue;
       }
       if (steps == 0) {  // the clone of the smallest input is the answer
-        if (threadIdx.x == 0) passthrough_w(d0, A.payload, out + t);
+        wg_passthrough(t, d0, A.payload, oc, &shp);
         continue;
       }
       kind = st_kind;
     }
 
-    uint64_t src;
-    uint32_t len;
-    emit_container(kind, r, c, slot, acc, tmp, sh, &src, &len);
-    if (threadIdx.x == 0) write_out(out + t, src, len, c, tk.key, kind);
+    const uint32_t len = stage_container(kind, r, c, acc, tmp, sh);
+    wg_place(t, true, nullptr, true, tmp, len, (uint32_t)c, tk.key, kind, oc, &shp);
   }
 }
 
-void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, ODesc* out,
-                 uint8_t* scratch, uint32_t* task_card) {
+void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
+                 uint32_t* task_card) {
   switch (mode) {
     case WIDE_OR:
-      hipLaunchKernelGGL((k_wide<WIDE_OR>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_OR>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     case WIDE_OR_CARD:
-      hipLaunchKernelGGL((k_wide<WIDE_OR_CARD>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_OR_CARD>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     case WIDE_XOR:
-      hipLaunchKernelGGL((k_wide<WIDE_XOR>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_XOR>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     case WIDE_AND_SHY:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     case WIDE_AND_SHY_CARD:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY_CARD>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch,
-                         task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY_CARD>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     default:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_NAIVE>), dim3(grid), dim3(256), 0, s, tasks, nt, args, out, scratch,
-                         task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_AND_NAIVE>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
   }
 }
@@ -517,9 +525,9 @@ __global__ __launch_bounds__(256) void k_synth_c2(uint64_t seed, CDesc* __restri
     if (kind_pick == DK_R) kind = eff(c, count_runs(r, acc, sh));  // runOptimize of a run container
     else kind = by_card(c);
     uint8_t* slot = payload + (size_t)k * kSlotBytes;
-    uint64_t src;
-    uint32_t len;
-    emit_container(kind, r, c, slot, acc, tmp, sh, &src, &len);
+    const uint32_t len = stage_container(kind, r, c, acc, tmp, sh);
+    copy_lds_to_global<NT>(slot + (kind == DK_R ? 2 : 0), tmp, len, t);
+    __syncthreads();
     if (t == 0) {
       CDesc d;
       d.slot = (uint64_t)k * kSlotBytes;
