@@ -65,6 +65,7 @@ struct ResultInfo {
 // per-task output record, consumed by the header kernels
 struct __align__(16) ORec {
   uint64_t off;  // payload offset within the payload region
+  uint64_t src;  // scan placement: device address of the serialized payload (scratch or input)
   uint32_t idx;  // output container index (valid if keep)
   uint32_t card;
   uint32_t ser_len;
@@ -78,10 +79,13 @@ struct __align__(16) ORec {
 struct OutCtx {
   uint8_t* out;
   uint64_t payload_base;
-  uint64_t* status;
+  uint64_t* status;  // per-task look-back words (also the totals word status[n_tasks-1])
   uint32_t* ticket;
   uint32_t* err;
   ORec* recs;
+  uint8_t* scratch;  // scan placement: one kSlotBytes slot per task (null = look-back placement)
+  uint64_t* tile_status;  // scan placement: per-tile look-back words
+  uint32_t* tile_ticket;
 };
 
 struct OperandView {

@@ -39,7 +39,8 @@ static void set_err(const std::string& s) { g_err = s; }
 
 constexpr size_t kSlack = 256;  // every device buffer carries read slack (group_copy)
 constexpr int kMaxKeys = 65536;
-constexpr size_t kLbHeader = 256;
+constexpr size_t kLbHeader = 256;  // look-back state: ticket @0, error @64, tile ticket @128, statuses @256
+constexpr size_t kMaxTiles = 128;  // tile statuses follow the 65536 task statuses
 
 // RBG_DEBUG_SYNC=1: synchronise and report after every pipeline stage (debugging aid)
 static bool debug_sync() {
@@ -102,7 +103,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Batch>> batches;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw, items,
-      scalar;
+      scalar, scratch;
   size_t result_cap = 0;
   size_t n_cards = 0;
   int last = 0;  // 0 none, 1 serialized result, 2 cardinality, 3 batch cardinalities
@@ -150,7 +151,7 @@ static int ctx_init(Ctx* c, int device) {
   CHK(c->tasks.ensure(sizeof(Task) * kMaxKeys));
   CHK(c->ntasks.ensure(64));
   CHK(c->wg_count.ensure(4 * 256));
-  CHK(c->lb.ensure(kLbHeader + 8 * kMaxKeys));
+  CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + kMaxTiles)));
   CHK(c->recs.ensure(sizeof(ORec) * kMaxKeys));
   CHK(c->kind_by_out.ensure(kMaxKeys));
   CHK(c->scalar.ensure(64));
@@ -321,18 +322,42 @@ static uint64_t header_reserve(size_t max_tasks) {
   return round16(8 + (max_tasks + 7) / 8 + 8 * (uint64_t)max_tasks + 16);
 }
 
-static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc) {
+// Placement of the results: "scan" (default) parks every computed container in a
+// fixed scratch slot and places all of them with a uniform tile scan + copy;
+// "lookback" (RBG_PLACEMENT=lookback) places each container from inside the
+// compute kernel with a per-task decoupled look-back (no scratch traffic, but a
+// slow container stalls every later one).
+static bool scan_placement() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("RBG_PLACEMENT");
+    v = (e && std::strcmp(e, "lookback") == 0) ? 0 : 1;
+  }
+  return v == 1;
+}
+
+static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc, bool allow_scan = true) {
   const uint64_t P0 = header_reserve(max_tasks);
   CHK(c->result.ensure(P0 + max_payload + 64));
   c->result_cap = P0 + max_payload;
-  HIPCHK(hipMemsetAsync(c->lb.p, 0, kLbHeader + 8 * std::max<size_t>(max_tasks, 1), c->stream));
   uint8_t* lb = c->lb.as<uint8_t>();
+  const bool scan = allow_scan && scan_placement();
+  if (scan) {
+    CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1) + 64));
+    HIPCHK(hipMemsetAsync(lb, 0, kLbHeader, c->stream));
+    HIPCHK(hipMemsetAsync(lb + kLbHeader + 8 * kMaxKeys, 0, 8 * kMaxTiles, c->stream));
+  } else {
+    HIPCHK(hipMemsetAsync(lb, 0, kLbHeader + 8 * std::max<size_t>(max_tasks, 1), c->stream));
+  }
   oc->out = c->result.as<uint8_t>();
   oc->payload_base = P0;
   oc->ticket = reinterpret_cast<uint32_t*>(lb);
   oc->err = reinterpret_cast<uint32_t*>(lb + 64);
+  oc->tile_ticket = reinterpret_cast<uint32_t*>(lb + 128);
   oc->status = reinterpret_cast<uint64_t*>(lb + kLbHeader);
+  oc->tile_status = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * kMaxKeys);
   oc->recs = c->recs.as<ORec>();
+  oc->scratch = scan ? c->scratch.as<uint8_t>() : nullptr;
   return RBG_OK;
 }
 
@@ -376,7 +401,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     default: ub = std::min<size_t>((size_t)na + nb, kMaxKeys); break;
   }
   OutCtx oc;
-  CHK(prepare_output(c, ub, card_only ? 0 : A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc));
+  CHK(prepare_output(c, ub, card_only ? 0 : A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, !card_only));
   c->mark(0);
   dbg(s, "memset");
   launch_plan_pairwise(s, plan_op, ka, na, kb, nb, c->by_key.as<Task>(), c->flag.as<uint8_t>(),
@@ -386,7 +411,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
                  c->ntasks.as<uint32_t>());
   dbg(s, "compact");
   c->mark(1);
-  const int grid = grid_for((ub + 3) / 4, 1024);  // 4 waves (tasks) per workgroup
+  const int grid = grid_for((ub + 3) / 4, oc.scratch || card_only ? 16384 : 1024);  // 4 waves (tasks) per workgroup
   launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(),
                   OperandView{da, A->payload.as<uint8_t>()}, OperandView{db, B->payload.as<uint8_t>()}, oc,
                   c->task_card.as<uint32_t>());
@@ -481,7 +506,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
   {
     const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
     OutCtx oc;
-    CHK(prepare_output(c, ub, card_only ? 0 : (size_t)8194 * ub + B->payload_bytes, &oc));
+    CHK(prepare_output(c, ub, card_only ? 0 : (size_t)8194 * ub + B->payload_bytes, &oc, !card_only));
     if (!skip.empty()) {
       CHK(c->skip.ensure(skip.size()));
       HIPCHK(hipMemcpyAsync(c->skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
@@ -499,7 +524,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.skip = skip.empty() ? nullptr : c->skip.as<uint8_t>();
     wa.start_bm = start_bm;
     c->mark(1);
-    launch_wide(s, mode, grid_for(ub, 2048), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
+    launch_wide(s, mode, grid_for(ub, oc.scratch || card_only ? 65536 : 2048), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
                 c->task_card.as<uint32_t>());
     c->mark(2);
     if (card_only) {
@@ -1136,7 +1161,8 @@ int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, i
   (void)n;
   (void)key_lo;
   (void)key_hi;
-  if (kind != 0) {
+  // kind 0: C2 mix; 16 + DK_A/DK_B/DK_R: the same generator with one container family
+  if (kind != 0 && !(kind >= 16 && kind <= 18)) {
     set_err("synthetic kind not available");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
@@ -1161,7 +1187,7 @@ int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, i
   HIPCHK(hipMemsetAsync(b.bm.p, 0, 4 * C, s));
   HIPCHK(hipMemcpyAsync(b.key_off.p, key_off.data(), 4 * (kMaxKeys + 1), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 8, hipMemcpyHostToDevice, s));
-  launch_synth_c2(s, seed, b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.payload.as<uint8_t>());
+  launch_synth_c2(s, seed, kind == 0 ? -1 : kind - 16, b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.payload.as<uint8_t>());
   HIPCHK(hipGetLastError());
   std::vector<CDesc> d(C);
   HIPCHK(hipMemcpyAsync(d.data(), b.desc.p, sizeof(CDesc) * C, hipMemcpyDeviceToHost, s));

@@ -152,6 +152,28 @@ constexpr int kQcap = 64;  // long-run queue per wave
 __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
                                         uint32_t len, uint32_t card, uint32_t key, int kind, OutCtx oc) {
   const int l = lane_id();
+  if (oc.scratch) {
+    // scan placement: park the payload (staged results go to the task's slot), record its source
+    uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
+    if (keep && staged) {
+      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+      copy_lds_to_global<64>(slot, lds, len, l);
+      srcaddr = reinterpret_cast<uint64_t>(slot);
+    }
+    if (l == 0) {
+      ORec r;
+      r.off = 0;
+      r.src = srcaddr;
+      r.idx = 0;
+      r.card = card;
+      r.ser_len = len;
+      r.key = (uint16_t)key;
+      r.kind = (uint8_t)kind;
+      r.keep = keep ? 1 : 0;
+      oc.recs[t] = r;
+    }
+    return;
+  }
   const Prefix p = lookback(oc.status, t, keep ? 1u : 0u, keep ? len : 0u, (keep && kind == DK_R) ? 1u : 0u, oc.err);
   const uint32_t idx = p.idx;
   const uint64_t off = p.off;
@@ -163,6 +185,7 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
   if (l == 0) {
     ORec r;
     r.off = off;
+    r.src = 0;
     r.idx = idx;
     r.card = card;
     r.ser_len = len;
@@ -218,12 +241,22 @@ __global__ __launch_bounds__(256) void k_pair_wave(const Task* __restrict__ task
   uint32_t* lds = lds_all[w];
   int* q = q_all[w];
   const uint32_t nt = uni(*n_tasks);
+  // Look-back placement (MODE 0 without scratch) must take tasks in ticket
+  // order; the scan placement and the cardinality mode use a static stride --
+  // one contended counter costs ~12 ns per task chip-wide.
+  const bool ticketed = oc.scratch == nullptr && MODE == 0;
+  const uint32_t wstride = gridDim.x * kWaves;
+  uint32_t t = blockIdx.x * kWaves + w - wstride;
   for (;;) {
-    // every lane runs the atomic (lane 0 adds 1, the others 0): the ticket is
-    // provably wave-uniform, so all control flow below stays scalar.  (A
-    // lane-0-only atomic + shuffle made the compiler treat the task as divergent
-    // and the resulting kernel hung on gfx950.)
-    const uint32_t t = uni(atomicAdd(oc.ticket, l == 0 ? 1u : 0u));
+    if (ticketed) {
+      // every lane runs the atomic (lane 0 adds 1, the others 0): the ticket is
+      // provably wave-uniform, so all control flow below stays scalar.  (A
+      // lane-0-only atomic + shuffle made the compiler treat the task as
+      // divergent and the resulting kernel hung on gfx950.)
+      t = uni(atomicAdd(oc.ticket, l == 0 ? 1u : 0u));
+    } else {
+      t = uni(t + wstride);
+    }
     if (t >= nt) break;
     Task tk = tasks[t];
     tk.a = (int32_t)uni((uint32_t)tk.a);
@@ -394,6 +427,105 @@ __global__ __launch_bounds__(256) void k_batch_bytes(const CDesc* __restrict__ d
 }
 
 // ===========================================================================
+// scan placement: tile scan of the task records (uniform tiles, so a decoupled
+// look-back over tiles never waits on a slow container), then the payload copy
+// ===========================================================================
+constexpr int kTile = 1024;  // tasks per workgroup tile (4 per thread)
+
+__global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_tasks, OutCtx oc) {
+  __shared__ int wsum[3][4];
+  __shared__ unsigned long long wbytes[4];
+  __shared__ Prefix shp;
+  __shared__ uint32_t tsh;
+  const uint32_t nt = *n_tasks;
+  const uint32_t ntiles = (nt + kTile - 1) / kTile;
+  for (;;) {
+    __syncthreads();
+    if (threadIdx.x == 0) tsh = atomicAdd(oc.tile_ticket, 1u);
+    __syncthreads();
+    const uint32_t tile = uni(tsh);
+    if (tile >= ntiles) break;
+    const uint32_t t0 = tile * kTile + 4 * threadIdx.x;
+    uint32_t keep[4], len[4], run[4];
+    uint32_t c = 0, r = 0;
+    unsigned long long b = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      keep[i] = len[i] = run[i] = 0;
+      if (t0 + i < nt) {
+        const ORec x = oc.recs[t0 + i];
+        keep[i] = x.keep;
+        len[i] = x.keep ? x.ser_len : 0;
+        run[i] = x.keep && x.kind == DK_R;
+      }
+      c += keep[i];
+      b += len[i];
+      r |= run[i];
+    }
+    // workgroup exclusive scan of (count, bytes), OR of run
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int tc;
+    const int pc = wave_excl((int)c, &tc);
+    unsigned long long sb = b;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long u = __shfl_up(sb, o, 64);
+      if (lane >= o) sb += u;
+    }
+    const unsigned long long wb = __shfl(sb, 63, 64);
+    const int wr = __any(r) ? 1 : 0;
+    if (lane == 0) {
+      wsum[0][w] = tc;
+      wsum[1][w] = wr;
+      wbytes[w] = wb;
+    }
+    __syncthreads();
+    uint32_t oc_c = 0, tot_c = 0, tot_r = 0;
+    unsigned long long oc_b = 0, tot_b = 0;
+    for (int i = 0; i < 4; i++) {
+      if (i < w) {
+        oc_c += wsum[0][i];
+        oc_b += wbytes[i];
+      }
+      tot_c += wsum[0][i];
+      tot_b += wbytes[i];
+      tot_r |= wsum[1][i];
+    }
+    if (threadIdx.x < 64) {
+      const Prefix pw = lookback(oc.tile_status, tile, tot_c, tot_b, tot_r, oc.err);
+      if (threadIdx.x == 0) shp = pw;
+    }
+    __syncthreads();
+    uint32_t idx = shp.idx + oc_c + (uint32_t)pc;
+    unsigned long long off = shp.off + oc_b + (sb - b);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (t0 + i < nt) {
+        oc.recs[t0 + i].idx = idx;
+        oc.recs[t0 + i].off = off;
+      }
+      idx += keep[i];
+      off += len[i];
+    }
+    if (tile == ntiles - 1 && threadIdx.x == 0) {
+      // totals word where the header kernels look for it (status[n_tasks - 1])
+      const uint64_t incl = __hip_atomic_load(oc.tile_status + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(oc.status + nt - 1, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// payload copies of the scan placement: one workgroup per task (grid-stride)
+__global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ n_tasks, OutCtx oc) {
+  const uint32_t nt = *n_tasks;
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const ORec r = oc.recs[t];
+    if (!r.keep) continue;
+    group_copy<NT>(oc.out + oc.payload_base + r.off, reinterpret_cast<const uint8_t*>(r.src), r.ser_len,
+                   threadIdx.x);
+  }
+}
+
+// ===========================================================================
 // host launchers
 // ===========================================================================
 void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const uint16_t* kb, int nb, Task* by_key,
@@ -430,6 +562,10 @@ void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* task
 }
 
 void launch_header(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out, ResultInfo* info) {
+  if (oc.scratch) {
+    hipLaunchKernelGGL(k_place, dim3(64), dim3(256), 0, s, nt, oc);
+    hipLaunchKernelGGL(k_emit, dim3(4096), dim3(256), 0, s, nt, oc);
+  }
   hipLaunchKernelGGL(k_header, dim3(grid), dim3(256), 0, s, nt, oc, kind_by_out, info);
   hipLaunchKernelGGL(k_runflags, dim3(32), dim3(256), 0, s, nt, oc, (const uint8_t*)kind_by_out);
 }

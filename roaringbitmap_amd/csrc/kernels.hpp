@@ -53,6 +53,7 @@ void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_o
                            const uint8_t* payload, int32_t* out);
 
 // synthetic generators (synth.hip)
-void launch_synth_c2(hipStream_t s, uint64_t seed, CDesc* desc, uint16_t* keys, uint8_t* payload);
+// force < 0: C2 mix (kind drawn per key); force = DK_A/DK_B/DK_R: every key drawn from that family
+void launch_synth_c2(hipStream_t s, uint64_t seed, int force, CDesc* desc, uint16_t* keys, uint8_t* payload);
 
 }  // namespace rbg

@@ -13,6 +13,28 @@ namespace rbg {
 __device__ __forceinline__ void wg_place(uint32_t t, bool keep, const uint8_t* src, bool staged,
                                          const uint32_t* stage, uint32_t len, uint32_t card, uint32_t key, int kind,
                                          const OutCtx& oc, Prefix* shp) {
+  if (oc.scratch) {  // scan placement: park staged results in the task's slot
+    uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
+    if (keep && staged) {
+      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+      copy_lds_to_global<NT>(slot, stage, len, threadIdx.x);
+      srcaddr = reinterpret_cast<uint64_t>(slot);
+    }
+    if (threadIdx.x == 0) {
+      ORec r;
+      r.off = 0;
+      r.src = srcaddr;
+      r.idx = 0;
+      r.card = card;
+      r.ser_len = len;
+      r.key = (uint16_t)key;
+      r.kind = (uint8_t)kind;
+      r.keep = keep ? 1 : 0;
+      oc.recs[t] = r;
+    }
+    __syncthreads();
+    return;
+  }
   if (threadIdx.x < 64) {  // wave 0 runs the (wave-uniform) look-back
     const Prefix pw = lookback(oc.status, t, keep ? 1u : 0u, keep ? len : 0u, (keep && kind == DK_R) ? 1u : 0u, oc.err);
     if (threadIdx.x == 0) *shp = pw;
@@ -27,6 +49,7 @@ __device__ __forceinline__ void wg_place(uint32_t t, bool keep, const uint8_t* s
   if (threadIdx.x == 0) {
     ORec r;
     r.off = p.off;
+    r.src = 0;
     r.idx = p.idx;
     r.card = card;
     r.ser_len = len;
@@ -138,11 +161,19 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
   __shared__ Prefix shp;
   __shared__ uint32_t tsh;
   const uint32_t nt = *n_tasks;
+  // look-back placement needs tasks in ticket order; scan placement and the
+  // cardinality modes take a static grid stride (no contended counter)
+  const bool ticketed = oc.scratch == nullptr && MODE != WIDE_OR_CARD && MODE != WIDE_AND_SHY_CARD;
+  uint32_t t = blockIdx.x - gridDim.x;
   while (true) {
-    __syncthreads();
-    if (threadIdx.x == 0) tsh = atomicAdd(oc.ticket, 1u);
-    __syncthreads();
-    const uint32_t t = uni(tsh);
+    if (ticketed) {
+      __syncthreads();
+      if (threadIdx.x == 0) tsh = atomicAdd(oc.ticket, 1u);
+      __syncthreads();
+      t = uni(tsh);
+    } else {
+      t += gridDim.x;
+    }
     if (t >= nt) break;
     const Task tk = tasks[t];
     const uint32_t s = uni((uint32_t)tk.a), n = uni((uint32_t)tk.b);
@@ -478,15 +509,15 @@ __device__ __forceinline__ uint64_t bernoulli_word(uint64_t seed, uint32_t thr) 
   return w;
 }
 
-__global__ __launch_bounds__(256) void k_synth_c2(uint64_t seed, CDesc* __restrict__ desc, uint16_t* __restrict__ keys,
-                                                  uint8_t* __restrict__ payload) {
+__global__ __launch_bounds__(256) void k_synth_c2(uint64_t seed, int force, CDesc* __restrict__ desc,
+                                                  uint16_t* __restrict__ keys, uint8_t* __restrict__ payload) {
   __shared__ __align__(16) uint32_t acc[2048];
   __shared__ __align__(16) uint32_t tmp[2048];
   __shared__ int q[257];
   __shared__ int sh[8];
   for (uint32_t k = blockIdx.x; k < 65536; k += gridDim.x) {
     const uint64_t hk = splitmix(seed ^ ((uint64_t)k << 20));
-    const int kind_pick = (int)(hk % 3);
+    const int kind_pick = force >= 0 ? force : (int)(hk % 3);
     uint64_t r[4];
     const uint32_t t = threadIdx.x;
     const uint32_t widx[4] = {2 * t, 2 * t + 1, 512 + 2 * t, 513 + 2 * t};
@@ -541,8 +572,8 @@ __global__ __launch_bounds__(256) void k_synth_c2(uint64_t seed, CDesc* __restri
   }
 }
 
-void launch_synth_c2(hipStream_t s, uint64_t seed, CDesc* desc, uint16_t* keys, uint8_t* payload) {
-  hipLaunchKernelGGL(k_synth_c2, dim3(4096), dim3(256), 0, s, seed, desc, keys, payload);
+void launch_synth_c2(hipStream_t s, uint64_t seed, int force, CDesc* desc, uint16_t* keys, uint8_t* payload) {
+  hipLaunchKernelGGL(k_synth_c2, dim3(4096), dim3(256), 0, s, seed, force, desc, keys, payload);
 }
 
 }  // namespace rbg
