@@ -1,0 +1,139 @@
+"""Host-side checks that need no GPU: the C-ABI library loads and exports every
+entry point include/roaring_mi355x.h declares, the host format helpers match the
+oracle byte for byte, error behaviour mirrors the reference's, and compute calls
+fail loudly (no CPU fallback) when no gfx950 device is present.
+"""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from roaringbitmap_amd import _lib as L
+from roaringbitmap_amd import RoaringBitmap, FastAggregation
+from roaringbitmap_amd._lib import DeviceError, InvalidRoaringFormat, TruncatedInput, IllegalArgumentException
+
+import _oracle as O
+from _gen import MODES, container
+
+
+def bitmap_values(rng, mode, n_keys):
+    """Values of a bitmap whose n_keys containers all come from generator mode `mode`."""
+    keys = np.sort(rng.choice(65536, size=n_keys, replace=False)).astype(np.uint32)
+    return np.concatenate([(k << 16) | container(rng, mode)[1].astype(np.uint32) for k in keys])
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "roaring_mi355x.h")
+TESTDATA = os.path.join(ROOT, "tests", "golden", "testdata")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"//[^\n]*", "", src)
+    return sorted(set(re.findall(r"\b(rbg_\w+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert "rbg_pairwise" in names and "rbg_wide" in names and "rbg_ctx_fetch_shard" in names
+    assert len(names) >= 30
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(L.LIB_PATH)
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_python_binding_covers_header():
+    assert sorted(L.EXPORTED) == sorted(n for n in _declared() if n in L.EXPORTED)
+    assert set(_declared()) <= set(L.EXPORTED)
+
+
+def test_version():
+    assert L.lib().rbg_version() >= 1
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("run_opt", [False, True])
+def test_from_values_matches_oracle(mode, run_opt):
+    rng = np.random.default_rng(hash(mode) & 0xFFFF)
+    vals = bitmap_values(rng, mode, n_keys=4)
+    got = RoaringBitmap.from_values(vals, run_optimize=run_opt).serialize()
+    assert got == O.from_values(vals, run_optimize=run_opt)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_run_optimize_and_to_values(mode):
+    rng = np.random.default_rng(7 + (hash(mode) & 0xFF))
+    vals = bitmap_values(rng, mode, n_keys=3)
+    rb = RoaringBitmap.from_values(vals)
+    rb2 = rb.clone()
+    rb2.runOptimize()
+    assert rb2.serialize() == O.run_optimize(rb.serialize())
+    assert np.array_equal(rb2.toArray(), np.unique(np.asarray(vals, dtype=np.uint32)))
+    assert rb2.getLongCardinality() == len(np.unique(vals))
+
+
+@pytest.mark.parametrize("name", ["bitmapwithruns.bin", "bitmapwithoutruns.bin"])
+def test_deserialize_reference_files(name):
+    data = open(os.path.join(TESTDATA, name), "rb").read()
+    rb = RoaringBitmap.deserialize(data)
+    st = O.stats(data)
+    assert rb.getLongCardinality() == st["card"]
+    assert np.array_equal(rb.toArray(), O.to_values(data))
+
+
+@pytest.mark.parametrize("i", range(1, 9))
+def test_crashprone_inputs_raise_like_reference(i):
+    """TestAdversarialInputs.java:50-54: deserialize of the crashprone inputs must
+    throw an IOException (both our errors are OSError) and never crash.  The
+    engine also rejects non-increasing keys (which Java leaves unchecked), so
+    the exact subclass may differ from the oracle's first failure."""
+    data = open(os.path.join(TESTDATA, f"crashproneinput{i}.bin"), "rb").read()
+    st, _, _ = O.roundtrip(data)
+    assert st != 0
+    with pytest.raises(OSError):
+        RoaringBitmap.deserialize(data)
+
+
+def test_truncated_and_bad_cookie():
+    data = RoaringBitmap.bitmapOf(1, 2, 3, 70000).serialize()
+    with pytest.raises(TruncatedInput):
+        RoaringBitmap.deserialize(data[:-1])
+    with pytest.raises(InvalidRoaringFormat):
+        RoaringBitmap.deserialize(b"\x00\x00\x00\x00" + data[4:])
+
+
+def test_java_int_cardinality_wraps():
+    rb = RoaringBitmap.from_values(np.arange(0, 1 << 31, 1 << 10, dtype=np.uint32))
+    assert rb.getLongCardinality() == 1 << 21
+    assert rb.getCardinality() == 1 << 21
+
+
+def _have_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.mark.skipif(_have_gpu(), reason="checks the no-device failure mode")
+def test_compute_fails_loudly_without_device():
+    a = RoaringBitmap.bitmapOf(1, 2, 3)
+    b = RoaringBitmap.bitmapOf(2, 3, 4)
+    with pytest.raises(DeviceError):
+        RoaringBitmap.and_(a, b)
+    with pytest.raises(DeviceError):
+        RoaringBitmap.andCardinality(a, b)
+    with pytest.raises(DeviceError):
+        FastAggregation.or_(a, b)
+
+
+def test_illegal_argument_type():
+    assert issubclass(IllegalArgumentException, ValueError)
+    with pytest.raises(IllegalArgumentException):
+        L.check(L.RBG_ERR_ILLEGAL_ARGUMENT)
