@@ -145,7 +145,6 @@ __device__ __forceinline__ uint32_t ser_len_of(const CDesc& d, const uint8_t* pa
 }
 
 constexpr int kWaves = 4;  // waves per workgroup in the wave-per-task kernels
-constexpr int kQcap = 64;  // long-run queue per wave
 
 // Emits one task's output: look-back placement + payload write + record.
 // `staged` = payload is in the wave's LDS; otherwise copied from `src` (global).
@@ -199,7 +198,7 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
 // One task, processed by one wave.  Every branch below is wave-uniform (scalar).
 template <int OP, int MODE>
 __device__ __forceinline__ void pair_task(uint32_t t, const Task& tk, const OperandView& A, const OperandView& B,
-                                          const OutCtx& oc, uint32_t* task_card, uint32_t* lds, int* q) {
+                                          const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
   const int l = lane_id();
   if (tk.a < 0 || tk.b < 0) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
     if (MODE == 0) {
@@ -213,8 +212,8 @@ __device__ __forceinline__ void pair_task(uint32_t t, const Task& tk, const Oper
     const CDesc da = A.desc[tk.a];
     const CDesc db = B.desc[tk.b];
     WCtr x;
-    w_materialize(da, A.payload, lds, q, kQcap, x);
-    w_combine<OP>(db, B.payload, lds, q, kQcap, x);
+    w_materialize(da, A.payload, lds, x);
+    w_combine<OP>(db, B.payload, lds, x);
     const int c = w_card(x);
     if (MODE == 1) {
       if (l == 0) task_card[t] = (uint32_t)c;
@@ -236,10 +235,8 @@ __global__ __launch_bounds__(256) void k_pair_wave(const Task* __restrict__ task
                                                    OperandView A, OperandView B, OutCtx oc,
                                                    uint32_t* __restrict__ task_card) {
   __shared__ __align__(16) uint32_t lds_all[kWaves][2048];
-  __shared__ int q_all[kWaves][kQcap];
   const int w = threadIdx.x >> 6, l = lane_id();
   uint32_t* lds = lds_all[w];
-  int* q = q_all[w];
   const uint32_t nt = uni(*n_tasks);
   // Look-back placement (MODE 0 without scratch) must take tasks in ticket
   // order; the scan placement and the cardinality mode use a static stride --
@@ -262,7 +259,7 @@ __global__ __launch_bounds__(256) void k_pair_wave(const Task* __restrict__ task
     tk.a = (int32_t)uni((uint32_t)tk.a);
     tk.b = (int32_t)uni((uint32_t)tk.b);
     tk.key = uni(tk.key);
-    pair_task<OP, MODE>(t, tk, A, B, oc, task_card, lds, q);
+    pair_task<OP, MODE>(t, tk, A, B, oc, task_card, lds);
   }
 }
 

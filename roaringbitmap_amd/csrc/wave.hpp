@@ -87,74 +87,124 @@ __device__ __forceinline__ void w_clear_lds(uint32_t* lds) {
   for (int i = 0; i < 8; i++) q[64 * i] = make_uint4(0, 0, 0, 0);
 }
 
-// OR/XOR the values of an array container into the wave's LDS bitmap
+// OR/XOR the values of an array container (<= 4096 values, 16 B aligned slot)
+// into the wave's LDS bitmap.  All of a lane's 16 B vectors are loaded before
+// the first LDS atomic so the loads overlap (one memory latency per container),
+// and bits of consecutive sorted values that share a 32-bit word are merged
+// into one atomic.
+constexpr int kVecRound = 4;  // 16 B vectors per lane loaded per round
+
 template <int MODE>  // 0 or, 1 xor
 __device__ __forceinline__ void w_scatter_array(uint32_t* lds, const uint16_t* vals, int card) {
-  const int nvec = (card + 7) >> 3;
+  const int nvec = (card + 7) >> 3;  // <= 512 = 8 per lane, in rounds of 4
   const uint4* v4 = reinterpret_cast<const uint4*>(vals);
-  for (int i = lane_id(); i < nvec; i += WL) {
-    const uint4 v = v4[i];
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    const int base = i * 8;
+  const int l = lane_id();
+#pragma unroll 1
+  for (int j0 = 0; 64 * j0 < nvec; j0 += kVecRound) {
+    uint4 v[kVecRound];
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-      if (base + j < card) {
-        const uint32_t x = (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFF;
-        if (MODE == 0) atomicOr(&lds[x >> 5], 1u << (x & 31));
-        else atomicXor(&lds[x >> 5], 1u << (x & 31));
+    for (int j = 0; j < kVecRound; j++) {
+      const int k = 64 * (j0 + j) + l;
+      v[j] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+  for (int j = 0; j < kVecRound; j++) {
+    const int base = 8 * (64 * (j0 + j) + l);
+    if (base >= card) break;
+    const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    uint32_t cur = 0xFFFFFFFFu, mask = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      if (base + i < card) {
+        const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
+        if ((x >> 5) != cur) {
+          if (mask) {
+            if (MODE == 0) atomicOr(&lds[cur], mask);
+            else atomicXor(&lds[cur], mask);
+          }
+          cur = x >> 5;
+          mask = 0;
+        }
+        mask |= 1u << (x & 31);
       }
     }
+    if (mask) {
+      if (MODE == 0) atomicOr(&lds[cur], mask);
+      else atomicXor(&lds[cur], mask);
+    }
+  }
   }
 }
 
-// OR the runs of a run container into the wave's LDS bitmap.  Runs spanning more
-// than 8 words go through a per-wave queue (capacity qcap) and are filled by all
-// lanes together.
-__device__ __forceinline__ void w_or_runs(uint32_t* lds, const uint32_t* pairs, int nruns, int* q, int qcap) {
+// Run containers are materialised without per-word fills: every run toggles its
+// first bit and the bit after its last one in a cleared LDS bitmap (2 LDS
+// atomics per run, no divergence on run length), and an inclusive prefix-XOR
+// over the 65536 bits then turns the toggles into the filled runs.  Valid run
+// containers have disjoint runs, so toggles of adjacent runs cancel correctly.
+__device__ __forceinline__ void w_toggle_runs(uint32_t* lds, const uint8_t* slot, int nruns) {
+  // slot = [u16 pad][u16 nruns][u32 (start, len-1) pairs]: u32 k of the slot is
+  // run k-1, so the slot streams as aligned 16 B vectors (input run containers
+  // may hold up to 32768 runs; results hold at most 2047)
+  const int nvec = (nruns + 4) >> 2;
+  const uint4* v4 = reinterpret_cast<const uint4*>(slot);
   const int l = lane_id();
-  int nq = 0;
-  for (int base = 0; base < nruns; base += WL) {
-    const int i = base + l;
-    bool is_long = false;
-    int s = 0, e = 0;
-    if (i < nruns) {
-      const uint32_t p = pairs[i];
-      s = (int)(p & 0xFFFF);
-      e = s + (int)(p >> 16);
-      is_long = (e >> 5) - (s >> 5) > 8;
-      if (!is_long) lds_or_run_serial(lds, s, e);
+#pragma unroll 1
+  for (int j0 = 0; 64 * j0 < nvec; j0 += kVecRound) {
+    uint4 v[kVecRound];
+#pragma unroll
+    for (int j = 0; j < kVecRound; j++) {
+      const int k = 64 * (j0 + j) + l;
+      v[j] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
     }
-    const uint64_t m = __ballot(is_long);
-    if (m) {
-      const int pos = nq + __popcll(m & ((1ULL << l) - 1));
-      if (is_long) {
-        if (pos < qcap) q[pos] = i;
-        else lds_or_run_serial(lds, s, e);
+#pragma unroll
+  for (int j = 0; j < kVecRound; j++) {
+    const int r0 = 4 * (64 * (j0 + j) + l) - 1;
+    if (r0 >= nruns) break;
+    const uint32_t u[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int r = r0 + c;
+      if (r >= 0 && r < nruns) {
+        const uint32_t s = u[c] & 0xFFFF, e1 = s + (u[c] >> 16) + 1;
+        atomicXor(&lds[s >> 5], 1u << (s & 31));
+        if (e1 < 65536) atomicXor(&lds[e1 >> 5], 1u << (e1 & 31));
       }
-      nq += __popcll(m);
     }
   }
-  wsync();
-  nq = min(nq, qcap);
-  for (int k = 0; k < nq; k++) {
-    const uint32_t p = pairs[q[k]];
-    const int s = (int)(p & 0xFFFF);
-    const int e = s + (int)(p >> 16);
-    const int ws = s >> 5, we = e >> 5;
-    for (int w = ws + l; w <= we; w += WL) {
-      uint32_t m = ~0u;
-      if (w == ws) m &= ~0u << (s & 31);
-      if (w == we) m &= ~0u >> (31 - (e & 31));
-      if (m == ~0u) lds[w] = ~0u;
-      else atomicOr(&lds[w], m);
-    }
   }
-  wsync();
+}
+
+__device__ __forceinline__ uint64_t prefix_xor64(uint64_t x) {
+  x ^= x << 1;
+  x ^= x << 2;
+  x ^= x << 4;
+  x ^= x << 8;
+  x ^= x << 16;
+  x ^= x << 32;
+  return x;
+}
+
+// Chunk i (words 128i + 2l + {0,1}) of the filled run bitmap from the toggle
+// bitmap in LDS.  `carry` (wave-uniform) is the parity of all earlier chunks.
+__device__ __forceinline__ void w_run_chunk(const uint32_t* lds, int i, uint32_t& carry, uint64_t& w0, uint64_t& w1) {
+  const int l = lane_id();
+  const uint4 v = reinterpret_cast<const uint4*>(lds)[64 * i + l];
+  uint64_t a = prefix_xor64((uint64_t)v.x | ((uint64_t)v.y << 32));
+  uint64_t b = prefix_xor64((uint64_t)v.z | ((uint64_t)v.w << 32));
+  if (a >> 63) b = ~b;
+  const uint64_t m = __ballot((b >> 63) != 0);  // per-lane parity of its two words
+  const uint32_t pre = ((uint32_t)__popcll(m & ((1ULL << l) - 1)) & 1u) ^ carry;
+  if (pre) {
+    a = ~a;
+    b = ~b;
+  }
+  carry ^= (uint32_t)__popcll(m) & 1u;
+  w0 = a;
+  w1 = b;
 }
 
 // Materialise any container into registers.  `lds` is the wave's 8 KiB bitmap.
-__device__ __forceinline__ void w_materialize(const CDesc& d, const uint8_t* payload, uint32_t* lds, int* q,
-                                              int qcap, WCtr& x) {
+__device__ __forceinline__ void w_materialize(const CDesc& d, const uint8_t* payload, uint32_t* lds, WCtr& x) {
   const uint8_t* slot = payload + d.slot;
   if (d.kind == DK_B) {
     w_load_bitmap(slot, x);
@@ -166,11 +216,15 @@ __device__ __forceinline__ void w_materialize(const CDesc& d, const uint8_t* pay
   if (d.kind == DK_A) {
     w_scatter_array<0>(lds, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
     wsync();
+    w_read_lds(lds, x);
   } else {
     const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
-    w_or_runs(lds, reinterpret_cast<const uint32_t*>(slot + 4), nr, q, qcap);
+    w_toggle_runs(lds, slot, nr);
+    wsync();
+    uint32_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) w_run_chunk(lds, i, carry, x.w[2 * i], x.w[2 * i + 1]);
   }
-  w_read_lds(lds, x);
 }
 
 // x = x OP (container d), materialising d chunk by chunk (no second register copy).
@@ -182,9 +236,25 @@ __device__ __forceinline__ uint64_t w_op(uint64_t a, uint64_t b) {
   return a & ~b;
 }
 template <int OP>
-__device__ __forceinline__ void w_combine(const CDesc& d, const uint8_t* payload, uint32_t* lds, int* q, int qcap,
-                                          WCtr& x) {
+__device__ __forceinline__ void w_combine(const CDesc& d, const uint8_t* payload, uint32_t* lds, WCtr& x) {
   const uint8_t* slot = payload + d.slot;
+  if (d.kind == DK_R) {
+    wsync();
+    w_clear_lds(lds);
+    wsync();
+    const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
+    w_toggle_runs(lds, slot, nr);
+    wsync();
+    uint32_t carry = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      uint64_t a, b;
+      w_run_chunk(lds, i, carry, a, b);
+      x.w[2 * i] = w_op<OP>(x.w[2 * i], a);
+      x.w[2 * i + 1] = w_op<OP>(x.w[2 * i + 1], b);
+    }
+    return;
+  }
   const uint4* src;
   if (d.kind == DK_B) {
     src = reinterpret_cast<const uint4*>(slot) + lane_id();
@@ -192,13 +262,8 @@ __device__ __forceinline__ void w_combine(const CDesc& d, const uint8_t* payload
     wsync();
     w_clear_lds(lds);
     wsync();
-    if (d.kind == DK_A) {
-      w_scatter_array<0>(lds, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
-      wsync();
-    } else {
-      const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
-      w_or_runs(lds, reinterpret_cast<const uint32_t*>(slot + 4), nr, q, qcap);
-    }
+    w_scatter_array<0>(lds, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
+    wsync();
     src = reinterpret_cast<const uint4*>(lds) + lane_id();
   }
 #pragma unroll
