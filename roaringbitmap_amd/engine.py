@@ -112,6 +112,10 @@ class Engine:
         check(lib().rbg_ctx_result_stats(self._ctx, s))
         return {"containers": s[0], "payload_bytes": s[1], "has_run": s[2], "cardinality": s[3]}
 
+    def serialize(self):
+        """Enqueue the on-device portable serialization of the last result."""
+        check(lib().rbg_ctx_serialize(self._ctx))
+
     def fetch(self) -> RoaringBitmap:
         b = _lib.rbg_buffer()
         check(lib().rbg_ctx_fetch(self._ctx, ctypes.byref(b)))
