@@ -41,7 +41,7 @@ def _pmc_traffic():
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("k_pairwise_and", {}).get("hbm_bytes_per_launch")
+            return json.load(f).get("k_pair_wave", {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
 

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile.sh run (gpurun_out/prof_<tag>) into profiles/<tag>/.
+
+Writes
+  profiles/<tag>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<tag>/bench_kt.json      the bench line printed under the kernel trace
+  profiles/<tag>/pmc_summary.json   per-kernel mean counters over the --pmc passes
+  profiles/pmc_traffic.json         HBM bytes per launch of the dominant kernel (read by bench.py)
+
+HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE reports half the bytes of 16 B/lane streaming reads, so it is
+doubled; WRITE_SIZE is exact for 16 B/lane stores.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DOMINANT = "k_pair_wave"
+
+
+def counters(path):
+    acc = defaultdict(lambda: defaultdict(list))
+    if not os.path.exists(path):
+        return acc
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            name = row["Kernel_Name"].split("(")[0].strip()
+            acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return acc
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles", tag)
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    if os.path.exists(os.path.join(src, "bench_kt.json")):
+        shutil.copy(os.path.join(src, "bench_kt.json"), os.path.join(dst, "bench_kt.json"))
+    summary = {}
+    for sub in sorted(os.listdir(src)):
+        p = os.path.join(src, sub, "run_counter_collection.csv")
+        if not sub.startswith("pmc") or not os.path.exists(p):
+            continue
+        for k, cs in counters(p).items():
+            for c, vals in cs.items():
+                summary.setdefault(k, {})[c] = {"mean": sum(vals) / len(vals), "n": len(vals)}
+    with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1, sort_keys=True)
+    d = summary.get(DOMINANT, {})
+    if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+        rd = 2.0 * d["FETCH_SIZE"]["mean"] * 1024
+        wr = d["WRITE_SIZE"]["mean"] * 1024
+        traffic = {DOMINANT: {"hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
+                              "source": f"profiles/{tag}/pmc_summary.json",
+                              "correction": "FETCH_SIZE x2 (gfx950 streaming-read tally), KiB -> bytes"}}
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
+            json.dump(traffic, f, indent=1)
+        print(json.dumps(traffic))
+    print("wrote", dst)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
