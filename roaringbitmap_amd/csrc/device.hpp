@@ -48,6 +48,17 @@ struct Task {
   int32_t aux;
 };
 
+// Pairwise task (32 B): the plan kernel resolves both operands' descriptors so
+// the compute kernel reads one record per task with scalar loads.
+constexpr uint8_t kAbsent = 0xFF;
+struct __align__(16) PTask {
+  uint64_t slot_a, slot_b;  // payload slot offsets in the operands' arenas
+  uint32_t card_a, card_b;
+  uint16_t key;
+  uint8_t kind_a, kind_b;   // DK_A / DK_B / DK_R, or kAbsent (key not in that operand)
+  uint16_t nruns_a, nruns_b;  // run count of R operands (0 otherwise)
+};
+
 struct ResultInfo {
   uint32_t n_out;
   uint32_t has_run;
@@ -106,20 +117,32 @@ __device__ __forceinline__ int eff(int c, int r) {
 // ---------------------------------------------------------------------------
 // wave / block reductions and scans
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+// Wave-wide inclusive prefix sum with DPP (row shifts, then row broadcasts):
+// six VALU ops, no LDS round trips (ds_bpermute-based shuffles cost ~100
+// cycles of latency each and serialise every scan).
+__device__ __forceinline__ int dpp_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
 }
-__device__ __forceinline__ int wave_incl_scan(int v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    int u = __shfl_up(v, o, 64);
-    if (lane >= o) v += u;
-  }
-  return v;
+// value of lane 63 / lane 0 (wave-uniform, SGPR)
+__device__ __forceinline__ int lane63(int x) { return __builtin_amdgcn_readlane(x, 63); }
+__device__ __forceinline__ uint32_t lane63u(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 63); }
+__device__ __forceinline__ uint32_t lane0u(uint32_t x) { return (uint32_t)__builtin_amdgcn_readlane((int)x, 0); }
+// lane l receives lane l-1's / l+1's value; lane 0 / lane 63 receive 0
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t x) {
+  return __builtin_amdgcn_update_dpp(0u, x, 0x138, 0xf, 0xf, false);  // wave_shr:1
 }
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
+  return __builtin_amdgcn_update_dpp(0u, x, 0x130, 0xf, 0xf, false);  // wave_shl:1
+}
+
+__device__ __forceinline__ int wave_sum(int v) { return lane63(dpp_incl_scan(v)); }
+__device__ __forceinline__ int wave_incl_scan(int v) { return dpp_incl_scan(v); }
 
 // Sum of (a, b) over the workgroup; `sh` needs 8 ints.  Ends with a barrier.
 __device__ __forceinline__ void block_sum2(int& a, int& b, int* sh) {

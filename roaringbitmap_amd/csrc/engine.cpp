@@ -149,9 +149,9 @@ static int ctx_init(Ctx* c, int device) {
   }
   c->device = device;
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  CHK(c->by_key.ensure(sizeof(Task) * kMaxKeys));
+  CHK(c->by_key.ensure(sizeof(PTask) * kMaxKeys));  // Task (wide) or PTask (pairwise) records
   CHK(c->flag.ensure(kMaxKeys));
-  CHK(c->tasks.ensure(sizeof(Task) * kMaxKeys));
+  CHK(c->tasks.ensure(sizeof(PTask) * kMaxKeys));
   CHK(c->ntasks.ensure(64));
   CHK(c->wg_count.ensure(4 * 256));
   CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + kMaxTiles)));
@@ -413,17 +413,14 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only));
   c->mark(0);
   dbg(s, "memset");
-  launch_plan_pairwise(s, plan_op, ka, na, kb, nb, c->by_key.as<Task>(), c->flag.as<uint8_t>(),
-                       c->wg_count.as<uint32_t>());
-  dbg(s, "plan");
-  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
-                 c->ntasks.as<uint32_t>());
+  launch_plan_pairwise(s, plan_op, ka, na, da, A->payload.as<uint8_t>(), kb, nb, db, B->payload.as<uint8_t>(),
+                       c->by_key.as<PTask>(), c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(),
+                       c->tasks.as<PTask>(), c->ntasks.as<uint32_t>());
   dbg(s, "compact");
   c->mark(1);
   const int grid = grid_for((ub + 3) / 4, 16384);  // 4 waves (tasks) per workgroup, clamped to the resident grid
-  launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(),
-                  OperandView{da, A->payload.as<uint8_t>()}, OperandView{db, B->payload.as<uint8_t>()}, oc,
-                  c->task_card.as<uint32_t>());
+  launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(),
+                  A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), oc, c->task_card.as<uint32_t>());
   dbg(s, "pairwise");
   c->mark(2);
   if (card_only) {

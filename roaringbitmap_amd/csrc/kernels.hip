@@ -23,47 +23,6 @@ namespace rbg {
 // ===========================================================================
 // plan / compact
 // ===========================================================================
-__device__ __forceinline__ int lower_bound_u16(const uint16_t* keys, int n, uint32_t k) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (keys[mid] < k) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-__device__ __forceinline__ void plan_count(int f, uint32_t* wg_count) {
-  __shared__ int wc[4];
-  const uint64_t m = __ballot(f);
-  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
-  __syncthreads();
-  if (threadIdx.x == 0) wg_count[blockIdx.x] = (uint32_t)(wc[0] + wc[1] + wc[2] + wc[3]);
-}
-
-// Key alignment of two sorted key arrays (the advanceUntil walks of
-// RB/RoaringBitmap.java:382-400, :864-896, :1076-1113, :449-471), one thread per key.
-__global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint16_t* __restrict__ ka, int na,
-                                                       const uint16_t* __restrict__ kb, int nb,
-                                                       Task* __restrict__ by_key, uint8_t* __restrict__ flag,
-                                                       uint32_t* __restrict__ wg_count) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  const int pa = lower_bound_u16(ka, na, k);
-  const int pb = lower_bound_u16(kb, nb, k);
-  const int ia = (pa < na && ka[pa] == k) ? pa : -1;
-  const int ib = (pb < nb && kb[pb] == k) ? pb : -1;
-  int f;
-  switch (op) {
-    case OP_OR:
-    case OP_XOR: f = (ia >= 0) || (ib >= 0); break;
-    case OP_ANDNOT: f = ia >= 0; break;
-    default: f = (ia >= 0) && (ib >= 0); break;  // AND and every cardinality op
-  }
-  flag[k] = (uint8_t)f;
-  by_key[k] = Task{k, ia, ib, 0};
-  plan_count(f, wg_count);
-}
-
 // Wide plan from the key-major CSR: n_k = key_off[k+1] - key_off[k].
 // mode 0: n_k > 0 (or / xor / orCardinality); mode 1: n_k == n_req (and).
 __global__ __launch_bounds__(256) void k_plan_wide(int mode, const uint32_t* __restrict__ key_off, uint32_t n_req,
@@ -79,8 +38,9 @@ __global__ __launch_bounds__(256) void k_plan_wide(int mode, const uint32_t* __r
 }
 
 // 256 workgroups x 256 keys: each sums the counts of the workgroups before it.
-__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ flag, const Task* __restrict__ by_key,
-                                                 const uint32_t* __restrict__ wg_count, Task* __restrict__ tasks,
+template <class T>
+__global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ flag, const T* __restrict__ by_key,
+                                                 const uint32_t* __restrict__ wg_count, T* __restrict__ tasks,
                                                  uint32_t* __restrict__ n_tasks) {
   __shared__ int wsum[4];
   __shared__ uint32_t base_sh;
@@ -105,134 +65,10 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t* __restrict__ fla
   if (blockIdx.x == gridDim.x - 1 && t == 0) *n_tasks = base_sh + wt[0] + wt[1] + wt[2] + wt[3];
 }
 
-// ===========================================================================
-// pairwise compute, one wavefront per matched key
-// ===========================================================================
-// Result container type of the static pairwise ops as a function of the operand
-// kinds and the result's cardinality c and run count r (DESIGN.md §Type contract,
-// derived from RB/{Array,Bitmap,Run}Container.java):
-//   AND   : R&R -> EFF(c,r) (RB/RunContainer.java:381-456); else BY_CARD(c)
-//   OR    : A|R, R|A, R|R -> EFF(c,r) (:1926-1986); A|A -> BY_CARD(c)
-//           (RB/ArrayContainer.java:949-963); B|x, x|B -> c==65536 ? R.full : B
-//           (RB/BitmapContainer.java:1064-1096, RB/RunContainer.java:1932-1949)
-//   XOR   : R^R -> EFF; R^A, A^R with |A| < 32 -> EFF (RB/RunContainer.java:2410-2424);
-//           else BY_CARD (RB/BitmapContainer.java:1372-1408)
-//   ANDNOT: R\R -> EFF (:637-692); R\A with |A| < 32 -> EFF (:574-591); else BY_CARD
-__device__ __forceinline__ bool pairwise_needs_runs(int op, int ka, int ca, int kb, int cb) {
-  switch (op) {
-    case OP_AND: return ka == DK_R && kb == DK_R;
-    case OP_OR: return (ka == DK_R && kb != DK_B) || (kb == DK_R && ka != DK_B);
-    case OP_XOR:
-      return (ka == DK_R && kb == DK_R) || (ka == DK_R && kb == DK_A && cb < 32) ||
-             (kb == DK_R && ka == DK_A && ca < 32);
-    default:  // ANDNOT
-      return ka == DK_R && (kb == DK_R || (kb == DK_A && cb < 32));
-  }
-}
-__device__ __forceinline__ int pairwise_kind(int op, int ka, int kb, bool use_eff, int c, int r) {
-  if (use_eff) return eff(c, r);
-  if (op == OP_OR && (ka == DK_B || kb == DK_B)) return c == 65536 ? DK_R : DK_B;
-  return by_card(c);
-}
-
-template <int OP>
-__device__ __forceinline__ uint64_t apply_op(uint64_t x, uint64_t y) {
-  if (OP == OP_AND) return x & y;
-  if (OP == OP_OR) return x | y;
-  if (OP == OP_XOR) return x ^ y;
-  return x & ~y;
-}
-
 __device__ __forceinline__ uint32_t ser_len_of(const CDesc& d, const uint8_t* payload) {
   if (d.kind == DK_A) return 2 * d.card;
   if (d.kind == DK_B) return 8192;
   return 2 + 4 * (uint32_t)(*reinterpret_cast<const uint16_t*>(payload + d.slot + 2));
-}
-
-constexpr int kWaves = 4;  // waves per workgroup in the wave-per-task kernels
-
-// Records one task's output: staged results are parked in the task's scratch
-// slot (same layout as an arena slot), pass-through containers are referenced
-// in place.  Placement (k_place) and serialization (k_emit/k_header) follow.
-__device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
-                                        uint32_t len, uint32_t card, uint32_t key, int kind, OutCtx oc) {
-  const int l = lane_id();
-  uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
-  if (keep && staged) {
-    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
-    copy_lds_to_global<64>(slot, lds, len, l);
-    srcaddr = reinterpret_cast<uint64_t>(slot);
-  }
-  if (l == 0) {
-    ORec r;
-    r.off = 0;
-    r.src = srcaddr;
-    r.idx = 0;
-    r.card = card;
-    r.ser_len = len;
-    r.key = (uint16_t)key;
-    r.kind = (uint8_t)kind;
-    r.keep = keep ? 1 : 0;
-    oc.recs[t] = r;
-  }
-}
-
-// One task, processed by one wave.  Every branch below is wave-uniform (scalar).
-template <int OP, int MODE>
-__device__ __forceinline__ void pair_task(uint32_t t, const Task& tk, const OperandView& A, const OperandView& B,
-                                          const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
-  const int l = lane_id();
-  if (tk.a < 0 || tk.b < 0) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
-    if (MODE == 0) {
-      const bool from_a = tk.a >= 0;
-      const CDesc d = from_a ? A.desc[tk.a] : B.desc[tk.b];
-      const uint8_t* pl = from_a ? A.payload : B.payload;
-      w_place(t, true, pl + d.slot + (d.kind == DK_R ? 2 : 0), false, lds, ser_len_of(d, pl), d.card, d.key, d.kind,
-              oc);
-    }
-  } else {
-    const CDesc da = A.desc[tk.a];
-    const CDesc db = B.desc[tk.b];
-    WCtr x;
-    w_materialize(da, A.payload, lds, x);
-    w_combine<OP>(db, B.payload, lds, x);
-    const int c = w_card(x);
-    if (MODE == 1) {
-      if (l == 0) task_card[t] = (uint32_t)c;
-    } else if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389,456,1084)
-      w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
-    } else {
-      const bool use_eff = pairwise_needs_runs(OP, da.kind, (int)da.card, db.kind, (int)db.card);
-      const int nr = use_eff ? w_runs(x) : 0;
-      const int kind = pairwise_kind(OP, da.kind, db.kind, use_eff, c, nr);
-      const uint32_t len = w_stage(kind, x, c, lds);
-      w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, oc);
-    }
-  }
-}
-
-// MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
-template <int OP, int MODE>
-__global__ __launch_bounds__(256) void k_pair_wave(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
-                                                   OperandView A, OperandView B, OutCtx oc,
-                                                   uint32_t* __restrict__ task_card) {
-  __shared__ __align__(16) uint32_t lds_all[kWaves][2048];
-  const int w = threadIdx.x >> 6, l = lane_id();
-  uint32_t* lds = lds_all[w];
-  const uint32_t nt = uni(*n_tasks);
-  // static stride over a resident grid: a contended ticket counter costs
-  // ~12 ns per task chip-wide, a workgroup per task pays a dispatch each
-  const uint32_t wstride = gridDim.x * kWaves;
-  uint32_t t = blockIdx.x * kWaves + w - wstride;
-  for (;;) {
-    t = uni(t + wstride);
-    if (t >= nt) break;
-    Task tk = tasks[t];
-    tk.a = (int32_t)uni((uint32_t)tk.a);
-    tk.b = (int32_t)uni((uint32_t)tk.b);
-    tk.key = uni(tk.key);
-    pair_task<OP, MODE>(t, tk, A, B, oc, task_card, lds);
-  }
 }
 
 __device__ __forceinline__ uint64_t header_bytes(uint32_t size, uint32_t has_run) {
@@ -527,10 +363,6 @@ int resident_grid(const void* kernel) {
 }
 
 static inline int clamp_grid(int grid, const void* kernel) { return std::max(1, std::min(grid, resident_grid(kernel))); }
-void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const uint16_t* kb, int nb, Task* by_key,
-                          uint8_t* flag, uint32_t* wg_count) {
-  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, ka, na, kb, nb, by_key, flag, wg_count);
-}
 void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,
                       Task* by_key, uint8_t* flag, uint32_t* wg_count) {
   hipLaunchKernelGGL(k_plan_wide, dim3(256), dim3(256), 0, s, mode, key_off, n_req, key_lo, key_hi, by_key, flag,
@@ -538,28 +370,11 @@ void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t
 }
 void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
                     uint32_t* n_tasks) {
-  hipLaunchKernelGGL(k_compact, dim3(256), dim3(256), 0, s, flag, by_key, wg_count, tasks, n_tasks);
+  hipLaunchKernelGGL(k_compact<Task>, dim3(256), dim3(256), 0, s, flag, by_key, wg_count, tasks, n_tasks);
 }
-
-template <int OP>
-static void launch_pw(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, OperandView A,
-                      OperandView B, OutCtx oc, uint32_t* task_card) {
-  if (mode == 0)
-    hipLaunchKernelGGL((k_pair_wave<OP, 0>), dim3(clamp_grid(grid, (const void*)&k_pair_wave<OP, 0>)), dim3(256), 0,
-                       s, tasks, nt, A, B, oc, task_card);
-  else
-    hipLaunchKernelGGL((k_pair_wave<OP, 1>), dim3(clamp_grid(grid, (const void*)&k_pair_wave<OP, 1>)), dim3(256), 0,
-                       s, tasks, nt, A, B, oc, task_card);
-}
-
-void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* tasks, const uint32_t* nt, OperandView A,
-                     OperandView B, OutCtx oc, uint32_t* task_card) {
-  switch (op) {
-    case OP_AND: launch_pw<OP_AND>(s, mode, grid, tasks, nt, A, B, oc, task_card); break;
-    case OP_OR: launch_pw<OP_OR>(s, mode, grid, tasks, nt, A, B, oc, task_card); break;
-    case OP_XOR: launch_pw<OP_XOR>(s, mode, grid, tasks, nt, A, B, oc, task_card); break;
-    default: launch_pw<OP_ANDNOT>(s, mode, grid, tasks, nt, A, B, oc, task_card); break;
-  }
+void launch_compact(hipStream_t s, const uint8_t* flag, const PTask* by_key, const uint32_t* wg_count, PTask* tasks,
+                    uint32_t* n_tasks) {
+  hipLaunchKernelGGL(k_compact<PTask>, dim3(256), dim3(256), 0, s, flag, by_key, wg_count, tasks, n_tasks);
 }
 
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info) {

@@ -39,14 +39,19 @@ struct WideArgs {
 // wave pays a launch per task (cached per kernel).
 int resident_grid(const void* kernel);
 
-void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const uint16_t* kb, int nb, Task* by_key,
-                          uint8_t* flag, uint32_t* wg_count);
 void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,
                       Task* by_key, uint8_t* flag, uint32_t* wg_count);
 void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
                     uint32_t* n_tasks);
-void launch_pairwise(hipStream_t s, int op, int mode, int grid, const Task* tasks, const uint32_t* nt, OperandView A,
-                     OperandView B, OutCtx oc, uint32_t* task_card);
+// pairwise.hip: plan (key alignment + descriptor resolution) and the wave-per-key compute
+// plan + compact: tasks[] in key order, *n_tasks
+void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const CDesc* da, const uint8_t* pa,
+                          const uint16_t* kb, int nb, const CDesc* db, const uint8_t* pb, PTask* by_key,
+                          uint8_t* flag, uint32_t* wg_count, PTask* tasks, uint32_t* n_tasks);
+void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
+                     const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card);
+void launch_compact(hipStream_t s, const uint8_t* flag, const PTask* by_key, const uint32_t* wg_count, PTask* tasks,
+                    uint32_t* n_tasks);
 void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
                  uint32_t* task_card);
 // result materialisation: k_place = compaction scan over the task records

@@ -1,0 +1,293 @@
+// Pairwise static ops (RB/RoaringBitmap.java and :377, or :860, xor :1071,
+// andNot :444, andCardinality :413) on the MI355X.  RB/ = reference
+// RoaringBitmap/src/main/java/org/roaringbitmap/.
+//
+//   k_plan_pairwise : one thread per key: key alignment of the two sorted key
+//                     arrays (the advanceUntil walks) and resolution of both
+//                     operands' descriptors into a 32 B task record
+//   k_compact       : dense task list (kernels.hip)
+//   k_pair_wave     : one wavefront per task over a resident grid; the next
+//                     task's record is fetched with scalar loads while the
+//                     current one runs, and both operand payloads are requested
+//                     before either is consumed
+#include <algorithm>
+
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace rbg {
+
+__device__ __forceinline__ void resolve(const uint16_t* keys, int n, const CDesc* desc, const uint8_t* payload,
+                                        uint32_t k, uint64_t& slot, uint32_t& card, uint8_t& kind,
+                                        uint16_t& nruns) {
+  const int p = lower_bound_u16(keys, n, k);
+  if (p < n && keys[p] == k) {
+    const CDesc d = desc[p];
+    slot = d.slot;
+    card = d.card;
+    kind = d.kind;
+    nruns = d.kind == DK_R ? *reinterpret_cast<const uint16_t*>(payload + d.slot + 2) : 0;
+  } else {
+    slot = 0;
+    card = 0;
+    kind = kAbsent;
+    nruns = 0;
+  }
+}
+
+// Task class: 1 = filter class (pass-through clones, AND with an array, ANDNOT
+// of an array: results are subsets of one array), 2 = bitmap class.
+__device__ __forceinline__ int pair_class(int op, int ka, int kb) {
+  if (ka == kAbsent || kb == kAbsent) return 1;
+  if (op == OP_AND && (ka == DK_A || kb == DK_A)) return 1;
+  if (op == OP_ANDNOT && ka == DK_A) return 1;
+  return 2;
+}
+
+// RB/RoaringBitmap.java:382-400 (and), :864-896 (or), :1076-1113 (xor), :449-471 (andNot)
+__global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint16_t* __restrict__ ka, int na,
+                                                       const CDesc* __restrict__ da, const uint8_t* __restrict__ pa,
+                                                       const uint16_t* __restrict__ kb, int nb,
+                                                       const CDesc* __restrict__ db, const uint8_t* __restrict__ pb,
+                                                       PTask* __restrict__ by_key, uint8_t* __restrict__ flag,
+                                                       uint32_t* __restrict__ wg_count) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  PTask t;
+  resolve(ka, na, da, pa, k, t.slot_a, t.card_a, t.kind_a, t.nruns_a);
+  resolve(kb, nb, db, pb, k, t.slot_b, t.card_b, t.kind_b, t.nruns_b);
+  t.key = (uint16_t)k;
+  const bool ia = t.kind_a != kAbsent, ib = t.kind_b != kAbsent;
+  int f;
+  switch (op) {
+    case OP_OR:
+    case OP_XOR: f = ia || ib; break;
+    case OP_ANDNOT: f = ia; break;
+    default: f = ia && ib; break;  // AND and andCardinality
+  }
+  flag[k] = (uint8_t)f;
+  by_key[k] = t;
+  plan_count(f, wg_count);
+}
+
+// Result container type of the static pairwise ops as a function of the operand
+// kinds and the result's cardinality c and run count r:
+//   AND   : R&R -> EFF(c,r) (RB/RunContainer.java:381-456); else BY_CARD(c)
+//   OR    : A|R, R|A, R|R -> EFF(c,r) (:1926-1986); A|A -> BY_CARD(c)
+//           (RB/ArrayContainer.java:949-963); B|x, x|B -> c==65536 ? R.full : B
+//           (RB/BitmapContainer.java:1064-1096, RB/RunContainer.java:1932-1949)
+//   XOR   : R^R -> EFF; R^A, A^R with |A| < 32 -> EFF (RB/RunContainer.java:2410-2424);
+//           else BY_CARD (RB/BitmapContainer.java:1372-1408)
+//   ANDNOT: R\R -> EFF (:637-692); R\A with |A| < 32 -> EFF (:574-591); else BY_CARD
+__device__ __forceinline__ bool pairwise_needs_runs(int op, int ka, int ca, int kb, int cb) {
+  switch (op) {
+    case OP_AND: return ka == DK_R && kb == DK_R;
+    case OP_OR: return (ka == DK_R && kb != DK_B) || (kb == DK_R && ka != DK_B);
+    case OP_XOR:
+      return (ka == DK_R && kb == DK_R) || (ka == DK_R && kb == DK_A && cb < 32) ||
+             (kb == DK_R && ka == DK_A && ca < 32);
+    default:  // ANDNOT
+      return ka == DK_R && (kb == DK_R || (kb == DK_A && cb < 32));
+  }
+}
+__device__ __forceinline__ int pairwise_kind(int op, int ka, int kb, int c) {
+  if (op == OP_OR && (ka == DK_B || kb == DK_B)) return c == 65536 ? DK_R : DK_B;
+  return by_card(c);
+}
+
+constexpr int kWaves = 4;  // waves per workgroup
+
+// Records one task's output.  Staged results (LDS) are copied to the task's
+// scratch slot (arena slot layout); results already in the slot or pass-through
+// containers are referenced in place.  k_place and the serializer follow.
+__device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
+                                        uint32_t len, uint32_t card, uint32_t key, int kind, const OutCtx& oc) {
+  const int l = lane_id();
+  uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
+  if (keep && staged) {
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+    copy_lds_to_global<64>(slot, lds, len, l);
+    srcaddr = reinterpret_cast<uint64_t>(slot);
+  }
+  if (l == 0) {
+    ORec r;
+    r.off = 0;
+    r.src = srcaddr;
+    r.idx = 0;
+    r.card = card;
+    r.ser_len = len;
+    r.key = (uint16_t)key;
+    r.kind = (uint8_t)kind;
+    r.keep = keep ? 1 : 0;
+    oc.recs[t] = r;
+  }
+}
+
+// Filter path: AND with an array operand and ANDNOT of an array c1 always give an
+// array that is a subset of that array (App. A.1 / A.3; RB/ArrayContainer.java:
+// 184-271, RB/BitmapContainer.java:162-171, RB/RunContainer.java:305-334).  The
+// other operand is made an LDS membership map, the array's values are probed
+// (kept = member, or non-member for ANDNOT) and the kept values -- still sorted
+// -- go straight to the task's scratch slot.
+template <int OP, int MODE>
+__device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard, const uint8_t* pslot, int mkind,
+                                            int mcard, const uint8_t* mslot, const OutCtx& oc, uint32_t* task_card,
+                                            uint32_t* lds) {
+  w_map_lds(mkind, mcard, mslot, lds);
+  const uint16_t* pv = reinterpret_cast<const uint16_t*>(pslot);
+  if (MODE == 1) {
+    const int c = w_probe_array<false, false>(lds, pv, pcard, nullptr);
+    if (lane_id() == 0) task_card[t] = (uint32_t)c;
+    return;
+  }
+  uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+  uint16_t* out = reinterpret_cast<uint16_t*>(slot);
+  const int c = OP == OP_ANDNOT ? w_probe_array<true, true>(lds, pv, pcard, out)
+                                : w_probe_array<false, true>(lds, pv, pcard, out);
+  // empty results are dropped (RB/RoaringBitmap.java:389,456)
+  w_place(t, c > 0, slot, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, oc);
+}
+
+// Filter-class task (pass-through clone, or a filter), one wave, wave-uniform branches.
+template <int OP, int MODE>
+__device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
+                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
+  const int ka = tk.kind_a, kb = tk.kind_b;
+  if (ka == kAbsent || kb == kAbsent) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
+    if (MODE == 0) {
+      const bool from_a = ka != kAbsent;
+      const int kind = from_a ? ka : kb;
+      const uint32_t card = from_a ? tk.card_a : tk.card_b;
+      const uint32_t nr = from_a ? tk.nruns_a : tk.nruns_b;
+      const uint8_t* src = (from_a ? pa + tk.slot_a : pb + tk.slot_b) + (kind == DK_R ? 2 : 0);
+      const uint32_t len = kind == DK_A ? 2 * card : kind == DK_B ? 8192u : 2 + 4 * nr;
+      w_place(t, true, src, false, lds, len, card, tk.key, kind, oc);
+    }
+    return;
+  }
+  const int ca = (int)tk.card_a, cb = (int)tk.card_b;
+  const uint8_t* sa = pa + tk.slot_a;
+  const uint8_t* sb = pb + tk.slot_b;
+  // filter the array (A & A: the smaller one; A \ x: c1) through a map of the other operand
+  if (ka == DK_A && (OP == OP_ANDNOT || kb != DK_A || ca <= cb))
+    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, oc, task_card, lds);
+  else
+    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, oc, task_card, lds);
+}
+
+// Bitmap-class task: both operands in registers (16 words per lane), combined,
+// counted, typed (App. A) and written out (B straight from registers, A and R
+// staged in LDS).  One wave, wave-uniform branches.
+template <int OP, int MODE>
+__device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
+                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
+  const int l = lane_id();
+  const int ka = tk.kind_a, kb = tk.kind_b;
+  const int ca = (int)tk.card_a, cb = (int)tk.card_b;
+  WCtr x;
+  w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, (uint8_t)ka, 0}, pa, lds, x);
+  w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
+  const int c = w_card(x);
+  if (MODE == 1) {
+    if (l == 0) task_card[t] = (uint32_t)c;
+    return;
+  }
+  if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389,456,1084)
+    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
+    return;
+  }
+  const bool use_eff = pairwise_needs_runs(OP, ka, ca, kb, cb);
+  const int kind = use_eff ? eff(c, w_runs(x)) : pairwise_kind(OP, ka, kb, c);
+  if (kind == DK_B) {
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+#if RBG_EXP_NOSTORE
+    if (x.w[0] == 0x123456789ULL) w_store_bitmap(slot, x);  // experiment: (almost) never store
+#else
+    w_store_bitmap(slot, x);
+#endif
+    w_place(t, true, slot, false, lds, 8192, (uint32_t)c, tk.key, DK_B, oc);
+    return;
+  }
+  uint32_t len;
+  if (kind == DK_A) len = w_stage(DK_A, x, c, lds);
+  else len = 2u + 4u * (uint32_t)w_stage_runs(x, lds);
+  w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, oc);
+}
+
+// 32 B task record through the scalar cache (wave-uniform address)
+__device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
+  typedef const __attribute__((address_space(4))) uint64_t* CU64;
+  const CU64 q = reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(tasks + t));
+  union {
+    uint64_t u[4];
+    PTask p;
+  } r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r.u[i] = q[i];
+  return r.p;
+}
+
+// One wave per task, static stride over a resident grid (a contended ticket
+// counter costs ~12 ns per task chip-wide, a workgroup per task pays a dispatch
+// each).  The next task's record is loaded while this one runs.  Filter-class
+// and bitmap-class tasks share the launch: separate kernels per class were
+// measured 15 % slower on the C2 mix (tail + an extra dependent index load).
+// MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
+template <int OP, int MODE>
+__device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
+                                         const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
+  if (pair_class(OP, tk.kind_a, tk.kind_b) == 1) filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds);
+  else bitmap_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds);
+}
+template <int OP, int MODE>
+__global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
+                                                      const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
+                                                      const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card) {
+  __shared__ __align__(16) uint32_t lds_all[kWaves][2048];
+  const int w = threadIdx.x >> 6;
+  uint32_t* lds = lds_all[w];
+  const uint32_t nt = uni(*n_tasks);
+  const uint32_t stride = gridDim.x * kWaves;
+  uint32_t t = uni(blockIdx.x * kWaves + w);
+  if (t >= nt) return;
+  PTask cur = load_task(tasks, t);
+  for (;;) {
+    const uint32_t tn = t + stride;
+    PTask nxt;
+    if (tn < nt) nxt = load_task(tasks, tn);  // in flight while this task runs
+    any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds);
+    if (tn >= nt) break;
+    t = tn;
+    cur = nxt;
+  }
+}
+
+template <int OP, int MODE>
+static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
+                      const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
+  const void* k = (const void*)&k_pair_wave<OP, MODE>;
+  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(std::max(1, std::min(grid, resident_grid(k)))), dim3(256), 0, s,
+                     tasks, nt, pa, pb, oc, task_card);
+}
+
+void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const CDesc* da, const uint8_t* pa,
+                          const uint16_t* kb, int nb, const CDesc* db, const uint8_t* pb, PTask* by_key,
+                          uint8_t* flag, uint32_t* wg_count, PTask* tasks, uint32_t* n_tasks) {
+  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, ka, na, da, pa, kb, nb, db, pb, by_key, flag,
+                     wg_count);
+  launch_compact(s, flag, by_key, wg_count, tasks, n_tasks);
+}
+
+void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
+#define RBG_LPW(O)                                                                    \
+  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card);   \
+  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card);
+  switch (op) {
+    case OP_AND: RBG_LPW(OP_AND) break;
+    case OP_OR: RBG_LPW(OP_OR) break;
+    case OP_XOR: RBG_LPW(OP_XOR) break;
+    default: RBG_LPW(OP_ANDNOT) break;
+  }
+#undef RBG_LPW
+}
+
+}  // namespace rbg

@@ -14,6 +14,12 @@ namespace rbg {
 constexpr int WL = 64;  // lanes per wave
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+// wave-uniform copy (value of the first active lane, in an SGPR)
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+         (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
 
 // Orders this wave's LDS accesses (LDS ops of one wave complete in issue order;
 // this keeps the compiler from reordering across the point).
@@ -23,21 +29,11 @@ __device__ __forceinline__ void wsync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-// exclusive prefix over lanes; returns the wave total in *tot
+__device__ __forceinline__ int wave_sum_i(int v) { return lane63(dpp_incl_scan(v)); }
+// exclusive prefix over lanes; returns the wave total in *tot (wave-uniform)
 __device__ __forceinline__ int wave_excl(int v, int* tot) {
-  const int l = lane_id();
-  int s = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int u = __shfl_up(s, o, 64);
-    if (l >= o) s += u;
-  }
-  *tot = __shfl(s, 63, 64);
+  const int s = dpp_incl_scan(v);
+  *tot = lane63(s);
   return s - v;
 }
 
@@ -94,6 +90,32 @@ __device__ __forceinline__ void w_clear_lds(uint32_t* lds) {
 // into one atomic.
 constexpr int kVecRound = 4;  // 16 B vectors per lane loaded per round
 
+// OR/XOR the 8 values of one 16 B vector (values base..base+7, those < card).
+template <int MODE>  // 0 or, 1 xor
+__device__ __forceinline__ void scatter_vec(uint32_t* lds, const uint4 v, int base, int card) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t cur = 0xFFFFFFFFu, mask = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if (base + i < card) {
+      const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
+      if ((x >> 5) != cur) {
+        if (mask) {
+          if (MODE == 0) atomicOr(&lds[cur], mask);
+          else atomicXor(&lds[cur], mask);
+        }
+        cur = x >> 5;
+        mask = 0;
+      }
+      mask |= 1u << (x & 31);
+    }
+  }
+  if (mask) {
+    if (MODE == 0) atomicOr(&lds[cur], mask);
+    else atomicXor(&lds[cur], mask);
+  }
+}
+
 template <int MODE>  // 0 or, 1 xor
 __device__ __forceinline__ void w_scatter_array(uint32_t* lds, const uint16_t* vals, int card) {
   const int nvec = (card + 7) >> 3;  // <= 512 = 8 per lane, in rounds of 4
@@ -108,31 +130,11 @@ __device__ __forceinline__ void w_scatter_array(uint32_t* lds, const uint16_t* v
       v[j] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-  for (int j = 0; j < kVecRound; j++) {
-    const int base = 8 * (64 * (j0 + j) + l);
-    if (base >= card) break;
-    const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-    uint32_t cur = 0xFFFFFFFFu, mask = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      if (base + i < card) {
-        const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
-        if ((x >> 5) != cur) {
-          if (mask) {
-            if (MODE == 0) atomicOr(&lds[cur], mask);
-            else atomicXor(&lds[cur], mask);
-          }
-          cur = x >> 5;
-          mask = 0;
-        }
-        mask |= 1u << (x & 31);
-      }
+    for (int j = 0; j < kVecRound; j++) {
+      const int base = 8 * (64 * (j0 + j) + l);
+      if (base >= card) break;
+      scatter_vec<MODE>(lds, v[j], base, card);
     }
-    if (mask) {
-      if (MODE == 0) atomicOr(&lds[cur], mask);
-      else atomicXor(&lds[cur], mask);
-    }
-  }
   }
 }
 
@@ -141,15 +143,29 @@ __device__ __forceinline__ void w_scatter_array(uint32_t* lds, const uint16_t* v
 // atomics per run, no divergence on run length), and an inclusive prefix-XOR
 // over the 65536 bits then turns the toggles into the filled runs.  Valid run
 // containers have disjoint runs, so toggles of adjacent runs cancel correctly.
-__device__ __forceinline__ void w_toggle_runs(uint32_t* lds, const uint8_t* slot, int nruns) {
-  // slot = [u16 pad][u16 nruns][u32 (start, len-1) pairs]: u32 k of the slot is
-  // run k-1, so the slot streams as aligned 16 B vectors (input run containers
-  // may hold up to 32768 runs; results hold at most 2047)
+// Toggles of the runs held in one 16 B vector of a run slot (runs r0..r0+3).
+__device__ __forceinline__ void toggle_vec(uint32_t* lds, const uint4 v, int r0, int nruns) {
+  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int r = r0 + c;
+    if (r >= 0 && r < nruns) {
+      const uint32_t s = u[c] & 0xFFFF, e1 = s + (u[c] >> 16) + 1;
+      atomicXor(&lds[s >> 5], 1u << (s & 31));
+      if (e1 < 65536) atomicXor(&lds[e1 >> 5], 1u << (e1 & 31));
+    }
+  }
+}
+
+// slot = [u16 pad][u16 nruns][u32 (start, len-1) pairs]: u32 k of the slot is
+// run k-1, so the slot streams as aligned 16 B vectors (input run containers
+// may hold up to 32768 runs; results hold at most 2047).  Vectors from j0 on.
+__device__ __forceinline__ void w_toggle_runs(uint32_t* lds, const uint8_t* slot, int nruns, int j_first = 0) {
   const int nvec = (nruns + 4) >> 2;
   const uint4* v4 = reinterpret_cast<const uint4*>(slot);
   const int l = lane_id();
 #pragma unroll 1
-  for (int j0 = 0; 64 * j0 < nvec; j0 += kVecRound) {
+  for (int j0 = j_first; 64 * j0 < nvec; j0 += kVecRound) {
     uint4 v[kVecRound];
 #pragma unroll
     for (int j = 0; j < kVecRound; j++) {
@@ -157,20 +173,11 @@ __device__ __forceinline__ void w_toggle_runs(uint32_t* lds, const uint8_t* slot
       v[j] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-  for (int j = 0; j < kVecRound; j++) {
-    const int r0 = 4 * (64 * (j0 + j) + l) - 1;
-    if (r0 >= nruns) break;
-    const uint32_t u[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int r = r0 + c;
-      if (r >= 0 && r < nruns) {
-        const uint32_t s = u[c] & 0xFFFF, e1 = s + (u[c] >> 16) + 1;
-        atomicXor(&lds[s >> 5], 1u << (s & 31));
-        if (e1 < 65536) atomicXor(&lds[e1 >> 5], 1u << (e1 & 31));
-      }
+    for (int j = 0; j < kVecRound; j++) {
+      const int r0 = 4 * (64 * (j0 + j) + l) - 1;
+      if (r0 >= nruns) break;
+      toggle_vec(lds, v[j], r0, nruns);
     }
-  }
   }
 }
 
@@ -286,13 +293,12 @@ __device__ __forceinline__ int w_card(const WCtr& x) {
 template <int I>
 __device__ __forceinline__ void w_chunk_edges(const WCtr& x, uint64_t& s0, uint64_t& s1, uint64_t& e0, uint64_t& e1) {
   const int l = lane_id();
-  const int up = (l + 63) & 63, dn = (l + 1) & 63;
   const uint64_t w0 = x.w[2 * I], w1 = x.w[2 * I + 1];
-  const uint64_t top1 = __shfl(w1 >> 63, up, 64);  // lane l-1's word 1 top bit
-  const uint64_t pchunk = I > 0 ? __shfl(x.w[2 * (I > 0 ? I - 1 : 0) + 1] >> 63, 63, 64) : 0;
+  const uint32_t top1 = from_prev_lane((uint32_t)(w1 >> 63));  // lane l-1's word 1 top bit
+  const uint32_t pchunk = I > 0 ? lane63u((uint32_t)(x.w[2 * (I > 0 ? I - 1 : 0) + 1] >> 63)) : 0u;
   const uint64_t prev0 = (l == 0) ? pchunk : top1;
-  const uint64_t bot0 = __shfl(w0 & 1, dn, 64);  // lane l+1's word 0 bit 0
-  const uint64_t nchunk = I < 7 ? __shfl(x.w[2 * (I < 7 ? I + 1 : 7)] & 1, 0, 64) : 0;
+  const uint32_t bot0 = from_next_lane((uint32_t)(w0 & 1));  // lane l+1's word 0 bit 0
+  const uint32_t nchunk = I < 7 ? lane0u((uint32_t)(x.w[2 * (I < 7 ? I + 1 : 7)] & 1)) : 0u;
   const uint64_t next1 = (l == 63) ? nchunk : bot0;
   s0 = w0 & ~((w0 << 1) | prev0);
   s1 = w1 & ~((w1 << 1) | (w0 >> 63));
@@ -312,52 +318,7 @@ __device__ __forceinline__ int w_runs(const WCtr& x) {
   return (int)__builtin_amdgcn_readfirstlane((uint32_t)wave_sum_i(c));
 }
 
-template <int I>
-__device__ __forceinline__ int w_stage_starts(const WCtr& x, uint16_t* st, int base) {
-  const int l = lane_id();
-  uint64_t s0, s1, e0, e1;
-  w_chunk_edges<I>(x, s0, s1, e0, e1);
-  int tot;
-  int p = base + wave_excl(__popcll(s0) + __popcll(s1), &tot);
-  const int wb = (128 * I + 2 * l) * 64;
-  uint64_t v = s0;
-  while (v) {
-    if (p < 2047) st[1 + 2 * p] = (uint16_t)(wb + __builtin_ctzll(v));
-    p++;
-    v &= v - 1;
-  }
-  v = s1;
-  while (v) {
-    if (p < 2047) st[1 + 2 * p] = (uint16_t)(wb + 64 + __builtin_ctzll(v));
-    p++;
-    v &= v - 1;
-  }
-  if (I < 7) return w_stage_starts<(I < 7 ? I + 1 : 7)>(x, st, base + tot);
-  return base + tot;
-}
-
-template <int I>
-__device__ __forceinline__ void w_stage_ends(const WCtr& x, uint16_t* st, int base) {
-  const int l = lane_id();
-  uint64_t s0, s1, e0, e1;
-  w_chunk_edges<I>(x, s0, s1, e0, e1);
-  int tot;
-  int p = base + wave_excl(__popcll(e0) + __popcll(e1), &tot);
-  const int wb = (128 * I + 2 * l) * 64;
-  uint64_t v = e0;
-  while (v) {
-    if (p < 2047) st[2 + 2 * p] = (uint16_t)(wb + __builtin_ctzll(v) - st[1 + 2 * p]);
-    p++;
-    v &= v - 1;
-  }
-  v = e1;
-  while (v) {
-    if (p < 2047) st[2 + 2 * p] = (uint16_t)(wb + 64 + __builtin_ctzll(v) - st[1 + 2 * p]);
-    p++;
-    v &= v - 1;
-  }
-  if (I < 7) w_stage_ends<(I < 7 ? I + 1 : 7)>(x, st, base + tot);
-}
+__device__ __forceinline__ int w_stage_runs(const WCtr& x, uint32_t* lds);
 
 // Serialized payload of the owned container, staged in the wave's LDS
 // (A: u16 values; B: 1024 u64 words; R: u16 nruns + (start, len-1) pairs).
@@ -376,34 +337,391 @@ __device__ __forceinline__ uint32_t w_stage(int kind, const WCtr& x, int card, u
     int base = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      const int c0 = __popcll(x.w[2 * i]);
-      const int c = c0 + __popcll(x.w[2 * i + 1]);
+      uint64_t v0 = x.w[2 * i], v1 = x.w[2 * i + 1];
+      const int c0 = __popcll(v0);
       int tot;
-      int p = base + wave_excl(c, &tot);
+      int p0 = base + wave_excl(c0 + __popcll(v1), &tot);
+      int p1 = p0 + c0;
       const int wb = (128 * i + 2 * l) * 64;
-      uint64_t v = x.w[2 * i];
-      while (v) {
-        st[p++] = (uint16_t)(wb + __builtin_ctzll(v));
-        v &= v - 1;
-      }
-      v = x.w[2 * i + 1];
-      while (v) {
-        st[p++] = (uint16_t)(wb + 64 + __builtin_ctzll(v));
-        v &= v - 1;
+      // both words drained together: iterations = max(popc) instead of the sum
+      while (v0 | v1) {
+        if (v0) {
+          st[p0++] = (uint16_t)(wb + __builtin_ctzll(v0));
+          v0 &= v0 - 1;
+        }
+        if (v1) {
+          st[p1++] = (uint16_t)(wb + 64 + __builtin_ctzll(v1));
+          v1 &= v1 - 1;
+        }
       }
       base += tot;
     }
     wsync();
     return 2u * (uint32_t)card;
   }
-  // run container: starts first (writes st[1 + 2k]), then ends (st[2 + 2k] = end - start)
+  return 2u + 4u * (uint32_t)w_stage_runs(x, lds);
+}
+
+// ---------------------------------------------------------------------------
+// key planning helpers (one thread per key)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int lower_bound_u16(const uint16_t* keys, int n, uint32_t k) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (keys[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void plan_count(int f, uint32_t* wg_count) {
+  __shared__ int wc[4];
+  const uint64_t m = __ballot(f);
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
+  __syncthreads();
+  if (threadIdx.x == 0) wg_count[blockIdx.x] = (uint32_t)(wc[0] + wc[1] + wc[2] + wc[3]);
+}
+
+// Bitmap from registers straight to a 16 B-aligned global slot (8 coalesced
+// 16 B stores per lane; no LDS round trip).
+__device__ __forceinline__ void w_store_bitmap(uint8_t* p, const WCtr& x) {
+  uint4* q = reinterpret_cast<uint4*>(p) + lane_id();
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint4 v = make_uint4((uint32_t)x.w[2 * i], (uint32_t)(x.w[2 * i] >> 32), (uint32_t)x.w[2 * i + 1],
+                               (uint32_t)(x.w[2 * i + 1] >> 32));
+#if RBG_NO_NT
+    q[64 * i] = v;
+#else
+    // streaming (nontemporal) stores: results are read back only by later kernels
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 nv = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(nv, reinterpret_cast<u32x4*>(q + 64 * i));
+#endif
+  }
+}
+
+// ---------------------------------------------------------------------------
+// prefetched operands: both operands' payloads are requested up front (one
+// memory latency per task instead of one per operand), then consumed from
+// registers.  Lane l holds vectors 64*j + l (j < kPre) of the slot: all of an
+// A or B payload, and R payloads of up to 2043 runs (longer inputs stream the
+// rest from memory).
+// ---------------------------------------------------------------------------
+constexpr int kPre = 8;
+struct WPre {
+  uint4 v[kPre];
+};
+
+// 16 B vectors of a slot that hold payload (A: 2c bytes; B: 8192; R: 4 + 4 nruns)
+__device__ __forceinline__ int slot_nvec(int kind, int card, int nruns) {
+  return kind == DK_A ? (2 * card + 15) >> 4 : kind == DK_B ? 512 : (nruns + 4) >> 2;
+}
+
+__device__ __forceinline__ void w_prefetch(const uint8_t* slot, int nvec, WPre& p) {
+  const uint4* q = reinterpret_cast<const uint4*>(slot) + lane_id();
+  const int l = lane_id();
+#pragma unroll
+  for (int j = 0; j < kPre; j++) p.v[j] = (64 * j + l < nvec) ? q[64 * j] : make_uint4(0, 0, 0, 0);
+}
+
+template <int MODE>
+__device__ __forceinline__ void w_scatter_pre(uint32_t* lds, const WPre& p, int card) {
+  const int l = lane_id();
+#pragma unroll
+  for (int j = 0; j < kPre; j++) {
+    if (512 * j >= card) break;  // wave-uniform
+    scatter_vec<MODE>(lds, p.v[j], 8 * (64 * j + l), card);
+    __builtin_amdgcn_sched_barrier(0);  // one vector at a time: keeps register pressure flat
+  }
+}
+
+__device__ __forceinline__ void w_toggle_pre(uint32_t* lds, const WPre& p, const uint8_t* slot, int nruns) {
+  const int l = lane_id();
+  const int nvec = (nruns + 4) >> 2;
+#pragma unroll
+  for (int j = 0; j < kPre; j++) {
+    if (64 * j >= nvec) break;  // wave-uniform
+    toggle_vec(lds, p.v[j], 4 * (64 * j + l) - 1, nruns);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  if (nvec > 64 * kPre) w_toggle_runs(lds, slot, nruns, kPre);
+}
+
+__device__ __forceinline__ void pre_to_words(const WPre& p, WCtr& x) {
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    x.w[2 * i] = (uint64_t)p.v[i].x | ((uint64_t)p.v[i].y << 32);
+    x.w[2 * i + 1] = (uint64_t)p.v[i].z | ((uint64_t)p.v[i].w << 32);
+  }
+}
+
+// operand (kind, card, nruns) of a prefetched slot -> owned registers
+__device__ __forceinline__ void w_materialize_pre(int kind, int card, int nruns, const WPre& p, const uint8_t* slot,
+                                                  uint32_t* lds, WCtr& x) {
+  if (kind == DK_B) {
+    pre_to_words(p, x);
+    return;
+  }
   wsync();
-  int sb = w_stage_starts<0>(x, st, 0);
+  w_clear_lds(lds);
   wsync();
-  w_stage_ends<0>(x, st, 0);
-  if (l == 0) st[0] = (uint16_t)sb;
+  if (kind == DK_A) {
+    w_scatter_pre<0>(lds, p, card);
+    wsync();
+    w_read_lds(lds, x);
+    return;
+  }
+  w_toggle_pre(lds, p, slot, nruns);
   wsync();
-  return 2u + 4u * (uint32_t)sb;
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) w_run_chunk(lds, i, carry, x.w[2 * i], x.w[2 * i + 1]);
+}
+
+template <int OP>  // 0 and, 1 or, 2 xor, 3 andnot
+__device__ __forceinline__ void w_combine_pre(int kind, int card, int nruns, const WPre& p, const uint8_t* slot,
+                                              uint32_t* lds, WCtr& x) {
+  if (kind == DK_B) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      x.w[2 * i] = w_op<OP>(x.w[2 * i], (uint64_t)p.v[i].x | ((uint64_t)p.v[i].y << 32));
+      x.w[2 * i + 1] = w_op<OP>(x.w[2 * i + 1], (uint64_t)p.v[i].z | ((uint64_t)p.v[i].w << 32));
+    }
+    return;
+  }
+  wsync();
+  w_clear_lds(lds);
+  wsync();
+  if (kind == DK_A) {
+    w_scatter_pre<0>(lds, p, card);
+    wsync();
+    const uint4* q = reinterpret_cast<const uint4*>(lds) + lane_id();
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint4 v = q[64 * i];
+      x.w[2 * i] = w_op<OP>(x.w[2 * i], (uint64_t)v.x | ((uint64_t)v.y << 32));
+      x.w[2 * i + 1] = w_op<OP>(x.w[2 * i + 1], (uint64_t)v.z | ((uint64_t)v.w << 32));
+    }
+    return;
+  }
+  w_toggle_pre(lds, p, slot, nruns);
+  wsync();
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t a, b;
+    w_run_chunk(lds, i, carry, a, b);
+    x.w[2 * i] = w_op<OP>(x.w[2 * i], a);
+    x.w[2 * i + 1] = w_op<OP>(x.w[2 * i + 1], b);
+  }
+}
+
+// Any container as a 65536-bit membership map in the wave's LDS (u32[2048]),
+// for probing: B is written from registers, A scattered, R toggled and
+// prefix-XOR filled in place.
+__device__ __forceinline__ void w_map_pre(int kind, int card, int nruns, const WPre& p, const uint8_t* slot,
+                                          uint32_t* lds) {
+  const int l = lane_id();
+  uint4* q = reinterpret_cast<uint4*>(lds) + l;
+  wsync();
+  if (kind == DK_B) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) q[64 * i] = p.v[i];
+    wsync();
+    return;
+  }
+  w_clear_lds(lds);
+  wsync();
+  if (kind == DK_A) {
+    w_scatter_pre<0>(lds, p, card);
+    wsync();
+    return;
+  }
+  w_toggle_pre(lds, p, slot, nruns);
+  wsync();
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t a, b;
+    w_run_chunk(lds, i, carry, a, b);  // reads this lane's vector of chunk i, then overwrites it
+    q[64 * i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+  }
+  wsync();
+}
+
+// The same map built from a container streamed from memory.
+__device__ __forceinline__ void w_map_lds(int kind, int card, const uint8_t* slot, uint32_t* lds) {
+  const int l = lane_id();
+  uint4* q = reinterpret_cast<uint4*>(lds) + l;
+  wsync();
+  if (kind == DK_B) {
+    const uint4* g = reinterpret_cast<const uint4*>(slot) + l;
+#pragma unroll
+    for (int h = 0; h < 8; h += 4) {
+      uint4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) v[i] = g[64 * (h + i)];
+#pragma unroll
+      for (int i = 0; i < 4; i++) q[64 * (h + i)] = v[i];
+    }
+    wsync();
+    return;
+  }
+  w_clear_lds(lds);
+  wsync();
+  if (kind == DK_A) {
+    w_scatter_array<0>(lds, reinterpret_cast<const uint16_t*>(slot), card);
+    wsync();
+    return;
+  }
+  w_toggle_runs(lds, slot, *reinterpret_cast<const uint16_t*>(slot + 2));
+  wsync();
+  uint32_t carry = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    uint64_t a, b;
+    w_run_chunk(lds, i, carry, a, b);  // reads this lane's vector of chunk i, then overwrites it
+    q[64 * i] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+  }
+  wsync();
+}
+
+// Filter the sorted values of an array container (streamed from memory) by
+// membership in the wave's LDS map; see w_probe_pre.
+constexpr int kProbeRound = 2;  // 16 B vectors per lane per probe round
+template <bool INV, bool WRITE>
+__device__ __forceinline__ int w_probe_array(const uint32_t* lds, const uint16_t* vals, int n, uint16_t* out) {
+  const int l = lane_id();
+  const uint4* v4 = reinterpret_cast<const uint4*>(vals);
+  const int nvec = (n + 7) >> 3;  // <= 512 = 8 per lane
+  int base = 0;
+#pragma unroll 1
+  for (int j0 = 0; 64 * j0 < nvec; j0 += kProbeRound) {
+    uint4 v[kProbeRound];
+#pragma unroll
+    for (int j = 0; j < kProbeRound; j++) {
+      const int k = 64 * (j0 + j) + l;
+      v[j] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kProbeRound; j++) {
+      if (64 * (j0 + j) >= nvec) break;  // wave-uniform
+      const int first = 8 * (64 * (j0 + j) + l);
+      const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+      uint32_t hit = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
+        const uint32_t m = (lds[x >> 5] >> (x & 31)) & 1u;
+        hit |= ((INV ? (m ^ 1u) : m) & (first + i < n ? 1u : 0u)) << i;
+      }
+      int tot;
+      int q = base + wave_excl(__popc(hit), &tot);
+      if (WRITE) {
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if ((hit >> i) & 1u) out[q++] = (uint16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF);
+      }
+      base += tot;
+    }
+  }
+  return (int)uni((uint32_t)base);
+}
+
+// Filter the sorted values of a prefetched array container by membership in
+// the wave's LDS map: keep members (INV = false, A AND x) or non-members
+// (INV = true, A ANDNOT x).  The kept values stay sorted; with WRITE they are
+// stored to `out` (u16, in order).  Returns the kept count (wave-uniform).
+// This is the result of RB/ArrayContainer.java:184-271 (and / andNot with any
+// container), RB/BitmapContainer.java:162-171 and RB/RunContainer.java:305-334
+// without materialising a result bitmap.
+template <bool INV, bool WRITE>
+__device__ __forceinline__ int w_probe_pre(const uint32_t* lds, const WPre& p, int n, uint16_t* out) {
+  const int l = lane_id();
+  int base = 0;
+#pragma unroll
+  for (int j = 0; j < kPre; j++) {
+    if (512 * j >= n) break;  // wave-uniform
+    const int first = 8 * (64 * j + l);
+    const uint32_t w[4] = {p.v[j].x, p.v[j].y, p.v[j].z, p.v[j].w};
+    uint32_t hit = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
+      const uint32_t m = (lds[x >> 5] >> (x & 31)) & 1u;
+      hit |= ((INV ? (m ^ 1u) : m) & (first + i < n ? 1u : 0u)) << i;
+    }
+    int tot;
+    int q = base + wave_excl(__popc(hit), &tot);
+    if (WRITE) {
+#pragma unroll
+      for (int i = 0; i < 8; i++)
+        if ((hit >> i) & 1u) out[q++] = (uint16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF);
+    }
+    base += tot;
+  }
+  return (int)uni((uint32_t)base);
+}
+
+// Runs of the owned container staged in one pass: per chunk the start and end
+// masks are computed once, one packed (starts | ends << 16) scan places both,
+// and the four bit streams (starts / ends of the lane's two words) are drained
+// together.  Ends are written as absolute positions; a final pass turns them
+// into lengths.  The k-th end closes the k-th run.  Stages (u16 nruns,
+// (start, len-1) pairs) in LDS when the result has <= 2047 runs (the most a run
+// result can have: EFF keeps R only if 2 + 4 * nruns <= 8192).  Returns the
+// run count.
+template <int I>
+__device__ __forceinline__ int w_stage_runs_chunk(const WCtr& x, uint16_t* st, int base, int base_e) {
+  const int l = lane_id();
+  uint64_t s0, s1, e0, e1;
+  w_chunk_edges<I>(x, s0, s1, e0, e1);
+  const int cs0 = __popcll(s0), ce0 = __popcll(e0);
+  const int cs = cs0 + __popcll(s1), ce = ce0 + __popcll(e1);
+  int tot;
+  const int packed = wave_excl(cs | (ce << 16), &tot);
+  const int wb = (128 * I + 2 * l) * 64;
+  int ps0 = base + (packed & 0xFFFF), ps1 = ps0 + cs0;
+  int pe0 = base_e + (packed >> 16), pe1 = pe0 + ce0;
+  while (s0 | s1 | e0 | e1) {
+    if (s0) {
+      if (ps0 < 2047) st[1 + 2 * ps0] = (uint16_t)(wb + __builtin_ctzll(s0));
+      ps0++;
+      s0 &= s0 - 1;
+    }
+    if (s1) {
+      if (ps1 < 2047) st[1 + 2 * ps1] = (uint16_t)(wb + 64 + __builtin_ctzll(s1));
+      ps1++;
+      s1 &= s1 - 1;
+    }
+    if (e0) {
+      if (pe0 < 2047) st[2 + 2 * pe0] = (uint16_t)(wb + __builtin_ctzll(e0));
+      pe0++;
+      e0 &= e0 - 1;
+    }
+    if (e1) {
+      if (pe1 < 2047) st[2 + 2 * pe1] = (uint16_t)(wb + 64 + __builtin_ctzll(e1));
+      pe1++;
+      e1 &= e1 - 1;
+    }
+  }
+  const int nb = base + (tot & 0xFFFF), nbe = base_e + (tot >> 16);
+  if (I < 7) return w_stage_runs_chunk<(I < 7 ? I + 1 : 7)>(x, st, nb, nbe);
+  return nb;
+}
+
+__device__ __forceinline__ int w_stage_runs(const WCtr& x, uint32_t* lds) {
+  uint16_t* st = reinterpret_cast<uint16_t*>(lds);
+  wsync();
+  const int nr = (int)uni((uint32_t)w_stage_runs_chunk<0>(x, st, 0, 0));
+  const int ns = nr < 2047 ? nr : 2047;
+  wsync();
+  for (int k = lane_id(); k < ns; k += 64) st[2 + 2 * k] = (uint16_t)(st[2 + 2 * k] - st[1 + 2 * k]);
+  if (lane_id() == 0) st[0] = (uint16_t)ns;
+  wsync();
+  return nr;
 }
 
 // Copy n bytes (n even) from 16 B-aligned LDS to an even global address.
@@ -447,11 +765,6 @@ __device__ __forceinline__ uint64_t lb_pack(uint64_t st, uint64_t run, uint64_t 
   return (st << 62) | (run << 61) | (cnt << 44) | bytes;
 }
 
-__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ uint64_t uni64(uint64_t x) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
-         (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
-}
 
 // Called by ALL lanes of ONE wave with identical (wave-uniform) arguments; the
 // spin loop is wave-uniform and single-exit.  Publishes this task's aggregate,

@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_kinds
 mkdir -p $OUT
-for case in "A A and" "A A card" "R R and" "B B and" "M M and"; do
+for case in "A B and" "A B card" "R R and" "R R card" "B B and" "B B card" "M M and"; do
   set -- $case
   tag=$1$2_$3
   timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS --kernel-include-regex "k_pair" --output-format csv -d $OUT/$tag -o run -- python3 scripts/kind_one.py $1 $2 $3 3 > /dev/null 2> $OUT/$tag.err || { echo "$tag failed"; tail -5 $OUT/$tag.err; exit 1; }
