@@ -165,6 +165,17 @@ int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b,
  * rbg_wide (may be NULL). */
 int rbg_ctx_wide(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, const int32_t* ids);
 int rbg_ctx_wide_card(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi);
+/* rbg_ctx_wide with the naive_and start input given by the caller (start_bm >= 0).
+ * A key-range shard passes the input with the fewest containers over the whole
+ * universe (RB/FastAggregation.java:333-339), which its key slice cannot see. */
+int rbg_ctx_wide_start(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, const int32_t* ids,
+                       int32_t start_bm);
+/* Containers per input bitmap of a batch (out has n == bitmaps entries). */
+int rbg_ctx_batch_counts(rbg_ctx* ctx, int32_t batch, uint32_t* out, size_t n);
+/* Algorithmic input bytes per key (payload + 4 B descriptor per container) of the
+ * synthetic C3 workloads (kind 1 uniform, 2 clustered), for key-range partitioning
+ * by equal bytes; out has 65536 entries.  Host only. */
+int rbg_synth_key_bytes(int kind, uint64_t seed, size_t n, uint64_t* out);
 /* Enqueue batched andCardinality over pairs (2i, 2i+1) of a batch; results stay on device. */
 int rbg_ctx_batch_and_card(rbg_ctx* ctx, int32_t batch);
 

@@ -34,7 +34,8 @@ EXPORTED = [
     "rbg_ctx_load", "rbg_ctx_synth", "rbg_ctx_release", "rbg_ctx_batch_stats", "rbg_ctx_batch_fetch",
     "rbg_ctx_pairwise", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
     "rbg_ctx_batch_and_card", "rbg_ctx_card", "rbg_ctx_cards", "rbg_ctx_result_stats", "rbg_ctx_fetch",
-    "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read", "rbg_ctx_serialize",
+    "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read", "rbg_ctx_serialize", "rbg_ctx_wide_start",
+    "rbg_ctx_batch_counts", "rbg_synth_key_bytes",
 ]
 
 _lib = None
@@ -75,6 +76,9 @@ def _declare(L):
     L.rbg_ctx_pairwise_card.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz]
     L.rbg_ctx_wide.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int, P(i32)]
     L.rbg_ctx_wide_card.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int]
+    L.rbg_ctx_wide_start.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int, P(i32), i32]
+    L.rbg_ctx_batch_counts.argtypes = [vp, i32, P(ctypes.c_uint32), sz]
+    L.rbg_synth_key_bytes.argtypes = [ctypes.c_int, ctypes.c_uint64, sz, P(ctypes.c_uint64)]
     L.rbg_ctx_batch_and_card.argtypes = [vp, i32]
     L.rbg_ctx_serialize.argtypes = [vp]
     L.rbg_ctx_card.argtypes = [vp, P(i32)]

@@ -106,6 +106,27 @@ struct OperandView {
 
 __device__ __forceinline__ int popc64(uint64_t x) { return __popcll(x); }
 
+// splitmix64 finaliser (host and device: the synthetic generators share it)
+__host__ __device__ inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ULL;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
+  return x ^ (x >> 31);
+}
+
+// Synthetic C3 workloads, shared by the device generators and
+// the host-side CSR construction:
+//   uniform  : bitmap i holds every key; card(i, k) in [1, 29] (mean 15, ~1M
+//              values per bitmap), values stratified over the 65536 range
+//   clustered: bitmap i holds keys base(i) .. base(i)+15 as dense bitmap
+//              containers (each bit set with p = 0.95)
+__host__ __device__ inline uint32_t c3u_card(uint64_t seed, uint32_t i, uint32_t k) {
+  return 1 + (uint32_t)(splitmix64(seed ^ ((uint64_t)i << 17) ^ (uint64_t)k) % 29);
+}
+__host__ __device__ inline uint32_t c3c_base(uint64_t seed, uint32_t i) {
+  return (uint32_t)(splitmix64(seed ^ 0xC3100000ULL ^ (uint64_t)i) % (4096 - 16));
+}
+
 __device__ __forceinline__ int by_card(int c) { return c <= 4096 ? DK_A : DK_B; }
 // RunContainer.toEfficientContainer (RB/RunContainer.java:2326-2335)
 __device__ __forceinline__ int eff(int c, int r) {

@@ -96,6 +96,7 @@ struct Batch {
   int64_t n_kind[3] = {0, 0, 0};
   int64_t ser_bytes = 0;
   int64_t long_card = 0;
+  size_t max_ser = 0;  // Σ serialized payload of containers larger than 8194 B (long run inputs)
 };
 
 struct Ctx {
@@ -272,6 +273,7 @@ static int ctx_load(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size
       h_desc[p] = d;
       items[p] = IngestItem{raw_base[i] + hc.ser_off, slot_off[p], hc.ser_len, hc.kind};
       b.n_kind[hc.kind]++;
+      if (hc.ser_len > 8194) b.max_ser += hc.ser_len;
     }
   }
   b.payload_bytes = slot_off[C];
@@ -437,8 +439,10 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
 }
 
 // FastAggregation dispatch (RB/FastAggregation.java:26-101,653-666,823-836)
+// start_override >= 0: naive_and starts from that input (key-range shards pass the
+// input with the fewest containers over the WHOLE universe, RB/FastAggregation.java:333-339)
 static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const int32_t* ids, bool card_only,
-                    int* host_card_out, bool* host_card_valid) {
+                    int* host_card_out, bool* host_card_valid, int32_t start_override = -1) {
   Batch* B;
   CHK(get_batch(c, id, &B));
   if (!B->key_major) {
@@ -491,8 +495,12 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
           skip.assign(std::max<size_t>(N, 1), 0);
           if (op != RBG_WIDE_AND_ITER) {
             // the input with the fewest containers, first on ties (:333-339)
-            for (size_t i = 1; i < N; i++)
-              if (B->h_bm_nctr[i] < B->h_bm_nctr[start_bm]) start_bm = (uint32_t)i;
+            if (start_override >= 0 && (size_t)start_override < N) {
+              start_bm = (uint32_t)start_override;
+            } else {
+              for (size_t i = 1; i < N; i++)
+                if (B->h_bm_nctr[i] < B->h_bm_nctr[start_bm]) start_bm = (uint32_t)i;
+            }
             for (size_t i = 0; i < N; i++)
               skip[i] = (i == start_bm) || (ids && ids[i] == ids[start_bm]);  // :341 identity skip
           } else {
@@ -511,7 +519,8 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
   {
     const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
     OutCtx oc;
-    CHK(prepare_output(c, ub, (size_t)8194 * ub + B->payload_bytes, &oc, card_only));
+    // each result container is staged (<= 8194 B) or a clone of one input container
+    CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, card_only));
     if (!skip.empty()) {
       CHK(c->skip.ensure(skip.size()));
       HIPCHK(hipMemcpyAsync(c->skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
@@ -1073,6 +1082,33 @@ int rbg_ctx_wide(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, co
   bool hv;
   return ctx_wide(&ctx->c, op, batch, key_lo, key_hi, ids, false, &hc, &hv);
 }
+int rbg_ctx_wide_start(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, const int32_t* ids,
+                       int32_t start_bm) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  int hc;
+  bool hv;
+  return ctx_wide(&ctx->c, op, batch, key_lo, key_hi, ids, false, &hc, &hv, start_bm);
+}
+int rbg_ctx_batch_counts(rbg_ctx* ctx, int32_t batch, uint32_t* out, size_t n) {
+  Batch* b;
+  CHK(get_batch(&ctx->c, batch, &b));
+  if (!out || n != b->n_bm) return RBG_ERR_ILLEGAL_ARGUMENT;
+  for (size_t i = 0; i < n; i++) out[i] = b->h_bm_nctr[i];
+  return RBG_OK;
+}
+int rbg_synth_key_bytes(int kind, uint64_t seed, size_t n, uint64_t* out) {
+  if (!out || (kind != 1 && kind != 2)) return RBG_ERR_ILLEGAL_ARGUMENT;
+  for (int k = 0; k < kMaxKeys; k++) out[k] = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (kind == 1) {
+      for (int k = 0; k < kMaxKeys; k++) out[k] += 4 + 2 * (uint64_t)c3u_card(seed, (uint32_t)i, (uint32_t)k);
+    } else {
+      const uint32_t b0 = c3c_base(seed, (uint32_t)i);
+      for (uint32_t k = b0; k < b0 + 16; k++) out[k] += 4 + 8192;
+    }
+  }
+  return RBG_OK;
+}
 int rbg_ctx_wide_card(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi) {
   HIPCHK(hipSetDevice(ctx->c.device));
   int hc;
@@ -1164,12 +1200,107 @@ int rbg_ctx_fetch_shard(rbg_ctx* ctx, int64_t total_containers, int has_run, int
   return emit_host(payload, out_payload);
 }
 
+// C3 synthetic key slice [key_lo, key_hi) of n bitmaps (kind 1 uniform, 2 clustered)
+static int synth_c3(Ctx* c, int kind, uint64_t seed, size_t n, int key_lo, int key_hi, int32_t* out_id) {
+  key_lo = std::max(0, key_lo);
+  key_hi = std::min(kMaxKeys, key_hi);
+  if (n == 0 || n > 0x7FFFFFFF || key_hi < key_lo) {
+    set_err("synthetic C3 needs 0 < n and key_lo <= key_hi");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  const int nkeys = key_hi - key_lo;
+  hipStream_t s = c->stream;
+  std::vector<uint32_t> key_off(kMaxKeys + 1, 0);
+  std::vector<uint16_t> h_keys;
+  std::vector<uint32_t> h_bm, nctr(n, 0);
+  if (kind == 1) {
+    for (int k = 0; k < kMaxKeys; k++) {
+      const bool in = k >= key_lo && k < key_hi;
+      key_off[k + 1] = key_off[k] + (in ? (uint32_t)n : 0u);
+    }
+    for (size_t i = 0; i < n; i++) nctr[i] = (uint32_t)nkeys;
+  } else {
+    std::vector<uint32_t> base(n);
+    for (size_t i = 0; i < n; i++) {
+      base[i] = c3c_base(seed, (uint32_t)i);
+      for (uint32_t k = base[i]; k < base[i] + 16; k++)
+        if ((int)k >= key_lo && (int)k < key_hi) {
+          key_off[k + 1]++;
+          nctr[i]++;
+        }
+    }
+    for (int k = 0; k < kMaxKeys; k++) key_off[k + 1] += key_off[k];
+    h_keys.resize(key_off[kMaxKeys]);
+    h_bm.resize(key_off[kMaxKeys]);
+    std::vector<uint32_t> cur(key_off.begin(), key_off.end() - 1);
+    for (size_t i = 0; i < n; i++)  // ascending i: input order within each key
+      for (uint32_t k = base[i]; k < base[i] + 16; k++)
+        if ((int)k >= key_lo && (int)k < key_hi) {
+          h_keys[cur[k]] = (uint16_t)k;
+          h_bm[cur[k]++] = (uint32_t)i;
+        }
+  }
+  const size_t C = key_off[kMaxKeys];
+  const int32_t id = new_batch(c);
+  Batch& b = *c->batches[id];
+  b.n_bm = n;
+  b.n_ctr = C;
+  b.key_major = true;
+  b.h_bm_nctr = nctr;
+  b.h_bm_card.assign(n, 0);
+  CHK(b.keys.ensure(2 * C + 16));
+  CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
+  CHK(b.bm.ensure(4 * C + 16));
+  CHK(b.key_off.ensure(4 * (kMaxKeys + 1)));
+  CHK(b.bm_off.ensure(8));
+  HIPCHK(hipMemcpyAsync(b.key_off.p, key_off.data(), 4 * (kMaxKeys + 1), hipMemcpyHostToDevice, s));
+  if (kind == 1) {
+    CHK(c->scratch.ensure(16 * (size_t)kMaxKeys));
+    unsigned long long* kb = c->scratch.as<unsigned long long>();
+    launch_synth_c3u(s, seed, (uint32_t)n, key_lo, nkeys, kb, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+    std::vector<unsigned long long> bytes(nkeys + 1, 0);
+    if (nkeys) HIPCHK(hipMemcpyAsync(bytes.data(), kb, 8 * nkeys, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    unsigned long long tot = 0;
+    for (int k = 0; k < nkeys; k++) {
+      const unsigned long long x = bytes[k];
+      bytes[k] = tot;
+      tot += x;
+    }
+    b.payload_bytes = tot;
+    CHK(b.payload.ensure(tot + 64));
+    HIPCHK(hipMemcpyAsync(kb, bytes.data(), 8 * std::max(nkeys, 1), hipMemcpyHostToDevice, s));
+    launch_synth_c3u(s, seed, (uint32_t)n, key_lo, nkeys, nullptr, kb, b.desc.as<CDesc>(), b.keys.as<uint16_t>(),
+                     b.bm.as<uint32_t>(), b.payload.as<uint8_t>(), 1);
+    b.n_kind[DK_A] = (int64_t)C;
+  } else {
+    b.payload_bytes = 8192 * C;
+    CHK(b.payload.ensure(b.payload_bytes + 64));
+    if (C) {
+      HIPCHK(hipMemcpyAsync(b.keys.p, h_keys.data(), 2 * C, hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(b.bm.p, h_bm.data(), 4 * C, hipMemcpyHostToDevice, s));
+    }
+    launch_synth_c3c(s, seed, C, b.keys.as<uint16_t>(), b.bm.as<uint32_t>(), b.desc.as<CDesc>(),
+                     b.payload.as<uint8_t>());
+    b.n_kind[DK_B] = (int64_t)C;
+  }
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemsetAsync(c->scalar.p, 0, 8, s));
+  launch_sum_cards(s, b.desc.as<CDesc>(), C, c->scalar.as<unsigned long long>());
+  unsigned long long card = 0;
+  HIPCHK(hipMemcpyAsync(&card, c->scalar.p, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  b.long_card = (int64_t)card;
+  b.ser_bytes = 0;
+  b.live = true;
+  *out_id = id;
+  return RBG_OK;
+}
+
 int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi, int32_t* batch) {
   Ctx* c = &ctx->c;
   HIPCHK(hipSetDevice(c->device));
-  (void)n;
-  (void)key_lo;
-  (void)key_hi;
+  if (kind == 1 || kind == 2) return synth_c3(c, kind, seed, n, key_lo, key_hi, batch);
   // kind 0: C2 mix; 16 + DK_A/DK_B/DK_R: the same generator with one container family
   if (kind != 0 && !(kind >= 16 && kind <= 18)) {
     set_err("synthetic kind not available");
@@ -1201,16 +1332,13 @@ int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, i
   std::vector<CDesc> d(C);
   HIPCHK(hipMemcpyAsync(d.data(), b.desc.p, sizeof(CDesc) * C, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  int64_t card = 0, ser = 0;
-  bool has_run = false;
+  int64_t card = 0;
   for (const CDesc& x : d) {
     b.n_kind[x.kind]++;
     card += x.card;
-    has_run |= x.kind == KR;
   }
   b.long_card = card;
   b.h_bm_card = {card};
-  (void)ser;
   b.ser_bytes = 0;
   b.live = true;
   *batch = id;

@@ -69,6 +69,15 @@ void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_o
                            const uint8_t* payload, int32_t* out);
 
 // synthetic generators (synth.hip)
+// C3 uniform key slice [key_lo, key_lo + nkeys): pass 0 writes per-key slot bytes,
+// pass 1 (given the exclusive per-key byte offsets) fills desc/keys/bm/payload
+void launch_synth_c3u(hipStream_t s, uint64_t seed, uint32_t n, int key_lo, int nkeys, unsigned long long* key_bytes,
+                      const unsigned long long* key_base, CDesc* desc, uint16_t* keys, uint32_t* bm,
+                      uint8_t* payload, int pass);
+// C3 clustered: keys/bm of every container given (host CSR); fills desc + 8192 B bitmap slots
+void launch_synth_c3c(hipStream_t s, uint64_t seed, uint64_t n_ctr, const uint16_t* keys, const uint32_t* bm,
+                      CDesc* desc, uint8_t* payload);
+void launch_sum_cards(hipStream_t s, const CDesc* desc, uint64_t n, unsigned long long* out);
 // force < 0: C2 mix (kind drawn per key); force = DK_A/DK_B/DK_R: every key drawn from that family
 void launch_synth_c2(hipStream_t s, uint64_t seed, int force, CDesc* desc, uint16_t* keys, uint8_t* payload);
 

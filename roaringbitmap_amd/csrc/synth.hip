@@ -1,0 +1,204 @@
+// Synthetic workloads generated straight into device-resident batches
+// (DESIGN.md §8): C2 operands, C3 uniform / clustered key slices.
+#include <algorithm>
+
+#include "kernels.hpp"
+#include "wave.hpp"
+
+namespace rbg {
+
+// 64 Bernoulli(p = thr / 2^32) bits
+__device__ __forceinline__ uint64_t bernoulli_word(uint64_t seed, uint32_t thr) {
+  uint64_t w = 0;
+#pragma unroll 8
+  for (int i = 0; i < 64; i += 2) {
+    const uint64_t h = splitmix64(seed + (uint64_t)i);
+    w |= (uint64_t)((uint32_t)h < thr) << i;
+    w |= (uint64_t)((uint32_t)(h >> 32) < thr) << (i + 1);
+  }
+  return w;
+}
+
+// ===========================================================================
+// C3 uniform: one workgroup per key, n containers (one per bitmap) per key
+// ===========================================================================
+__device__ __forceinline__ uint32_t c3u_slot_bytes(uint32_t card) { return (2 * card + 15) & ~15u; }
+
+__global__ __launch_bounds__(256) void k_synth_c3u_sizes(uint64_t seed, uint32_t n, int key_lo,
+                                                         unsigned long long* __restrict__ key_bytes) {
+  __shared__ int sh[8];
+  const uint32_t k = key_lo + blockIdx.x;
+  int sum = 0;
+  for (uint32_t i = threadIdx.x; i < n; i += NT) sum += (int)c3u_slot_bytes(c3u_card(seed, i, k));
+  int u = 0;
+  block_sum2(sum, u, sh);
+  if (threadIdx.x == 0) key_bytes[blockIdx.x] = (unsigned long long)sum;
+}
+
+__global__ __launch_bounds__(256) void k_synth_c3u_fill(uint64_t seed, uint32_t n, int key_lo,
+                                                        const unsigned long long* __restrict__ key_base,
+                                                        CDesc* __restrict__ desc, uint16_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ bm, uint8_t* __restrict__ payload) {
+  __shared__ int sh[8];
+  const uint32_t k = key_lo + blockIdx.x;
+  const uint64_t seg = (uint64_t)blockIdx.x * n;
+  uint64_t running = key_base[blockIdx.x];
+  for (uint32_t i0 = 0; i0 < n; i0 += NT) {
+    const uint32_t i = i0 + threadIdx.x;
+    const uint32_t card = i < n ? c3u_card(seed, i, k) : 0;
+    const int sz = (int)c3u_slot_bytes(card);
+    // workgroup exclusive scan of the slot sizes
+    const int incl = wave_incl_scan(sz);
+    if ((threadIdx.x & 63) == 63) sh[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    int pre = incl - sz, tot = 0;
+    for (int w = 0; w < 4; w++) {
+      if (w < (int)(threadIdx.x >> 6)) pre += sh[w];
+      tot += sh[w];
+    }
+    __syncthreads();
+    if (i < n) {
+      const uint64_t p = seg + i, off = running + (uint64_t)pre;
+      desc[p] = CDesc{off, card, (uint16_t)k, DK_A, 0};
+      keys[p] = (uint16_t)k;
+      bm[p] = i;
+      // stratified sorted distinct values: one per stride of 65536 / card
+      uint16_t* v = reinterpret_cast<uint16_t*>(payload + off);
+      const uint32_t step = 65536u / card;
+      const uint64_t h = splitmix64(seed ^ 0x5EEDULL ^ ((uint64_t)i << 20) ^ ((uint64_t)k << 40));
+      for (uint32_t j = 0; j < card; j++) v[j] = (uint16_t)(j * step + (uint32_t)(splitmix64(h + j) % step));
+    }
+    running += (uint64_t)tot;
+  }
+}
+
+// ===========================================================================
+// C3 clustered: one workgroup per container, all bitmap containers (8192 B slots)
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_synth_c3c_fill(uint64_t seed, uint64_t n_ctr,
+                                                        const uint16_t* __restrict__ keys,
+                                                        const uint32_t* __restrict__ bm, CDesc* __restrict__ desc,
+                                                        uint8_t* __restrict__ payload) {
+  __shared__ int sh[8];
+  const uint32_t thr = (uint32_t)(0.95 * 4294967296.0);
+  for (uint64_t p = blockIdx.x; p < n_ctr; p += gridDim.x) {
+    const uint32_t k = keys[p], i = bm[p];
+    const uint64_t h = splitmix64(seed ^ ((uint64_t)i << 24) ^ ((uint64_t)k << 48) ^ 0xC3C0ULL);
+    const uint32_t t = threadIdx.x;
+    const uint32_t widx[4] = {2 * t, 2 * t + 1, 512 + 2 * t, 513 + 2 * t};
+    uint64_t r[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) r[q] = bernoulli_word(splitmix64(h ^ ((uint64_t)widx[q] * 0x100000001B3ULL)), thr);
+    store_bitmap_owned(payload + p * 8192, r);
+    int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
+    int u = 0;
+    block_sum2(c, u, sh);
+    if (t == 0) desc[p] = CDesc{p * 8192, (uint32_t)c, (uint16_t)k, DK_B, 0};
+  }
+}
+
+// total cardinality of a batch (64-bit)
+__global__ __launch_bounds__(256) void k_sum_cards(const CDesc* __restrict__ desc, uint64_t n,
+                                                   unsigned long long* __restrict__ out) {
+  unsigned long long s = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    s += desc[i].card;
+  const int lo = wave_sum_i((int)(uint32_t)(s & 0xFFFFFF));
+  const int hi = wave_sum_i((int)(uint32_t)(s >> 24));
+  if ((threadIdx.x & 63) == 0) atomicAdd(out, (unsigned long long)(uint32_t)lo + ((unsigned long long)(uint32_t)hi << 24));
+}
+
+void launch_synth_c3u(hipStream_t s, uint64_t seed, uint32_t n, int key_lo, int nkeys, unsigned long long* key_bytes,
+                      const unsigned long long* key_base, CDesc* desc, uint16_t* keys, uint32_t* bm,
+                      uint8_t* payload, int pass) {
+  if (nkeys <= 0) return;
+  if (pass == 0)
+    hipLaunchKernelGGL(k_synth_c3u_sizes, dim3(nkeys), dim3(256), 0, s, seed, n, key_lo, key_bytes);
+  else
+    hipLaunchKernelGGL(k_synth_c3u_fill, dim3(nkeys), dim3(256), 0, s, seed, n, key_lo, key_base, desc, keys, bm,
+                       payload);
+}
+void launch_synth_c3c(hipStream_t s, uint64_t seed, uint64_t n_ctr, const uint16_t* keys, const uint32_t* bm,
+                      CDesc* desc, uint8_t* payload) {
+  if (n_ctr == 0) return;
+  const unsigned g = (unsigned)std::min<uint64_t>(n_ctr, 16384);
+  hipLaunchKernelGGL(k_synth_c3c_fill, dim3(g), dim3(256), 0, s, seed, n_ctr, keys, bm, desc, payload);
+}
+void launch_sum_cards(hipStream_t s, const CDesc* desc, uint64_t n, unsigned long long* out) {
+  if (n == 0) return;
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(k_sum_cards, dim3(g), dim3(256), 0, s, desc, n, out);
+}
+
+// ===========================================================================
+// synthetic C2 operand: one workgroup per key, written straight into 8208 B slots
+// ===========================================================================
+
+__global__ __launch_bounds__(256) void k_synth_c2(uint64_t seed, int force, CDesc* __restrict__ desc,
+                                                  uint16_t* __restrict__ keys, uint8_t* __restrict__ payload) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int q[257];
+  __shared__ int sh[8];
+  for (uint32_t k = blockIdx.x; k < 65536; k += gridDim.x) {
+    const uint64_t hk = splitmix64(seed ^ ((uint64_t)k << 20));
+    const int kind_pick = force >= 0 ? force : (int)(hk % 3);
+    uint64_t r[4];
+    const uint32_t t = threadIdx.x;
+    const uint32_t widx[4] = {2 * t, 2 * t + 1, 512 + 2 * t, 513 + 2 * t};
+    if (kind_pick != DK_R) {
+      // A: target card U[1,4096]; B: U[4097,65535]; realised by Bernoulli bits
+      const uint32_t target = kind_pick == DK_A ? 1 + (uint32_t)((hk >> 8) % 4096) : 4097 + (uint32_t)((hk >> 8) % 61439);
+      const uint32_t thr = (uint32_t)(((uint64_t)target << 32) / 65536);
+#pragma unroll
+      for (int i = 0; i < 4; i++) r[i] = bernoulli_word(splitmix64(hk ^ ((uint64_t)widx[i] * 0x100000001B3ULL)), thr);
+    } else {
+      // R: nr in U[1,2047] runs, one per equal segment, each followed by a gap
+      const int nr = 1 + (int)((hk >> 8) % 2047);
+      const int seg = 65536 / nr;
+      __syncthreads();
+      lds_clear(acc);
+      __syncthreads();
+      for (int i = t; i < nr; i += NT) {
+        const uint64_t h = splitmix64(hk + 0x51ULL * (uint64_t)(i + 1));
+        const int half = max(seg / 2, 1);
+        const int start = i * seg + (int)(h % (uint64_t)half);
+        const int maxlen = (i + 1) * seg - 1 - start;  // keeps a gap before the next segment
+        const int len = maxlen > 0 ? 1 + (int)((h >> 32) % (uint64_t)maxlen) : 1;
+        lds_or_run_serial(acc, start, start + len - 1);
+      }
+      __syncthreads();
+      lds_read_owned(acc, r);
+    }
+    int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
+    int u = 0;
+    block_sum2(c, u, sh);
+    if (c == 0) {  // never emit an empty container
+      if (t == 0) r[0] |= 1ULL << (k & 63);
+      c = 1;
+    }
+    int kind;
+    if (kind_pick == DK_R) kind = eff(c, count_runs(r, acc, sh));  // runOptimize of a run container
+    else kind = by_card(c);
+    uint8_t* slot = payload + (size_t)k * kSlotBytes;
+    const uint32_t len = stage_container(kind, r, c, acc, tmp, sh);
+    copy_lds_to_global<NT>(slot + (kind == DK_R ? 2 : 0), tmp, len, t);
+    __syncthreads();
+    if (t == 0) {
+      CDesc d;
+      d.slot = (uint64_t)k * kSlotBytes;
+      d.card = (uint32_t)c;
+      d.key = (uint16_t)k;
+      d.kind = (uint8_t)kind;
+      d.flags = 0;
+      desc[k] = d;
+      keys[k] = (uint16_t)k;
+    }
+  }
+}
+
+void launch_synth_c2(hipStream_t s, uint64_t seed, int force, CDesc* desc, uint16_t* keys, uint8_t* payload) {
+  hipLaunchKernelGGL(k_synth_c2, dim3(4096), dim3(256), 0, s, seed, force, desc, keys, payload);
+}
+
+}  // namespace rbg

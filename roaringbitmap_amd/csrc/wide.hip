@@ -454,93 +454,4 @@ void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_o
   hipLaunchKernelGGL(k_batch_and_card, dim3((unsigned)g), dim3(256), 0, s, n_pairs, bm_off, desc, payload, out);
 }
 
-// ===========================================================================
-// synthetic C2 operand: one workgroup per key, written straight into 8208 B slots
-// ===========================================================================
-__device__ __forceinline__ uint64_t splitmix(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ULL;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ULL;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBULL;
-  return x ^ (x >> 31);
-}
-
-// 64 Bernoulli(p = thr / 2^32) bits
-__device__ __forceinline__ uint64_t bernoulli_word(uint64_t seed, uint32_t thr) {
-  uint64_t w = 0;
-#pragma unroll 8
-  for (int i = 0; i < 64; i += 2) {
-    const uint64_t h = splitmix(seed + (uint64_t)i);
-    w |= (uint64_t)((uint32_t)h < thr) << i;
-    w |= (uint64_t)((uint32_t)(h >> 32) < thr) << (i + 1);
-  }
-  return w;
-}
-
-__global__ __launch_bounds__(256) void k_synth_c2(uint64_t seed, int force, CDesc* __restrict__ desc,
-                                                  uint16_t* __restrict__ keys, uint8_t* __restrict__ payload) {
-  __shared__ __align__(16) uint32_t acc[2048];
-  __shared__ __align__(16) uint32_t tmp[2048];
-  __shared__ int q[257];
-  __shared__ int sh[8];
-  for (uint32_t k = blockIdx.x; k < 65536; k += gridDim.x) {
-    const uint64_t hk = splitmix(seed ^ ((uint64_t)k << 20));
-    const int kind_pick = force >= 0 ? force : (int)(hk % 3);
-    uint64_t r[4];
-    const uint32_t t = threadIdx.x;
-    const uint32_t widx[4] = {2 * t, 2 * t + 1, 512 + 2 * t, 513 + 2 * t};
-    if (kind_pick != DK_R) {
-      // A: target card U[1,4096]; B: U[4097,65535]; realised by Bernoulli bits
-      const uint32_t target = kind_pick == DK_A ? 1 + (uint32_t)((hk >> 8) % 4096) : 4097 + (uint32_t)((hk >> 8) % 61439);
-      const uint32_t thr = (uint32_t)(((uint64_t)target << 32) / 65536);
-#pragma unroll
-      for (int i = 0; i < 4; i++) r[i] = bernoulli_word(splitmix(hk ^ ((uint64_t)widx[i] * 0x100000001B3ULL)), thr);
-    } else {
-      // R: nr in U[1,2047] runs, one per equal segment, each followed by a gap
-      const int nr = 1 + (int)((hk >> 8) % 2047);
-      const int seg = 65536 / nr;
-      __syncthreads();
-      lds_clear(acc);
-      __syncthreads();
-      for (int i = t; i < nr; i += NT) {
-        const uint64_t h = splitmix(hk + 0x51ULL * (uint64_t)(i + 1));
-        const int half = max(seg / 2, 1);
-        const int start = i * seg + (int)(h % (uint64_t)half);
-        const int maxlen = (i + 1) * seg - 1 - start;  // keeps a gap before the next segment
-        const int len = maxlen > 0 ? 1 + (int)((h >> 32) % (uint64_t)maxlen) : 1;
-        lds_or_run_serial(acc, start, start + len - 1);
-      }
-      __syncthreads();
-      lds_read_owned(acc, r);
-    }
-    int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
-    int u = 0;
-    block_sum2(c, u, sh);
-    if (c == 0) {  // never emit an empty container
-      if (t == 0) r[0] |= 1ULL << (k & 63);
-      c = 1;
-    }
-    int kind;
-    if (kind_pick == DK_R) kind = eff(c, count_runs(r, acc, sh));  // runOptimize of a run container
-    else kind = by_card(c);
-    uint8_t* slot = payload + (size_t)k * kSlotBytes;
-    const uint32_t len = stage_container(kind, r, c, acc, tmp, sh);
-    copy_lds_to_global<NT>(slot + (kind == DK_R ? 2 : 0), tmp, len, t);
-    __syncthreads();
-    if (t == 0) {
-      CDesc d;
-      d.slot = (uint64_t)k * kSlotBytes;
-      d.card = (uint32_t)c;
-      d.key = (uint16_t)k;
-      d.kind = (uint8_t)kind;
-      d.flags = 0;
-      desc[k] = d;
-      keys[k] = (uint16_t)k;
-    }
-  }
-}
-
-void launch_synth_c2(hipStream_t s, uint64_t seed, int force, CDesc* desc, uint16_t* keys, uint8_t* payload) {
-  hipLaunchKernelGGL(k_synth_c2, dim3(4096), dim3(256), 0, s, seed, force, desc, keys, payload);
-}
-
 }  // namespace rbg

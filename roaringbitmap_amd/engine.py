@@ -14,6 +14,14 @@ from .roaring import RoaringBitmap
 SYNTH_C2, SYNTH_C3_UNIFORM, SYNTH_C3_CLUSTERED, SYNTH_C4_PAIRS = 0, 1, 2, 3
 
 
+def synth_key_bytes(kind, seed, n) -> np.ndarray:
+    """Per-key algorithmic input bytes of a synthetic C3 workload (host, for key-range partitioning)."""
+    out = np.zeros(65536, dtype=np.uint64)
+    check(lib().rbg_synth_key_bytes(int(kind), int(seed), int(n),
+                                    out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))))
+    return out
+
+
 class Engine:
     def __init__(self, device=0):
         self._ctx = ctypes.c_void_p()
@@ -89,6 +97,22 @@ class Engine:
         if ids is not None:
             idp = (ctypes.c_int32 * len(ids))(*ids)
         check(lib().rbg_ctx_wide(self._ctx, _lib.WIDE_OP[op], int(batch), int(key_lo), int(key_hi), idp))
+
+    def wide_start(self, op, batch, key_lo, key_hi, start_bm, ids=None):
+        """wide op whose naive_and chain starts from input `start_bm` (key-range shards)."""
+        idp = None
+        if ids is not None:
+            idp = (ctypes.c_int32 * len(ids))(*ids)
+        check(lib().rbg_ctx_wide_start(self._ctx, _lib.WIDE_OP[op], int(batch), int(key_lo), int(key_hi), idp,
+                                       int(start_bm)))
+
+    def batch_counts(self, batch) -> np.ndarray:
+        """containers per input bitmap of a batch"""
+        n = self.batch_stats(batch)["bitmaps"]
+        out = np.zeros(n, dtype=np.uint32)
+        check(lib().rbg_ctx_batch_counts(self._ctx, int(batch), out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)),
+                                         n))
+        return out
 
     def wide_card(self, op, batch, key_lo=0, key_hi=65536):
         check(lib().rbg_ctx_wide_card(self._ctx, _lib.WIDE_CARD_OP[op], int(batch), int(key_lo), int(key_hi)))
