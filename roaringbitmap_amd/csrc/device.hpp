@@ -87,6 +87,10 @@ struct __align__(16) ORec {
 
 // where an op writes its result: payload region at out + payload_base, header in
 // front of it; look-back state (ticket, error word, per-task status) and records
+// the result's long cardinality is accumulated at ((u64*)OutCtx::err)[kCardWord]
+// (inside the zeroed look-back header, 32 B past the error word)
+constexpr int kCardWord = 4;
+
 struct OutCtx {
   uint8_t* out;
   uint64_t payload_base;

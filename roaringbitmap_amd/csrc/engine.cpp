@@ -39,7 +39,7 @@ static void set_err(const std::string& s) { g_err = s; }
 
 constexpr size_t kSlack = 256;  // every device buffer carries read slack (group_copy)
 constexpr int kMaxKeys = 65536;
-constexpr size_t kLbHeader = 256;  // look-back state: ticket @0, error @64, tile ticket @128, statuses @256
+constexpr size_t kLbHeader = 256;  // look-back state: ticket @0, error @64, result card @96, tile ticket @128
 constexpr size_t kMaxTiles = 128;  // tile statuses follow the 65536 task statuses
 
 // RBG_DEBUG_SYNC=1: synchronise and report after every pipeline stage (debugging aid)
@@ -537,6 +537,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.payload = B->payload.as<uint8_t>();
     wa.skip = skip.empty() ? nullptr : c->skip.as<uint8_t>();
     wa.start_bm = start_bm;
+    wa.all_array = (B->n_kind[DK_B] == 0 && B->n_kind[DK_R] == 0) ? 1u : 0u;
     c->mark(1);
     launch_wide(s, mode, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
                 c->task_card.as<uint32_t>());
@@ -556,7 +557,14 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
 
 static int ctx_info(Ctx* c, ResultInfo* ri) {
   HIPCHK(hipMemcpyAsync(ri, c->info.p, sizeof(ResultInfo), hipMemcpyDeviceToHost, c->stream));
+  uint64_t card = 0;
+  if (c->last == 1)  // materialised result: k_place accumulated its cardinality
+    HIPCHK(hipMemcpyAsync(&card, c->lb.as<uint8_t>() + 64 + 8 * kCardWord, 8, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
+  if (c->last == 1) {
+    ri->long_card = (int64_t)card;
+    ri->card32 = (uint32_t)card;
+  }
   return RBG_OK;
 }
 

@@ -225,6 +225,14 @@ __global__ __launch_bounds__(256) void k_ingest(const uint8_t* __restrict__ raw,
     const IngestItem it = items[i];
     uint8_t* dst = payload + it.dst + (it.kind == DK_R ? 2 : 0);
     group_copy<64>(dst, raw + it.src, it.len, lane);
+    if (it.kind == DK_A && it.len) {
+      // pad the slot to 16 B with copies of the last value: a run of A slots is
+      // then a plain u16 value stream that OR-type reductions can scatter whole
+      const uint16_t last = (uint16_t)(raw[it.src + it.len - 2] | (raw[it.src + it.len - 1] << 8));
+      uint16_t* d16 = reinterpret_cast<uint16_t*>(payload + it.dst);
+      const uint32_t v0 = it.len / 2, v1 = ((it.len + 15) & ~15u) / 2;
+      for (uint32_t v = v0 + lane; v < v1; v += 64) d16[v] = last;
+    }
   }
 }
 
@@ -266,6 +274,7 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
     uint32_t keep[4], len[4], run[4];
     uint32_t c = 0, r = 0;
     unsigned long long b = 0;
+    uint32_t card = 0;  // <= 4 x 65536 per thread
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       keep[i] = len[i] = run[i] = 0;
@@ -274,10 +283,19 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
         keep[i] = x.keep;
         len[i] = x.keep ? x.ser_len : 0;
         run[i] = x.keep && x.kind == DK_R;
+        card += x.keep ? x.card : 0;
       }
       c += keep[i];
       b += len[i];
       r |= run[i];
+    }
+    // result cardinality: per-wave sum, one 64-bit atomic per wave (read by ctx_info)
+    {
+      const int cw = wave_sum_i((int)(card >> 4));  // 64 x 2^14 fits an int
+      const int lw = wave_sum_i((int)(card & 15));
+      if ((threadIdx.x & 63) == 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(oc.err) + kCardWord,
+                  ((unsigned long long)(uint32_t)cw << 4) + (uint32_t)lw);
     }
     // workgroup exclusive scan of (count, bytes), OR of run
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;

@@ -31,6 +31,7 @@ struct WideArgs {
   const uint8_t* payload; // arena
   const uint8_t* skip;    // naive_and: per input bitmap, 1 = skip (identity with the start)
   uint32_t start_bm;      // naive_and: input bitmap the chain starts from
+  uint32_t all_array;     // every container is an array (slots padded with their last value)
 };
 
 // Workgroups of `kernel` (256 threads) that are resident on the whole device at

@@ -66,7 +66,9 @@ __global__ __launch_bounds__(256) void k_synth_c3u_fill(uint64_t seed, uint32_t 
       uint16_t* v = reinterpret_cast<uint16_t*>(payload + off);
       const uint32_t step = 65536u / card;
       const uint64_t h = splitmix64(seed ^ 0x5EEDULL ^ ((uint64_t)i << 20) ^ ((uint64_t)k << 40));
-      for (uint32_t j = 0; j < card; j++) v[j] = (uint16_t)(j * step + (uint32_t)(splitmix64(h + j) % step));
+      uint16_t x = 0;
+      for (uint32_t j = 0; j < card; j++) v[j] = x = (uint16_t)(j * step + (uint32_t)(splitmix64(h + j) % step));
+      for (uint32_t j = card; j < (uint32_t)sz / 2; j++) v[j] = x;  // slot padding repeats the last value
     }
     running += (uint64_t)tot;
   }

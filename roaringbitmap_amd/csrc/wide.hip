@@ -110,6 +110,23 @@ __device__ __forceinline__ void accumulate_segment(const CDesc* desc, const uint
   for (int i = 0; i < 4; i++) r[i] = MODE == 0 ? (r[i] | x[i]) : (r[i] ^ x[i]);
 }
 
+// OR a stream of u16 values (16 B vectors, every value valid) into the LDS
+// bitmap: four vectors per thread in flight per round.
+__device__ __forceinline__ void stream_or_values(uint32_t* acc, const uint4* v4, uint32_t nvec) {
+  constexpr int U = 4;
+  for (uint32_t j0 = 0; j0 < nvec; j0 += U * NT) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t k = j0 + u * NT + threadIdx.x;
+      v[u] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (j0 + u * NT + threadIdx.x < nvec) scatter_vec<0>(acc, v[u], 0, 8);
+  }
+}
+
 __device__ __forceinline__ int block_card(const uint64_t r[4], int* sh) {
   int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
   int u = 0;
@@ -166,6 +183,26 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         materialize(d, A.payload, tmp, q, r);  // toBitmapOrArrayContainer
         c = (int)d.card;
         kind = by_card(c);
+      } else if (A.all_array) {
+        // every slot of the segment is an array padded with its last value, and
+        // the slots are contiguous: the segment is one u16 value stream
+        __syncthreads();
+        lds_clear(acc);
+#pragma unroll
+        for (int i = 0; i < 4; i++) r[i] = 0;
+        const CDesc d0 = A.desc[s], d1 = A.desc[s + n - 1];
+        const uint4* v4 = reinterpret_cast<const uint4*>(A.payload + d0.slot);
+        const uint32_t nvec = (uint32_t)((d1.slot + ((2 * d1.card + 15) & ~15u) - d0.slot) >> 4);
+        __syncthreads();
+        stream_or_values(acc, v4, nvec);
+        __syncthreads();
+        lds_read_owned(acc, r);
+        c = block_card(r, sh);
+        if (MODE == WIDE_OR_CARD) {
+          if (threadIdx.x == 0) task_card[t] = (uint32_t)c;
+          continue;
+        }
+        kind = c == 65536 ? DK_R : by_card(c);
       } else {
         __syncthreads();
         lds_clear(acc);

@@ -73,7 +73,12 @@ def test_c3_synthetic_matches_oracle(gpu, kind):
     assert sum(O.stats(b)["card"] for b in bms) == st["cardinality"]
     for op in ["or", "xor", "and"]:
         e.wide(op, batch)
-        assert e.fetch().serialize() == O.wide(op, bms), op
+        exp = O.wide(op, bms)
+        rs = e.result_stats()  # device-side result facts before serialization
+        so = O.stats(exp)
+        assert rs["cardinality"] == so["card"] and rs["payload_bytes"] == so["payload"], op
+        assert rs["containers"] == so["array"] + so["bitmap"] + so["run"], op
+        assert e.fetch().serialize() == exp, op
     # key-sliced generation: a slice equals the restriction of the full batch
     if kind == 2:
         ranges = shard.key_ranges(shard_key_bytes(kind, n), 3)
