@@ -46,6 +46,74 @@ def _pmc_traffic():
         return None
 
 
+def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev):
+    """C3 wide OR of n synthetic bitmaps, key-range sharded over the ranks.
+
+    Each rank generates and reduces only its key slice (equal input bytes); one
+    step = the slice's FastAggregation.or + the RCCL all-gather of the shard
+    layout (containers, payload bytes, has_run) that places every shard in the
+    global portable result.  Strong scaling: the 10,000-bitmap job is fixed.
+    """
+    import torch
+    from roaringbitmap_amd import shard
+    from roaringbitmap_amd.engine import synth_key_bytes
+    seed = 0xC3000000
+    if kind == 1:
+        ranges = [((65536 * r) // world, (65536 * (r + 1)) // world) for r in range(world)]  # uniform: equal keys
+    else:
+        ranges = shard.key_ranges(synth_key_bytes(kind, seed, n), world)
+    lo, hi = ranges[rank]
+    b = eng.synth(kind, seed, n, lo, hi)
+    st = eng.batch_stats(b)
+    in_bytes = st["payload_bytes"] + 4 * st["containers"]
+    dev = torch.device("cuda", torch.cuda.current_device()) if cdev == "cuda" else torch.device("cpu")
+
+    def step():
+        eng.wide("or", b, lo, hi)
+        if dist is not None:
+            rs = eng.result_stats()
+            shard.global_layout(rs["containers"], rs["payload_bytes"], rs["has_run"], device=dev)
+
+    for _ in range(warmup):
+        step()
+    eng.sync()
+    rs = eng.result_stats()
+    out_bytes = rs["payload_bytes"] + 4 * rs["containers"]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    eng.sync()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    eng.profile(steps)
+    for _ in range(steps):
+        eng.wide("or", b, lo, hi)
+    k, ph = eng.profile_read()
+    eng.profile(0)
+    kern_ms = ph[1] / max(k, 1)
+    t = torch.tensor([wall, float(in_bytes), float(out_bytes)], dtype=torch.float64, device=dev)
+    if dist is not None:
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        t[0] = tm[0]
+    wall, tin, tout = float(t[0]), float(t[1]), float(t[2])
+    eng.release(b)
+    ms = wall / steps * 1e3
+    ach = (in_bytes + out_bytes) / (kern_ms / 1e3) / 1e9
+    return {"workload": f"C3 {'uniform' if kind == 1 else 'clustered'}: FastAggregation.or of {n} synthetic bitmaps, "
+                        f"key-range sharded over {world} GPU(s)",
+            "input_GBps": round(tin / (wall / steps) / 1e9, 1), "ms_per_step": round(ms, 4),
+            "input_bytes": int(tin), "output_bytes": int(tout), "containers_in": st["containers"],
+            "rank0_keys": [lo, hi],
+            "roofline_rank0": {"kernel": "k_wide<OR>", "achieved_GBps": round(ach, 1),
+                               "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern_ms, 4)}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -53,6 +121,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c3-n", type=int, default=10000, help="bitmaps of the C3 wide-OR workloads (0 = skip)")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo to rehearse "
+                                                       "several ranks on one GPU)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -60,11 +131,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import torch
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)  # rehearsal: several ranks may share one GPU (gloo)
     torch.cuda.set_device(local)
     dist = None
+    cdev = "cuda"
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
+            cdev = "cpu"
 
     from roaringbitmap_amd import Engine
 
@@ -123,7 +201,12 @@ def main():
     eng.profile(0)
     ph_avg = [x / max(n_ops, 1) for x in ph]
 
-    t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device="cuda")
+    c3 = {}
+    if args.c3_n > 0:
+        for kind, name in ((1, "c3_uniform_or"), (2, "c3_clustered_or")):
+            c3[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev)
+
+    t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device=cdev)
     if dist is not None:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
@@ -182,6 +265,7 @@ def main():
                 "operand_mix": {k: [sa[k], sb[k]] for k in ["array", "bitmap", "run"]},
                 "result": rs,
                 "input_frac_of_peak": round(total_in / step_s / 1e9 / world / HBM_PEAK_GBS, 4),
+                **c3,
             },
         }
         print(json.dumps(line), flush=True)
