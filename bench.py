@@ -114,6 +114,37 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev):
                                "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern_ms, 4)}}
 
 
+def c4_batch_and_card(eng, n_pairs, rank, world, dist, steps, warmup, cdev):
+    """C4: batched andCardinality of n_pairs small sparse pairs per rank (weak scaling)."""
+    import torch
+    b = eng.synth(3, 0xC4 + 0x10000 * rank, n_pairs)
+    matched, allb = eng.pair_bytes(b)
+    for _ in range(warmup):
+        eng.batch_and_card(b)
+    eng.sync()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.batch_and_card(b)
+    eng.sync()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall, float(n_pairs), float(matched)], dtype=torch.float64, device=cdev)
+    if dist is not None:
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        t[0] = tm[0]
+    step = float(t[0]) / steps
+    eng.release(b)
+    return {"workload": f"C4: batched RoaringBitmap.andCardinality of {n_pairs} small sparse pairs per GPU",
+            "pairs_per_s": round(float(t[1]) / step, 1), "ms_per_step": round(step * 1e3, 4),
+            "input_GBps": round(float(t[2]) / step / 1e9, 1), "input_bytes_per_rank": matched,
+            "all_bytes_per_rank": allb}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -122,6 +153,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-n", type=int, default=10000, help="bitmaps of the C3 wide-OR workloads (0 = skip)")
+    ap.add_argument("--c4-pairs", type=int, default=1000000, help="pairs of the C4 workload per GPU (0 = skip)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo to rehearse "
                                                        "several ranks on one GPU)")
     args = ap.parse_args()
@@ -205,6 +237,9 @@ def main():
     if args.c3_n > 0:
         for kind, name in ((1, "c3_uniform_or"), (2, "c3_clustered_or")):
             c3[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev)
+    if args.c4_pairs > 0:
+        c3["c4_batch_and_card"] = c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, max(3, args.steps // 4), 1,
+                                                    cdev)
 
     t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device=cdev)
     if dist is not None:

@@ -142,7 +142,8 @@ int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, s
  *   kind 0: C2 operand: one bitmap, all 65536 keys, per key A/B/R with p=1/3 (seed)
  *   kind 1: C3 uniform: n bitmaps x keys [key_lo,key_hi), ~15.26 values per (bitmap,key)
  *   kind 2: C3 clustered: n bitmaps, 16 dense bitmap keys each, restricted to [key_lo,key_hi)
- *   kind 3: C4 pairs: n bitmaps (2 per pair), 1-4 array keys in [0,64) each */
+ *   kind 3: C4 pairs: n pairs = 2n bitmaps, bitmap-major (pairs adjacent), 1-4 array keys in
+ *           [0,64) each, card 16..512 (key_lo / key_hi ignored) */
 int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi,
                   int32_t* batch);
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch);
@@ -170,6 +171,10 @@ int rbg_ctx_wide_card(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_h
  * universe (RB/FastAggregation.java:333-339), which its key slice cannot see. */
 int rbg_ctx_wide_start(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, const int32_t* ids,
                        int32_t start_bm);
+/* Algorithmic input bytes of batched andCardinality over the pairs of a bitmap-major
+ * batch (array / bitmap payloads; synthetic C4 batches have no run containers):
+ * out2[0] = matched payload + 4 B per descriptor, out2[1] = all of it. */
+int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2);
 /* Containers per input bitmap of a batch (out has n == bitmaps entries). */
 int rbg_ctx_batch_counts(rbg_ctx* ctx, int32_t batch, uint32_t* out, size_t n);
 /* Algorithmic input bytes per key (payload + 4 B descriptor per container) of the

@@ -1117,6 +1117,38 @@ int rbg_synth_key_bytes(int kind, uint64_t seed, size_t n, uint64_t* out) {
   }
   return RBG_OK;
 }
+int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2) {
+  Batch* b;
+  CHK(get_batch(&ctx->c, batch, &b));
+  if (!out2 || b->key_major || b->n_bm % 2) {
+    set_err("needs a bitmap-major batch of pairs");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  HIPCHK(hipSetDevice(ctx->c.device));
+  HIPCHK(hipStreamSynchronize(ctx->c.stream));
+  std::vector<CDesc> d(b->n_ctr);
+  if (b->n_ctr) HIPCHK(hipMemcpy(d.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
+  auto pay = [](const CDesc& x) -> int64_t { return x.kind == KA ? 2 * (int64_t)x.card : x.kind == KB ? 8192 : 0; };
+  int64_t matched = 0, all = 0;
+  for (size_t p = 0; p < b->n_bm / 2; p++) {
+    uint32_t i = b->h_bm_off[2 * p], ie = b->h_bm_off[2 * p + 1], j = ie, je = b->h_bm_off[2 * p + 2];
+    all += 4 * (int64_t)(je - i);
+    while (i < ie && j < je) {
+      if (d[i].key == d[j].key) {
+        matched += pay(d[i++]) + pay(d[j++]);
+      } else if (d[i].key < d[j].key) {
+        i++;
+      } else {
+        j++;
+      }
+    }
+  }
+  out2[0] = matched + all;  // matched payload + descriptors
+  int64_t tot = 0;
+  for (const CDesc& x : d) tot += pay(x) + 4;
+  out2[1] = tot;  // every payload + descriptors
+  return RBG_OK;
+}
 int rbg_ctx_wide_card(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi) {
   HIPCHK(hipSetDevice(ctx->c.device));
   int hc;
@@ -1305,10 +1337,71 @@ static int synth_c3(Ctx* c, int kind, uint64_t seed, size_t n, int key_lo, int k
   return RBG_OK;
 }
 
+// C4: n pairs = 2n small bitmaps, bitmap-major (pairs adjacent).  Each bitmap has
+// K in [1,4] keys from [0,64), each an array container of card in [16,512].
+static int synth_c4(Ctx* c, uint64_t seed, size_t n_pairs, int32_t* out_id) {
+  const size_t nb = 2 * n_pairs;
+  if (nb == 0 || nb > 0x7FFFFFFF) return RBG_ERR_ILLEGAL_ARGUMENT;
+  const int32_t id = new_batch(c);
+  Batch& b = *c->batches[id];
+  b.n_bm = nb;
+  b.key_major = false;
+  b.h_bm_off.assign(nb + 1, 0);
+  b.h_bm_nctr.resize(nb);
+  b.h_bm_card.resize(nb);
+  std::vector<CDesc> d;
+  d.reserve(nb * 5 / 2 + 16);
+  uint64_t off = 0;
+  for (size_t j = 0; j < nb; j++) {
+    const uint64_t h = splitmix64(seed ^ (0xC4000000ULL + j));
+    const int K = 1 + (int)(h % 4);
+    uint64_t used = 0;
+    int got = 0;
+    for (uint64_t t = 1; got < K; t++) {
+      const int k = (int)(splitmix64(h + t) & 63);
+      if (!((used >> k) & 1)) {
+        used |= 1ULL << k;
+        got++;
+      }
+    }
+    int64_t card_sum = 0;
+    for (int k = 0; k < 64; k++)
+      if ((used >> k) & 1) {
+        const uint32_t card = 16 + (uint32_t)(splitmix64(h ^ ((uint64_t)k << 40)) % 497);
+        d.push_back(CDesc{off, card, (uint16_t)k, DK_A, 0});
+        off += (2 * card + 15) & ~15ull;
+        card_sum += card;
+      }
+    b.h_bm_nctr[j] = (uint32_t)K;
+    b.h_bm_off[j + 1] = b.h_bm_off[j] + (uint32_t)K;
+    b.h_bm_card[j] = card_sum;
+    b.long_card += card_sum;
+  }
+  const size_t C = d.size();
+  b.n_ctr = C;
+  b.n_kind[DK_A] = (int64_t)C;
+  b.payload_bytes = off;
+  CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
+  CHK(b.keys.ensure(2 * C + 16));
+  CHK(b.bm.ensure(4 * C + 16));
+  CHK(b.bm_off.ensure(4 * (nb + 1)));
+  CHK(b.payload.ensure(off + 64));
+  hipStream_t s = c->stream;
+  HIPCHK(hipMemcpyAsync(b.desc.p, d.data(), sizeof(CDesc) * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (nb + 1), hipMemcpyHostToDevice, s));
+  launch_synth_arrays(s, seed, b.desc.as<CDesc>(), C, b.payload.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));
+  b.live = true;
+  *out_id = id;
+  return RBG_OK;
+}
+
 int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi, int32_t* batch) {
   Ctx* c = &ctx->c;
   HIPCHK(hipSetDevice(c->device));
   if (kind == 1 || kind == 2) return synth_c3(c, kind, seed, n, key_lo, key_hi, batch);
+  if (kind == 3) return synth_c4(c, seed, n, batch);
   // kind 0: C2 mix; 16 + DK_A/DK_B/DK_R: the same generator with one container family
   if (kind != 0 && !(kind >= 16 && kind <= 18)) {
     set_err("synthetic kind not available");

@@ -99,6 +99,27 @@ __global__ __launch_bounds__(256) void k_synth_c3c_fill(uint64_t seed, uint64_t 
   }
 }
 
+// Array payloads of given descriptors (one thread per container): stratified
+// sorted distinct values, slot padded with the last value.
+__global__ __launch_bounds__(256) void k_synth_arrays(uint64_t seed, const CDesc* __restrict__ desc, uint64_t n,
+                                                      uint8_t* __restrict__ payload) {
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x) {
+    const CDesc d = desc[p];
+    uint16_t* v = reinterpret_cast<uint16_t*>(payload + d.slot);
+    const uint32_t step = 65536u / d.card;
+    const uint64_t h = splitmix64(seed ^ 0xA77AULL ^ (p << 8));
+    uint16_t x = 0;
+    for (uint32_t j = 0; j < d.card; j++) v[j] = x = (uint16_t)(j * step + (uint32_t)(splitmix64(h + j) % step));
+    for (uint32_t j = d.card; j < ((2 * d.card + 15) & ~15u) / 2; j++) v[j] = x;
+  }
+}
+
+void launch_synth_arrays(hipStream_t s, uint64_t seed, const CDesc* desc, uint64_t n, uint8_t* payload) {
+  if (n == 0) return;
+  const unsigned g = (unsigned)std::min<uint64_t>((n + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_synth_arrays, dim3(g), dim3(256), 0, s, seed, desc, n, payload);
+}
+
 // total cardinality of a batch (64-bit)
 __global__ __launch_bounds__(256) void k_sum_cards(const CDesc* __restrict__ desc, uint64_t n,
                                                    unsigned long long* __restrict__ out) {

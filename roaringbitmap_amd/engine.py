@@ -106,6 +106,12 @@ class Engine:
         check(lib().rbg_ctx_wide_start(self._ctx, _lib.WIDE_OP[op], int(batch), int(key_lo), int(key_hi), idp,
                                        int(start_bm)))
 
+    def pair_bytes(self, batch):
+        """(matched payload + descriptors, all payload + descriptors) of a batch of pairs (C4)."""
+        out = (ctypes.c_int64 * 2)()
+        check(lib().rbg_ctx_pair_bytes(self._ctx, int(batch), out))
+        return int(out[0]), int(out[1])
+
     def batch_counts(self, batch) -> np.ndarray:
         """containers per input bitmap of a batch"""
         n = self.batch_stats(batch)["bitmaps"]

@@ -22,3 +22,21 @@ def test_batch_and_card(gpu, seed):
     got = rb.batch_and_cardinality([(rb.RoaringBitmap(a), rb.RoaringBitmap(b)) for a, b in pairs])
     exp = np.array([O.pairwise_card("and", a, b) for a, b in pairs], dtype=np.int32)
     np.testing.assert_array_equal(got, exp)
+
+
+def test_c4_synthetic_pairs(gpu):
+    """C4 batches generated on the device: batched andCardinality == oracle per pair."""
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+    n = 3000
+    b = e.synth(3, 0xC4, n)
+    st = e.batch_stats(b)
+    assert st["bitmaps"] == 2 * n and st["array"] == st["containers"]
+    e.batch_and_card(b)
+    got = e.cards(n)
+    bms = [e.batch_fetch(b, i).serialize() for i in range(2 * n)]
+    exp = np.array([O.pairwise_card("and", bms[2 * i], bms[2 * i + 1]) for i in range(n)], dtype=np.int32)
+    np.testing.assert_array_equal(got, exp)
+    assert sum(O.stats(x)["card"] for x in bms) == st["cardinality"]
+    matched, allb = e.pair_bytes(b)
+    assert 0 < matched <= allb
