@@ -175,6 +175,9 @@ int rbg_ctx_wide_start(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_
  * batch (array / bitmap payloads; synthetic C4 batches have no run containers):
  * out2[0] = matched payload + 4 B per descriptor, out2[1] = all of it. */
 int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2);
+/* Diagnostics: per-phase shader-clock totals of the pairwise kernel (all zero unless the
+ * library was built with -DRBG_STAMPS=1); reset != 0 clears them. */
+int rbg_debug_stamps(uint64_t* out16, int reset);
 /* Containers per input bitmap of a batch (out has n == bitmaps entries). */
 int rbg_ctx_batch_counts(rbg_ctx* ctx, int32_t batch, uint32_t* out, size_t n);
 /* Algorithmic input bytes per key (payload + 4 B descriptor per container) of the

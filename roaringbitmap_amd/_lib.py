@@ -35,7 +35,7 @@ EXPORTED = [
     "rbg_ctx_pairwise", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
     "rbg_ctx_batch_and_card", "rbg_ctx_card", "rbg_ctx_cards", "rbg_ctx_result_stats", "rbg_ctx_fetch",
     "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read", "rbg_ctx_serialize", "rbg_ctx_wide_start",
-    "rbg_ctx_batch_counts", "rbg_synth_key_bytes", "rbg_ctx_pair_bytes",
+    "rbg_ctx_batch_counts", "rbg_synth_key_bytes", "rbg_ctx_pair_bytes", "rbg_debug_stamps",
 ]
 
 _lib = None
@@ -78,6 +78,7 @@ def _declare(L):
     L.rbg_ctx_wide_card.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int]
     L.rbg_ctx_wide_start.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int, P(i32), i32]
     L.rbg_ctx_batch_counts.argtypes = [vp, i32, P(ctypes.c_uint32), sz]
+    L.rbg_debug_stamps.argtypes = [P(ctypes.c_uint64), ctypes.c_int]
     L.rbg_ctx_pair_bytes.argtypes = [vp, i32, P(ctypes.c_int64)]
     L.rbg_synth_key_bytes.argtypes = [ctypes.c_int, ctypes.c_uint64, sz, P(ctypes.c_uint64)]
     L.rbg_ctx_batch_and_card.argtypes = [vp, i32]

@@ -1117,6 +1117,11 @@ int rbg_synth_key_bytes(int kind, uint64_t seed, size_t n, uint64_t* out) {
   }
   return RBG_OK;
 }
+int rbg_debug_stamps(uint64_t* out16, int reset) {
+  if (!out16) return RBG_ERR_ILLEGAL_ARGUMENT;
+  debug_stamps(out16, reset != 0);
+  return RBG_OK;
+}
 int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2) {
   Batch* b;
   CHK(get_batch(&ctx->c, batch, &b));

@@ -96,6 +96,33 @@ __device__ __forceinline__ int pairwise_kind(int op, int ka, int kb, int c) {
 
 constexpr int kWaves = 4;  // waves per workgroup
 
+// Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
+// pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
+// their own; no result depends on them.
+#if RBG_STAMPS
+__device__ unsigned long long g_stamp[16];
+// per-wave accumulators (registers); flushed once at the end of the kernel
+struct StampAcc {
+  uint64_t v[12];
+};
+#define STAMP_DECL uint64_t st_prev = __builtin_amdgcn_s_memtime();
+#define STAMP(ph)                                          \
+  do {                                                     \
+    const uint64_t st_now = __builtin_amdgcn_s_memtime();  \
+    sacc.v[ph] += st_now - st_prev;                        \
+    st_prev = st_now;                                      \
+  } while (0)
+#define SACC_PARAM , StampAcc& sacc
+#define SACC_ARG , sacc
+#else
+#define SACC_PARAM
+#define SACC_ARG
+#define STAMP_DECL
+#define STAMP(ph) \
+  do {            \
+  } while (0)
+#endif
+
 // Records one task's output.  Staged results (LDS) are copied to the task's
 // scratch slot (arena slot layout); results already in the slot or pass-through
 // containers are referenced in place.  k_place and the serializer follow.
@@ -131,26 +158,72 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
 template <int OP, int MODE>
 __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard, const uint8_t* pslot, int mkind,
                                             int mcard, const uint8_t* mslot, const OutCtx& oc, uint32_t* task_card,
-                                            uint32_t* lds) {
+                                            uint32_t* lds SACC_PARAM) {
+  STAMP_DECL
+  // the array's values are requested first, so their memory latency overlaps the
+  // map construction (one round trip per task instead of two)
+  const int l = lane_id();
+  const int nvec = (pcard + 7) >> 3;  // <= 512: 8 vectors per lane
+  const uint4* pv = reinterpret_cast<const uint4*>(pslot) + l;
+  uint4 v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) v[j] = (64 * j + l < nvec) ? pv[64 * j] : make_uint4(0, 0, 0, 0);
   w_map_lds(mkind, mcard, mslot, lds);
-  const uint16_t* pv = reinterpret_cast<const uint16_t*>(pslot);
+  STAMP(4);
+  uint32_t hit[8];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    hit[j] = 0;
+    if (512 * j < pcard) {  // wave-uniform
+      const int first = 8 * (64 * j + l);
+      const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
+        const uint32_t m = (lds[x >> 5] >> (x & 31)) & 1u;
+        hit[j] |= (((OP == OP_ANDNOT) ? (m ^ 1u) : m) & (first + i < pcard ? 1u : 0u)) << i;
+      }
+      cnt += __popc(hit[j]);
+    }
+  }
   if (MODE == 1) {
-    const int c = w_probe_array<false, false>(lds, pv, pcard, nullptr);
-    if (lane_id() == 0) task_card[t] = (uint32_t)c;
+    const int c = wave_sum_i(cnt);
+    STAMP(5);
+    if (l == 0) task_card[t] = (uint32_t)c;
     return;
   }
+  // the map is dead: compact the kept values over it, then 16 B stores
+  uint16_t* st = reinterpret_cast<uint16_t*>(lds);
+  wsync();
+  int base = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    if (512 * j >= pcard) break;  // wave-uniform
+    int tot;
+    int q = base + wave_excl(__popc(hit[j]), &tot);
+    const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+    for (int i = 0; i < 8; i++)
+      if ((hit[j] >> i) & 1u) st[q++] = (uint16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF);
+    base += tot;
+  }
+  const int c = (int)uni((uint32_t)base);
+  wsync();
   uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
-  uint16_t* out = reinterpret_cast<uint16_t*>(slot);
-  const int c = OP == OP_ANDNOT ? w_probe_array<true, true>(lds, pv, pcard, out)
-                                : w_probe_array<false, true>(lds, pv, pcard, out);
+  const uint4* sv = reinterpret_cast<const uint4*>(lds);
+  uint4* dv = reinterpret_cast<uint4*>(slot);
+  for (int k = l; k < (2 * c + 15) >> 4; k += 64) dv[k] = sv[k];  // the slot has room for the rounded tail
+  STAMP(5);
   // empty results are dropped (RB/RoaringBitmap.java:389,456)
   w_place(t, c > 0, slot, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, oc);
+  STAMP(6);
 }
 
 // Filter-class task (pass-through clone, or a filter), one wave, wave-uniform branches.
 template <int OP, int MODE>
 __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
+                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
   const int ka = tk.kind_a, kb = tk.kind_b;
   if (ka == kAbsent || kb == kAbsent) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
     if (MODE == 0) {
@@ -169,9 +242,9 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
   const uint8_t* sb = pb + tk.slot_b;
   // filter the array (A & A: the smaller one; A \ x: c1) through a map of the other operand
   if (ka == DK_A && (OP == OP_ANDNOT || kb != DK_A || ca <= cb))
-    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, oc, task_card, lds);
+    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, oc, task_card, lds SACC_ARG);
   else
-    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, oc, task_card, lds);
+    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, oc, task_card, lds SACC_ARG);
 }
 
 // Bitmap-class task: both operands in registers (16 words per lane), combined,
@@ -179,13 +252,25 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
 // staged in LDS).  One wave, wave-uniform branches.
 template <int OP, int MODE>
 __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
+                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
   const int l = lane_id();
   const int ka = tk.kind_a, kb = tk.kind_b;
   const int ca = (int)tk.card_a, cb = (int)tk.card_b;
+  STAMP_DECL
   WCtr x;
+#if RBG_BPRE
+  WPre xb;
+  const uint8_t* sb = pb + tk.slot_b;
+  if (kb == DK_B) w_prefetch(sb, 512, xb);
+#endif
   w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, (uint8_t)ka, 0}, pa, lds, x);
-  w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
+  STAMP(0);
+#if RBG_BPRE
+  if (kb == DK_B) w_combine_pre<OP>(DK_B, cb, 0, xb, sb, lds, x);
+  else
+#endif
+    w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
+  STAMP(1);
   const int c = w_card(x);
   if (MODE == 1) {
     if (l == 0) task_card[t] = (uint32_t)c;
@@ -197,6 +282,7 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
   }
   const bool use_eff = pairwise_needs_runs(OP, ka, ca, kb, cb);
   const int kind = use_eff ? eff(c, w_runs(x)) : pairwise_kind(OP, ka, kb, c);
+  STAMP(2);
   if (kind == DK_B) {
     uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
 #if RBG_EXP_NOSTORE
@@ -205,12 +291,15 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
     w_store_bitmap(slot, x);
 #endif
     w_place(t, true, slot, false, lds, 8192, (uint32_t)c, tk.key, DK_B, oc);
+    STAMP(3);
     return;
   }
   uint32_t len;
   if (kind == DK_A) len = w_stage(DK_A, x, c, lds);
   else len = 2u + 4u * (uint32_t)w_stage_runs(x, lds);
+  STAMP(7);
   w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, oc);
+  STAMP(8);
 }
 
 // 32 B task record through the scalar cache (wave-uniform address)
@@ -234,9 +323,11 @@ __device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
 // MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
 template <int OP, int MODE>
 __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                         const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
-  if (pair_class(OP, tk.kind_a, tk.kind_b) == 1) filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds);
-  else bitmap_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds);
+                                         const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+  if (pair_class(OP, tk.kind_a, tk.kind_b) == 1)
+    filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
+  else
+    bitmap_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
 }
 template <int OP, int MODE>
 __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
@@ -250,15 +341,31 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
   uint32_t t = uni(blockIdx.x * kWaves + w);
   if (t >= nt) return;
   PTask cur = load_task(tasks, t);
+#if RBG_STAMPS
+  StampAcc sacc = {};
+  const uint64_t t_kernel = __builtin_amdgcn_s_memtime();
+#endif
   for (;;) {
     const uint32_t tn = t + stride;
     PTask nxt;
     if (tn < nt) nxt = load_task(tasks, tn);  // in flight while this task runs
-    any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds);
+#if RBG_STAMPS
+    const uint64_t t_in = __builtin_amdgcn_s_memtime();
+    sacc.v[10] += 1;
+#endif
+    any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
+#if RBG_STAMPS
+    sacc.v[11] += __builtin_amdgcn_s_memtime() - t_in;
+#endif
     if (tn >= nt) break;
     t = tn;
     cur = nxt;
   }
+#if RBG_STAMPS
+  sacc.v[9] += __builtin_amdgcn_s_memtime() - t_kernel;
+  if (lane_id() == 0)
+    for (int i = 0; i < 12; i++) atomicAdd(&g_stamp[i], (unsigned long long)sacc.v[i]);
+#endif
 }
 
 template <int OP, int MODE>
@@ -268,6 +375,21 @@ static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_
   hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(std::max(1, std::min(grid, resident_grid(k)))), dim3(256), 0, s,
                      tasks, nt, pa, pb, oc, task_card);
 }
+
+#if RBG_STAMPS
+void debug_stamps(uint64_t* out16, bool reset) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamp), 16 * 8, 0, hipMemcpyDeviceToHost);
+  if (reset) {
+    unsigned long long z[16] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+}
+#else
+void debug_stamps(uint64_t* out16, bool) {
+  for (int i = 0; i < 16; i++) out16[i] = 0;
+}
+#endif
 
 void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const CDesc* da, const uint8_t* pa,
                           const uint16_t* kb, int nb, const CDesc* db, const uint8_t* pb, PTask* by_key,
