@@ -94,6 +94,21 @@ int rbg_wide_card(int op, const uint8_t* const* bufs, const size_t* lens, size_t
 int rbg_batch_and_card(size_t n_pairs, const uint8_t* const* a_bufs, const size_t* a_lens,
                        const uint8_t* const* b_bufs, const size_t* b_lens, int32_t* out);
 
+/* ---- bit-sliced index (bsi/src/main/java/org/roaringbitmap/bsi/RoaringBitmapSliceIndex.java) ----
+ * A BSI crosses the boundary as its fields: the serialized existence bitmap ebM, the
+ * serialized slices bA[0..nbits-1] (bit 0 first) and minValue / maxValue.
+ * op is BitmapSliceIndex.Operation's ordinal (BitmapSliceIndex.java:23-38). */
+enum { RBG_BSI_EQ = 0, RBG_BSI_NEQ = 1, RBG_BSI_LE = 2, RBG_BSI_LT = 3, RBG_BSI_GE = 4, RBG_BSI_GT = 5,
+       RBG_BSI_RANGE = 6 };
+/* compare(op, startOrValue, end, foundSet) -> RoaringBitmap (RoaringBitmapSliceIndex.java:482-513);
+ * found may be NULL (foundSet == null). */
+int rbg_bsi_compare(int op, int32_t start, int32_t end, const uint8_t* ebm, size_t ebm_len,
+                    const uint8_t* const* slices, const size_t* slice_lens, size_t nbits, int32_t min_value,
+                    int32_t max_value, const uint8_t* found, size_t found_len, rbg_buffer* out);
+/* sum(foundSet) -> Pair<Long, Long> (RoaringBitmapSliceIndex.java:581-592): out2 = {sum, count}. */
+int rbg_bsi_sum(const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* slice_lens,
+                size_t nbits, const uint8_t* found, size_t found_len, int64_t* out2);
+
 void rbg_free(rbg_buffer* buf);
 
 /* Select the HIP devices the one-shot calls may use (bit i = device i).  Returns the
@@ -175,6 +190,13 @@ int rbg_ctx_wide_start(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_
  * batch (array / bitmap payloads; synthetic C4 batches have no run containers):
  * out2[0] = matched payload + 4 B per descriptor, out2[1] = all of it. */
 int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2);
+/* BSI over a device-resident key-major batch [ebM, bA[0..nbits-1], foundSet if has_found]:
+ * op = RBG_BSI_* (compare; min/max decide compareUsingMinMax's shortcuts) or 8 = sum(foundSet)
+ * alone; want_sum fuses sum(result) into the compare pass.  The result is fetched like any
+ * other (rbg_ctx_fetch); rbg_ctx_bsi_sums returns {sum, count} of the last BSI call. */
+int rbg_ctx_bsi(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
+                int32_t min_value, int32_t max_value, int want_sum);
+int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2);
 /* Diagnostics: per-phase shader-clock totals of the pairwise kernel (all zero unless the
  * library was built with -DRBG_STAMPS=1); reset != 0 clears them. */
 int rbg_debug_stamps(uint64_t* out16, int reset);

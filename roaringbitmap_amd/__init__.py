@@ -9,6 +9,7 @@ from ._lib import (DeviceError, IllegalArgumentException, InvalidRoaringFormat, 
                    TruncatedInput)
 from .engine import Engine  # noqa: F401
 from .roaring import FastAggregation, RoaringBitmap, batch_and_cardinality  # noqa: F401
+from .bsi import RoaringBitmapSliceIndex  # noqa: F401
 
-__all__ = ["RoaringBitmap", "FastAggregation", "Engine", "batch_and_cardinality", "InvalidRoaringFormat",
+__all__ = ["RoaringBitmap", "FastAggregation", "RoaringBitmapSliceIndex", "Engine", "batch_and_cardinality", "InvalidRoaringFormat",
            "TruncatedInput", "IllegalArgumentException", "DeviceError", "RoaringError"]

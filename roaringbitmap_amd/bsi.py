@@ -1,0 +1,83 @@
+"""Host-side mirror of RoaringBitmapSliceIndex's query path.
+
+Mirrors bsi/src/main/java/org/roaringbitmap/bsi/RoaringBitmapSliceIndex.java (BSI/):
+compare(Operation, startOrValue, end, foundSet) (BSI/:482-513) and
+sum(foundSet) (BSI/:581-592). Both run as one fused MI355X pass per key over the
+slices (csrc/bsi.hip), and the results are the reference's bytes, container types
+included. Construction (setValue) is host-side.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import IllegalArgumentException, check, lib, take
+from .roaring import RoaringBitmap
+
+OPERATIONS = ("EQ", "NEQ", "LE", "LT", "GE", "GT", "RANGE")  # BitmapSliceIndex.Operation order
+
+
+class RoaringBitmapSliceIndex:
+    """ebM (existence bitmap), bA (slices, bit 0 first), minValue, maxValue (BSI/:16-38)."""
+
+    def __init__(self, ebm=None, slices=(), min_value=0, max_value=0):
+        self.ebM = ebm if ebm is not None else RoaringBitmap()
+        self.bA = list(slices)
+        self.minValue = int(min_value)
+        self.maxValue = int(max_value)
+
+    @classmethod
+    def from_columns(cls, columns, values, run_optimize=False):
+        """setValue(c, v) for each pair, in order (BSI/:320-347); runOptimize() if asked (BSI/:141-150)."""
+        columns = np.asarray(columns, dtype=np.int64)
+        values = np.asarray(values, dtype=np.int64)
+        if columns.shape != values.shape:
+            raise IllegalArgumentException("columns and values differ in length")
+        if (values < 0).any():
+            raise IllegalArgumentException("Values should be non-negative")
+        mn = mx = 0
+        if values.size:  # ensureCapacityInternal: first value sets both, then min or else max
+            mn = mx = int(values[0])
+            for v in values[1:]:
+                v = int(v)
+                if mn > v:
+                    mn = v
+                elif mx < v:
+                    mx = v
+        nbits = (len(bin(mx)) - 2) if values.size else 0
+        ebm = RoaringBitmap.from_values(columns, run_optimize)
+        ba = [RoaringBitmap.from_values(columns[(values >> i) & 1 == 1], run_optimize) for i in range(nbits)]
+        return cls(ebm, ba, mn, mx)
+
+    def bitCount(self):
+        return len(self.bA)
+
+    def getExistenceBitmap(self):
+        return self.ebM
+
+    def getLongCardinality(self):
+        return self.ebM.getLongCardinality()
+
+    def _slices(self):
+        bufs = [b.serialize() for b in self.bA]
+        return _lib.buf_array(bufs)
+
+    def compare(self, operation, startOrValue, end=0, foundSet=None):
+        """BSI/:482-513 -> RoaringBitmap"""
+        op = OPERATIONS.index(operation) if isinstance(operation, str) else int(operation)
+        arr, lens = self._slices()
+        e = self.ebM.serialize()
+        f = foundSet.serialize() if foundSet is not None else None
+        out = _lib.rbg_buffer()
+        check(lib().rbg_bsi_compare(op, int(startOrValue), int(end), e, len(e), arr, lens, len(self.bA),
+                                    self.minValue, self.maxValue, f, len(f) if f else 0, ctypes.byref(out)))
+        return RoaringBitmap(take(out))
+
+    def sum(self, foundSet):
+        """BSI/:581-592 -> (sum, count) as Java longs"""
+        arr, lens = self._slices()
+        e = self.ebM.serialize()
+        f = foundSet.serialize() if foundSet is not None else None
+        out = (ctypes.c_int64 * 2)()
+        check(lib().rbg_bsi_sum(e, len(e), arr, lens, len(self.bA), f, len(f) if f else 0, out))
+        return int(out[0]), int(out[1])

@@ -103,6 +103,8 @@ struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Batch>> batches;
+  DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
+  int bsi_nbits = 0;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw, items,
       scalar, scratch;
   size_t result_cap = 0;
@@ -552,6 +554,99 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     c->mark(3);
     HIPCHK(hipGetLastError());
   }
+  return RBG_OK;
+}
+
+// compareUsingMinMax (BSI/:515-579): 0 = run the circuit, 1 = all, 2 = empty
+static int bsi_minmax(int op, int32_t s, int32_t e, int32_t lo, int32_t hi) {
+  switch (op) {
+    case BSI_LT: return s > hi ? 1 : s <= lo ? 2 : 0;
+    case BSI_LE: return s >= hi ? 1 : s < lo ? 2 : 0;
+    case BSI_GT: return s < lo ? 1 : s >= hi ? 2 : 0;
+    case BSI_GE: return s <= lo ? 1 : s > hi ? 2 : 0;
+    case BSI_EQ:
+      if (lo == hi && lo == s) return 1;
+      return (s < lo || s > hi) ? 2 : 0;
+    case BSI_NEQ:
+      if (lo == hi) return lo == s ? 2 : 1;
+      return 0;
+    case BSI_RANGE:
+      if (s <= lo && e >= hi) return 1;
+      return (s > hi || e < lo) ? 2 : 0;
+    default: return 0;
+  }
+}
+
+// RoaringBitmapSliceIndex.compare (BSI/:482-513) and / or sum (BSI/:581-592) over a
+// key-major batch [ebM, bA[0..nbits-1], foundSet?]; the result is materialised like a
+// wide op's, the sums land in c->bsi_sums.
+static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t start, int32_t end,
+                   int32_t min_value, int32_t max_value, int want_sum) {
+  Batch* B;
+  CHK(get_batch(c, id, &B));
+  if (!B->key_major || nbits < 0 || nbits + 2 > kBsiMaxInputs || B->n_bm != (size_t)(1 + nbits + (has_found ? 1 : 0)) ||
+      op < 0 || op > BSI_SUM_ONLY || (op == BSI_SUM_ONLY && !has_found)) {
+    set_err("bsi: batch must hold ebM, nbits slices and the optional foundSet; bad op");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  hipStream_t s = c->stream;
+  CHK(c->bsi_sums.ensure(8 * (kBsiMaxInputs + 1)));
+  HIPCHK(hipMemsetAsync(c->bsi_sums.p, 0, 8 * (kBsiMaxInputs + 1), s));
+  c->bsi_nbits = nbits;
+  int mode = op;
+  if (op != BSI_SUM_ONLY) {
+    const int mm = bsi_minmax(op, start, end, min_value, max_value);
+    if (mm == 1) mode = BSI_ALL;
+    if (mm == 2) mode = -1;  // empty result
+  }
+  const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
+  OutCtx oc;
+  CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, op == BSI_SUM_ONLY));
+  const uint32_t need = mode == -1 ? 0xFFFFFFFFu : (op == BSI_SUM_ONLY ? (uint32_t)(nbits + 1) : 0u);
+  c->mark(0);
+  launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
+                  c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>());
+  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
+                 c->ntasks.as<uint32_t>());
+  c->mark(1);
+  WideArgs wa{};
+  wa.desc = B->desc.as<CDesc>();
+  wa.bm = B->bm.as<uint32_t>();
+  wa.payload = B->payload.as<uint8_t>();
+  BsiArgs p{mode < 0 ? BSI_EQ : mode, nbits, has_found, (uint32_t)start, (uint32_t)end};
+  launch_bsi(s, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, p, oc,
+             want_sum ? c->bsi_sums.as<unsigned long long>() : nullptr);
+  c->mark(2);
+  if (op == BSI_SUM_ONLY) {
+    c->last = 0;
+  } else {
+    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
+    c->last = 1;
+  }
+  c->mark(3);
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
+
+// (sum, count) as Java longs from the device totals: each slice's andCardinality is a
+// Java int (RB/RoaringBitmap.java:413-434), weighted by (long) (1 << x)
+static int ctx_bsi_sums(Ctx* c, int64_t* out2) {
+  unsigned long long h[kBsiMaxInputs + 1];
+  HIPCHK(hipMemcpyAsync(h, c->bsi_sums.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const uint64_t count = h[kBsiMaxInputs];
+  if (count == 0) {
+    out2[0] = out2[1] = 0;
+    return RBG_OK;
+  }
+  uint64_t sum = 0;
+  for (int x = 0; x < c->bsi_nbits; x++) {
+    const int64_t card = (int32_t)(uint32_t)h[x];
+    const int64_t w = (int64_t)(int32_t)(1u << x);
+    sum += (uint64_t)(w * card);
+  }
+  out2[0] = (int64_t)sum;
+  out2[1] = (int64_t)count;
   return RBG_OK;
 }
 
@@ -1116,6 +1211,60 @@ int rbg_synth_key_bytes(int kind, uint64_t seed, size_t n, uint64_t* out) {
     }
   }
   return RBG_OK;
+}
+int rbg_ctx_bsi(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
+                int32_t min_value, int32_t max_value, int want_sum) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_bsi(&ctx->c, batch, op, nbits, has_found, start, end, min_value, max_value, want_sum);
+}
+int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2) {
+  if (!out2) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_bsi_sums(&ctx->c, out2);
+}
+static int bsi_load(Ctx* c, const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* lens,
+                    size_t nbits, const uint8_t* found, size_t found_len, int32_t* id) {
+  if (!ebm || (nbits && (!slices || !lens)) || nbits + 2 > (size_t)kBsiMaxInputs) return RBG_ERR_ILLEGAL_ARGUMENT;
+  std::vector<const uint8_t*> bufs{ebm};
+  std::vector<size_t> ls{ebm_len};
+  for (size_t i = 0; i < nbits; i++) {
+    bufs.push_back(slices[i]);
+    ls.push_back(lens[i]);
+  }
+  if (found) {
+    bufs.push_back(found);
+    ls.push_back(found_len);
+  }
+  return ctx_load(c, bufs.data(), ls.data(), bufs.size(), id);
+}
+int rbg_bsi_compare(int op, int32_t start, int32_t end, const uint8_t* ebm, size_t ebm_len,
+                    const uint8_t* const* slices, const size_t* slice_lens, size_t nbits, int32_t min_value,
+                    int32_t max_value, const uint8_t* found, size_t found_len, rbg_buffer* out) {
+  if (!out || op < 0 || op > BSI_RANGE) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(bsi_load(c, ebm, ebm_len, slices, slice_lens, nbits, found, found_len, &id));
+  g.ids.push_back(id);
+  CHK(ctx_bsi(c, id, op, (int)nbits, found ? 1 : 0, start, end, min_value, max_value, 0));
+  return ctx_fetch(c, out);
+}
+int rbg_bsi_sum(const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* slice_lens,
+                size_t nbits, const uint8_t* found, size_t found_len, int64_t* out2) {
+  if (!out2) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!found) {  // BSI/:582: null foundSet -> (0, 0)
+    out2[0] = out2[1] = 0;
+    return RBG_OK;
+  }
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(bsi_load(c, ebm, ebm_len, slices, slice_lens, nbits, found, found_len, &id));
+  g.ids.push_back(id);
+  CHK(ctx_bsi(c, id, BSI_SUM_ONLY, (int)nbits, 1, 0, 0, 0, 0, 1));
+  return ctx_bsi_sums(c, out2);
 }
 int rbg_debug_stamps(uint64_t* out16, int reset) {
   if (!out16) return RBG_ERR_ILLEGAL_ARGUMENT;

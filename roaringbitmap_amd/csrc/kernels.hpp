@@ -34,6 +34,21 @@ struct WideArgs {
   uint32_t all_array;     // every container is an array (slots padded with their last value)
 };
 
+// bit-sliced index (bsi.hip); ops in the order of BitmapSliceIndex.Operation
+// (bsi/src/main/java/org/roaringbitmap/bsi/BitmapSliceIndex.java:23-38)
+// BSI_ALL: compareUsingMinMax's "all" (BSI/:516: ebM, or and(ebM, foundSet));
+// BSI_SUM_ONLY: sum(foundSet) alone
+enum BsiOp : int { BSI_EQ = 0, BSI_NEQ = 1, BSI_LE = 2, BSI_LT = 3, BSI_GE = 4, BSI_GT = 5, BSI_RANGE = 6,
+                   BSI_ALL = 7, BSI_SUM_ONLY = 8 };
+constexpr int kBsiMaxInputs = 34;  // ebM + up to 32 slices + foundSet
+struct BsiArgs {
+  int op;         // BsiOp
+  int nbits;      // slices
+  int has_found;  // input nbits+1 is the foundSet
+  uint32_t pred0;  // predicate (RANGE: start)
+  uint32_t pred1;  // RANGE: end
+};
+
 // Workgroups of `kernel` (256 threads) that are resident on the whole device at
 // once: CUs x occupancy.  Task kernels launch at most this many workgroups and
 // stride over their tasks, so no workgroup waits for a dispatch slot and no
@@ -66,6 +81,12 @@ void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, ui
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info);
 void launch_ingest(hipStream_t s, const uint8_t* raw, const IngestItem* items, uint64_t n, uint8_t* payload);
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload, unsigned long long* out);
+
+void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
+                     uint8_t* flag, uint32_t* wg_count);
+// sums: kBsiMaxInputs + 1 u64 (per-slice |bA[x] & found|, then the found count); null = no sum
+void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
+                unsigned long long* sums);
 
 // batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch
 void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const CDesc* desc,

@@ -69,31 +69,6 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint16_t* _
   plan_count(f, wg_count);
 }
 
-// Result container type of the static pairwise ops as a function of the operand
-// kinds and the result's cardinality c and run count r:
-//   AND   : R&R -> EFF(c,r) (RB/RunContainer.java:381-456); else BY_CARD(c)
-//   OR    : A|R, R|A, R|R -> EFF(c,r) (:1926-1986); A|A -> BY_CARD(c)
-//           (RB/ArrayContainer.java:949-963); B|x, x|B -> c==65536 ? R.full : B
-//           (RB/BitmapContainer.java:1064-1096, RB/RunContainer.java:1932-1949)
-//   XOR   : R^R -> EFF; R^A, A^R with |A| < 32 -> EFF (RB/RunContainer.java:2410-2424);
-//           else BY_CARD (RB/BitmapContainer.java:1372-1408)
-//   ANDNOT: R\R -> EFF (:637-692); R\A with |A| < 32 -> EFF (:574-591); else BY_CARD
-__device__ __forceinline__ bool pairwise_needs_runs(int op, int ka, int ca, int kb, int cb) {
-  switch (op) {
-    case OP_AND: return ka == DK_R && kb == DK_R;
-    case OP_OR: return (ka == DK_R && kb != DK_B) || (kb == DK_R && ka != DK_B);
-    case OP_XOR:
-      return (ka == DK_R && kb == DK_R) || (ka == DK_R && kb == DK_A && cb < 32) ||
-             (kb == DK_R && ka == DK_A && ca < 32);
-    default:  // ANDNOT
-      return ka == DK_R && (kb == DK_R || (kb == DK_A && cb < 32));
-  }
-}
-__device__ __forceinline__ int pairwise_kind(int op, int ka, int kb, int c) {
-  if (op == OP_OR && (ka == DK_B || kb == DK_B)) return c == 65536 ? DK_R : DK_B;
-  return by_card(c);
-}
-
 constexpr int kWaves = 4;  // waves per workgroup
 
 // Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the

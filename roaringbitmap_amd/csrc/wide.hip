@@ -11,41 +11,6 @@
 
 namespace rbg {
 
-// Workgroup-level output record: staged results go to the task's scratch slot.
-__device__ __forceinline__ void wg_place(uint32_t t, bool keep, const uint8_t* src, bool staged,
-                                         const uint32_t* stage, uint32_t len, uint32_t card, uint32_t key, int kind,
-                                         const OutCtx& oc, Prefix* shp) {
-  (void)shp;
-  uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
-  if (keep && staged) {
-    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
-    copy_lds_to_global<NT>(slot, stage, len, threadIdx.x);
-    srcaddr = reinterpret_cast<uint64_t>(slot);
-  }
-  if (threadIdx.x == 0) {
-    ORec r;
-    r.off = 0;
-    r.src = srcaddr;
-    r.idx = 0;
-    r.card = card;
-    r.ser_len = len;
-    r.key = (uint16_t)key;
-    r.kind = (uint8_t)kind;
-    r.keep = keep ? 1 : 0;
-    oc.recs[t] = r;
-  }
-  __syncthreads();
-}
-
-__device__ __forceinline__ void wg_passthrough(uint32_t t, const CDesc& d, const uint8_t* payload, const OutCtx& oc,
-                                               Prefix* shp) {
-  uint32_t len;
-  if (d.kind == DK_A) len = 2 * d.card;
-  else if (d.kind == DK_B) len = 8192;
-  else len = 2 + 4 * (uint32_t)(*reinterpret_cast<const uint16_t*>(payload + d.slot + 2));
-  wg_place(t, true, payload + d.slot + (d.kind == DK_R ? 2 : 0), false, nullptr, len, d.card, d.key, d.kind, oc, shp);
-}
-
 // Thread-serial OR/XOR of a small array container into LDS (16 B vector loads).
 template <int MODE>
 __device__ __forceinline__ void thread_scatter_array(uint32_t* lds, const uint16_t* vals, int card) {

@@ -1,0 +1,123 @@
+"""CPU ORACLE of the bit-sliced index query path (test infrastructure only).
+
+Restates bsi/src/main/java/org/roaringbitmap/bsi/RoaringBitmapSliceIndex.java
+(BSI/ below) on top of the container-exact oracle's pairwise ops (tests/_oracle.py),
+so every intermediate and final bitmap has the reference's container types:
+  compareUsingMinMax  BSI/:515-579     oNeilCompare  BSI/:432-468
+  compare             BSI/:482-513     sum           BSI/:581-592
+  construction        setValue / ensureCapacityInternal BSI/:320-347 (bitmapOf-typed slices)
+Bitmaps are portable serialized bytes.
+"""
+import numpy as np
+
+import _oracle as O
+
+EMPTY = bytes.fromhex("3a30000000000000")
+OPS = ("EQ", "NEQ", "LE", "LT", "GE", "GT", "RANGE")
+
+
+class BSI:
+    """ebM, bA (slice 0 = least significant bit), minValue, maxValue."""
+
+    def __init__(self, ebm, slices, min_value, max_value):
+        self.ebm, self.ba, self.min, self.max = ebm, list(slices), int(min_value), int(max_value)
+
+    @classmethod
+    def from_columns(cls, columns, values, run_optimize=False):
+        """setValue(c, v) for every (c, v): slices are set-equal to the bits of the values
+        and typed like bitmapOf (only adds, BSI/:320-331); min/max as ensureCapacityInternal
+        (BSI/:333-347, values set in the given order)."""
+        columns = np.asarray(columns, dtype=np.int64)
+        values = np.asarray(values, dtype=np.int64)
+        if (values < 0).any():
+            raise ValueError("Values should be non-negative")
+        mn = mx = 0
+        for i, v in enumerate(values):
+            v = int(v)
+            if i == 0:
+                mn = mx = v
+            elif mn > v:
+                mn = v
+            elif mx < v:
+                mx = v
+        nbits = len(bin(mx)) - 2 if len(values) else 0
+        ebm = O.from_values(columns, run_optimize)
+        ba = [O.from_values(columns[(values >> i) & 1 == 1], run_optimize) for i in range(nbits)]
+        return cls(ebm, ba, mn, mx)
+
+    def bit_count(self):
+        return len(self.ba)
+
+    # BSI/:432-468
+    def _oneil(self, op, predicate, found):
+        fixed = self.ebm if found is None else found
+        gt, lt, eq = EMPTY, EMPTY, self.ebm
+        for i in range(self.bit_count() - 1, -1, -1):
+            if (predicate >> i) & 1:
+                lt = O.pairwise("or", lt, O.pairwise("andnot", eq, self.ba[i]))
+                eq = O.pairwise("and", eq, self.ba[i])
+            else:
+                gt = O.pairwise("or", gt, O.pairwise("and", eq, self.ba[i]))
+                eq = O.pairwise("andnot", eq, self.ba[i])
+        eq = O.pairwise("and", fixed, eq)
+        if op == "EQ":
+            return eq
+        if op == "NEQ":
+            return O.pairwise("andnot", fixed, eq)
+        if op == "GT":
+            return O.pairwise("and", gt, fixed)
+        if op == "LT":
+            return O.pairwise("and", lt, fixed)
+        if op == "LE":
+            return O.pairwise("or", lt, eq)
+        if op == "GE":
+            return O.pairwise("or", gt, eq)
+        raise ValueError(op)
+
+    # BSI/:515-579 -> bytes, or None to run the circuit
+    def _minmax(self, op, start, end, found):
+        all_ = self.ebm if found is None else O.pairwise("and", self.ebm, found)
+        lo, hi = self.min, self.max
+        if op == "LT":
+            return all_ if start > hi else EMPTY if start <= lo else None
+        if op == "LE":
+            return all_ if start >= hi else EMPTY if start < lo else None
+        if op == "GT":
+            return all_ if start < lo else EMPTY if start >= hi else None
+        if op == "GE":
+            return all_ if start <= lo else EMPTY if start > hi else None
+        if op == "EQ":
+            if lo == hi and lo == start:
+                return all_
+            return EMPTY if (start < lo or start > hi) else None
+        if op == "NEQ":
+            if lo == hi:
+                return EMPTY if lo == start else all_
+            return None
+        if op == "RANGE":
+            if start <= lo and end >= hi:
+                return all_
+            return EMPTY if (start > hi or end < lo) else None
+        return None
+
+    # BSI/:482-513
+    def compare(self, op, start, end=0, found=None):
+        r = self._minmax(op, start, end, found)
+        if r is not None:
+            return r
+        if op == "RANGE":
+            left = self._oneil("GE", start, found)
+            right = self._oneil("LE", end, found)
+            return O.pairwise("and", left, right)
+        return self._oneil(op, start, found)
+
+    # BSI/:581-592 -> (sum, count) as Java longs
+    def sum(self, found):
+        if found is None or O.stats(found)["card"] == 0:
+            return 0, 0
+        count = O.stats(found)["card"]
+        s = 0
+        for x in range(self.bit_count()):
+            shift = np.int64(np.int32(np.uint32(1) << np.uint32(x)))  # (long) (1 << x), Java int shift
+            s += int(shift) * O.pairwise_card("and", self.ba[x], found)
+        return int(np.int64(np.uint64(s % (1 << 64)))), count
