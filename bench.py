@@ -145,6 +145,59 @@ def c4_batch_and_card(eng, n_pairs, rank, world, dist, steps, warmup, cdev):
             "all_bytes_per_rank": allb}
 
 
+def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
+    """C5: RoaringBitmapSliceIndex.compare(RANGE) + sum over `rows` rows (31 slices),
+    rows sharded by key range across the ranks (strong scaling); one step = the fused
+    compare + sum pass + the (sum, count) all-reduce."""
+    import torch
+    nkeys = (rows + 65535) // 65536
+    lo_k, hi_k = (nkeys * rank) // world, (nkeys * (rank + 1)) // world
+    b = eng.synth(4, 0xC5, rows, lo_k, hi_k)
+    st = eng.batch_stats(b)
+    mn, mx = eng.batch_minmax(b)
+    mm = torch.tensor([mn, -mx], dtype=torch.int64, device=cdev)
+    if dist is not None:
+        dist.all_reduce(mm, op=dist.ReduceOp.MIN)  # the BSI's min / max are global
+    mn, mx = int(mm[0]), -int(mm[1])
+    lo, hi = 1 << 29, 1 << 30
+
+    def step():
+        eng.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=True)
+        sc = eng.bsi_sums()
+        if dist is not None:
+            t = torch.tensor(sc, dtype=torch.int64, device=cdev)
+            dist.all_reduce(t)
+            sc = (int(t[0]), int(t[1]))
+        return sc
+
+    for _ in range(warmup):
+        sc = step()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sc = step()
+    eng.sync()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    ein = st["payload_bytes"] + 4 * st["containers"]
+    t = torch.tensor([wall, float(ein)], dtype=torch.float64, device=cdev)
+    if dist is not None:
+        tm = t.clone()
+        dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        t[0] = tm[0]
+    step_s = float(t[0]) / steps
+    eng.release(b)
+    # compare streams ebM + every slice once, sum re-reads the slices: about 2x the index bytes
+    return {"workload": f"C5: RoaringBitmapSliceIndex.compare(RANGE, 2^29, 2^30) + sum over {rows} rows x 31 slices, "
+                        f"key-range sharded over {world} GPU(s)",
+            "rows_per_s": round(rows / step_s, 1), "ms_per_step": round(step_s * 1e3, 4),
+            "index_bytes": int(t[1]), "input_GBps_2pass": round(2 * float(t[1]) / step_s / 1e9, 1),
+            "sum_count": list(sc), "min_max": [mn, mx]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -154,6 +207,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-n", type=int, default=10000, help="bitmaps of the C3 wide-OR workloads (0 = skip)")
     ap.add_argument("--c4-pairs", type=int, default=1000000, help="pairs of the C4 workload per GPU (0 = skip)")
+    ap.add_argument("--c5-rows", type=int, default=1000000000, help="rows of the C5 BSI workload (0 = skip)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo to rehearse "
                                                        "several ranks on one GPU)")
     args = ap.parse_args()
@@ -240,6 +294,8 @@ def main():
     if args.c4_pairs > 0:
         c3["c4_batch_and_card"] = c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, max(3, args.steps // 4), 1,
                                                     cdev)
+    if args.c5_rows > 0:
+        c3["c5_bsi_range_sum"] = c5_bsi(eng, args.c5_rows, rank, world, dist, max(3, args.steps // 4), 1, cdev)
 
     t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device=cdev)
     if dist is not None:

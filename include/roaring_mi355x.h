@@ -157,11 +157,15 @@ int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, s
  *   kind 0: C2 operand: one bitmap, all 65536 keys, per key A/B/R with p=1/3 (seed)
  *   kind 1: C3 uniform: n bitmaps x keys [key_lo,key_hi), ~15.26 values per (bitmap,key)
  *   kind 2: C3 clustered: n bitmaps, 16 dense bitmap keys each, restricted to [key_lo,key_hi)
+ *   kind 4: C5 bit-sliced index over n rows (value = hash & 0x7FFFFFFF, 31 slices) as the batch
+ *           [ebM, bA[0..30]] of rbg_ctx_bsi (runOptimize'd types); min / max: rbg_ctx_batch_minmax
  *   kind 3: C4 pairs: n pairs = 2n bitmaps, bitmap-major (pairs adjacent), 1-4 array keys in
  *           [0,64) each, card 16..512 (key_lo / key_hi ignored) */
 int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi,
                   int32_t* batch);
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch);
+/* min / max of the values of a synthetic C5 batch (out2). */
+int rbg_ctx_batch_minmax(rbg_ctx* ctx, int32_t batch, int32_t* out2);
 /* Batch facts: stats[0..7] = bitmaps, containers, #array, #bitmap, #run, payload bytes,
  * long cardinality, serialized bytes. (synchronous) */
 int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* stats8);

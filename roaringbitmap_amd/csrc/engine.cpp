@@ -97,6 +97,7 @@ struct Batch {
   int64_t ser_bytes = 0;
   int64_t long_card = 0;
   size_t max_ser = 0;  // Σ serialized payload of containers larger than 8194 B (long run inputs)
+  int32_t bsi_min = 0, bsi_max = 0;  // synthetic C5: min / max of the indexed values
 };
 
 struct Ctx {
@@ -1551,9 +1552,88 @@ static int synth_c4(Ctx* c, uint64_t seed, size_t n_pairs, int32_t* out_id) {
   return RBG_OK;
 }
 
+// C5: a bit-sliced index over rows 0..rows-1 with 31 slices, as the key-major batch
+// [ebM, bA[0..30]] of rbg_ctx_bsi; the value min / max go to b.bsi_min / bsi_max
+static int synth_c5(Ctx* c, uint64_t seed, size_t rows, int key_lo, int key_hi, int32_t* out_id) {
+  const int nbits = 31, nin = nbits + 1;
+  if (rows == 0 || rows > (1ull << 32)) return RBG_ERR_ILLEGAL_ARGUMENT;
+  key_lo = std::max(0, key_lo);
+  key_hi = (int)std::min<uint64_t>((uint64_t)std::min(key_hi, kMaxKeys), (rows + 65535) / 65536);
+  const int nkeys = std::max(0, key_hi - key_lo);
+  hipStream_t s = c->stream;
+  const size_t G = (size_t)nkeys * nin;
+  CHK(c->scratch.ensure(8 * G + 64));
+  uint32_t* cards = c->scratch.as<uint32_t>();
+  uint32_t* pos = cards + G;
+  unsigned int* mm = reinterpret_cast<unsigned int*>(c->scalar.p);
+  const unsigned int mm0[2] = {0xFFFFFFFFu, 0u};
+  HIPCHK(hipMemcpyAsync(mm, mm0, 8, hipMemcpyHostToDevice, s));
+  launch_synth_c5(s, seed, rows, key_lo, nbits, nkeys, 0, cards, nullptr, mm, nullptr, nullptr, nullptr, nullptr);
+  std::vector<uint32_t> h(G);
+  unsigned int mmh[2];
+  HIPCHK(hipMemcpyAsync(h.data(), cards, 4 * G, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(mmh, mm, 8, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<uint32_t> key_off(kMaxKeys + 1, 0), hp(G, 0);
+  uint32_t C = 0;
+  for (int k = 0; k < kMaxKeys; k++) {
+    const int j = k - key_lo;
+    if (j >= 0 && j < nkeys)
+      for (int i = 0; i < nin; i++)
+        if (h[(size_t)j * nin + i]) hp[(size_t)j * nin + i] = C++;
+    key_off[k + 1] = C;
+  }
+  const int32_t id = new_batch(c);
+  Batch& b = *c->batches[id];
+  b.n_bm = nin;
+  b.n_ctr = C;
+  b.key_major = true;
+  b.payload_bytes = (size_t)kSlotBytes * C;
+  b.h_bm_nctr.assign(nin, 0);
+  b.h_bm_card.assign(nin, 0);
+  for (int k = 0; k < nkeys; k++)
+    for (int i = 0; i < nin; i++)
+      if (h[(size_t)k * nin + i]) {
+        b.h_bm_nctr[i]++;
+        b.h_bm_card[i] += h[(size_t)k * nin + i];
+      }
+  for (int i = 0; i < nin; i++) b.long_card += b.h_bm_card[i];
+  CHK(b.keys.ensure(2 * (size_t)C + 16));
+  CHK(b.desc.ensure(sizeof(CDesc) * (size_t)C + 16));
+  CHK(b.bm.ensure(4 * (size_t)C + 16));
+  CHK(b.key_off.ensure(4 * (kMaxKeys + 1)));
+  CHK(b.bm_off.ensure(8));
+  CHK(b.payload.ensure(b.payload_bytes + 64));
+  HIPCHK(hipMemcpyAsync(b.key_off.p, key_off.data(), 4 * (kMaxKeys + 1), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(pos, hp.data(), 4 * G, hipMemcpyHostToDevice, s));
+  launch_synth_c5(s, seed, rows, key_lo, nbits, nkeys, 1, nullptr, pos, nullptr, b.desc.as<CDesc>(),
+                  b.keys.as<uint16_t>(),
+                  b.bm.as<uint32_t>(), b.payload.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  std::vector<CDesc> d(C);
+  if (C) HIPCHK(hipMemcpyAsync(d.data(), b.desc.p, sizeof(CDesc) * C, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  for (const CDesc& x : d) b.n_kind[x.kind]++;
+  b.bsi_min = (int32_t)mmh[0];
+  b.bsi_max = (int32_t)mmh[1];
+  b.live = true;
+  *out_id = id;
+  return RBG_OK;
+}
+
+int rbg_ctx_batch_minmax(rbg_ctx* ctx, int32_t batch, int32_t* out2) {
+  Batch* b;
+  CHK(get_batch(&ctx->c, batch, &b));
+  if (!out2) return RBG_ERR_ILLEGAL_ARGUMENT;
+  out2[0] = b->bsi_min;
+  out2[1] = b->bsi_max;
+  return RBG_OK;
+}
+
 int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi, int32_t* batch) {
   Ctx* c = &ctx->c;
   HIPCHK(hipSetDevice(c->device));
+  if (kind == 4) return synth_c5(c, seed, n, key_lo, key_hi, batch);
   if (kind == 1 || kind == 2) return synth_c3(c, kind, seed, n, key_lo, key_hi, batch);
   if (kind == 3) return synth_c4(c, seed, n, batch);
   // kind 0: C2 mix; 16 + DK_A/DK_B/DK_R: the same generator with one container family

@@ -102,6 +102,11 @@ void launch_synth_c3u(hipStream_t s, uint64_t seed, uint32_t n, int key_lo, int 
 void launch_synth_c3c(hipStream_t s, uint64_t seed, uint64_t n_ctr, const uint16_t* keys, const uint32_t* bm,
                       CDesc* desc, uint8_t* payload);
 void launch_sum_cards(hipStream_t s, const CDesc* desc, uint64_t n, unsigned long long* out);
+// C5 BSI rows 0..rows-1 (nbits slices): pass 0 cards[(key, input)] + minmax, pass 1 fills at pos[(key, input)]
+void launch_synth_c5(hipStream_t s, uint64_t seed, uint64_t rows, int key_lo, int nbits, int nkeys, int pass,
+                     uint32_t* cards,
+                     const uint32_t* pos, unsigned int* minmax, CDesc* desc, uint16_t* keys, uint32_t* bm,
+                     uint8_t* payload);
 // array payloads for host-built descriptors (C4 pairs)
 void launch_synth_arrays(hipStream_t s, uint64_t seed, const CDesc* desc, uint64_t n, uint8_t* payload);
 // force < 0: C2 mix (kind drawn per key); force = DK_A/DK_B/DK_R: every key drawn from that family

@@ -120,6 +120,110 @@ void launch_synth_arrays(hipStream_t s, uint64_t seed, const CDesc* desc, uint64
   hipLaunchKernelGGL(k_synth_arrays, dim3(g), dim3(256), 0, s, seed, desc, n, payload);
 }
 
+// ===========================================================================
+// C5 bit-sliced index over rows 0..rows-1: value(row) = hash & 0x7FFFFFFF, 31
+// slices; container (key, input) with input 0 = ebM, 1 + i = slice i.  Typed as
+// the reference's BSI after runOptimize (BSI/:141-150): ebM runs, slices by
+// RB/BitmapContainer.java:1218-1237 / RB/ArrayContainer.java:1085-1099.
+// pass 0: cardinality per (key, input) + value min / max; pass 1: payload + desc.
+// ===========================================================================
+__device__ __forceinline__ uint32_t c5_value(uint64_t seed, uint64_t row) {
+  return (uint32_t)(splitmix64(seed ^ (row * 0x9E3779B97F4A7C15ULL)) & 0x7FFFFFFFu);
+}
+
+__device__ __forceinline__ void c5_words(uint64_t seed, uint64_t rows, uint32_t key, int input, uint64_t r[4],
+                                         uint32_t* vmin, uint32_t* vmax) {
+  const uint32_t t = threadIdx.x;
+  const uint32_t widx[4] = {2 * t, 2 * t + 1, 512 + 2 * t, 513 + 2 * t};
+  uint32_t mn = 0xFFFFFFFFu, mx = 0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint64_t w = 0;
+    const uint64_t base = (uint64_t)key * 65536 + 64ull * widx[q];
+    for (int b = 0; b < 64; b++) {
+      const uint64_t row = base + b;
+      if (row >= rows) break;
+      if (input == 0) {
+        w |= 1ull << b;
+        if (vmin) {
+          const uint32_t v = c5_value(seed, row);
+          mn = min(mn, v);
+          mx = max(mx, v);
+        }
+      } else {
+        w |= (uint64_t)((c5_value(seed, row) >> (input - 1)) & 1u) << b;
+      }
+    }
+    r[q] = w;
+  }
+  if (vmin) {
+    *vmin = mn;
+    *vmax = mx;
+  }
+}
+
+__device__ __forceinline__ int c5_kind(int input, int card, int nruns) {
+  (void)input;  // ebM and slices alike: built by add(), then runOptimize
+  if (card <= 4096) return 2 * card > 2 + 4 * nruns ? DK_R : DK_A;  // ArrayContainer.runOptimize (strict >)
+  return 2 + 4 * nruns < 8192 ? DK_R : DK_B;                         // BitmapContainer.runOptimize
+}
+
+__global__ __launch_bounds__(256) void k_synth_c5(uint64_t seed, uint64_t rows, int key_lo, int nbits, int pass,
+                                                  uint32_t* __restrict__ cards, const uint32_t* __restrict__ pos,
+                                                  unsigned int* __restrict__ minmax, CDesc* __restrict__ desc,
+                                                  uint16_t* __restrict__ keys, uint32_t* __restrict__ bm,
+                                                  uint8_t* __restrict__ payload) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int sh[8];
+  const int nin = nbits + 1;
+  const uint32_t key = key_lo + blockIdx.x / nin;
+  const int input = (int)(blockIdx.x % nin);
+  uint64_t r[4];
+  uint32_t mn, mx;
+  const bool mm = pass == 0 && input == 0;
+  c5_words(seed, rows, key, input, r, mm ? &mn : nullptr, &mx);
+  int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
+  int u = 0;
+  block_sum2(c, u, sh);
+  if (pass == 0) {
+    if (threadIdx.x == 0) cards[blockIdx.x] = (uint32_t)c;
+    if (mm) {
+      // workgroup min / max, one atomic each
+      for (int o = 32; o > 0; o >>= 1) {
+        mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+      }
+      if ((threadIdx.x & 63) == 0) {
+        atomicMin(&minmax[0], mn);
+        atomicMax(&minmax[1], mx);
+      }
+    }
+    return;
+  }
+  if (c == 0) return;  // empty containers are not stored
+  const int kind = c5_kind(input, c, count_runs(r, acc, sh));
+  const uint32_t p = pos[blockIdx.x];
+  uint8_t* slot = payload + (uint64_t)p * kSlotBytes;
+  const uint32_t len = stage_container(kind, r, c, acc, tmp, sh);
+  copy_lds_to_global<NT>(slot + (kind == DK_R ? 2 : 0), tmp, len, threadIdx.x);
+  if (threadIdx.x == 0) {
+    desc[p] = CDesc{(uint64_t)p * kSlotBytes, (uint32_t)c, (uint16_t)key, (uint8_t)kind, 0};
+    keys[p] = (uint16_t)key;
+    bm[p] = (uint32_t)input;
+  }
+}
+
+void launch_synth_c5(hipStream_t s, uint64_t seed, uint64_t rows, int key_lo, int nbits, int nkeys, int pass,
+                     uint32_t* cards,
+                     const uint32_t* pos, unsigned int* minmax, CDesc* desc, uint16_t* keys, uint32_t* bm,
+                     uint8_t* payload) {
+  const unsigned g = (unsigned)(nkeys * (nbits + 1));
+  if (g == 0) return;
+  hipLaunchKernelGGL(k_synth_c5, dim3(g), dim3(256), 0, s, seed, rows, key_lo, nbits, pass, cards, pos, minmax, desc,
+                     keys, bm, payload);
+}
+
 // total cardinality of a batch (64-bit)
 __global__ __launch_bounds__(256) void k_sum_cards(const CDesc* __restrict__ desc, uint64_t n,
                                                    unsigned long long* __restrict__ out) {

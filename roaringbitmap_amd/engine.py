@@ -11,7 +11,7 @@ from . import _lib
 from ._lib import check, lib, take
 from .roaring import RoaringBitmap
 
-SYNTH_C2, SYNTH_C3_UNIFORM, SYNTH_C3_CLUSTERED, SYNTH_C4_PAIRS = 0, 1, 2, 3
+SYNTH_C2, SYNTH_C3_UNIFORM, SYNTH_C3_CLUSTERED, SYNTH_C4_PAIRS, SYNTH_C5_BSI = 0, 1, 2, 3, 4
 
 
 def synth_key_bytes(kind, seed, n) -> np.ndarray:
@@ -110,6 +110,24 @@ class Engine:
         """(matched payload + descriptors, all payload + descriptors) of a batch of pairs (C4)."""
         out = (ctypes.c_int64 * 2)()
         check(lib().rbg_ctx_pair_bytes(self._ctx, int(batch), out))
+        return int(out[0]), int(out[1])
+
+    def batch_minmax(self, batch):
+        out = (ctypes.c_int32 * 2)()
+        check(lib().rbg_ctx_batch_minmax(self._ctx, int(batch), out))
+        return int(out[0]), int(out[1])
+
+    def bsi(self, batch, op, nbits, start, end=0, min_value=0, max_value=0, has_found=False, want_sum=False):
+        """RoaringBitmapSliceIndex.compare (op in BitmapSliceIndex.Operation order; 8 = sum alone) over a
+        key-major batch [ebM, bA[0..nbits-1], foundSet?]; want_sum fuses sum(result)."""
+        from .bsi import OPERATIONS
+        code = OPERATIONS.index(op) if isinstance(op, str) else int(op)
+        check(lib().rbg_ctx_bsi(self._ctx, int(batch), code, int(nbits), int(bool(has_found)), int(start), int(end),
+                                int(min_value), int(max_value), int(bool(want_sum))))
+
+    def bsi_sums(self):
+        out = (ctypes.c_int64 * 2)()
+        check(lib().rbg_ctx_bsi_sums(self._ctx, out))
         return int(out[0]), int(out[1])
 
     def batch_counts(self, batch) -> np.ndarray:

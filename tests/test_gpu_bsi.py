@@ -77,3 +77,34 @@ def test_single_value_and_empty(gpu):
     g, o = _pair([0, 1, 2], [0, 0, 1])
     _check(g, o, "EQ", 0, 0)
     _check(g, o, "EQ", 1, 0)
+
+
+def _splitmix(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15))
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def test_c5_synthetic_bsi(gpu):
+    """C5 generator (csrc/synth.hip) + fused compare(RANGE) + sum, against the oracle on the same bitmaps."""
+    from roaringbitmap_amd import Engine
+    rows, seed = 200_000, 0xC5
+    e = Engine(0)
+    b = e.synth(4, seed, rows)
+    mn, mx = e.batch_minmax(b)
+    with np.errstate(over="ignore"):
+        r = np.arange(rows, dtype=np.uint64)
+        v = (_splitmix(np.uint64(seed) ^ (r * np.uint64(0x9E3779B97F4A7C15))) & np.uint64(0x7FFFFFFF)).astype(np.int64)
+    assert (mn, mx) == (int(v.min()), int(v.max()))
+    bms = [e.batch_fetch(b, i).serialize() for i in range(32)]
+    assert list(O.to_values(bms[0])) == list(range(rows))
+    assert list(O.to_values(bms[5])) == np.nonzero((v >> 4) & 1)[0].tolist()  # slice 4
+    assert O.run_optimize(bms[7]) == bms[7]  # runOptimize'd types
+    o = _bsi.BSI(bms[0], bms[1:], mn, mx)
+    lo, hi = 1 << 29, 1 << 30
+    e.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=True)
+    exp = o.compare("RANGE", lo, hi)
+    assert e.fetch().serialize() == exp
+    assert e.bsi_sums() == o.sum(exp)
+    assert o.sum(exp)[0] == int(v[(v >= lo) & (v <= hi)].sum())
