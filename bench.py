@@ -342,7 +342,7 @@ def main():
                        "per_rank": "one independent C2 pair per GPU", "parallelism": f"dp{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(),
-                         "kernel": "k_pairwise<AND> (container compute)",
+                         "kernel": "k_pair_wave<AND> (container compute)",
                          "bytes_per_launch": int(in_bytes + out_bytes)},
             "cpu_baseline": cpu,
             "extra": {
