@@ -122,7 +122,8 @@ __device__ __forceinline__ void oneil_finish(int op, const VB& fixed, const VB& 
 
 __global__ __launch_bounds__(256) void k_plan_bsi(const uint32_t* __restrict__ key_off, const uint32_t* __restrict__ bm,
                                                   uint32_t need, Task* __restrict__ by_key, uint8_t* __restrict__ flag,
-                                                  uint32_t* __restrict__ wg_count) {
+                                                  uint32_t* __restrict__ wg_count, uint64_t* zlb, uint64_t* ztile) {
+  plan_zero(zlb, ztile);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t s = key_off[k], n = key_off[k + 1] - s;
   // a key yields a result only where input `need` (ebM, or foundSet for sum alone) has a container
@@ -223,8 +224,8 @@ __global__ __launch_bounds__(256) void k_bsi(const Task* __restrict__ tasks, con
 }
 
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
-                     uint8_t* flag, uint32_t* wg_count) {
-  hipLaunchKernelGGL(k_plan_bsi, dim3(256), dim3(256), 0, s, key_off, bm, need, by_key, flag, wg_count);
+                     uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile) {
+  hipLaunchKernelGGL(k_plan_bsi, dim3(256), dim3(256), 0, s, key_off, bm, need, by_key, flag, wg_count, zlb, ztile);
 }
 
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,

@@ -104,6 +104,8 @@ struct Ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Batch>> batches;
+  uint64_t* zlb = nullptr;    // look-back state the next plan kernel zeroes (null: none)
+  uint64_t* ztile = nullptr;
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
   int bsi_nbits = 0;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw, items,
@@ -349,13 +351,15 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   oc->recs = c->recs.as<ORec>();
   c->serialized = false;
   c->pending_ub = 0;
+  c->zlb = c->ztile = nullptr;
   if (card_only) return RBG_OK;
   const uint64_t P0 = header_reserve(max_tasks);
   CHK(c->result.ensure(P0 + max_payload + 64));
   c->result_cap = P0 + max_payload;
   CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1) + 64));
-  HIPCHK(hipMemsetAsync(lb, 0, kLbHeader, c->stream));
-  HIPCHK(hipMemsetAsync(lb + kLbHeader + 8 * kMaxKeys, 0, 8 * kMaxTiles, c->stream));
+  // the look-back header and tile statuses are zeroed by the op's plan kernel
+  c->zlb = reinterpret_cast<uint64_t*>(lb);
+  c->ztile = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * kMaxKeys);
   oc->out = c->result.as<uint8_t>();
   oc->payload_base = P0;
   oc->scratch = c->scratch.as<uint8_t>();
@@ -386,8 +390,8 @@ static int operand(Batch* b, size_t i, const uint16_t** keys, const CDesc** desc
     set_err("bitmap index out of range");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
-  if (b->n_bm != 1) {
-    set_err("pairwise operands must be single-bitmap batches");
+  if (b->n_bm != 1 || !b->key_major) {
+    set_err("pairwise operands must be single-bitmap key-major batches");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   *keys = b->keys.as<uint16_t>();
@@ -418,9 +422,9 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only));
   c->mark(0);
   dbg(s, "memset");
-  launch_plan_pairwise(s, plan_op, ka, na, da, A->payload.as<uint8_t>(), kb, nb, db, B->payload.as<uint8_t>(),
-                       c->by_key.as<PTask>(), c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(),
-                       c->tasks.as<PTask>(), c->ntasks.as<uint32_t>());
+  launch_plan_pairwise(s, plan_op, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), B->key_off.as<uint32_t>(),
+                       db, B->payload.as<uint8_t>(), c->by_key.as<PTask>(), c->flag.as<uint8_t>(),
+                       c->wg_count.as<uint32_t>(), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), c->zlb, c->ztile);
   dbg(s, "compact");
   c->mark(1);
   const int grid = grid_for((ub + 3) / 4, 16384);  // 4 waves (tasks) per workgroup, clamped to the resident grid
@@ -531,7 +535,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     const uint32_t n_req = plan_mode == 2 ? 0xFFFFFFFFu : (uint32_t)N;
     c->mark(0);
     launch_plan_wide(s, plan_mode == 0 ? 0 : 1, B->key_off.as<uint32_t>(), n_req, key_lo, key_hi,
-                     c->by_key.as<Task>(), c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>());
+                     c->by_key.as<Task>(), c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile);
     launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
                    c->ntasks.as<uint32_t>());
     WideArgs wa;
@@ -606,7 +610,7 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
   const uint32_t need = mode == -1 ? 0xFFFFFFFFu : (op == BSI_SUM_ONLY ? (uint32_t)(nbits + 1) : 0u);
   c->mark(0);
   launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
-                  c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>());
+                  c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile);
   launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
                  c->ntasks.as<uint32_t>());
   c->mark(1);
@@ -875,7 +879,7 @@ static int ctx_load_bitmap_major(Ctx* c, const uint8_t* const* bufs, const size_
   const int32_t id = new_batch(c);
   Batch& b = *c->batches[id];
   b.n_bm = n;
-  b.key_major = n <= 1;
+  b.key_major = false;  // no key CSR: not usable as a pairwise operand or wide input
   b.h_bm_off.assign(n + 1, 0);
   b.h_bm_nctr.resize(n);
   b.h_bm_card.resize(n);

@@ -27,7 +27,9 @@ namespace rbg {
 // mode 0: n_k > 0 (or / xor / orCardinality); mode 1: n_k == n_req (and).
 __global__ __launch_bounds__(256) void k_plan_wide(int mode, const uint32_t* __restrict__ key_off, uint32_t n_req,
                                                    int key_lo, int key_hi, Task* __restrict__ by_key,
-                                                   uint8_t* __restrict__ flag, uint32_t* __restrict__ wg_count) {
+                                                   uint8_t* __restrict__ flag, uint32_t* __restrict__ wg_count,
+                                                   uint64_t* zlb, uint64_t* ztile) {
+  plan_zero(zlb, ztile);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t s = key_off[k], n = key_off[k + 1] - s;
   int f = (mode == 0) ? (n > 0) : (n == n_req && n > 0);
@@ -382,9 +384,9 @@ int resident_grid(const void* kernel) {
 
 static inline int clamp_grid(int grid, const void* kernel) { return std::max(1, std::min(grid, resident_grid(kernel))); }
 void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,
-                      Task* by_key, uint8_t* flag, uint32_t* wg_count) {
+                      Task* by_key, uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile) {
   hipLaunchKernelGGL(k_plan_wide, dim3(256), dim3(256), 0, s, mode, key_off, n_req, key_lo, key_hi, by_key, flag,
-                     wg_count);
+                     wg_count, zlb, ztile);
 }
 void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
                     uint32_t* n_tasks) {

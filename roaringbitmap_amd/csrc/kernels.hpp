@@ -55,15 +55,16 @@ struct BsiArgs {
 // wave pays a launch per task (cached per kernel).
 int resident_grid(const void* kernel);
 
+// plan kernels also zero the op's look-back header (zlb, 32 u64) and tile statuses (ztile, 128 u64)
 void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,
-                      Task* by_key, uint8_t* flag, uint32_t* wg_count);
+                      Task* by_key, uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile);
 void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
                     uint32_t* n_tasks);
 // pairwise.hip: plan (key alignment + descriptor resolution) and the wave-per-key compute
 // plan + compact: tasks[] in key order, *n_tasks
-void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const CDesc* da, const uint8_t* pa,
-                          const uint16_t* kb, int nb, const CDesc* db, const uint8_t* pb, PTask* by_key,
-                          uint8_t* flag, uint32_t* wg_count, PTask* tasks, uint32_t* n_tasks);
+void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
+                          const uint32_t* kob, const CDesc* db, const uint8_t* pb, PTask* by_key, uint8_t* flag,
+                          uint32_t* wg_count, PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile);
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
                      const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card);
 // diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
@@ -83,7 +84,7 @@ void launch_ingest(hipStream_t s, const uint8_t* raw, const IngestItem* items, u
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload, unsigned long long* out);
 
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
-                     uint8_t* flag, uint32_t* wg_count);
+                     uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile);
 // sums: kBsiMaxInputs + 1 u64 (per-slice |bA[x] & found|, then the found count); null = no sum
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
                 unsigned long long* sums);

@@ -2,9 +2,10 @@
 // andNot :444, andCardinality :413) on the MI355X.  RB/ = reference
 // RoaringBitmap/src/main/java/org/roaringbitmap/.
 //
-//   k_plan_pairwise : one thread per key: key alignment of the two sorted key
-//                     arrays (the advanceUntil walks) and resolution of both
-//                     operands' descriptors into a 32 B task record
+//   k_plan_pairwise : one thread per key: key alignment of the two operands
+//                     (the advanceUntil walks, here O(1) lookups in each batch's
+//                     key CSR) and resolution of both operands' descriptors into
+//                     a 32 B task record
 //   k_compact       : dense task list (kernels.hip)
 //   k_pair_wave     : one wavefront per task over a resident grid; the next
 //                     task's record is fetched with scalar loads while the
@@ -17,11 +18,11 @@
 
 namespace rbg {
 
-__device__ __forceinline__ void resolve(const uint16_t* keys, int n, const CDesc* desc, const uint8_t* payload,
-                                        uint32_t k, uint64_t& slot, uint32_t& card, uint8_t& kind,
-                                        uint16_t& nruns) {
-  const int p = lower_bound_u16(keys, n, k);
-  if (p < n && keys[p] == k) {
+// Descriptor of key k in a single-bitmap batch through its key CSR (O(1), no search)
+__device__ __forceinline__ void resolve(const uint32_t* key_off, const CDesc* desc, const uint8_t* payload, uint32_t k,
+                                        uint64_t& slot, uint32_t& card, uint8_t& kind, uint16_t& nruns) {
+  const uint32_t p = key_off[k];
+  if (key_off[k + 1] > p) {
     const CDesc d = desc[p];
     slot = d.slot;
     card = d.card;
@@ -45,16 +46,17 @@ __device__ __forceinline__ int pair_class(int op, int ka, int kb) {
 }
 
 // RB/RoaringBitmap.java:382-400 (and), :864-896 (or), :1076-1113 (xor), :449-471 (andNot)
-__global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint16_t* __restrict__ ka, int na,
+__global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* __restrict__ koa,
                                                        const CDesc* __restrict__ da, const uint8_t* __restrict__ pa,
-                                                       const uint16_t* __restrict__ kb, int nb,
+                                                       const uint32_t* __restrict__ kob,
                                                        const CDesc* __restrict__ db, const uint8_t* __restrict__ pb,
                                                        PTask* __restrict__ by_key, uint8_t* __restrict__ flag,
-                                                       uint32_t* __restrict__ wg_count) {
+                                                       uint32_t* __restrict__ wg_count, uint64_t* zlb, uint64_t* ztile) {
+  plan_zero(zlb, ztile);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   PTask t;
-  resolve(ka, na, da, pa, k, t.slot_a, t.card_a, t.kind_a, t.nruns_a);
-  resolve(kb, nb, db, pb, k, t.slot_b, t.card_b, t.kind_b, t.nruns_b);
+  resolve(koa, da, pa, k, t.slot_a, t.card_a, t.kind_a, t.nruns_a);
+  resolve(kob, db, pb, k, t.slot_b, t.card_b, t.kind_b, t.nruns_b);
   t.key = (uint16_t)k;
   const bool ia = t.kind_a != kAbsent, ib = t.kind_b != kAbsent;
   int f;
@@ -366,11 +368,11 @@ void debug_stamps(uint64_t* out16, bool) {
 }
 #endif
 
-void launch_plan_pairwise(hipStream_t s, int op, const uint16_t* ka, int na, const CDesc* da, const uint8_t* pa,
-                          const uint16_t* kb, int nb, const CDesc* db, const uint8_t* pb, PTask* by_key,
-                          uint8_t* flag, uint32_t* wg_count, PTask* tasks, uint32_t* n_tasks) {
-  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, ka, na, da, pa, kb, nb, db, pb, by_key, flag,
-                     wg_count);
+void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
+                          const uint32_t* kob, const CDesc* db, const uint8_t* pb, PTask* by_key, uint8_t* flag,
+                          uint32_t* wg_count, PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile) {
+  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, koa, da, pa, kob, db, pb, by_key, flag, wg_count,
+                     zlb, ztile);
   launch_compact(s, flag, by_key, wg_count, tasks, n_tasks);
 }
 

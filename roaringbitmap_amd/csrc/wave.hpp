@@ -375,6 +375,14 @@ __device__ __forceinline__ int lower_bound_u16(const uint16_t* keys, int n, uint
   return lo;
 }
 
+// Zeroes the output look-back state of the op about to run (block 0 of a plan
+// kernel; saves two memset launches per op).  Either pointer may be null.
+__device__ __forceinline__ void plan_zero(uint64_t* lb_header, uint64_t* tile_status) {
+  if (blockIdx.x != 0) return;
+  if (lb_header && threadIdx.x < 32) lb_header[threadIdx.x] = 0;
+  if (tile_status && threadIdx.x < 128) tile_status[threadIdx.x] = 0;
+}
+
 __device__ __forceinline__ void plan_count(int f, uint32_t* wg_count) {
   __shared__ int wc[4];
   const uint64_t m = __ballot(f);
