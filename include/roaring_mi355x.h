@@ -201,9 +201,9 @@ int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2);
 int rbg_ctx_bsi(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
                 int32_t min_value, int32_t max_value, int want_sum);
 int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2);
-/* Diagnostics: per-phase shader-clock totals of the pairwise kernel (all zero unless the
+/* Diagnostics: 20 per-phase shader-clock totals of the pairwise kernel (all zero unless the
  * library was built with -DRBG_STAMPS=1); reset != 0 clears them. */
-int rbg_debug_stamps(uint64_t* out16, int reset);
+int rbg_debug_stamps(uint64_t* out20, int reset);
 /* Containers per input bitmap of a batch (out has n == bitmaps entries). */
 int rbg_ctx_batch_counts(rbg_ctx* ctx, int32_t batch, uint32_t* out, size_t n);
 /* Algorithmic input bytes per key (payload + 4 B descriptor per container) of the

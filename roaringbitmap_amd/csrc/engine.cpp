@@ -1271,9 +1271,9 @@ int rbg_bsi_sum(const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices
   CHK(ctx_bsi(c, id, BSI_SUM_ONLY, (int)nbits, 1, 0, 0, 0, 0, 1));
   return ctx_bsi_sums(c, out2);
 }
-int rbg_debug_stamps(uint64_t* out16, int reset) {
-  if (!out16) return RBG_ERR_ILLEGAL_ARGUMENT;
-  debug_stamps(out16, reset != 0);
+int rbg_debug_stamps(uint64_t* out20, int reset) {
+  if (!out20) return RBG_ERR_ILLEGAL_ARGUMENT;
+  debug_stamps(out20, reset != 0);
   return RBG_OK;
 }
 int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2) {

@@ -68,7 +68,7 @@ void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDes
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
                      const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card);
 // diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
-void debug_stamps(uint64_t* out16, bool reset);
+void debug_stamps(uint64_t* out20, bool reset);
 void launch_compact(hipStream_t s, const uint8_t* flag, const PTask* by_key, const uint32_t* wg_count, PTask* tasks,
                     uint32_t* n_tasks);
 void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,

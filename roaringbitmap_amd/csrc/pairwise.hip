@@ -12,6 +12,8 @@
 //                     current one runs, and both operand payloads are requested
 //                     before either is consumed
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 #include "kernels.hpp"
 #include "wave.hpp"
@@ -77,7 +79,8 @@ constexpr int kWaves = 4;  // waves per workgroup
 // pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
 // their own; no result depends on them.
 #if RBG_STAMPS
-__device__ unsigned long long g_stamp[16];
+__device__ unsigned long long g_stamp[20];
+__device__ uint4 g_wave[16384];  // per wave: start, end (realtime), XCC_ID, HW_ID
 // per-wave accumulators (registers); flushed once at the end of the kernel
 struct StampAcc {
   uint64_t v[12];
@@ -321,6 +324,7 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 #if RBG_STAMPS
   StampAcc sacc = {};
   const uint64_t t_kernel = __builtin_amdgcn_s_memtime();
+  const uint64_t r_kernel = __builtin_amdgcn_s_memrealtime();
 #endif
   for (;;) {
     const uint32_t tn = t + stride;
@@ -339,9 +343,23 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
     cur = nxt;
   }
 #if RBG_STAMPS
-  sacc.v[9] += __builtin_amdgcn_s_memtime() - t_kernel;
-  if (lane_id() == 0)
+  const uint64_t life = __builtin_amdgcn_s_memtime() - t_kernel;
+  sacc.v[9] += life;
+  if (lane_id() == 0) {
     for (int i = 0; i < 12; i++) atomicAdd(&g_stamp[i], (unsigned long long)sacc.v[i]);
+    atomicMax(&g_stamp[12], (unsigned long long)life);  // longest wave
+    atomicAdd(&g_stamp[13], 1ull);                      // waves
+    const uint64_t r_end = __builtin_amdgcn_s_memrealtime();
+    atomicMax(&g_stamp[14], ~(unsigned long long)r_kernel);  // earliest wave start (complemented)
+    atomicMax(&g_stamp[15], (unsigned long long)r_end);     // latest wave end
+    atomicAdd(&g_stamp[16], (unsigned long long)(r_end - r_kernel));
+    atomicMax(&g_stamp[17], (unsigned long long)r_kernel);  // latest wave start
+    uint32_t xcc, hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    const uint32_t wid = blockIdx.x * kWaves + (threadIdx.x >> 6);
+    if (wid < 16384) g_wave[wid] = make_uint4((uint32_t)r_kernel, (uint32_t)r_end, xcc, hw);
+  }
 #endif
 }
 
@@ -349,22 +367,34 @@ template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
                       const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
   const void* k = (const void*)&k_pair_wave<OP, MODE>;
-  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(std::max(1, std::min(grid, resident_grid(k)))), dim3(256), 0, s,
+#ifndef RBG_GRID_MULT
+#define RBG_GRID_MULT 1
+#endif
+  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(std::max(1, std::min(grid, RBG_GRID_MULT * resident_grid(k)))),
+                     dim3(256), 0, s,
                      tasks, nt, pa, pb, oc, task_card);
 }
 
 #if RBG_STAMPS
-void debug_stamps(uint64_t* out16, bool reset) {
+void debug_stamps(uint64_t* out20, bool reset) {
   (void)hipDeviceSynchronize();
-  (void)hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_stamp), 16 * 8, 0, hipMemcpyDeviceToHost);
+  (void)hipMemcpyFromSymbol(out20, HIP_SYMBOL(g_stamp), 20 * 8, 0, hipMemcpyDeviceToHost);
+  if (const char* f = getenv("RBG_WAVE_DUMP")) {
+    static uint4 h[16384];
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_wave), sizeof(h), 0, hipMemcpyDeviceToHost);
+    if (FILE* fp = fopen(f, "ab")) {
+      fwrite(h, sizeof(h), 1, fp);
+      fclose(fp);
+    }
+  }
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[20] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z), 0, hipMemcpyHostToDevice);
   }
 }
 #else
-void debug_stamps(uint64_t* out16, bool) {
-  for (int i = 0; i < 16; i++) out16[i] = 0;
+void debug_stamps(uint64_t* out20, bool) {
+  for (int i = 0; i < 20; i++) out20[i] = 0;
 }
 #endif
 
