@@ -164,6 +164,15 @@ int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, s
 int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi,
                   int32_t* batch);
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch);
+/* RoaringBitmap.runOptimize() (RB/RoaringBitmap.java:2764-2774) applied on the device to
+ * every bitmap of a batch; the result is a new batch (same bitmaps, keys and order).
+ * answers (n bitmaps, nullable) receives runOptimize's boolean per bitmap.  Also backs
+ * RoaringBitmapSliceIndex.runOptimize (bsi/.../RoaringBitmapSliceIndex.java:141-150). */
+int rbg_ctx_run_optimize(rbg_ctx* ctx, int32_t batch, int32_t* out_batch, uint8_t* answers);
+/* One-shot form: runOptimize each of n serialized bitmaps on the device; outs[i] receives
+ * the optimized bytes (free each with rbg_free), answers[i] (nullable) the boolean. */
+int rbg_run_optimize_many(const uint8_t* const* bufs, const size_t* lens, size_t n, rbg_buffer* outs,
+                          uint8_t* answers);
 /* min / max of the values of a synthetic C5 batch (out2). */
 int rbg_ctx_batch_minmax(rbg_ctx* ctx, int32_t batch, int32_t* out2);
 /* Batch facts: stats[0..7] = bitmaps, containers, #array, #bitmap, #run, payload bytes,

@@ -12,7 +12,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import IllegalArgumentException, check, lib, take
-from .roaring import RoaringBitmap
+from .roaring import RoaringBitmap, run_optimize_many
 
 OPERATIONS = ("EQ", "NEQ", "LE", "LT", "GE", "GT", "RANGE")  # BitmapSliceIndex.Operation order
 
@@ -25,6 +25,7 @@ class RoaringBitmapSliceIndex:
         self.bA = list(slices)
         self.minValue = int(min_value)
         self.maxValue = int(max_value)
+        self.runOptimized = False
 
     @classmethod
     def from_columns(cls, columns, values, run_optimize=False):
@@ -48,6 +49,11 @@ class RoaringBitmapSliceIndex:
         ebm = RoaringBitmap.from_values(columns, run_optimize)
         ba = [RoaringBitmap.from_values(columns[(values >> i) & 1 == 1], run_optimize) for i in range(nbits)]
         return cls(ebm, ba, mn, mx)
+
+    def runOptimize(self):
+        """BSI/:141-150: runOptimize of ebM and of every slice (one device pass over all of them)."""
+        run_optimize_many([self.ebM] + self.bA)
+        self.runOptimized = True
 
     def bitCount(self):
         return len(self.bA)

@@ -1104,12 +1104,19 @@ int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* st) {
   }
   return RBG_OK;
 }
+static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out);
 int rbg_ctx_batch_fetch(rbg_ctx* ctx, int32_t batch, size_t i, rbg_buffer* out) {
-  Batch* b;
-  CHK(get_batch(&ctx->c, batch, &b));
-  if (i >= b->n_bm || !out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
   HIPCHK(hipSetDevice(ctx->c.device));
-  HIPCHK(hipStreamSynchronize(ctx->c.stream));
+  return ctx_batch_fetch(&ctx->c, batch, i, out);
+}
+}  // extern "C"
+
+static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out) {
+  Batch* b;
+  CHK(get_batch(c, batch, &b));
+  if (i >= b->n_bm || !out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipStreamSynchronize(c->stream));
   std::vector<CDesc> all(b->n_ctr);
   if (b->n_ctr) HIPCHK(hipMemcpy(all.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
   std::vector<CDesc> mine;
@@ -1172,6 +1179,8 @@ int rbg_ctx_batch_fetch(rbg_ctx* ctx, int32_t batch, size_t i, rbg_buffer* out) 
   }
   return emit_host(o, out);
 }
+
+extern "C" {
 int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
   HIPCHK(hipSetDevice(ctx->c.device));
   return ctx_pairwise(&ctx->c, op, a, ia, b, ib, false);
@@ -1623,6 +1632,103 @@ static int synth_c5(Ctx* c, uint64_t seed, size_t rows, int key_lo, int key_hi, 
   b.live = true;
   *out_id = id;
   return RBG_OK;
+}
+
+// RoaringBitmap.runOptimize (RB/RoaringBitmap.java:2764-2774) over every bitmap of a
+// batch, into a new batch: plan (new kind + slot size per container), scan of the
+// slot sizes, write.  answers[i] = 1 iff bitmap i holds a run container afterwards.
+static int copy_dev(DevBuf& dst, const DevBuf& src, hipStream_t s) {
+  CHK(dst.ensure(src.cap));
+  if (src.cap) HIPCHK(hipMemcpyAsync(dst.p, src.p, src.cap, hipMemcpyDeviceToDevice, s));
+  return RBG_OK;
+}
+
+static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answers) {
+  Batch* a;
+  CHK(get_batch(c, id, &a));
+  hipStream_t s = c->stream;
+  const size_t C = a->n_ctr, n = a->n_bm;
+  DevBuf info, size, part, flags;
+  CHK(info.ensure(4 * C + 16));
+  CHK(size.ensure(8 * C + 16));
+  CHK(part.ensure(8 * (scan_parts(C) + 1)));
+  CHK(flags.ensure(4 * n + 16));
+  CHK(c->scalar.ensure(64));
+  HIPCHK(hipMemsetAsync(flags.p, 0, 4 * n + 16, s));
+  HIPCHK(hipMemsetAsync(c->scalar.p, 0, 64, s));
+  unsigned long long* tot = c->scalar.as<unsigned long long>();
+  launch_runopt_plan(s, a->desc.as<CDesc>(), a->bm.as<uint32_t>(), a->payload.as<uint8_t>(), C, info.as<uint32_t>(),
+                     size.as<uint64_t>(), flags.as<uint32_t>(), tot);
+  launch_exclusive_scan(s, size.as<uint64_t>(), size.as<uint64_t>(), C, part.as<uint64_t>(),
+                        reinterpret_cast<uint64_t*>(tot + 4));
+  HIPCHK(hipGetLastError());
+  unsigned long long h[5] = {};
+  std::vector<uint32_t> hf(n);
+  HIPCHK(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s));
+  if (n) HIPCHK(hipMemcpyAsync(hf.data(), flags.p, 4 * n, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const int32_t bid = new_batch(c);
+  Batch& b = *c->batches[bid];
+  b.n_bm = n;
+  b.n_ctr = C;
+  b.key_major = a->key_major;
+  b.h_bm_off = a->h_bm_off;
+  b.h_bm_nctr = a->h_bm_nctr;
+  b.h_bm_card = a->h_bm_card;
+  b.long_card = a->long_card;
+  b.bsi_min = a->bsi_min;
+  b.bsi_max = a->bsi_max;
+  for (int k = 0; k < 3; k++) b.n_kind[k] = (int64_t)h[k];
+  b.payload_bytes = h[4];
+  b.max_ser = 0;  // runOptimize leaves no container above 8194 serialized bytes
+  int64_t ser = (int64_t)h[3];
+  for (size_t i = 0; i < n; i++) {
+    const size_t nc = a->h_bm_nctr.empty() ? 0 : a->h_bm_nctr[i];
+    ser += (int64_t)header_size(nc, hf[i] != 0);
+    if (answers) answers[i] = hf[i] != 0;
+  }
+  b.ser_bytes = a->ser_bytes ? ser : 0;  // batches built on the device carry no serialized size
+  CHK(copy_dev(b.keys, a->keys, s));
+  CHK(copy_dev(b.bm, a->bm, s));
+  CHK(copy_dev(b.key_off, a->key_off, s));
+  CHK(copy_dev(b.bm_off, a->bm_off, s));
+  CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
+  CHK(b.payload.ensure(b.payload_bytes + 64));
+  launch_runopt_write(s, a->desc.as<CDesc>(), a->payload.as<uint8_t>(), C, info.as<uint32_t>(), size.as<uint64_t>(),
+                      b.desc.as<CDesc>(), b.payload.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(s));  // the scratch buffers above are freed on return
+  b.live = true;
+  *out_id = bid;
+  return RBG_OK;
+}
+
+int rbg_run_optimize_many(const uint8_t* const* bufs, const size_t* lens, size_t n, rbg_buffer* outs,
+                          uint8_t* answers) {
+  if (n && !outs) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t in = -1, opt = -1;
+  CHK(ctx_load(c, bufs, lens, n, &in));
+  g.ids.push_back(in);
+  CHK(ctx_run_optimize(c, in, &opt, answers));
+  g.ids.push_back(opt);
+  for (size_t i = 0; i < n; i++) {
+    outs[i] = rbg_buffer{};
+    const int st = ctx_batch_fetch(c, opt, i, &outs[i]);
+    if (st) {
+      for (size_t j = 0; j < i; j++) rbg_free(&outs[j]);
+      return st;
+    }
+  }
+  return RBG_OK;
+}
+
+int rbg_ctx_run_optimize(rbg_ctx* ctx, int32_t batch, int32_t* out_batch, uint8_t* answers) {
+  if (!ctx || !out_batch) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_run_optimize(&ctx->c, batch, out_batch, answers);
 }
 
 int rbg_ctx_batch_minmax(rbg_ctx* ctx, int32_t batch, int32_t* out2) {

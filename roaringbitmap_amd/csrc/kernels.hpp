@@ -113,4 +113,16 @@ void launch_synth_arrays(hipStream_t s, uint64_t seed, const CDesc* desc, uint64
 // force < 0: C2 mix (kind drawn per key); force = DK_A/DK_B/DK_R: every key drawn from that family
 void launch_synth_c2(hipStream_t s, uint64_t seed, int force, CDesc* desc, uint16_t* keys, uint8_t* payload);
 
+// runopt.hip: device-wide exclusive scan of u64 (part: scan_parts(n) u64 scratch;
+// *total = sum), and RoaringBitmap.runOptimize over a batch
+uint64_t scan_parts(uint64_t n);
+void launch_exclusive_scan(hipStream_t s, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* part,
+                           uint64_t* total);
+// info[i] = new kind | changed << 2 | nruns << 3; size[i] = new slot bytes; bm_has_run[bitmap] = 1
+// where an R container results; totals = {#A, #B, #R, serialized payload bytes}
+void launch_runopt_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
+                        uint32_t* info, uint64_t* size, uint32_t* bm_has_run, unsigned long long* totals);
+void launch_runopt_write(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, const uint32_t* info,
+                         const uint64_t* off, CDesc* out_desc, uint8_t* out_payload);
+
 }  // namespace rbg

@@ -112,6 +112,15 @@ class Engine:
         check(lib().rbg_ctx_pair_bytes(self._ctx, int(batch), out))
         return int(out[0]), int(out[1])
 
+    def run_optimize(self, batch):
+        """RoaringBitmap.runOptimize (RB/RoaringBitmap.java:2764-2774) of every bitmap of a batch, on the
+        device -> (new batch id, [runOptimize's boolean per bitmap]).  Synchronous."""
+        n = self.batch_stats(batch)["bitmaps"]
+        out = ctypes.c_int32()
+        ans = (ctypes.c_uint8 * max(n, 1))()
+        check(lib().rbg_ctx_run_optimize(self._ctx, int(batch), ctypes.byref(out), ans))
+        return int(out.value), [bool(x) for x in ans[:n]]
+
     def batch_minmax(self, batch):
         out = (ctypes.c_int32 * 2)()
         check(lib().rbg_ctx_batch_minmax(self._ctx, int(batch), out))

@@ -305,5 +305,22 @@ def batch_and_cardinality(pairs):
     return out
 
 
+def run_optimize_many(bitmaps):
+    """RoaringBitmap.runOptimize() (RB/RoaringBitmap.java:2764-2774) applied in place to every bitmap,
+    as one device pass over all their containers; returns runOptimize's boolean per bitmap."""
+    bitmaps = list(bitmaps)
+    n = len(bitmaps)
+    if n == 0:
+        return []
+    arr, lens = _lib.buf_array([b._buf for b in bitmaps])
+    outs = (_lib.rbg_buffer * n)()
+    ans = (ctypes.c_uint8 * n)()
+    check(lib().rbg_run_optimize_many(arr, lens, n, outs, ans))
+    for b, o in zip(bitmaps, outs):
+        b._buf = take(o)
+        b._lcard = None
+    return [bool(x) for x in ans]
+
+
 def _chain(*its):
     return itertools.chain(*its)

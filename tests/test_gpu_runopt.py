@@ -1,0 +1,76 @@
+"""runOptimize on the device (RB/RoaringBitmap.java:2764-2774) vs the oracle's runOptimize.
+
+Every container family of tests/_gen.py (arrays, bitmaps, runs, full containers, edge
+cardinalities) is run through rbg_run_optimize_many / Engine.run_optimize; the result
+bytes must equal the oracle's, and runOptimize's boolean must be "any run container".
+"""
+import numpy as np
+import pytest
+
+import _gen
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _answer(buf):
+    return O.stats(buf)["run"] > 0
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_run_optimize_many_families(gpu, seed):
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(900 + seed)
+    bufs = []
+    for i in range(60):
+        keys = np.sort(rng.choice(1 << 16, size=int(rng.integers(1, 12)), replace=False))
+        bufs.append(_gen.bitmap(rng, keys))
+    bufs.append(O.from_values([]))                             # empty bitmap
+    bufs.append(O.from_values(np.arange(1 << 16)))              # one full container
+    bufs.append(O.from_values(np.arange(0, 1 << 17, 2)))        # alternating bits: stays B
+    bufs.append(O.from_values(np.arange(100, 4196)))            # A -> R
+    bufs.append(O.from_values([5, 70000, 140000]))               # single values stay A
+    bms = [rb.RoaringBitmap(b) for b in bufs]
+    ans = rb.run_optimize_many(bms)
+    for b, bm, a in zip(bufs, bms, ans):
+        exp = O.run_optimize(b)
+        assert bm.serialize() == exp
+        assert a == _answer(exp)
+
+
+def test_engine_run_optimize_c2_batch(gpu):
+    """A synthetic C2 operand (65,536 keys, mixed A/B/R) optimized on the device and then
+    used as an operand: bytes equal to the oracle's runOptimize, and AND results equal to
+    the oracle's AND of the optimized inputs."""
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+    a = e.synth(0, 0xC2A0)
+    b = e.synth(0, 0xC2B0)
+    oa, ans = e.run_optimize(a)
+    ob, _ = e.run_optimize(b)
+    src_a, src_b = e.batch_fetch(a).serialize(), e.batch_fetch(b).serialize()
+    opt_a, opt_b = e.batch_fetch(oa).serialize(), e.batch_fetch(ob).serialize()
+    assert opt_a == O.run_optimize(src_a)
+    assert opt_b == O.run_optimize(src_b)
+    assert ans == [_answer(opt_a)]
+    st = e.batch_stats(oa)
+    ost = O.stats(opt_a)
+    assert (st["array"], st["bitmap"], st["run"]) == (ost["array"], ost["bitmap"], ost["run"])
+    assert st["serialized_bytes"] in (0, len(opt_a))
+    e.pairwise("and", oa, ob)
+    assert e.fetch().serialize() == O.pairwise("and", opt_a, opt_b)
+    for x in (a, b, oa, ob):
+        e.release(x)
+
+
+def test_bsi_run_optimize(gpu):
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(5)
+    cols = np.sort(rng.choice(1 << 20, 20000, replace=False))
+    v = rng.integers(0, 1 << 12, cols.size)
+    bsi = rb.RoaringBitmapSliceIndex.from_columns(cols, v)
+    before = [bsi.ebM.serialize()] + [s.serialize() for s in bsi.bA]
+    bsi.runOptimize()
+    assert bsi.runOptimized
+    after = [bsi.ebM.serialize()] + [s.serialize() for s in bsi.bA]
+    assert after == [O.run_optimize(b) for b in before]
