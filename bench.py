@@ -145,6 +145,23 @@ def c4_batch_and_card(eng, n_pairs, rank, world, dist, steps, warmup, cdev):
             "all_bytes_per_rank": allb}
 
 
+def run_optimize_c2(eng, a, sa, steps):
+    """RoaringBitmap.runOptimize of one C2 operand on the device (plan, scan, write into a new
+    batch); wall time per call, new-batch allocation and the host read-back of the totals included."""
+    o, _ = eng.run_optimize(a)
+    so = eng.batch_stats(o)
+    eng.release(o)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        o, _ = eng.run_optimize(a)
+        eng.release(o)
+    dt = (time.perf_counter() - t0) / steps
+    return {"workload": "RoaringBitmap.runOptimize of one C2 operand (65,536 containers)",
+            "ms_per_call": round(dt * 1e3, 4), "input_GBps": round(sa["payload_bytes"] / dt / 1e9, 1),
+            "types_before": [sa["array"], sa["bitmap"], sa["run"]],
+            "types_after": [so["array"], so["bitmap"], so["run"]]}
+
+
 def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
     """C5: RoaringBitmapSliceIndex.compare(RANGE) + sum over `rows` rows (31 slices),
     rows sharded by key range across the ranks (strong scaling); one step = the fused
@@ -296,6 +313,9 @@ def main():
                                                     cdev)
     if args.c5_rows > 0:
         c3["c5_bsi_range_sum"] = c5_bsi(eng, args.c5_rows, rank, world, dist, max(3, args.steps // 4), 1, cdev)
+
+    if args.c3_n > 0 or args.c4_pairs > 0 or args.c5_rows > 0:
+        c3["run_optimize_c2"] = run_optimize_c2(eng, a, sa, max(3, args.steps // 4))
 
     t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device=cdev)
     if dist is not None:

@@ -100,8 +100,13 @@ struct Batch {
   int32_t bsi_min = 0, bsi_max = 0;  // synthetic C5: min / max of the indexed values
 };
 
+struct DecBufs {  // scratch of the device decode (decode.hip), reused across loads
+  DevBuf meta, head, nctr, base, err, card, cons, part, q, qkey, sort, skey, iota, perm, size, cpart;
+};
+
 struct Ctx {
   int device = 0;
+  DecBufs dec;
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Batch>> batches;
   uint64_t* zlb = nullptr;    // look-back state the next plan kernel zeroes (null: none)
@@ -203,123 +208,192 @@ static int32_t new_batch(Ctx* c) {
   return (int32_t)(c->batches.size() - 1);
 }
 
+// drops the listed batches on scope exit
+struct BatchGuard {
+  Ctx* c;
+  std::vector<int32_t> ids;
+  ~BatchGuard() {
+    for (int32_t id : ids)
+      if (id >= 0 && (size_t)id < c->batches.size()) c->batches[id].reset();
+  }
+};
+
 // ---------------------------------------------------------------------------
-// upload: parse headers on the host, H2D the raw bytes once, GPU ingest
+// upload: the host concatenates the serialized inputs (16 B aligned) and copies
+// them once; decode.hip parses every header and places every payload on the GPU
 // ---------------------------------------------------------------------------
-static int ctx_load(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out_id) {
-  if (n && (!bufs || !lens)) return RBG_ERR_ILLEGAL_ARGUMENT;
-  std::vector<HostBitmap> hb(n);
-  for (size_t i = 0; i < n; i++) {
-    std::string err;
-    int st = parse(bufs[i], lens[i], &hb[i], &err);
-    if (st) {
-      set_err("input " + std::to_string(i) + ": " + err);
+static const char* dec_message(uint32_t e, int* status) {
+  *status = RBG_ERR_TRUNCATED;
+  switch (e) {
+    case DEC_TRUNC_COOKIE: return "truncated input: cookie";
+    case DEC_BAD_COOKIE: *status = RBG_ERR_INVALID_FORMAT; return "I failed to find one of the right cookies.";
+    case DEC_TRUNC_SIZE: return "truncated input: size";
+    case DEC_SIZE_LARGE: *status = RBG_ERR_INVALID_FORMAT; return "Size too large";
+    case DEC_SIZE_NEG: *status = RBG_ERR_INVALID_FORMAT; return "negative container count";
+    case DEC_TRUNC_FLAGS: return "truncated input: run flags";
+    case DEC_TRUNC_DESC: return "truncated input: descriptors";
+    case DEC_KEY_ORDER: *status = RBG_ERR_INVALID_FORMAT; return "container keys are not strictly increasing";
+    case DEC_TRUNC_OFFSETS: return "truncated input: offsets";
+    case DEC_TRUNC_RUNS: return "truncated input: run count";
+    default: return "truncated input: container payload";
+  }
+}
+
+static int dec_report(Ctx* c, size_t n) {
+  std::vector<uint32_t> e(n);
+  HIPCHK(hipMemcpy(e.data(), c->dec.err.p, 4 * n, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < n; i++)
+    if (e[i]) {
+      int st;
+      const char* m = dec_message(e[i], &st);
+      set_err("input " + std::to_string(i) + ": " + m);
       return st;
     }
+  set_err("decode reported an error but no input carries one");
+  return RBG_ERR_DEVICE;
+}
+
+// key_major: containers sorted by (key, input) with a key CSR (operands of every op);
+// otherwise input order (bitmap-major, batched andCardinality)
+static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, bool key_major,
+                         int32_t* out_id) {
+  if (n && (!bufs || !lens)) return RBG_ERR_ILLEGAL_ARGUMENT;
+  for (size_t i = 0; i < n; i++)
+    if (!bufs[i] && lens[i]) return RBG_ERR_ILLEGAL_ARGUMENT;
+  DecBufs& d = c->dec;
+  hipStream_t s = c->stream;
+  // inputs at 16 B aligned offsets of one upload
+  std::vector<uint64_t> meta(2 * n + 2, 0);  // in_off[n], in_len[n]
+  uint64_t raw_bytes = 0;
+  for (size_t i = 0; i < n; i++) {
+    meta[i] = raw_bytes;
+    meta[n + i] = lens[i];
+    raw_bytes = round16(raw_bytes + lens[i]);
   }
+  CHK(c->raw.ensure(raw_bytes + 64));
+  CHK(pinned_ensure(c, raw_bytes + 64));
+  uint8_t* pin = reinterpret_cast<uint8_t*>(c->pinned);
+  const int nthr =
+      raw_bytes > (64u << 20) ? (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  auto copy_range = [&](size_t t, size_t step) {
+    for (size_t i = t; i < n; i += step)
+      if (lens[i]) std::memcpy(pin + meta[i], bufs[i], lens[i]);
+  };
+  if (nthr == 1) {
+    copy_range(0, 1);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthr; t++) th.emplace_back(copy_range, (size_t)t, (size_t)nthr);
+    for (auto& x : th) x.join();
+  }
+  CHK(d.meta.ensure(8 * (2 * n + 2)));
+  CHK(d.head.ensure(sizeof(DecHead) * n + 16));
+  CHK(d.nctr.ensure(8 * n + 16));
+  CHK(d.base.ensure(8 * n + 16));
+  CHK(d.err.ensure(4 * n + 16));
+  CHK(d.card.ensure(8 * n + 16));
+  CHK(d.cons.ensure(8 * n + 16));
+  CHK(d.part.ensure(8 * (scan_parts(std::max<size_t>(n, 1)) + 1)));
+  CHK(c->scalar.ensure(64));
+  const uint64_t* in_off = d.meta.as<uint64_t>();
+  const uint64_t* in_len = in_off + n;
+  unsigned long long* sc = c->scalar.as<unsigned long long>();  // [0] any error, [1] C, [2..5] totals, [6] bytes
+  HIPCHK(hipMemcpyAsync(c->raw.p, pin, raw_bytes, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(d.meta.p, meta.data(), 8 * (2 * n + 2), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(sc, 0, 64, s));
+  uint32_t* any_err = reinterpret_cast<uint32_t*>(sc);
+  launch_dec_head(s, c->raw.as<uint8_t>(), in_off, in_len, n, d.head.as<DecHead>(), d.nctr.as<uint64_t>(),
+                  d.err.as<uint32_t>(), any_err);
+  launch_exclusive_scan(s, d.nctr.as<uint64_t>(), d.base.as<uint64_t>(), n, d.part.as<uint64_t>(),
+                        reinterpret_cast<uint64_t*>(sc + 1));
+  HIPCHK(hipGetLastError());
+  unsigned long long h[8] = {};
+  HIPCHK(hipMemcpyAsync(h, sc, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (h[0]) return dec_report(c, n);
+  const uint64_t C = h[1];
+  if (C > 0x7FFFFFFFull) {
+    set_err("a batch holds at most 2^31 - 1 containers");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  CHK(d.q.ensure(sizeof(DecCtr) * C + 16));
+  CHK(d.qkey.ensure(2 * C + 16));
+  launch_dec_ctrs(s, c->raw.as<uint8_t>(), in_off, in_len, n, d.head.as<DecHead>(), d.base.as<uint64_t>(),
+                  d.q.as<DecCtr>(), d.qkey.as<uint16_t>(), d.card.as<uint64_t>(), d.cons.as<uint64_t>(),
+                  d.err.as<uint32_t>(), any_err);
   const int32_t id = new_batch(c);
   Batch& b = *c->batches[id];
+  BatchGuard guard{c, {id}};  // dropped unless the load completes
   b.n_bm = n;
-  b.key_major = true;  // one bitmap is trivially key-major; several are sorted by key
-  size_t C = 0;
-  b.h_bm_nctr.resize(n);
-  b.h_bm_card.resize(n);
-  b.h_bm_off.assign(n + 1, 0);
-  for (size_t i = 0; i < n; i++) {
-    b.h_bm_nctr[i] = (uint32_t)hb[i].ctrs.size();
-    b.h_bm_card[i] = hb[i].card;
-    b.h_bm_off[i + 1] = b.h_bm_off[i] + (uint32_t)hb[i].ctrs.size();
-    C += hb[i].ctrs.size();
-    b.long_card += hb[i].card;
-    b.ser_bytes += (int64_t)hb[i].consumed;
-  }
   b.n_ctr = C;
-  // key-major order: stable counting sort by key (input order kept within a key)
-  std::vector<uint32_t> key_off(kMaxKeys + 1, 0);
-  for (size_t i = 0; i < n; i++)
-    for (const HostCtr& hc : hb[i].ctrs) key_off[hc.key + 1]++;
-  for (int k = 0; k < kMaxKeys; k++) key_off[k + 1] += key_off[k];
-  std::vector<uint32_t> cursor(key_off.begin(), key_off.end() - 1);
-  std::vector<uint16_t> h_keys(C);
-  std::vector<CDesc> h_desc(C);
-  std::vector<uint32_t> h_bm(C);
-  std::vector<IngestItem> items(C);
-  // raw layout: concatenated inputs
-  std::vector<uint64_t> raw_base(n + 1, 0);
-  for (size_t i = 0; i < n; i++) raw_base[i + 1] = raw_base[i] + hb[i].consumed;
-  std::vector<uint32_t> pos_of(C);  // position of (input i, container j) in key-major order
-  for (size_t i = 0; i < n; i++) {
-    for (size_t j = 0; j < hb[i].ctrs.size(); j++) {
-      const HostCtr& hc = hb[i].ctrs[j];
-      pos_of[b.h_bm_off[i] + j] = cursor[hc.key]++;
-    }
-  }
-  // slot offsets follow key-major order so a key's fan-in is contiguous
-  std::vector<uint64_t> slot_size(C);
-  for (size_t i = 0; i < n; i++)
-    for (size_t j = 0; j < hb[i].ctrs.size(); j++) {
-      const HostCtr& hc = hb[i].ctrs[j];
-      slot_size[pos_of[b.h_bm_off[i] + j]] = slot_bytes(hc.kind, hc.ser_len);
-    }
-  std::vector<uint64_t> slot_off(C + 1, 0);
-  for (size_t p = 0; p < C; p++) slot_off[p + 1] = slot_off[p] + slot_size[p];
-  for (size_t i = 0; i < n; i++) {
-    for (size_t j = 0; j < hb[i].ctrs.size(); j++) {
-      const HostCtr& hc = hb[i].ctrs[j];
-      const uint32_t p = pos_of[b.h_bm_off[i] + j];
-      h_keys[p] = hc.key;
-      h_bm[p] = (uint32_t)i;
-      CDesc d;
-      d.slot = slot_off[p];
-      d.card = hc.card;
-      d.key = hc.key;
-      d.kind = hc.kind;
-      d.flags = 0;
-      h_desc[p] = d;
-      items[p] = IngestItem{raw_base[i] + hc.ser_off, slot_off[p], hc.ser_len, hc.kind};
-      b.n_kind[hc.kind]++;
-      if (hc.ser_len > 8194) b.max_ser += hc.ser_len;
-    }
-  }
-  b.payload_bytes = slot_off[C];
-  // device allocations
+  b.key_major = key_major;
   CHK(b.keys.ensure(2 * C + 16));
   CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
   CHK(b.bm.ensure(4 * C + 16));
-  CHK(b.key_off.ensure(4 * (kMaxKeys + 1)));
   CHK(b.bm_off.ensure(4 * (n + 1)));
-  CHK(b.payload.ensure(b.payload_bytes + 64));
-  const size_t raw_bytes = raw_base[n];
-  CHK(c->raw.ensure(raw_bytes + 64));
-  CHK(c->items.ensure(sizeof(IngestItem) * C + 16));
-  // stage raw bytes in pinned memory (parallel memcpy for large uploads)
-  CHK(pinned_ensure(c, raw_bytes + 64));
-  uint8_t* pin = reinterpret_cast<uint8_t*>(c->pinned);
-  const int nthr = raw_bytes > (64u << 20) ? (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
-  if (nthr == 1) {
-    for (size_t i = 0; i < n; i++) std::memcpy(pin + raw_base[i], bufs[i], hb[i].consumed);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nthr; t++)
-      th.emplace_back([&, t]() {
-        for (size_t i = t; i < n; i += nthr) std::memcpy(pin + raw_base[i], bufs[i], hb[i].consumed);
-      });
-    for (auto& x : th) x.join();
+  const uint32_t* perm = nullptr;
+  if (key_major) {
+    CHK(b.key_off.ensure(4 * (kMaxKeys + 1)));
+    const uint16_t* sorted = d.qkey.as<uint16_t>();
+    if (n > 1 && C > 0) {  // one bitmap is key-sorted already
+      const size_t tb = dec_sort_temp_bytes(C);
+      CHK(d.sort.ensure(tb + 16));
+      CHK(d.skey.ensure(2 * C + 16));
+      CHK(d.iota.ensure(4 * C + 16));
+      CHK(d.perm.ensure(4 * C + 16));
+      if (launch_dec_sort(s, d.sort.p, tb, d.qkey.as<uint16_t>(), d.skey.as<uint16_t>(), d.iota.as<uint32_t>(),
+                          d.perm.as<uint32_t>(), C) != 0) {
+        set_err("radix sort of the container keys failed");
+        return RBG_ERR_DEVICE;
+      }
+      sorted = d.skey.as<uint16_t>();
+      perm = d.perm.as<uint32_t>();
+    }
+    launch_dec_key_off(s, sorted, C, b.key_off.as<uint32_t>());
   }
-  hipStream_t s = c->stream;
-  HIPCHK(hipMemcpyAsync(c->raw.p, pin, raw_bytes, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(c->items.p, items.data(), sizeof(IngestItem) * C, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.keys.p, h_keys.data(), 2 * C, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.desc.p, h_desc.data(), sizeof(CDesc) * C, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.bm.p, h_bm.data(), 4 * C, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.key_off.p, key_off.data(), 4 * (kMaxKeys + 1), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
-  launch_ingest(s, c->raw.as<uint8_t>(), c->items.as<IngestItem>(), C, b.payload.as<uint8_t>());
+  CHK(d.size.ensure(8 * C + 16));
+  CHK(d.cpart.ensure(8 * (scan_parts(std::max<uint64_t>(C, 1)) + 1)));
+  launch_dec_sizes(s, d.q.as<DecCtr>(), perm, C, d.size.as<uint64_t>(), sc + 2);
+  launch_exclusive_scan(s, d.size.as<uint64_t>(), d.size.as<uint64_t>(), C, d.cpart.as<uint64_t>(),
+                        reinterpret_cast<uint64_t*>(sc + 6));
   HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(h, sc, 64, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
+  if (h[0]) return dec_report(c, n);
+  for (int k = 0; k < 3; k++) b.n_kind[k] = (int64_t)h[2 + k];
+  b.max_ser = h[5];
+  b.payload_bytes = h[6];
+  CHK(b.payload.ensure(b.payload_bytes + 64));
+  launch_dec_fill(s, c->raw.as<uint8_t>(), d.q.as<DecCtr>(), d.qkey.as<uint16_t>(), perm, d.size.as<uint64_t>(), C,
+                  b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.bm.as<uint32_t>(), b.payload.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  std::vector<uint64_t> nctr(n), card(n), cons(n);
+  if (n) {
+    HIPCHK(hipMemcpyAsync(nctr.data(), d.nctr.p, 8 * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(card.data(), d.card.p, 8 * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(cons.data(), d.cons.p, 8 * n, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  b.h_bm_off.assign(n + 1, 0);
+  b.h_bm_nctr.resize(n);
+  b.h_bm_card.resize(n);
+  for (size_t i = 0; i < n; i++) {
+    b.h_bm_nctr[i] = (uint32_t)nctr[i];
+    b.h_bm_off[i + 1] = b.h_bm_off[i] + (uint32_t)nctr[i];
+    b.h_bm_card[i] = (int64_t)card[i];
+    b.long_card += (int64_t)card[i];
+    b.ser_bytes += (int64_t)cons[i];
+  }
+  HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  guard.ids.clear();
   b.live = true;
   *out_id = id;
   return RBG_OK;
+}
+
+static int ctx_load(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out_id) {
+  return ctx_load_impl(c, bufs, lens, n, true, out_id);
 }
 
 // ---------------------------------------------------------------------------
@@ -719,14 +793,6 @@ static int tl_ctx(Ctx** out) {
   return RBG_OK;
 }
 
-struct BatchGuard {
-  Ctx* c;
-  std::vector<int32_t> ids;
-  ~BatchGuard() {
-    for (int32_t id : ids)
-      if (id >= 0 && (size_t)id < c->batches.size()) c->batches[id].reset();
-  }
-};
 
 }  // namespace rbg
 
@@ -867,74 +933,7 @@ static int ctx_batch_card(Ctx* c, int32_t id) {
 
 // bitmap-major upload used by batched andCardinality (pairs kept adjacent)
 static int ctx_load_bitmap_major(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out_id) {
-  std::vector<HostBitmap> hb(n);
-  for (size_t i = 0; i < n; i++) {
-    std::string err;
-    int st = parse(bufs[i], lens[i], &hb[i], &err);
-    if (st) {
-      set_err("input " + std::to_string(i) + ": " + err);
-      return st;
-    }
-  }
-  const int32_t id = new_batch(c);
-  Batch& b = *c->batches[id];
-  b.n_bm = n;
-  b.key_major = false;  // no key CSR: not usable as a pairwise operand or wide input
-  b.h_bm_off.assign(n + 1, 0);
-  b.h_bm_nctr.resize(n);
-  b.h_bm_card.resize(n);
-  std::vector<uint64_t> raw_base(n + 1, 0);
-  for (size_t i = 0; i < n; i++) {
-    b.h_bm_off[i + 1] = b.h_bm_off[i] + (uint32_t)hb[i].ctrs.size();
-    b.h_bm_nctr[i] = (uint32_t)hb[i].ctrs.size();
-    b.h_bm_card[i] = hb[i].card;
-    b.long_card += hb[i].card;
-    b.ser_bytes += (int64_t)hb[i].consumed;
-    raw_base[i + 1] = raw_base[i] + hb[i].consumed;
-  }
-  const size_t C = b.h_bm_off[n];
-  b.n_ctr = C;
-  std::vector<uint16_t> h_keys(C);
-  std::vector<CDesc> h_desc(C);
-  std::vector<uint32_t> h_bm(C);
-  std::vector<IngestItem> items(C);
-  uint64_t off = 0;
-  for (size_t i = 0; i < n; i++)
-    for (size_t j = 0; j < hb[i].ctrs.size(); j++) {
-      const HostCtr& hc = hb[i].ctrs[j];
-      const size_t p = b.h_bm_off[i] + j;
-      h_keys[p] = hc.key;
-      h_bm[p] = (uint32_t)i;
-      h_desc[p] = CDesc{off, hc.card, hc.key, hc.kind, 0};
-      items[p] = IngestItem{raw_base[i] + hc.ser_off, off, hc.ser_len, hc.kind};
-      off += slot_bytes(hc.kind, hc.ser_len);
-      b.n_kind[hc.kind]++;
-    }
-  b.payload_bytes = off;
-  CHK(b.keys.ensure(2 * C + 16));
-  CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
-  CHK(b.bm.ensure(4 * C + 16));
-  CHK(b.bm_off.ensure(4 * (n + 1)));
-  CHK(b.payload.ensure(off + 64));
-  const size_t raw_bytes = raw_base[n];
-  CHK(c->raw.ensure(raw_bytes + 64));
-  CHK(c->items.ensure(sizeof(IngestItem) * C + 16));
-  CHK(pinned_ensure(c, raw_bytes + 64));
-  uint8_t* pin = reinterpret_cast<uint8_t*>(c->pinned);
-  for (size_t i = 0; i < n; i++) std::memcpy(pin + raw_base[i], bufs[i], hb[i].consumed);
-  hipStream_t s = c->stream;
-  HIPCHK(hipMemcpyAsync(c->raw.p, pin, raw_bytes, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(c->items.p, items.data(), sizeof(IngestItem) * C, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.keys.p, h_keys.data(), 2 * C, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.desc.p, h_desc.data(), sizeof(CDesc) * C, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.bm.p, h_bm.data(), 4 * C, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
-  launch_ingest(s, c->raw.as<uint8_t>(), c->items.as<IngestItem>(), C, b.payload.as<uint8_t>());
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));
-  b.live = true;
-  *out_id = id;
-  return RBG_OK;
+  return ctx_load_impl(c, bufs, lens, n, false, out_id);
 }
 
 int rbg_batch_and_card(size_t n_pairs, const uint8_t* const* a_bufs, const size_t* a_lens,
@@ -1120,20 +1119,23 @@ static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out) {
   std::vector<CDesc> all(b->n_ctr);
   if (b->n_ctr) HIPCHK(hipMemcpy(all.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
   std::vector<CDesc> mine;
+  std::vector<size_t> idx;
   if (b->n_bm == 1 || !b->key_major) {
-    for (uint32_t p = b->h_bm_off[i]; p < b->h_bm_off[i + 1]; p++) mine.push_back(all[p]);
+    for (uint32_t p = b->h_bm_off[i]; p < b->h_bm_off[i + 1]; p++) idx.push_back(p);
   } else {
     std::vector<uint32_t> bm(b->n_ctr);
     HIPCHK(hipMemcpy(bm.data(), b->bm.p, 4 * b->n_ctr, hipMemcpyDeviceToHost));
     for (size_t p = 0; p < b->n_ctr; p++)
-      if (bm[p] == i) mine.push_back(all[p]);
+      if (bm[p] == i) idx.push_back(p);
   }
+  // slots are consecutive in descriptor order: a slot ends where the next one starts
   uint64_t lo = ~0ULL, hi = 0;
-  for (const CDesc& d : mine) {
-    lo = std::min<uint64_t>(lo, d.slot);
-    hi = std::max<uint64_t>(hi, d.slot + kSlotBytes);
+  for (size_t p : idx) {
+    mine.push_back(all[p]);
+    lo = std::min<uint64_t>(lo, all[p].slot);
+    hi = std::max<uint64_t>(hi, p + 1 < b->n_ctr ? all[p + 1].slot : b->payload_bytes);
   }
-  hi = std::min<uint64_t>(hi, b->payload_bytes + 64);
+  hi = std::min<uint64_t>(std::max(hi, lo), b->payload_bytes + 64);
   std::vector<uint8_t> pay(mine.empty() ? 0 : hi - lo);
   if (!pay.empty()) HIPCHK(hipMemcpy(pay.data(), b->payload.as<uint8_t>() + lo, hi - lo, hipMemcpyDeviceToHost));
   const size_t n = mine.size();

@@ -125,4 +125,49 @@ void launch_runopt_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, co
 void launch_runopt_write(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, const uint32_t* info,
                          const uint64_t* off, CDesc* out_desc, uint8_t* out_payload);
 
+// decode.hip: portable-format decode on the device
+enum DecErr : uint32_t {
+  DEC_OK = 0,
+  DEC_TRUNC_COOKIE,
+  DEC_BAD_COOKIE,
+  DEC_TRUNC_SIZE,
+  DEC_SIZE_LARGE,
+  DEC_SIZE_NEG,
+  DEC_TRUNC_FLAGS,
+  DEC_TRUNC_DESC,
+  DEC_KEY_ORDER,
+  DEC_TRUNC_OFFSETS,
+  DEC_TRUNC_RUNS,
+  DEC_TRUNC_PAYLOAD,
+};
+struct DecHead {  // per input: table geometry (byte positions within the input)
+  uint64_t pay_pos;
+  uint32_t desc_pos, flags_pos, off_pos;
+  int32_t size;
+  uint32_t flags;
+  uint32_t pad;
+};
+struct DecCtr {  // per container, input order
+  uint64_t src;  // payload byte offset in the raw upload
+  uint32_t len;  // serialized payload bytes
+  uint32_t card;
+  uint32_t bm;
+  uint32_t kind;
+};
+void launch_dec_head(hipStream_t s, const uint8_t* raw, const uint64_t* in_off, const uint64_t* in_len, uint64_t n,
+                     DecHead* hd, uint64_t* nctr, uint32_t* err, uint32_t* any_err);
+void launch_dec_ctrs(hipStream_t s, const uint8_t* raw, const uint64_t* in_off, const uint64_t* in_len, uint64_t n,
+                     const DecHead* hd, const uint64_t* ctr_base, DecCtr* q, uint16_t* qkey, uint64_t* bm_card,
+                     uint64_t* consumed, uint32_t* err, uint32_t* any_err);
+size_t dec_sort_temp_bytes(uint64_t C);
+// stable sort of the container keys: perm[p] = input-order index of key-major position p
+int launch_dec_sort(hipStream_t s, void* temp, size_t temp_bytes, const uint16_t* qkey, uint16_t* skey,
+                    uint32_t* iota, uint32_t* perm, uint64_t C);
+void launch_dec_key_off(hipStream_t s, const uint16_t* skey, uint64_t C, uint32_t* key_off);
+// perm null: input order.  totals += {#A, #B, #R, bytes of payloads above 8194 B}
+void launch_dec_sizes(hipStream_t s, const DecCtr* q, const uint32_t* perm, uint64_t C, uint64_t* size,
+                      unsigned long long* totals);
+void launch_dec_fill(hipStream_t s, const uint8_t* raw, const DecCtr* q, const uint16_t* qkey, const uint32_t* perm,
+                     const uint64_t* slot, uint64_t C, CDesc* desc, uint16_t* keys, uint32_t* bm, uint8_t* payload);
+
 }  // namespace rbg

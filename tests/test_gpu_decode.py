@@ -1,0 +1,115 @@
+"""Portable-format decode on the device (decode.hip) vs the reference's deserialize rules.
+
+Valid inputs: every container family of tests/_gen.py, loaded as one key-major batch and
+fetched back bitmap by bitmap, must give the input bytes back (canonical inputs), and
+the batch statistics must match the oracle's.  Malformed inputs: every truncation point
+of run / no-run bitmaps (with and without an offset table), bad cookies, oversized and
+negative sizes, and unordered keys must raise the same exception class with the same
+message as the host-side restatement of RoaringArray.deserialize (RB/RoaringArray.java:
+547-629) used by RoaringBitmap.deserialize.  An offset table that disagrees with the
+payload walk is ignored, as the reference ignores it.
+"""
+import re
+import struct
+
+import numpy as np
+import pytest
+
+import _gen
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _host_error(buf):
+    from roaringbitmap_amd import RoaringBitmap
+    try:
+        RoaringBitmap.deserialize(buf)
+    except Exception as e:  # noqa: BLE001
+        return type(e), re.sub(r"^status -?\d+: ", "", str(e))
+    return None
+
+
+def _gpu_error(e, bufs):
+    try:
+        b = e.load(bufs)
+    except Exception as ex:  # noqa: BLE001
+        return type(ex), re.sub(r"^status -?\d+: ", "", str(ex))
+    e.release(b)
+    return None
+
+
+def _samples():
+    rng = np.random.default_rng(31)
+    out = [O.from_values([1, 2, 3]), O.from_values(np.arange(0, 300000, 7)),
+           O.from_values(np.arange(1000, 5000), run_optimize=True),               # run cookie, size 1
+           O.from_values(np.concatenate([np.arange(k << 16, (k << 16) + 500) for k in range(6)]),
+                         run_optimize=True)]                                        # run cookie, size 6
+    for _ in range(4):
+        keys = np.sort(rng.choice(1 << 16, size=int(rng.integers(2, 7)), replace=False))
+        out.append(_gen.bitmap(rng, keys))
+    return out
+
+
+def test_roundtrip_families(gpu):
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+    rng = np.random.default_rng(8)
+    bufs = [O.from_values([])]
+    for _ in range(80):
+        keys = np.sort(rng.choice(1 << 16, size=int(rng.integers(1, 20)), replace=False))
+        bufs.append(_gen.bitmap(rng, keys))
+    bufs += _samples()
+    b = e.load(bufs)
+    st = e.batch_stats(b)
+    assert st["bitmaps"] == len(bufs)
+    assert st["serialized_bytes"] == sum(len(x) for x in bufs)
+    assert st["cardinality"] == sum(O.stats(x)["card"] for x in bufs)
+    for k in ("array", "bitmap", "run"):
+        assert st[k] == sum(O.stats(x)[k] for x in bufs)
+    for i, x in enumerate(bufs):
+        assert e.batch_fetch(b, i).serialize() == x
+    # the key-major batch as a wide-op input
+    e.wide("or", b)
+    assert e.fetch().serialize() == O.wide("or", bufs)
+    e.release(b)
+
+
+def test_trailing_bytes_and_bad_offsets_are_ignored(gpu):
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+    x = O.from_values(np.arange(0, 300000, 7))  # no-run cookie, offsets present
+    size = struct.unpack_from("<I", x, 4)[0]
+    y = bytearray(x)
+    struct.pack_into("<I", y, 8 + 4 * size + 4, 12345)  # corrupt offset[1]: the walk is still valid
+    b = e.load([bytes(y) + b"\x00" * 7, x + b"junk"])
+    assert e.batch_fetch(b, 0).serialize() == x
+    assert e.batch_fetch(b, 1).serialize() == x
+    e.release(b)
+
+
+def test_malformed_inputs_match_host_errors(gpu):
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+    bad = []
+    for x in _samples():
+        for cut in range(0, len(x), max(1, len(x) // 97)):
+            bad.append(x[:cut])
+        bad.append(x[:-1])
+    x = _samples()[1]
+    bad.append(b"\x00\x00\x00\x00" + x[4:])                    # bad cookie
+    bad.append(struct.pack("<II", 12346, 70000) + x[8:])       # Size too large
+    bad.append(struct.pack("<Ii", 12346, -5) + x[8:])          # negative size
+    y = bytearray(x)                                            # keys not increasing
+    y[8:12], y[12:16] = x[12:16], x[8:12]
+    bad.append(bytes(y))
+    checked = 0
+    for buf in bad:
+        he = _host_error(buf)
+        if he is None:
+            continue
+        ge = _gpu_error(e, [O.from_values([9]), buf])
+        assert ge is not None, (len(buf), he)
+        assert ge[0] is he[0] and ge[1] == "input 1: " + he[1], (len(buf), he, ge)
+        checked += 1
+    assert checked > 100
