@@ -145,6 +145,22 @@ def c4_batch_and_card(eng, n_pairs, rank, world, dist, steps, warmup, cdev):
             "all_bytes_per_rank": allb}
 
 
+def decode_c2(eng, a, steps):
+    """Upload + device decode of one serialized C2 operand (Engine.load: pinned staging, one H2D
+    copy, header parse, key sort, slot placement, payload copy); wall time per load."""
+    x = eng.batch_fetch(a).serialize()
+    b = eng.load([x])
+    eng.release(b)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        b = eng.load([x])
+        eng.release(b)
+    dt = (time.perf_counter() - t0) / steps
+    return {"workload": "Engine.load of one serialized C2 operand (65,536 containers), PCIe included",
+            "ms_per_load": round(dt * 1e3, 4), "serialized_MB": round(len(x) / 1e6, 2),
+            "GBps": round(len(x) / dt / 1e9, 2)}
+
+
 def run_optimize_c2(eng, a, sa, steps):
     """RoaringBitmap.runOptimize of one C2 operand on the device (plan, scan, write into a new
     batch); wall time per call, new-batch allocation and the host read-back of the totals included."""
@@ -316,6 +332,7 @@ def main():
 
     if args.c3_n > 0 or args.c4_pairs > 0 or args.c5_rows > 0:
         c3["run_optimize_c2"] = run_optimize_c2(eng, a, sa, max(3, args.steps // 4))
+        c3["decode_c2"] = decode_c2(eng, a, max(3, args.steps // 4))
 
     t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device=cdev)
     if dist is not None:

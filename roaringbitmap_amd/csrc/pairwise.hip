@@ -310,7 +310,10 @@ __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint
     bitmap_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
 }
 template <int OP, int MODE>
-__global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
+#ifndef RBG_PW_BLOCKS
+#define RBG_PW_BLOCKS 4
+#endif
+__global__ __launch_bounds__(256, RBG_PW_BLOCKS) void k_pair_wave(const PTask* __restrict__ tasks,
                                                       const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
                                                       const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card) {
   __shared__ __align__(16) uint32_t lds_all[kWaves][2048];

@@ -8,7 +8,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/roaringbitmap_amd/csrc
 OUT=$ROOT/roaringbitmap_amd/lib/variants/$NAME
 mkdir -p $OUT
-for s in kernels.hip pairwise.hip wide.hip synth.hip bsi.hip; do
+for s in $(cd $C && ls *.hip); do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $FLAGS -x hip -c $C/$s -o $OUT/$s.o &
 done
 for s in engine.cpp format.cpp; do
