@@ -98,6 +98,8 @@ struct Batch {
   int64_t long_card = 0;
   size_t max_ser = 0;  // Σ serialized payload of containers larger than 8194 B (long run inputs)
   int32_t bsi_min = 0, bsi_max = 0;  // synthetic C5: min / max of the indexed values
+  bool pair_cap_known = false;        // batched andCardinality: item capacity computed
+  uint64_t pair_items_cap = 0;
 };
 
 struct DecBufs {  // scratch of the device decode (decode.hip), reused across loads
@@ -107,6 +109,7 @@ struct DecBufs {  // scratch of the device decode (decode.hip), reused across lo
 struct Ctx {
   int device = 0;
   DecBufs dec;
+  DevBuf pc_cnt, pc_part, pc_items, pc_large;  // batched andCardinality scratch
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Batch>> batches;
   uint64_t* zlb = nullptr;    // look-back state the next plan kernel zeroes (null: none)
@@ -619,6 +622,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.skip = skip.empty() ? nullptr : c->skip.as<uint8_t>();
     wa.start_bm = start_bm;
     wa.all_array = (B->n_kind[DK_B] == 0 && B->n_kind[DK_R] == 0) ? 1u : 0u;
+    wa.slot32 = B->payload_bytes < (1ull << 36) ? 1u : 0u;
     c->mark(1);
     launch_wide(s, mode, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
                 c->task_card.as<uint32_t>());
@@ -921,8 +925,19 @@ static int ctx_batch_card(Ctx* c, int32_t id) {
   }
   c->mark(0);
   c->mark(1);
-  launch_batch_and_card(c->stream, np, B->bm_off.as<uint32_t>(), B->desc.as<CDesc>(), B->payload.as<uint8_t>(),
-                        c->cards.as<int32_t>());
+  if (!B->pair_cap_known) {
+    B->pair_items_cap = batch_pair_items_cap(B->h_bm_nctr.data(), np);
+    B->pair_cap_known = true;
+  }
+  CHK(c->pc_cnt.ensure(8 * std::max<size_t>(np, 1)));
+  CHK(c->pc_part.ensure(8 * (scan_parts(std::max<size_t>(np, 1)) + 1)));
+  CHK(c->pc_items.ensure(sizeof(PairItem) * std::max<uint64_t>(B->pair_items_cap, 1)));
+  CHK(c->pc_large.ensure(4 * std::max<size_t>(np, 1)));
+  CHK(c->scalar.ensure(64));
+  launch_batch_and_card(c->stream, np, B->bm_off.as<uint32_t>(), B->keys.as<uint16_t>(), B->desc.as<CDesc>(),
+                        B->payload.as<uint8_t>(), c->cards.as<int32_t>(), c->pc_cnt.as<uint64_t>(),
+                        c->pc_part.as<uint64_t>(), c->scalar.as<uint64_t>() + 7, c->pc_items.as<PairItem>(),
+                        c->pc_large.as<uint32_t>());
   c->mark(2);
   c->mark(3);
   HIPCHK(hipGetLastError());
@@ -1557,7 +1572,16 @@ static int synth_c4(Ctx* c, uint64_t seed, size_t n_pairs, int32_t* out_id) {
   CHK(b.bm_off.ensure(4 * (nb + 1)));
   CHK(b.payload.ensure(off + 64));
   hipStream_t s = c->stream;
+  std::vector<uint16_t> hk(C);
+  std::vector<uint32_t> hbm(C);
+  for (size_t j = 0; j < nb; j++)
+    for (uint32_t p = b.h_bm_off[j]; p < b.h_bm_off[j + 1]; p++) {
+      hk[p] = d[p].key;
+      hbm[p] = (uint32_t)j;
+    }
   HIPCHK(hipMemcpyAsync(b.desc.p, d.data(), sizeof(CDesc) * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.keys.p, hk.data(), 2 * C, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(b.bm.p, hbm.data(), 4 * C, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (nb + 1), hipMemcpyHostToDevice, s));
   launch_synth_arrays(s, seed, b.desc.as<CDesc>(), C, b.payload.as<uint8_t>());
   HIPCHK(hipGetLastError());

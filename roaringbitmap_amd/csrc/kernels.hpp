@@ -32,6 +32,7 @@ struct WideArgs {
   const uint8_t* skip;    // naive_and: per input bitmap, 1 = skip (identity with the start)
   uint32_t start_bm;      // naive_and: input bitmap the chain starts from
   uint32_t all_array;     // every container is an array (slots padded with their last value)
+  uint32_t slot32;        // every slot offset / 16 fits 32 bits (payload < 64 GiB)
 };
 
 // bit-sliced index (bsi.hip); ops in the order of BitmapSliceIndex.Operation
@@ -89,9 +90,17 @@ void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm,
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
                 unsigned long long* sums);
 
-// batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch
-void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const CDesc* desc,
-                           const uint8_t* payload, int32_t* out);
+// batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch: per-pair key
+// alignment (count, scan, emit), then one wave per matched key; pairs of more than 64
+// keys take one wave per pair.  Scratch: cnt (n_pairs u64), part (scan_parts(n_pairs)
+// u64), tot (u64: items | large pairs << 32), items (batch_pair_items_cap), large (n_pairs).
+struct PairItem {
+  uint32_t pair, ia, ib;
+};
+void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const uint16_t* keys,
+                           const CDesc* desc, const uint8_t* payload, int32_t* out, uint64_t* cnt, uint64_t* part,
+                           uint64_t* tot, PairItem* items, uint32_t* large);
+uint64_t batch_pair_items_cap(const uint32_t* h_bm_nctr, uint64_t n_pairs);
 
 // synthetic generators (synth.hip)
 // C3 uniform key slice [key_lo, key_lo + nkeys): pass 0 writes per-key slot bytes,

@@ -34,28 +34,50 @@ constexpr int kSmallArray = 64;  // arrays up to this size are scattered by one 
 // Accumulate (OR or XOR, no run containers for XOR) every container of a key
 // segment: small arrays lane-serial, large arrays / runs cooperatively into LDS,
 // bitmaps into registers.
+#ifndef RBG_BGROUP
+#define RBG_BGROUP 2  // 4 costs the all-array path registers (C3 uniform -8%)
+#endif
+constexpr int kBGroup = RBG_BGROUP;
+
 template <int MODE>
 __device__ __forceinline__ void accumulate_segment(const CDesc* desc, const uint8_t* payload, uint32_t s, uint32_t n,
-                                                   uint32_t* acc, int* q, int* big, int* nbig, uint64_t r[4]) {
+                                                   uint32_t* acc, int* q, int* big, int* nbig, uint32_t* bslot,
+                                                   bool slot32, uint64_t r[4]) {
   for (uint32_t base = 0; base < n; base += NT) {
     __syncthreads();
-    if (threadIdx.x == 0) *nbig = 0;
+    if (threadIdx.x == 0) nbig[0] = nbig[1] = 0;
     __syncthreads();
     const uint32_t j = base + threadIdx.x;
     if (j < n) {
       const CDesc d = desc[s + j];
       if (d.kind == DK_A && d.card <= (uint32_t)kSmallArray) {
         thread_scatter_array<MODE>(acc, reinterpret_cast<const uint16_t*>(payload + d.slot), (int)d.card);
+      } else if (d.kind == DK_B && slot32) {
+        bslot[atomicAdd(&nbig[1], 1)] = (uint32_t)(d.slot >> 4);  // bitmaps: loaded in groups below
       } else {
-        big[atomicAdd(nbig, 1)] = (int)(s + j);
+        big[atomicAdd(&nbig[0], 1)] = (int)(s + j);
       }
     }
     __syncthreads();
-    const int nb = *nbig;
-    for (int k = 0; k < nb; k++) {
+    // bitmap containers: the loads of up to kBGroup are in flight together
+    const int nb = nbig[1];
+    for (int k = 0; k < nb; k += kBGroup) {
+      uint64_t x[kBGroup][4];
+#pragma unroll
+      for (int u = 0; u < kBGroup; u++)
+        if (k + u < nb) load_bitmap_owned(payload + ((uint64_t)bslot[k + u] << 4), x[u]);
+#pragma unroll
+      for (int u = 0; u < kBGroup; u++)
+        if (k + u < nb) {
+#pragma unroll
+          for (int i = 0; i < 4; i++) r[i] = MODE == 0 ? (r[i] | x[u][i]) : (r[i] ^ x[u][i]);
+        }
+    }
+    const int no = nbig[0];
+    for (int k = 0; k < no; k++) {
       const CDesc d = desc[big[k]];
       const uint8_t* slot = payload + d.slot;
-      if (d.kind == DK_B) {
+      if (d.kind == DK_B) {  // (payloads of 64 GiB and more)
         uint64_t x[4];
         load_bitmap_owned(slot, x);
 #pragma unroll
@@ -114,7 +136,8 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
   __shared__ __align__(16) uint32_t tmp[2048];
   __shared__ int q[257];
   __shared__ int big[NT];
-  __shared__ int nbig;
+  __shared__ int nbig[2];
+  __shared__ uint32_t bslot[NT];
   __shared__ int sh[8];
   __shared__ Prefix shp;
   const uint32_t nt = *n_tasks;
@@ -173,7 +196,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         lds_clear(acc);
 #pragma unroll
         for (int i = 0; i < 4; i++) r[i] = 0;
-        accumulate_segment<0>(A.desc, A.payload, s, n, acc, q, big, &nbig, r);
+        accumulate_segment<0>(A.desc, A.payload, s, n, acc, q, big, nbig, bslot, A.slot32 != 0, r);
         c = block_card(r, sh);
         if (MODE == WIDE_OR_CARD) {
           if (threadIdx.x == 0) task_card[t] = (uint32_t)c;
@@ -193,7 +216,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         lds_clear(acc);
 #pragma unroll
         for (int i = 0; i < 4; i++) r[i] = 0;
-        accumulate_segment<1>(A.desc, A.payload, s, n, acc, q, big, &nbig, r);
+        accumulate_segment<1>(A.desc, A.payload, s, n, acc, q, big, nbig, bslot, A.slot32 != 0, r);
         c = block_card(r, sh);
         if (c == 0) {
           wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
@@ -423,15 +446,85 @@ __device__ __forceinline__ uint32_t wave_and_card(const CDesc& x, const CDesc& y
   return c;
 }
 
-__global__ __launch_bounds__(256) void k_batch_and_card(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
-                                                        const CDesc* __restrict__ desc, const uint8_t* __restrict__ payload,
-                                                        int32_t* __restrict__ out) {
+// Batched andCardinality, planned: one thread per pair aligns the (few) keys of
+// small pairs (RoaringBitmap.andCardinality, RB/RoaringBitmap.java:402-420) and
+// emits one item per matched key; items then take one wave each.  Pairs with
+// more than kSmallPairKeys keys keep the wave-per-pair merge.
+constexpr uint32_t kSmallPairKeys = 64;
+
+// count (emit = false) or write (emit = true) the matched keys of pair p
+template <bool EMIT>
+__device__ __forceinline__ uint64_t pair_matches(uint64_t p, const uint32_t* bm_off, const uint16_t* keys,
+                                                 const uint64_t* off, PairItem* items, uint32_t* large) {
+  const uint32_t a0 = bm_off[2 * p], a1 = bm_off[2 * p + 1], b1 = bm_off[2 * p + 2];
+  if ((a1 - a0) + (b1 - a1) > kSmallPairKeys) {
+    if (EMIT) large[off[p] >> 32] = (uint32_t)p;
+    return 1ull << 32;
+  }
+  uint64_t q = EMIT ? (off[p] & 0xFFFFFFFFull) : 0;
+  uint32_t ia = a0, ib = a1, m = 0;
+  uint32_t ka = ia < a1 ? keys[ia] : 0, kb = ib < b1 ? keys[ib] : 0;
+  while (ia < a1 && ib < b1) {
+    if (ka == kb) {
+      if (EMIT) items[q++] = PairItem{(uint32_t)p, ia, ib};
+      m++;
+      ia++;
+      ib++;
+      if (ia < a1) ka = keys[ia];
+      if (ib < b1) kb = keys[ib];
+    } else if (ka < kb) {
+      if (++ia < a1) ka = keys[ia];
+    } else {
+      if (++ib < b1) kb = keys[ib];
+    }
+  }
+  return m;
+}
+
+__global__ __launch_bounds__(256) void k_pairs_count(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
+                                                     const uint16_t* __restrict__ keys, uint64_t* __restrict__ cnt) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n_pairs) cnt[p] = pair_matches<false>(p, bm_off, keys, nullptr, nullptr, nullptr);
+}
+
+__global__ __launch_bounds__(256) void k_pairs_emit(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
+                                                    const uint16_t* __restrict__ keys, const uint64_t* __restrict__ off,
+                                                    PairItem* __restrict__ items, uint32_t* __restrict__ large,
+                                                    int32_t* __restrict__ out) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n_pairs) return;
+  out[p] = 0;
+  pair_matches<true>(p, bm_off, keys, off, items, large);
+}
+
+// one wave per matched key; sums wrap like Java ints
+__global__ __launch_bounds__(256) void k_pair_items(const PairItem* __restrict__ items, const uint64_t* __restrict__ tot,
+                                                    const CDesc* __restrict__ desc, const uint8_t* __restrict__ payload,
+                                                    int32_t* __restrict__ out) {
   __shared__ __align__(16) uint32_t lds[4][2048];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (uint64_t p = (uint64_t)blockIdx.x * 4 + w; p < n_pairs; p += (uint64_t)gridDim.x * 4) {
+  const uint64_t n = *tot & 0xFFFFFFFFull;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + w; i < n; i += (uint64_t)gridDim.x * 4) {
+    const PairItem it = items[i];
+    const uint32_t c = wave_and_card(desc[it.ia], desc[it.ib], payload, lds[w], lane);
+    if (lane == 0 && c) atomicAdd(reinterpret_cast<uint32_t*>(out) + it.pair, c);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_batch_and_card_large(const uint32_t* __restrict__ large,
+                                                              const uint64_t* __restrict__ tot,
+                                                              const uint32_t* __restrict__ bm_off,
+                                                              const CDesc* __restrict__ desc,
+                                                              const uint8_t* __restrict__ payload,
+                                                              int32_t* __restrict__ out) {
+  __shared__ __align__(16) uint32_t lds[4][2048];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t n = *tot >> 32;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + w; i < n; i += (uint64_t)gridDim.x * 4) {
+    const uint32_t p = large[i];
     uint32_t ia = bm_off[2 * p], a1 = bm_off[2 * p + 1];
     uint32_t ib = a1, b1 = bm_off[2 * p + 2];
-    uint32_t sum = 0;  // Java int accumulation (wraps), RB/RoaringBitmap.java:414
+    uint32_t sum = 0;
     while (ia < a1 && ib < b1) {
       const CDesc da = desc[ia], db = desc[ib];
       if (da.key == db.key) {
@@ -448,12 +541,29 @@ __global__ __launch_bounds__(256) void k_batch_and_card(uint64_t n_pairs, const 
   }
 }
 
-void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const CDesc* desc,
-                           const uint8_t* payload, int32_t* out) {
-  uint64_t g = (n_pairs + 3) / 4;
-  if (g > 16384) g = 16384;
-  if (g == 0) return;
-  hipLaunchKernelGGL(k_batch_and_card, dim3((unsigned)g), dim3(256), 0, s, n_pairs, bm_off, desc, payload, out);
+void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const uint16_t* keys,
+                           const CDesc* desc, const uint8_t* payload, int32_t* out, uint64_t* cnt, uint64_t* part,
+                           uint64_t* tot, PairItem* items, uint32_t* large) {
+  if (n_pairs == 0) return;
+  const unsigned g = (unsigned)((n_pairs + 255) / 256);
+  hipLaunchKernelGGL(k_pairs_count, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, cnt);
+  launch_exclusive_scan(s, cnt, cnt, n_pairs, part, tot);
+  hipLaunchKernelGGL(k_pairs_emit, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, (const uint64_t*)cnt, items, large,
+                     out);
+  hipLaunchKernelGGL(k_pair_items, dim3(4096), dim3(256), 0, s, (const PairItem*)items, (const uint64_t*)tot, desc,
+                     payload, out);
+  hipLaunchKernelGGL(k_batch_and_card_large, dim3(1024), dim3(256), 0, s, (const uint32_t*)large,
+                     (const uint64_t*)tot, bm_off, desc, payload, out);
+}
+
+// upper bound of the items of a batch: sum over small pairs of min(keys of a, keys of b)
+uint64_t batch_pair_items_cap(const uint32_t* h_bm_nctr, uint64_t n_pairs) {
+  uint64_t cap = 0;
+  for (uint64_t p = 0; p < n_pairs; p++) {
+    const uint32_t na = h_bm_nctr[2 * p], nb = h_bm_nctr[2 * p + 1];
+    if (na + nb <= kSmallPairKeys) cap += std::min(na, nb);
+  }
+  return cap;
 }
 
 }  // namespace rbg

@@ -40,3 +40,30 @@ def test_c4_synthetic_pairs(gpu):
     assert sum(O.stats(x)["card"] for x in bms) == st["cardinality"]
     matched, allb = e.pair_bytes(b)
     assert 0 < matched <= allb
+
+
+def test_batch_and_card_large_and_mixed_pairs(gpu):
+    """Pairs above the 64-key small-pair threshold (one wave per pair) mixed with small
+    ones (one thread per pair aligns keys, one wave per matched key), every container
+    family, empty bitmaps included."""
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(4242)
+    pairs = []
+    for i in range(120):
+        if i % 4 == 0:
+            ka = np.sort(rng.choice(200, size=int(rng.integers(40, 120)), replace=False))
+            kb = np.sort(rng.choice(200, size=int(rng.integers(40, 120)), replace=False))
+        elif i % 4 == 1:
+            ka = np.sort(rng.choice(64, size=int(rng.integers(1, 30)), replace=False))
+            kb = np.sort(rng.choice(64, size=int(rng.integers(1, 30)), replace=False))
+        elif i % 4 == 2:
+            ka, kb = np.array([], dtype=np.int64), np.sort(rng.choice(64, size=3, replace=False))
+        else:
+            ka = np.sort(rng.choice(8, size=int(rng.integers(1, 8)), replace=False))
+            kb = ka
+        a = _gen.bitmap(rng, ka, p_present=1.0) if ka.size else O.from_values([])
+        b = _gen.bitmap(rng, kb, p_present=1.0) if kb.size else O.from_values([])
+        pairs.append((a, b))
+    got = rb.batch_and_cardinality([(rb.RoaringBitmap(a), rb.RoaringBitmap(b)) for a, b in pairs])
+    exp = np.array([O.pairwise_card("and", a, b) for a, b in pairs], dtype=np.int32)
+    np.testing.assert_array_equal(got, exp)
