@@ -94,8 +94,11 @@ void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, 
 // alignment (count, scan, emit), then one wave per matched key; pairs of more than 64
 // keys take one wave per pair.  Scratch: cnt (n_pairs u64), part (scan_parts(n_pairs)
 // u64), tot (u64: items | large pairs << 32), items (batch_pair_items_cap), large (n_pairs).
-struct PairItem {
-  uint32_t pair, ia, ib;
+struct PairItem {  // one matched key of a pair: both descriptors resolved (32 B, scalar-loaded)
+  uint64_t slot_a, slot_b;
+  uint32_t card_a, card_b;
+  uint32_t pair;
+  uint8_t kind_a, kind_b, pad0, pad1;
 };
 void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_off, const uint16_t* keys,
                            const CDesc* desc, const uint8_t* payload, int32_t* out, uint64_t* cnt, uint64_t* part,

@@ -455,7 +455,8 @@ constexpr uint32_t kSmallPairKeys = 64;
 // count (emit = false) or write (emit = true) the matched keys of pair p
 template <bool EMIT>
 __device__ __forceinline__ uint64_t pair_matches(uint64_t p, const uint32_t* bm_off, const uint16_t* keys,
-                                                 const uint64_t* off, PairItem* items, uint32_t* large) {
+                                                 const CDesc* desc, const uint64_t* off, PairItem* items,
+                                                 uint32_t* large) {
   const uint32_t a0 = bm_off[2 * p], a1 = bm_off[2 * p + 1], b1 = bm_off[2 * p + 2];
   if ((a1 - a0) + (b1 - a1) > kSmallPairKeys) {
     if (EMIT) large[off[p] >> 32] = (uint32_t)p;
@@ -466,7 +467,10 @@ __device__ __forceinline__ uint64_t pair_matches(uint64_t p, const uint32_t* bm_
   uint32_t ka = ia < a1 ? keys[ia] : 0, kb = ib < b1 ? keys[ib] : 0;
   while (ia < a1 && ib < b1) {
     if (ka == kb) {
-      if (EMIT) items[q++] = PairItem{(uint32_t)p, ia, ib};
+      if (EMIT) {
+        const CDesc da = desc[ia], db = desc[ib];
+        items[q++] = PairItem{da.slot, db.slot, da.card, db.card, (uint32_t)p, da.kind, db.kind, 0, 0};
+      }
       m++;
       ia++;
       ib++;
@@ -484,30 +488,86 @@ __device__ __forceinline__ uint64_t pair_matches(uint64_t p, const uint32_t* bm_
 __global__ __launch_bounds__(256) void k_pairs_count(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
                                                      const uint16_t* __restrict__ keys, uint64_t* __restrict__ cnt) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < n_pairs) cnt[p] = pair_matches<false>(p, bm_off, keys, nullptr, nullptr, nullptr);
+  if (p < n_pairs) cnt[p] = pair_matches<false>(p, bm_off, keys, nullptr, nullptr, nullptr, nullptr);
 }
 
 __global__ __launch_bounds__(256) void k_pairs_emit(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
-                                                    const uint16_t* __restrict__ keys, const uint64_t* __restrict__ off,
-                                                    PairItem* __restrict__ items, uint32_t* __restrict__ large,
-                                                    int32_t* __restrict__ out) {
+                                                    const uint16_t* __restrict__ keys, const CDesc* __restrict__ desc,
+                                                    const uint64_t* __restrict__ off, PairItem* __restrict__ items,
+                                                    uint32_t* __restrict__ large, int32_t* __restrict__ out) {
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n_pairs) return;
   out[p] = 0;
-  pair_matches<true>(p, bm_off, keys, off, items, large);
+  pair_matches<true>(p, bm_off, keys, desc, off, items, large);
 }
 
-// one wave per matched key; sums wrap like Java ints
+__device__ __forceinline__ PairItem load_item(const PairItem* items, uint64_t i) {
+  typedef const __attribute__((address_space(4))) uint64_t* CU64;
+  const CU64 q = reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(items + i));
+  union {
+    uint64_t u[4];
+    PairItem p;
+  } r;
+#pragma unroll
+  for (int k = 0; k < 4; k++) r.u[k] = q[k];
+  return r.p;
+}
+
+// |a & b| of two arrays of <= 512 values: both payloads requested at once (one
+// 16 B vector per lane each), the larger scattered into the wave's LDS map, the
+// smaller probed (RB/ArrayContainer.java:232-240 andCardinality)
+__device__ __forceinline__ uint32_t small_arrays_and_card(const uint8_t* pa, uint32_t ca, const uint8_t* pb,
+                                                         uint32_t cb, uint32_t* lds, int lane) {
+  const uint32_t na = (ca + 7) >> 3, nb = (cb + 7) >> 3;
+  const uint4 va = (uint32_t)lane < na ? reinterpret_cast<const uint4*>(pa)[lane] : make_uint4(0, 0, 0, 0);
+  const uint4 vb = (uint32_t)lane < nb ? reinterpret_cast<const uint4*>(pb)[lane] : make_uint4(0, 0, 0, 0);
+  uint4* l4 = reinterpret_cast<uint4*>(lds);
+#pragma unroll
+  for (int i = 0; i < 8; i++) l4[64 * i + lane] = make_uint4(0, 0, 0, 0);
+  wave_sync();
+  const bool a_map = ca >= cb;
+  scatter_vec<0>(lds, a_map ? va : vb, 8 * lane, (int)(a_map ? ca : cb));
+  wave_sync();
+  const uint4 v = a_map ? vb : va;
+  const int card = (int)(a_map ? cb : ca);
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
+    c += (8 * lane + i < card) ? ((lds[x >> 5] >> (x & 31)) & 1u) : 0u;
+  }
+  wave_sync();
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  return c;
+}
+
+// one wave per matched key (resident grid, the next item's record prefetched
+// through the scalar cache); sums wrap like Java ints
 __global__ __launch_bounds__(256) void k_pair_items(const PairItem* __restrict__ items, const uint64_t* __restrict__ tot,
-                                                    const CDesc* __restrict__ desc, const uint8_t* __restrict__ payload,
-                                                    int32_t* __restrict__ out) {
+                                                    const uint8_t* __restrict__ payload, int32_t* __restrict__ out) {
   __shared__ __align__(16) uint32_t lds[4][2048];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t n = *tot & 0xFFFFFFFFull;
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + w; i < n; i += (uint64_t)gridDim.x * 4) {
-    const PairItem it = items[i];
-    const uint32_t c = wave_and_card(desc[it.ia], desc[it.ib], payload, lds[w], lane);
-    if (lane == 0 && c) atomicAdd(reinterpret_cast<uint32_t*>(out) + it.pair, c);
+  const uint64_t stride = (uint64_t)gridDim.x * 4;
+  uint64_t i = (uint64_t)blockIdx.x * 4 + w;
+  if (i >= n) return;
+  PairItem cur = load_item(items, i);
+  for (;;) {
+    const uint64_t in = i + stride;
+    PairItem nxt;
+    if (in < n) nxt = load_item(items, in);
+    uint32_t c;
+    if (cur.kind_a == DK_A && cur.kind_b == DK_A && cur.card_a <= 512 && cur.card_b <= 512) {
+      c = small_arrays_and_card(payload + cur.slot_a, cur.card_a, payload + cur.slot_b, cur.card_b, lds[w], lane);
+    } else {
+      const CDesc da{cur.slot_a, cur.card_a, 0, cur.kind_a, 0}, db{cur.slot_b, cur.card_b, 0, cur.kind_b, 0};
+      c = wave_and_card(da, db, payload, lds[w], lane);
+    }
+    if (lane == 0 && c) atomicAdd(reinterpret_cast<uint32_t*>(out) + cur.pair, c);
+    if (in >= n) break;
+    i = in;
+    cur = nxt;
   }
 }
 
@@ -548,10 +608,10 @@ void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_o
   const unsigned g = (unsigned)((n_pairs + 255) / 256);
   hipLaunchKernelGGL(k_pairs_count, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, cnt);
   launch_exclusive_scan(s, cnt, cnt, n_pairs, part, tot);
-  hipLaunchKernelGGL(k_pairs_emit, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, (const uint64_t*)cnt, items, large,
-                     out);
-  hipLaunchKernelGGL(k_pair_items, dim3(4096), dim3(256), 0, s, (const PairItem*)items, (const uint64_t*)tot, desc,
-                     payload, out);
+  hipLaunchKernelGGL(k_pairs_emit, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, desc, (const uint64_t*)cnt, items,
+                     large, out);
+  hipLaunchKernelGGL(k_pair_items, dim3(resident_grid((const void*)&k_pair_items)), dim3(256), 0, s,
+                     (const PairItem*)items, (const uint64_t*)tot, payload, out);
   hipLaunchKernelGGL(k_batch_and_card_large, dim3(1024), dim3(256), 0, s, (const uint32_t*)large,
                      (const uint64_t*)tot, bm_off, desc, payload, out);
 }
