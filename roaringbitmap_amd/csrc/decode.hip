@@ -37,13 +37,16 @@ __device__ __forceinline__ uint32_t rd32b(const uint8_t* p) {
   return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
 }
 
+constexpr uint32_t kDecChunk = 1024;  // containers per wave of k_dec_ctrs
+
 // DecHead::flags
 constexpr uint32_t kHdRun = 1, kHdOffsets = 2, kHdOffTrunc = 4;
 
 __global__ __launch_bounds__(256) void k_dec_head(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ in_off,
                                                   const uint64_t* __restrict__ in_len, uint64_t n,
                                                   DecHead* __restrict__ hd, uint64_t* __restrict__ nctr,
-                                                  uint32_t* __restrict__ err, uint32_t* __restrict__ any_err) {
+                                                  uint64_t* __restrict__ nch, uint32_t* __restrict__ err,
+                                                  uint32_t* __restrict__ any_err) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* p = raw + in_off[i];
@@ -108,42 +111,60 @@ __global__ __launch_bounds__(256) void k_dec_head(const uint8_t* __restrict__ ra
   } while (0);
   hd[i] = h;
   nctr[i] = e ? 0 : (uint64_t)size;
+  nch[i] = e ? 0 : ((uint64_t)size + kDecChunk - 1) / kDecChunk;
   err[i] = e;
   if (e) atomicOr(any_err, 1u);
 }
 
+// chunk -> input table (thread per input)
+__global__ __launch_bounds__(256) void k_dec_chunk_map(const uint64_t* __restrict__ nch,
+                                                       const uint64_t* __restrict__ ch_base, uint64_t n,
+                                                       uint32_t* __restrict__ map) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t b = ch_base[i], c = nch[i];
+  for (uint64_t k = 0; k < c; k++) map[b + k] = (uint32_t)i;
+}
+
+// one wave per chunk of kDecChunk containers of one input: descriptors, key order,
+// and the offset table checked against the payload walk; per-input verdicts are
+// OR-ed into bm_flag (1: keys out of order, 2: offsets are not the walk)
 __global__ __launch_bounds__(256) void k_dec_ctrs(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ in_off,
-                                                  const uint64_t* __restrict__ in_len, uint64_t n,
-                                                  const DecHead* __restrict__ hd, const uint64_t* __restrict__ ctr_base,
-                                                  DecCtr* __restrict__ q, uint16_t* __restrict__ qkey,
-                                                  uint64_t* __restrict__ bm_card, uint64_t* __restrict__ consumed,
-                                                  uint32_t* __restrict__ err, uint32_t* __restrict__ any_err) {
+                                                  const uint64_t* __restrict__ in_len, const uint32_t* __restrict__ map,
+                                                  const uint64_t* __restrict__ ch_base, const uint64_t* __restrict__ tot,
+                                                  const DecHead* __restrict__ hd,
+                                                  const uint64_t* __restrict__ ctr_base, DecCtr* __restrict__ q,
+                                                  uint16_t* __restrict__ qkey, uint64_t* __restrict__ bm_card,
+                                                  uint32_t* __restrict__ bm_flag, uint64_t* __restrict__ consumed) {
   const uint64_t nw = (uint64_t)gridDim.x * 4;
+  const uint64_t n_chunks = *tot;
   const int lane = lane_id();
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
-    if (err[i]) continue;
+  for (uint64_t ch = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); ch < n_chunks; ch += nw) {
+    const uint32_t i = map[ch];
     const DecHead h = hd[i];
     const uint8_t* p = raw + in_off[i];
     const uint64_t len = in_len[i];
     const int size = h.size;
+    const int kbeg = (int)(ch - ch_base[i]) * (int)kDecChunk;
+    const int kend = min(size, kbeg + (int)kDecChunk);
     const uint64_t qb = ctr_base[i];
     const bool hasrun = h.flags & kHdRun;
     bool fast = (h.flags & kHdOffsets) && !(h.flags & kHdOffTrunc);
     bool bad_key = false;
-    uint64_t card_sum = 0, end = h.pay_pos;
-    for (int k0 = 0; k0 < size; k0 += 64) {
+    uint64_t card_sum = 0, end = 0;
+    for (int k0 = kbeg; k0 < kend; k0 += 64) {
       const int k = k0 + lane;
-      if (k < size) {
+      if (k < kend) {
         const uint8_t* d = p + h.desc_pos + 4 * (uint64_t)k;
         const uint32_t key = rd16b(d), card = rd16b(d + 2) + 1;
         if (k > 0 && rd16b(d - 4) >= key) bad_key = true;
         const bool isrun = hasrun && ((p[h.flags_pos + k / 8] >> (k % 8)) & 1);
-        const uint8_t kind = isrun ? DK_R : (card > 4096 ? DK_B : DK_A);
+        const uint32_t kind = isrun ? DK_R : (card > 4096 ? DK_B : DK_A);
         card_sum += card;
         DecCtr c;
         c.card = card;
         c.kind = kind;
-        c.bm = (uint32_t)i;
+        c.bm = i;
         c.src = 0;
         c.len = 0;
         if (fast) {
@@ -170,51 +191,73 @@ __global__ __launch_bounds__(256) void k_dec_ctrs(const uint8_t* __restrict__ ra
         q[qb + k] = c;
         qkey[qb + k] = (uint16_t)key;
       }
-      // wave-uniform verdicts
       bad_key = __ballot(bad_key) != 0;
       fast = __ballot(!fast) == 0;
     }
-    uint32_t e = DEC_OK;
-    if (bad_key) e = DEC_KEY_ORDER;
-    else if (h.flags & kHdOffTrunc) e = DEC_TRUNC_OFFSETS;
-    if (!e && !fast && lane == 0) {
-      // the reference's serial walk (RB/RoaringArray.java:593-629)
-      uint64_t pos = h.pay_pos;
-      for (int k = 0; k < size && !e; k++) {
-        DecCtr c = q[qb + k];
-        uint32_t l;
-        if (c.kind == DK_B) {
-          l = 8192;
-        } else if (c.kind == DK_R) {
-          if (len < pos + 2) {
-            e = DEC_TRUNC_RUNS;
-            break;
-          }
-          l = 2 + 4 * rd16b(p + pos);
-        } else {
-          l = 2 * c.card;
-        }
-        if (len < pos + l) {
-          e = DEC_TRUNC_PAYLOAD;
+    for (int o = 32; o > 0; o >>= 1) card_sum += (uint64_t)__shfl_xor((long long)card_sum, o, 64);
+    const uint64_t e_last = (uint64_t)__shfl((long long)end, (size - 1) & 63, 64);
+    if (lane == 0) {
+      atomicAdd(reinterpret_cast<unsigned long long*>(&bm_card[i]), (unsigned long long)card_sum);
+      const uint32_t f = (bad_key ? 1u : 0u) | (fast ? 0u : 2u);
+      if (f) atomicOr(&bm_flag[i], f);
+      if (kend == size && fast) consumed[i] = e_last;
+    }
+  }
+}
+
+// per input: the verdict in the reference's order, and the serial payload walk
+// (RB/RoaringArray.java:593-629) wherever the offset table was absent or not the walk
+__global__ __launch_bounds__(256) void k_dec_finish(const uint8_t* __restrict__ raw, const uint64_t* __restrict__ in_off,
+                                                    const uint64_t* __restrict__ in_len, uint64_t n,
+                                                    const DecHead* __restrict__ hd,
+                                                    const uint64_t* __restrict__ ctr_base,
+                                                    const uint32_t* __restrict__ bm_flag, DecCtr* __restrict__ q,
+                                                    uint64_t* __restrict__ consumed, uint32_t* __restrict__ err,
+                                                    uint32_t* __restrict__ any_err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n || err[i]) return;
+  const DecHead h = hd[i];
+  const uint32_t f = bm_flag[i];
+  uint32_t e = DEC_OK;
+  if (f & 1) {
+    e = DEC_KEY_ORDER;
+  } else if (h.flags & kHdOffTrunc) {
+    e = DEC_TRUNC_OFFSETS;
+  } else if (h.size == 0) {
+    consumed[i] = h.pay_pos;
+  } else if (f & 2) {
+    const uint8_t* p = raw + in_off[i];
+    const uint64_t len = in_len[i];
+    const uint64_t qb = ctr_base[i];
+    uint64_t pos = h.pay_pos;
+    for (int k = 0; k < h.size; k++) {
+      DecCtr c = q[qb + k];
+      uint32_t l;
+      if (c.kind == DK_B) {
+        l = 8192;
+      } else if (c.kind == DK_R) {
+        if (len < pos + 2) {
+          e = DEC_TRUNC_RUNS;
           break;
         }
-        c.src = in_off[i] + pos;
-        c.len = l;
-        q[qb + k] = c;
-        pos += l;
+        l = 2 + 4 * rd16b(p + pos);
+      } else {
+        l = 2 * c.card;
       }
-      end = pos;
+      if (len < pos + l) {
+        e = DEC_TRUNC_PAYLOAD;
+        break;
+      }
+      c.src = in_off[i] + pos;
+      c.len = l;
+      q[qb + k] = c;
+      pos += l;
     }
-    e = __shfl(e, 0, 64);
-    for (int o = 32; o > 0; o >>= 1) card_sum += (uint64_t)__shfl_xor((long long)card_sum, o, 64);
-    if (fast) end = (uint64_t)__shfl((long long)end, (size - 1) & 63, 64);
-    else end = (uint64_t)__shfl((long long)end, 0, 64);
-    if (lane == 0) {
-      err[i] = e;
-      if (e) atomicOr(any_err, 1u);
-      bm_card[i] = card_sum;
-      consumed[i] = size ? end : h.pay_pos;
-    }
+    consumed[i] = pos;
+  }
+  if (e) {
+    err[i] = e;
+    atomicOr(any_err, 1u);
   }
 }
 
@@ -295,18 +338,23 @@ static unsigned grid_of(uint64_t n, uint64_t per, uint64_t cap) {
 }
 
 void launch_dec_head(hipStream_t s, const uint8_t* raw, const uint64_t* in_off, const uint64_t* in_len, uint64_t n,
-                     DecHead* hd, uint64_t* nctr, uint32_t* err, uint32_t* any_err) {
+                     DecHead* hd, uint64_t* nctr, uint64_t* nch, uint32_t* err, uint32_t* any_err) {
   if (!n) return;
   hipLaunchKernelGGL(k_dec_head, dim3(grid_of(n, 256, 1u << 30)), dim3(256), 0, s, raw, in_off, in_len, n, hd, nctr,
-                     err, any_err);
+                     nch, err, any_err);
 }
 
 void launch_dec_ctrs(hipStream_t s, const uint8_t* raw, const uint64_t* in_off, const uint64_t* in_len, uint64_t n,
-                     const DecHead* hd, const uint64_t* ctr_base, DecCtr* q, uint16_t* qkey, uint64_t* bm_card,
-                     uint64_t* consumed, uint32_t* err, uint32_t* any_err) {
+                     const DecHead* hd, const uint64_t* ctr_base, const uint64_t* nch, const uint64_t* ch_base,
+                     const uint64_t* n_chunks, uint64_t max_chunks, uint32_t* map, DecCtr* q, uint16_t* qkey,
+                     uint64_t* bm_card, uint32_t* bm_flag, uint64_t* consumed, uint32_t* err, uint32_t* any_err) {
   if (!n) return;
-  hipLaunchKernelGGL(k_dec_ctrs, dim3(grid_of(n, 4, 8192)), dim3(256), 0, s, raw, in_off, in_len, n, hd, ctr_base, q,
-                     qkey, bm_card, consumed, err, any_err);
+  hipLaunchKernelGGL(k_dec_chunk_map, dim3(grid_of(n, 256, 1u << 30)), dim3(256), 0, s, nch, ch_base, n, map);
+  if (max_chunks)
+    hipLaunchKernelGGL(k_dec_ctrs, dim3(grid_of(max_chunks, 4, 8192)), dim3(256), 0, s, raw, in_off, in_len,
+                       (const uint32_t*)map, ch_base, n_chunks, hd, ctr_base, q, qkey, bm_card, bm_flag, consumed);
+  hipLaunchKernelGGL(k_dec_finish, dim3(grid_of(n, 256, 1u << 30)), dim3(256), 0, s, raw, in_off, in_len, n, hd,
+                     ctr_base, (const uint32_t*)bm_flag, q, consumed, err, any_err);
 }
 
 size_t dec_sort_temp_bytes(uint64_t C) {

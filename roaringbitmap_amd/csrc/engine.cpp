@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -11,6 +12,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <chrono>
 #include <vector>
 
 #include "../../include/roaring_mi355x.h"
@@ -53,8 +55,12 @@ static bool debug_sync() {
 }
 static void dbg(hipStream_t s, const char* what) {
   if (!debug_sync()) return;
+  static auto last = std::chrono::steady_clock::now();
   hipError_t e = hipStreamSynchronize(s);
-  std::fprintf(stderr, "[rbg] %s done: %s\n", what, hipGetErrorString(e));
+  const auto now = std::chrono::steady_clock::now();
+  std::fprintf(stderr, "[rbg] %s done: %s (+%.3f ms)\n", what, hipGetErrorString(e),
+               std::chrono::duration<double, std::milli>(now - last).count());
+  last = now;
   std::fflush(stderr);
 }  // look-back state: ticket @0, error word @64, statuses @256
 
@@ -103,7 +109,8 @@ struct Batch {
 };
 
 struct DecBufs {  // scratch of the device decode (decode.hip), reused across loads
-  DevBuf meta, head, nctr, base, err, card, cons, part, q, qkey, sort, skey, iota, perm, size, cpart;
+  DevBuf meta, head, nctr, base, nch, chbase, chmap, flag, err, card, cons, part, q, qkey, sort, skey, iota, perm,
+      size, cpart;
 };
 
 struct Ctx {
@@ -256,6 +263,65 @@ static int dec_report(Ctx* c, size_t n) {
   return RBG_ERR_DEVICE;
 }
 
+// Host side of an upload: the inputs are copied into pinned staging (worker
+// threads over <= 4 MiB pieces, in offset order) and each ~32 MiB group goes to the
+// device as soon as its pieces are staged, so the copies overlap the DMA.
+static int stage_upload(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, const uint64_t* dst_off,
+                        uint64_t raw_bytes) {
+  uint8_t* pin = reinterpret_cast<uint8_t*>(c->pinned);
+  uint8_t* dev = c->raw.as<uint8_t>();
+  hipStream_t s = c->stream;
+  constexpr uint64_t kPiece = 4ull << 20, kGroup = 32ull << 20;
+  if (raw_bytes <= kGroup) {
+    for (size_t i = 0; i < n; i++)
+      if (lens[i]) std::memcpy(pin + dst_off[i], bufs[i], lens[i]);
+    if (raw_bytes) HIPCHK(hipMemcpyAsync(dev, pin, raw_bytes, hipMemcpyHostToDevice, s));
+    return RBG_OK;
+  }
+  struct Piece {
+    uint64_t dst;
+    const uint8_t* src;
+    uint64_t len;
+    uint32_t g0, g1;  // groups the piece touches (pieces are smaller than a group)
+  };
+  std::vector<Piece> pieces;
+  for (size_t i = 0; i < n; i++)
+    for (uint64_t o = 0; o < lens[i]; o += kPiece) {
+      const uint64_t d = dst_off[i] + o;
+      const uint64_t l = std::min<uint64_t>(kPiece, lens[i] - o);
+      pieces.push_back(Piece{d, bufs[i] + o, l, (uint32_t)(d / kGroup), (uint32_t)((d + l - 1) / kGroup)});
+    }
+  const uint32_t groups = (uint32_t)((raw_bytes + kGroup - 1) / kGroup);
+  std::unique_ptr<std::atomic<int>[]> left(new std::atomic<int>[groups]);
+  for (uint32_t g = 0; g < groups; g++) left[g].store(0);
+  for (const Piece& p : pieces) {
+    left[p.g0].fetch_add(1);
+    if (p.g1 != p.g0) left[p.g1].fetch_add(1);
+  }
+  std::atomic<size_t> next{0};
+  const int nthr = (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthr; t++)
+    th.emplace_back([&]() {
+      for (size_t k; (k = next.fetch_add(1)) < pieces.size();) {
+        std::memcpy(pin + pieces[k].dst, pieces[k].src, pieces[k].len);
+        left[pieces[k].g0].fetch_sub(1, std::memory_order_release);
+        if (pieces[k].g1 != pieces[k].g0) left[pieces[k].g1].fetch_sub(1, std::memory_order_release);
+      }
+    });
+  int st = RBG_OK;
+  for (uint32_t g = 0; g < groups; g++) {
+    while (left[g].load(std::memory_order_acquire) > 0) std::this_thread::yield();
+    const uint64_t lo = (uint64_t)g * kGroup, hi = std::min<uint64_t>(raw_bytes, lo + kGroup);
+    if (st == RBG_OK && hipMemcpyAsync(dev + lo, pin + lo, hi - lo, hipMemcpyHostToDevice, s) != hipSuccess) {
+      set_err("host-to-device copy of the upload failed");
+      st = RBG_ERR_DEVICE;
+    }
+  }
+  for (auto& x : th) x.join();
+  return st;
+}
+
 // key_major: containers sorted by (key, input) with a key CSR (operands of every op);
 // otherwise input order (bitmap-major, batched andCardinality)
 static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, bool key_major,
@@ -275,24 +341,15 @@ static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens,
   }
   CHK(c->raw.ensure(raw_bytes + 64));
   CHK(pinned_ensure(c, raw_bytes + 64));
-  uint8_t* pin = reinterpret_cast<uint8_t*>(c->pinned);
-  const int nthr =
-      raw_bytes > (64u << 20) ? (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency())) : 1;
-  auto copy_range = [&](size_t t, size_t step) {
-    for (size_t i = t; i < n; i += step)
-      if (lens[i]) std::memcpy(pin + meta[i], bufs[i], lens[i]);
-  };
-  if (nthr == 1) {
-    copy_range(0, 1);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < nthr; t++) th.emplace_back(copy_range, (size_t)t, (size_t)nthr);
-    for (auto& x : th) x.join();
-  }
+  CHK(stage_upload(c, bufs, lens, n, meta.data(), raw_bytes));
+  dbg(s, "load: host staging copy");
   CHK(d.meta.ensure(8 * (2 * n + 2)));
   CHK(d.head.ensure(sizeof(DecHead) * n + 16));
   CHK(d.nctr.ensure(8 * n + 16));
   CHK(d.base.ensure(8 * n + 16));
+  CHK(d.nch.ensure(8 * n + 16));
+  CHK(d.chbase.ensure(8 * n + 16));
+  CHK(d.flag.ensure(4 * n + 16));
   CHK(d.err.ensure(4 * n + 16));
   CHK(d.card.ensure(8 * n + 16));
   CHK(d.cons.ensure(8 * n + 16));
@@ -300,18 +357,21 @@ static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens,
   CHK(c->scalar.ensure(64));
   const uint64_t* in_off = d.meta.as<uint64_t>();
   const uint64_t* in_len = in_off + n;
-  unsigned long long* sc = c->scalar.as<unsigned long long>();  // [0] any error, [1] C, [2..5] totals, [6] bytes
-  HIPCHK(hipMemcpyAsync(c->raw.p, pin, raw_bytes, hipMemcpyHostToDevice, s));
+  unsigned long long* sc = c->scalar.as<unsigned long long>();  // [0] any error, [1] C, [2..5] totals, [6] bytes,
+                                                                // [7] chunks
   HIPCHK(hipMemcpyAsync(d.meta.p, meta.data(), 8 * (2 * n + 2), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(sc, 0, 64, s));
+  dbg(s, "load: H2D");
   uint32_t* any_err = reinterpret_cast<uint32_t*>(sc);
   launch_dec_head(s, c->raw.as<uint8_t>(), in_off, in_len, n, d.head.as<DecHead>(), d.nctr.as<uint64_t>(),
-                  d.err.as<uint32_t>(), any_err);
+                  d.nch.as<uint64_t>(), d.err.as<uint32_t>(), any_err);
   launch_exclusive_scan(s, d.nctr.as<uint64_t>(), d.base.as<uint64_t>(), n, d.part.as<uint64_t>(),
                         reinterpret_cast<uint64_t*>(sc + 1));
+  launch_exclusive_scan(s, d.nch.as<uint64_t>(), d.chbase.as<uint64_t>(), n, d.part.as<uint64_t>(),
+                        reinterpret_cast<uint64_t*>(sc + 7));
   HIPCHK(hipGetLastError());
   unsigned long long h[8] = {};
-  HIPCHK(hipMemcpyAsync(h, sc, 16, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(h, sc, 64, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   if (h[0]) return dec_report(c, n);
   const uint64_t C = h[1];
@@ -319,11 +379,17 @@ static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens,
     set_err("a batch holds at most 2^31 - 1 containers");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
+  dbg(s, "load: headers");
+  const uint64_t n_chunks = h[7];
   CHK(d.q.ensure(sizeof(DecCtr) * C + 16));
   CHK(d.qkey.ensure(2 * C + 16));
+  CHK(d.chmap.ensure(4 * n_chunks + 16));
+  HIPCHK(hipMemsetAsync(d.card.p, 0, 8 * n + 16, s));
+  HIPCHK(hipMemsetAsync(d.flag.p, 0, 4 * n + 16, s));
   launch_dec_ctrs(s, c->raw.as<uint8_t>(), in_off, in_len, n, d.head.as<DecHead>(), d.base.as<uint64_t>(),
-                  d.q.as<DecCtr>(), d.qkey.as<uint16_t>(), d.card.as<uint64_t>(), d.cons.as<uint64_t>(),
-                  d.err.as<uint32_t>(), any_err);
+                  d.nch.as<uint64_t>(), d.chbase.as<uint64_t>(), reinterpret_cast<uint64_t*>(sc + 7), n_chunks,
+                  d.chmap.as<uint32_t>(), d.q.as<DecCtr>(), d.qkey.as<uint16_t>(), d.card.as<uint64_t>(),
+                  d.flag.as<uint32_t>(), d.cons.as<uint64_t>(), d.err.as<uint32_t>(), any_err);
   const int32_t id = new_batch(c);
   Batch& b = *c->batches[id];
   BatchGuard guard{c, {id}};  // dropped unless the load completes
@@ -354,6 +420,7 @@ static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens,
     }
     launch_dec_key_off(s, sorted, C, b.key_off.as<uint32_t>());
   }
+  dbg(s, "load: containers + sort");
   CHK(d.size.ensure(8 * C + 16));
   CHK(d.cpart.ensure(8 * (scan_parts(std::max<uint64_t>(C, 1)) + 1)));
   launch_dec_sizes(s, d.q.as<DecCtr>(), perm, C, d.size.as<uint64_t>(), sc + 2);
@@ -367,6 +434,7 @@ static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens,
   b.max_ser = h[5];
   b.payload_bytes = h[6];
   CHK(b.payload.ensure(b.payload_bytes + 64));
+  dbg(s, "load: sizes + payload alloc");
   launch_dec_fill(s, c->raw.as<uint8_t>(), d.q.as<DecCtr>(), d.qkey.as<uint16_t>(), perm, d.size.as<uint64_t>(), C,
                   b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.bm.as<uint32_t>(), b.payload.as<uint8_t>());
   HIPCHK(hipGetLastError());
@@ -389,6 +457,7 @@ static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens,
   }
   HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
+  dbg(s, "load: fill + readback");
   guard.ids.clear();
   b.live = true;
   *out_id = id;

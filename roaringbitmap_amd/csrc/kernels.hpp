@@ -167,10 +167,12 @@ struct DecCtr {  // per container, input order
   uint32_t kind;
 };
 void launch_dec_head(hipStream_t s, const uint8_t* raw, const uint64_t* in_off, const uint64_t* in_len, uint64_t n,
-                     DecHead* hd, uint64_t* nctr, uint32_t* err, uint32_t* any_err);
+                     DecHead* hd, uint64_t* nctr, uint64_t* nch, uint32_t* err, uint32_t* any_err);
+// bm_card and bm_flag zeroed by the caller; *n_chunks = sum of nch (device), max_chunks its host bound
 void launch_dec_ctrs(hipStream_t s, const uint8_t* raw, const uint64_t* in_off, const uint64_t* in_len, uint64_t n,
-                     const DecHead* hd, const uint64_t* ctr_base, DecCtr* q, uint16_t* qkey, uint64_t* bm_card,
-                     uint64_t* consumed, uint32_t* err, uint32_t* any_err);
+                     const DecHead* hd, const uint64_t* ctr_base, const uint64_t* nch, const uint64_t* ch_base,
+                     const uint64_t* n_chunks, uint64_t max_chunks, uint32_t* map, DecCtr* q, uint16_t* qkey,
+                     uint64_t* bm_card, uint32_t* bm_flag, uint64_t* consumed, uint32_t* err, uint32_t* any_err);
 size_t dec_sort_temp_bytes(uint64_t C);
 // stable sort of the container keys: perm[p] = input-order index of key-major position p
 int launch_dec_sort(hipStream_t s, void* temp, size_t temp_bytes, const uint16_t* qkey, uint16_t* skey,
