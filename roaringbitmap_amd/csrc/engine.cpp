@@ -1,5 +1,6 @@
 // Host side of the MI355X Roaring engine: device contexts, batch upload
-// (parse -> raw H2D -> GPU ingest into the slotted arena), op pipelines and
+// (staged H2D of the serialized bytes -> device decode into the slotted arena,
+// decode.hip), op pipelines and
 // the exported C ABI of include/roaring_mi355x.h.
 #include <hip/hip_runtime.h>
 
@@ -123,7 +124,7 @@ struct Ctx {
   uint64_t* ztile = nullptr;
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
   int bsi_nbits = 0;
-  DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw, items,
+  DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw,
       scalar, scratch;
   size_t result_cap = 0;
   OutCtx pending{};         // output state of the last materialising op

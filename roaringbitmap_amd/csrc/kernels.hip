@@ -216,28 +216,8 @@ __global__ __launch_bounds__(1024) void k_reduce_card(const uint32_t* __restrict
 }
 
 // ===========================================================================
-// ingest: raw serialized buffers -> slotted payload arena (one wave per container)
+// batch statistics
 // ===========================================================================
-__global__ __launch_bounds__(256) void k_ingest(const uint8_t* __restrict__ raw, const IngestItem* __restrict__ items,
-                                                uint64_t n_items, uint8_t* __restrict__ payload) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
-  for (uint64_t i = wave; i < n_items; i += nw) {
-    const IngestItem it = items[i];
-    uint8_t* dst = payload + it.dst + (it.kind == DK_R ? 2 : 0);
-    group_copy<64>(dst, raw + it.src, it.len, lane);
-    if (it.kind == DK_A && it.len) {
-      // pad the slot to 16 B with copies of the last value: a run of A slots is
-      // then a plain u16 value stream that OR-type reductions can scatter whole
-      const uint16_t last = (uint16_t)(raw[it.src + it.len - 2] | (raw[it.src + it.len - 1] << 8));
-      uint16_t* d16 = reinterpret_cast<uint16_t*>(payload + it.dst);
-      const uint32_t v0 = it.len / 2, v1 = ((it.len + 15) & ~15u) / 2;
-      for (uint32_t v = v0 + lane; v < v1; v += 64) d16[v] = last;
-    }
-  }
-}
-
 // serialized payload bytes of a batch (for statistics)
 __global__ __launch_bounds__(256) void k_batch_bytes(const CDesc* __restrict__ desc, uint64_t n,
                                                      const uint8_t* __restrict__ payload,
@@ -407,12 +387,6 @@ void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, ui
 }
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info) {
   hipLaunchKernelGGL(k_reduce_card, dim3(1), dim3(1024), 0, s, task_card, nt, info);
-}
-void launch_ingest(hipStream_t s, const uint8_t* raw, const IngestItem* items, uint64_t n, uint8_t* payload) {
-  uint64_t g = (n + 3) / 4;
-  if (g > 8192) g = 8192;
-  if (g == 0) return;
-  hipLaunchKernelGGL(k_ingest, dim3((unsigned)g), dim3(256), 0, s, raw, items, n, payload);
 }
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload,
                         unsigned long long* out) {

@@ -8,13 +8,6 @@ namespace rbg {
 
 enum OpCode : int { OP_AND = 0, OP_OR = 1, OP_XOR = 2, OP_ANDNOT = 3 };
 
-struct IngestItem {  // one container copy raw -> arena slot
-  uint64_t src;  // byte offset in the raw upload
-  uint64_t dst;  // slot byte offset in the payload arena
-  uint32_t len;  // serialized payload length
-  uint32_t kind;
-};
-
 // wide-op flavours (wide.hip)
 enum WideMode : int {
   WIDE_OR = 0,         // FastAggregation.naive_or
@@ -81,7 +74,6 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info);
 void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out);
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info);
-void launch_ingest(hipStream_t s, const uint8_t* raw, const IngestItem* items, uint64_t n, uint8_t* payload);
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload, unsigned long long* out);
 
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,

@@ -191,7 +191,7 @@ __global__ __launch_bounds__(256) void k_runopt_write(const CDesc* __restrict__ 
         w_store_bitmap(dst, x);
       } else {
         uint32_t copy = w_stage(kind, x, (int)d.card, lds);
-        if (kind == DK_A) {  // pad the slot to 16 B with the last value (ingest layout)
+        if (kind == DK_A) {  // pad the slot to 16 B with the last value (batch layout)
           uint16_t* st = reinterpret_cast<uint16_t*>(lds);
           const uint32_t c = d.card, padded = (2u * c + 15) & ~15u;
           const uint16_t last = st[c - 1];
