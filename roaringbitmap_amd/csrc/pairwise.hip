@@ -74,6 +74,12 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* _
 }
 
 constexpr int kWaves = 4;  // waves per workgroup
+// u32 words of LDS per wave: the 8 KiB bitmap map / staging area, plus room for
+// the run lists of run-domain R AND R (4 waves x 10 KiB x 4 workgroups = 160 KiB)
+#ifndef RBG_WAVE_LDS
+#define RBG_WAVE_LDS 2560
+#endif
+constexpr int kWaveLds = RBG_WAVE_LDS;
 
 // Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
 // pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
@@ -227,6 +233,122 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
     filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, oc, task_card, lds SACC_ARG);
 }
 
+// R AND R in the run domain (RB/RunContainer.java and(RunContainer)): the
+// intersection of two sorted disjoint run lists is the list of overlaps of their
+// runs, already canonical.  Both run lists go to the wave's LDS as
+// (start | end << 16) -- kWaveLds u32 words hold na + nb runs -- and the lanes
+// split the merge path evenly (rr_merge).  Pass 1 counts runs and cardinality; the type is EFF
+// (App. A.1); an R result is written by pass 2 straight into the task's scratch
+// slot.  Returns false (nothing written) when the result is not a run container or
+// the runs do not fit: the bitmap path then runs.
+// Merge path over the run ends: step d of the two-pointer intersection advances
+// whichever current run ends first (A on ties); every overlapping pair of runs is
+// current at exactly one step, and overlaps come out in ascending order.  Lane l
+// takes steps [d0, d1) of na + nb, found by a binary search on the diagonal.
+template <bool EMIT>
+__device__ __forceinline__ void rr_merge(const uint32_t* al, int na, const uint32_t* bl, int nb, int d0, int d1,
+                                         int& cnt, int& card, uint32_t* out) {
+  int lo = max(0, d0 - nb), hi = min(d0, na);
+  while (lo < hi) {
+    const int m = (lo + hi) >> 1;
+    if ((al[m] >> 16) <= (bl[d0 - m - 1] >> 16)) lo = m + 1;
+    else hi = m;
+  }
+  int i = lo, j = d0 - lo;
+  // current and next run of each side in registers: the LDS read of a side's
+  // next-but-one run is off the step's dependency chain
+  uint32_t a = i < na ? al[i] : 0, b = j < nb ? bl[j] : 0;
+  uint32_t an = i + 1 < na ? al[i + 1] : 0, bn = j + 1 < nb ? bl[j + 1] : 0;
+  for (int d = d0; d < d1 && i < na && j < nb; d++) {
+    const int as = (int)(a & 0xFFFF), ae = (int)(a >> 16), bs = (int)(b & 0xFFFF), be = (int)(b >> 16);
+    const int s0 = max(as, bs), e0 = min(ae, be);
+    if (s0 <= e0) {
+      if (EMIT) out[cnt] = (uint32_t)s0 | ((uint32_t)(e0 - s0) << 16);
+      cnt++;
+      card += e0 - s0 + 1;
+    }
+    if (ae <= be) {
+      i++;
+      a = an;
+      an = i + 1 < na ? al[i + 1] : 0;
+    } else {
+      j++;
+      b = bn;
+      bn = j + 1 < nb ? bl[j + 1] : 0;
+    }
+  }
+}
+
+// run list of a slot -> LDS as (start | end << 16), from 16 B slot vectors (vector q
+// holds runs 4q - 1 .. 4q + 2; run -1 is the pad and count)
+__device__ __forceinline__ void run_vec_to_lds(const uint4 v, int q, int n, uint32_t* dst) {
+  const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const int r = 4 * q + c - 1;
+    if (r >= 0 && r < n) dst[r] = (u[c] & 0xFFFF) | (min((u[c] & 0xFFFF) + (u[c] >> 16), 65535u) << 16);
+  }
+}
+
+// both operands' run lists, all of a round's vectors requested before any is used
+__device__ __forceinline__ void runs_to_lds2(const uint8_t* sa, int na, uint32_t* da, const uint8_t* sb, int nb,
+                                             uint32_t* db) {
+  constexpr int R = 4;
+  const int l = lane_id();
+  const int nva = (na + 4) >> 2, nvb = (nb + 4) >> 2;
+  const uint4* a4 = reinterpret_cast<const uint4*>(sa);
+  const uint4* b4 = reinterpret_cast<const uint4*>(sb);
+#pragma unroll 1
+  for (int j0 = 0; 64 * j0 < max(nva, nvb); j0 += R) {
+    uint4 va[R], vb[R];
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      const int q = 64 * (j0 + j) + l;
+      va[j] = q < nva ? a4[q] : make_uint4(0, 0, 0, 0);
+      vb[j] = q < nvb ? b4[q] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      const int q = 64 * (j0 + j) + l;
+      run_vec_to_lds(va[j], q, na, da);
+      run_vec_to_lds(vb[j], q, nb, db);
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
+                                            const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
+  const int na = tk.nruns_a, nb = tk.nruns_b;
+  if (na + nb > kWaveLds) return false;
+  const int l = lane_id();
+  wsync();
+  runs_to_lds2(pa + tk.slot_a, na, lds, pb + tk.slot_b, nb, lds + na);
+  wsync();
+  const int d0 = (l * (na + nb)) >> 6, d1 = ((l + 1) * (na + nb)) >> 6;
+  int cnt = 0, card = 0;
+  rr_merge<false>(lds, na, lds + na, nb, d0, d1, cnt, card, nullptr);
+  const int c = (int)uni((uint32_t)wave_sum_i(card));
+  if (MODE == 1) {
+    if (l == 0) task_card[t] = (uint32_t)c;
+    return true;
+  }
+  if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389)
+    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
+    return true;
+  }
+  int nr;
+  const int off = wave_excl(cnt, &nr);
+  nr = (int)uni((uint32_t)nr);
+  if (eff(c, nr) != DK_R) return false;
+  uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+  int cnt2 = 0, card2 = 0;
+  rr_merge<true>(lds, na, lds + na, nb, d0, d1, cnt2, card2, reinterpret_cast<uint32_t*>(slot + 4) + off);
+  if (l == 0) *reinterpret_cast<uint16_t*>(slot + 2) = (uint16_t)nr;
+  w_place(t, true, slot + 2, false, lds, 2u + 4u * (uint32_t)nr, (uint32_t)c, tk.key, DK_R, oc);
+  return true;
+}
+
 // Bitmap-class task: both operands in registers (16 words per lane), combined,
 // counted, typed (App. A) and written out (B straight from registers, A and R
 // staged in LDS).  One wave, wave-uniform branches.
@@ -236,6 +358,9 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
   const int l = lane_id();
   const int ka = tk.kind_a, kb = tk.kind_b;
   const int ca = (int)tk.card_a, cb = (int)tk.card_b;
+#if !RBG_NO_RR_RUNS
+  if (OP == OP_AND && ka == DK_R && kb == DK_R && rr_and_task<MODE>(t, tk, pa, pb, oc, task_card, lds)) return;
+#endif
   STAMP_DECL
   WCtr x;
 #if RBG_BPRE
@@ -316,7 +441,7 @@ template <int OP, int MODE>
 __global__ __launch_bounds__(256, RBG_PW_BLOCKS) void k_pair_wave(const PTask* __restrict__ tasks,
                                                       const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
                                                       const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card) {
-  __shared__ __align__(16) uint32_t lds_all[kWaves][2048];
+  __shared__ __align__(16) uint32_t lds_all[kWaves][kWaveLds];
   const int w = threadIdx.x >> 6;
   uint32_t* lds = lds_all[w];
   const uint32_t nt = uni(*n_tasks);
