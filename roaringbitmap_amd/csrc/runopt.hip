@@ -118,6 +118,38 @@ __device__ __forceinline__ uint64_t slot_size_of(int kind, uint32_t ser_len) {
   return kind == DK_R ? (uint64_t)((ser_len + 2 + 15) & ~15u) : (uint64_t)((ser_len + 15) & ~15u);
 }
 
+// number of runs of a sorted array (<= 4096 values): 16 B vectors, all requested
+// at once; a value starts a run unless it follows its predecessor (the predecessor
+// of a vector's first value is the last value of the previous vector: the previous
+// lane's, or lane 63's of the previous round)
+__device__ __forceinline__ int array_runs(const uint8_t* slot, int card) {
+  const int l = lane_id();
+  const int nvec = (card + 7) >> 3;  // <= 512
+  const uint4* v4 = reinterpret_cast<const uint4*>(slot);
+  uint4 v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) v[j] = 64 * j + l < nvec ? v4[64 * j + l] : make_uint4(0, 0, 0, 0);
+  int c = 0;
+  uint32_t carry = 0;  // last value of the previous round (lane 63)
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    if (64 * j >= nvec) break;  // wave-uniform
+    const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    const uint32_t prev_last = from_prev_lane(w[3] >> 16);
+    uint32_t prev = l == 0 ? carry : prev_last;
+    const int first = 8 * (64 * j + l);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
+      const int idx = first + i;
+      if (idx < card) c += (idx == 0 || x != prev + 1) ? 1 : 0;
+      prev = x;
+    }
+    carry = lane63u(w[3] >> 16);
+  }
+  return (int)uni((uint32_t)wave_sum_i(c));
+}
+
 // info word: kind | changed << 2 | nruns << 3
 __global__ __launch_bounds__(256) void k_runopt_plan(const CDesc* __restrict__ desc, const uint32_t* __restrict__ bm,
                                                      const uint8_t* __restrict__ payload, uint64_t n,
@@ -132,10 +164,7 @@ __global__ __launch_bounds__(256) void k_runopt_plan(const CDesc* __restrict__ d
     const int card = (int)d.card;
     int nruns, kind;
     if (d.kind == DK_A) {
-      const uint16_t* v = reinterpret_cast<const uint16_t*>(slot);
-      int c = 0;
-      for (int j = lane_id(); j < card; j += 64) c += (j == 0) || (v[j] != (uint16_t)(v[j - 1] + 1));
-      nruns = (int)uni((uint32_t)wave_sum_i(c));
+      nruns = array_runs(slot, card);
       kind = 2 * card > 2 + 4 * nruns ? DK_R : DK_A;
     } else if (d.kind == DK_B) {
       WCtr x;

@@ -10,7 +10,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-RX='k_pair|k_emit|k_compact|k_plan|k_place|k_wide|k_batch|k_bsi'
+RX='k_pair|k_emit|k_compact|k_plan|k_place|k_wide|k_batch|k_bsi|k_dec|k_runopt|k_scan'
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/kt -o run -- python3 bench.py $ARGS > $OUT/bench_kt.json 2> $OUT/kt.err || { echo "kt failed"; tail $OUT/kt.err; exit 1; }
 echo "kernel trace done"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --kernel-include-regex "$RX" --output-format csv -d $OUT/pmc_fetch -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --c3-n 2000 --c4-pairs 200000 --c5-rows 100000000 > /dev/null 2> $OUT/pmc_fetch.err || { echo "fetch failed"; tail $OUT/pmc_fetch.err; exit 1; }
