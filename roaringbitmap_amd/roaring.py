@@ -287,6 +287,51 @@ class FastAggregation:
         return _wide_card("or", bms)
 
 
+    # The priority-queue / horizontal variants (RB/FastAggregation.java:110-300, 677-822)
+    # compute the same sets as or / xor.  horizontal_or(Iterator) is naive_or itself
+    # (:110-112), so its bytes are the reference's; for the List / varargs forms and
+    # priorityqueue_*, whose per-key container types follow their own lazyOR chains,
+    # the result is set-equal to the reference's with FastAggregation.or / xor types.
+    @staticmethod
+    def horizontal_or(*args):
+        if len(args) == 1 and isinstance(args[0], Iterator):
+            return _wide("or", list(args[0]))
+        bms = list(args[0]) if len(args) == 1 and isinstance(args[0], (list, tuple)) else list(args)
+        return _wide("or", bms)
+
+    @staticmethod
+    def priorityqueue_or(*args):
+        return FastAggregation.horizontal_or(*args)
+
+    @staticmethod
+    def horizontal_xor(*bitmaps):
+        return _wide("xor", list(bitmaps))
+
+    @staticmethod
+    def priorityqueue_xor(*bitmaps):
+        return _wide("xor", list(bitmaps))
+
+
+class ParallelAggregation:
+    """RB/ParallelAggregation.java: or (:161-175) and xor (:182-195).
+
+    The reference's ForkJoin reduction is the CPU baseline of this path.  Its sets are
+    FastAggregation's; its per-key container types depend on the pool's parallelism
+    for keys with 512 or more containers (:218-223), so byte parity is defined
+    against FastAggregation -- these return FastAggregation.or /
+    xor results, which the reference's own ParallelAggregationTest accepts (it
+    compares sets)."""
+
+    @staticmethod
+    def or_(*bitmaps):
+        return _wide("or", list(bitmaps))
+
+    @staticmethod
+    def xor(*bitmaps):
+        return _wide("xor", list(bitmaps))
+
+
+setattr(ParallelAggregation, "or", ParallelAggregation.or_)
 setattr(FastAggregation, "and", FastAggregation.and_)
 setattr(FastAggregation, "or", FastAggregation.or_)
 

@@ -99,3 +99,26 @@ def test_wide_realdata(gpu, run_opt):
         assert got.getLongCardinality() == known[ds]["wide_or"]
         got = rb.FastAggregation.and_(iter([rb.RoaringBitmap(b) for b in bufs]))
         assert got.getLongCardinality() == known[ds]["wide_and"]
+
+
+def test_parallel_and_horizontal_aggregation_sets(gpu):
+    """ParallelAggregation.or/xor and FastAggregation.horizontal_*/priorityqueue_* give the
+    reference's sets (RBT/ParallelAggregationTest compares sets); horizontal_or(Iterator)
+    is naive_or itself, byte for byte."""
+    import numpy as np
+    import roaringbitmap_amd as rb
+    import _gen
+    import _oracle as O
+    rng = np.random.default_rng(77)
+    bufs = [_gen.bitmap(rng, np.sort(rng.choice(40, size=int(rng.integers(1, 12)), replace=False)))
+            for _ in range(9)]
+    bms = [rb.RoaringBitmap(b) for b in bufs]
+    union = set(O.to_values(O.wide("or", bufs)).tolist())
+    sym = set(O.to_values(O.wide("xor", bufs)).tolist())
+    for got in (getattr(rb.ParallelAggregation, "or")(*bms), rb.FastAggregation.horizontal_or(bms),
+                rb.FastAggregation.horizontal_or(*bms), rb.FastAggregation.priorityqueue_or(*bms)):
+        assert set(got.toArray().tolist()) == union
+    for got in (rb.ParallelAggregation.xor(*bms), rb.FastAggregation.horizontal_xor(*bms),
+                rb.FastAggregation.priorityqueue_xor(*bms)):
+        assert set(got.toArray().tolist()) == sym
+    assert rb.FastAggregation.horizontal_or(iter(bms)).serialize() == O.wide("or", bufs)
