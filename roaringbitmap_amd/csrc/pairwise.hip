@@ -80,6 +80,7 @@ constexpr int kWaves = 4;  // waves per workgroup
 #define RBG_WAVE_LDS 2560
 #endif
 constexpr int kWaveLds = RBG_WAVE_LDS;
+static_assert(kWaveLds >= 2048 + 32, "filter compaction keeps per-lane dummy slots past the 8 KiB map");
 
 // Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
 // pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
@@ -179,26 +180,42 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
     if (l == 0) task_card[t] = (uint32_t)c;
     return;
   }
-  // the map is dead: compact the kept values over it, then 16 B stores
+  // the map is dead: compact the kept values over it, then 16 B stores.  Vectors
+  // j and j+1 share one scan (16-bit count fields); every value is written, the
+  // dropped ones to a per-lane dummy past the map, so the writes need no branches.
   uint16_t* st = reinterpret_cast<uint16_t*>(lds);
+  const uint32_t dummy = 4096u + (uint32_t)l;  // u16 index in the wave's LDS past the 8 KiB map
   wsync();
   int base = 0;
 #pragma unroll
-  for (int j = 0; j < 8; j++) {
+  for (int j = 0; j < 8; j += 2) {
     if (512 * j >= pcard) break;  // wave-uniform
     int tot;
-    int q = base + wave_excl(__popc(hit[j]), &tot);
-    const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+    const int ex = wave_excl(__popc(hit[j]) | (__popc(hit[j + 1]) << 16), &tot);
+    int q0 = base + (ex & 0xFFFF);
+    int q1 = base + (tot & 0xFFFF) + (ex >> 16);
 #pragma unroll
-    for (int i = 0; i < 8; i++)
-      if ((hit[j] >> i) & 1u) st[q++] = (uint16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF);
-    base += tot;
+    for (int h = 0; h < 2; h++) {
+      const uint32_t hj = hit[j + h];
+      int q = h == 0 ? q0 : q1;
+      const uint32_t w[4] = {v[j + h].x, v[j + h].y, v[j + h].z, v[j + h].w};
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint32_t keep = (hj >> i) & 1u;
+        st[keep ? (uint32_t)q : dummy] = (uint16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF);
+        q += (int)keep;
+      }
+    }
+    base += (tot & 0xFFFF) + (tot >> 16);
   }
   const int c = (int)uni((uint32_t)base);
   wsync();
   uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
   const uint4* sv = reinterpret_cast<const uint4*>(lds);
   uint4* dv = reinterpret_cast<uint4*>(slot);
+#if RBG_EXP_NOSTORE
+  if (c == 0x7FFFFFFF)  // experiment: (almost) never store the filter output
+#endif
   for (int k = l; k < (2 * c + 15) >> 4; k += 64) dv[k] = sv[k];  // the slot has room for the rounded tail
   STAMP(5);
   // empty results are dropped (RB/RoaringBitmap.java:389,456)
