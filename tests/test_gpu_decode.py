@@ -113,3 +113,30 @@ def test_malformed_inputs_match_host_errors(gpu):
         assert ge[0] is he[0] and ge[1] == "input 1: " + he[1], (len(buf), he, ge)
         checked += 1
     assert checked > 100
+
+
+def test_multi_chunk_inputs(gpu):
+    """Inputs of more than 1,024 containers span several decode waves: keys, cards and
+    payload positions across chunk boundaries, with and without run containers, and an
+    offset table corrupted in the second chunk (the serial walk takes over)."""
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+    rng = np.random.default_rng(99)
+    big = []
+    for modes in (["a_tiny", "a_small", "b_edge"], ["a_tiny", "r_few", "r_mid", "a_32"]):
+        keys = np.sort(rng.choice(1 << 16, size=3000, replace=False))
+        big.append(_gen.bitmap(rng, keys, modes=modes, p_present=1.0))
+    x = big[0]  # no run containers: offset table always present
+    size = struct.unpack_from("<I", x, 4)[0]
+    y = bytearray(x)
+    struct.pack_into("<I", y, 8 + 4 * size + 4 * 1500, 7)  # offset of container 1500
+    b = e.load(big + [bytes(y)])
+    for i, want in enumerate(big + [x]):
+        assert e.batch_fetch(b, i).serialize() == want
+    st = e.batch_stats(b)
+    assert st["cardinality"] == sum(O.stats(v)["card"] for v in big + [x])
+    e.release(b)
+    # truncation inside the second chunk
+    ge = _gpu_error(e, [big[1][: len(big[1]) - 5]])
+    assert ge is not None and ge == (_host_error(big[1][: len(big[1]) - 5])[0],
+                                     "input 0: " + _host_error(big[1][: len(big[1]) - 5])[1])

@@ -140,3 +140,44 @@ def test_bad_inputs_raise_ioerror(gpu, i):
     good = encode([])
     with pytest.raises(OSError):
         rb.RoaringBitmap._pair("and", rb.RoaringBitmap(bad), rb.RoaringBitmap(good))
+
+
+def _run_vals(rng, nruns, lo=0, hi=65536, min_len=1, max_len=None):
+    """Sorted values forming exactly `nruns` disjoint, non-adjacent runs inside [lo, hi)."""
+    span = hi - lo
+    seg = span // nruns
+    vals = []
+    for i in range(nruns):
+        s0 = lo + i * seg
+        ml = max_len if max_len else max(1, seg // 2)
+        ln = int(rng.integers(min_len, max(min_len, min(ml, seg - 1)) + 1))
+        st = s0 + int(rng.integers(0, max(1, seg - ln)))
+        vals.append(np.arange(st, min(st + ln, s0 + seg - 1)))
+    return np.unique(np.concatenate(vals))
+
+
+@pytest.mark.parametrize("na,nb", [(1, 1), (1, 2000), (2000, 1), (1279, 1281), (1280, 1280), (1281, 1280),
+                                   (2047, 2047), (700, 900), (2, 3)])
+def test_run_and_run_domain_boundaries(gpu, na, nb):
+    """R AND R: the run-domain merge (na + nb <= 2560 runs) and the bitmap fallback
+    above it give the oracle's bytes; also full containers, runs touching 0 and 65535,
+    and results that EFF turns into arrays or bitmaps."""
+    import roaringbitmap_amd as rb
+    from _fmt import R, encode
+    rng = np.random.default_rng(na * 7919 + nb)
+    cases = []
+    a = _run_vals(rng, na)
+    b = _run_vals(rng, nb)
+    cases.append((a, b))
+    cases.append((np.arange(65536), b))                                  # full container
+    cases.append((np.concatenate([np.arange(0, 10), np.arange(65500, 65536)]), a))  # edges
+    if na == nb:
+        cases.append((a, a))                                             # identical
+        cases.append((a, np.setdiff1d(np.arange(65536), a)))             # disjoint: empty
+    for x, y in cases:
+        bx = encode([(5, R, x), (9, R, y)])
+        by = encode([(5, R, y), (9, R, x)])
+        got = rb.RoaringBitmap.and_(rb.RoaringBitmap(bx), rb.RoaringBitmap(by)).serialize()
+        assert got == O.pairwise("and", bx, by)
+        assert rb.RoaringBitmap.andCardinality(rb.RoaringBitmap(bx), rb.RoaringBitmap(by)) == \
+            O.pairwise_card("and", bx, by)
