@@ -100,6 +100,7 @@ struct OutCtx {
   ORec* recs;
   uint8_t* scratch;  // scan placement: one kSlotBytes slot per task (null = look-back placement)
   uint64_t* tile_status;  // scan placement: per-tile look-back words
+  uint64_t* tile_card;    // scan placement: per-tile result cardinality
   uint32_t* tile_ticket;
 };
 

@@ -176,7 +176,7 @@ static int ctx_init(Ctx* c, int device) {
   CHK(c->tasks.ensure(sizeof(PTask) * kMaxKeys));
   CHK(c->ntasks.ensure(64));
   CHK(c->wg_count.ensure(4 * 256));
-  CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + kMaxTiles)));
+  CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + 2 * kMaxTiles)));
   CHK(c->recs.ensure(sizeof(ORec) * kMaxKeys));
   CHK(c->kind_by_out.ensure(kMaxKeys));
   CHK(c->scalar.ensure(64));
@@ -495,6 +495,7 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   oc->tile_ticket = reinterpret_cast<uint32_t*>(lb + 128);
   oc->status = reinterpret_cast<uint64_t*>(lb + kLbHeader);
   oc->tile_status = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * kMaxKeys);
+  oc->tile_card = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * (kMaxKeys + kMaxTiles));
   oc->recs = c->recs.as<ORec>();
   c->serialized = false;
   c->pending_ub = 0;

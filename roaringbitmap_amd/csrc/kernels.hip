@@ -235,95 +235,147 @@ __global__ __launch_bounds__(256) void k_batch_bytes(const CDesc* __restrict__ d
 // ===========================================================================
 constexpr int kTile = 1024;  // tasks per workgroup tile (4 per thread)
 
+// Look-back of tile t over all earlier tiles at once (t < 64): lane i reads the
+// status of tile t - 1 - i; the nearest inclusive status ends the window, and every
+// status before it must at least hold its aggregate (else spin).  Lane 0 then
+// publishes t's inclusive status.  One wave.
+__device__ __forceinline__ Prefix lookback_wave(uint64_t* status, uint32_t t, uint32_t cnt, uint64_t bytes,
+                                                uint32_t run, uint32_t* err) {
+  const int lane = lane_id();
+  if (lane == 0)
+    __hip_atomic_store(status + t, lb_pack(t == 0 ? 2 : 1, run, cnt, bytes), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t acc_cnt = 0, acc_bytes = 0, acc_run = 0;
+  if (t != 0) {
+    const int j = (int)t - 1 - lane;
+    uint32_t spins = 0;
+    for (;;) {
+      const uint64_t sv = j >= 0 ? __hip_atomic_load(status + j, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                                 : (2ull << 62);  // before tile 0: an empty inclusive prefix
+      const uint32_t st = (uint32_t)(sv >> 62);
+      const uint64_t incl = __ballot(st == 2);  // lane t-1-0 ... : the nearest inclusive is the lowest lane
+      const int k = __builtin_ctzll(incl);       // exists: lane t (tile -1) is always inclusive
+      const uint64_t window = k >= 63 ? ~0ull : ((2ull << k) - 1);
+      if ((__ballot(st == 0) & window) == 0) {
+        const bool in = lane <= k;
+        uint64_t c = in ? (sv >> 44) & 0x1FFFF : 0, by = in ? sv & ((1ULL << 44) - 1) : 0;
+        const uint32_t r = in ? (uint32_t)((sv >> 61) & 1) : 0u;
+        for (int o = 32; o > 0; o >>= 1) {
+          c += __shfl_xor(c, o, 64);
+          by += __shfl_xor(by, o, 64);
+        }
+        acc_cnt = c;
+        acc_bytes = by;
+        acc_run = __ballot(r != 0) ? 1 : 0;
+        break;
+      }
+      if (++spins > (1u << 22)) {
+        if (lane == 0) atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0)
+      __hip_atomic_store(status + t, lb_pack(2, run | acc_run, cnt + acc_cnt, bytes + acc_bytes), __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return Prefix{(uint32_t)acc_cnt, acc_bytes};
+}
+
+// One workgroup per tile of kTile task records (all tiles resident: <= 64), in
+// blockIdx order: counts, payload bytes and run flags scanned in the workgroup and
+// across tiles by lookback_wave; each tile's result cardinality goes to tile_card
+// before its status is published, and the last tile sums them.
 __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_tasks, OutCtx oc, ResultInfo* __restrict__ info) {
   __shared__ int wsum[3][4];
   __shared__ unsigned long long wbytes[4];
+  __shared__ unsigned long long wcard[4];
   __shared__ Prefix shp;
-  __shared__ uint32_t tsh;
   const uint32_t nt = *n_tasks;
   const uint32_t ntiles = (nt + kTile - 1) / kTile;
   if (nt == 0) {
     if (blockIdx.x == 0 && threadIdx.x == 0) write_info(info, oc, 0, 0, 0);
     return;
   }
-  for (;;) {
-    __syncthreads();
-    if (threadIdx.x == 0) tsh = atomicAdd(oc.tile_ticket, 1u);
-    __syncthreads();
-    const uint32_t tile = uni(tsh);
-    if (tile >= ntiles) break;
-    const uint32_t t0 = tile * kTile + 4 * threadIdx.x;
-    uint32_t keep[4], len[4], run[4];
-    uint32_t c = 0, r = 0;
-    unsigned long long b = 0;
-    uint32_t card = 0;  // <= 4 x 65536 per thread
+  const uint32_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  const uint32_t t0 = tile * kTile + 4 * threadIdx.x;
+  uint32_t keep[4], len[4], run[4];
+  uint32_t c = 0, r = 0;
+  unsigned long long b = 0;
+  uint32_t card = 0;  // <= 4 x 65536 per thread
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      keep[i] = len[i] = run[i] = 0;
-      if (t0 + i < nt) {
-        const ORec x = oc.recs[t0 + i];
-        keep[i] = x.keep;
-        len[i] = x.keep ? x.ser_len : 0;
-        run[i] = x.keep && x.kind == DK_R;
-        card += x.keep ? x.card : 0;
-      }
-      c += keep[i];
-      b += len[i];
-      r |= run[i];
+  for (int i = 0; i < 4; i++) {
+    keep[i] = len[i] = run[i] = 0;
+    if (t0 + i < nt) {
+      const ORec x = oc.recs[t0 + i];
+      keep[i] = x.keep;
+      len[i] = x.keep ? x.ser_len : 0;
+      run[i] = x.keep && x.kind == DK_R;
+      card += x.keep ? x.card : 0;
     }
-    // result cardinality: per-wave sum, one 64-bit atomic per wave (read by ctx_info)
-    {
-      const int cw = wave_sum_i((int)(card >> 4));  // 64 x 2^14 fits an int
-      const int lw = wave_sum_i((int)(card & 15));
-      if ((threadIdx.x & 63) == 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(oc.err) + kCardWord,
-                  ((unsigned long long)(uint32_t)cw << 4) + (uint32_t)lw);
+    c += keep[i];
+    b += len[i];
+    r |= run[i];
+  }
+  // workgroup exclusive scan of (count, bytes), OR of run, sum of cardinality
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int tc;
+  const int pc = wave_excl((int)c, &tc);
+  unsigned long long sb = b;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long u = __shfl_up(sb, o, 64);
+    if (lane >= o) sb += u;
+  }
+  const unsigned long long wb = __shfl(sb, 63, 64);
+  unsigned long long cw = card;
+  for (int o = 32; o > 0; o >>= 1) cw += __shfl_xor(cw, o, 64);
+  const int wr = __any(r) ? 1 : 0;
+  if (lane == 0) {
+    wsum[0][w] = tc;
+    wsum[1][w] = wr;
+    wbytes[w] = wb;
+    wcard[w] = cw;
+  }
+  __syncthreads();
+  uint32_t oc_c = 0, tot_c = 0, tot_r = 0;
+  unsigned long long oc_b = 0, tot_b = 0, tot_card = 0;
+  for (int i = 0; i < 4; i++) {
+    if (i < w) {
+      oc_c += wsum[0][i];
+      oc_b += wbytes[i];
     }
-    // workgroup exclusive scan of (count, bytes), OR of run
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int tc;
-    const int pc = wave_excl((int)c, &tc);
-    unsigned long long sb = b;
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned long long u = __shfl_up(sb, o, 64);
-      if (lane >= o) sb += u;
-    }
-    const unsigned long long wb = __shfl(sb, 63, 64);
-    const int wr = __any(r) ? 1 : 0;
-    if (lane == 0) {
-      wsum[0][w] = tc;
-      wsum[1][w] = wr;
-      wbytes[w] = wb;
-    }
-    __syncthreads();
-    uint32_t oc_c = 0, tot_c = 0, tot_r = 0;
-    unsigned long long oc_b = 0, tot_b = 0;
-    for (int i = 0; i < 4; i++) {
-      if (i < w) {
-        oc_c += wsum[0][i];
-        oc_b += wbytes[i];
-      }
-      tot_c += wsum[0][i];
-      tot_b += wbytes[i];
-      tot_r |= wsum[1][i];
-    }
-    if (threadIdx.x < 64) {
-      const Prefix pw = lookback(oc.tile_status, tile, tot_c, tot_b, tot_r, oc.err);
-      if (threadIdx.x == 0) shp = pw;
-    }
-    __syncthreads();
-    uint32_t idx = shp.idx + oc_c + (uint32_t)pc;
-    unsigned long long off = shp.off + oc_b + (sb - b);
+    tot_c += wsum[0][i];
+    tot_b += wbytes[i];
+    tot_r |= wsum[1][i];
+    tot_card += wcard[i];
+  }
+  if (threadIdx.x < 64) {
+    if (threadIdx.x == 0) oc.tile_card[tile] = tot_card;  // published by the release store of the status
+    const Prefix pw = lookback_wave(oc.tile_status, tile, tot_c, tot_b, tot_r, oc.err);
+    if (threadIdx.x == 0) shp = pw;
+  }
+  __syncthreads();
+  uint32_t idx = shp.idx + oc_c + (uint32_t)pc;
+  unsigned long long off = shp.off + oc_b + (sb - b);
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if (t0 + i < nt) {
-        oc.recs[t0 + i].idx = idx;
-        oc.recs[t0 + i].off = off;
-      }
-      idx += keep[i];
-      off += len[i];
+  for (int i = 0; i < 4; i++) {
+    if (t0 + i < nt) {
+      oc.recs[t0 + i].idx = idx;
+      oc.recs[t0 + i].off = off;
     }
-    if (tile == ntiles - 1 && threadIdx.x == 0) {
+    idx += keep[i];
+    off += len[i];
+  }
+  if (tile == ntiles - 1 && threadIdx.x < 64) {
+    // every earlier tile is published (its status was read as aggregate or inclusive,
+    // with acquire): sum the tile cardinalities
+    unsigned long long cs = threadIdx.x == 0 ? tot_card : 0;
+    if (threadIdx.x < tile)
+      cs += __hip_atomic_load(oc.tile_card + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int o = 32; o > 0; o >>= 1) cs += __shfl_xor(cs, o, 64);
+    if (threadIdx.x == 0) {
+      reinterpret_cast<unsigned long long*>(oc.err)[kCardWord] = cs;
       // totals word where the header kernels look for it (status[n_tasks - 1])
       const uint64_t incl = __hip_atomic_load(oc.tile_status + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(oc.status + nt - 1, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
