@@ -117,6 +117,8 @@ struct DecBufs {  // scratch of the device decode (decode.hip), reused across lo
 struct Ctx {
   int device = 0;
   DecBufs dec;
+  DevBuf wg_epoch;         // pairwise plan: per-workgroup task counts tagged with the op epoch
+  uint32_t epoch = 0;
   DevBuf pc_cnt, pc_part, pc_items, pc_large;  // batched andCardinality scratch
   hipStream_t stream = nullptr;
   std::vector<std::unique_ptr<Batch>> batches;
@@ -176,6 +178,8 @@ static int ctx_init(Ctx* c, int device) {
   CHK(c->tasks.ensure(sizeof(PTask) * kMaxKeys));
   CHK(c->ntasks.ensure(64));
   CHK(c->wg_count.ensure(4 * 256));
+  CHK(c->wg_epoch.ensure(8 * 256));
+  HIPCHK(hipMemset(c->wg_epoch.p, 0, 8 * 256));
   CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + 2 * kMaxTiles)));
   CHK(c->recs.ensure(sizeof(ORec) * kMaxKeys));
   CHK(c->kind_by_out.ensure(kMaxKeys));
@@ -198,6 +202,12 @@ static int pinned_ensure(Ctx* c, size_t bytes) {
 static inline uint64_t round16(uint64_t x) { return (x + 15) & ~15ULL; }
 static inline uint64_t slot_bytes(uint8_t kind, uint32_t ser_len) {
   return kind == KR ? round16(ser_len + 2) : round16(ser_len);
+}
+
+// epoch of the next pairwise plan (never 0, the value the tags start from)
+static uint32_t next_epoch(Ctx* c) {
+  if (++c->epoch == 0) ++c->epoch;
+  return c->epoch;
 }
 
 static int get_batch(Ctx* c, int32_t id, Batch** out) {
@@ -571,8 +581,8 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   c->mark(0);
   dbg(s, "memset");
   launch_plan_pairwise(s, plan_op, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), B->key_off.as<uint32_t>(),
-                       db, B->payload.as<uint8_t>(), c->by_key.as<PTask>(), c->flag.as<uint8_t>(),
-                       c->wg_count.as<uint32_t>(), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), c->zlb, c->ztile);
+                       db, B->payload.as<uint8_t>(), c->wg_epoch.as<uint64_t>(), next_epoch(c), c->tasks.as<PTask>(),
+                       c->ntasks.as<uint32_t>(), c->zlb, c->ztile, oc.err);
   dbg(s, "compact");
   c->mark(1);
   const int grid = grid_for((ub + 3) / 4, 16384);  // 4 waves (tasks) per workgroup, clamped to the resident grid

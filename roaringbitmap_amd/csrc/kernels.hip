@@ -424,10 +424,6 @@ void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, cons
                     uint32_t* n_tasks) {
   hipLaunchKernelGGL(k_compact<Task>, dim3(256), dim3(256), 0, s, flag, by_key, wg_count, tasks, n_tasks);
 }
-void launch_compact(hipStream_t s, const uint8_t* flag, const PTask* by_key, const uint32_t* wg_count, PTask* tasks,
-                    uint32_t* n_tasks) {
-  hipLaunchKernelGGL(k_compact<PTask>, dim3(256), dim3(256), 0, s, flag, by_key, wg_count, tasks, n_tasks);
-}
 
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info) {
   hipLaunchKernelGGL(k_place, dim3(64), dim3(256), 0, s, nt, oc, info);

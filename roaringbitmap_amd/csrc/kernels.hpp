@@ -55,16 +55,15 @@ void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t
 void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
                     uint32_t* n_tasks);
 // pairwise.hip: plan (key alignment + descriptor resolution) and the wave-per-key compute
-// plan + compact: tasks[] in key order, *n_tasks
+// plan + compaction in one launch: tasks[] in key order, *n_tasks.  wg_epoch: 256 u64
+// (zeroed once per context), epoch: unique per op of the context.
 void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
-                          const uint32_t* kob, const CDesc* db, const uint8_t* pb, PTask* by_key, uint8_t* flag,
-                          uint32_t* wg_count, PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile);
+                          const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_epoch, uint32_t epoch,
+                          PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile, uint32_t* err);
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
                      const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card);
 // diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
 void debug_stamps(uint64_t* out20, bool reset);
-void launch_compact(hipStream_t s, const uint8_t* flag, const PTask* by_key, const uint32_t* wg_count, PTask* tasks,
-                    uint32_t* n_tasks);
 void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
                  uint32_t* task_card);
 // result materialisation: k_place = compaction scan over the task records

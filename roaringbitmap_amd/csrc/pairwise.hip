@@ -48,12 +48,19 @@ __device__ __forceinline__ int pair_class(int op, int ka, int kb) {
 }
 
 // RB/RoaringBitmap.java:382-400 (and), :864-896 (or), :1076-1113 (xor), :449-471 (andNot)
+// One thread per key, 256 workgroups of 256 keys, all resident.  Each workgroup
+// publishes its task count tagged with this op's epoch, sums the counts of the
+// workgroups before it (one per thread, waiting for the epoch), and writes its
+// tasks straight into the dense task list -- plan and compaction in one launch.
 __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* __restrict__ koa,
                                                        const CDesc* __restrict__ da, const uint8_t* __restrict__ pa,
                                                        const uint32_t* __restrict__ kob,
                                                        const CDesc* __restrict__ db, const uint8_t* __restrict__ pb,
-                                                       PTask* __restrict__ by_key, uint8_t* __restrict__ flag,
-                                                       uint32_t* __restrict__ wg_count, uint64_t* zlb, uint64_t* ztile) {
+                                                       uint64_t* __restrict__ wg_epoch, uint32_t epoch,
+                                                       PTask* __restrict__ tasks, uint32_t* __restrict__ n_tasks,
+                                                       uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
+  __shared__ int wt[4];
+  __shared__ int wb[4];
   plan_zero(zlb, ztile);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   PTask t;
@@ -68,9 +75,37 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* _
     case OP_ANDNOT: f = ia; break;
     default: f = ia && ib; break;  // AND and andCardinality
   }
-  flag[k] = (uint8_t)f;
-  by_key[k] = t;
-  plan_count(f, wg_count);
+  int tot;
+  const int lane_pre = wave_excl(f, &tot);
+  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = tot;
+  __syncthreads();
+  const int cnt = wt[0] + wt[1] + wt[2] + wt[3];
+  if (threadIdx.x == 0)
+    __hip_atomic_store(wg_epoch + blockIdx.x, ((uint64_t)epoch << 32) | (uint32_t)cnt, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  // counts of the workgroups before this one
+  uint32_t c = 0;
+  if (threadIdx.x < blockIdx.x) {
+    uint64_t v;
+    uint32_t spins = 0;
+    while (((v = __hip_atomic_load(wg_epoch + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
+           epoch) {
+      if (++spins > (1u << 22)) {
+        atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    c = (uint32_t)v;
+  }
+  const int sw = wave_sum_i((int)c);
+  if ((threadIdx.x & 63) == 0) wb[threadIdx.x >> 6] = sw;
+  __syncthreads();
+  const uint32_t base = (uint32_t)(wb[0] + wb[1] + wb[2] + wb[3]);
+  int wpre = 0;
+  for (int i = 0; i < (int)(threadIdx.x >> 6); i++) wpre += wt[i];
+  if (f) tasks[base + wpre + lane_pre] = t;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_tasks = base + cnt;
 }
 
 constexpr int kWaves = 4;  // waves per workgroup
@@ -544,11 +579,10 @@ void debug_stamps(uint64_t* out20, bool) {
 #endif
 
 void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
-                          const uint32_t* kob, const CDesc* db, const uint8_t* pb, PTask* by_key, uint8_t* flag,
-                          uint32_t* wg_count, PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile) {
-  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, koa, da, pa, kob, db, pb, by_key, flag, wg_count,
-                     zlb, ztile);
-  launch_compact(s, flag, by_key, wg_count, tasks, n_tasks);
+                          const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_epoch, uint32_t epoch,
+                          PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
+  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, koa, da, pa, kob, db, pb, wg_epoch, epoch, tasks,
+                     n_tasks, zlb, ztile, err);
 }
 
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
