@@ -294,10 +294,17 @@ __global__ __launch_bounds__(256) void k_dec_sizes(const DecCtr* __restrict__ q,
     for (int k = 0; k < 3; k++) cnt[k] += (uint64_t)__shfl_xor((long long)cnt[k], o, 64);
     big += (uint64_t)__shfl_xor((long long)big, o, 64);
   }
+  // workgroup totals, one atomic per counter per workgroup
+  __shared__ unsigned long long wsum[4][4];
   if (lane_id() == 0) {
-    for (int k = 0; k < 3; k++)
-      if (cnt[k]) atomicAdd(&totals[k], (unsigned long long)cnt[k]);
-    if (big) atomicAdd(&totals[3], (unsigned long long)big);
+    for (int k = 0; k < 3; k++) wsum[threadIdx.x >> 6][k] = cnt[k];
+    wsum[threadIdx.x >> 6][3] = big;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const unsigned long long v =
+        wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] + wsum[3][threadIdx.x];
+    if (v) atomicAdd(&totals[threadIdx.x], v);
   }
 }
 
@@ -378,7 +385,7 @@ void launch_dec_key_off(hipStream_t s, const uint16_t* skey, uint64_t C, uint32_
 void launch_dec_sizes(hipStream_t s, const DecCtr* q, const uint32_t* perm, uint64_t C, uint64_t* size,
                       unsigned long long* totals) {
   if (!C) return;
-  hipLaunchKernelGGL(k_dec_sizes, dim3(grid_of(C, 256, 4096)), dim3(256), 0, s, q, perm, C, size, totals);
+  hipLaunchKernelGGL(k_dec_sizes, dim3(grid_of(C, 256, 1024)), dim3(256), 0, s, q, perm, C, size, totals);
 }
 
 void launch_dec_fill(hipStream_t s, const uint8_t* raw, const DecCtr* q, const uint16_t* qkey, const uint32_t* perm,

@@ -179,15 +179,27 @@ __global__ __launch_bounds__(256) void k_runopt_plan(const CDesc* __restrict__ d
     if (lane_id() == 0) {
       info[i] = (uint32_t)kind | ((kind != d.kind) ? 4u : 0u) | ((uint32_t)nruns << 3);
       size[i] = slot_size_of(kind, len);
-      if (kind == DK_R) bm_has_run[bm[i]] = 1;
+      // one bitmap can own every container: read before writing, so the flag's line
+      // takes a few stores rather than one per run container
+      if (kind == DK_R) {
+        uint32_t* f = bm_has_run + bm[i];
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) *f = 1;
+      }
     }
     cnt[kind]++;
     ser += len;
   }
+  // workgroup totals, one atomic per counter per workgroup
+  __shared__ unsigned long long wsum[4][4];
   if (lane_id() == 0) {
-    for (int k = 0; k < 3; k++)
-      if (cnt[k]) atomicAdd(&totals[k], (unsigned long long)cnt[k]);
-    if (ser) atomicAdd(&totals[3], (unsigned long long)ser);
+    for (int k = 0; k < 3; k++) wsum[threadIdx.x >> 6][k] = cnt[k];
+    wsum[threadIdx.x >> 6][3] = ser;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const unsigned long long v =
+        wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] + wsum[3][threadIdx.x];
+    if (v) atomicAdd(&totals[threadIdx.x], v);
   }
 }
 
@@ -239,7 +251,7 @@ __global__ __launch_bounds__(256) void k_runopt_write(const CDesc* __restrict__ 
 void launch_runopt_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
                         uint32_t* info, uint64_t* size, uint32_t* bm_has_run, unsigned long long* totals) {
   if (!n) return;
-  const uint64_t g = std::min<uint64_t>((n + 3) / 4, 8192);
+  const uint64_t g = std::min<uint64_t>((n + 3) / 4, 2048);
   hipLaunchKernelGGL(k_runopt_plan, dim3((unsigned)g), dim3(256), 0, s, desc, bm, payload, n, info, size, bm_has_run,
                      totals);
 }
