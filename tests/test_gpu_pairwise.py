@@ -181,3 +181,23 @@ def test_run_and_run_domain_boundaries(gpu, na, nb):
         assert got == O.pairwise("and", bx, by)
         assert rb.RoaringBitmap.andCardinality(rb.RoaringBitmap(bx), rb.RoaringBitmap(by)) == \
             O.pairwise_card("and", bx, by)
+
+
+@pytest.mark.parametrize("na,nb", [(1, 1), (1, 2000), (1279, 1281), (1281, 1280), (700, 900), (2, 3)])
+def test_run_or_run(gpu, na, nb):
+    """R OR R: overlapping, adjacent (coalescing) and nested runs, full containers,
+    identical operands, many-run operands."""
+    import roaringbitmap_amd as rb
+    from _fmt import R, encode
+    rng = np.random.default_rng(na * 31 + nb)
+    a = _run_vals(rng, na)
+    b = _run_vals(rng, nb)
+    adj = np.concatenate([np.arange(0, 100), np.arange(300, 400)])
+    adj2 = np.concatenate([np.arange(100, 300), np.arange(400, 401), np.arange(65000, 65536)])
+    for x, y in [(a, b), (a, a), (np.arange(65536), b), (adj, adj2), (adj2, adj), (a, np.arange(10, 20))]:
+        bx = encode([(5, R, x), (9, R, y)])
+        by = encode([(5, R, y), (9, R, x)])
+        got = rb.RoaringBitmap.or_(rb.RoaringBitmap(bx), rb.RoaringBitmap(by)).serialize()
+        assert got == O.pairwise("or", bx, by)
+        assert rb.RoaringBitmap.orCardinality(rb.RoaringBitmap(bx), rb.RoaringBitmap(by)) == \
+            O.pairwise_card("or", bx, by)
