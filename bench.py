@@ -324,6 +324,28 @@ def main():
     ph_avg = [x / max(n_ops, 1) for x in ph]
 
     c3 = {}
+    # RoaringBitmap.andCardinality on the same pair: the same input bytes,
+    # no result containers
+    for _ in range(args.warmup):
+        eng.and_cardinality(a, b)
+    eng.sync()
+    t0c = time.perf_counter()
+    for _ in range(args.steps):
+        eng.and_cardinality(a, b)
+    eng.sync()
+    card_wall = (time.perf_counter() - t0c) / args.steps
+    eng.profile(args.steps)
+    for _ in range(args.steps):
+        eng.and_cardinality(a, b)
+    kc, phc = eng.profile_read()
+    eng.profile(0)
+    card_kern = phc[1] / max(kc, 1)
+    c3["c2_and_cardinality"] = {
+        "workload": "RoaringBitmap.andCardinality on the C2 pair (device-resident)",
+        "ms_per_step": round(card_wall * 1e3, 4), "input_GBps": round(in_bytes / card_wall / 1e9, 1),
+        "roofline": {"kernel": "k_pair_wave<AND, card>", "kernel_ms": round(card_kern, 4),
+                     "achieved_GBps": round(in_bytes / (card_kern / 1e3) / 1e9, 1),
+                     "frac": round(in_bytes / (card_kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}}
     if args.c3_n > 0:
         for kind, name in ((1, "c3_uniform_or"), (2, "c3_clustered_or")):
             c3[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev)
