@@ -200,12 +200,19 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
     if (512 * j < pcard) {  // wave-uniform
       const int first = 8 * (64 * j + l);
       const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+      // 5 VALU per value: bit-field word index + address, shift, place (the
+      // hardware shift reads only the low 5 bits, so no masking); the tail of
+      // the array is masked once per vector, not per value
+      uint32_t h = 0;
 #pragma unroll
       for (int i = 0; i < 8; i++) {
-        const uint32_t x = (w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF;
-        const uint32_t m = (lds[x >> 5] >> (x & 31)) & 1u;
-        hit[j] |= (((OP == OP_ANDNOT) ? (m ^ 1u) : m) & (first + i < pcard ? 1u : 0u)) << i;
+        const uint32_t wi = w[i >> 1];
+        const uint32_t word = lds[(i & 1) ? bfe_hi_word(wi) : bfe_lo_word(wi)];
+        h |= bit_at(word, (i & 1) ? (wi >> 16) : wi) << i;
       }
+      if (OP == OP_ANDNOT) h = ~h & 0xFFu;
+      const int rem = pcard - first;
+      hit[j] = rem >= 8 ? h : h & ((1u << max(rem, 0)) - 1u);
       cnt += __popc(hit[j]);
     }
   }

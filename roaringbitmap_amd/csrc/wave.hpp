@@ -13,12 +13,48 @@ namespace rbg {
 
 constexpr int WL = 64;  // lanes per wave
 
+#ifndef RBG_OPAQUE_LANE
+#define RBG_OPAQUE_LANE 0
+#endif
+#if RBG_OPAQUE_LANE
+// Lane index the compiler cannot hoist: every use recomputes it (2 VALU), so
+// lane-derived addresses are rebuilt per task instead of being held in VGPRs for
+// the whole kernel.
+__device__ __forceinline__ int lane_id() {
+  int v;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
+  return v;
+}
+#else
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+#endif
 // wave-uniform copy (value of the first active lane, in an SGPR)
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
   return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
          (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+
+// Bit-field helpers for map probes.  Written as v_bfe_u32 directly: the compiler
+// otherwise turns a field extract into shift + mask (2 VALU instead of 1), and a
+// variable bit test into shift + shift + and.  The hardware reads only the low
+// 5 bits of a bfe offset, so no masking of `bit` is needed.
+// map word index of the low / high u16 value packed in a u32 (bits 5..15 / 21..31)
+__device__ __forceinline__ uint32_t bfe_lo_word(uint32_t w) {
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, 5, 11" : "=v"(r) : "v"(w));
+  return r;
+}
+__device__ __forceinline__ uint32_t bfe_hi_word(uint32_t w) {
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, 21, 11" : "=v"(r) : "v"(w));
+  return r;
+}
+// bit (bit & 31) of word, as 0 / 1
+__device__ __forceinline__ uint32_t bit_at(uint32_t word, uint32_t bit) {
+  uint32_t r;
+  asm("v_bfe_u32 %0, %1, %2, 1" : "=v"(r) : "v"(word), "v"(bit));
+  return r;
 }
 
 // Orders this wave's LDS accesses (LDS ops of one wave complete in issue order;
@@ -85,15 +121,35 @@ __device__ __forceinline__ void w_clear_lds(uint32_t* lds) {
 
 // OR/XOR the values of an array container (<= 4096 values, 16 B aligned slot)
 // into the wave's LDS bitmap.  All of a lane's 16 B vectors are loaded before
-// the first LDS atomic so the loads overlap (one memory latency per container),
-// and bits of consecutive sorted values that share a 32-bit word are merged
-// into one atomic.
+// the first LDS atomic so the loads overlap (one memory latency per container).
+// RBG_SCATTER_MERGE=1 keeps the older variant that merges the bits of
+// consecutive values sharing a 32-bit word into one atomic.
 constexpr int kVecRound = 4;  // 16 B vectors per lane loaded per round
 
 // OR/XOR the 8 values of one 16 B vector (values base..base+7, those < card).
-template <int MODE>  // 0 or, 1 xor
+#ifndef RBG_SCATTER_MERGE
+#define RBG_SCATTER_MERGE 0
+#endif
+template <int MODE, bool MERGE = (RBG_SCATTER_MERGE != 0)>  // MODE 0 or, 1 xor
 __device__ __forceinline__ void scatter_vec(uint32_t* lds, const uint4 v, int base, int card) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  if (!MERGE) {
+    // Branch-free: one LDS atomic per value, 4 VALU (word index, address, valid
+    // bit, bit mask).  Values past the card get a zero mask (the valid bits are
+    // formed once per vector).  An average array has about one value per map word,
+    // so merging same-word neighbours saved few atomics but cost divergent branches.
+    const int rem = card - base;
+    const uint32_t vm = rem >= 8 ? 0xFFu : (1u << max(rem, 0)) - 1u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t wi = w[i >> 1];
+      uint32_t* p = lds + ((i & 1) ? bfe_hi_word(wi) : bfe_lo_word(wi));
+      const uint32_t m = ((vm >> i) & 1u) << (((i & 1) ? (wi >> 16) : wi) & 31u);
+      if (MODE == 0) atomicOr(p, m);
+      else atomicXor(p, m);
+    }
+    return;
+  }
   uint32_t cur = 0xFFFFFFFFu, mask = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {

@@ -526,7 +526,7 @@ __device__ __forceinline__ uint32_t small_arrays_and_card(const uint8_t* pa, uin
   for (int i = 0; i < 8; i++) l4[64 * i + lane] = make_uint4(0, 0, 0, 0);
   wave_sync();
   const bool a_map = ca >= cb;
-  scatter_vec<0>(lds, a_map ? va : vb, 8 * lane, (int)(a_map ? ca : cb));
+  scatter_vec<0, true>(lds, a_map ? va : vb, 8 * lane, (int)(a_map ? ca : cb));
   wave_sync();
   const uint4 v = a_map ? vb : va;
   const int card = (int)(a_map ? cb : ca);
