@@ -8,10 +8,10 @@ include/roaring_mi355x.h.
 from ._lib import (DeviceError, IllegalArgumentException, InvalidRoaringFormat, RoaringError,  # noqa: F401
                    TruncatedInput)
 from .engine import Engine  # noqa: F401
-from .roaring import (FastAggregation, ParallelAggregation, RoaringBitmap, batch_and_cardinality,  # noqa: F401
+from .roaring import (BufferFastAggregation, FastAggregation, ParallelAggregation, RoaringBitmap, batch_and_cardinality,  # noqa: F401
                       run_optimize_many)
 from .bsi import RoaringBitmapSliceIndex  # noqa: F401
 
-__all__ = ["RoaringBitmap", "FastAggregation", "ParallelAggregation", "RoaringBitmapSliceIndex", "Engine", "batch_and_cardinality", "run_optimize_many",
+__all__ = ["RoaringBitmap", "FastAggregation", "BufferFastAggregation", "ParallelAggregation", "RoaringBitmapSliceIndex", "Engine", "batch_and_cardinality", "run_optimize_many",
            "InvalidRoaringFormat",
            "TruncatedInput", "IllegalArgumentException", "DeviceError", "RoaringError"]

@@ -15,6 +15,17 @@
 #include <cstdio>
 #include <cstdlib>
 
+// RBG_PW5=1: five 4-wave workgroups per CU (20 waves) instead of four.  Needs
+// <= 8 KiB of LDS per wave (R AND R in the run domain then takes na + nb <= 2048
+// runs) and <= 96 VGPRs, which the non-hoisted lane index gives.
+#ifndef RBG_PW5
+#define RBG_PW5 0
+#endif
+#if RBG_PW5
+#define RBG_OPAQUE_LANE 1
+#define RBG_WAVE_LDS 2048
+#define RBG_PW_BLOCKS 5
+#endif
 #include "kernels.hpp"
 #include "wave.hpp"
 
@@ -115,7 +126,7 @@ constexpr int kWaves = 4;  // waves per workgroup
 #define RBG_WAVE_LDS 2560
 #endif
 constexpr int kWaveLds = RBG_WAVE_LDS;
-static_assert(kWaveLds >= 2048 + 32, "filter compaction keeps per-lane dummy slots past the 8 KiB map");
+static_assert(kWaveLds >= 2048, "the 8 KiB bitmap map / staging area");
 
 // Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
 // pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
@@ -224,9 +235,13 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
   }
   // the map is dead: compact the kept values over it, then 16 B stores.  Vectors
   // j and j+1 share one scan (16-bit count fields); every value is written, the
-  // dropped ones to a per-lane dummy past the map, so the writes need no branches.
+  // dropped ones to a per-lane dummy just past the kept ones (u16 index ctot + l),
+  // so the writes need no branches.  When fewer than 64 u16 are left past the
+  // kept values (ctot > 4032), only kept values are written.
   uint16_t* st = reinterpret_cast<uint16_t*>(lds);
-  const uint32_t dummy = 4096u + (uint32_t)l;  // u16 index in the wave's LDS past the 8 KiB map
+  const uint32_t ctot = uni((uint32_t)wave_sum_i(cnt));
+  const bool dummies = ctot <= 4096u - 64u;  // wave-uniform
+  const uint32_t dummy = ctot + (uint32_t)l;
   wsync();
   int base = 0;
 #pragma unroll
@@ -244,13 +259,15 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         const uint32_t keep = (hj >> i) & 1u;
-        st[keep ? (uint32_t)q : dummy] = (uint16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF);
+        const uint16_t val = (uint16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF);
+        if (dummies) st[keep ? (uint32_t)q : dummy] = val;
+        else if (keep) st[q] = val;
         q += (int)keep;
       }
     }
     base += (tot & 0xFFFF) + (tot >> 16);
   }
-  const int c = (int)uni((uint32_t)base);
+  const int c = (int)ctot;
   wsync();
   uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
   const uint4* sv = reinterpret_cast<const uint4*>(lds);

@@ -331,6 +331,87 @@ class ParallelAggregation:
         return _wide("xor", list(bitmaps))
 
 
+class BufferFastAggregation:
+    """RB/buffer/BufferFastAggregation.java over ImmutableRoaringBitmap inputs.
+
+    An ImmutableRoaringBitmap is a mapped portable-format buffer, which is exactly
+    what RoaringBitmap(serialized) holds, so every form takes the same objects.
+    The algorithms are FastAggregation's (buffer workShyAnd :426-494 is
+    FastAggregation.workShyAnd :356-414 over Mappeable containers; naive_or
+    :774-781 is naivelazyor + repairAfterLazy like :603-610; naive_xor :827-833
+    is the xor chain of :637-644).  The dispatch differs in three places:
+      - and(Iterator) :66-89 always runs workShyAnd (FastAggregation's runs
+        naive_and, :26-28);
+      - and(MutableRoaringBitmap...) :100-102 goes through convertToImmutable,
+        i.e. the Iterator form, so workShyAnd too;
+      - naive_and(MutableRoaringBitmap...) :407-416 chains from a clone of the
+        first bitmap (no smallest-first choice, like naive_and(Iterator) :383-396).
+    """
+
+    @staticmethod
+    def and_(*args):
+        """and(ImmutableRoaringBitmap...) :28-33, and(long[], ...) :43-58, and(Iterator) :66-89"""
+        kind, buf, bms = _split_args(args)
+        if kind == "iter":
+            return _wide("workshy_and", bms) if bms else RoaringBitmap()
+        return FastAggregation.and_(*args)
+
+    @staticmethod
+    def and_mutable(*bitmaps):
+        """and(MutableRoaringBitmap...) :100-102 -> and(convertToImmutable(...)) -> workShyAnd"""
+        return BufferFastAggregation.and_(iter(list(bitmaps)))
+
+    @staticmethod
+    def naive_and(*args):
+        """naive_and(ImmutableRoaringBitmap...) :347-368 (smallest first), naive_and(Iterator) :383-396"""
+        return FastAggregation.naive_and(*args)
+
+    @staticmethod
+    def naive_and_mutable(*bitmaps):
+        """naive_and(MutableRoaringBitmap...) :407-416: clone of the first, then the and chain"""
+        return _wide("and_iter", list(bitmaps))
+
+    @staticmethod
+    def workShyAnd(buffer, *bitmaps):
+        """workShyAnd(long[], ImmutableRoaringBitmap...) :426-494"""
+        return FastAggregation.workShyAnd(buffer, *bitmaps)
+
+    @staticmethod
+    def or_(*args):
+        """or(ImmutableRoaringBitmap...) :875-877, or(Iterator) :886-888, or(Mutable...) :896-898 -> naive_or"""
+        return FastAggregation.or_(*args)
+
+    @staticmethod
+    def xor(*args):
+        """xor(ImmutableRoaringBitmap...) :1061-1063, xor(Iterator) :1072-1074 -> naive_xor"""
+        return FastAggregation.xor(*args)
+
+    @staticmethod
+    def naive_or(*args):
+        return FastAggregation.naive_or(*args)
+
+    @staticmethod
+    def naive_xor(*args):
+        return FastAggregation.naive_xor(*args)
+
+    @staticmethod
+    def andCardinality(*args) -> int:
+        """:110-121 (0 -> 0, 1 -> card, 2 -> pairwise, else workShyAndCardinality)"""
+        return FastAggregation.andCardinality(*args)
+
+    @staticmethod
+    def orCardinality(*args) -> int:
+        """:129-140"""
+        return FastAggregation.orCardinality(*args)
+
+    horizontal_or = staticmethod(FastAggregation.horizontal_or)
+    horizontal_xor = staticmethod(FastAggregation.horizontal_xor)
+    priorityqueue_or = staticmethod(FastAggregation.priorityqueue_or)
+    priorityqueue_xor = staticmethod(FastAggregation.priorityqueue_xor)
+
+
+setattr(BufferFastAggregation, "and", BufferFastAggregation.and_)
+setattr(BufferFastAggregation, "or", BufferFastAggregation.or_)
 setattr(ParallelAggregation, "or", ParallelAggregation.or_)
 setattr(FastAggregation, "and", FastAggregation.and_)
 setattr(FastAggregation, "or", FastAggregation.or_)

@@ -122,3 +122,34 @@ def test_parallel_and_horizontal_aggregation_sets(gpu):
                 rb.FastAggregation.priorityqueue_xor(*bms)):
         assert set(got.toArray().tolist()) == sym
     assert rb.FastAggregation.horizontal_or(iter(bms)).serialize() == O.wide("or", bufs)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 5, 10, 11, 14])
+def test_buffer_fast_aggregation_dispatch(gpu, n):
+    """RB/buffer/BufferFastAggregation.java: and(Iterator) :66-89 and and(Mutable...)
+    :100-102 run workShyAnd for every N (FastAggregation's Iterator form runs
+    naive_and); naive_and(Mutable...) :407-416 chains from the first bitmap; the
+    varargs forms dispatch like FastAggregation (workShyAnd above 10 inputs)."""
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(900 + n)
+    bufs = [_gen.bitmap(rng, np.arange(8), p_present=0.85) for _ in range(n)]
+    bms = [rb.RoaringBitmap(b) for b in bufs]
+    B = rb.BufferFastAggregation
+    empty = rb.RoaringBitmap().serialize()
+    ws = O.wide("workshy_and", bufs) if n else empty
+    assert B.and_(iter(bms)).serialize() == ws
+    assert B.and_mutable(*bms).serialize() == ws
+    assert getattr(B, "and")(*bms).serialize() == O.wide("and", bufs, list(range(n)))
+    assert B.naive_and(*bms).serialize() == O.wide("naive_and", bufs, list(range(n)))
+    assert B.naive_and(iter(bms)).serialize() == O.wide("and_iter", bufs)
+    assert B.naive_and_mutable(*bms).serialize() == O.wide("and_iter", bufs)
+    assert B.or_(*bms).serialize() == O.wide("or", bufs)
+    assert B.or_(iter(bms)).serialize() == O.wide("or", bufs)
+    assert B.xor(*bms).serialize() == O.wide("xor", bufs)
+    assert B.andCardinality(*bms) == O.wide_card("and", bufs)
+    assert B.orCardinality(*bms) == O.wide_card("or", bufs)
+    if n > 10:
+        buf = np.zeros(1024, dtype=np.int64)
+        assert B.and_(buf, *bms).serialize() == ws
+        with pytest.raises(rb.IllegalArgumentException):
+            B.and_(np.zeros(10, dtype=np.int64), *bms)
