@@ -156,6 +156,36 @@ struct StampAcc {
   } while (0)
 #endif
 
+// Wave priority (RBG_PRIO, default 1): a task runs at priority 3 until its
+// operand loads have been consumed, then drops to 0, so waves that are issuing
+// loads win instruction arbitration over waves in their compute / output phases
+// and more of the CU's memory requests are in flight (C2 AND -1 %, andCardinality
+// -2.5 %).  RBG_PRIO=2 also raises the output phase to 2 (no further change).
+#ifndef RBG_PRIO
+#define RBG_PRIO 1
+#endif
+#if RBG_PRIO
+#define PRIO_HI() __builtin_amdgcn_s_setprio(3)
+#define PRIO_LO() __builtin_amdgcn_s_setprio(0)
+#if RBG_PRIO == 2
+#define PRIO_OUT() __builtin_amdgcn_s_setprio(2)
+#else
+#define PRIO_OUT() \
+  do {            \
+  } while (0)
+#endif
+#else
+#define PRIO_OUT() \
+  do {            \
+  } while (0)
+#define PRIO_HI() \
+  do {            \
+  } while (0)
+#define PRIO_LO() \
+  do {            \
+  } while (0)
+#endif
+
 // Records one task's output.  Staged results (LDS) are copied to the task's
 // scratch slot (arena slot layout); results already in the slot or pass-through
 // containers are referenced in place.  k_place and the serializer follow.
@@ -202,6 +232,7 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
 #pragma unroll
   for (int j = 0; j < 8; j++) v[j] = (64 * j + l < nvec) ? pv[64 * j] : make_uint4(0, 0, 0, 0);
   w_map_lds(mkind, mcard, mslot, lds);
+  PRIO_LO();
   STAMP(4);
   uint32_t hit[8];
   int cnt = 0;
@@ -233,6 +264,7 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
     if (l == 0) task_card[t] = (uint32_t)c;
     return;
   }
+  PRIO_OUT();
   // the map is dead: compact the kept values over it, then 16 B stores.  Vectors
   // j and j+1 share one scan (16-bit count fields); every value is written, the
   // dropped ones to a per-lane dummy just past the kept ones (u16 index ctot + l),
@@ -400,6 +432,7 @@ __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const u
   const int l = lane_id();
   wsync();
   runs_to_lds2(pa + tk.slot_a, na, lds, pb + tk.slot_b, nb, lds + na);
+  PRIO_LO();
   wsync();
   const int d0 = (l * (na + nb)) >> 6, d1 = ((l + 1) * (na + nb)) >> 6;
   int cnt = 0, card = 0;
@@ -452,11 +485,13 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
 #endif
     w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
   STAMP(1);
+  PRIO_LO();
   const int c = w_card(x);
   if (MODE == 1) {
     if (l == 0) task_card[t] = (uint32_t)c;
     return;
   }
+  PRIO_OUT();
   if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389,456,1084)
     w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
     return;
@@ -505,6 +540,7 @@ __device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
 template <int OP, int MODE>
 __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
                                          const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+  PRIO_HI();
   if (pair_class(OP, tk.kind_a, tk.kind_b) == 1)
     filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
   else
