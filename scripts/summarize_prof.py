@@ -19,7 +19,34 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-DOMINANT = "k_pair_wave"
+DOMINANT = "k_pair_wave<0, 0>"  # AND, results materialised (the bench headline kernel)
+
+
+def short_name(n):
+    """'void rbg::k_pair_wave<0, 0>(rbg::PTask const*, ...)' -> 'k_pair_wave<0, 0>'"""
+    n = n.strip()
+    if n.startswith("void "):
+        n = n[5:]
+    depth = 0
+    for i, ch in enumerate(n):  # cut at the argument list (the first '(' outside <>)
+        depth += ch == "<"
+        depth -= ch == ">"
+        if ch == "(" and depth == 0:
+            n = n[:i]
+            break
+    return n.replace("rbg::", "").strip()
+
+
+def kernel_stats(src, dst):
+    """run_kernel_stats.csv with short names (template arguments kept)."""
+    with open(src) as f:
+        rows = list(csv.DictReader(f))
+    with open(dst, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=list(rows[0].keys()), quoting=csv.QUOTE_NONNUMERIC)
+        w.writeheader()
+        for r in rows:
+            r["Name"] = short_name(r["Name"])
+            w.writerow(r)
 
 
 def counters(path):
@@ -28,7 +55,7 @@ def counters(path):
         return acc
     with open(path) as f:
         for row in csv.DictReader(f):
-            name = row["Kernel_Name"].split("(")[0].strip()
+            name = short_name(row["Kernel_Name"])
             acc[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
     return acc
 
@@ -37,7 +64,7 @@ def main(tag):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    kernel_stats(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
     if os.path.exists(os.path.join(src, "bench_kt.json")):
         shutil.copy(os.path.join(src, "bench_kt.json"), os.path.join(dst, "bench_kt.json"))
     summary = {}
@@ -54,7 +81,7 @@ def main(tag):
     if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
         rd = 2.0 * d["FETCH_SIZE"]["mean"] * 1024
         wr = d["WRITE_SIZE"]["mean"] * 1024
-        traffic = {DOMINANT: {"hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
+        traffic = {"k_pair_wave": {"kernel": DOMINANT, "hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
                               "source": f"profiles/{tag}/pmc_summary.json",
                               "correction": "FETCH_SIZE x2 (gfx950 streaming-read tally), KiB -> bytes"}}
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
