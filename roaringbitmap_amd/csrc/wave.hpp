@@ -318,20 +318,28 @@ __device__ __forceinline__ void w_combine(const CDesc& d, const uint8_t* payload
     }
     return;
   }
-  const uint4* src;
+  // B from global memory and A from the LDS map take separate loops: one loop
+  // over a pointer that may be either compiles to flat loads, which wait on both
+  // the vector-memory and the LDS counters
   if (d.kind == DK_B) {
-    src = reinterpret_cast<const uint4*>(slot) + lane_id();
-  } else {
-    wsync();
-    w_clear_lds(lds);
-    wsync();
-    w_scatter_array<0>(lds, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
-    wsync();
-    src = reinterpret_cast<const uint4*>(lds) + lane_id();
+    const uint4* g = reinterpret_cast<const uint4*>(slot) + lane_id();
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint4 v = g[64 * i];
+      x.w[2 * i] = w_op<OP>(x.w[2 * i], (uint64_t)v.x | ((uint64_t)v.y << 32));
+      x.w[2 * i + 1] = w_op<OP>(x.w[2 * i + 1], (uint64_t)v.z | ((uint64_t)v.w << 32));
+    }
+    return;
   }
+  wsync();
+  w_clear_lds(lds);
+  wsync();
+  w_scatter_array<0>(lds, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
+  wsync();
+  const uint4* q = reinterpret_cast<const uint4*>(lds) + lane_id();
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint4 v = src[64 * i];
+    const uint4 v = q[64 * i];
     x.w[2 * i] = w_op<OP>(x.w[2 * i], (uint64_t)v.x | ((uint64_t)v.y << 32));
     x.w[2 * i + 1] = w_op<OP>(x.w[2 * i + 1], (uint64_t)v.z | ((uint64_t)v.w << 32));
   }
