@@ -180,6 +180,9 @@ int rbg_ctx_batch_minmax(rbg_ctx* ctx, int32_t batch, int32_t* out2);
 int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* stats8);
 /* Download bitmap i of a batch as serialized bytes (synchronous). */
 int rbg_ctx_batch_fetch(rbg_ctx* ctx, int32_t batch, size_t i, rbg_buffer* out);
+/* Download bitmaps [first, first + count) of a batch: outs[k] receives bitmap first + k
+ * (free each with rbg_free).  One device gather and one copy for the whole range. */
+int rbg_ctx_batch_fetch_range(rbg_ctx* ctx, int32_t batch, size_t first, size_t count, rbg_buffer* outs);
 
 /* Enqueue a pairwise op between bitmap ia of batch a and bitmap ib of batch b.  The
  * result is materialised on the device (containers in slots + a compacted

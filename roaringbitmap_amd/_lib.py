@@ -37,7 +37,7 @@ EXPORTED = [
     "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read", "rbg_ctx_serialize", "rbg_ctx_wide_start",
     "rbg_ctx_batch_counts", "rbg_synth_key_bytes", "rbg_ctx_pair_bytes", "rbg_debug_stamps",
     "rbg_bsi_compare", "rbg_bsi_sum", "rbg_ctx_bsi", "rbg_ctx_bsi_sums", "rbg_ctx_batch_minmax",
-    "rbg_ctx_run_optimize", "rbg_run_optimize_many",
+    "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
 ]
 
 _lib = None
@@ -74,6 +74,7 @@ def _declare(L):
     L.rbg_ctx_release.argtypes = [vp, i32]
     L.rbg_ctx_batch_stats.argtypes = [vp, i32, P(ctypes.c_int64)]
     L.rbg_ctx_batch_fetch.argtypes = [vp, i32, sz, buf]
+    L.rbg_ctx_batch_fetch_range.argtypes = [vp, i32, sz, sz, vp]
     L.rbg_ctx_pairwise.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz]
     L.rbg_ctx_pairwise_card.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz]
     L.rbg_ctx_wide.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int, P(i32)]

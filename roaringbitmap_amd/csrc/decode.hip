@@ -312,7 +312,8 @@ __global__ __launch_bounds__(256) void k_dec_fill(const uint8_t* __restrict__ ra
                                                   const uint16_t* __restrict__ qkey, const uint32_t* __restrict__ perm,
                                                   const uint64_t* __restrict__ slot, uint64_t C,
                                                   CDesc* __restrict__ desc, uint16_t* __restrict__ keys,
-                                                  uint32_t* __restrict__ bm, uint8_t* __restrict__ payload) {
+                                                  uint32_t* __restrict__ bm, uint8_t* __restrict__ payload,
+                                                  uint64_t* __restrict__ bm_card) {
   const int lane = lane_id();
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   for (uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < C; p += nw) {
@@ -327,8 +328,21 @@ __global__ __launch_bounds__(256) void k_dec_fill(const uint8_t* __restrict__ ra
       uint16_t* d16 = reinterpret_cast<uint16_t*>(payload + off);
       for (uint32_t v = c.len / 2 + lane; v < ((c.len + 15) & ~15u) / 2; v += 64) d16[v] = last;
     }
+    uint32_t card = c.card;
+    if (c.kind == DK_R) {
+      // The deserializer builds the RunContainer from its runs and ignores the header
+      // cardinality (RB/RoaringArray.java:583-597, RunContainer.getCardinality
+      // RB/RunContainer.java:1003-1009): derive it from the runs.
+      const uint32_t nr = (c.len - 2) / 4;
+      uint32_t s = 0;
+      for (uint32_t j = lane; j < nr; j += 64) s += rd16b(raw + c.src + 2 + 4 * j + 2) + 1;
+      card = (uint32_t)wave_sum_i((int)s);
+      if (lane == 0 && card != c.card)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&bm_card[c.bm]),
+                  (unsigned long long)((int64_t)card - (int64_t)c.card));
+    }
     if (lane == 0) {
-      desc[p] = CDesc{off, c.card, key, (uint8_t)c.kind, 0};
+      desc[p] = CDesc{off, card, key, (uint8_t)c.kind, 0};
       keys[p] = key;
       bm[p] = c.bm;
     }
@@ -389,10 +403,11 @@ void launch_dec_sizes(hipStream_t s, const DecCtr* q, const uint32_t* perm, uint
 }
 
 void launch_dec_fill(hipStream_t s, const uint8_t* raw, const DecCtr* q, const uint16_t* qkey, const uint32_t* perm,
-                     const uint64_t* slot, uint64_t C, CDesc* desc, uint16_t* keys, uint32_t* bm, uint8_t* payload) {
+                     const uint64_t* slot, uint64_t C, CDesc* desc, uint16_t* keys, uint32_t* bm, uint8_t* payload,
+                     uint64_t* bm_card) {
   if (!C) return;
   hipLaunchKernelGGL(k_dec_fill, dim3(grid_of(C, 4, 8192)), dim3(256), 0, s, raw, q, qkey, perm, slot, C, desc, keys,
-                     bm, payload);
+                     bm, payload, bm_card);
 }
 
 }  // namespace rbg

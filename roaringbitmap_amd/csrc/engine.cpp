@@ -107,6 +107,11 @@ struct Batch {
   int32_t bsi_min = 0, bsi_max = 0;  // synthetic C5: min / max of the indexed values
   bool pair_cap_known = false;        // batched andCardinality: item capacity computed
   uint64_t pair_items_cap = 0;
+  // host copy of the container table for fetches (batches are immutable once loaded):
+  // h_desc in container order, h_pos[h_pos_off[i] .. h_pos_off[i+1]) = bitmap i's containers
+  bool h_index = false;
+  std::vector<CDesc> h_desc;
+  std::vector<uint32_t> h_pos, h_pos_off;
 };
 
 struct DecBufs {  // scratch of the device decode (decode.hip), reused across loads
@@ -125,11 +130,13 @@ struct Ctx {
   uint64_t* zlb = nullptr;    // look-back state the next plan kernel zeroes (null: none)
   uint64_t* ztile = nullptr;
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
+  DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   int bsi_nbits = 0;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw,
       scalar, scratch;
   size_t result_cap = 0;
   OutCtx pending{};         // output state of the last materialising op
+  std::vector<int32_t> pending_src;  // batches the pending result's pass-through records point into
   size_t pending_ub = 0;
   bool serialized = false;  // pending result already in the portable layout
   size_t n_cards = 0;
@@ -447,7 +454,8 @@ static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens,
   CHK(b.payload.ensure(b.payload_bytes + 64));
   dbg(s, "load: sizes + payload alloc");
   launch_dec_fill(s, c->raw.as<uint8_t>(), d.q.as<DecCtr>(), d.qkey.as<uint16_t>(), perm, d.size.as<uint64_t>(), C,
-                  b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.bm.as<uint32_t>(), b.payload.as<uint8_t>());
+                  b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.bm.as<uint32_t>(), b.payload.as<uint8_t>(),
+                  d.card.as<uint64_t>());
   HIPCHK(hipGetLastError());
   std::vector<uint64_t> nctr(n), card(n), cons(n);
   if (n) {
@@ -510,7 +518,11 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   c->serialized = false;
   c->pending_ub = 0;
   c->zlb = c->ztile = nullptr;
-  if (card_only) return RBG_OK;
+  c->pending_src.clear();
+  if (card_only) {
+    c->zlb = reinterpret_cast<uint64_t*>(lb);  // the error word must not carry over from an earlier op
+    return RBG_OK;
+  }
   const uint64_t P0 = header_reserve(max_tasks);
   CHK(c->result.ensure(P0 + max_payload + 64));
   c->result_cap = P0 + max_payload;
@@ -578,6 +590,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   }
   OutCtx oc;
   CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only));
+  c->pending_src = {ia, ib};
   c->mark(0);
   dbg(s, "memset");
   launch_plan_pairwise(s, plan_op, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), B->key_off.as<uint32_t>(),
@@ -591,7 +604,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   dbg(s, "pairwise");
   c->mark(2);
   if (card_only) {
-    launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
+    launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>(), oc.err);
     c->last = 2;
   } else {
     launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
@@ -686,6 +699,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     OutCtx oc;
     // each result container is staged (<= 8194 B) or a clone of one input container
     CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, card_only));
+    c->pending_src = {id};
     if (!skip.empty()) {
       CHK(c->skip.ensure(skip.size()));
       HIPCHK(hipMemcpyAsync(c->skip.p, skip.data(), skip.size(), hipMemcpyHostToDevice, s));
@@ -709,7 +723,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
                 c->task_card.as<uint32_t>());
     c->mark(2);
     if (card_only) {
-      launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>());
+      launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>(), oc.err);
       c->last = 2;
     } else {
       launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
@@ -766,6 +780,7 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
   const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
   OutCtx oc;
   CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, op == BSI_SUM_ONLY));
+  c->pending_src = {id};
   const uint32_t need = mode == -1 ? 0xFFFFFFFFu : (op == BSI_SUM_ONLY ? (uint32_t)(nbits + 1) : 0u);
   c->mark(0);
   launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
@@ -824,6 +839,10 @@ static int ctx_info(Ctx* c, ResultInfo* ri) {
     ri->long_card = (int64_t)card;
     ri->card32 = (uint32_t)card;
   }
+  if ((c->last == 1 || c->last == 2) && ri->err) {
+    set_err("a look-back spin of the op's plan or placement timed out: the result is invalid");
+    return RBG_ERR_DEVICE;
+  }
   return RBG_OK;
 }
 
@@ -835,10 +854,6 @@ static int ctx_fetch(Ctx* c, rbg_buffer* out) {
   CHK(ctx_serialize(c));
   ResultInfo ri;
   CHK(ctx_info(c, &ri));
-  if (ri.err) {
-    set_err("look-back placement timed out");
-    return RBG_ERR_DEVICE;
-  }
   uint8_t* p = (uint8_t*)std::malloc(ri.total ? ri.total : 1);
   if (!p) return RBG_ERR_OUT_OF_MEMORY;
   HIPCHK(hipMemcpyAsync(p, c->result.as<uint8_t>() + ri.start, ri.total, hipMemcpyDeviceToHost, c->stream));
@@ -1168,11 +1183,17 @@ int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, s
   return ctx_load(&ctx->c, bufs, lens, n, batch);
 }
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch) {
+  Ctx& c = ctx->c;
   Batch* b;
-  CHK(get_batch(&ctx->c, batch, &b));
-  HIPCHK(hipSetDevice(ctx->c.device));
-  HIPCHK(hipStreamSynchronize(ctx->c.stream));
-  ctx->c.batches[batch].reset();
+  CHK(get_batch(&c, batch, &b));
+  HIPCHK(hipSetDevice(c.device));
+  // A materialised result references pass-through containers inside its operand
+  // batches (ORec::src) until it is serialized: serialize it before an operand goes.
+  if (c.last == 1 && !c.serialized &&
+      std::find(c.pending_src.begin(), c.pending_src.end(), batch) != c.pending_src.end())
+    CHK(ctx_serialize(&c));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  c.batches[batch].reset();
   return RBG_OK;
 }
 int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* st) {
@@ -1200,82 +1221,131 @@ int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* st) {
   return RBG_OK;
 }
 static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out);
+static int ctx_batch_fetch_range(Ctx* c, int32_t batch, size_t i0, size_t i1, rbg_buffer* outs);
 int rbg_ctx_batch_fetch(rbg_ctx* ctx, int32_t batch, size_t i, rbg_buffer* out) {
   if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
   HIPCHK(hipSetDevice(ctx->c.device));
   return ctx_batch_fetch(&ctx->c, batch, i, out);
 }
+int rbg_ctx_batch_fetch_range(rbg_ctx* ctx, int32_t batch, size_t first, size_t count, rbg_buffer* outs) {
+  if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_batch_fetch_range(&ctx->c, batch, first, first + count, outs);
+}
 }  // extern "C"
 
-static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out) {
+// Host index of a batch's containers, built once per batch: the container table and,
+// per input bitmap, its container positions (in key order).
+static int batch_host_index(Ctx* c, Batch* b) {
+  if (b->h_index) return RBG_OK;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  b->h_desc.resize(b->n_ctr);
+  if (b->n_ctr) HIPCHK(hipMemcpy(b->h_desc.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
+  b->h_pos_off.assign(b->n_bm + 1, 0);
+  b->h_pos.resize(b->n_ctr);
+  if ((b->n_bm == 1 || !b->key_major) && b->h_bm_off.size() == b->n_bm + 1) {
+    for (size_t i = 0; i <= b->n_bm; i++) b->h_pos_off[i] = b->h_bm_off[i];
+    for (size_t p = 0; p < b->n_ctr; p++) b->h_pos[p] = (uint32_t)p;
+  } else {  // key-major: counting sort of the positions by input bitmap (stable, so key order)
+    std::vector<uint32_t> bm(b->n_ctr);
+    if (b->n_ctr) HIPCHK(hipMemcpy(bm.data(), b->bm.p, 4 * b->n_ctr, hipMemcpyDeviceToHost));
+    for (uint32_t x : bm) b->h_pos_off[x + 1]++;
+    for (size_t i = 0; i < b->n_bm; i++) b->h_pos_off[i + 1] += b->h_pos_off[i];
+    std::vector<uint32_t> fill(b->h_pos_off.begin(), b->h_pos_off.end() - 1);
+    for (size_t p = 0; p < b->n_ctr; p++) b->h_pos[fill[bm[p]]++] = (uint32_t)p;
+  }
+  b->h_index = true;
+  return RBG_OK;
+}
+
+// Download bitmaps [i0, i1) of a batch as portable serialized bytes: their slots are
+// gathered on the device into one buffer (one D2H copy), the headers built here.
+static int ctx_batch_fetch_range(Ctx* c, int32_t batch, size_t i0, size_t i1, rbg_buffer* outs) {
   Batch* b;
   CHK(get_batch(c, batch, &b));
-  if (i >= b->n_bm || !out) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipStreamSynchronize(c->stream));
-  std::vector<CDesc> all(b->n_ctr);
-  if (b->n_ctr) HIPCHK(hipMemcpy(all.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
-  std::vector<CDesc> mine;
-  std::vector<size_t> idx;
-  if (b->n_bm == 1 || !b->key_major) {
-    for (uint32_t p = b->h_bm_off[i]; p < b->h_bm_off[i + 1]; p++) idx.push_back(p);
-  } else {
-    std::vector<uint32_t> bm(b->n_ctr);
-    HIPCHK(hipMemcpy(bm.data(), b->bm.p, 4 * b->n_ctr, hipMemcpyDeviceToHost));
-    for (size_t p = 0; p < b->n_ctr; p++)
-      if (bm[p] == i) idx.push_back(p);
+  if (i0 > i1 || i1 > b->n_bm || (i1 > i0 && !outs)) return RBG_ERR_ILLEGAL_ARGUMENT;
+  CHK(batch_host_index(c, b));
+  const std::vector<CDesc>& D = b->h_desc;
+  // slots are consecutive in container order: a slot ends where the next one starts
+  auto slot_end = [&](uint32_t p) -> uint64_t { return p + 1 < b->n_ctr ? D[p + 1].slot : b->payload_bytes; };
+  std::vector<GatherItem> items;
+  uint64_t tot = 0;
+  for (size_t i = i0; i < i1; i++)
+    for (uint32_t k = b->h_pos_off[i]; k < b->h_pos_off[i + 1]; k++) {
+      const uint32_t p = b->h_pos[k];
+      const uint64_t len = slot_end(p) - D[p].slot;
+      items.push_back(GatherItem{D[p].slot, tot, len});
+      tot = round16(tot + len);
+    }
+  std::vector<uint8_t> pay(tot + 16);
+  if (!items.empty()) {
+    CHK(c->gather_items.ensure(sizeof(GatherItem) * items.size()));
+    CHK(c->gather_out.ensure(tot + 16));
+    HIPCHK(hipMemcpyAsync(c->gather_items.p, items.data(), sizeof(GatherItem) * items.size(), hipMemcpyHostToDevice,
+                          c->stream));
+    launch_gather(c->stream, c->gather_items.as<GatherItem>(), items.size(), b->payload.as<uint8_t>(),
+                  c->gather_out.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(pay.data(), c->gather_out.p, tot, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
   }
-  // slots are consecutive in descriptor order: a slot ends where the next one starts
-  uint64_t lo = ~0ULL, hi = 0;
-  for (size_t p : idx) {
-    mine.push_back(all[p]);
-    lo = std::min<uint64_t>(lo, all[p].slot);
-    hi = std::max<uint64_t>(hi, p + 1 < b->n_ctr ? all[p + 1].slot : b->payload_bytes);
-  }
-  hi = std::min<uint64_t>(std::max(hi, lo), b->payload_bytes + 64);
-  std::vector<uint8_t> pay(mine.empty() ? 0 : hi - lo);
-  if (!pay.empty()) HIPCHK(hipMemcpy(pay.data(), b->payload.as<uint8_t>() + lo, hi - lo, hipMemcpyDeviceToHost));
-  const size_t n = mine.size();
-  bool has_run = false;
-  for (const CDesc& d : mine) has_run |= d.kind == KR;
-  std::vector<uint8_t> o;
-  auto put16 = [&](uint32_t v) { o.push_back((uint8_t)v); o.push_back((uint8_t)(v >> 8)); };
-  auto put32 = [&](uint32_t v) { for (int k = 0; k < 4; k++) o.push_back((uint8_t)(v >> (8 * k))); };
-  std::vector<uint32_t> lens(n);
-  for (size_t k = 0; k < n; k++) {
-    const CDesc& d = mine[k];
-    if (d.kind == KA) lens[k] = 2 * d.card;
-    else if (d.kind == KB) lens[k] = 8192;
-    else {
-      const uint8_t* q = pay.data() + (d.slot - lo) + 2;
-      lens[k] = 2 + 4 * (uint32_t)(q[0] | (q[1] << 8));
+  size_t it = 0;
+  for (size_t i = i0; i < i1; i++) {
+    const uint32_t k0 = b->h_pos_off[i], n = b->h_pos_off[i + 1] - k0;
+    bool has_run = false;
+    std::vector<uint32_t> lens(n);
+    for (uint32_t k = 0; k < n; k++) {
+      const CDesc& d = D[b->h_pos[k0 + k]];
+      has_run |= d.kind == KR;
+      if (d.kind == KA) lens[k] = 2 * d.card;
+      else if (d.kind == KB) lens[k] = 8192;
+      else {
+        const uint8_t* q = pay.data() + items[it + k].dst + 2;
+        lens[k] = 2 + 4 * (uint32_t)(q[0] | (q[1] << 8));
+      }
+    }
+    std::vector<uint8_t> o;
+    auto put16 = [&](uint32_t v) { o.push_back((uint8_t)v); o.push_back((uint8_t)(v >> 8)); };
+    auto put32 = [&](uint32_t v) { for (int j = 0; j < 4; j++) o.push_back((uint8_t)(v >> (8 * j))); };
+    if (has_run) {
+      put32(12347u | (uint32_t)((n - 1) << 16));
+      std::vector<uint8_t> fl((n + 7) / 8, 0);
+      for (uint32_t k = 0; k < n; k++)
+        if (D[b->h_pos[k0 + k]].kind == KR) fl[k / 8] |= (uint8_t)(1u << (k % 8));
+      o.insert(o.end(), fl.begin(), fl.end());
+    } else {
+      put32(12346u);
+      put32(n);
+    }
+    for (uint32_t k = 0; k < n; k++) {
+      const CDesc& d = D[b->h_pos[k0 + k]];
+      put16(d.key);
+      put16(d.card - 1);
+    }
+    if (!has_run || n >= 4) {
+      uint32_t start = (uint32_t)header_size(n, has_run);
+      for (uint32_t k = 0; k < n; k++) {
+        put32(start);
+        start += lens[k];
+      }
+    }
+    for (uint32_t k = 0; k < n; k++) {
+      const uint8_t* q = pay.data() + items[it + k].dst + (D[b->h_pos[k0 + k]].kind == KR ? 2 : 0);
+      o.insert(o.end(), q, q + lens[k]);
+    }
+    it += n;
+    const int st = emit_host(o, &outs[i - i0]);
+    if (st != RBG_OK) {
+      for (size_t j = i0; j < i; j++) rbg_free(&outs[j - i0]);
+      return st;
     }
   }
-  if (has_run) {
-    put32(12347u | (uint32_t)((n - 1) << 16));
-    std::vector<uint8_t> fl((n + 7) / 8, 0);
-    for (size_t k = 0; k < n; k++)
-      if (mine[k].kind == KR) fl[k / 8] |= (uint8_t)(1u << (k % 8));
-    o.insert(o.end(), fl.begin(), fl.end());
-  } else {
-    put32(12346u);
-    put32((uint32_t)n);
-  }
-  for (const CDesc& d : mine) {
-    put16(d.key);
-    put16(d.card - 1);
-  }
-  if (!has_run || n >= 4) {
-    uint32_t start = (uint32_t)header_size(n, has_run);
-    for (size_t k = 0; k < n; k++) {
-      put32(start);
-      start += lens[k];
-    }
-  }
-  for (size_t k = 0; k < n; k++) {
-    const uint8_t* q = pay.data() + (mine[k].slot - lo) + (mine[k].kind == KR ? 2 : 0);
-    o.insert(o.end(), q, q + lens[k]);
-  }
-  return emit_host(o, out);
+  return RBG_OK;
+}
+
+static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  return ctx_batch_fetch_range(c, batch, i, i + 1, out);
 }
 
 extern "C" {

@@ -98,6 +98,11 @@ int parse(const uint8_t* p, size_t n, HostBitmap* out, std::string* err) {
       c.ser_len = 2 * c.card;
     }
     if (n < pos + c.ser_len) return trunc("container payload");
+    if (c.kind == KR) {  // RunContainer cardinality comes from its runs, not the header (RB/RunContainer.java:1003-1009)
+      uint32_t rc = 0;
+      for (uint32_t j = 0; j < c.nruns; j++) rc += 1u + rd16(p + pos + 2 + 4 * j + 2);
+      c.card = rc;
+    }
     pos += c.ser_len;
     out->card += c.card;
   }

@@ -181,8 +181,11 @@ __global__ __launch_bounds__(256) void k_runflags(const uint32_t* __restrict__ n
 }
 
 // Java-int sum of task cardinalities (mod 2^32) plus "any nonzero" for intersects.
+// `err` is the op's look-back error word: a plan spin that timed out makes the task list
+// (and so the sum) invalid, which ctx_info reports as a device error.
 __global__ __launch_bounds__(1024) void k_reduce_card(const uint32_t* __restrict__ task_card,
-                                                      const uint32_t* __restrict__ n_tasks, ResultInfo* __restrict__ info) {
+                                                      const uint32_t* __restrict__ n_tasks, ResultInfo* __restrict__ info,
+                                                      const uint32_t* __restrict__ err) {
   __shared__ unsigned long long ws[16];
   __shared__ int wa[16];
   const uint32_t nt = *n_tasks;
@@ -211,6 +214,7 @@ __global__ __launch_bounds__(1024) void k_reduce_card(const uint32_t* __restrict
     r.long_card = (int64_t)tot;
     r.card32 = (uint32_t)tot;
     r.any = (uint32_t)an;
+    r.err = *err;
     *info = r;
   }
 }
@@ -396,6 +400,18 @@ __global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ n_tas
 }
 
 // ===========================================================================
+// slot gather (batch fetch): one wave per slot, into a contiguous download buffer
+// ===========================================================================
+__global__ __launch_bounds__(256) void k_gather(const GatherItem* __restrict__ items, uint64_t n,
+                                                const uint8_t* __restrict__ src, uint8_t* __restrict__ dst) {
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
+    const GatherItem it = items[i];
+    group_copy<64>(dst + it.dst, src + it.src, (uint32_t)it.len, lane_id());
+  }
+}
+
+// ===========================================================================
 // host launchers
 // ===========================================================================
 
@@ -433,8 +449,9 @@ void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, ui
   hipLaunchKernelGGL(k_header, dim3(grid), dim3(256), 0, s, nt, oc, kind_by_out, (ResultInfo*)nullptr);
   hipLaunchKernelGGL(k_runflags, dim3(32), dim3(256), 0, s, nt, oc, (const uint8_t*)kind_by_out);
 }
-void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info) {
-  hipLaunchKernelGGL(k_reduce_card, dim3(1), dim3(1024), 0, s, task_card, nt, info);
+void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info,
+                        const uint32_t* err) {
+  hipLaunchKernelGGL(k_reduce_card, dim3(1), dim3(1024), 0, s, task_card, nt, info, err);
 }
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload,
                         unsigned long long* out) {
@@ -442,6 +459,12 @@ void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint
   if (g > 4096) g = 4096;
   if (g == 0) return;
   hipLaunchKernelGGL(k_batch_bytes, dim3((unsigned)g), dim3(256), 0, s, desc, n, payload, out);
+}
+
+void launch_gather(hipStream_t s, const GatherItem* items, uint64_t n, const uint8_t* src, uint8_t* dst) {
+  if (!n) return;
+  const unsigned g = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((n + 3) / 4, 8192));
+  hipLaunchKernelGGL(k_gather, dim3(g), dim3(256), 0, s, items, n, src, dst);
 }
 
 }  // namespace rbg

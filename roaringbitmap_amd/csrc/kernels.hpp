@@ -72,8 +72,14 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
 // cookie) runs only when the result is fetched
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info);
 void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out);
-void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info);
+void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info,
+                        const uint32_t* err);
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload, unsigned long long* out);
+// dst[it.dst .. +it.len) = src[it.src .. +it.len) for every item (wave per item; src needs 16 B read slack)
+struct GatherItem {
+  uint64_t src, dst, len;
+};
+void launch_gather(hipStream_t s, const GatherItem* items, uint64_t n, const uint8_t* src, uint8_t* dst);
 
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
                      uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile);
@@ -173,6 +179,7 @@ void launch_dec_key_off(hipStream_t s, const uint16_t* skey, uint64_t C, uint32_
 void launch_dec_sizes(hipStream_t s, const DecCtr* q, const uint32_t* perm, uint64_t C, uint64_t* size,
                       unsigned long long* totals);
 void launch_dec_fill(hipStream_t s, const uint8_t* raw, const DecCtr* q, const uint16_t* qkey, const uint32_t* perm,
-                     const uint64_t* slot, uint64_t C, CDesc* desc, uint16_t* keys, uint32_t* bm, uint8_t* payload);
+                     const uint64_t* slot, uint64_t C, CDesc* desc, uint16_t* keys, uint32_t* bm, uint8_t* payload,
+                     uint64_t* bm_card);  // bm_card: run-container cardinalities are re-derived from the runs
 
 }  // namespace rbg

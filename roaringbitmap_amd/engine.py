@@ -85,6 +85,14 @@ class Engine:
         check(lib().rbg_ctx_batch_fetch(self._ctx, int(batch), int(i), ctypes.byref(b)))
         return RoaringBitmap(take(b))
 
+    def batch_fetch_range(self, batch, first=0, count=None) -> list:
+        """Bitmaps [first, first + count) of a batch (default: all), one device gather + one copy."""
+        if count is None:
+            count = self.batch_stats(batch)["bitmaps"] - first
+        outs = (_lib.rbg_buffer * max(count, 1))()
+        check(lib().rbg_ctx_batch_fetch_range(self._ctx, int(batch), int(first), int(count), outs))
+        return [RoaringBitmap(take(outs[k])) for k in range(count)]
+
     # ---- ops (asynchronous) -------------------------------------------------------
     def pairwise(self, op, a, b, ia=0, ib=0):
         check(lib().rbg_ctx_pairwise(self._ctx, _lib.OP[op], int(a), int(ia), int(b), int(ib)))

@@ -100,3 +100,66 @@ def decode(buf):
 
 def kinds(buf):
     return [c[1] for c in decode(buf)]
+
+
+def container_table(buf):
+    """Fast container table of a serialized bitmap (numpy over the descriptors and the
+    offset table): -> (keys, kinds, cards, payload offsets, payload lengths)."""
+    cookie = struct.unpack_from("<I", buf, 0)[0]
+    has_run = (cookie & 0xFFFF) == 12347
+    if has_run:
+        size = (cookie >> 16) + 1
+        fl = np.frombuffer(buf, dtype=np.uint8, count=(size + 7) // 8, offset=4)
+        pos = 4 + (size + 7) // 8
+        is_run = ((fl[np.arange(size) // 8] >> (np.arange(size) % 8)) & 1).astype(bool)
+    else:
+        size = struct.unpack_from("<I", buf, 4)[0]
+        pos = 8
+        is_run = np.zeros(size, dtype=bool)
+    d = np.frombuffer(buf, dtype="<u2", count=2 * size, offset=pos).reshape(-1, 2).astype(np.int64)
+    keys, cards = d[:, 0], d[:, 1] + 1
+    pos += 4 * size
+    kinds = np.where(is_run, R, np.where(cards > 4096, B, A))
+    if not has_run or size >= 4:
+        offs = np.frombuffer(buf, dtype="<u4", count=size, offset=pos).astype(np.int64)
+    else:  # walk (size < 4)
+        offs, p = [], pos
+        for i in range(size):
+            offs.append(p)
+            p += 2 + 4 * struct.unpack_from("<H", buf, p)[0] if kinds[i] == R else (8192 if kinds[i] == B else 2 * cards[i])
+        offs = np.array(offs, dtype=np.int64)
+    lens = np.where(kinds == B, 8192, 2 * cards)
+    for i in np.nonzero(kinds == R)[0]:
+        lens[i] = 2 + 4 * struct.unpack_from("<H", buf, int(offs[i]))[0]
+    return keys, kinds, cards, offs, lens
+
+
+def sub_bitmap(buf, keep_keys):
+    """The serialized bitmap holding only the containers of `buf` whose key is in keep_keys
+    (payload bytes copied verbatim; header per RB/RoaringArray.java:896-940)."""
+    keys, kinds, cards, offs, lens = container_table(buf)
+    sel = np.nonzero(np.isin(keys, np.asarray(list(keep_keys), dtype=np.int64)))[0]
+    size = len(sel)
+    has_run = bool(np.any(kinds[sel] == R))
+    out = bytearray()
+    if has_run:
+        out += struct.pack("<I", 12347 | ((size - 1) << 16))
+        fl = bytearray((size + 7) // 8)
+        for j, i in enumerate(sel):
+            if kinds[i] == R:
+                fl[j // 8] |= 1 << (j % 8)
+        out += fl
+        header = 4 + len(fl) + (4 * size if size < 4 else 8 * size)
+    else:
+        out += struct.pack("<II", 12346, size)
+        header = 8 + 8 * size
+    for i in sel:
+        out += struct.pack("<HH", int(keys[i]), int(cards[i] - 1))
+    if not has_run or size >= 4:
+        off = header
+        for i in sel:
+            out += struct.pack("<I", off)
+            off += int(lens[i])
+    for i in sel:
+        out += buf[int(offs[i]):int(offs[i] + lens[i])]
+    return bytes(out)
