@@ -245,6 +245,16 @@ int rbg_ctx_fetch(rbg_ctx* ctx, rbg_buffer* out);
 int rbg_ctx_fetch_shard(rbg_ctx* ctx, int64_t total_containers, int has_run,
                         int64_t first_container, int64_t payload_base, rbg_buffer* out_desc,
                         rbg_buffer* out_offsets, rbg_buffer* out_payload);
+/* Device form of rbg_ctx_fetch_shard, enqueued on the context stream (no host copy): the
+ * pending result's n containers are written as a key shard of the global bitmap straight
+ * into device memory -- desc_dst (4n bytes), offsets_dst (4n bytes of the global offset
+ * table; required iff the global bitmap has one: !has_run || total_containers >= 4),
+ * runflag_dst (n bytes, 1 = run container; used iff has_run, nullable otherwise) and
+ * payload_dst (this shard's payload bytes).  Any byte alignment.  Destinations may be
+ * views into the final global bitmap (each shard writes its slice at its
+ * global offset); the run-flag bytes are packed into the header by the assembler. */
+int rbg_ctx_fetch_shard_device(rbg_ctx* ctx, int64_t total_containers, int has_run, int64_t payload_base,
+                               void* desc_dst, void* offsets_dst, void* runflag_dst, void* payload_dst);
 
 #ifdef __cplusplus
 }

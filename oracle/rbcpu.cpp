@@ -4,6 +4,8 @@
 // RoaringBitmap/src/main/java/org/roaringbitmap/).
 #include "rbcpu.hpp"
 
+#include <map>
+
 #include <algorithm>
 #include <cstring>
 #include <stdexcept>
@@ -1426,6 +1428,364 @@ int32_t fa_or_card(const std::vector<const Bitmap*>& bms) {  // :90-101, horizon
     }
   }
   return (int32_t)card;
+}
+
+// ============================================================================
+// Lazy OR algebra and the alternative aggregations (ParallelAggregation,
+// horizontal_*, priorityqueue_*, BufferFastAggregation over Mutable bitmaps)
+// ============================================================================
+// ArrayContainer.lazyor(ArrayContainer), RB/ArrayContainer.java:1449-1463
+static Ctr A_lazyor_A(const Ctr& a, const Ctr& x) {
+  if (a.card + x.card > kArrayLazyLowerBound) return b_ilazyor(to_bitmap(a), x);  // toBitmapContainer().lazyIOR
+  return make_array(v_union(a.vals, x.vals));
+}
+// RunContainer.ilazyor(ArrayContainer), RB/RunContainer.java:1198-1240: a full container
+// is returned as is; otherwise ilazyorToRun, whose merge equals lazyorToRun's (a full
+// merge is the single run (0, 65535) either way) + convertToLazyBitmapIfNeeded
+static Ctr R_ilazyor_A(const Ctr& r, const Ctr& a) { return r.full() ? r : R_lazyor_A(r, a); }
+// RunContainer.ior(BitmapContainer) :1500-1506 / ior(RunContainer) :1508-1550 (the merge of
+// ior(R) then toEfficientContainer; R_or_R's extra full checks give the same container)
+static Ctr R_ior_B(const Ctr& r, const Ctr& b) { return r.full() ? r : R_or_B(r, b); }
+static Ctr R_ior_R(const Ctr& r, const Ctr& x) { return r.full() ? r : R_or_R(r, x); }
+
+// Container.lazyIOR, RB/Container.java:717-740
+Ctr c_lazy_ior(const Ctr& cur, const Ctr& x) {
+  switch (cur.kind) {
+    case ARRAY:
+      if (x.kind == ARRAY) return A_lazyor_A(cur, x);
+      if (x.kind == BITMAP) return B_or_A(x, cur);  // ior(BitmapContainer) = x.or(this), :748-750
+      return R_lazyor_A(x, cur);                     // x.lazyor(this)
+    case RUN:
+      if (x.kind == ARRAY) return R_ilazyor_A(cur, x);
+      if (x.kind == BITMAP) return R_ior_B(cur, x);
+      return R_ior_R(cur, x);
+    default:
+      return b_ilazyor(cur, x);  // BitmapContainer.ilazyor(A|B|R), RB/BitmapContainer.java:648-676
+  }
+}
+
+// Container.lazyOR, RB/Container.java:752-774 (not in place)
+Ctr c_lazy_or(const Ctr& a, const Ctr& x) {
+  switch (a.kind) {
+    case ARRAY:
+      if (x.kind == ARRAY) return A_lazyor_A(a, x);
+      if (x.kind == BITMAP) return b_ilazyor(x, a);  // BitmapContainer.lazyor(A): clone, card -1 (:878-888)
+      return R_lazyor_A(x, a);
+    case RUN:
+      if (x.kind == ARRAY) return R_lazyor_A(a, x);
+      if (x.kind == BITMAP) return b_ilazyor(x, a);  // BitmapContainer.lazyor(R) (:900-909)
+      return R_or_R(a, x);
+    default:
+      return b_ilazyor(a, x);  // BitmapContainer.lazyor(A|B|R) :878-909
+  }
+}
+
+// java.util.PriorityQueue (OpenJDK): array binary heap; add = siftUp, poll = last element
+// sifted down from the root.  Ties are resolved by this exact structure, so the poll order
+// of equal elements is reproduced.
+template <class T, class Cmp>
+struct JavaPQ {
+  std::vector<T> q;
+  Cmp cmp;
+  explicit JavaPQ(Cmp c) : cmp(c) {}
+  bool empty() const { return q.empty(); }
+  size_t size() const { return q.size(); }
+  const T& peek() const { return q[0]; }
+  void add(T x) {
+    size_t k = q.size();
+    q.push_back(x);
+    while (k > 0) {
+      size_t p = (k - 1) >> 1;
+      if (cmp(x, q[p]) >= 0) break;
+      q[k] = q[p];
+      k = p;
+    }
+    q[k] = x;
+  }
+  T poll() {
+    T r = q[0];
+    T x = q.back();
+    q.pop_back();
+    size_t n = q.size();
+    if (n > 0) {
+      size_t k = 0, half = n >> 1;
+      while (k < half) {
+        size_t c = 2 * k + 1, rr = c + 1;
+        if (rr < n && cmp(q[c], q[rr]) > 0) c = rr;
+        if (cmp(x, q[c]) <= 0) break;
+        q[k] = q[c];
+        k = c;
+      }
+      q[k] = x;
+    }
+    return r;
+  }
+};
+
+static std::map<uint16_t, std::vector<const Ctr*>> group_by_key(const std::vector<const Bitmap*>& bms) {
+  std::map<uint16_t, std::vector<const Ctr*>> g;  // ParallelAggregation.groupByKey :137-153
+  for (const Bitmap* b : bms)
+    for (size_t i = 0; i < b->size(); i++) g[b->keys[i]].push_back(&b->ctrs[i]);
+  return g;
+}
+
+// ParallelAggregation.or(List<Container>), RB/ParallelAggregation.java:197-223.  At 512 and
+// more containers the reference splits the list over the ForkJoin pool and ORs each part's
+// result into a lazy bitmap (OrCollector :103-130); like the 16..511 branch that ends in
+// BitmapContainer.repairAfterLazy of the lazy union, so both take the lazy-bitmap branch here.
+Ctr pa_or_key(const std::vector<const Ctr*>& cs) {
+  if (cs.size() < 16) {
+    Ctr r = *cs[0];
+    for (size_t i = 1; i < cs.size(); i++) r = c_lazy_ior(r, *cs[i]);
+    return repair_after_lazy(r);
+  }
+  Ctr r = make_bitmap_zero();
+  r.card = -1;
+  for (const Ctr* c : cs) r = b_ilazyor(r, *c);
+  return repair_after_lazy(r);
+}
+
+// ParallelAggregation.xor(List<Container>) :189-195: clone + ixor chain, no restart
+Ctr pa_xor_key(const std::vector<const Ctr*>& cs) {
+  Ctr r = *cs[0];
+  for (size_t i = 1; i < cs.size(); i++) r = c_ixor(r, *cs[i]);
+  return r;
+}
+
+Bitmap pa_or(const std::vector<const Bitmap*>& bms) {  // :161-175 (empty results kept, none occur)
+  Bitmap ans;
+  for (auto& kv : group_by_key(bms)) {
+    ans.keys.push_back(kv.first);
+    ans.ctrs.push_back(pa_or_key(kv.second));
+  }
+  return ans;
+}
+
+Bitmap pa_xor(const std::vector<const Bitmap*>& bms) {  // :182-187, ContainerCollector drops empties :71-77
+  Bitmap ans;
+  for (auto& kv : group_by_key(bms)) {
+    Ctr c = pa_xor_key(kv.second);
+    if (!c.empty()) {
+      ans.keys.push_back(kv.first);
+      ans.ctrs.push_back(std::move(c));
+    }
+  }
+  return ans;
+}
+
+// RoaringBitmap.lazyor(RoaringBitmap) in place, RB/RoaringBitmap.java:2357-2400
+// (MutableRoaringBitmap.lazyor, RB/buffer/MutableRoaringBitmap.java:1309-1351, has the same
+// per-key algebra through MappeableContainer.lazyIOR, RB/buffer/MappeableContainer.java:639-662)
+static void ip_lazy_or(Bitmap& a, const Bitmap& x2) {
+  size_t p1 = 0, p2 = 0;
+  while (p1 < a.size() && p2 < x2.size()) {
+    uint16_t s1 = a.keys[p1], s2 = x2.keys[p2];
+    if (s1 == s2) {
+      a.ctrs[p1] = c_lazy_ior(a.ctrs[p1], x2.ctrs[p2]);
+      p1++;
+      p2++;
+    } else if (s1 < s2) {
+      p1++;
+    } else {
+      a.keys.insert(a.keys.begin() + p1, s2);
+      a.ctrs.insert(a.ctrs.begin() + p1, x2.ctrs[p2]);
+      p1++;
+      p2++;
+    }
+  }
+  for (; p2 < x2.size(); p2++) { a.keys.push_back(x2.keys[p2]); a.ctrs.push_back(x2.ctrs[p2]); }
+}
+
+static void repair_all(Bitmap& b) {  // RoaringBitmap.repairAfterLazy :2752-2757
+  for (Ctr& c : b.ctrs) c = repair_after_lazy(c);
+}
+
+// BufferFastAggregation.naive_or(MutableRoaringBitmap...) :810-817 (and or(Mutable...) :896-898)
+Bitmap buf_or_mutable(const std::vector<const Bitmap*>& bms) {
+  Bitmap ans;
+  for (const Bitmap* b : bms) ip_lazy_or(ans, *b);
+  repair_all(ans);
+  return ans;
+}
+
+// ContainerPointer order (RB/RoaringArray.java:708-713): key, then larger cardinality first
+namespace {
+struct CPtr {
+  const Bitmap* b;
+  size_t i;
+  uint16_t key() const { return b->keys[i]; }
+  const Ctr& ctr() const { return b->ctrs[i]; }
+};
+struct CPtrCmp {
+  int operator()(const CPtr& x, const CPtr& y) const {
+    if (x.key() != y.key()) return (int)x.key() - (int)y.key();
+    return y.ctr().cardinality() - x.ctr().cardinality();
+  }
+};
+}  // namespace
+
+// FastAggregation.horizontal_or(List / RoaringBitmap...), RB/FastAggregation.java:124-231;
+// horizontal_xor(RoaringBitmap...) :243-289 (xor = true).  The poll order of the
+// container-pointer heap decides each key's chain.
+static Bitmap horizontal(const std::vector<const Bitmap*>& bms, bool xor_) {
+  Bitmap ans;
+  if (bms.empty()) return ans;
+  JavaPQ<CPtr, CPtrCmp> pq{CPtrCmp()};
+  for (const Bitmap* b : bms)
+    if (b->size()) pq.add(CPtr{b, 0});
+  auto advance_add = [&](CPtr x) {
+    x.i++;
+    if (x.i < x.b->size()) pq.add(x);
+  };
+  while (!pq.empty()) {
+    CPtr x1 = pq.poll();
+    if (pq.empty() || pq.peek().key() != x1.key()) {
+      ans.keys.push_back(x1.key());
+      ans.ctrs.push_back(x1.ctr());  // clone, no repair
+      advance_add(x1);
+      continue;
+    }
+    CPtr x2 = pq.poll();
+    Ctr newc = xor_ ? c_xor(x1.ctr(), x2.ctr()) : c_lazy_or(x1.ctr(), x2.ctr());
+    while (!pq.empty() && pq.peek().key() == x1.key()) {
+      CPtr x = pq.poll();
+      newc = xor_ ? c_ixor(newc, x.ctr()) : c_lazy_ior(newc, x.ctr());
+      x.i++;
+      if (x.i < x.b->size()) {
+        pq.add(x);
+      } else if (pq.empty()) {
+        break;
+      }
+    }
+    if (!xor_) newc = repair_after_lazy(newc);
+    ans.keys.push_back(x1.key());
+    ans.ctrs.push_back(std::move(newc));  // appended even when empty (xor)
+    advance_add(x1);
+    advance_add(x2);
+  }
+  return ans;
+}
+Bitmap fa_horizontal_or(const std::vector<const Bitmap*>& bms) { return horizontal(bms, false); }
+Bitmap fa_horizontal_xor(const std::vector<const Bitmap*>& bms) { return horizontal(bms, true); }
+
+// RoaringBitmap.getLongSizeInBytes, RB/RoaringBitmap.java:2212-2219 (A :450, B :498, R :1043)
+int64_t long_size_in_bytes(const Bitmap& b) {
+  int64_t size = 8;
+  for (const Ctr& c : b.ctrs)
+    size += 2 + (c.kind == ARRAY ? 2 * (int64_t)c.vals.size() + 4 : c.kind == BITMAP ? 8192 : 4 * (int64_t)c.nruns() + 4);
+  return size;
+}
+
+// FastAggregation.priorityqueue_xor(RoaringBitmap...), RB/FastAggregation.java:790-812
+Bitmap fa_priorityqueue_xor(const std::vector<const Bitmap*>& bms) {
+  if (bms.empty()) return Bitmap();
+  std::vector<Bitmap> pool;
+  pool.reserve(2 * bms.size());
+  std::vector<int64_t> sizes;
+  for (const Bitmap* b : bms) {
+    pool.push_back(*b);
+    sizes.push_back(long_size_in_bytes(*b));
+  }
+  auto cmp = [&](int a, int b) { return (int)(int32_t)(uint32_t)(uint64_t)(sizes[a] - sizes[b]); };
+  JavaPQ<int, decltype(cmp)> pq(cmp);
+  for (int k = 0; k < (int)bms.size(); k++) pq.add(k);
+  while (pq.size() > 1) {
+    int x1 = pq.poll(), x2 = pq.poll();
+    pool.push_back(op_xor(pool[x1], pool[x2]));
+    sizes.push_back(long_size_in_bytes(pool.back()));
+    pq.add((int)pool.size() - 1);
+  }
+  return pool[pq.poll()];
+}
+
+// RoaringBitmap.lazyor(x1, x2) static, RB/RoaringBitmap.java:723-767
+static Bitmap static_lazy_or(const Bitmap& x1, const Bitmap& x2) {
+  Bitmap a;
+  size_t p1 = 0, p2 = 0;
+  while (p1 < x1.size() && p2 < x2.size()) {
+    if (x1.keys[p1] == x2.keys[p2]) {
+      a.keys.push_back(x1.keys[p1]);
+      a.ctrs.push_back(c_lazy_or(x1.ctrs[p1++], x2.ctrs[p2++]));
+    } else if (x1.keys[p1] < x2.keys[p2]) {
+      a.keys.push_back(x1.keys[p1]);
+      a.ctrs.push_back(x1.ctrs[p1++]);
+    } else {
+      a.keys.push_back(x2.keys[p2]);
+      a.ctrs.push_back(x2.ctrs[p2++]);
+    }
+  }
+  for (; p1 < x1.size(); p1++) { a.keys.push_back(x1.keys[p1]); a.ctrs.push_back(x1.ctrs[p1]); }
+  for (; p2 < x2.size(); p2++) { a.keys.push_back(x2.keys[p2]); a.ctrs.push_back(x2.ctrs[p2]); }
+  return a;
+}
+
+// RoaringBitmap.lazyorfromlazyinputs, RB/RoaringBitmap.java:769-818: a bitmap container
+// goes first, then lazyIOR
+static Bitmap lazy_or_from_lazy(const Bitmap& x1, const Bitmap& x2) {
+  Bitmap a;
+  size_t p1 = 0, p2 = 0;
+  while (p1 < x1.size() && p2 < x2.size()) {
+    if (x1.keys[p1] == x2.keys[p2]) {
+      const Ctr* c1 = &x1.ctrs[p1];
+      const Ctr* c2 = &x2.ctrs[p2];
+      if (c2->kind == BITMAP && c1->kind != BITMAP) std::swap(c1, c2);
+      a.keys.push_back(x1.keys[p1]);
+      a.ctrs.push_back(c_lazy_ior(*c1, *c2));
+      p1++;
+      p2++;
+    } else if (x1.keys[p1] < x2.keys[p2]) {
+      a.keys.push_back(x1.keys[p1]);
+      a.ctrs.push_back(x1.ctrs[p1++]);
+    } else {
+      a.keys.push_back(x2.keys[p2]);
+      a.ctrs.push_back(x2.ctrs[p2++]);
+    }
+  }
+  for (; p1 < x1.size(); p1++) { a.keys.push_back(x1.keys[p1]); a.ctrs.push_back(x1.ctrs[p1]); }
+  for (; p2 < x2.size(); p2++) { a.keys.push_back(x2.keys[p2]); a.ctrs.push_back(x2.ctrs[p2]); }
+  return a;
+}
+
+// FastAggregation.priorityqueue_or(RoaringBitmap...), RB/FastAggregation.java:733-781
+Bitmap fa_priorityqueue_or(const std::vector<const Bitmap*>& bms) {
+  if (bms.empty()) return Bitmap();
+  const size_t n = bms.size();
+  std::vector<Bitmap> buf;
+  buf.reserve(n);
+  std::vector<int64_t> sizes(n);
+  std::vector<char> istmp(n, 0);
+  for (size_t k = 0; k < n; k++) {
+    buf.push_back(*bms[k]);
+    sizes[k] = long_size_in_bytes(buf[k]);
+  }
+  auto cmp = [&](int a, int b) { return (int)(int32_t)(uint32_t)(uint64_t)(sizes[a] - sizes[b]); };
+  JavaPQ<int, decltype(cmp)> pq(cmp);
+  for (int k = 0; k < (int)n; k++) pq.add(k);
+  while (pq.size() > 1) {
+    int x1 = pq.poll(), x2 = pq.poll();
+    if (istmp[x2] && istmp[x1]) {
+      buf[x1] = lazy_or_from_lazy(buf[x1], buf[x2]);
+      sizes[x1] = long_size_in_bytes(buf[x1]);
+      istmp[x1] = 1;
+      pq.add(x1);
+    } else if (istmp[x2]) {
+      ip_lazy_or(buf[x2], buf[x1]);
+      sizes[x2] = long_size_in_bytes(buf[x2]);
+      pq.add(x2);
+    } else if (istmp[x1]) {
+      ip_lazy_or(buf[x1], buf[x2]);
+      sizes[x1] = long_size_in_bytes(buf[x1]);
+      pq.add(x1);
+    } else {
+      buf[x1] = static_lazy_or(buf[x1], buf[x2]);
+      sizes[x1] = long_size_in_bytes(buf[x1]);
+      istmp[x1] = 1;
+      pq.add(x1);
+    }
+  }
+  Bitmap ans = buf[pq.poll()];
+  repair_all(ans);
+  return ans;
 }
 
 // ============================================================================

@@ -112,6 +112,21 @@ Bitmap fa_workshy_and(const std::vector<const Bitmap*>& bms);               // :
 int32_t fa_and_card(const std::vector<const Bitmap*>& bms);                 // :71-82
 int32_t fa_or_card(const std::vector<const Bitmap*>& bms);                  // :90-101
 
+// lazy OR algebra, RB/Container.java:717-774
+Ctr c_lazy_ior(const Ctr& cur, const Ctr& x);  // lazyIOR
+Ctr c_lazy_or(const Ctr& a, const Ctr& x);     // lazyOR
+// alternative aggregations (their result container types follow their own chains)
+Bitmap pa_or(const std::vector<const Bitmap*>& bms);                 // ParallelAggregation.or :161-175
+Bitmap pa_xor(const std::vector<const Bitmap*>& bms);                // ParallelAggregation.xor :182-195
+Ctr pa_or_key(const std::vector<const Ctr*>& cs);                    // :197-223
+Ctr pa_xor_key(const std::vector<const Ctr*>& cs);                   // :189-195
+Bitmap buf_or_mutable(const std::vector<const Bitmap*>& bms);        // BufferFastAggregation.naive_or(Mutable...)
+Bitmap fa_horizontal_or(const std::vector<const Bitmap*>& bms);      // FastAggregation.horizontal_or :124-231
+Bitmap fa_horizontal_xor(const std::vector<const Bitmap*>& bms);     // :243-289
+Bitmap fa_priorityqueue_or(const std::vector<const Bitmap*>& bms);   // :733-781
+Bitmap fa_priorityqueue_xor(const std::vector<const Bitmap*>& bms);  // :790-812
+int64_t long_size_in_bytes(const Bitmap& b);                         // RoaringBitmap.getLongSizeInBytes
+
 // ---- portable format, RB/RoaringArray.java ---------------------------------
 enum Status : int { OK = 0, ERR_FORMAT = -1, ERR_TRUNCATED = -2, ERR_ARG = -3 };
 std::vector<uint8_t> serialize(const Bitmap& b);                            // :896-940

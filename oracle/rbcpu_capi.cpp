@@ -1,8 +1,12 @@
 // C entry points of the CPU ORACLE (test infrastructure only; see rbcpu.hpp).
 // Loaded through ctypes by tests/ and by bench.py's cpu_baseline leg.
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <thread>
 #include <vector>
 
 #include "rbcpu.hpp"
@@ -75,7 +79,10 @@ int rbo_pairwise_card(int op, const uint8_t* a, size_t an, const uint8_t* b, siz
   return ERR_ARG;
 }
 
-// op: 0 FastAggregation.and(varargs), 1 or, 2 xor, 3 and(Iterator), 4 naive_and, 5 workShyAnd
+// op: 0 FastAggregation.and(varargs), 1 or, 2 xor, 3 and(Iterator), 4 naive_and, 5 workShyAnd,
+//     6 ParallelAggregation.or, 7 ParallelAggregation.xor, 8 BufferFastAggregation.or(Mutable...),
+//     9 FastAggregation.horizontal_or(varargs/List), 10 horizontal_xor, 11 priorityqueue_or,
+//     12 priorityqueue_xor
 int rbo_wide(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, const int* ids,
              uint8_t** out, size_t* out_len) {
   std::vector<Bitmap> bms;
@@ -89,8 +96,22 @@ int rbo_wide(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, c
     case 3: return emit(fa_and_iter(ptrs), out, out_len);
     case 4: return emit(fa_naive_and(ptrs, ids), out, out_len);
     case 5: return emit(n ? fa_workshy_and(ptrs) : Bitmap(), out, out_len);
+    case 6: return emit(pa_or(ptrs), out, out_len);
+    case 7: return emit(pa_xor(ptrs), out, out_len);
+    case 8: return emit(buf_or_mutable(ptrs), out, out_len);
+    case 9: return emit(fa_horizontal_or(ptrs), out, out_len);
+    case 10: return emit(fa_horizontal_xor(ptrs), out, out_len);
+    case 11: return emit(fa_priorityqueue_or(ptrs), out, out_len);
+    case 12: return emit(fa_priorityqueue_xor(ptrs), out, out_len);
   }
   return ERR_ARG;
+}
+
+// RoaringBitmap.getLongSizeInBytes of a serialized bitmap (RB/RoaringBitmap.java:2212-2219)
+int64_t rbo_long_size(const uint8_t* a, size_t an) {
+  Bitmap b;
+  if (load(a, an, &b)) return -1;
+  return long_size_in_bytes(b);
 }
 
 // op: 0 andCardinality(varargs), 1 orCardinality(varargs)
@@ -184,6 +205,87 @@ double rbo_time_wide(int op, const uint8_t* const* bufs, const size_t* lens, siz
       case 1: sink += (int64_t)fa_or(ptrs).size(); break;
       case 2: sink += (int64_t)fa_xor(ptrs).size(); break;
     }
+  }
+  return now_s() - t0;
+}
+
+// ---- multi-threaded legs (key-parallel, like ParallelAggregation's ForkJoin stream over
+// keys, RB/ParallelAggregation.java:171-173): `threads` workers take key groups from a
+// shared counter.  op 0: ParallelAggregation.or, 1: ParallelAggregation.xor.  Returns
+// seconds for `reps` runs (inputs parsed outside the clock; groupByKey inside, as in Java).
+double rbo_time_wide_parallel(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int threads,
+                              int reps) {
+  std::vector<Bitmap> bms;
+  std::vector<const Bitmap*> ptrs;
+  if (load_many(bufs, lens, n, &bms, &ptrs)) return -1.0;
+  volatile int64_t sink = 0;
+  double t0 = now_s();
+  for (int r = 0; r < reps; r++) {
+    std::map<uint16_t, std::vector<const Ctr*>> g;  // groupByKey :137-153
+    for (const Bitmap* b : ptrs)
+      for (size_t i = 0; i < b->size(); i++) g[b->keys[i]].push_back(&b->ctrs[i]);
+    std::vector<const std::vector<const Ctr*>*> slices;
+    std::vector<uint16_t> keys;
+    for (auto& kv : g) {
+      keys.push_back(kv.first);
+      slices.push_back(&kv.second);
+    }
+    std::vector<Ctr> vals(slices.size());
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, threads); t++)
+      th.emplace_back([&]() {
+        for (size_t k; (k = next.fetch_add(16)) < slices.size();)
+          for (size_t j = k; j < std::min(slices.size(), k + 16); j++)
+            vals[j] = op == 0 ? pa_or_key(*slices[j]) : pa_xor_key(*slices[j]);
+      });
+    for (auto& x : th) x.join();
+    Bitmap ans;
+    for (size_t j = 0; j < vals.size(); j++)
+      if (op == 0 || !vals[j].empty()) {
+        ans.keys.push_back(keys[j]);
+        ans.ctrs.push_back(std::move(vals[j]));
+      }
+    sink += (int64_t)ans.size();
+  }
+  return now_s() - t0;
+}
+
+// Key-parallel RoaringBitmap.and(x1, x2) (the per-key container AND of :377-401 over
+// `threads` contiguous key ranges); seconds for `reps` runs.
+double rbo_time_and_parallel(const uint8_t* a, size_t an, const uint8_t* b, size_t bn, int threads, int reps) {
+  Bitmap x, y;
+  if (load(a, an, &x) || load(b, bn, &y)) return -1.0;
+  const int T = std::max(1, threads);
+  volatile int64_t sink = 0;
+  double t0 = now_s();
+  for (int r = 0; r < reps; r++) {
+    std::vector<Bitmap> part(T);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      th.emplace_back([&, t]() {
+        const int klo = (65536 * t) / T, khi = (65536 * (t + 1)) / T;
+        size_t p1 = std::lower_bound(x.keys.begin(), x.keys.end(), (uint16_t)klo) - x.keys.begin();
+        size_t p2 = std::lower_bound(y.keys.begin(), y.keys.end(), (uint16_t)klo) - y.keys.begin();
+        Bitmap& o = part[t];
+        while (p1 < x.size() && p2 < y.size() && x.keys[p1] < khi && y.keys[p2] < khi) {
+          if (x.keys[p1] == y.keys[p2]) {
+            Ctr c = c_and(x.ctrs[p1], y.ctrs[p2]);
+            if (!c.empty()) {
+              o.keys.push_back(x.keys[p1]);
+              o.ctrs.push_back(std::move(c));
+            }
+            p1++;
+            p2++;
+          } else if (x.keys[p1] < y.keys[p2]) {
+            p1++;
+          } else {
+            p2++;
+          }
+        }
+      });
+    for (auto& z : th) z.join();
+    for (auto& p : part) sink += (int64_t)p.size();
   }
   return now_s() - t0;
 }

@@ -38,6 +38,7 @@ EXPORTED = [
     "rbg_ctx_batch_counts", "rbg_synth_key_bytes", "rbg_ctx_pair_bytes", "rbg_debug_stamps",
     "rbg_bsi_compare", "rbg_bsi_sum", "rbg_ctx_bsi", "rbg_ctx_bsi_sums", "rbg_ctx_batch_minmax",
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
+    "rbg_ctx_fetch_shard_device",
 ]
 
 _lib = None
@@ -100,6 +101,7 @@ def _declare(L):
     L.rbg_ctx_fetch.argtypes = [vp, buf]
     L.rbg_ctx_profile.argtypes = [vp, ctypes.c_int]
     L.rbg_ctx_profile_read.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_int)]
+    L.rbg_ctx_fetch_shard_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp]
     L.rbg_ctx_fetch_shard.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, buf, buf,
                                       buf]
 

@@ -1535,45 +1535,76 @@ int rbg_ctx_fetch(rbg_ctx* ctx, rbg_buffer* out) {
   HIPCHK(hipSetDevice(ctx->c.device));
   return ctx_fetch(&ctx->c, out);
 }
+// Key-shard placement of the pending result inside a global portable bitmap of
+// total_containers containers, enqueued on the context stream.
+static int ctx_fetch_shard_device(Ctx* c, int64_t total_containers, int has_run, int64_t payload_base, void* desc_dst,
+                                  void* offsets_dst, void* runflag_dst, void* payload_dst) {
+  if (c->last != 1) {
+    set_err("no materialised result pending");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  if (total_containers < 0 || total_containers > kMaxKeys || payload_base < 0 || !desc_dst || !payload_dst) {
+    set_err("fetch_shard: bad layout or null destination");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  const bool offsets = !has_run || total_containers >= 4;  // RB/RoaringArray.java:927-933
+  if (offsets && !offsets_dst) {
+    set_err("fetch_shard: the global bitmap has an offset table; offsets_dst is required");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  const uint64_t off0 = header_size((size_t)total_containers, has_run != 0) + (uint64_t)payload_base;
+  if (off0 > 0xFFFFFFFFull) {
+    set_err("fetch_shard: payload offsets exceed 32 bits");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  uint8_t* emit_dst = (uint8_t*)payload_dst;
+  if (c->serialized) {
+    // already serialized (possibly because an operand batch was released since): copy the
+    // payload region rather than re-reading the operands' pass-through containers
+    ResultInfo ri;
+    CHK(ctx_info(c, &ri));
+    if (ri.payload)
+      HIPCHK(hipMemcpyAsync(payload_dst, c->result.as<uint8_t>() + c->pending.payload_base, ri.payload,
+                            hipMemcpyDeviceToDevice, c->stream));
+    emit_dst = nullptr;
+  }
+  launch_serialize_shard(c->stream, grid_for((c->pending_ub + 255) / 256, 256), c->ntasks.as<uint32_t>(), c->pending,
+                         emit_dst, off0, (uint8_t*)desc_dst, offsets ? (uint8_t*)offsets_dst : nullptr,
+                         has_run ? (uint8_t*)runflag_dst : nullptr);
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
+
+int rbg_ctx_fetch_shard_device(rbg_ctx* ctx, int64_t total_containers, int has_run, int64_t payload_base,
+                               void* desc_dst, void* offsets_dst, void* runflag_dst, void* payload_dst) {
+  if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_fetch_shard_device(&ctx->c, total_containers, has_run, payload_base, desc_dst, offsets_dst, runflag_dst,
+                                payload_dst);
+}
+
 int rbg_ctx_fetch_shard(rbg_ctx* ctx, int64_t total_containers, int has_run, int64_t first_container,
                         int64_t payload_base, rbg_buffer* out_desc, rbg_buffer* out_offsets, rbg_buffer* out_payload) {
-  HIPCHK(hipSetDevice(ctx->c.device));
-  rbg_buffer local = {nullptr, 0};
-  CHK(ctx_fetch(&ctx->c, &local));
-  std::unique_ptr<uint8_t, void (*)(void*)> hold(local.data, std::free);
+  if (!ctx || !out_desc || !out_offsets || !out_payload) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx& c = ctx->c;
+  HIPCHK(hipSetDevice(c.device));
+  (void)first_container;  // the shard's own buffers start at its first container
   ResultInfo ri;
-  CHK(ctx_info(&ctx->c, &ri));
+  CHK(ctx_info(&c, &ri));
   const size_t n = ri.n_out;
-  const size_t desc_base = ri.has_run ? 4 + (n + 7) / 8 : 8;
-  std::vector<uint8_t> desc(local.data + desc_base, local.data + desc_base + 4 * n);
-  std::vector<uint8_t> payload(local.data + ri.header, local.data + ri.total);
-  // global offsets: header(total, has_run) + payload_base + local payload offset
-  std::vector<uint8_t> offs;
-  const bool global_offsets = !has_run || total_containers >= 4;
-  if (global_offsets && n) {
-    const uint64_t gh = header_size((size_t)total_containers, has_run != 0);
-    // local payload offsets from the descriptors: recompute sizes by walking payloads
-    uint64_t pos = 0;
-    const uint8_t* flags = ri.has_run ? local.data + 4 : nullptr;
-    for (size_t i = 0; i < n; i++) {
-      const uint32_t o = (uint32_t)(gh + payload_base + pos);
-      for (int k = 0; k < 4; k++) offs.push_back((uint8_t)(o >> (8 * k)));
-      const uint16_t card1 = (uint16_t)(desc[4 * i + 2] | (desc[4 * i + 3] << 8));
-      const bool is_run = flags && (flags[i / 8] & (1 << (i % 8)));
-      if (is_run) {
-        const uint8_t* q = local.data + ri.header + pos;
-        pos += 2 + 4 * (uint64_t)(q[0] | (q[1] << 8));
-      } else if ((uint32_t)card1 + 1 > 4096) {
-        pos += 8192;
-      } else {
-        pos += 2 * ((uint64_t)card1 + 1);
-      }
-    }
-  }
-  (void)first_container;
-  CHK(emit_host(desc, out_desc));
-  CHK(emit_host(offs, out_offsets));
-  return emit_host(payload, out_payload);
+  const bool offsets = !has_run || total_containers >= 4;
+  DevBuf d;
+  CHK(d.ensure(9 * n + ri.payload + 64));
+  uint8_t* base = d.as<uint8_t>();
+  CHK(ctx_fetch_shard_device(&c, total_containers, has_run, payload_base, base, base + 4 * n, base + 8 * n,
+                             base + 9 * n));
+  std::vector<uint8_t> h(9 * n + ri.payload);
+  if (!h.empty()) HIPCHK(hipMemcpyAsync(h.data(), base, h.size(), hipMemcpyDeviceToHost, c.stream));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  CHK(emit_host(std::vector<uint8_t>(h.begin(), h.begin() + 4 * n), out_desc));
+  CHK(emit_host(offsets ? std::vector<uint8_t>(h.begin() + 4 * n, h.begin() + 8 * n) : std::vector<uint8_t>(),
+                out_offsets));
+  return emit_host(std::vector<uint8_t>(h.begin() + 9 * n, h.end()), out_payload);
 }
 
 // C3 synthetic key slice [key_lo, key_hi) of n bitmaps (kind 1 uniform, 2 clustered)

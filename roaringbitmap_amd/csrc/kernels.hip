@@ -389,13 +389,33 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
 }
 
 // payload copies of the scan placement: one workgroup per task (grid-stride)
-__global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ n_tasks, OutCtx oc) {
+// dst: the payload region (oc.out + oc.payload_base, or a key shard's place in a global bitmap)
+__global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ n_tasks, OutCtx oc, uint8_t* __restrict__ dst) {
   const uint32_t nt = *n_tasks;
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     const ORec r = oc.recs[t];
     if (!r.keep) continue;
-    group_copy<NT>(oc.out + oc.payload_base + r.off, reinterpret_cast<const uint8_t*>(r.src), r.ser_len,
-                   threadIdx.x);
+    group_copy<NT>(dst + r.off, reinterpret_cast<const uint8_t*>(r.src), r.ser_len, threadIdx.x);
+  }
+}
+
+// Key-shard placement: this shard's descriptors, its entries of the
+// global offset table (global header bytes + the shard's payload base + local offset) and
+// one run-flag byte per container, written straight into the caller's buffers.
+__global__ __launch_bounds__(256) void k_shard_table(const uint32_t* __restrict__ n_tasks, OutCtx oc, uint64_t off0,
+                                                     uint8_t* __restrict__ desc, uint8_t* __restrict__ offs,
+                                                     uint8_t* __restrict__ runb) {
+  const uint32_t nt = *n_tasks;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    const ORec r = oc.recs[t];
+    if (!r.keep) continue;
+    const uint32_t d = (uint32_t)r.key | ((r.card - 1) << 16);
+    for (int k = 0; k < 4; k++) desc[4ull * r.idx + k] = (uint8_t)(d >> (8 * k));
+    if (offs) {
+      const uint32_t o = (uint32_t)(off0 + r.off);
+      for (int k = 0; k < 4; k++) offs[4ull * r.idx + k] = (uint8_t)(o >> (8 * k));
+    }
+    if (runb) runb[r.idx] = r.kind == DK_R ? 1 : 0;
   }
 }
 
@@ -445,9 +465,14 @@ void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info
   hipLaunchKernelGGL(k_place, dim3(64), dim3(256), 0, s, nt, oc, info);
 }
 void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out) {
-  hipLaunchKernelGGL(k_emit, dim3(4096), dim3(256), 0, s, nt, oc);
+  hipLaunchKernelGGL(k_emit, dim3(4096), dim3(256), 0, s, nt, oc, oc.out + oc.payload_base);
   hipLaunchKernelGGL(k_header, dim3(grid), dim3(256), 0, s, nt, oc, kind_by_out, (ResultInfo*)nullptr);
   hipLaunchKernelGGL(k_runflags, dim3(32), dim3(256), 0, s, nt, oc, (const uint8_t*)kind_by_out);
+}
+void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* payload_dst, uint64_t off0,
+                            uint8_t* desc, uint8_t* offs, uint8_t* runb) {
+  if (payload_dst) hipLaunchKernelGGL(k_emit, dim3(4096), dim3(256), 0, s, nt, oc, payload_dst);
+  hipLaunchKernelGGL(k_shard_table, dim3(grid), dim3(256), 0, s, nt, oc, off0, desc, offs, runb);
 }
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info,
                         const uint32_t* err) {

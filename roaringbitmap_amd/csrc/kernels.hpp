@@ -72,6 +72,10 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
 // cookie) runs only when the result is fetched
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info);
 void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out);
+// key shard of a global bitmap: payloads into payload_dst, 4 B descriptors into desc, global
+// offsets (off0 + local offset) into offs (nullable), one run-flag byte per container into runb (nullable)
+void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* payload_dst, uint64_t off0,
+                            uint8_t* desc, uint8_t* offs, uint8_t* runb);
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info,
                         const uint32_t* err);
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload, unsigned long long* out);

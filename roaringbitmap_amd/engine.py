@@ -186,6 +186,17 @@ class Engine:
         check(lib().rbg_ctx_fetch(self._ctx, ctypes.byref(b)))
         return RoaringBitmap(take(b))
 
+    def fetch_shard_device(self, total_containers, has_run, payload_base, desc, offsets, runflags, payload):
+        """Enqueue the pending result as a key shard of a global bitmap, written straight into
+        device memory (torch tensors or raw pointers; offsets / runflags may be None when the
+        global layout has no offset table / no run container).  Asynchronous: sync() before use."""
+        def ptr(t):
+            if t is None:
+                return None
+            return int(t) if isinstance(t, int) else int(t.data_ptr())
+        check(lib().rbg_ctx_fetch_shard_device(self._ctx, int(total_containers), int(bool(has_run)), int(payload_base),
+                                               ptr(desc), ptr(offsets), ptr(runflags), ptr(payload)))
+
     def fetch_shard(self, total_containers, has_run, first_container, payload_base):
         d, o, p = _lib.rbg_buffer(), _lib.rbg_buffer(), _lib.rbg_buffer()
         check(lib().rbg_ctx_fetch_shard(self._ctx, int(total_containers), int(has_run), int(first_container),

@@ -18,8 +18,11 @@ are small ones:
 * for andCardinality / orCardinality, an all-reduce of the int64 partial sums,
   wrapped to a Java int at the end.
 
-`concat_serialized` builds the global bitmap from the shard results. On a
-distributed run, `gather_bytes` brings every shard to every rank first.
+The result is assembled on rank 0's device (`assemble`): every rank writes its slice's
+descriptors, global offset-table entries, run bytes and payload (`engine_fill`, i.e.
+rbg_ctx_fetch_shard_device) and rank 0 receives each slice straight into its place in
+the global bitmap over point-to-point RCCL. `concat_serialized` / `gather_bytes` are the
+host-bytes form of the same assembly.
 
 The collectives run over torch.distributed ("nccl" = RCCL over xGMI on ROCm; the
 CPU tests use "gloo"). The per-shard compute is passed in as a callable;
@@ -207,6 +210,178 @@ def sharded_wide_card(partial, group=None, device="cpu"):
     t = torch.tensor([int(partial)], dtype=torch.int64, device=device)
     dist.all_reduce(t, group=group)
     return int(np.int64(t.item()).astype(np.int32))
+
+
+# ---------------------------------------------------------------------------
+# device-resident result assembly
+# ---------------------------------------------------------------------------
+class GlobalLayout:
+    """Where every shard's slice goes in the global portable bitmap (RB/RoaringArray.java:896-940).
+
+    per_rank: int64 [world, 3] = (containers, payload bytes, has_run) of every rank's key slice,
+    in key-range order.
+    """
+
+    def __init__(self, per_rank):
+        a = np.asarray(per_rank, dtype=np.int64).reshape(-1, 3)
+        self.n = a[:, 0].copy()
+        self.pay = a[:, 1].copy()
+        self.total = int(self.n.sum())
+        self.has_run = bool(a[:, 2].any())
+        self.first = np.concatenate([[0], np.cumsum(self.n)[:-1]]).astype(np.int64)
+        self.base = np.concatenate([[0], np.cumsum(self.pay)[:-1]]).astype(np.int64)
+        self.header = header_size(self.total, self.has_run)
+        self.flag_bytes = (self.total + 7) // 8 if self.has_run else 0
+        self.desc_base = 4 + self.flag_bytes if self.has_run else 8
+        self.offsets = (not self.has_run) or self.total >= 4
+        self.off_base = self.desc_base + 4 * self.total
+        self.nbytes = self.header + int(self.pay.sum())
+
+    def cookie(self) -> bytes:
+        if self.has_run:
+            return (SERIAL_COOKIE | ((self.total - 1) << 16)).to_bytes(4, "little")
+        return SERIAL_COOKIE_NO_RUN.to_bytes(4, "little") + self.total.to_bytes(4, "little")
+
+
+def exchange_layout(n_containers, payload_bytes, has_run, group=None, device="cpu"):
+    """All-gather of (containers, payload bytes, has_run) -> GlobalLayout (single process: world 1)."""
+    import torch
+    mine = [int(n_containers), int(payload_bytes), int(bool(has_run))]
+    dist = _dist()
+    if not (dist.is_available() and dist.is_initialized()):
+        return GlobalLayout([mine])
+    t = torch.tensor(mine, dtype=torch.int64, device=device)
+    allv = [torch.zeros_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(allv, t, group=group)
+    return GlobalLayout(torch.stack(allv).cpu().numpy())
+
+
+def _pack_flags(runb):
+    """One byte per container (1 = run) -> the run-flag bitset (bit i%8 of byte i/8)."""
+    import torch
+    n = runb.numel()
+    pad = torch.zeros(((n + 7) // 8) * 8, dtype=torch.int32, device=runb.device)
+    pad[:n] = runb.to(torch.int32)
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.int32, device=runb.device)
+    return (pad.view(-1, 8) * w).sum(dim=1).to(torch.uint8)
+
+
+def assemble(fill, lay, rank=0, group=None, fill_device="cuda", comm_device="cuda", sync=None):
+    """Assemble the global portable bitmap on rank 0 from every rank's key slice.
+
+    fill(total, has_run, payload_base, desc, offsets, runflags, payload) writes this rank's
+    slice into the given uint8 tensors (on fill_device): its descriptors, its entries of the
+    global offset table, one run byte per container and its payload (Engine.fetch_shard_device
+    for the HIP engine).  sync() (optional) waits for the fill.  Rank 0 owns the output buffer;
+    its own slice is written in place and every other slice is received straight into its
+    place (point-to-point over RCCL/xGMI, or gloo on the CPU) -- no all-gather of bulk data.
+    Returns the uint8 tensor of the global bitmap on rank 0, None elsewhere.
+    """
+    import torch
+    r = rank
+    n, pay = int(lay.n[r]), int(lay.pay[r])
+
+    def views(buf, runb, rr):
+        nr, f, b = int(lay.n[rr]), int(lay.first[rr]), int(lay.base[rr])
+        d = buf[lay.desc_base + 4 * f: lay.desc_base + 4 * (f + nr)]
+        o = buf[lay.off_base + 4 * f: lay.off_base + 4 * (f + nr)] if lay.offsets else None
+        rb_ = runb[f: f + nr] if runb is not None else None
+        p = buf[lay.header + b: lay.header + b + int(lay.pay[rr])]
+        return d, o, rb_, p
+
+    def local(dev):
+        d = torch.empty(4 * n, dtype=torch.uint8, device=dev)
+        o = torch.empty(4 * n, dtype=torch.uint8, device=dev) if lay.offsets else None
+        rb_ = torch.empty(n, dtype=torch.uint8, device=dev) if lay.has_run else None
+        p = torch.empty(pay, dtype=torch.uint8, device=dev)
+        return d, o, rb_, p
+
+    def do_fill(parts):
+        if n:
+            fill(lay.total, lay.has_run, int(lay.base[r]), *parts)
+            if sync is not None:
+                sync()
+
+    world = len(lay.n)
+    if r == 0:
+        out = torch.empty(lay.nbytes, dtype=torch.uint8, device=comm_device)
+        runb = torch.zeros(lay.total, dtype=torch.uint8, device=comm_device) if lay.has_run else None
+        mine = views(out, runb, 0)
+        if torch.device(fill_device) == torch.device(comm_device):
+            do_fill(mine)
+        else:
+            tmp = local(fill_device)
+            do_fill(tmp)
+            for dst, src in zip(mine, tmp):
+                if dst is not None:
+                    dst.copy_(src)
+        ops = []
+        if world > 1:
+            dist = _dist()
+            for rr in range(1, world):
+                if not int(lay.n[rr]):
+                    continue
+                src = rr if group is None else dist.get_global_rank(group, rr)
+                ops += [(t, src) for t in views(out, runb, rr) if t is not None and t.numel()]
+        reqs = _p2p([(dist.irecv, t, peer) for t, peer in ops], group) if ops else []
+        out[:len(lay.cookie())] = torch.tensor(list(lay.cookie()), dtype=torch.uint8, device=comm_device)
+        for q in reqs:
+            q.wait()
+        if lay.has_run and lay.total:
+            out[4:4 + lay.flag_bytes] = _pack_flags(runb)
+        return out
+    parts = local(fill_device)
+    do_fill(parts)
+    if n:
+        dist = _dist()
+        dst = 0 if group is None else dist.get_global_rank(group, 0)
+        sends = [t if torch.device(fill_device) == torch.device(comm_device) else t.to(comm_device)
+                 for t in parts if t is not None and t.numel()]
+        for q in _p2p([(dist.isend, t, dst) for t in sends], group):
+            q.wait()
+    return None
+
+
+def _p2p(ops, group):
+    """Point-to-point ops; grouped (one ncclGroup, all peers' transfers concurrent over their
+    own xGMI links) on RCCL, posted in order on gloo."""
+    dist = _dist()
+    if dist.get_backend(group) == "nccl":
+        return dist.batch_isend_irecv([dist.P2POp(fn, t, peer, group) for fn, t, peer in ops])
+    kw = {} if group is None else {"group": group}
+    return [fn(t, peer, **kw) for fn, t, peer in ops]
+
+
+def engine_fill(engine):
+    """fill() of assemble() for the HIP engine's pending result (Engine.fetch_shard_device)."""
+    def fill(total, has_run, payload_base, desc, offsets, runflags, payload):
+        engine.fetch_shard_device(total, has_run, payload_base, desc, offsets, runflags, payload)
+    return fill
+
+
+def serialized_fill(buf):
+    """fill() of assemble() from a shard result held as serialized bytes (CPU stand-in for tests)."""
+    import torch
+    keys, cm1, runs, sizes, payload = parse_layout(buf)
+
+    def fill(total, has_run, payload_base, desc, offsets, runflags, pay):
+        d = np.empty((len(keys), 2), dtype="<u2")
+        d[:, 0], d[:, 1] = keys, cm1
+        desc.copy_(torch.frombuffer(bytearray(d.tobytes()), dtype=torch.uint8))
+        if offsets is not None:
+            o = header_size(total, has_run) + payload_base + np.concatenate([[0], np.cumsum(sizes)[:-1]])
+            offsets.copy_(torch.frombuffer(bytearray(np.asarray(o, dtype="<u4").tobytes()), dtype=torch.uint8))
+        if runflags is not None:
+            runflags.copy_(torch.from_numpy(runs.astype(np.uint8)))
+        if len(payload):
+            pay.copy_(torch.frombuffer(bytearray(payload), dtype=torch.uint8))
+    return fill
+
+
+def shard_stats(buf):
+    """(containers, payload bytes, has_run) of a serialized shard result."""
+    keys, _, runs, sizes, _ = parse_layout(buf)
+    return len(keys), int(sizes.sum()), bool(runs.any())
 
 
 def engine_shard(engine, op, batch, key_lo, key_hi, ids=None):

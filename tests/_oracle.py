@@ -52,6 +52,15 @@ def lib():
         L.rbo_time_wide.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
                                     ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_int]
         L.rbo_time_wide.restype = ctypes.c_double
+        L.rbo_time_wide_parallel.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p),
+                                             ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_int,
+                                             ctypes.c_int]
+        L.rbo_time_wide_parallel.restype = ctypes.c_double
+        L.rbo_time_and_parallel.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                                            ctypes.c_int, ctypes.c_int]
+        L.rbo_time_and_parallel.restype = ctypes.c_double
+        L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
     return _lib
 
@@ -75,7 +84,9 @@ def _check(st):
 
 OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3}
 CARD_OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
-WIDE_OPS = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5}
+WIDE_OPS = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5,
+            "parallel_or": 6, "parallel_xor": 7, "buffer_or_mutable": 8, "horizontal_or": 9, "horizontal_xor": 10,
+            "priorityqueue_or": 11, "priorityqueue_xor": 12}
 
 
 def pairwise(op, a: bytes, b: bytes) -> bytes:
@@ -166,3 +177,19 @@ def time_pairwise(op, a, b, reps):
 def time_wide(op, bufs, reps):
     arr, lens = _bufs(bufs)
     return lib().rbo_time_wide({"and": 0, "or": 1, "xor": 2}[op], arr, lens, len(bufs), reps)
+
+
+def time_wide_parallel(op, bufs, threads, reps):
+    """ParallelAggregation.or / xor semantics, key groups over `threads` workers; seconds for reps runs."""
+    arr, lens = _bufs(bufs)
+    return lib().rbo_time_wide_parallel({"or": 0, "xor": 1}[op], arr, lens, len(bufs), threads, reps)
+
+
+def time_and_parallel(a, b, threads, reps):
+    """Key-parallel RoaringBitmap.and over `threads` key ranges; seconds for reps runs."""
+    return lib().rbo_time_and_parallel(a, len(a), b, len(b), threads, reps)
+
+
+def long_size(buf) -> int:
+    """RoaringBitmap.getLongSizeInBytes (RB/RoaringBitmap.java:2212-2219)."""
+    return int(lib().rbo_long_size(buf, len(buf)))

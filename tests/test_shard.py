@@ -74,6 +74,18 @@ def _fmt_kind(k):
     return R if k % 2 else A
 
 
+@pytest.mark.parametrize("n_keys", [1, 3, 5, 40])
+def test_assemble_single_process(n_keys):
+    """assemble() at world 1 (no process group): the global bitmap of one shard, including
+    the run-flag packing and the size < 4 layout without offsets."""
+    bufs = _inputs(5 + n_keys, 6, nkeys=n_keys)
+    for op in ("or", "xor"):
+        part = O.wide(op, bufs)
+        lay = shard.GlobalLayout([shard.shard_stats(part)])
+        out = shard.assemble(shard.serialized_fill(part), lay, 0, fill_device="cpu", comm_device="cpu")
+        assert bytes(out.numpy().tobytes()) == part
+
+
 def test_parse_layout_golden():
     gold = os.path.join(os.path.dirname(__file__), "golden", "testdata")
     for name in ("bitmapwithruns.bin", "bitmapwithoutruns.bin"):
@@ -114,19 +126,28 @@ def _worker(rank, world, port, outdir):
         counts = np.array([len(decode(b)) for b in mine], dtype=np.int64)
         res["start"] = shard.global_start("naive_and", counts)
         res["card_or"] = shard.sharded_wide_card(O.wide_card("or", mine) if any(len(decode(b)) for b in mine) else 0)
+        # device-style assembly on rank 0: slices received straight into their global place
+        for op in ("or", "xor", "workshy_and"):
+            part = O.wide(op, mine)
+            lay = shard.exchange_layout(*shard.shard_stats(part))
+            out = shard.assemble(shard.serialized_fill(part), lay, rank, fill_device="cpu", comm_device="cpu")
+            if rank == 0:
+                res[op + "_assembled"] = bytes(out.numpy().tobytes())
         if rank == 0:
             np.save(os.path.join(outdir, "res.npy"), np.array([res], dtype=object), allow_pickle=True)
     finally:
         dist.destroy_process_group()
 
 
-def test_world2_gloo_sharded_wide():
+@pytest.mark.parametrize("world", [2, 3])
+def test_world_gloo_sharded_wide(world):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
         res = np.load(os.path.join(d, "res.npy"), allow_pickle=True)[0]  # written by this test's own worker
     bufs = _inputs(77, 13)
     for op in ("or", "xor", "workshy_and"):
         assert res[op] == O.wide(op, bufs), op
+        assert res[op + "_assembled"] == O.wide(op, bufs), op
         full = decode(O.wide(op, bufs))
         n_total, has_run, first, base = res[op + "_layout"]
         assert n_total == len(full) and first == 0 and base == 0
