@@ -67,7 +67,18 @@ enum { RBG_CARD_AND = 0, RBG_CARD_OR = 1, RBG_CARD_XOR = 2, RBG_CARD_ANDNOT = 3,
  *   RBG_WIDE_NAIVE_AND   naive_and(RoaringBitmap...) :328-346 for any N
  *   RBG_WIDE_WORKSHY_AND workShyAnd(long[], RoaringBitmap...) :356-414 for any N >= 1 */
 enum { RBG_WIDE_AND = 0, RBG_WIDE_OR = 1, RBG_WIDE_XOR = 2, RBG_WIDE_AND_ITER = 3, RBG_WIDE_NAIVE_AND = 4,
-       RBG_WIDE_WORKSHY_AND = 5 };
+       RBG_WIDE_WORKSHY_AND = 5,
+/* alternative aggregations, each with its own result container types:
+ *   RBG_WIDE_PARALLEL_OR        ParallelAggregation.or(RoaringBitmap...)  RB/ParallelAggregation.java:161-175,197-223
+ *   RBG_WIDE_PARALLEL_XOR       ParallelAggregation.xor(RoaringBitmap...) :182-195
+ *   RBG_WIDE_BUFFER_OR_MUTABLE  BufferFastAggregation.or / naive_or(MutableRoaringBitmap...)
+ *                               RB/buffer/BufferFastAggregation.java:810-817,896-898 (lazyor chain)
+ *   RBG_WIDE_HORIZONTAL_OR      FastAggregation.horizontal_or(List / RoaringBitmap...) RB/FastAggregation.java:124-231
+ *   RBG_WIDE_HORIZONTAL_XOR     FastAggregation.horizontal_xor(RoaringBitmap...) :243-289
+ * The horizontal_* chain order is the poll order of the reference's container-pointer
+ * priority queue, planned from the container table (keys and cardinalities). */
+       RBG_WIDE_PARALLEL_OR = 6, RBG_WIDE_PARALLEL_XOR = 7, RBG_WIDE_BUFFER_OR_MUTABLE = 8,
+       RBG_WIDE_HORIZONTAL_OR = 9, RBG_WIDE_HORIZONTAL_XOR = 10 };
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
 

@@ -131,6 +131,7 @@ struct Ctx {
   uint64_t* ztile = nullptr;
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
+  DevBuf order;                     // horizontal_*: chain order of every key segment
   int bsi_nbits = 0;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw,
       scalar, scratch;
@@ -616,6 +617,101 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   return RBG_OK;
 }
 
+static int batch_host_index(Ctx* c, Batch* b);
+
+// Chain order of horizontal_or / horizontal_xor (RB/FastAggregation.java:124-289): the
+// reference drains a java.util.PriorityQueue of one container pointer per bitmap, ordered
+// by key, then larger cardinality first (RB/RoaringArray.java:708-713), with the heap's own
+// tie order.  The heap is replayed here over the container table (keys and cardinalities
+// only -- no payload); order[key_off[k] + j] = the j-th container of key k's chain.
+namespace {
+struct HPtr {
+  uint32_t bm, i, key, card, pos;
+};
+static int hcmp(const HPtr& x, const HPtr& y) {  // ContainerPointer.compareTo
+  if (x.key != y.key) return (int)x.key - (int)y.key;
+  return (int)y.card - (int)x.card;
+}
+struct JHeap {  // java.util.PriorityQueue siftUp / siftDown (OpenJDK)
+  std::vector<HPtr> q;
+  void add(const HPtr& x) {
+    size_t k = q.size();
+    q.push_back(x);
+    while (k > 0) {
+      const size_t p = (k - 1) >> 1;
+      if (hcmp(x, q[p]) >= 0) break;
+      q[k] = q[p];
+      k = p;
+    }
+    q[k] = x;
+  }
+  HPtr poll() {
+    const HPtr r = q[0];
+    const HPtr x = q.back();
+    q.pop_back();
+    const size_t n = q.size();
+    if (n) {
+      size_t k = 0;
+      const size_t half = n >> 1;
+      while (k < half) {
+        size_t ch = 2 * k + 1;
+        if (ch + 1 < n && hcmp(q[ch], q[ch + 1]) > 0) ch++;
+        if (hcmp(x, q[ch]) <= 0) break;
+        q[k] = q[ch];
+        k = ch;
+      }
+      q[k] = x;
+    }
+    return r;
+  }
+};
+}  // namespace
+
+static int horizontal_order(Ctx* c, Batch* B) {
+  CHK(batch_host_index(c, B));
+  std::vector<uint32_t> order;
+  order.reserve(B->n_ctr);
+  auto ptr = [&](uint32_t bm, uint32_t i) {
+    const uint32_t pos = B->h_pos[B->h_pos_off[bm] + i];
+    const CDesc& d = B->h_desc[pos];
+    return HPtr{bm, i, d.key, d.card, pos};
+  };
+  auto has = [&](uint32_t bm, uint32_t i) { return B->h_pos_off[bm] + i < B->h_pos_off[bm + 1]; };
+  JHeap pq;
+  for (uint32_t b = 0; b < B->n_bm; b++)
+    if (has(b, 0)) pq.add(ptr(b, 0));
+  auto advance_add = [&](const HPtr& x) {
+    if (has(x.bm, x.i + 1)) pq.add(ptr(x.bm, x.i + 1));
+  };
+  while (!pq.q.empty()) {
+    const HPtr x1 = pq.poll();
+    order.push_back(x1.pos);
+    if (pq.q.empty() || pq.q[0].key != x1.key) {
+      advance_add(x1);
+      continue;
+    }
+    const HPtr x2 = pq.poll();
+    order.push_back(x2.pos);
+    while (!pq.q.empty() && pq.q[0].key == x1.key) {
+      const HPtr x = pq.poll();
+      order.push_back(x.pos);
+      if (has(x.bm, x.i + 1)) pq.add(ptr(x.bm, x.i + 1));
+      else if (pq.q.empty()) break;
+    }
+    advance_add(x1);
+    advance_add(x2);
+  }
+  if (order.size() != B->n_ctr) {
+    set_err("horizontal order: container table inconsistent");
+    return RBG_ERR_DEVICE;
+  }
+  CHK(c->order.ensure(4 * std::max<size_t>(order.size(), 1)));
+  if (!order.empty())
+    HIPCHK(hipMemcpyAsync(c->order.p, order.data(), 4 * order.size(), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));  // `order` is a stack vector
+  return RBG_OK;
+}
+
 // FastAggregation dispatch (RB/FastAggregation.java:26-101,653-666,823-836)
 // start_override >= 0: naive_and starts from that input (key-range shards pass the
 // input with the fewest containers over the WHOLE universe, RB/FastAggregation.java:333-339)
@@ -633,7 +729,8 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
   const size_t N = B->n_bm;
   *host_card_valid = false;
   int mode = WIDE_OR, plan_mode = 0;
-  uint32_t start_bm = 0;
+  uint32_t start_bm = 0, chain = 0;
+  const uint32_t* order = nullptr;
   std::vector<uint8_t> skip;
   if (card_only) {
     // andCardinality: 0 -> 0, 1 -> card, >= 2 -> per-key AND sum (== andCardinality / workShyAndCardinality)
@@ -687,6 +784,16 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
           }
         }
         break;
+      case RBG_WIDE_PARALLEL_OR: mode = WIDE_LAZY_CHAIN; chain = kChainLimit16; break;
+      case RBG_WIDE_PARALLEL_XOR: mode = WIDE_XOR_CHAIN; break;
+      case RBG_WIDE_BUFFER_OR_MUTABLE: mode = WIDE_LAZY_CHAIN; break;
+      case RBG_WIDE_HORIZONTAL_OR:
+      case RBG_WIDE_HORIZONTAL_XOR:
+        mode = op == RBG_WIDE_HORIZONTAL_OR ? WIDE_LAZY_CHAIN : WIDE_XOR_CHAIN;
+        chain = op == RBG_WIDE_HORIZONTAL_OR ? kChainN1Clone : kChainKeepEmpty;
+        CHK(horizontal_order(c, B));
+        order = c->order.as<uint32_t>();
+        break;
       default: return RBG_ERR_ILLEGAL_ARGUMENT;
     }
   }
@@ -718,6 +825,8 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.start_bm = start_bm;
     wa.all_array = (B->n_kind[DK_B] == 0 && B->n_kind[DK_R] == 0) ? 1u : 0u;
     wa.slot32 = B->payload_bytes < (1ull << 36) ? 1u : 0u;
+    wa.order = order;
+    wa.chain = chain;
     c->mark(1);
     launch_wide(s, mode, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
                 c->task_card.as<uint32_t>());
@@ -971,7 +1080,7 @@ int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, 
 }
 
 int rbg_wide(int op, const uint8_t* const* bufs, const size_t* lens, const int32_t* ids, size_t n, rbg_buffer* out) {
-  if (!out || op < 0 || op > 5) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!out || op < 0 || op > RBG_WIDE_HORIZONTAL_XOR) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
@@ -1234,6 +1343,7 @@ int rbg_ctx_batch_fetch_range(rbg_ctx* ctx, int32_t batch, size_t first, size_t 
 }
 }  // extern "C"
 
+namespace rbg {
 // Host index of a batch's containers, built once per batch: the container table and,
 // per input bitmap, its container positions (in key order).
 static int batch_host_index(Ctx* c, Batch* b) {
@@ -1257,6 +1367,8 @@ static int batch_host_index(Ctx* c, Batch* b) {
   b->h_index = true;
   return RBG_OK;
 }
+
+}  // namespace rbg
 
 // Download bitmaps [i0, i1) of a batch as portable serialized bytes: their slots are
 // gathered on the device into one buffer (one D2H copy), the headers built here.

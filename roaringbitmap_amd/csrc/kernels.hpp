@@ -16,7 +16,15 @@ enum WideMode : int {
   WIDE_AND_SHY = 3,    // workShyAnd
   WIDE_AND_SHY_CARD = 4,  // workShyAndCardinality
   WIDE_AND_NAIVE = 5,  // naive_and chain
+  WIDE_LAZY_CHAIN = 6,  // lazyIOR chain + repairAfterLazy: ParallelAggregation.or, BufferFastAggregation.or(Mutable...),
+                        // horizontal_or
+  WIDE_XOR_CHAIN = 7,   // clone + ixor chain without restart: ParallelAggregation.xor, horizontal_xor
 };
+
+// WideArgs::chain flags
+constexpr uint32_t kChainLimit16 = 1;  // ParallelAggregation.or: 16+ containers per key take the lazy-bitmap branch
+constexpr uint32_t kChainN1Clone = 2;  // a key of one container is a plain clone (no repairAfterLazy)
+constexpr uint32_t kChainKeepEmpty = 4;  // horizontal_xor appends empty results
 
 struct WideArgs {
   const CDesc* desc;      // key-major container table
@@ -26,6 +34,8 @@ struct WideArgs {
   uint32_t start_bm;      // naive_and: input bitmap the chain starts from
   uint32_t all_array;     // every container is an array (slots padded with their last value)
   uint32_t slot32;        // every slot offset / 16 fits 32 bits (payload < 64 GiB)
+  const uint32_t* order;  // chain modes: container index at chain position j of a key segment (null: input order)
+  uint32_t chain;         // chain modes: kChain* flags
 };
 
 // bit-sliced index (bsi.hip); ops in the order of BitmapSliceIndex.Operation

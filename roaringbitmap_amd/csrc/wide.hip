@@ -265,6 +265,119 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         c = st_card;
         kind = st_kind;
       }
+    } else if (MODE == WIDE_LAZY_CHAIN) {
+      // Container.lazyIOR chain from a clone of the first container, then repairAfterLazy
+      // (RB/Container.java:717-740; ParallelAggregation.or :197-206, RoaringBitmap.lazyor
+      // :2357-2400 for BufferFastAggregation.or(Mutable...), horizontal_or :124-231, whose
+      // lazyOR first step types alike).  The state is the container class of the running
+      // result; its set is the running union r:
+      //   A + A: ArrayContainer.lazyor, a lazy bitmap above 1024 values (:1449-1463)
+      //   A + B, R + B, B + any: a bitmap (full bitmaps end as R.full either way)
+      //   A + R, R + A: lazyorToRun / ilazyorToRun, a lazy bitmap above 4096 runs (:1765-1813)
+      //   R + R: RunContainer.ior -> toEfficientContainer (:1508-1550)
+      // Once a bitmap, always a bitmap: the rest of the segment is OR-ed in bulk.
+      const CDesc d0 = A.desc[A.order ? A.order[s] : s];
+      if (n == 1) {
+        if ((A.chain & kChainN1Clone) || d0.kind != DK_R) {
+          wg_passthrough(t, d0, A.payload, oc, &shp);
+          continue;
+        }
+        const int nr = *reinterpret_cast<const uint16_t*>(A.payload + d0.slot + 2);
+        if (eff((int)d0.card, nr) == DK_R) {
+          wg_passthrough(t, d0, A.payload, oc, &shp);
+          continue;
+        }
+        materialize(d0, A.payload, tmp, q, r);  // toBitmapOrArrayContainer
+        c = (int)d0.card;
+        kind = by_card(c);
+      } else {
+        int st = d0.kind, cur = (int)d0.card;
+        bool bulk = (A.chain & kChainLimit16) && n >= 16;  // ParallelAggregation.or :208-214
+        if (bulk) {  // a lazy bitmap from the start
+          st = DK_B;
+#pragma unroll
+          for (int i = 0; i < 4; i++) r[i] = 0;
+        } else {
+          materialize(d0, A.payload, tmp, q, r);
+          for (uint32_t j = 1; j < n; j++) {
+            if (st == DK_B) {
+              bulk = true;
+              break;
+            }
+            const CDesc d = A.desc[A.order ? A.order[s + j] : s + j];
+            uint64_t x[4];
+            materialize(d, A.payload, tmp, q, x);
+#pragma unroll
+            for (int i = 0; i < 4; i++) r[i] |= x[i];
+            if (st == DK_A && d.kind == DK_A) {
+              if (cur + (int)d.card > 1024) st = DK_B;
+              else cur = block_card(r, sh);
+            } else if (d.kind == DK_B) {
+              st = DK_B;
+            } else if (st == DK_R && d.kind == DK_R) {
+              const int cc = block_card(r, sh);
+              st = eff(cc, count_runs(r, acc, sh));
+              cur = cc;
+            } else {  // A + R, R + A
+              st = count_runs(r, acc, sh) > 4096 ? DK_B : DK_R;
+            }
+          }
+        }
+        if (bulk) {
+          __syncthreads();
+          lds_clear(acc);
+          accumulate_segment<0>(A.desc, A.payload, s, n, acc, q, big, nbig, bslot, A.slot32 != 0, r);
+        }
+        c = block_card(r, sh);
+        if (st == DK_B) kind = c == 65536 ? DK_R : by_card(c);  // BitmapContainer.repairAfterLazy
+        else if (st == DK_R) kind = eff(c, count_runs(r, acc, sh));  // RunContainer.repairAfterLazy
+        else kind = DK_A;
+      }
+    } else if (MODE == WIDE_XOR_CHAIN) {
+      // clone + ixor chain with no restart after an empty result (ParallelAggregation.xor
+      // :189-195; horizontal_xor :243-289, whose first xor types like ixor).  An empty run
+      // container XOR a run container is a clone of the latter (RB/RunContainer.java:2445-2452).
+      int clone = (int)(A.order ? A.order[s] : s);
+      const CDesc d0 = A.desc[clone];
+      if (n == 1) {
+        wg_passthrough(t, d0, A.payload, oc, &shp);
+        continue;
+      }
+      materialize(d0, A.payload, tmp, q, r);
+      int st_kind = d0.kind, st_card = (int)d0.card;
+      for (uint32_t j = 1; j < n; j++) {
+        const int idx = (int)(A.order ? A.order[s + j] : s + j);
+        const CDesc d = A.desc[idx];
+        if (st_kind == DK_R && d.kind == DK_R && d.card == 0) continue;  // x empty: this.clone()
+        uint64_t x[4];
+        materialize(d, A.payload, tmp, q, x);
+        if (st_kind == DK_R && st_card == 0 && d.kind == DK_R) {  // this empty: x.clone()
+#pragma unroll
+          for (int i = 0; i < 4; i++) r[i] = x[i];
+          st_card = (int)d.card;
+          clone = idx;
+          continue;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) r[i] ^= x[i];
+        const int cc = block_card(r, sh);
+        const bool need_r = (st_kind == DK_R && d.kind == DK_R) ||
+                            (st_kind == DK_R && d.kind == DK_A && d.card < 32) ||
+                            (st_kind == DK_A && d.kind == DK_R && st_card < 32);
+        st_kind = need_r ? eff(cc, count_runs(r, acc, sh)) : by_card(cc);
+        st_card = cc;
+        clone = -1;
+      }
+      if (st_card == 0 && !(A.chain & kChainKeepEmpty)) {
+        wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
+        continue;
+      }
+      if (clone >= 0) {
+        wg_passthrough(t, A.desc[clone], A.payload, oc, &shp);
+        continue;
+      }
+      c = st_card;
+      kind = st_kind;
     } else if (MODE == WIDE_AND_SHY || MODE == WIDE_AND_SHY_CARD) {
 #pragma unroll
       for (int i = 0; i < 4; i++) r[i] = ~0ULL;
@@ -355,6 +468,12 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
       break;
     case WIDE_AND_SHY_CARD:
       hipLaunchKernelGGL((k_wide<WIDE_AND_SHY_CARD>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_AND_SHY_CARD>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+      break;
+    case WIDE_LAZY_CHAIN:
+      hipLaunchKernelGGL((k_wide<WIDE_LAZY_CHAIN>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_LAZY_CHAIN>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+      break;
+    case WIDE_XOR_CHAIN:
+      hipLaunchKernelGGL((k_wide<WIDE_XOR_CHAIN>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_XOR_CHAIN>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
       break;
     default:
       hipLaunchKernelGGL((k_wide<WIDE_AND_NAIVE>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_AND_NAIVE>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);

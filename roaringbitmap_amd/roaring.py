@@ -287,25 +287,30 @@ class FastAggregation:
         return _wide_card("or", bms)
 
 
-    # The priority-queue / horizontal variants (RB/FastAggregation.java:110-300, 677-822)
-    # compute the same sets as or / xor.  horizontal_or(Iterator) is naive_or itself
-    # (:110-112), so its bytes are the reference's; for the List / varargs forms and
-    # priorityqueue_*, whose per-key container types follow their own lazyOR chains,
-    # the result is set-equal to the reference's with FastAggregation.or / xor types.
+    # The horizontal / priority-queue variants (RB/FastAggregation.java:110-300, 677-822) compute
+    # the same sets as or / xor, but each fixes its own result container types through its
+    # own chain; every form below reproduces those types (byte parity with the reference).
     @staticmethod
     def horizontal_or(*args):
+        """horizontal_or(Iterator) :110-112 is naive_or; horizontal_or(List) :124-175 and
+        horizontal_or(RoaringBitmap...) :185-231 run the container-pointer priority queue"""
+        if len(args) == 1 and isinstance(args[0], Iterator):
+            return _wide("or", list(args[0]))
+        bms = list(args[0]) if len(args) == 1 and isinstance(args[0], (list, tuple)) else list(args)
+        return _wide("horizontal_or", bms)
+
+    @staticmethod
+    def horizontal_xor(*bitmaps):
+        """horizontal_xor(RoaringBitmap...) :243-289 (empty results are kept as empty containers)"""
+        bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
+        return _wide("horizontal_xor", bms)
+
+    @staticmethod
+    def priorityqueue_or(*args):
         if len(args) == 1 and isinstance(args[0], Iterator):
             return _wide("or", list(args[0]))
         bms = list(args[0]) if len(args) == 1 and isinstance(args[0], (list, tuple)) else list(args)
         return _wide("or", bms)
-
-    @staticmethod
-    def priorityqueue_or(*args):
-        return FastAggregation.horizontal_or(*args)
-
-    @staticmethod
-    def horizontal_xor(*bitmaps):
-        return _wide("xor", list(bitmaps))
 
     @staticmethod
     def priorityqueue_xor(*bitmaps):
@@ -313,22 +318,23 @@ class FastAggregation:
 
 
 class ParallelAggregation:
-    """RB/ParallelAggregation.java: or (:161-175) and xor (:182-195).
+    """RB/ParallelAggregation.java: or (:161-175, per key :197-223) and xor (:182-195).
 
-    The reference's ForkJoin reduction is the CPU baseline of this path.  Its sets are
-    FastAggregation's; its per-key container types depend on the pool's parallelism
-    for keys with 512 or more containers (:218-223), so byte parity is defined
-    against FastAggregation -- these return FastAggregation.or /
-    xor results, which the reference's own ParallelAggregationTest accepts (it
-    compares sets)."""
+    The reference reduces each key's containers on the ForkJoin pool; the engine reduces
+    every key in parallel on the GPU with the reference's per-key algorithm, so the result
+    container types are ParallelAggregation's own: below 16 containers a key is a lazyIOR
+    chain from a clone of the first (repairAfterLazy at the end), from 16 on a lazy bitmap;
+    xor is a clone + ixor chain without FastAggregation's restart, empty keys dropped."""
 
     @staticmethod
     def or_(*bitmaps):
-        return _wide("or", list(bitmaps))
+        bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
+        return _wide("parallel_or", bms)
 
     @staticmethod
     def xor(*bitmaps):
-        return _wide("xor", list(bitmaps))
+        bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
+        return _wide("parallel_xor", bms)
 
 
 class BufferFastAggregation:
@@ -388,7 +394,18 @@ class BufferFastAggregation:
 
     @staticmethod
     def naive_or(*args):
+        """naive_or(ImmutableRoaringBitmap...) :774-781 / (Iterator) :791-798: naivelazyor chain"""
         return FastAggregation.naive_or(*args)
+
+    @staticmethod
+    def or_mutable(*bitmaps):
+        """or(MutableRoaringBitmap...) :896-898 -> naive_or(MutableRoaringBitmap...) :810-817:
+        MutableRoaringBitmap.lazyor per input (RB/buffer/MutableRoaringBitmap.java:1309-1351),
+        i.e. a lazyIOR chain per key, then repairAfterLazy"""
+        bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
+        return _wide("buffer_or_mutable", bms)
+
+    naive_or_mutable = or_mutable
 
     @staticmethod
     def naive_xor(*args):

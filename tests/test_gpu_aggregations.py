@@ -1,0 +1,95 @@
+"""ParallelAggregation, BufferFastAggregation.or(Mutable...), horizontal_or / horizontal_xor on
+the GPU, byte-exact against the oracle's restatements (tests/test_aggregation_oracle.py pins
+those to the reference's tests).
+
+Inputs mix every container family of tests/_gen.py at few keys so that many keys hold
+2..15 containers (the lazyIOR chain of ParallelAggregation.or, RB/ParallelAggregation.java:
+200-206) and some hold 16+ (its lazy-bitmap branch :208-214), plus equal-cardinality
+array / run containers at one key, whose chain order comes from the heap's tie order
+(horizontal_*, RB/FastAggregation.java:124-289).
+"""
+import numpy as np
+import pytest
+
+import _gen
+import _oracle as O
+from _fmt import A, R, encode
+
+pytestmark = pytest.mark.gpu
+
+OPS = ["parallel_or", "parallel_xor", "buffer_or_mutable", "horizontal_or", "horizontal_xor"]
+
+
+def _wide(op, bufs):
+    import roaringbitmap_amd as rb
+    from roaringbitmap_amd.roaring import _wide as w
+    return w(op, [rb.RoaringBitmap(b) for b in bufs]).serialize()
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 15, 16, 40])
+def test_aggregations_random(gpu, seed, n):
+    rng = np.random.default_rng(1000 * n + seed)
+    keys = np.sort(rng.choice(65536, 12, replace=False))
+    bufs = [_gen.bitmap(rng, keys, p_present=0.6) for _ in range(n)]
+    for op in OPS:
+        assert _wide(op, bufs) == O.wide(op, bufs), (op, n, seed)
+
+
+@pytest.mark.parametrize("modes", [["a_tiny", "a_small"], ["a_small", "r_tiny", "r_single"], ["r_tie", "r_few", "a_32"],
+                                   ["a_mid", "r_mid"], ["r_many", "a_small"], ["b_mid", "a_small", "r_tiny"]])
+def test_aggregations_mode_mixes(gpu, modes):
+    """Mixes that walk the chain's thresholds: 1024 values for A + A, 4096 runs for A + R,
+    toEfficientContainer for R + R, empty XOR results (kept by horizontal_xor)."""
+    rng = np.random.default_rng(len("".join(modes)))
+    keys = np.arange(0, 8)
+    for n in (2, 4, 9, 15):
+        bufs = [_gen.bitmap(rng, keys, modes=modes, p_present=0.9) for _ in range(n)]
+        bufs.append(bufs[0])  # identical containers: XOR chains reach empty results
+        for op in OPS:
+            assert _wide(op, bufs) == O.wide(op, bufs), (op, modes, n)
+
+
+def test_horizontal_equal_cardinality_ties(gpu):
+    """Array and run containers of equal cardinality at one key: the chain order is the
+    reference heap's tie order."""
+    rng = np.random.default_rng(3)
+    bufs = []
+    for i in range(9):
+        card = 100 if i % 3 else 700
+        if i % 2:
+            s = int(rng.integers(0, 60000))
+            ctr = (0, R, np.arange(s, s + card, dtype=np.uint16))
+        else:
+            ctr = (0, A, np.sort(rng.choice(65536, card, replace=False)).astype(np.uint16))
+        bufs.append(encode([ctr, (1, A, np.array([i], dtype=np.uint16))]))
+    for op in OPS:
+        assert _wide(op, bufs) == O.wide(op, bufs), op
+
+
+def test_aggregations_c3_slices(gpu):
+    """C3-style inputs (many bitmaps, mostly small arrays per key) through the chain modes."""
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+    for kind, lo, hi in ((1, 5000, 5040), (2, 0, 65536)):
+        b = e.synth(kind, 0xC3000000, 40, lo, hi)
+        bms = [x.serialize() for x in e.batch_fetch_range(b)]
+        for op in OPS:
+            e.wide(op, b)
+            assert e.fetch().serialize() == O.wide(op, bms), (kind, op)
+        e.release(b)
+
+
+def test_host_api_names(gpu):
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(11)
+    keys = np.sort(rng.choice(4000, 20, replace=False))
+    bufs = [_gen.bitmap(rng, keys, p_present=0.7) for _ in range(6)]
+    bms = [rb.RoaringBitmap(b) for b in bufs]
+    assert getattr(rb.ParallelAggregation, "or")(*bms).serialize() == O.wide("parallel_or", bufs)
+    assert rb.ParallelAggregation.xor(*bms).serialize() == O.wide("parallel_xor", bufs)
+    assert rb.BufferFastAggregation.or_mutable(*bms).serialize() == O.wide("buffer_or_mutable", bufs)
+    assert rb.FastAggregation.horizontal_or(bms).serialize() == O.wide("horizontal_or", bufs)
+    assert rb.FastAggregation.horizontal_or(*bms).serialize() == O.wide("horizontal_or", bufs)
+    assert rb.FastAggregation.horizontal_or(iter(bms)).serialize() == O.wide("or", bufs)
+    assert rb.FastAggregation.horizontal_xor(*bms).serialize() == O.wide("horizontal_xor", bufs)
