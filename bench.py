@@ -17,8 +17,15 @@ barrier + synchronize bracket the timed loop and the max time over ranks is used
 Prints ONE JSON line (rank 0).  Extra fields:
   roofline     - dominant kernel (container compute) achieved algorithmic GB/s vs
                  the 8 TB/s HBM peak, timed with HIP events on the engine's stream
-  cpu_baseline - the CPU oracle (C++ restatement, 1 thread) on the same pair
-  extra        - per-phase times, container mix, result size
+  cpu_baseline - the CPU oracle (C++ restatement of the reference, not the JVM: no JDK here) on
+                 this host: key-parallel RoaringBitmap.and on the same C2 pair (value), plus
+                 legs for 1 thread and for C3 wide OR samples (FastAggregation 1 thread,
+                 ParallelAggregation key-parallel), host nproc / CPU model
+  extra        - per-phase times, container mix, result size, C3 (whole sharded op with the
+                 result assembled on GPU 0), C4, C5, runOptimize, decode
+
+`python bench.py --gpus N` without a launcher re-runs itself under torch.distributed.run with N
+ranks; `--only W` runs one workload alone (per-workload rocprofv3 --pmc passes).
 """
 import argparse
 import json
@@ -34,25 +41,46 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 METRIC = "wide-OR/pairwise-AND input GB/s + % of HBM peak at 1/2/4/8 MI355X"
 
 
-def _pmc_traffic():
-    """Per-launch HBM bytes of the compute kernel from a committed rocprofv3 --pmc pass."""
+def _pmc_traffic(key="k_pair_wave"):
+    """Per-launch HBM bytes of a kernel from a committed rocprofv3 --pmc pass of that workload
+    alone (profiles/pmc_traffic.json, written by scripts/summarize_prof.py)."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
         with open(p) as f:
-            return json.load(f).get("k_pair_wave", {}).get("hbm_bytes_per_launch")
+            return json.load(f).get(key, {}).get("hbm_bytes_per_launch")
     except Exception:
         return None
+
+
+def _cpu_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity": avail, "model": model}
 
 
 def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
     """C3 wide OR (or AND) of n synthetic bitmaps, key-range sharded over the ranks.
 
-    Each rank generates and reduces only its key slice (equal input bytes); one
-    step = the slice's FastAggregation.or + the RCCL all-gather of the shard
-    layout (containers, payload bytes, has_run) that places every shard in the
-    global portable result.  Strong scaling: the 10,000-bitmap job is fixed.
+    Each rank generates and reduces only its key slice (equal input bytes).  One step is the
+    whole sharded op with its result assembled on rank 0's GPU as the portable bitmap:
+    the slice's FastAggregation.or, the RCCL all-gather of the shard layout (containers,
+    payload bytes, has_run), every rank writing its descriptors / global offsets / payload
+    (rbg_ctx_fetch_shard_device) and rank 0 receiving each slice straight into its place
+    (point-to-point RCCL).  At one GPU the same step writes the whole bitmap in place.
+    Strong scaling: the 10,000-bitmap job is fixed.
     """
     import torch
     from roaringbitmap_amd import shard
@@ -66,26 +94,33 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
     b = eng.synth(kind, seed, n, lo, hi)
     st = eng.batch_stats(b)
     in_bytes = st["payload_bytes"] + 4 * st["containers"]
-    dev = torch.device("cuda", torch.cuda.current_device()) if cdev == "cuda" else torch.device("cpu")
+    dev = torch.device("cuda", torch.cuda.current_device())
+    comm = dev if cdev == "cuda" else torch.device("cpu")
+    fill = shard.engine_fill(eng)
 
     def step():
         eng.wide(op, b, lo, hi)
-        if dist is not None:
-            rs = eng.result_stats()
-            shard.global_layout(rs["containers"], rs["payload_bytes"], rs["has_run"], device=dev)
+        if dist is None:  # one GPU: the device serialization is the whole bitmap, no host round trip
+            eng.serialize()
+            return None, None
+        rs = eng.result_stats()
+        lay = shard.exchange_layout(rs["containers"], rs["payload_bytes"], rs["has_run"], device=comm)
+        return shard.assemble(fill, lay, rank, fill_device=dev, comm_device=comm, sync=eng.sync), lay
 
     for _ in range(warmup):
-        step()
-    eng.sync()
+        out, lay = step()
+    torch.cuda.synchronize()
     rs = eng.result_stats()
     out_bytes = rs["payload_bytes"] + 4 * rs["containers"]
+    total_bytes = lay.nbytes if lay is not None else shard.header_size(rs["containers"], rs["has_run"]) + \
+        rs["payload_bytes"]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
-    eng.sync()
+        out, lay = step()
+    torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     wall = time.perf_counter() - t0
@@ -95,7 +130,7 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
     k, ph = eng.profile_read()
     eng.profile(0)
     kern_ms = ph[1] / max(k, 1)
-    t = torch.tensor([wall, float(in_bytes), float(out_bytes)], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, float(in_bytes), float(out_bytes)], dtype=torch.float64, device=comm)
     if dist is not None:
         tm = t.clone()
         dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
@@ -105,13 +140,15 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
     eng.release(b)
     ms = wall / steps * 1e3
     ach = (in_bytes + out_bytes) / (kern_ms / 1e3) / 1e9
+    tkey = f"k_wide<OR>_{'uniform' if kind == 1 else 'clustered'}"
     return {"workload": f"C3 {'uniform' if kind == 1 else 'clustered'}: FastAggregation.{op} of {n} synthetic bitmaps, "
-                        f"key-range sharded over {world} GPU(s)",
+                        f"key-range sharded over {world} GPU(s), result assembled on GPU 0",
             **({"input_GBps": round(tin / (wall / steps) / 1e9, 1)} if op == "or" else {}),
             "ms_per_step": round(ms, 4), "input_bytes": int(tin), "output_bytes": int(tout),
-            "containers_in": st["containers"], "rank0_keys": [lo, hi],
+            "result_serialized_bytes": int(total_bytes), "containers_in": st["containers"], "rank0_keys": [lo, hi],
             "roofline_rank0": ({"kernel": "k_wide<OR>", "achieved_GBps": round(ach, 1),
-                                "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern_ms, 4)} if op == "or" else
+                                "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern_ms, 4),
+                                "traffic": _pmc_traffic(tkey)} if op == "or" else
                                {"kernel": "k_wide<AND_SHY>", "kernel_ms": round(kern_ms, 4),
                                 "note": "per key the chain stops at an empty intersection: the bytes read are far "
                                         "below input_bytes, so no roofline fraction is claimed"})}
@@ -230,8 +267,74 @@ def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
     return {"workload": f"C5: RoaringBitmapSliceIndex.compare(RANGE, 2^29, 2^30) + sum over {rows} rows x 31 slices, "
                         f"key-range sharded over {world} GPU(s)",
             "rows_per_s": round(rows / step_s, 1), "ms_per_step": round(step_s * 1e3, 4),
-            "index_bytes": int(t[1]), "input_GBps_2pass": round(2 * float(t[1]) / step_s / 1e9, 1),
+            "index_bytes": int(t[1]), "index_GBps": round(float(t[1]) / step_s / 1e9, 1),
+            "frac_of_peak_1pass": round(float(t[1]) / step_s / 1e9 / HBM_PEAK_GBS, 4),
+            "traffic_k_bsi": _pmc_traffic("k_bsi"),
             "sum_count": list(sc), "min_max": [mn, mx]}
+
+
+def cpu_baselines(eng, a, b, in_bytes, budget_s):
+    """CPU legs on this host (rank 0, N=1): the oracle's C++ restatement of the reference
+    (the JVM reference cannot run here: no JDK), 1 thread with FastAggregation / RoaringBitmap
+    semantics and `threads` workers with ParallelAggregation's key-parallel semantics
+    (RB/ParallelAggregation.java:171-173), on bounded samples of the C2 and C3 workloads."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O  # CPU baseline leg only
+    info = _cpu_info()
+    threads = max(1, min(16, info["affinity"] or 1))
+    per_leg = budget_s / 6.0
+    xa = eng.batch_fetch(a).serialize()
+    xb = eng.batch_fetch(b).serialize()
+
+    def timed(fn):
+        t1 = fn(1)
+        reps = max(1, int(math.ceil(per_leg / max(t1, 1e-3))))
+        return reps, fn(reps)
+
+    legs = {}
+    reps, t = timed(lambda r: O.time_pairwise("and", xa, xb, r))
+    legs["c2_and_1t"] = {"GBps": round(in_bytes * reps / t / 1e9, 3), "threads": 1, "reps": reps, "s": round(t, 2),
+                         "what": "RoaringBitmap.and(x1, x2) on the full C2 pair"}
+    reps, t = timed(lambda r: O.time_and_parallel(xa, xb, threads, r))
+    legs["c2_and_mt"] = {"GBps": round(in_bytes * reps / t / 1e9, 3), "threads": threads, "reps": reps,
+                         "s": round(t, 2), "what": f"key-parallel RoaringBitmap.and over {threads} key ranges"}
+    # C3: all 10,000 bitmaps restricted to a key sample (uniform: 128 keys; clustered: 512 keys)
+    for kind, name, keys in ((1, "uniform", 128), (2, "clustered", 512)):
+        sb = eng.synth(kind, 0xC3000000, 10000, 0, keys)
+        st = eng.batch_stats(sb)
+        sbytes = st["payload_bytes"] + 4 * st["containers"]
+        bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
+        eng.release(sb)
+        reps, t = timed(lambda r: O.time_wide("or", bufs, r))
+        legs[f"c3_{name}_or_1t"] = {"GBps": round(sbytes * reps / t / 1e9, 3), "threads": 1, "reps": reps,
+                                    "s": round(t, 2),
+                                    "what": f"FastAggregation.or of 10,000 C3 {name} bitmaps, keys [0, {keys})"}
+        reps, t = timed(lambda r: O.time_wide_parallel("or", bufs, threads, r))
+        legs[f"c3_{name}_or_mt"] = {"GBps": round(sbytes * reps / t / 1e9, 3), "threads": threads, "reps": reps,
+                                    "s": round(t, 2),
+                                    "what": f"ParallelAggregation.or (key groups over {threads} workers), same sample"}
+        del bufs
+    best = legs["c2_and_mt"]
+    return {"value": best["GBps"], "unit": "GB/s", "cores": best["threads"], "kind": "port",
+            "sample": f"full C2 pair (same bytes as the GPU step), {best['reps']} x key-parallel RoaringBitmap.and on "
+                      f"{best['threads']} threads of the C++ restatement oracle/rbcpu -- C++ restatement, not the "
+                      f"reference JVM (no JDK on this image)",
+            "host": info, "legs": legs}
+
+
+def _relaunch(args):
+    """`bench.py --gpus N` without a launcher: run N ranks under torch.distributed.run as a
+    child process (nothing has touched the GPU yet) and exit with its status."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    sys.exit(subprocess.call(cmd, env=env))
 
 
 def main():
@@ -239,18 +342,23 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0, help="bounded CPU-baseline budget (all legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-n", type=int, default=10000, help="bitmaps of the C3 wide-OR workloads (0 = skip)")
     ap.add_argument("--c4-pairs", type=int, default=1000000, help="pairs of the C4 workload per GPU (0 = skip)")
     ap.add_argument("--c5-rows", type=int, default=1000000000, help="rows of the C5 BSI workload (0 = skip)")
+    ap.add_argument("--only", default="", help="profiling: run one workload alone (c2, c2card, c3u, c3c, c4, c5)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo to rehearse "
                                                        "several ranks on one GPU)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        _relaunch(args)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"bench: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
 
     import torch
     ndev = torch.cuda.device_count()
@@ -269,6 +377,11 @@ def main():
     from roaringbitmap_amd import Engine
 
     eng = Engine(local)
+    if args.only:
+        _only(eng, args, rank, world, dist, cdev)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     a = eng.synth(0, 0xC2A0 + 0x10000 * rank)
     b = eng.synth(0, 0xC2B0 + 0x10000 * rank)
     sa, sb = eng.batch_stats(a), eng.batch_stats(b)
@@ -315,7 +428,8 @@ def main():
         ser_ms += e0.elapsed_time(e1)
     ser_ms /= args.steps
 
-    # per-phase device time of the same op (separate pass: events between phases)
+    # per-phase device time of the same op (separate pass: HIP events between phases, on the
+    # engine's stream)
     eng.profile(args.steps)
     for _ in range(args.steps):
         eng.pairwise("and", a, b)
@@ -323,7 +437,7 @@ def main():
     eng.profile(0)
     ph_avg = [x / max(n_ops, 1) for x in ph]
 
-    c3 = {}
+    extra = {}
     # RoaringBitmap.andCardinality on the same pair: the same input bytes,
     # no result containers
     for _ in range(args.warmup):
@@ -340,28 +454,30 @@ def main():
     kc, phc = eng.profile_read()
     eng.profile(0)
     card_kern = phc[1] / max(kc, 1)
-    c3["c2_and_cardinality"] = {
+    extra["c2_and_cardinality"] = {
         "workload": "RoaringBitmap.andCardinality on the C2 pair (device-resident)",
         "ms_per_step": round(card_wall * 1e3, 4), "input_GBps": round(in_bytes / card_wall / 1e9, 1),
         "roofline": {"kernel": "k_pair_wave<AND, card>", "kernel_ms": round(card_kern, 4),
                      "achieved_GBps": round(in_bytes / (card_kern / 1e3) / 1e9, 1),
-                     "frac": round(in_bytes / (card_kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4)}}
+                     "frac": round(in_bytes / (card_kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "traffic": _pmc_traffic("k_pair_wave_card")}}
     if args.c3_n > 0:
         for kind, name in ((1, "c3_uniform_or"), (2, "c3_clustered_or")):
-            c3[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev)
+            extra[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev)
         # FastAggregation.and (N > 10: workShyAnd): per key the chain stops once the
         # intersection is empty, so it reads far less than the algorithmic input bytes
         for kind, name in ((1, "c3_uniform_and"), (2, "c3_clustered_and")):
-            c3[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev, op="and")
+            extra[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev,
+                                     op="and")
     if args.c4_pairs > 0:
-        c3["c4_batch_and_card"] = c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, max(3, args.steps // 4), 1,
-                                                    cdev)
+        extra["c4_batch_and_card"] = c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, max(3, args.steps // 4),
+                                                       1, cdev)
     if args.c5_rows > 0:
-        c3["c5_bsi_range_sum"] = c5_bsi(eng, args.c5_rows, rank, world, dist, max(3, args.steps // 4), 1, cdev)
+        extra["c5_bsi_range_sum"] = c5_bsi(eng, args.c5_rows, rank, world, dist, max(3, args.steps // 4), 1, cdev)
 
     if args.c3_n > 0 or args.c4_pairs > 0 or args.c5_rows > 0:
-        c3["run_optimize_c2"] = run_optimize_c2(eng, a, sa, max(3, args.steps // 4))
-        c3["decode_c2"] = decode_c2(eng, a, max(3, args.steps // 4))
+        extra["run_optimize_c2"] = run_optimize_c2(eng, a, sa, max(3, args.steps // 4))
+        extra["decode_c2"] = decode_c2(eng, a, max(3, args.steps // 4))
 
     t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device=cdev)
     if dist is not None:
@@ -375,16 +491,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import _oracle as O  # CPU baseline leg only
-        xa = eng.batch_fetch(a).serialize()
-        xb = eng.batch_fetch(b).serialize()
-        t1 = O.time_pairwise("and", xa, xb, 1)
-        reps = max(1, int(math.ceil(args.cpu_seconds / max(t1, 1e-3))))
-        tc = O.time_pairwise("and", xa, xb, reps)
-        cpu = {"value": round(in_bytes * reps / tc / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-               "sample": f"full C2 pair (same bytes as the GPU step), {reps} x RoaringBitmap.and on the C++ "
-                         f"restatement oracle/rbcpu (JVM reference not runnable: no JDK), {tc:.1f} s"}
+        cpu = cpu_baselines(eng, a, b, in_bytes, args.cpu_seconds)
 
     if rank == 0:
         step_s = wall_max / args.steps
@@ -422,12 +529,39 @@ def main():
                 "operand_mix": {k: [sa[k], sb[k]] for k in ["array", "bitmap", "run"]},
                 "result": rs,
                 "input_frac_of_peak": round(total_in / step_s / 1e9 / world / HBM_PEAK_GBS, 4),
-                **c3,
+                **extra,
             },
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def _only(eng, args, rank, world, dist, cdev):
+    """One workload alone (for per-workload rocprofv3 --pmc passes): prints a short JSON line."""
+    w = args.only
+    steps = args.steps
+    if w in ("c2", "c2card"):
+        a = eng.synth(0, 0xC2A0 + 0x10000 * rank)
+        b = eng.synth(0, 0xC2B0 + 0x10000 * rank)
+        for _ in range(args.warmup + steps):
+            if w == "c2":
+                eng.pairwise("and", a, b)
+            else:
+                eng.and_cardinality(a, b)
+        eng.sync()
+        res = {"only": w}
+    elif w in ("c3u", "c3c"):
+        res = {"only": w, **c3_wide_or(eng, 1 if w == "c3u" else 2, args.c3_n, rank, world, dist, steps,
+                                       args.warmup, cdev)}
+    elif w == "c4":
+        res = {"only": w, **c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, steps, args.warmup, cdev)}
+    elif w == "c5":
+        res = {"only": w, **c5_bsi(eng, args.c5_rows, rank, world, dist, steps, args.warmup, cdev)}
+    else:
+        raise SystemExit(f"unknown workload {w}")
+    if rank == 0:
+        print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -5,7 +5,8 @@ Writes
   profiles/<tag>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   profiles/<tag>/bench_kt.json      the bench line printed under the kernel trace
   profiles/<tag>/pmc_summary.json   per-kernel mean counters over the --pmc passes
-  profiles/pmc_traffic.json         HBM bytes per launch of the dominant kernel (read by bench.py)
+  profiles/pmc_traffic.json         HBM bytes per launch of each workload's dominant kernel, from
+                                    that workload's own passes (read by bench.py)
 
 HBM traffic follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE reports half the bytes of 16 B/lane streaming reads, so it is
@@ -60,35 +61,48 @@ def counters(path):
     return acc
 
 
+# workload (bench.py --only) -> (traffic key in pmc_traffic.json, dominant kernel)
+WORKLOADS = {"c2": ("k_pair_wave", "k_pair_wave<0, 0>"), "c2card": ("k_pair_wave_card", "k_pair_wave<0, 1>"),
+             "c3u": ("k_wide<OR>_uniform", "k_wide<0>"), "c3c": ("k_wide<OR>_clustered", "k_wide<0>"),
+             "c5": ("k_bsi", "k_bsi")}
+
+
 def main(tag):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles", tag)
     os.makedirs(dst, exist_ok=True)
-    kernel_stats(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+    kt = os.path.join(src, "kt", "run_kernel_stats.csv")
+    if os.path.exists(kt):
+        kernel_stats(kt, os.path.join(dst, "kernel_stats.csv"))
     if os.path.exists(os.path.join(src, "bench_kt.json")):
         shutil.copy(os.path.join(src, "bench_kt.json"), os.path.join(dst, "bench_kt.json"))
     summary = {}
     for sub in sorted(os.listdir(src)):
         p = os.path.join(src, sub, "run_counter_collection.csv")
-        if not sub.startswith("pmc") or not os.path.exists(p):
+        if not (sub.startswith("pmc_") or sub.startswith("sq_")) or not os.path.exists(p):
             continue
+        w = sub.split("_")[1]
         for k, cs in counters(p).items():
             for c, vals in cs.items():
-                summary.setdefault(k, {})[c] = {"mean": sum(vals) / len(vals), "n": len(vals)}
+                summary.setdefault(w, {}).setdefault(k, {})[c] = {"mean": sum(vals) / len(vals), "n": len(vals)}
     with open(os.path.join(dst, "pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1, sort_keys=True)
-    d = summary.get(DOMINANT, {})
-    if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-        rd = 2.0 * d["FETCH_SIZE"]["mean"] * 1024
-        wr = d["WRITE_SIZE"]["mean"] * 1024
-        traffic = {"k_pair_wave": {"kernel": DOMINANT, "hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
-                              "source": f"profiles/{tag}/pmc_summary.json",
-                              "correction": "FETCH_SIZE x2 (gfx950 streaming-read tally), KiB -> bytes"}}
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as f:
-            json.dump(traffic, f, indent=1)
-        print(json.dumps(traffic))
+    tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    traffic = json.load(open(tp)) if os.path.exists(tp) else {}
+    for w, (key, kern) in WORKLOADS.items():
+        d = summary.get(w, {}).get(kern, {})
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            rd = 2.0 * d["FETCH_SIZE"]["mean"] * 1024
+            wr = d["WRITE_SIZE"]["mean"] * 1024
+            traffic[key] = {"kernel": kern, "workload": w, "hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd),
+                            "write_bytes": int(wr), "launches": d["FETCH_SIZE"]["n"],
+                            "source": f"profiles/{tag}/pmc_summary.json ({w}, run alone)",
+                            "correction": "FETCH_SIZE x2 (gfx950 streaming-read tally), KiB -> bytes"}
+    with open(tp, "w") as f:
+        json.dump(traffic, f, indent=1)
+    print(json.dumps(traffic, indent=1))
     print("wrote", dst)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r02")

@@ -1,0 +1,88 @@
+"""Multi-process key sharding through the HIP engine on the one GPU of the box.
+
+Two ranks (gloo: RCCL refuses two ranks on one device) each generate and reduce their own
+key slice of a C3 batch with the engine, then `shard.assemble` builds the global portable
+bitmap on rank 0: rank 0 writes its slice in place, rank 1's descriptors, global offsets,
+run bytes and payload are received straight into their places.  The result must be
+byte-identical to the unsharded engine result (which tests/test_gpu_shard.py and
+tests/test_gpu_fullsize.py pin to the oracle).  bench.py's own multi-rank path is
+rehearsed the same way (`--gpus 2 --backend gloo`).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, outdir, kind, op):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from roaringbitmap_amd import Engine, shard
+        from roaringbitmap_amd.engine import synth_key_bytes
+        n, seed = 200, 0xC3000000
+        e = Engine(0)
+        ranges = shard.key_ranges(synth_key_bytes(kind, seed, n), world)
+        lo, hi = ranges[rank]
+        b = e.synth(kind, seed, n, lo, hi)
+        e.wide(op, b, lo, hi)
+        rs = e.result_stats()
+        lay = shard.exchange_layout(rs["containers"], rs["payload_bytes"], rs["has_run"], device="cpu")
+        out = shard.assemble(shard.engine_fill(e), lay, rank, fill_device=torch.device("cuda", 0),
+                             comm_device="cpu", sync=e.sync)
+        if rank == 0:
+            full = e.synth(kind, seed, n)
+            e.wide(op, full)
+            ref = e.fetch().serialize()
+            with open(os.path.join(outdir, "res.bin"), "wb") as f:
+                f.write(bytes(out.numpy().tobytes()))
+            with open(os.path.join(outdir, "ref.bin"), "wb") as f:
+                f.write(ref)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,op", [(1, "or"), (2, "or"), (2, "xor"), (1, "workshy_and")])
+def test_two_rank_engine_assembly(gpu, kind, op):
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(2, _free_port(), d, kind, op), nprocs=2, join=True)
+        res = open(os.path.join(d, "res.bin"), "rb").read()
+        ref = open(os.path.join(d, "ref.bin"), "rb").read()
+    assert res == ref
+
+
+def _bench(gpus):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo", "--steps", "2",
+           "--warmup", "1", "--c3-n", "64", "--c4-pairs", "2000", "--c5-rows", "2000000", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_bench_two_ranks_rehearsal(gpu):
+    one, two = _bench(1), _bench(2)
+    assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    for w in ("c3_uniform_or", "c3_clustered_or", "c3_uniform_and"):
+        assert two["extra"][w]["result_serialized_bytes"] == one["extra"][w]["result_serialized_bytes"], w
+        assert two["extra"][w]["output_bytes"] == one["extra"][w]["output_bytes"], w
+    assert two["extra"]["c5_bsi_range_sum"]["sum_count"] == one["extra"]["c5_bsi_range_sum"]["sum_count"]
