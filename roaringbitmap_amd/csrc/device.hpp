@@ -14,7 +14,12 @@
 namespace rbg {
 
 constexpr int NT = 256;
-constexpr int kSlotBytes = 8208;  // max serialized payload (8194) rounded to 16
+#ifndef RBG_SLOT_BYTES
+#define RBG_SLOT_BYTES 8320
+#endif
+// max serialized payload (8194) rounded up to 128 B, so every slot (and the B payload
+// at its start) is cache-line aligned: C2 AND -1.3 % against 8208 (16 B rounding)
+constexpr int kSlotBytes = RBG_SLOT_BYTES;
 
 enum DKind : uint8_t { DK_A = 0, DK_B = 1, DK_R = 2 };
 

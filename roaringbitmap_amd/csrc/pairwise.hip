@@ -344,7 +344,7 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
 // R AND R in the run domain (RB/RunContainer.java and(RunContainer)): the
 // intersection of two sorted disjoint run lists is the list of overlaps of their
 // runs, already canonical.  Both run lists go to the wave's LDS as
-// (start | end << 16) -- kWaveLds u32 words hold na + nb runs -- and the lanes
+// (start | end << 16) -- kWaveLds u32 words hold na + nb runs and two sentinels -- and the lanes
 // split the merge path evenly (rr_merge).  Pass 1 counts runs and cardinality; the type is EFF
 // (App. A.1); an R result is written by pass 2 straight into the task's scratch
 // slot.  Returns false (nothing written) when the result is not a run container or
@@ -353,9 +353,19 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
 // whichever current run ends first (A on ties); every overlapping pair of runs is
 // current at exactly one step, and overlaps come out in ascending order.  Lane l
 // takes steps [d0, d1) of na + nb, found by a binary search on the diagonal.
+// A's run list lives at lds[0, na) followed by a sentinel at lds[na], B's at
+// lds[na + 1, na + 1 + nb) followed by a sentinel.  The sentinel is the empty run
+// (start 0xFFFF, end 0xFFFE): it overlaps nothing, so a lane may keep stepping
+// after either side is exhausted (no further overlap exists then; the index is
+// clamped at the sentinel) and every lane runs its d1 - d0 steps without branches:
+// each step selects which side advances and issues one LDS read for that side's
+// next-but-one run (R AND R card -8 % against the branching two-pointer loop).
+constexpr uint32_t kRunSentinel = 0xFFFEFFFFu;
 template <bool EMIT>
-__device__ __forceinline__ void rr_merge(const uint32_t* al, int na, const uint32_t* bl, int nb, int d0, int d1,
-                                         int& cnt, int& card, uint32_t* out) {
+__device__ __forceinline__ void rr_merge(const uint32_t* lds, int na, int nb, int d0, int d1, int& cnt, int& card,
+                                         uint32_t* out) {
+  const uint32_t* al = lds;
+  const uint32_t* bl = lds + na + 1;
   int lo = max(0, d0 - nb), hi = min(d0, na);
   while (lo < hi) {
     const int m = (lo + hi) >> 1;
@@ -365,25 +375,23 @@ __device__ __forceinline__ void rr_merge(const uint32_t* al, int na, const uint3
   int i = lo, j = d0 - lo;
   // current and next run of each side in registers: the LDS read of a side's
   // next-but-one run is off the step's dependency chain
-  uint32_t a = i < na ? al[i] : 0, b = j < nb ? bl[j] : 0;
-  uint32_t an = i + 1 < na ? al[i + 1] : 0, bn = j + 1 < nb ? bl[j + 1] : 0;
-  for (int d = d0; d < d1 && i < na && j < nb; d++) {
-    const int as = (int)(a & 0xFFFF), ae = (int)(a >> 16), bs = (int)(b & 0xFFFF), be = (int)(b >> 16);
-    const int s0 = max(as, bs), e0 = min(ae, be);
-    if (s0 <= e0) {
-      if (EMIT) out[cnt] = (uint32_t)s0 | ((uint32_t)(e0 - s0) << 16);
-      cnt++;
-      card += e0 - s0 + 1;
-    }
-    if (ae <= be) {
-      i++;
-      a = an;
-      an = i + 1 < na ? al[i + 1] : 0;
-    } else {
-      j++;
-      b = bn;
-      bn = j + 1 < nb ? bl[j + 1] : 0;
-    }
+  uint32_t a = al[i], b = bl[j];
+  uint32_t an = al[min(i + 1, na)], bn = bl[min(j + 1, nb)];
+  for (int d = d0; d < d1; d++) {
+    const uint32_t as = a & 0xFFFF, ae = a >> 16, bs = b & 0xFFFF, be = b >> 16;
+    const uint32_t s0 = max(as, bs), e0 = min(ae, be);
+    const bool ov = s0 <= e0;
+    if (EMIT && ov) out[cnt] = s0 | ((e0 - s0) << 16);
+    cnt += ov ? 1 : 0;
+    card += ov ? (int)(e0 - s0 + 1) : 0;
+    const bool adv = ae <= be;  // A's run ends first (A on ties)
+    i = adv ? min(i + 1, na) : i;
+    j = adv ? j : min(j + 1, nb);
+    const uint32_t nx = adv ? al[min(i + 1, na)] : bl[min(j + 1, nb)];
+    b = adv ? b : bn;
+    bn = adv ? bn : nx;
+    a = adv ? an : a;
+    an = adv ? nx : an;
   }
 }
 
@@ -428,15 +436,19 @@ template <int MODE>
 __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
                                             const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
   const int na = tk.nruns_a, nb = tk.nruns_b;
-  if (na + nb > kWaveLds) return false;
+  if (na + nb + 2 > kWaveLds) return false;
   const int l = lane_id();
   wsync();
-  runs_to_lds2(pa + tk.slot_a, na, lds, pb + tk.slot_b, nb, lds + na);
+  runs_to_lds2(pa + tk.slot_a, na, lds, pb + tk.slot_b, nb, lds + na + 1);
+  if (l == 0) {
+    lds[na] = kRunSentinel;
+    lds[na + 1 + nb] = kRunSentinel;
+  }
   PRIO_LO();
   wsync();
   const int d0 = (l * (na + nb)) >> 6, d1 = ((l + 1) * (na + nb)) >> 6;
   int cnt = 0, card = 0;
-  rr_merge<false>(lds, na, lds + na, nb, d0, d1, cnt, card, nullptr);
+  rr_merge<false>(lds, na, nb, d0, d1, cnt, card, nullptr);
   const int c = (int)uni((uint32_t)wave_sum_i(card));
   if (MODE == 1) {
     if (l == 0) task_card[t] = (uint32_t)c;
@@ -452,7 +464,7 @@ __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const u
   if (eff(c, nr) != DK_R) return false;
   uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
   int cnt2 = 0, card2 = 0;
-  rr_merge<true>(lds, na, lds + na, nb, d0, d1, cnt2, card2, reinterpret_cast<uint32_t*>(slot + 4) + off);
+  rr_merge<true>(lds, na, nb, d0, d1, cnt2, card2, reinterpret_cast<uint32_t*>(slot + 4) + off);
   if (l == 0) *reinterpret_cast<uint16_t*>(slot + 2) = (uint16_t)nr;
   w_place(t, true, slot + 2, false, lds, 2u + 4u * (uint32_t)nr, (uint32_t)c, tk.key, DK_R, oc);
   return true;

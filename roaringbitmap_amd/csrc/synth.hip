@@ -258,7 +258,7 @@ void launch_sum_cards(hipStream_t s, const CDesc* desc, uint64_t n, unsigned lon
 }
 
 // ===========================================================================
-// synthetic C2 operand: one workgroup per key, written straight into 8208 B slots
+// synthetic C2 operand: one workgroup per key, written straight into kSlotBytes slots
 // ===========================================================================
 
 __global__ __launch_bounds__(256) void k_synth_c2(uint64_t seed, int force, CDesc* __restrict__ desc,
