@@ -263,13 +263,13 @@ def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
         t[0] = tm[0]
     step_s = float(t[0]) / steps
     eng.release(b)
-    # compare streams ebM + every slice once, sum re-reads the slices: about 2x the index bytes
+    # compare + sum read ebM and every slice once (k_bsi_reg holds a key's slices in registers)
     return {"workload": f"C5: RoaringBitmapSliceIndex.compare(RANGE, 2^29, 2^30) + sum over {rows} rows x 31 slices, "
                         f"key-range sharded over {world} GPU(s)",
             "rows_per_s": round(rows / step_s, 1), "ms_per_step": round(step_s * 1e3, 4),
             "index_bytes": int(t[1]), "index_GBps": round(float(t[1]) / step_s / 1e9, 1),
             "frac_of_peak_1pass": round(float(t[1]) / step_s / 1e9 / HBM_PEAK_GBS, 4),
-            "traffic_k_bsi": _pmc_traffic("k_bsi"),
+            "traffic_k_bsi_reg": _pmc_traffic("k_bsi_reg"),
             "sum_count": list(sc), "min_max": [mn, mx]}
 
 

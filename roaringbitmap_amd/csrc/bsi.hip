@@ -1,17 +1,22 @@
 // Bit-sliced index query on the MI355X: RoaringBitmapSliceIndex.compare + sum
 // (bsi/src/main/java/org/roaringbitmap/bsi/RoaringBitmapSliceIndex.java, BSI/
-// below) as ONE fused pass per key.
+// below).
 //
 // The reference runs the O'Neil circuit (BSI/:432-468) as a chain of whole-bitmap
-// pairwise ops, about 4 per slice. Each op is independent per high-16 key, so one
-// workgroup takes one key. It keeps every bitmap of the circuit (EQ, GT, LT, for
-// one or two predicates) in registers (4 words per thread) and streams each slice
-// container of the key once. The result container types must be the reference's,
-// so every step replays the pairwise type rule of the op it stands for (App. A,
+// pairwise ops, about 4 per slice. Each op is independent per high-16 key, so a
+// workgroup takes one key. The result container types must be the reference's,
+// so every step follows the pairwise type rule of the op it stands for (App. A,
 // device.hpp): present / absent (an unmatched container is cloned, an empty result
-// dropped), kind, cardinality, and the run count where EFF decides. sum
-// (BSI/:581-592) is fused: after the result container of the key is known, each
-// slice is re-read and |slice & found| is added to a per-slice total.
+// dropped), kind, cardinality, and the run count where EFF decides.
+//
+// Two forms:
+//  * k_bsi_reg + k_bsi_types (compare ops, <= 32 slices): the slices of a key are
+//    held in registers and read once; bits, counts and types are separate passes
+//    (see "Register-resident query" below).  sum (BSI/:581-592) comes from the
+//    same registers.
+//  * bsi_task_streamed (k_bsi: BSI_ALL / sum alone, and k_bsi_defer: keys whose
+//    type replay needs a run count): slices streamed step by step, each step's
+//    cardinality reduced over the workgroup; sum re-reads the slices.
 //
 // Batch inputs (key-major): input 0 = ebM, inputs 1..nb = bA[0..nb-1],
 // input nb+1 = foundSet (optional).
@@ -134,6 +139,90 @@ __global__ __launch_bounds__(256) void k_plan_bsi(const uint32_t* __restrict__ k
   plan_count(f, wg_count);
 }
 
+// One key of the query, streamed: every slice container is loaded when its
+// circuit step runs and every pairwise step reduces its cardinality over the
+// workgroup right away (two barriers per step); sum re-reads the slices against
+// the result.  Used for BSI_ALL / BSI_SUM_ONLY and, inside k_bsi_reg, for keys
+// whose type replay needs a run count.
+__device__ __forceinline__ void bsi_task_streamed(uint32_t t, const Task tk, const WideArgs& A, const BsiArgs& P,
+                                               const OutCtx& oc, unsigned long long* __restrict__ sums, uint32_t* acc,
+                                               uint32_t* tmp, int* q, int* sh, int* pos) {
+  const int nb = P.nbits;
+  const uint32_t s = uni((uint32_t)tk.a), n = uni((uint32_t)tk.b);
+  __syncthreads();
+  for (int j = threadIdx.x; j < kBsiMaxInputs; j += NT) pos[j] = -1;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < n; j += NT) pos[A.bm[s + j]] = (int)(s + j);
+  __syncthreads();
+  VB res;
+  if (P.op == BSI_SUM_ONLY) {
+    vb_load(pos[nb + 1], A, tmp, q, res);
+  } else if (P.op == BSI_ALL) {
+    VB ebm;
+    vb_load(pos[0], A, tmp, q, ebm);
+    if (P.has_found) {
+      VB f;
+      vb_load(pos[nb + 1], A, tmp, q, f);
+      vb_op<OPR_AND>(ebm, f, res, acc, sh);
+    } else {
+      res = ebm;  // ebM.clone()
+    }
+  } else {
+    VB ebm, eq0, gt0, lt0, eq1, gt1, lt1, sl, tv;
+    vb_load(pos[0], A, tmp, q, ebm);
+    eq0 = ebm;
+    eq1 = ebm;
+    vb_absent(gt0);
+    vb_absent(lt0);
+    vb_absent(gt1);
+    vb_absent(lt1);
+    const bool two = P.op == BSI_RANGE;
+    for (int i = nb - 1; i >= 0; i--) {
+      vb_load(pos[1 + i], A, tmp, q, sl);
+      oneil_step((P.pred0 >> i) & 1, sl, gt0, lt0, eq0, tv, acc, sh);
+      if (two) oneil_step((P.pred1 >> i) & 1, sl, gt1, lt1, eq1, tv, acc, sh);
+    }
+    VB fixed;
+    if (P.has_found) vb_load(pos[nb + 1], A, tmp, q, fixed);
+    else fixed = ebm;
+    if (two) {  // RANGE = and(GE(start), LE(end)), BSI/:503-507
+      VB left, right;
+      oneil_finish(BSI_GE, fixed, gt0, lt0, eq0, left, acc, sh);
+      oneil_finish(BSI_LE, fixed, gt1, lt1, eq1, right, acc, sh);
+      vb_op<OPR_AND>(left, right, res, acc, sh);
+    } else {
+      oneil_finish(P.op, fixed, gt0, lt0, eq0, res, acc, sh);
+    }
+  }
+  if (sums) {
+    // sum: |bA[x] & found| per slice (Java int per slice, wrapped on the host), count
+    if (res.present) {
+      for (int x = 0; x < nb; x++) {
+        const int p = pos[1 + x];
+        if (p < 0) continue;
+        uint64_t r[4];
+        materialize(A.desc[p], A.payload, tmp, q, r);
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < 4; i++) c += popc64(r[i] & res.r[i]);
+        int u = 0;
+        block_sum2(c, u, sh);
+        if (threadIdx.x == 0 && c) atomicAdd(&sums[x], (unsigned long long)c);
+      }
+      if (threadIdx.x == 0) atomicAdd(&sums[kBsiMaxInputs], (unsigned long long)res.card);
+    }
+  }
+  if (P.op == BSI_SUM_ONLY) return;
+  if (!res.present) {
+    wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, nullptr);
+  } else if (res.src >= 0) {
+    wg_passthrough(t, A.desc[res.src], A.payload, oc, nullptr);
+  } else {
+    const uint32_t len = stage_container(res.kind, res.r, res.card, acc, tmp, sh);
+    wg_place(t, true, nullptr, true, tmp, len, (uint32_t)res.card, tk.key, res.kind, oc, nullptr);
+  }
+}
+
 // mode: BSI_* op (compare, + sum of the result when `sums` is set), or BSI_SUM_ONLY
 __global__ __launch_bounds__(256) void k_bsi(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                              WideArgs A, BsiArgs P, OutCtx oc,
@@ -144,82 +233,539 @@ __global__ __launch_bounds__(256) void k_bsi(const Task* __restrict__ tasks, con
   __shared__ int sh[8];
   __shared__ int pos[kBsiMaxInputs];
   const uint32_t nt = *n_tasks;
-  const int nb = P.nbits;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    const Task tk = tasks[t];
-    const uint32_t s = uni((uint32_t)tk.a), n = uni((uint32_t)tk.b);
-    __syncthreads();
-    for (int j = threadIdx.x; j < kBsiMaxInputs; j += NT) pos[j] = -1;
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < n; j += NT) pos[A.bm[s + j]] = (int)(s + j);
-    __syncthreads();
-    VB res;
-    if (P.op == BSI_SUM_ONLY) {
-      vb_load(pos[nb + 1], A, tmp, q, res);
-    } else if (P.op == BSI_ALL) {
-      VB ebm;
-      vb_load(pos[0], A, tmp, q, ebm);
-      if (P.has_found) {
-        VB f;
-        vb_load(pos[nb + 1], A, tmp, q, f);
-        vb_op<OPR_AND>(ebm, f, res, acc, sh);
-      } else {
-        res = ebm;  // ebM.clone()
-      }
-    } else {
-      VB ebm, eq0, gt0, lt0, eq1, gt1, lt1, sl, tv;
-      vb_load(pos[0], A, tmp, q, ebm);
-      eq0 = ebm;
-      eq1 = ebm;
-      vb_absent(gt0);
-      vb_absent(lt0);
-      vb_absent(gt1);
-      vb_absent(lt1);
-      const bool two = P.op == BSI_RANGE;
-      for (int i = nb - 1; i >= 0; i--) {
-        vb_load(pos[1 + i], A, tmp, q, sl);
-        oneil_step((P.pred0 >> i) & 1, sl, gt0, lt0, eq0, tv, acc, sh);
-        if (two) oneil_step((P.pred1 >> i) & 1, sl, gt1, lt1, eq1, tv, acc, sh);
-      }
-      VB fixed;
-      if (P.has_found) vb_load(pos[nb + 1], A, tmp, q, fixed);
-      else fixed = ebm;
-      if (two) {  // RANGE = and(GE(start), LE(end)), BSI/:503-507
-        VB left, right;
-        oneil_finish(BSI_GE, fixed, gt0, lt0, eq0, left, acc, sh);
-        oneil_finish(BSI_LE, fixed, gt1, lt1, eq1, right, acc, sh);
-        vb_op<OPR_AND>(left, right, res, acc, sh);
-      } else {
-        oneil_finish(P.op, fixed, gt0, lt0, eq0, res, acc, sh);
-      }
-    }
-    if (sums) {
-      // sum: |bA[x] & found| per slice (Java int per slice, wrapped on the host), count
-      if (res.present) {
-        for (int x = 0; x < nb; x++) {
-          const int p = pos[1 + x];
-          if (p < 0) continue;
-          uint64_t r[4];
-          materialize(A.desc[p], A.payload, tmp, q, r);
-          int c = 0;
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) bsi_task_streamed(t, tasks[t], A, P, oc, sums, acc, tmp, q, sh, pos);
+}
+
+// ===========================================================================
+// Register-resident query (compare ops, nbits <= 32): k_bsi_reg + k_bsi_defer
+// ===========================================================================
+// The streamed form above is bound by its ~6 workgroup reductions per slice (two
+// barriers each, a dependent chain of ~190 per key) and reads every slice twice.
+// k_bsi_reg runs one key per 1,024-thread workgroup, thread t owning container
+// word t, and holds ALL slices of the key in registers (one u64 per slice per
+// thread):
+//   1. every slice of the key is requested at once;
+//   2. bits: the whole circuit on registers.  Per step only t = EQ & bA[i] (or
+//      EQ & ~bA[i]) is counted -- t and the new EQ partition the old EQ, and t is
+//      disjoint from GT / LT, so |EQ'| = |EQ| - |t| and |GT'| = |GT| + |t|.  Each
+//      thread stores its share (<= 64, a byte) in an LDS row per count; no
+//      barrier inside the circuit;
+//   4. sum shares |bA[x] & result| from the same registers (no second read);
+//      then the next key's slices start loading;
+//   3. the rows are summed, and one wave replays the reference's type rule of
+//      every step from those cardinalities (wave-uniform, no bits needed).  A
+//      step whose type needs a run count (EFF: run containers in AND / OR / ...)
+//      cannot be replayed so: such keys go to k_bsi_defer, which redoes them
+//      with bsi_task_streamed.
+// Results that are absent, clones or bitmap containers are written here (a
+// bitmap is one coalesced 8 B store per thread); array / run results are left
+// as raw bitmaps for k_bsi_defer to stage with the 256-thread helpers.
+constexpr int kBsiRegSlices = 32;
+constexpr int kNT1 = 1024;  // threads of k_bsi_reg
+constexpr int kBsiRows = 1 + 2 * kBsiRegSlices + 4 + kBsiRegSlices;  // |ebM|, counted steps, finish, sum shares
+constexpr int kRowB = kNT1 + 16;  // row stride in bytes: row sums of a wave spread over the banks
+
+// Wave-uniform type state of a circuit bitmap (the bits live elsewhere).  card 0
+// means absent: a present container is never empty (inputs hold >= 1 value,
+// empty results are dropped), so presence needs no field of its own.
+struct TB {
+  int kind, card;
+  int src;  // desc index of the input container it is a clone of, else -1
+  int pad;
+};
+__device__ __forceinline__ TB tb_absent() { return TB{DK_A, 0, -1, 0}; }
+
+// vb_op's type rule with the step's cardinality c already known, without
+// branches (scalar selects); `slow` is set when the rule needs the result's run
+// count.  AND: absent unless both present and c > 0; OR: a clone of the present
+// side when the other is absent; ANDNOT: a clone of x when y is absent.
+template <int OP>
+__device__ __forceinline__ TB tb_op(const TB& x, const TB& y, int c, int& slow) {
+  const bool xp = x.card > 0, yp = y.card > 0;
+  int kind = by_card(c);
+  if (OP == OPR_OR && (x.kind == DK_B || y.kind == DK_B)) kind = c == 65536 ? DK_R : DK_B;
+  const bool need = pairwise_needs_runs(OP, x.kind, x.card, y.kind, y.card);
+  const bool both = xp && yp && c > 0;
+  TB r;
+  if (OP == OPR_OR) {
+    r.kind = !xp ? y.kind : !yp ? x.kind : kind;
+    r.card = !xp ? y.card : !yp ? x.card : c;
+    r.src = !xp ? y.src : !yp ? x.src : -1;
+  } else if (OP == OPR_ANDNOT) {
+    r.kind = !yp ? x.kind : both ? kind : DK_A;
+    r.card = !yp ? x.card : both ? c : 0;
+    r.src = !yp ? x.src : -1;
+  } else {
+    r.kind = both ? kind : DK_A;
+    r.card = both ? c : 0;
+    r.src = -1;
+  }
+  r.pad = 0;
+  slow |= (both && need) ? 1 : 0;
+  return r;
+}
+
+// this thread's share of count k (<= 64)
+__device__ __forceinline__ void rec1(uint64_t z, int k, uint8_t* rows) {
+  rows[k * kRowB + threadIdx.x] = (uint8_t)popc64(z);
+}
+// row sums of rows [0, nk) -> tot[], one wave per row (a 16 B vector per lane,
+// then a DPP reduction); ends with a barrier
+__device__ __forceinline__ void sum_rows1(const uint8_t* rows, int nk, int* tot) {
+  lds_barrier();
+  const int lane = threadIdx.x & 63;
+  for (int r = threadIdx.x >> 6; r < nk; r += kNT1 / 64) {
+    const uint4 x = reinterpret_cast<const uint4*>(rows + r * kRowB)[lane];
+    // 16 bytes: sum the byte lanes pairwise into 16-bit fields (each <= 8 * 64)
+    const uint32_t a = (x.x & 0x00FF00FFu) + ((x.x >> 8) & 0x00FF00FFu) + (x.y & 0x00FF00FFu) +
+                       ((x.y >> 8) & 0x00FF00FFu) + (x.z & 0x00FF00FFu) + ((x.z >> 8) & 0x00FF00FFu) +
+                       (x.w & 0x00FF00FFu) + ((x.w >> 8) & 0x00FF00FFu);
+    const int c = wave_sum((int)((a & 0xFFFF) + (a >> 16)));
+    if (lane == 0) tot[r] = c;
+  }
+  lds_barrier();
+}
+// count k from the per-lane copies of the totals (tv[j] = tot[64 j + lane]), wave-uniform
+__device__ __forceinline__ int step_card(const int* tv, int k) {
+  const int j = k >> 6, l = k & 63;
+  const int v = j == 0 ? tv[0] : tv[1];
+  return __builtin_amdgcn_readlane(v, l);
+}
+
+// Type replay of a step / finish, in the order of the bits.  c* are the exact
+// cardinalities of the bits (0 for an absent bitmap).
+struct CircuitT {
+  TB gt, lt, eq;
+  int cgt, clt, ceq;
+};
+__device__ __forceinline__ void types_step(int bit, const TB& s, CircuitT& z, int& k, const int* tv, int& slow) {
+  const int ct = step_card(tv, k++);
+  if (bit) {
+    const TB t = tb_op<OPR_ANDNOT>(z.eq, s, ct, slow);
+    z.lt = tb_op<OPR_OR>(z.lt, t, z.clt + ct, slow);
+    z.eq = tb_op<OPR_AND>(z.eq, s, z.ceq - ct, slow);
+    z.clt += ct;
+  } else {
+    const TB t = tb_op<OPR_AND>(z.eq, s, ct, slow);
+    z.gt = tb_op<OPR_OR>(z.gt, t, z.cgt + ct, slow);
+    z.eq = tb_op<OPR_ANDNOT>(z.eq, s, z.ceq - ct, slow);
+    z.cgt += ct;
+  }
+  z.ceq -= ct;
+}
+// BSI/:453-467 on types: counted are fixed & EQ and the NEQ / GT / LT results;
+// LE / GE are disjoint unions
+__device__ __forceinline__ TB types_finish(int op, const TB& fixed, CircuitT& z, int& k, const int* tv, int& slow) {
+  const int ce = step_card(tv, k++);
+  z.eq = tb_op<OPR_AND>(fixed, z.eq, ce, slow);
+  z.ceq = ce;
+  switch (op) {
+    case BSI_EQ: return z.eq;
+    case BSI_NEQ: return tb_op<OPR_ANDNOT>(fixed, z.eq, step_card(tv, k++), slow);
+    case BSI_GT: return tb_op<OPR_AND>(z.gt, fixed, step_card(tv, k++), slow);
+    case BSI_LT: return tb_op<OPR_AND>(z.lt, fixed, step_card(tv, k++), slow);
+    case BSI_LE: return tb_op<OPR_OR>(z.lt, z.eq, z.clt + ce, slow);
+    default: return tb_op<OPR_OR>(z.gt, z.eq, z.cgt + ce, slow);  // GE
+  }
+}
+// the same on bits (thread's word), recording the counted steps
+__device__ __forceinline__ uint64_t bits_finish1(int op, uint64_t fixed, uint64_t gt, uint64_t lt, uint64_t& eq, int& k,
+                                                 uint8_t* rows) {
+  eq &= fixed;
+  rec1(eq, k++, rows);
+  uint64_t out;
+  switch (op) {
+    case BSI_EQ: return eq;
+    case BSI_NEQ: out = fixed & ~eq; break;
+    case BSI_GT: out = gt & fixed; break;
+    case BSI_LT: out = lt & fixed; break;
+    case BSI_LE: return lt | eq;
+    default: return gt | eq;  // GE
+  }
+  rec1(out, k++, rows);
+  return out;
+}
+
+// wave-uniform (SGPR) copy of a type state
+__device__ __forceinline__ TB tb_uni(const TB& x) {
+  return TB{(int)uni((uint32_t)x.kind), (int)uni((uint32_t)x.card), (int)uni((uint32_t)x.src), 0};
+}
+
+// Thread t's word of a container; non-bitmap ones through the 8 KiB LDS scratch `lds`:
+// arrays scattered; runs as toggles (run start, end + 1) whose prefix XOR is
+// taken inside each word and carried across words by a workgroup parity scan
+// (wpar: 16 ints).  All threads; contains barriers.
+__device__ __forceinline__ uint64_t mat_word1(const CDesc& d, const uint8_t* payload, uint32_t* lds, int* wpar) {
+  const int t = threadIdx.x;
+  const uint8_t* slot = payload + d.slot;
+  if (d.kind == DK_B) return reinterpret_cast<const uint64_t*>(slot)[t];
+  lds_barrier();
+  reinterpret_cast<uint64_t*>(lds)[t] = 0;
+  lds_barrier();
+  if (d.kind == DK_A) {
+    const int card = (int)d.card;
+    const int nvec = (card + 7) >> 3;
+    const uint4* v4 = reinterpret_cast<const uint4*>(slot);
+    for (int i = t; i < nvec; i += kNT1) {
+      const uint4 v = v4[i];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-          for (int i = 0; i < 4; i++) c += popc64(r[i] & res.r[i]);
-          int u = 0;
-          block_sum2(c, u, sh);
-          if (threadIdx.x == 0 && c) atomicAdd(&sums[x], (unsigned long long)c);
+      for (int j = 0; j < 8; j++) {
+        if (8 * i + j < card) {
+          const uint32_t x = (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFF;
+          atomicOr(&lds[x >> 5], 1u << (x & 31));
         }
-        if (threadIdx.x == 0) atomicAdd(&sums[kBsiMaxInputs], (unsigned long long)res.card);
       }
     }
-    if (P.op == BSI_SUM_ONLY) continue;
-    if (!res.present) {
-      wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, nullptr);
-    } else if (res.src >= 0) {
-      wg_passthrough(t, A.desc[res.src], A.payload, oc, nullptr);
-    } else {
-      const uint32_t len = stage_container(res.kind, res.r, res.card, acc, tmp, sh);
-      wg_place(t, true, nullptr, true, tmp, len, (uint32_t)res.card, tk.key, res.kind, oc, nullptr);
+    lds_barrier();
+    return reinterpret_cast<const uint64_t*>(lds)[t];
+  }
+  const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
+  const uint32_t* pairs = reinterpret_cast<const uint32_t*>(slot + 4);
+  for (int i = t; i < nr; i += kNT1) {
+    const uint32_t p = pairs[i];
+    const uint32_t st = p & 0xFFFF, e1 = st + (p >> 16) + 1;
+    atomicXor(&lds[st >> 5], 1u << (st & 31));
+    if (e1 < 65536) atomicXor(&lds[e1 >> 5], 1u << (e1 & 31));
+  }
+  lds_barrier();
+  uint64_t w = reinterpret_cast<const uint64_t*>(lds)[t];
+  const uint32_t par = (uint32_t)popc64(w) & 1u;
+  w = prefix_xor64(w);
+  const uint64_t m = __ballot(par);
+  const int lane = t & 63, wv = t >> 6;
+  uint32_t c = (uint32_t)__popcll(m & ((1ull << lane) - 1)) & 1u;
+  if (lane == 0) wpar[wv] = __popcll(m) & 1;
+  lds_barrier();
+  for (int j = 0; j < wv; j++) c ^= (uint32_t)wpar[j];
+  lds_barrier();
+  return c ? ~w : w;
+}
+
+// Diagnostic build only (-DRBG_BSI_STAMPS=1): per-phase shader-clock totals of
+// k_bsi_reg (thread 0 of every workgroup), read back with rbg_debug_stamps when
+// RBG_DEBUG_BSI is set.
+#if RBG_BSI_STAMPS
+__device__ unsigned long long g_bsi_stamp[20];
+#define BST_DECL                                   \
+  uint64_t bst_prev = __builtin_amdgcn_s_memtime(); \
+  uint64_t bst[10] = {};
+#define BST(ph)                                            \
+  do {                                                     \
+    const uint64_t bst_now = __builtin_amdgcn_s_memtime(); \
+    bst[ph] += bst_now - bst_prev;                         \
+    bst_prev = bst_now;                                    \
+  } while (0)
+#define BST_FLUSH()                                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0)                                                                    \
+      for (int i_ = 0; i_ < 10; i_++) atomicAdd(&g_bsi_stamp[i_], (unsigned long long)bst[i_]); \
+  } while (0)
+void debug_bsi_stamps(uint64_t* out20, bool reset) {
+  (void)hipDeviceSynchronize();
+  (void)hipMemcpyFromSymbol(out20, HIP_SYMBOL(g_bsi_stamp), 20 * 8, 0, hipMemcpyDeviceToHost);
+  if (reset) {
+    unsigned long long z[20] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bsi_stamp), z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+}
+#else
+#define BST_DECL
+#define BST(ph) \
+  do {          \
+  } while (0)
+#define BST_FLUSH() \
+  do {              \
+  } while (0)
+void debug_bsi_stamps(uint64_t* out20, bool) {
+  for (int i = 0; i < 20; i++) out20[i] = 0;
+}
+#endif
+
+// Per-key LDS state of k_bsi_reg (double-buffered: the next key's is set up while
+// the current key finishes)
+struct BsiKeyBuf {
+  int pos[kBsiMaxInputs];  // desc index of each input's container of the key, or -1
+  TB stype[kBsiRegSlices];
+  uint64_t sslot[kBsiRegSlices];
+  uint32_t mask;  // slices that are bitmap containers
+};
+
+// positions of the key's inputs and its slice descriptors (wave 0, one lane per
+// slice: one memory round trip); returns the bitmap-slice mask.  Contains barriers.
+__device__ __forceinline__ uint32_t bsi_key_setup(const Task& tk, const WideArgs& A, int nb, BsiKeyBuf& kb) {
+  const uint32_t s = uni((uint32_t)tk.a), n = uni((uint32_t)tk.b);
+  if ((int)threadIdx.x < kBsiMaxInputs) kb.pos[threadIdx.x] = -1;
+  lds_barrier();
+  for (uint32_t j = threadIdx.x; j < n; j += kNT1) kb.pos[A.bm[s + j]] = (int)(s + j);
+  lds_barrier();
+  if (threadIdx.x < 64) {
+    const int i = threadIdx.x;
+    const int p = i < nb ? kb.pos[1 + i] : -1;
+    CDesc d{};
+    if (p >= 0) d = A.desc[p];
+    if (i < kBsiRegSlices) {
+      kb.stype[i] = p >= 0 ? TB{d.kind, (int)d.card, p, 0} : tb_absent();
+      kb.sslot[i] = d.slot;
     }
+    const uint64_t m = __ballot(p >= 0 && d.kind == DK_B);
+    if (i == 0) kb.mask = (uint32_t)m;
+  }
+  lds_barrier();
+  return uni(kb.mask);
+}
+
+// bitmap slices straight to registers (thread t: word t); all loads of the key in flight at once
+__device__ __forceinline__ void bsi_issue_loads(const WideArgs& A, const BsiKeyBuf& kb, uint32_t mask,
+                                                uint64_t sl[kBsiRegSlices]) {
+#pragma unroll
+  for (int i = 0; i < kBsiRegSlices; i++)
+    sl[i] = ((mask >> i) & 1) ? reinterpret_cast<const uint64_t*>(A.payload + kb.sslot[i])[threadIdx.x] : 0;
+}
+
+// task record of a result written by k_bsi_reg / k_bsi_defer (wg_place's record)
+__device__ __forceinline__ void bsi_rec(uint32_t t, const OutCtx& oc, bool keep, const uint8_t* src, uint32_t len,
+                                        uint32_t card, uint32_t key, int kind) {
+  ORec r;
+  r.off = 0;
+  r.src = reinterpret_cast<uint64_t>(src);
+  r.idx = 0;
+  r.card = card;
+  r.ser_len = len;
+  r.key = (uint16_t)key;
+  r.kind = (uint8_t)kind;
+  r.keep = keep ? 1 : 0;
+  oc.recs[t] = r;
+}
+
+// compare ops (BSI_EQ .. BSI_RANGE) with nbits <= kBsiRegSlices: one 1,024-thread
+// workgroup per key computes the bits and the counts; k_bsi_types (a wave per key)
+// replays the types and writes the records.  cnts: kBsiCnt ints per task; kin:
+// kBsiKin input types per task (slices, ebM, the fixed found set).
+constexpr int kBsiCnt = 128;
+constexpr int kBsiKin = kBsiRegSlices + 2;
+static_assert(kBsiRows <= kBsiCnt, "count rows");
+__global__ __launch_bounds__(1024, 1) void k_bsi_reg(const Task* __restrict__ tasks,
+                                                     const uint32_t* __restrict__ n_tasks, WideArgs A, BsiArgs P,
+                                                     OutCtx oc, bool want_sum, int* __restrict__ cnts,
+                                                     TB* __restrict__ kin) {
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ __align__(16) uint8_t rows[kBsiRows * kRowB];
+  __shared__ int tot[128];
+  __shared__ BsiKeyBuf kbuf[2];
+  __shared__ int wpar[16];
+  const uint32_t nt = *n_tasks;
+  const int nb = P.nbits;
+  const bool two = P.op == BSI_RANGE;
+  const int tid = threadIdx.x;
+  uint32_t t = blockIdx.x;
+  if (t >= nt) return;
+  uint64_t sl[kBsiRegSlices];
+  int cb = 0;
+  Task tk = tasks[t];
+  bsi_issue_loads(A, kbuf[0], bsi_key_setup(tk, A, nb, kbuf[0]), sl);
+  BST_DECL
+  while (true) {
+    BsiKeyBuf& kb = kbuf[cb];
+    // the next key's positions and slice descriptors, while this key's slices load
+    const uint32_t tn = t + gridDim.x;
+    Task tkn;
+    uint32_t maskn = 0;
+    if (tn < nt) {
+      tkn = tasks[tn];
+      maskn = bsi_key_setup(tkn, A, nb, kbuf[cb ^ 1]);
+    }
+    const uint64_t ebm = mat_word1(A.desc[kb.pos[0]], A.payload, tmp, wpar);  // a task exists only where ebM has the key
+    uint64_t fixed = ebm;
+    if (P.has_found) fixed = kb.pos[nb + 1] >= 0 ? mat_word1(A.desc[kb.pos[nb + 1]], A.payload, tmp, wpar) : 0;
+    BST(0);
+    // array / run slices through the LDS scratch
+#pragma unroll
+    for (int i = 0; i < kBsiRegSlices; i++) {
+      if (i < nb && kb.stype[i].card > 0 && kb.stype[i].kind != DK_B)
+        sl[i] = mat_word1(A.desc[kb.pos[1 + i]], A.payload, tmp, wpar);
+    }
+    // 2. bits of the whole circuit
+    uint64_t eq0 = ebm, gt0 = 0, lt0 = 0, eq1 = ebm, gt1 = 0, lt1 = 0, res;
+    int k = 0;
+    rec1(ebm, k++, rows);  // |ebM| of the bits: the start of the derived cardinalities
+    // predicate bits i = 31 .. 0 as the top bit of running copies; the asm keeps the
+    // compiler from precomputing 64 per-step flags (SGPR spills)
+    uint32_t p0 = P.pred0, p1 = P.pred1;
+    int live = 32 - nb;  // steps i >= nb are skipped
+#pragma unroll
+    for (int i = kBsiRegSlices - 1; i >= 0; i--) {
+      asm volatile("" : "+s"(p0), "+s"(p1), "+s"(live));
+      if (live <= 0) {
+        const uint64_t m0 = (uint64_t)(int64_t)((int32_t)p0 >> 31);  // all ones iff bit i of pred0
+        const uint64_t tv = eq0 & (sl[i] ^ m0);                     // EQ & ~bA[i] / EQ & bA[i]
+        rec1(tv, k++, rows);
+        lt0 |= tv & m0;
+        gt0 |= tv & ~m0;
+        eq0 ^= tv;
+        if (two) {
+          const uint64_t m1 = (uint64_t)(int64_t)((int32_t)p1 >> 31);
+          const uint64_t tw = eq1 & (sl[i] ^ m1);
+          rec1(tw, k++, rows);
+          lt1 |= tw & m1;
+          gt1 |= tw & ~m1;
+          eq1 ^= tw;
+        }
+      }
+      p0 <<= 1;
+      p1 <<= 1;
+      live--;
+    }
+    if (two) {  // RANGE = and(GE(start), LE(end)), BSI/:503-507
+      const uint64_t left = bits_finish1(BSI_GE, fixed, gt0, lt0, eq0, k, rows);
+      const uint64_t right = bits_finish1(BSI_LE, fixed, gt1, lt1, eq1, k, rows);
+      res = left & right;
+      rec1(res, k++, rows);
+    } else {
+      res = bits_finish1(P.op, fixed, gt0, lt0, eq0, k, rows);
+    }
+    BST(1);
+    // 4. sum shares |bA[x] & result| (an absent result has no bits: all zero)
+    if (want_sum) {
+#pragma unroll
+      for (int x = 0; x < kBsiRegSlices; x++)
+        if (x < nb) rec1(sl[x] & res, k + x, rows);
+    }
+    BST(2);
+    // the slices of this key are dead: the next key's start loading now
+    if (tn < nt) bsi_issue_loads(A, kbuf[cb ^ 1], maskn, sl);
+    BST(3);
+    // the result bits to the task's scratch slot: the container itself when it is a
+    // bitmap, else the input k_bsi_types stages it from
+    reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[tid] = res;
+    sum_rows1(rows, k + (want_sum ? nb : 0), tot);
+    BST(4);
+    // counts and the input types of the key for k_bsi_types
+    if (tid < kBsiCnt) cnts[(size_t)t * kBsiCnt + tid] = tid < k + (want_sum ? nb : 0) ? tot[tid] : 0;
+    if (tid >= 64 && tid < 64 + kBsiKin) {
+      const int i = tid - 64;
+      TB x = tb_absent();
+      if (i < kBsiRegSlices) {
+        x = kb.stype[i];
+      } else {
+        const int p = i == kBsiRegSlices ? kb.pos[0] : (P.has_found ? kb.pos[nb + 1] : kb.pos[0]);
+        if (p >= 0) {
+          const CDesc d = A.desc[p];
+          x = TB{d.kind, (int)d.card, p, 0};
+        }
+      }
+      kin[(size_t)t * kBsiKin + i] = x;
+    }
+    BST(5);
+    if (tn >= nt) break;
+    lds_barrier();
+    t = tn;
+    tk = tkn;
+    cb ^= 1;
+  }
+  BST_FLUSH();
+}
+
+// w_place for k_bsi_types: a staged result (LDS) to the task's scratch slot and its record
+__device__ __forceinline__ void bsi_wave_place(uint32_t t, const uint32_t* lds, uint32_t len, uint32_t card,
+                                               uint32_t key, int kind, const OutCtx& oc) {
+  uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+  copy_lds_to_global<64>(slot, lds, len, lane_id());
+  if (lane_id() == 0) bsi_rec(t, oc, true, slot, len, card, key, kind);
+}
+
+// Types of the keys k_bsi_reg computed, one wave per key: the reference's type
+// rule of every step replayed from the counts (scalar, lane-indexed copies read
+// with v_readlane), then the result record -- a bitmap result is already in the
+// scratch slot; array / run results are staged from it with the wave helpers.
+// Keys whose replay needs a run count go to k_bsi_defer (bit 31 of the entry).
+__global__ __launch_bounds__(256) void k_bsi_types(const Task* __restrict__ tasks,
+                                                   const uint32_t* __restrict__ n_tasks, WideArgs A, BsiArgs P,
+                                                   OutCtx oc, unsigned long long* __restrict__ sums,
+                                                   const int* __restrict__ cnts, const TB* __restrict__ kin,
+                                                   uint32_t* __restrict__ defer) {
+  __shared__ __align__(16) uint32_t lds_all[4][2048];
+  const uint32_t nt = *n_tasks;
+  const int nb = P.nbits;
+  const bool two = P.op == BSI_RANGE;
+  const int w = threadIdx.x >> 6, lane = lane_id();
+  uint32_t* lds = lds_all[w];
+  for (uint32_t t = uni(blockIdx.x * 4 + w); t < nt; t += gridDim.x * 4) {
+    int tv[2];
+    tv[0] = cnts[(size_t)t * kBsiCnt + lane];
+    tv[1] = cnts[(size_t)t * kBsiCnt + 64 + lane];
+    const TB my = kin[(size_t)t * kBsiKin + (lane < kBsiKin ? lane : 0)];
+    const TB ebmT{__builtin_amdgcn_readlane(my.kind, kBsiRegSlices), __builtin_amdgcn_readlane(my.card, kBsiRegSlices),
+                  __builtin_amdgcn_readlane(my.src, kBsiRegSlices), 0};
+    const TB fixT{__builtin_amdgcn_readlane(my.kind, kBsiRegSlices + 1),
+                  __builtin_amdgcn_readlane(my.card, kBsiRegSlices + 1),
+                  __builtin_amdgcn_readlane(my.src, kBsiRegSlices + 1), 0};
+    int slow = 0;
+    int kk = 0;
+    const int cebm = step_card(tv, kk++);
+    CircuitT z0{tb_absent(), tb_absent(), ebmT, 0, 0, cebm}, z1 = z0;
+#pragma unroll 1
+    for (int i = nb - 1; i >= 0; i--) {
+      const TB sT{__builtin_amdgcn_readlane(my.kind, i), __builtin_amdgcn_readlane(my.card, i),
+                  __builtin_amdgcn_readlane(my.src, i), 0};
+      types_step((P.pred0 >> i) & 1, sT, z0, kk, tv, slow);
+      if (two) types_step((P.pred1 >> i) & 1, sT, z1, kk, tv, slow);
+    }
+    TB rt;
+    if (two) {
+      const TB left = types_finish(BSI_GE, fixT, z0, kk, tv, slow);
+      const TB right = types_finish(BSI_LE, fixT, z1, kk, tv, slow);
+      rt = tb_op<OPR_AND>(left, right, step_card(tv, kk++), slow);
+    } else {
+      rt = types_finish(P.op, fixT, z0, kk, tv, slow);
+    }
+    if (slow) {  // a step's type needs its run count: k_bsi_defer redoes this key
+      if (lane == 0) defer[1 + atomicAdd(defer, 1u)] = t | 0x80000000u;
+      continue;
+    }
+    const uint32_t key = tasks[t].key;
+    if (sums && rt.card > 0) {
+      // the sum shares follow the counted steps (kk of them)
+      const int k0 = kk;
+      const int c = lane < nb ? cnts[(size_t)t * kBsiCnt + k0 + lane] : 0;
+      if (c) atomicAdd(&sums[lane], (unsigned long long)c);
+      if (lane == 0) atomicAdd(&sums[kBsiMaxInputs], (unsigned long long)rt.card);
+    }
+    if (rt.card == 0) {
+      if (lane == 0) bsi_rec(t, oc, false, nullptr, 0, 0, key, DK_A);
+    } else if (rt.src >= 0) {  // an input container, cloned
+      if (lane == 0) {
+        const CDesc d = A.desc[rt.src];
+        const uint8_t* src = A.payload + d.slot;
+        const uint32_t len = d.kind == DK_A ? 2 * d.card
+                             : d.kind == DK_B ? 8192u
+                                              : 2u + 4u * *reinterpret_cast<const uint16_t*>(src + 2);
+        bsi_rec(t, oc, true, src + (d.kind == DK_R ? 2 : 0), len, d.card, key, d.kind);
+      }
+    } else if (rt.kind == DK_B) {
+      if (lane == 0) bsi_rec(t, oc, true, oc.scratch + (size_t)t * kSlotBytes, 8192, (uint32_t)rt.card, key, DK_B);
+    } else {  // array / run: staged from the bits in the scratch slot
+      WCtr x;
+      w_load_bitmap(oc.scratch + (size_t)t * kSlotBytes, x);
+      const uint32_t len = w_stage(rt.kind, x, rt.card, lds);
+      bsi_wave_place(t, lds, len, (uint32_t)rt.card, key, rt.kind, oc);
+    }
+  }
+}
+
+// keys k_bsi_types handed back: the streamed form, bit by bit
+__global__ __launch_bounds__(256) void k_bsi_defer(const Task* __restrict__ tasks, const uint32_t* __restrict__ defer,
+                                                   WideArgs A, BsiArgs P, OutCtx oc,
+                                                   unsigned long long* __restrict__ sums) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int q[257];
+  __shared__ int sh[8];
+  __shared__ int pos[kBsiMaxInputs];
+  const uint32_t n = defer[0];
+  for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
+    const uint32_t t = defer[1 + j] & 0x7FFFFFFFu;
+    bsi_task_streamed(t, tasks[t], A, P, oc, sums, acc, tmp, q, sh, pos);
   }
 }
 
@@ -229,7 +775,19 @@ void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm,
 }
 
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
-                unsigned long long* sums) {
+                unsigned long long* sums, BsiScratch* sc) {
+  if (p.op <= BSI_RANGE && p.nbits <= kBsiRegSlices && sc) {
+    (void)hipMemsetAsync(sc->defer, 0, 4, s);
+    const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_reg)));
+    hipLaunchKernelGGL(k_bsi_reg, dim3(g), dim3(kNT1), 0, s, tasks, nt, args, p, oc, sums != nullptr, sc->cnts,
+                       reinterpret_cast<TB*>(sc->kin));
+    const int g2 = std::max(1, std::min((grid + 3) / 4, resident_grid((const void*)&k_bsi_types)));
+    hipLaunchKernelGGL(k_bsi_types, dim3(g2), dim3(256), 0, s, tasks, nt, args, p, oc, sums, sc->cnts,
+                       reinterpret_cast<const TB*>(sc->kin), sc->defer);
+    const int g3 = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_defer)));
+    hipLaunchKernelGGL(k_bsi_defer, dim3(g3), dim3(256), 0, s, tasks, sc->defer, args, p, oc, sums);
+    return;
+  }
   const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi)));
   hipLaunchKernelGGL(k_bsi, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc, sums);
 }

@@ -202,6 +202,17 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t x) {
 __device__ __forceinline__ int wave_sum(int v) { return lane63(dpp_incl_scan(v)); }
 __device__ __forceinline__ int wave_incl_scan(int v) { return dpp_incl_scan(v); }
 
+// Workgroup barrier that orders LDS only.  __syncthreads() is also a release /
+// acquire of global memory, so it waits for every outstanding global load and
+// store of the wave; the building blocks below only hand LDS between threads, and
+// with this barrier a kernel can keep global loads (e.g. the next task's
+// operands) in flight across them.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Sum of (a, b) over the workgroup; `sh` needs 8 ints.  Ends with a barrier.
 __device__ __forceinline__ void block_sum2(int& a, int& b, int* sh) {
   a = wave_sum(a);
@@ -211,10 +222,10 @@ __device__ __forceinline__ void block_sum2(int& a, int& b, int* sh) {
     sh[w] = a;
     sh[4 + w] = b;
   }
-  __syncthreads();
+  lds_barrier();
   a = sh[0] + sh[1] + sh[2] + sh[3];
   b = sh[4] + sh[5] + sh[6] + sh[7];
-  __syncthreads();
+  lds_barrier();
 }
 
 // Exclusive scan in word order (first halves of threads 0..255, then second
@@ -227,7 +238,7 @@ __device__ __forceinline__ void block_scan_halves(int v0, int v1, int& p0, int& 
     sh[w] = s0;
     sh[4 + w] = s1;
   }
-  __syncthreads();
+  lds_barrier();
   int o0 = 0, o1 = 0, t0 = 0, t1 = 0;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
@@ -242,7 +253,7 @@ __device__ __forceinline__ void block_scan_halves(int v0, int v1, int& p0, int& 
   p0 = o0 + s0 - v0;
   p1 = t0 + o1 + s1 - v1;
   total = t0 + t1;
-  __syncthreads();
+  lds_barrier();
 }
 
 // ---------------------------------------------------------------------------
@@ -334,7 +345,7 @@ __device__ __forceinline__ void lds_or_run_serial(uint32_t* lds, int s, int e) {
 // ints of LDS.  Must be called by all threads; ends with a barrier.
 __device__ __forceinline__ void lds_or_runs(uint32_t* lds, const uint32_t* pairs, int nruns, int* q) {
   if (threadIdx.x == 0) q[256] = 0;
-  __syncthreads();
+  lds_barrier();
   for (int i = threadIdx.x; i < nruns; i += NT) {
     const uint32_t p = pairs[i];
     const int s = (int)(p & 0xFFFF);
@@ -347,7 +358,7 @@ __device__ __forceinline__ void lds_or_runs(uint32_t* lds, const uint32_t* pairs
       else lds_or_run_serial(lds, s, e);  // queue full: fall back to the serial fill
     }
   }
-  __syncthreads();
+  lds_barrier();
   const int nq = min(q[256], 256);
   for (int k = 0; k < nq; k++) {
     const uint32_t p = pairs[q[k]];
@@ -362,7 +373,7 @@ __device__ __forceinline__ void lds_or_runs(uint32_t* lds, const uint32_t* pairs
       else atomicOr(&lds[w], m);
     }
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // Materialise any container into the caller's owned registers.  `lds` is an
@@ -374,12 +385,12 @@ __device__ __forceinline__ void materialize(const CDesc& d, const uint8_t* paylo
     load_bitmap_owned(slot, r);
     return;
   }
-  __syncthreads();  // previous readers of lds are done
+  lds_barrier();  // previous readers of lds are done
   lds_clear(lds);
-  __syncthreads();
+  lds_barrier();
   if (d.kind == DK_A) {
     lds_scatter_array(lds, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
-    __syncthreads();
+    lds_barrier();
   } else {
     const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
     lds_or_runs(lds, reinterpret_cast<const uint32_t*>(slot + 4), nr, q);
@@ -392,9 +403,9 @@ __device__ __forceinline__ void materialize(const CDesc& d, const uint8_t* paylo
 // in e[4].  Contains barriers.
 __device__ __forceinline__ void run_edges(const uint64_t r[4], uint32_t* lds, uint64_t s[4],
                                           uint64_t e[4]) {
-  __syncthreads();
+  lds_barrier();
   lds_write_owned(lds, r);
-  __syncthreads();
+  lds_barrier();
   const uint64_t* w = reinterpret_cast<const uint64_t*>(lds);
   const int t = threadIdx.x;
   const uint64_t prev0 = (t == 0) ? 0 : (w[2 * t - 1] >> 63);
@@ -435,7 +446,7 @@ __device__ __forceinline__ uint32_t stage_array(const uint64_t r[4], int card, u
       x &= x - 1;
     }
   }
-  __syncthreads();
+  lds_barrier();
   return 2u * (uint32_t)card;
 }
 
@@ -459,7 +470,7 @@ __device__ __forceinline__ uint32_t stage_runs(const uint64_t r[4], uint32_t* ld
       x &= x - 1;
     }
   }
-  __syncthreads();
+  lds_barrier();
   int ep[4] = {pe0, pe0 + popc64(e[0]), pe1, pe1 + popc64(e[2])};
 #pragma unroll
   for (int k = 0; k < 4; k++) {
@@ -472,7 +483,7 @@ __device__ __forceinline__ uint32_t stage_runs(const uint64_t r[4], uint32_t* ld
     }
   }
   if (t == 0) st[0] = (uint16_t)nr;
-  __syncthreads();
+  lds_barrier();
   return 2u + 4u * (uint32_t)nr;
 }
 
@@ -489,9 +500,9 @@ __device__ __forceinline__ int count_runs(const uint64_t r[4], uint32_t* lds, in
 __device__ __forceinline__ uint32_t stage_container(int kind, const uint64_t r[4], int card, uint32_t* lds,
                                                     uint32_t* stage, int* sh) {
   if (kind == DK_B) {
-    __syncthreads();
+    lds_barrier();
     lds_write_owned(stage, r);
-    __syncthreads();
+    lds_barrier();
     return 8192;
   }
   if (kind == DK_A) return stage_array(r, card, stage, sh);

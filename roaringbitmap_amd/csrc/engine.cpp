@@ -129,6 +129,7 @@ struct Ctx {
   std::vector<std::unique_ptr<Batch>> batches;
   uint64_t* zlb = nullptr;    // look-back state the next plan kernel zeroes (null: none)
   uint64_t* ztile = nullptr;
+  DevBuf bsi_defer, bsi_cnts, bsi_kin;  // scratch of the register-resident BSI kernels
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   DevBuf order;                     // horizontal_*: chain order of every key segment
@@ -902,8 +903,15 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
   wa.bm = B->bm.as<uint32_t>();
   wa.payload = B->payload.as<uint8_t>();
   BsiArgs p{mode < 0 ? BSI_EQ : mode, nbits, has_found, (uint32_t)start, (uint32_t)end};
+  BsiScratch sc{};
+  if (mode >= 0 && mode <= BSI_RANGE) {
+    CHK(c->bsi_defer.ensure(4 * (ub + 1)));
+    CHK(c->bsi_cnts.ensure((size_t)512 * ub));
+    CHK(c->bsi_kin.ensure((size_t)16 * 34 * ub));
+    sc = BsiScratch{c->bsi_defer.as<uint32_t>(), c->bsi_cnts.as<int>(), c->bsi_kin.p};
+  }
   launch_bsi(s, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, p, oc,
-             want_sum ? c->bsi_sums.as<unsigned long long>() : nullptr);
+             want_sum ? c->bsi_sums.as<unsigned long long>() : nullptr, sc.defer ? &sc : nullptr);
   c->mark(2);
   if (op == BSI_SUM_ONLY) {
     c->last = 0;
@@ -1562,7 +1570,8 @@ int rbg_bsi_sum(const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices
 }
 int rbg_debug_stamps(uint64_t* out20, int reset) {
   if (!out20) return RBG_ERR_ILLEGAL_ARGUMENT;
-  debug_stamps(out20, reset != 0);
+  if (getenv("RBG_DEBUG_BSI")) debug_bsi_stamps(out20, reset != 0);
+  else debug_stamps(out20, reset != 0);
   return RBG_OK;
 }
 int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2) {

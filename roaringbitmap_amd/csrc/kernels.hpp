@@ -74,6 +74,8 @@ void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tas
                      const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card);
 // diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
 void debug_stamps(uint64_t* out20, bool reset);
+// diagnostic build (-DRBG_BSI_STAMPS=1): per-phase clock totals of k_bsi_reg
+void debug_bsi_stamps(uint64_t* out20, bool reset);
 void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
                  uint32_t* task_card);
 // result materialisation: k_place = compaction scan over the task records
@@ -98,8 +100,15 @@ void launch_gather(hipStream_t s, const GatherItem* items, uint64_t n, const uin
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
                      uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile);
 // sums: kBsiMaxInputs + 1 u64 (per-slice |bA[x] & found|, then the found count); null = no sum
+// scratch of the register-resident compare kernels (bsi.hip), per task of the op:
+// defer: 1 + tasks u32, cnts: 512 B, kin: 34 x 16 B.  Null: the streamed kernel only.
+struct BsiScratch {
+  uint32_t* defer;
+  int* cnts;
+  void* kin;
+};
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
-                unsigned long long* sums);
+                unsigned long long* sums, BsiScratch* sc);
 
 // batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch: per-pair key
 // alignment (count, scan, emit), then one wave per matched key; pairs of more than 64

@@ -451,7 +451,7 @@ __device__ __forceinline__ void plan_count(int f, uint32_t* wg_count) {
   __shared__ int wc[4];
   const uint64_t m = __ballot(f);
   if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = __popcll(m);
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) wg_count[blockIdx.x] = (uint32_t)(wc[0] + wc[1] + wc[2] + wc[3]);
 }
 
@@ -909,7 +909,7 @@ __device__ __forceinline__ void wg_place(uint32_t t, bool keep, const uint8_t* s
     r.keep = keep ? 1 : 0;
     oc.recs[t] = r;
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 __device__ __forceinline__ void wg_passthrough(uint32_t t, const CDesc& d, const uint8_t* payload, const OutCtx& oc,

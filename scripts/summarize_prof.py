@@ -64,7 +64,7 @@ def counters(path):
 # workload (bench.py --only) -> (traffic key in pmc_traffic.json, dominant kernel)
 WORKLOADS = {"c2": ("k_pair_wave", "k_pair_wave<0, 0>"), "c2card": ("k_pair_wave_card", "k_pair_wave<0, 1>"),
              "c3u": ("k_wide<OR>_uniform", "k_wide<0>"), "c3c": ("k_wide<OR>_clustered", "k_wide<0>"),
-             "c5": ("k_bsi", "k_bsi")}
+             "c5": ("k_bsi_reg", "k_bsi_reg")}
 
 
 def main(tag):
