@@ -134,7 +134,9 @@ int rbg_version(void);
  * RoaringBitmap.bitmapOf(int...) (RB/RoaringBitmap.java:566-570) optionally followed
  * by runOptimize() (:2764-2774); values need not be sorted or distinct. */
 int rbg_from_values(const uint32_t* values, size_t n, int run_optimize, rbg_buffer* out);
-/* RoaringBitmap.runOptimize() on a serialized bitmap. */
+/* RoaringBitmap.runOptimize() on a serialized bitmap (RB/RoaringBitmap.java:2764-2774),
+ * computed on the GPU: the device runOptimize pass of rbg_run_optimize_many over a
+ * one-bitmap batch.  Without a usable device it returns RBG_ERR_DEVICE. */
 int rbg_run_optimize(const uint8_t* buf, size_t len, rbg_buffer* out);
 /* RoaringBitmap.toArray(): ascending values (unsigned); out->data holds n*4 bytes. */
 int rbg_to_values(const uint8_t* buf, size_t len, rbg_buffer* out);

@@ -1203,16 +1203,12 @@ int rbg_from_values(const uint32_t* values, size_t n, int run_optimize, rbg_buff
   return emit_host(build_from_values(values, n, run_optimize != 0), out);
 }
 
+// RoaringBitmap.runOptimize() (RB/RoaringBitmap.java:2764-2774): the device pass
+// (runopt.hip) over a one-bitmap batch, like rbg_run_optimize_many.
 int rbg_run_optimize(const uint8_t* buf, size_t len, rbg_buffer* out) {
-  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
-  std::vector<uint8_t> v;
-  std::string err;
-  int st = run_optimize_serialized(buf, len, &v, &err);
-  if (st) {
-    set_err(err);
-    return st;
-  }
-  return emit_host(v, out);
+  if (!out || (!buf && len)) return RBG_ERR_ILLEGAL_ARGUMENT;
+  uint8_t answer = 0;
+  return rbg_run_optimize_many(&buf, &len, 1, out, &answer);
 }
 
 int rbg_to_values(const uint8_t* buf, size_t len, rbg_buffer* out) {

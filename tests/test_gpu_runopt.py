@@ -38,6 +38,23 @@ def test_run_optimize_many_families(gpu, seed):
         assert a == _answer(exp)
 
 
+@pytest.mark.parametrize("seed", range(2))
+def test_single_bitmap_run_optimize(gpu, seed):
+    """RoaringBitmap.runOptimize() (rbg_run_optimize: the device pass over a one-bitmap batch)."""
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(950 + seed)
+    for i in range(12):
+        keys = np.sort(rng.choice(1 << 16, size=int(rng.integers(1, 20)), replace=False))
+        buf = _gen.bitmap(rng, keys)
+        bm = rb.RoaringBitmap(buf)
+        answer = bm.runOptimize()
+        exp = O.run_optimize(buf)
+        assert bm.serialize() == exp
+        assert answer == _answer(exp)
+    bm = rb.RoaringBitmap(O.from_values([]))
+    assert bm.runOptimize() is False and bm.serialize() == O.from_values([])
+
+
 def test_engine_run_optimize_c2_batch(gpu):
     """A synthetic C2 operand (65,536 keys, mixed A/B/R) optimized on the device and then
     used as an operand: bytes equal to the oracle's runOptimize, and AND results equal to

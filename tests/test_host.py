@@ -67,11 +67,12 @@ def test_from_values_matches_oracle(mode, run_opt):
 
 @pytest.mark.parametrize("mode", MODES)
 def test_run_optimize_and_to_values(mode):
+    # construction with runOptimize (bitmapOf + runOptimize on the host); the
+    # RoaringBitmap.runOptimize() op itself runs on the GPU (test_gpu_runopt.py)
     rng = np.random.default_rng(7 + (hash(mode) & 0xFF))
     vals = bitmap_values(rng, mode, n_keys=3)
     rb = RoaringBitmap.from_values(vals)
-    rb2 = rb.clone()
-    rb2.runOptimize()
+    rb2 = RoaringBitmap.from_values(vals, run_optimize=True)
     assert rb2.serialize() == O.run_optimize(rb.serialize())
     assert np.array_equal(rb2.toArray(), np.unique(np.asarray(vals, dtype=np.uint32)))
     assert rb2.getLongCardinality() == len(np.unique(vals))
@@ -131,6 +132,8 @@ def test_compute_fails_loudly_without_device():
         RoaringBitmap.andCardinality(a, b)
     with pytest.raises(DeviceError):
         FastAggregation.or_(a, b)
+    with pytest.raises(DeviceError):  # RoaringBitmap.runOptimize runs the device pass
+        a.runOptimize()
 
 
 def test_illegal_argument_type():
