@@ -325,12 +325,13 @@ __device__ __forceinline__ void sum_rows1(const uint8_t* rows, int nk, int* tot)
   }
   lds_barrier();
 }
-// count k from the per-lane copies of the totals (tv[j] = tot[64 j + lane]), wave-uniform
-__device__ __forceinline__ int step_card(const int* tv, int k) {
-  const int j = k >> 6, l = k & 63;
-  const int v = j == 0 ? tv[0] : tv[1];
-  return __builtin_amdgcn_readlane(v, l);
-}
+// count k of this thread's key: the tables are transposed (row k of every key is
+// contiguous), so a wave reads 64 keys' count k with one coalesced load
+struct CountRows {
+  const int* p;  // cnts + key index
+  size_t stride;
+  __device__ __forceinline__ int operator()(int k) const { return p[(size_t)k * stride]; }
+};
 
 // Type replay of a step / finish, in the order of the bits.  c* are the exact
 // cardinalities of the bits (0 for an absent bitmap).
@@ -338,8 +339,9 @@ struct CircuitT {
   TB gt, lt, eq;
   int cgt, clt, ceq;
 };
-__device__ __forceinline__ void types_step(int bit, const TB& s, CircuitT& z, int& k, const int* tv, int& slow) {
-  const int ct = step_card(tv, k++);
+__device__ __forceinline__ void types_step(int bit, const TB& s, CircuitT& z, int& k, const CountRows& tv,
+                                           int& slow) {
+  const int ct = tv(k++);
   if (bit) {
     const TB t = tb_op<OPR_ANDNOT>(z.eq, s, ct, slow);
     z.lt = tb_op<OPR_OR>(z.lt, t, z.clt + ct, slow);
@@ -355,15 +357,16 @@ __device__ __forceinline__ void types_step(int bit, const TB& s, CircuitT& z, in
 }
 // BSI/:453-467 on types: counted are fixed & EQ and the NEQ / GT / LT results;
 // LE / GE are disjoint unions
-__device__ __forceinline__ TB types_finish(int op, const TB& fixed, CircuitT& z, int& k, const int* tv, int& slow) {
-  const int ce = step_card(tv, k++);
+__device__ __forceinline__ TB types_finish(int op, const TB& fixed, CircuitT& z, int& k, const CountRows& tv,
+                                           int& slow) {
+  const int ce = tv(k++);
   z.eq = tb_op<OPR_AND>(fixed, z.eq, ce, slow);
   z.ceq = ce;
   switch (op) {
     case BSI_EQ: return z.eq;
-    case BSI_NEQ: return tb_op<OPR_ANDNOT>(fixed, z.eq, step_card(tv, k++), slow);
-    case BSI_GT: return tb_op<OPR_AND>(z.gt, fixed, step_card(tv, k++), slow);
-    case BSI_LT: return tb_op<OPR_AND>(z.lt, fixed, step_card(tv, k++), slow);
+    case BSI_NEQ: return tb_op<OPR_ANDNOT>(fixed, z.eq, tv(k++), slow);
+    case BSI_GT: return tb_op<OPR_AND>(z.gt, fixed, tv(k++), slow);
+    case BSI_LT: return tb_op<OPR_AND>(z.lt, fixed, tv(k++), slow);
     case BSI_LE: return tb_op<OPR_OR>(z.lt, z.eq, z.clt + ce, slow);
     default: return tb_op<OPR_OR>(z.gt, z.eq, z.cgt + ce, slow);  // GE
   }
@@ -540,7 +543,7 @@ __device__ __forceinline__ void bsi_rec(uint32_t t, const OutCtx& oc, bool keep,
 
 // compare ops (BSI_EQ .. BSI_RANGE) with nbits <= kBsiRegSlices: one 1,024-thread
 // workgroup per key computes the bits and the counts; k_bsi_types (a wave per key)
-// replays the types and writes the records.  cnts: kBsiCnt ints per task; kin:
+// replays the types and writes the records.  cnts: kBsiCnt rows of one int per task; kin:
 // kBsiKin input types per task (slices, ebM, the fixed found set).
 constexpr int kBsiCnt = 128;
 constexpr int kBsiKin = kBsiRegSlices + 2;
@@ -548,7 +551,7 @@ static_assert(kBsiRows <= kBsiCnt, "count rows");
 __global__ __launch_bounds__(1024, 1) void k_bsi_reg(const Task* __restrict__ tasks,
                                                      const uint32_t* __restrict__ n_tasks, WideArgs A, BsiArgs P,
                                                      OutCtx oc, bool want_sum, int* __restrict__ cnts,
-                                                     TB* __restrict__ kin) {
+                                                     TB* __restrict__ kin, size_t tstride) {
   __shared__ __align__(16) uint32_t tmp[2048];
   __shared__ __align__(16) uint8_t rows[kBsiRows * kRowB];
   __shared__ int tot[128];
@@ -640,8 +643,9 @@ __global__ __launch_bounds__(1024, 1) void k_bsi_reg(const Task* __restrict__ ta
     reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[tid] = res;
     sum_rows1(rows, k + (want_sum ? nb : 0), tot);
     BST(4);
-    // counts and the input types of the key for k_bsi_types
-    if (tid < kBsiCnt) cnts[(size_t)t * kBsiCnt + tid] = tid < k + (want_sum ? nb : 0) ? tot[tid] : 0;
+    // counts and the input types of the key for k_bsi_types (transposed: row r of
+    // every key contiguous)
+    if (tid < k + (want_sum ? nb : 0)) cnts[(size_t)tid * tstride + t] = tot[tid];
     if (tid >= 64 && tid < 64 + kBsiKin) {
       const int i = tid - 64;
       TB x = tb_absent();
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(1024, 1) void k_bsi_reg(const Task* __restrict__ ta
           x = TB{d.kind, (int)d.card, p, 0};
         }
       }
-      kin[(size_t)t * kBsiKin + i] = x;
+      kin[(size_t)i * tstride + t] = x;
     }
     BST(5);
     if (tn >= nt) break;
@@ -674,86 +678,81 @@ __device__ __forceinline__ void bsi_wave_place(uint32_t t, const uint32_t* lds, 
   if (lane_id() == 0) bsi_rec(t, oc, true, slot, len, card, key, kind);
 }
 
-// Types of the keys k_bsi_reg computed, one wave per key: the reference's type
-// rule of every step replayed from the counts (scalar, lane-indexed copies read
-// with v_readlane), then the result record -- a bitmap result is already in the
-// scratch slot; array / run results are staged from it with the wave helpers.
-// Keys whose replay needs a run count go to k_bsi_defer (bit 31 of the entry).
+// Types of the keys k_bsi_reg computed, one THREAD per key: the reference's type
+// rule of every step is replayed from the counts (branch-free selects; the counts
+// and input types are read as transposed rows, coalesced across the keys of a
+// wave), then the result record.  A bitmap result is already in the scratch slot;
+// array / run results (staged from it by a wave) and keys whose replay needs a run
+// count go to k_bsi_defer.  Sums: per slice one wave reduction, one atomic.
 __global__ __launch_bounds__(256) void k_bsi_types(const Task* __restrict__ tasks,
                                                    const uint32_t* __restrict__ n_tasks, WideArgs A, BsiArgs P,
                                                    OutCtx oc, unsigned long long* __restrict__ sums,
                                                    const int* __restrict__ cnts, const TB* __restrict__ kin,
-                                                   uint32_t* __restrict__ defer) {
-  __shared__ __align__(16) uint32_t lds_all[4][2048];
+                                                   size_t tstride, uint32_t* __restrict__ defer) {
   const uint32_t nt = *n_tasks;
   const int nb = P.nbits;
   const bool two = P.op == BSI_RANGE;
-  const int w = threadIdx.x >> 6, lane = lane_id();
-  uint32_t* lds = lds_all[w];
-  for (uint32_t t = uni(blockIdx.x * 4 + w); t < nt; t += gridDim.x * 4) {
-    int tv[2];
-    tv[0] = cnts[(size_t)t * kBsiCnt + lane];
-    tv[1] = cnts[(size_t)t * kBsiCnt + 64 + lane];
-    const TB my = kin[(size_t)t * kBsiKin + (lane < kBsiKin ? lane : 0)];
-    const TB ebmT{__builtin_amdgcn_readlane(my.kind, kBsiRegSlices), __builtin_amdgcn_readlane(my.card, kBsiRegSlices),
-                  __builtin_amdgcn_readlane(my.src, kBsiRegSlices), 0};
-    const TB fixT{__builtin_amdgcn_readlane(my.kind, kBsiRegSlices + 1),
-                  __builtin_amdgcn_readlane(my.card, kBsiRegSlices + 1),
-                  __builtin_amdgcn_readlane(my.src, kBsiRegSlices + 1), 0};
-    int slow = 0;
-    int kk = 0;
-    const int cebm = step_card(tv, kk++);
-    CircuitT z0{tb_absent(), tb_absent(), ebmT, 0, 0, cebm}, z1 = z0;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (uni(blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) >= nt) return;  // whole waves past the end
+  const bool live = t < nt;
+  const uint32_t tt = live ? t : 0;
+  const CountRows tv{cnts + tt, tstride};
+  const TB ebmT = kin[(size_t)kBsiRegSlices * tstride + tt];
+  const TB fixT = kin[(size_t)(kBsiRegSlices + 1) * tstride + tt];
+  int slow = 0;
+  int kk = 0;
+  const int cebm = tv(kk++);
+  CircuitT z0{tb_absent(), tb_absent(), ebmT, 0, 0, cebm}, z1 = z0;
 #pragma unroll 1
-    for (int i = nb - 1; i >= 0; i--) {
-      const TB sT{__builtin_amdgcn_readlane(my.kind, i), __builtin_amdgcn_readlane(my.card, i),
-                  __builtin_amdgcn_readlane(my.src, i), 0};
-      types_step((P.pred0 >> i) & 1, sT, z0, kk, tv, slow);
-      if (two) types_step((P.pred1 >> i) & 1, sT, z1, kk, tv, slow);
+  for (int i = nb - 1; i >= 0; i--) {
+    const TB sT = kin[(size_t)i * tstride + tt];
+    types_step((P.pred0 >> i) & 1, sT, z0, kk, tv, slow);
+    if (two) types_step((P.pred1 >> i) & 1, sT, z1, kk, tv, slow);
+  }
+  TB rt;
+  if (two) {
+    const TB left = types_finish(BSI_GE, fixT, z0, kk, tv, slow);
+    const TB right = types_finish(BSI_LE, fixT, z1, kk, tv, slow);
+    rt = tb_op<OPR_AND>(left, right, tv(kk++), slow);
+  } else {
+    rt = types_finish(P.op, fixT, z0, kk, tv, slow);
+  }
+  const bool ok = live && !slow;
+  // sums: the sum shares follow the counted steps (kk of them); one atomic per slice per wave
+  if (sums) {
+    const bool add = ok && rt.card > 0;
+    for (int x = 0; x < nb; x++) {
+      const int c = wave_sum(add ? tv(kk + x) : 0);
+      if ((threadIdx.x & 63) == 0 && c) atomicAdd(&sums[x], (unsigned long long)(uint32_t)c);
     }
-    TB rt;
-    if (two) {
-      const TB left = types_finish(BSI_GE, fixT, z0, kk, tv, slow);
-      const TB right = types_finish(BSI_LE, fixT, z1, kk, tv, slow);
-      rt = tb_op<OPR_AND>(left, right, step_card(tv, kk++), slow);
-    } else {
-      rt = types_finish(P.op, fixT, z0, kk, tv, slow);
-    }
-    if (slow) {  // a step's type needs its run count: k_bsi_defer redoes this key
-      if (lane == 0) defer[1 + atomicAdd(defer, 1u)] = t | 0x80000000u;
-      continue;
-    }
-    const uint32_t key = tasks[t].key;
-    if (sums && rt.card > 0) {
-      // the sum shares follow the counted steps (kk of them)
-      const int k0 = kk;
-      const int c = lane < nb ? cnts[(size_t)t * kBsiCnt + k0 + lane] : 0;
-      if (c) atomicAdd(&sums[lane], (unsigned long long)c);
-      if (lane == 0) atomicAdd(&sums[kBsiMaxInputs], (unsigned long long)rt.card);
-    }
-    if (rt.card == 0) {
-      if (lane == 0) bsi_rec(t, oc, false, nullptr, 0, 0, key, DK_A);
-    } else if (rt.src >= 0) {  // an input container, cloned
-      if (lane == 0) {
-        const CDesc d = A.desc[rt.src];
-        const uint8_t* src = A.payload + d.slot;
-        const uint32_t len = d.kind == DK_A ? 2 * d.card
-                             : d.kind == DK_B ? 8192u
-                                              : 2u + 4u * *reinterpret_cast<const uint16_t*>(src + 2);
-        bsi_rec(t, oc, true, src + (d.kind == DK_R ? 2 : 0), len, d.card, key, d.kind);
-      }
-    } else if (rt.kind == DK_B) {
-      if (lane == 0) bsi_rec(t, oc, true, oc.scratch + (size_t)t * kSlotBytes, 8192, (uint32_t)rt.card, key, DK_B);
-    } else {  // array / run: staged from the bits in the scratch slot
-      WCtr x;
-      w_load_bitmap(oc.scratch + (size_t)t * kSlotBytes, x);
-      const uint32_t len = w_stage(rt.kind, x, rt.card, lds);
-      bsi_wave_place(t, lds, len, (uint32_t)rt.card, key, rt.kind, oc);
-    }
+    const int cc = wave_sum(add ? rt.card : 0);
+    if ((threadIdx.x & 63) == 0 && cc) atomicAdd(&sums[kBsiMaxInputs], (unsigned long long)(uint32_t)cc);
+  }
+  if (!live) return;
+  if (slow) {  // a step's type needs its run count: k_bsi_defer redoes this key
+    defer[1 + atomicAdd(defer, 1u)] = t | 0x80000000u;
+    return;
+  }
+  const uint32_t key = tasks[t].key;
+  if (rt.card == 0) {
+    bsi_rec(t, oc, false, nullptr, 0, 0, key, DK_A);
+  } else if (rt.src >= 0) {  // an input container, cloned
+    const CDesc d = A.desc[rt.src];
+    const uint8_t* src = A.payload + d.slot;
+    const uint32_t len = d.kind == DK_A ? 2 * d.card
+                         : d.kind == DK_B ? 8192u
+                                          : 2u + 4u * *reinterpret_cast<const uint16_t*>(src + 2);
+    bsi_rec(t, oc, true, src + (d.kind == DK_R ? 2 : 0), len, d.card, key, d.kind);
+  } else if (rt.kind == DK_B) {
+    bsi_rec(t, oc, true, oc.scratch + (size_t)t * kSlotBytes, 8192, (uint32_t)rt.card, key, DK_B);
+  } else {  // array / run: staged from the bits in the scratch slot by k_bsi_defer
+    defer[1 + atomicAdd(defer, 1u)] = t | ((rt.kind == DK_A ? 1u : 2u) << 29);
+    bsi_rec(t, oc, true, nullptr, 0, (uint32_t)rt.card, key, rt.kind);  // k_bsi_defer rewrites it
   }
 }
 
-// keys k_bsi_types handed back: the streamed form, bit by bit
+// keys k_bsi_types handed over (defer[1..]): bit 31 = redo with the streamed form,
+// bits 29-30 = stage the array (1) / run (2) result from the bits in the scratch slot
 __global__ __launch_bounds__(256) void k_bsi_defer(const Task* __restrict__ tasks, const uint32_t* __restrict__ defer,
                                                    WideArgs A, BsiArgs P, OutCtx oc,
                                                    unsigned long long* __restrict__ sums) {
@@ -764,8 +763,19 @@ __global__ __launch_bounds__(256) void k_bsi_defer(const Task* __restrict__ task
   __shared__ int pos[kBsiMaxInputs];
   const uint32_t n = defer[0];
   for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
-    const uint32_t t = defer[1 + j] & 0x7FFFFFFFu;
-    bsi_task_streamed(t, tasks[t], A, P, oc, sums, acc, tmp, q, sh, pos);
+    const uint32_t e = defer[1 + j];
+    const uint32_t t = e & 0x1FFFFFFFu;
+    if (e >> 31) {
+      bsi_task_streamed(t, tasks[t], A, P, oc, sums, acc, tmp, q, sh, pos);
+      continue;
+    }
+    const int kind = ((e >> 29) & 3) == 1 ? DK_A : DK_R;
+    const uint32_t card = oc.recs[t].card;
+    uint64_t r[4];
+    load_bitmap_owned(oc.scratch + (size_t)t * kSlotBytes, r);
+    lds_barrier();
+    const uint32_t len = stage_container(kind, r, (int)card, acc, tmp, sh);
+    wg_place(t, true, nullptr, true, tmp, len, card, tasks[t].key, kind, oc, nullptr);
   }
 }
 
@@ -780,10 +790,10 @@ void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, 
     (void)hipMemsetAsync(sc->defer, 0, 4, s);
     const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_reg)));
     hipLaunchKernelGGL(k_bsi_reg, dim3(g), dim3(kNT1), 0, s, tasks, nt, args, p, oc, sums != nullptr, sc->cnts,
-                       reinterpret_cast<TB*>(sc->kin));
-    const int g2 = std::max(1, std::min((grid + 3) / 4, resident_grid((const void*)&k_bsi_types)));
+                       reinterpret_cast<TB*>(sc->kin), sc->stride);
+    const int g2 = (int)((sc->stride + 255) / 256);
     hipLaunchKernelGGL(k_bsi_types, dim3(g2), dim3(256), 0, s, tasks, nt, args, p, oc, sums, sc->cnts,
-                       reinterpret_cast<const TB*>(sc->kin), sc->defer);
+                       reinterpret_cast<const TB*>(sc->kin), sc->stride, sc->defer);
     const int g3 = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_defer)));
     hipLaunchKernelGGL(k_bsi_defer, dim3(g3), dim3(256), 0, s, tasks, sc->defer, args, p, oc, sums);
     return;

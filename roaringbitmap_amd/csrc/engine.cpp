@@ -908,7 +908,7 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
     CHK(c->bsi_defer.ensure(4 * (ub + 1)));
     CHK(c->bsi_cnts.ensure((size_t)512 * ub));
     CHK(c->bsi_kin.ensure((size_t)16 * 34 * ub));
-    sc = BsiScratch{c->bsi_defer.as<uint32_t>(), c->bsi_cnts.as<int>(), c->bsi_kin.p};
+    sc = BsiScratch{c->bsi_defer.as<uint32_t>(), c->bsi_cnts.as<int>(), c->bsi_kin.p, ub};
   }
   launch_bsi(s, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, p, oc,
              want_sum ? c->bsi_sums.as<unsigned long long>() : nullptr, sc.defer ? &sc : nullptr);

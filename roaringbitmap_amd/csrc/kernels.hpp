@@ -100,12 +100,15 @@ void launch_gather(hipStream_t s, const GatherItem* items, uint64_t n, const uin
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
                      uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile);
 // sums: kBsiMaxInputs + 1 u64 (per-slice |bA[x] & found|, then the found count); null = no sum
-// scratch of the register-resident compare kernels (bsi.hip), per task of the op:
-// defer: 1 + tasks u32, cnts: 512 B, kin: 34 x 16 B.  Null: the streamed kernel only.
+// scratch of the register-resident compare kernels (bsi.hip), per task of the op
+// (stride = task capacity; the tables are transposed, row-major over the tasks):
+// defer: 1 + stride u32, cnts: 128 rows of stride ints, kin: 34 rows of stride x 16 B.
+// Null: the streamed kernel only.
 struct BsiScratch {
   uint32_t* defer;
   int* cnts;
   void* kin;
+  size_t stride;
 };
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
                 unsigned long long* sums, BsiScratch* sc);
