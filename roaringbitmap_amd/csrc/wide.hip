@@ -632,14 +632,20 @@ __device__ __forceinline__ PairItem load_item(const PairItem* items, uint64_t i)
   return r.p;
 }
 
-// |a & b| of two arrays of <= 512 values: both payloads requested at once (one
-// 16 B vector per lane each), the larger scattered into the wave's LDS map, the
-// smaller probed (RB/ArrayContainer.java:232-240 andCardinality)
-__device__ __forceinline__ uint32_t small_arrays_and_card(const uint8_t* pa, uint32_t ca, const uint8_t* pb,
-                                                         uint32_t cb, uint32_t* lds, int lane) {
-  const uint32_t na = (ca + 7) >> 3, nb = (cb + 7) >> 3;
-  const uint4 va = (uint32_t)lane < na ? reinterpret_cast<const uint4*>(pa)[lane] : make_uint4(0, 0, 0, 0);
-  const uint4 vb = (uint32_t)lane < nb ? reinterpret_cast<const uint4*>(pb)[lane] : make_uint4(0, 0, 0, 0);
+// |a & b| of two arrays of <= 512 values (RB/ArrayContainer.java:232-240
+// andCardinality): one 16 B vector per lane of each, the larger scattered into the
+// wave's LDS map, the smaller probed
+__device__ __forceinline__ bool small_pair(const PairItem& it) {
+  return it.kind_a == DK_A && it.kind_b == DK_A && it.card_a <= 512 && it.card_b <= 512;
+}
+__device__ __forceinline__ void small_pair_load(const PairItem& it, const uint8_t* payload, int lane, uint4& va,
+                                                uint4& vb) {
+  const uint32_t na = (it.card_a + 7) >> 3, nb = (it.card_b + 7) >> 3;
+  va = (uint32_t)lane < na ? reinterpret_cast<const uint4*>(payload + it.slot_a)[lane] : make_uint4(0, 0, 0, 0);
+  vb = (uint32_t)lane < nb ? reinterpret_cast<const uint4*>(payload + it.slot_b)[lane] : make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ uint32_t small_arrays_and_card(const uint4 va, uint32_t ca, const uint4 vb, uint32_t cb,
+                                                         uint32_t* lds, int lane) {
   uint4* l4 = reinterpret_cast<uint4*>(lds);
 #pragma unroll
   for (int i = 0; i < 8; i++) l4[64 * i + lane] = make_uint4(0, 0, 0, 0);
@@ -661,8 +667,9 @@ __device__ __forceinline__ uint32_t small_arrays_and_card(const uint8_t* pa, uin
   return c;
 }
 
-// one wave per matched key (resident grid, the next item's record prefetched
-// through the scalar cache); sums wrap like Java ints
+// one wave per matched key (resident grid), software-pipelined: while an item is
+// counted, the next item's payload vectors (small arrays) are already in flight and
+// the record after that is loaded through the scalar cache; sums wrap like Java ints
 __global__ __launch_bounds__(256) void k_pair_items(const PairItem* __restrict__ items, const uint64_t* __restrict__ tot,
                                                     const uint8_t* __restrict__ payload, int32_t* __restrict__ out) {
   __shared__ __align__(16) uint32_t lds[4][2048];
@@ -671,14 +678,21 @@ __global__ __launch_bounds__(256) void k_pair_items(const PairItem* __restrict__
   const uint64_t stride = (uint64_t)gridDim.x * 4;
   uint64_t i = (uint64_t)blockIdx.x * 4 + w;
   if (i >= n) return;
-  PairItem cur = load_item(items, i);
+  PairItem cur = load_item(items, i), nxt;
+  if (i + stride < n) nxt = load_item(items, i + stride);
+  uint4 va, vb;
+  bool pre = small_pair(cur);
+  if (pre) small_pair_load(cur, payload, lane, va, vb);
   for (;;) {
-    const uint64_t in = i + stride;
-    PairItem nxt;
-    if (in < n) nxt = load_item(items, in);
+    const uint64_t in = i + stride, in2 = in + stride;
+    PairItem nxt2;
+    if (in2 < n) nxt2 = load_item(items, in2);
+    uint4 na, nb;
+    const bool npre = in < n && small_pair(nxt);
+    if (npre) small_pair_load(nxt, payload, lane, na, nb);  // in flight while this item is counted
     uint32_t c;
-    if (cur.kind_a == DK_A && cur.kind_b == DK_A && cur.card_a <= 512 && cur.card_b <= 512) {
-      c = small_arrays_and_card(payload + cur.slot_a, cur.card_a, payload + cur.slot_b, cur.card_b, lds[w], lane);
+    if (pre) {
+      c = small_arrays_and_card(va, cur.card_a, vb, cur.card_b, lds[w], lane);
     } else {
       const CDesc da{cur.slot_a, cur.card_a, 0, cur.kind_a, 0}, db{cur.slot_b, cur.card_b, 0, cur.kind_b, 0};
       c = wave_and_card(da, db, payload, lds[w], lane);
@@ -687,6 +701,10 @@ __global__ __launch_bounds__(256) void k_pair_items(const PairItem* __restrict__
     if (in >= n) break;
     i = in;
     cur = nxt;
+    nxt = nxt2;
+    pre = npre;
+    va = na;
+    vb = nb;
   }
 }
 
