@@ -237,33 +237,42 @@ __global__ __launch_bounds__(256) void k_bsi(const Task* __restrict__ tasks, con
 }
 
 // ===========================================================================
-// Register-resident query (compare ops, nbits <= 32): k_bsi_reg + k_bsi_defer
+// Register-resident query (compare ops, nbits <= 32): k_bsi_reg + k_bsi_types
 // ===========================================================================
 // The streamed form above is bound by its ~6 workgroup reductions per slice (two
 // barriers each, a dependent chain of ~190 per key) and reads every slice twice.
-// k_bsi_reg runs one key per 1,024-thread workgroup, thread t owning container
-// word t, and holds ALL slices of the key in registers (one u64 per slice per
-// thread):
-//   1. every slice of the key is requested at once;
-//   2. bits: the whole circuit on registers.  Per step only t = EQ & bA[i] (or
-//      EQ & ~bA[i]) is counted -- t and the new EQ partition the old EQ, and t is
-//      disjoint from GT / LT, so |EQ'| = |EQ| - |t| and |GT'| = |GT| + |t|.  Each
-//      thread stores its share (<= 64, a byte) in an LDS row per count; no
-//      barrier inside the circuit;
-//   4. sum shares |bA[x] & result| from the same registers (no second read);
-//      then the next key's slices start loading;
-//   3. the rows are summed, and one wave replays the reference's type rule of
-//      every step from those cardinalities (wave-uniform, no bits needed).  A
-//      step whose type needs a run count (EFF: run containers in AND / OR / ...)
-//      cannot be replayed so: such keys go to k_bsi_defer, which redoes them
-//      with bsi_task_streamed.
-// Results that are absent, clones or bitmap containers are written here (a
-// bitmap is one coalesced 8 B store per thread); array / run results are left
-// as raw bitmaps for k_bsi_defer to stage with the 256-thread helpers.
+// The bits of the circuit are independent per container word; only the
+// cardinalities that decide the result types (App. A) need the whole key.  So:
+//  * k_bsi_reg works on units of 256 container words (a quarter key) with one
+//    thread per word.  A unit holds all of its slices in registers (one u64 per
+//    slice per thread), requests them all at once, runs the circuit on the bits
+//    and writes its quarter of the result bits to the task's scratch slot.  Per
+//    step only t = EQ & bA[i] (or EQ & ~bA[i]) is counted: t and the new EQ
+//    partition the old EQ, and t is disjoint from GT / LT, so |EQ'| = |EQ| - |t|
+//    and |GT'| = |GT| + |t| follow by arithmetic.  sum's shares |bA[x] & result|
+//    come from the same registers, so the index is read once.  Each unit writes
+//    its partial counts; several units per CU are resident, so one unit's loads
+//    overlap another's compute.
+//  * k_bsi_types, one thread per key, adds the units' partial counts and replays
+//    the reference's type rule of every step (see there).
+// A key whose replay needs a run count (EFF) is redone by k_bsi_defer with the
+// streamed form; array / run results are staged there from the bits.
+#ifndef RBG_BSI_WAVES
+#define RBG_BSI_WAVES 4  // waves per SIMD k_bsi_reg is compiled for
+#endif
 constexpr int kBsiRegSlices = 32;
-constexpr int kNT1 = 1024;  // threads of k_bsi_reg
-constexpr int kBsiRows = 1 + 2 * kBsiRegSlices + 4 + kBsiRegSlices;  // |ebM|, counted steps, finish, sum shares
-constexpr int kRowB = kNT1 + 16;  // row stride in bytes: row sums of a wave spread over the banks
+constexpr int kBsiUnits = 4;                // units per key
+constexpr int kUnitWords = 1024 / kBsiUnits;  // container words per unit = threads per workgroup
+static_assert(kUnitWords == NT, "a unit is one 256-thread workgroup");
+constexpr int kBsiRows = 69 + kBsiRegSlices;  // |ebM|, circuit steps, finish, sum shares (rows below)
+constexpr int kRowB = kUnitWords + 16;  // row stride in bytes (a wave reads a row; the pad spreads banks)
+// fixed count rows: |ebM|; one per circuit step (slice i, predicate p); the finish;
+// the sum shares.  Fixed (not sequential) so every row offset is a compile-time
+// constant in the unrolled circuit; rows of skipped steps are never read.
+constexpr int kRowEbm = 0;
+__host__ __device__ constexpr int step_row(int i, int p) { return 1 + 2 * (31 - i) + p; }
+constexpr int kRowFin = 65;  // single op: fixed & EQ, then NEQ / GT / LT; RANGE: GE's, LE's fixed & EQ, result
+constexpr int kRowSum = 69;  // + slice
 
 // Wave-uniform type state of a circuit bitmap (the bits live elsewhere).  card 0
 // means absent: a present container is never empty (inputs hold >= 1 value,
@@ -309,39 +318,36 @@ __device__ __forceinline__ TB tb_op(const TB& x, const TB& y, int c, int& slow) 
 __device__ __forceinline__ void rec1(uint64_t z, int k, uint8_t* rows) {
   rows[k * kRowB + threadIdx.x] = (uint8_t)popc64(z);
 }
-// row sums of rows [0, nk) -> tot[], one wave per row (a 16 B vector per lane,
-// then a DPP reduction); ends with a barrier
-__device__ __forceinline__ void sum_rows1(const uint8_t* rows, int nk, int* tot) {
+// row sums of rows [0, nk), one thread per row (16 B reads, v_dot4 over the bytes),
+// written as this unit's partial counts: cnt[(row * kBsiUnits + unit) * stride].
+// Begins and ends with a barrier.
+__device__ __forceinline__ void sum_rows_unit(const uint8_t* rows, int nk, int* cnt, size_t stride) {
   lds_barrier();
-  const int lane = threadIdx.x & 63;
-  for (int r = threadIdx.x >> 6; r < nk; r += kNT1 / 64) {
-    const uint4 x = reinterpret_cast<const uint4*>(rows + r * kRowB)[lane];
-    // 16 bytes: sum the byte lanes pairwise into 16-bit fields (each <= 8 * 64)
-    const uint32_t a = (x.x & 0x00FF00FFu) + ((x.x >> 8) & 0x00FF00FFu) + (x.y & 0x00FF00FFu) +
-                       ((x.y >> 8) & 0x00FF00FFu) + (x.z & 0x00FF00FFu) + ((x.z >> 8) & 0x00FF00FFu) +
-                       (x.w & 0x00FF00FFu) + ((x.w >> 8) & 0x00FF00FFu);
-    const int c = wave_sum((int)((a & 0xFFFF) + (a >> 16)));
-    if (lane == 0) tot[r] = c;
+  const int r = threadIdx.x;
+  if (r < nk) {
+    const uint4* v = reinterpret_cast<const uint4*>(rows + r * kRowB);
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < kUnitWords / 16; j++) {
+      const uint4 x = v[j];
+      c = __builtin_amdgcn_udot4(x.x, 0x01010101u, c, false);
+      c = __builtin_amdgcn_udot4(x.y, 0x01010101u, c, false);
+      c = __builtin_amdgcn_udot4(x.z, 0x01010101u, c, false);
+      c = __builtin_amdgcn_udot4(x.w, 0x01010101u, c, false);
+    }
+    cnt[(size_t)r * kBsiUnits * stride] = (int)c;
   }
   lds_barrier();
 }
-// count k of this thread's key: the tables are transposed (row k of every key is
-// contiguous), so a wave reads 64 keys' count k with one coalesced load
-struct CountRows {
-  const int* p;  // cnts + key index
-  size_t stride;
-  __device__ __forceinline__ int operator()(int k) const { return p[(size_t)k * stride]; }
-};
-
 // Type replay of a step / finish, in the order of the bits.  c* are the exact
 // cardinalities of the bits (0 for an absent bitmap).
 struct CircuitT {
   TB gt, lt, eq;
   int cgt, clt, ceq;
 };
-__device__ __forceinline__ void types_step(int bit, const TB& s, CircuitT& z, int& k, const CountRows& tv,
-                                           int& slow) {
-  const int ct = tv(k++);
+template <class CNT>
+__device__ __forceinline__ void types_step(int bit, const TB& s, CircuitT& z, int row, const CNT& tv, int& slow) {
+  const int ct = tv(row);
   if (bit) {
     const TB t = tb_op<OPR_ANDNOT>(z.eq, s, ct, slow);
     z.lt = tb_op<OPR_OR>(z.lt, t, z.clt + ct, slow);
@@ -355,27 +361,28 @@ __device__ __forceinline__ void types_step(int bit, const TB& s, CircuitT& z, in
   }
   z.ceq -= ct;
 }
-// BSI/:453-467 on types: counted are fixed & EQ and the NEQ / GT / LT results;
-// LE / GE are disjoint unions
-__device__ __forceinline__ TB types_finish(int op, const TB& fixed, CircuitT& z, int& k, const CountRows& tv,
+// BSI/:453-467 on types: counted are fixed & EQ (row re) and the NEQ / GT / LT
+// results (row ro); LE / GE are disjoint unions
+template <class CNT>
+__device__ __forceinline__ TB types_finish(int op, const TB& fixed, CircuitT& z, int re, int ro, const CNT& tv,
                                            int& slow) {
-  const int ce = tv(k++);
+  const int ce = tv(re);
   z.eq = tb_op<OPR_AND>(fixed, z.eq, ce, slow);
   z.ceq = ce;
   switch (op) {
     case BSI_EQ: return z.eq;
-    case BSI_NEQ: return tb_op<OPR_ANDNOT>(fixed, z.eq, tv(k++), slow);
-    case BSI_GT: return tb_op<OPR_AND>(z.gt, fixed, tv(k++), slow);
-    case BSI_LT: return tb_op<OPR_AND>(z.lt, fixed, tv(k++), slow);
+    case BSI_NEQ: return tb_op<OPR_ANDNOT>(fixed, z.eq, tv(ro), slow);
+    case BSI_GT: return tb_op<OPR_AND>(z.gt, fixed, tv(ro), slow);
+    case BSI_LT: return tb_op<OPR_AND>(z.lt, fixed, tv(ro), slow);
     case BSI_LE: return tb_op<OPR_OR>(z.lt, z.eq, z.clt + ce, slow);
     default: return tb_op<OPR_OR>(z.gt, z.eq, z.cgt + ce, slow);  // GE
   }
 }
-// the same on bits (thread's word), recording the counted steps
-__device__ __forceinline__ uint64_t bits_finish1(int op, uint64_t fixed, uint64_t gt, uint64_t lt, uint64_t& eq, int& k,
-                                                 uint8_t* rows) {
+// the same on bits (this thread's word); counted: fixed & EQ (row re), NEQ / GT / LT (row ro)
+__device__ __forceinline__ uint64_t bits_finish1(int op, uint64_t fixed, uint64_t gt, uint64_t lt, uint64_t& eq, int re,
+                                                 int ro, uint8_t* rows) {
   eq &= fixed;
-  rec1(eq, k++, rows);
+  rec1(eq, re, rows);
   uint64_t out;
   switch (op) {
     case BSI_EQ: return eq;
@@ -385,145 +392,32 @@ __device__ __forceinline__ uint64_t bits_finish1(int op, uint64_t fixed, uint64_
     case BSI_LE: return lt | eq;
     default: return gt | eq;  // GE
   }
-  rec1(out, k++, rows);
+  rec1(out, ro, rows);
   return out;
 }
 
-// wave-uniform (SGPR) copy of a type state
-__device__ __forceinline__ TB tb_uni(const TB& x) {
-  return TB{(int)uni((uint32_t)x.kind), (int)uni((uint32_t)x.card), (int)uni((uint32_t)x.src), 0};
-}
-
-// Thread t's word of a container; non-bitmap ones through the 8 KiB LDS scratch `lds`:
-// arrays scattered; runs as toggles (run start, end + 1) whose prefix XOR is
-// taken inside each word and carried across words by a workgroup parity scan
-// (wpar: 16 ints).  All threads; contains barriers.
-__device__ __forceinline__ uint64_t mat_word1(const CDesc& d, const uint8_t* payload, uint32_t* lds, int* wpar) {
-  const int t = threadIdx.x;
+// Word w of a container: a bitmap directly, arrays / runs through the 8 KiB LDS
+// scratch (the whole container, 256-thread helpers).  All threads; barriers.
+__device__ __forceinline__ uint64_t mat_unit_word(const CDesc& d, const uint8_t* payload, uint32_t* lds, int* q,
+                                                  int w) {
   const uint8_t* slot = payload + d.slot;
-  if (d.kind == DK_B) return reinterpret_cast<const uint64_t*>(slot)[t];
+  if (d.kind == DK_B) return reinterpret_cast<const uint64_t*>(slot)[w];
   lds_barrier();
-  reinterpret_cast<uint64_t*>(lds)[t] = 0;
+  lds_clear(lds);
   lds_barrier();
   if (d.kind == DK_A) {
-    const int card = (int)d.card;
-    const int nvec = (card + 7) >> 3;
-    const uint4* v4 = reinterpret_cast<const uint4*>(slot);
-    for (int i = t; i < nvec; i += kNT1) {
-      const uint4 v = v4[i];
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        if (8 * i + j < card) {
-          const uint32_t x = (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFF;
-          atomicOr(&lds[x >> 5], 1u << (x & 31));
-        }
-      }
-    }
+    lds_scatter_array(lds, reinterpret_cast<const uint16_t*>(slot), (int)d.card);
     lds_barrier();
-    return reinterpret_cast<const uint64_t*>(lds)[t];
+  } else {
+    lds_or_runs(lds, reinterpret_cast<const uint32_t*>(slot + 4), *reinterpret_cast<const uint16_t*>(slot + 2), q);
   }
-  const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
-  const uint32_t* pairs = reinterpret_cast<const uint32_t*>(slot + 4);
-  for (int i = t; i < nr; i += kNT1) {
-    const uint32_t p = pairs[i];
-    const uint32_t st = p & 0xFFFF, e1 = st + (p >> 16) + 1;
-    atomicXor(&lds[st >> 5], 1u << (st & 31));
-    if (e1 < 65536) atomicXor(&lds[e1 >> 5], 1u << (e1 & 31));
-  }
+  const uint64_t x = reinterpret_cast<const uint64_t*>(lds)[w];
   lds_barrier();
-  uint64_t w = reinterpret_cast<const uint64_t*>(lds)[t];
-  const uint32_t par = (uint32_t)popc64(w) & 1u;
-  w = prefix_xor64(w);
-  const uint64_t m = __ballot(par);
-  const int lane = t & 63, wv = t >> 6;
-  uint32_t c = (uint32_t)__popcll(m & ((1ull << lane) - 1)) & 1u;
-  if (lane == 0) wpar[wv] = __popcll(m) & 1;
-  lds_barrier();
-  for (int j = 0; j < wv; j++) c ^= (uint32_t)wpar[j];
-  lds_barrier();
-  return c ? ~w : w;
+  return x;
 }
 
-// Diagnostic build only (-DRBG_BSI_STAMPS=1): per-phase shader-clock totals of
-// k_bsi_reg (thread 0 of every workgroup), read back with rbg_debug_stamps when
-// RBG_DEBUG_BSI is set.
-#if RBG_BSI_STAMPS
-__device__ unsigned long long g_bsi_stamp[20];
-#define BST_DECL                                   \
-  uint64_t bst_prev = __builtin_amdgcn_s_memtime(); \
-  uint64_t bst[10] = {};
-#define BST(ph)                                            \
-  do {                                                     \
-    const uint64_t bst_now = __builtin_amdgcn_s_memtime(); \
-    bst[ph] += bst_now - bst_prev;                         \
-    bst_prev = bst_now;                                    \
-  } while (0)
-#define BST_FLUSH()                                                                          \
-  do {                                                                                       \
-    if (threadIdx.x == 0)                                                                    \
-      for (int i_ = 0; i_ < 10; i_++) atomicAdd(&g_bsi_stamp[i_], (unsigned long long)bst[i_]); \
-  } while (0)
-void debug_bsi_stamps(uint64_t* out20, bool reset) {
-  (void)hipDeviceSynchronize();
-  (void)hipMemcpyFromSymbol(out20, HIP_SYMBOL(g_bsi_stamp), 20 * 8, 0, hipMemcpyDeviceToHost);
-  if (reset) {
-    unsigned long long z[20] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bsi_stamp), z, sizeof(z), 0, hipMemcpyHostToDevice);
-  }
-}
-#else
-#define BST_DECL
-#define BST(ph) \
-  do {          \
-  } while (0)
-#define BST_FLUSH() \
-  do {              \
-  } while (0)
 void debug_bsi_stamps(uint64_t* out20, bool) {
   for (int i = 0; i < 20; i++) out20[i] = 0;
-}
-#endif
-
-// Per-key LDS state of k_bsi_reg (double-buffered: the next key's is set up while
-// the current key finishes)
-struct BsiKeyBuf {
-  int pos[kBsiMaxInputs];  // desc index of each input's container of the key, or -1
-  TB stype[kBsiRegSlices];
-  uint64_t sslot[kBsiRegSlices];
-  uint32_t mask;  // slices that are bitmap containers
-};
-
-// positions of the key's inputs and its slice descriptors (wave 0, one lane per
-// slice: one memory round trip); returns the bitmap-slice mask.  Contains barriers.
-__device__ __forceinline__ uint32_t bsi_key_setup(const Task& tk, const WideArgs& A, int nb, BsiKeyBuf& kb) {
-  const uint32_t s = uni((uint32_t)tk.a), n = uni((uint32_t)tk.b);
-  if ((int)threadIdx.x < kBsiMaxInputs) kb.pos[threadIdx.x] = -1;
-  lds_barrier();
-  for (uint32_t j = threadIdx.x; j < n; j += kNT1) kb.pos[A.bm[s + j]] = (int)(s + j);
-  lds_barrier();
-  if (threadIdx.x < 64) {
-    const int i = threadIdx.x;
-    const int p = i < nb ? kb.pos[1 + i] : -1;
-    CDesc d{};
-    if (p >= 0) d = A.desc[p];
-    if (i < kBsiRegSlices) {
-      kb.stype[i] = p >= 0 ? TB{d.kind, (int)d.card, p, 0} : tb_absent();
-      kb.sslot[i] = d.slot;
-    }
-    const uint64_t m = __ballot(p >= 0 && d.kind == DK_B);
-    if (i == 0) kb.mask = (uint32_t)m;
-  }
-  lds_barrier();
-  return uni(kb.mask);
-}
-
-// bitmap slices straight to registers (thread t: word t); all loads of the key in flight at once
-__device__ __forceinline__ void bsi_issue_loads(const WideArgs& A, const BsiKeyBuf& kb, uint32_t mask,
-                                                uint64_t sl[kBsiRegSlices]) {
-#pragma unroll
-  for (int i = 0; i < kBsiRegSlices; i++)
-    sl[i] = ((mask >> i) & 1) ? reinterpret_cast<const uint64_t*>(A.payload + kb.sslot[i])[threadIdx.x] : 0;
 }
 
 // task record of a result written by k_bsi_reg / k_bsi_defer (wg_place's record)
@@ -541,57 +435,104 @@ __device__ __forceinline__ void bsi_rec(uint32_t t, const OutCtx& oc, bool keep,
   oc.recs[t] = r;
 }
 
-// compare ops (BSI_EQ .. BSI_RANGE) with nbits <= kBsiRegSlices: one 1,024-thread
-// workgroup per key computes the bits and the counts; k_bsi_types (a wave per key)
-// replays the types and writes the records.  cnts: kBsiCnt rows of one int per task; kin:
-// kBsiKin input types per task (slices, ebM, the fixed found set).
 constexpr int kBsiCnt = 128;
 constexpr int kBsiKin = kBsiRegSlices + 2;
 static_assert(kBsiRows <= kBsiCnt, "count rows");
-__global__ __launch_bounds__(1024, 1) void k_bsi_reg(const Task* __restrict__ tasks,
-                                                     const uint32_t* __restrict__ n_tasks, WideArgs A, BsiArgs P,
-                                                     OutCtx oc, bool want_sum, int* __restrict__ cnts,
-                                                     TB* __restrict__ kin, size_t tstride) {
-  __shared__ __align__(16) uint32_t tmp[2048];
-  __shared__ __align__(16) uint8_t rows[kBsiRows * kRowB];
-  __shared__ int tot[128];
-  __shared__ BsiKeyBuf kbuf[2];
-  __shared__ int wpar[16];
+
+// One input of a key (16 B): its container's slot, cardinality and kind, or absent
+// (didx < 0).  k_bsi_table writes a row of kBsiKin per task, indexed by input
+// (ebM, bA[0..nb-1], foundSet), so a wave of k_bsi_reg reads a key's inputs with one
+// load (lane = input) and needs no search of the key segment.
+struct BsiIn {
+  uint64_t slot;
+  uint32_t card_kind;  // card | kind << 24
+  int32_t didx;        // desc index, -1 when the key has no container of this input
+};
+__global__ __launch_bounds__(256) void k_bsi_table(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                   WideArgs A, BsiIn* __restrict__ table) {
   const uint32_t nt = *n_tasks;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nt) return;
+  const Task tk = tasks[t];
+  BsiIn* row = table + (size_t)t * kBsiKin;
+  for (int i = 0; i < kBsiKin; i++) row[i] = BsiIn{0, 0, -1};
+  for (uint32_t j = 0; j < (uint32_t)tk.b; j++) {
+    const uint32_t p = (uint32_t)tk.a + j;
+    const uint32_t b = A.bm[p];
+    if (b < (uint32_t)kBsiKin) {
+      const CDesc d = A.desc[p];
+      row[b] = BsiIn{d.slot, d.card | ((uint32_t)d.kind << 24), (int32_t)p};
+    }
+  }
+}
+
+// Word w of a key's input from its table entry: a full container needs no memory
+// access, a bitmap one load, arrays / runs the LDS scratch (all threads; barriers).
+__device__ __forceinline__ uint64_t in_word(uint64_t slot, uint32_t card_kind, int32_t didx, const WideArgs& A,
+                                           uint32_t* lds, int* q, int w) {
+  if (didx < 0) return 0;
+  const uint32_t card = card_kind & 0xFFFFFF, kind = card_kind >> 24;
+  if (card == 65536) return ~0ull;
+  if (kind == DK_B) return reinterpret_cast<const uint64_t*>(A.payload + slot)[w];
+  return mat_unit_word(A.desc[didx], A.payload, lds, q, w);
+}
+
+// compare ops (BSI_EQ .. BSI_RANGE) with nbits <= kBsiRegSlices.  cnts: per count row,
+// kBsiUnits partial rows of one int per task; kin: kBsiKin rows of one input type per
+// task (slices, ebM, the fixed found set); both transposed with row stride `tstride`.
+__global__ __launch_bounds__(256, RBG_BSI_WAVES) void k_bsi_reg(const Task* __restrict__ tasks,
+                                                                const uint32_t* __restrict__ n_tasks,
+                                                 WideArgs A, BsiArgs P, OutCtx oc, bool want_sum,
+                                                 const BsiIn* __restrict__ table, int* __restrict__ cnts,
+                                                 TB* __restrict__ kin, size_t tstride) {
+  // the 8 KiB scratch for array / run inputs aliases the count rows: inputs are
+  // materialised before the circuit writes the rows, and after the last unit's sums
+  __shared__ __align__(16) uint8_t rows[kBsiRows * kRowB];
+  static_assert(kBsiRows * kRowB >= 8192, "scratch bitmap inside the rows");
+  uint32_t* tmp = reinterpret_cast<uint32_t*>(rows);
+  __shared__ int q[257];
+  const uint64_t nunits = (uint64_t)*n_tasks * kBsiUnits;
   const int nb = P.nbits;
   const bool two = P.op == BSI_RANGE;
-  const int tid = threadIdx.x;
-  uint32_t t = blockIdx.x;
-  if (t >= nt) return;
-  uint64_t sl[kBsiRegSlices];
-  int cb = 0;
-  Task tk = tasks[t];
-  bsi_issue_loads(A, kbuf[0], bsi_key_setup(tk, A, nb, kbuf[0]), sl);
-  BST_DECL
-  while (true) {
-    BsiKeyBuf& kb = kbuf[cb];
-    // the next key's positions and slice descriptors, while this key's slices load
-    const uint32_t tn = t + gridDim.x;
-    Task tkn;
-    uint32_t maskn = 0;
-    if (tn < nt) {
-      tkn = tasks[tn];
-      maskn = bsi_key_setup(tkn, A, nb, kbuf[cb ^ 1]);
-    }
-    const uint64_t ebm = mat_word1(A.desc[kb.pos[0]], A.payload, tmp, wpar);  // a task exists only where ebM has the key
-    uint64_t fixed = ebm;
-    if (P.has_found) fixed = kb.pos[nb + 1] >= 0 ? mat_word1(A.desc[kb.pos[nb + 1]], A.payload, tmp, wpar) : 0;
-    BST(0);
-    // array / run slices through the LDS scratch
+  const int tid = threadIdx.x, lane = tid & 63;
+  uint64_t wi = blockIdx.x;
+  if (wi >= nunits) return;
+  // this unit's key inputs: lane i holds input i (0 = ebM, 1 + x = bA[x], nb + 1 = foundSet);
+  // the next unit's row is requested while this unit runs
+  BsiIn e = lane < kBsiKin ? table[(wi / kBsiUnits) * kBsiKin + lane] : BsiIn{0, 0, -1};
+  for (;;) {
+    const uint32_t t = (uint32_t)(wi / kBsiUnits), u = (uint32_t)(wi % kBsiUnits);
+    const uint64_t wn = wi + gridDim.x;
+    BsiIn en{0, 0, -1};
+    if (wn < nunits && lane < kBsiKin) en = table[(wn / kBsiUnits) * kBsiKin + lane];
+    const int w = (int)(u * kUnitWords) + tid;  // this thread's container word
+    // 1. every bitmap slice word of the unit requested at once (slots through readlane)
+    uint64_t sl[kBsiRegSlices];
+    const uint32_t lo = (uint32_t)e.slot, hi = (uint32_t)(e.slot >> 32);
+    const bool bmp = e.didx >= 0 && (e.card_kind >> 24) == DK_B && (e.card_kind & 0xFFFFFF) != 65536;
+    const uint64_t bmask = __ballot(bmp && lane >= 1 && lane <= nb) >> 1;  // slice x at bit x
 #pragma unroll
-    for (int i = 0; i < kBsiRegSlices; i++) {
-      if (i < nb && kb.stype[i].card > 0 && kb.stype[i].kind != DK_B)
-        sl[i] = mat_word1(A.desc[kb.pos[1 + i]], A.payload, tmp, wpar);
+    for (int x = 0; x < kBsiRegSlices; x++) {
+      const uint64_t slot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, 1 + x) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 1 + x) << 32);
+      sl[x] = ((bmask >> x) & 1) ? reinterpret_cast<const uint64_t*>(A.payload + slot)[w] : 0;
     }
-    // 2. bits of the whole circuit
-    uint64_t eq0 = ebm, gt0 = 0, lt0 = 0, eq1 = ebm, gt1 = 0, lt1 = 0, res;
-    int k = 0;
-    rec1(ebm, k++, rows);  // |ebM| of the bits: the start of the derived cardinalities
+    auto input_word = [&](int i) -> uint64_t {
+      const uint64_t slot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, i) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, i) << 32);
+      return in_word(slot, (uint32_t)__builtin_amdgcn_readlane((int)e.card_kind, i),
+                     __builtin_amdgcn_readlane(e.didx, i), A, tmp, q, w);
+    };
+    const uint64_t ebm = input_word(0);  // a task exists only where ebM has the key
+    const uint64_t fixed = P.has_found ? input_word(nb + 1) : ebm;
+#pragma unroll
+    for (int x = 0; x < kBsiRegSlices; x++) {  // full, array and run slices
+      if (x < nb && !((bmask >> x) & 1) && __builtin_amdgcn_readlane(e.didx, 1 + x) >= 0) sl[x] = input_word(1 + x);
+    }
+    // 2. bits of the whole circuit; each thread's share of every count to LDS.  GT is
+    // not tracked: GT, LT and EQ partition ebM, so GT = ebM ^ LT ^ EQ at the end.
+    uint64_t eq0 = ebm, lt0 = 0, eq1 = ebm, lt1 = 0, res;
+    rec1(ebm, kRowEbm, rows);  // |ebM| of the bits: the start of the derived cardinalities
     // predicate bits i = 31 .. 0 as the top bit of running copies; the asm keeps the
     // compiler from precomputing 64 per-step flags (SGPR spills)
     uint32_t p0 = P.pred0, p1 = P.pred1;
@@ -600,19 +541,29 @@ __global__ __launch_bounds__(1024, 1) void k_bsi_reg(const Task* __restrict__ ta
     for (int i = kBsiRegSlices - 1; i >= 0; i--) {
       asm volatile("" : "+s"(p0), "+s"(p1), "+s"(live));
       if (live <= 0) {
-        const uint64_t m0 = (uint64_t)(int64_t)((int32_t)p0 >> 31);  // all ones iff bit i of pred0
-        const uint64_t tv = eq0 & (sl[i] ^ m0);                     // EQ & ~bA[i] / EQ & bA[i]
-        rec1(tv, k++, rows);
-        lt0 |= tv & m0;
-        gt0 |= tv & ~m0;
-        eq0 ^= tv;
+        // bit i of the predicate (the top bit of the opaque running copy) picks the
+        // step's form with a scalar branch
+        if ((int32_t)p0 < 0) {  // LT |= EQ & ~bA[i]; EQ &= bA[i]
+          const uint64_t tv = eq0 & ~sl[i];
+          rec1(tv, step_row(i, 0), rows);
+          lt0 |= tv;
+          eq0 ^= tv;
+        } else {  // GT |= EQ & bA[i]; EQ &= ~bA[i]
+          const uint64_t tv = eq0 & sl[i];
+          rec1(tv, step_row(i, 0), rows);
+          eq0 ^= tv;
+        }
         if (two) {
-          const uint64_t m1 = (uint64_t)(int64_t)((int32_t)p1 >> 31);
-          const uint64_t tw = eq1 & (sl[i] ^ m1);
-          rec1(tw, k++, rows);
-          lt1 |= tw & m1;
-          gt1 |= tw & ~m1;
-          eq1 ^= tw;
+          if ((int32_t)p1 < 0) {
+            const uint64_t tw = eq1 & ~sl[i];
+            rec1(tw, step_row(i, 1), rows);
+            lt1 |= tw;
+            eq1 ^= tw;
+          } else {
+            const uint64_t tw = eq1 & sl[i];
+            rec1(tw, step_row(i, 1), rows);
+            eq1 ^= tw;
+          }
         }
       }
       p0 <<= 1;
@@ -620,113 +571,99 @@ __global__ __launch_bounds__(1024, 1) void k_bsi_reg(const Task* __restrict__ ta
       live--;
     }
     if (two) {  // RANGE = and(GE(start), LE(end)), BSI/:503-507
-      const uint64_t left = bits_finish1(BSI_GE, fixed, gt0, lt0, eq0, k, rows);
-      const uint64_t right = bits_finish1(BSI_LE, fixed, gt1, lt1, eq1, k, rows);
+      const uint64_t left = bits_finish1(BSI_GE, fixed, ebm ^ lt0 ^ eq0, lt0, eq0, kRowFin, 0, rows);
+      const uint64_t right = bits_finish1(BSI_LE, fixed, ebm ^ lt1 ^ eq1, lt1, eq1, kRowFin + 1, 0, rows);
       res = left & right;
-      rec1(res, k++, rows);
+      rec1(res, kRowFin + 2, rows);
     } else {
-      res = bits_finish1(P.op, fixed, gt0, lt0, eq0, k, rows);
+      res = bits_finish1(P.op, fixed, ebm ^ lt0 ^ eq0, lt0, eq0, kRowFin, kRowFin + 1, rows);
     }
-    BST(1);
-    // 4. sum shares |bA[x] & result| (an absent result has no bits: all zero)
+    // sum shares |bA[x] & result| (an absent result has no bits: all zero)
     if (want_sum) {
 #pragma unroll
       for (int x = 0; x < kBsiRegSlices; x++)
-        if (x < nb) rec1(sl[x] & res, k + x, rows);
+        if (x < nb) rec1(sl[x] & res, kRowSum + x, rows);
     }
-    BST(2);
-    // the slices of this key are dead: the next key's start loading now
-    if (tn < nt) bsi_issue_loads(A, kbuf[cb ^ 1], maskn, sl);
-    BST(3);
-    // the result bits to the task's scratch slot: the container itself when it is a
-    // bitmap, else the input k_bsi_types stages it from
-    reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[tid] = res;
-    sum_rows1(rows, k + (want_sum ? nb : 0), tot);
-    BST(4);
-    // counts and the input types of the key for k_bsi_types (transposed: row r of
-    // every key contiguous)
-    if (tid < k + (want_sum ? nb : 0)) cnts[(size_t)tid * tstride + t] = tot[tid];
-    if (tid >= 64 && tid < 64 + kBsiKin) {
-      const int i = tid - 64;
-      TB x = tb_absent();
-      if (i < kBsiRegSlices) {
-        x = kb.stype[i];
-      } else {
-        const int p = i == kBsiRegSlices ? kb.pos[0] : (P.has_found ? kb.pos[nb + 1] : kb.pos[0]);
-        if (p >= 0) {
-          const CDesc d = A.desc[p];
-          x = TB{d.kind, (int)d.card, p, 0};
-        }
-      }
-      kin[(size_t)i * tstride + t] = x;
+    // this unit's result words to the task's scratch slot (the container itself when
+    // it is a bitmap, else the input k_bsi_defer stages it from)
+    reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[w] = res;
+    sum_rows_unit(rows, want_sum ? kRowSum + nb : kRowSum, cnts + (size_t)u * tstride + t, tstride);
+    if (u == 0 && tid < kBsiKin) {  // the key's input types, for k_bsi_types
+      const int i = tid == kBsiRegSlices ? 0 : tid == kBsiRegSlices + 1 ? (P.has_found ? nb + 1 : 0) : 1 + tid;
+      const BsiIn x = table[(size_t)t * kBsiKin + (i < kBsiKin ? i : 0)];
+      const bool present = x.didx >= 0 && (tid >= kBsiRegSlices || tid < nb);
+      kin[(size_t)tid * tstride + t] =
+          present ? TB{(int)(x.card_kind >> 24), (int)(x.card_kind & 0xFFFFFF), x.didx, 0} : tb_absent();
     }
-    BST(5);
-    if (tn >= nt) break;
-    lds_barrier();
-    t = tn;
-    tk = tkn;
-    cb ^= 1;
+    if (wn >= nunits) break;
+    wi = wn;
+    e = en;
   }
-  BST_FLUSH();
 }
 
-// w_place for k_bsi_types: a staged result (LDS) to the task's scratch slot and its record
-__device__ __forceinline__ void bsi_wave_place(uint32_t t, const uint32_t* lds, uint32_t len, uint32_t card,
-                                               uint32_t key, int kind, const OutCtx& oc) {
-  uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
-  copy_lds_to_global<64>(slot, lds, len, lane_id());
-  if (lane_id() == 0) bsi_rec(t, oc, true, slot, len, card, key, kind);
-}
-
-// Types of the keys k_bsi_reg computed, one THREAD per key: the reference's type
-// rule of every step is replayed from the counts (branch-free selects; the counts
-// and input types are read as transposed rows, coalesced across the keys of a
-// wave), then the result record.  A bitmap result is already in the scratch slot;
-// array / run results (staged from it by a wave) and keys whose replay needs a run
-// count go to k_bsi_defer.  Sums: per slice one wave reduction, one atomic.
-__global__ __launch_bounds__(256) void k_bsi_types(const Task* __restrict__ tasks,
-                                                   const uint32_t* __restrict__ n_tasks, WideArgs A, BsiArgs P,
-                                                   OutCtx oc, unsigned long long* __restrict__ sums,
-                                                   const int* __restrict__ cnts, const TB* __restrict__ kin,
-                                                   size_t tstride, uint32_t* __restrict__ defer) {
+// Types of the keys k_bsi_reg computed, one THREAD per key (64-thread blocks): the
+// key's counts (the units' partials added) and input types are first staged in LDS
+// -- every load independent, all in flight together -- then the reference's type
+// rule of every step is replayed from them with branch-free selects, and the result
+// record written.  A bitmap result is already in the scratch slot; array / run
+// results (staged from it) and keys whose replay needs a run count go to
+// k_bsi_defer.  Sums: per slice one wave reduction, one atomic.
+struct LdsCounts {
+  const int* col;  // this lane's column of the staged counts (row stride 64)
+  __device__ __forceinline__ int operator()(int r) const { return col[r * 64]; }
+};
+__global__ __launch_bounds__(64) void k_bsi_types(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                  WideArgs A, BsiArgs P, OutCtx oc,
+                                                  unsigned long long* __restrict__ sums, const int* __restrict__ cnts,
+                                                  const TB* __restrict__ kin, size_t tstride,
+                                                  uint32_t* __restrict__ defer) {
+  __shared__ int lc[kBsiRows * 64];
+  __shared__ TB lk[kBsiKin * 64];
   const uint32_t nt = *n_tasks;
   const int nb = P.nbits;
   const bool two = P.op == BSI_RANGE;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (uni(blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) >= nt) return;  // whole waves past the end
+  const int lane = threadIdx.x;
+  const uint32_t t = blockIdx.x * 64 + lane;
+  if (uni(blockIdx.x * 64) >= nt) return;
   const bool live = t < nt;
   const uint32_t tt = live ? t : 0;
-  const CountRows tv{cnts + tt, tstride};
-  const TB ebmT = kin[(size_t)kBsiRegSlices * tstride + tt];
-  const TB fixT = kin[(size_t)(kBsiRegSlices + 1) * tstride + tt];
+#pragma unroll 8
+  for (int r = 0; r < kBsiRows; r++) {
+    int c = 0;
+#pragma unroll
+    for (int u = 0; u < kBsiUnits; u++) c += cnts[((size_t)r * kBsiUnits + u) * tstride + tt];
+    lc[r * 64 + lane] = c;
+  }
+#pragma unroll 8
+  for (int i = 0; i < kBsiKin; i++) lk[i * 64 + lane] = kin[(size_t)i * tstride + tt];
+  const LdsCounts tv{lc + lane};
+  const TB ebmT = lk[kBsiRegSlices * 64 + lane];
+  const TB fixT = lk[(kBsiRegSlices + 1) * 64 + lane];
   int slow = 0;
-  int kk = 0;
-  const int cebm = tv(kk++);
-  CircuitT z0{tb_absent(), tb_absent(), ebmT, 0, 0, cebm}, z1 = z0;
+  CircuitT z0{tb_absent(), tb_absent(), ebmT, 0, 0, tv(kRowEbm)}, z1 = z0;
 #pragma unroll 1
   for (int i = nb - 1; i >= 0; i--) {
-    const TB sT = kin[(size_t)i * tstride + tt];
-    types_step((P.pred0 >> i) & 1, sT, z0, kk, tv, slow);
-    if (two) types_step((P.pred1 >> i) & 1, sT, z1, kk, tv, slow);
+    const TB sT = lk[i * 64 + lane];
+    types_step((P.pred0 >> i) & 1, sT, z0, step_row(i, 0), tv, slow);
+    if (two) types_step((P.pred1 >> i) & 1, sT, z1, step_row(i, 1), tv, slow);
   }
   TB rt;
   if (two) {
-    const TB left = types_finish(BSI_GE, fixT, z0, kk, tv, slow);
-    const TB right = types_finish(BSI_LE, fixT, z1, kk, tv, slow);
-    rt = tb_op<OPR_AND>(left, right, tv(kk++), slow);
+    const TB left = types_finish(BSI_GE, fixT, z0, kRowFin, 0, tv, slow);
+    const TB right = types_finish(BSI_LE, fixT, z1, kRowFin + 1, 0, tv, slow);
+    rt = tb_op<OPR_AND>(left, right, tv(kRowFin + 2), slow);
   } else {
-    rt = types_finish(P.op, fixT, z0, kk, tv, slow);
+    rt = types_finish(P.op, fixT, z0, kRowFin, kRowFin + 1, tv, slow);
   }
   const bool ok = live && !slow;
-  // sums: the sum shares follow the counted steps (kk of them); one atomic per slice per wave
   if (sums) {
     const bool add = ok && rt.card > 0;
     for (int x = 0; x < nb; x++) {
-      const int c = wave_sum(add ? tv(kk + x) : 0);
-      if ((threadIdx.x & 63) == 0 && c) atomicAdd(&sums[x], (unsigned long long)(uint32_t)c);
+      const int c = wave_sum(add ? tv(kRowSum + x) : 0);
+      if (lane == 0 && c) atomicAdd(&sums[x], (unsigned long long)(uint32_t)c);
     }
     const int cc = wave_sum(add ? rt.card : 0);
-    if ((threadIdx.x & 63) == 0 && cc) atomicAdd(&sums[kBsiMaxInputs], (unsigned long long)(uint32_t)cc);
+    if (lane == 0 && cc) atomicAdd(&sums[kBsiMaxInputs], (unsigned long long)(uint32_t)cc);
   }
   if (!live) return;
   if (slow) {  // a step's type needs its run count: k_bsi_defer redoes this key
@@ -788,11 +725,14 @@ void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, 
                 unsigned long long* sums, BsiScratch* sc) {
   if (p.op <= BSI_RANGE && p.nbits <= kBsiRegSlices && sc) {
     (void)hipMemsetAsync(sc->defer, 0, 4, s);
-    const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_reg)));
-    hipLaunchKernelGGL(k_bsi_reg, dim3(g), dim3(kNT1), 0, s, tasks, nt, args, p, oc, sums != nullptr, sc->cnts,
+    hipLaunchKernelGGL(k_bsi_table, dim3((unsigned)((sc->stride + 255) / 256)), dim3(256), 0, s, tasks, nt, args,
+                       reinterpret_cast<BsiIn*>(sc->table));
+    const int g = std::max(1, std::min(grid * kBsiUnits, resident_grid((const void*)&k_bsi_reg)));
+    hipLaunchKernelGGL(k_bsi_reg, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc, sums != nullptr,
+                       reinterpret_cast<const BsiIn*>(sc->table), sc->cnts,
                        reinterpret_cast<TB*>(sc->kin), sc->stride);
-    const int g2 = (int)((sc->stride + 255) / 256);
-    hipLaunchKernelGGL(k_bsi_types, dim3(g2), dim3(256), 0, s, tasks, nt, args, p, oc, sums, sc->cnts,
+    const int g2 = (int)((sc->stride + 63) / 64);
+    hipLaunchKernelGGL(k_bsi_types, dim3(g2), dim3(64), 0, s, tasks, nt, args, p, oc, sums, sc->cnts,
                        reinterpret_cast<const TB*>(sc->kin), sc->stride, sc->defer);
     const int g3 = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_defer)));
     hipLaunchKernelGGL(k_bsi_defer, dim3(g3), dim3(256), 0, s, tasks, sc->defer, args, p, oc, sums);

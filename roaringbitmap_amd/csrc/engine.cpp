@@ -129,7 +129,7 @@ struct Ctx {
   std::vector<std::unique_ptr<Batch>> batches;
   uint64_t* zlb = nullptr;    // look-back state the next plan kernel zeroes (null: none)
   uint64_t* ztile = nullptr;
-  DevBuf bsi_defer, bsi_cnts, bsi_kin;  // scratch of the register-resident BSI kernels
+  DevBuf bsi_defer, bsi_cnts, bsi_kin, bsi_table;  // scratch of the register-resident BSI kernels
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   DevBuf order;                     // horizontal_*: chain order of every key segment
@@ -906,9 +906,10 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
   BsiScratch sc{};
   if (mode >= 0 && mode <= BSI_RANGE) {
     CHK(c->bsi_defer.ensure(4 * (ub + 1)));
-    CHK(c->bsi_cnts.ensure((size_t)512 * ub));
+    CHK(c->bsi_cnts.ensure((size_t)4 * 128 * 4 * ub));  // count rows (< 128) x 4 units
     CHK(c->bsi_kin.ensure((size_t)16 * 34 * ub));
-    sc = BsiScratch{c->bsi_defer.as<uint32_t>(), c->bsi_cnts.as<int>(), c->bsi_kin.p, ub};
+    CHK(c->bsi_table.ensure((size_t)16 * 34 * ub));
+    sc = BsiScratch{c->bsi_defer.as<uint32_t>(), c->bsi_cnts.as<int>(), c->bsi_kin.p, ub, c->bsi_table.p};
   }
   launch_bsi(s, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, p, oc,
              want_sum ? c->bsi_sums.as<unsigned long long>() : nullptr, sc.defer ? &sc : nullptr);

@@ -102,13 +102,14 @@ void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm,
 // sums: kBsiMaxInputs + 1 u64 (per-slice |bA[x] & found|, then the found count); null = no sum
 // scratch of the register-resident compare kernels (bsi.hip), per task of the op
 // (stride = task capacity; the tables are transposed, row-major over the tasks):
-// defer: 1 + stride u32, cnts: 128 rows of stride ints, kin: 34 rows of stride x 16 B.
+// defer: 1 + stride u32, cnts: 128 x 4 rows of stride ints, kin: 34 rows of stride x 16 B.
 // Null: the streamed kernel only.
 struct BsiScratch {
   uint32_t* defer;
   int* cnts;
   void* kin;
   size_t stride;
+  void* table;  // 34 x 16 B per task: each input's container of the key
 };
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
                 unsigned long long* sums, BsiScratch* sc);
