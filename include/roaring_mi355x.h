@@ -75,10 +75,15 @@ enum { RBG_WIDE_AND = 0, RBG_WIDE_OR = 1, RBG_WIDE_XOR = 2, RBG_WIDE_AND_ITER = 
  *                               RB/buffer/BufferFastAggregation.java:810-817,896-898 (lazyor chain)
  *   RBG_WIDE_HORIZONTAL_OR      FastAggregation.horizontal_or(List / RoaringBitmap...) RB/FastAggregation.java:124-231
  *   RBG_WIDE_HORIZONTAL_XOR     FastAggregation.horizontal_xor(RoaringBitmap...) :243-289
+ *   RBG_WIDE_PQ_OR              FastAggregation.priorityqueue_or(Iterator / RoaringBitmap...) :677-781
+ *   RBG_WIDE_PQ_XOR             FastAggregation.priorityqueue_xor(RoaringBitmap...) :790-812
  * The horizontal_* chain order is the poll order of the reference's container-pointer
- * priority queue, planned from the container table (keys and cardinalities). */
+ * priority queue, planned from the container table (keys and cardinalities).  The
+ * priorityqueue_* ops replay the reference's bitmap queue ordered by getLongSizeInBytes:
+ * N - 1 dependent whole-bitmap steps, one device pass over the union keys each (full key
+ * range only: the queue order depends on every key). */
        RBG_WIDE_PARALLEL_OR = 6, RBG_WIDE_PARALLEL_XOR = 7, RBG_WIDE_BUFFER_OR_MUTABLE = 8,
-       RBG_WIDE_HORIZONTAL_OR = 9, RBG_WIDE_HORIZONTAL_XOR = 10 };
+       RBG_WIDE_HORIZONTAL_OR = 9, RBG_WIDE_HORIZONTAL_XOR = 10, RBG_WIDE_PQ_OR = 11, RBG_WIDE_PQ_XOR = 12 };
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
 

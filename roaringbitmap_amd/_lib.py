@@ -20,7 +20,8 @@ RBG_ERR_OUT_OF_MEMORY = -5
 OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3}
 CARD_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
 WIDE_OP = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5, "parallel_or": 6,
-           "parallel_xor": 7, "buffer_or_mutable": 8, "horizontal_or": 9, "horizontal_xor": 10}
+           "parallel_xor": 7, "buffer_or_mutable": 8, "horizontal_or": 9, "horizontal_xor": 10,
+           "priorityqueue_or": 11, "priorityqueue_xor": 12}
 WIDE_CARD_OP = {"and": 0, "or": 1}
 
 

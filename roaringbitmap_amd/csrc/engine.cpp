@@ -713,6 +713,181 @@ static int horizontal_order(Ctx* c, Batch* B) {
   return RBG_OK;
 }
 
+// FastAggregation.priorityqueue_or / priorityqueue_xor (RB/FastAggregation.java:677-812).
+// The reference keeps a java.util.PriorityQueue of bitmap indices ordered by
+// (int)(sizes[a] - sizes[b]) over getLongSizeInBytes; the queue is replayed here with
+// the heap's own tie order, and every step is one device pass over the union keys
+// (pq.hip, launch_pq_step) whose result size is read back to order the queue.
+namespace {
+template <class Cmp>
+struct IntHeap {  // java.util.PriorityQueue with a comparator (OpenJDK siftUp / siftDown)
+  std::vector<int> q;
+  Cmp cmp;
+  explicit IntHeap(Cmp c) : cmp(c) {}
+  void add(int x) {
+    size_t k = q.size();
+    q.push_back(x);
+    while (k > 0) {
+      const size_t p = (k - 1) >> 1;
+      if (cmp(x, q[p]) >= 0) break;
+      q[k] = q[p];
+      k = p;
+    }
+    q[k] = x;
+  }
+  int poll() {
+    const int r = q[0];
+    const int x = q.back();
+    q.pop_back();
+    const size_t n = q.size();
+    if (n) {
+      size_t k = 0;
+      const size_t half = n >> 1;
+      while (k < half) {
+        size_t ch = 2 * k + 1;
+        if (ch + 1 < n && cmp(q[ch], q[ch + 1]) > 0) ch++;
+        if (cmp(x, q[ch]) <= 0) break;
+        q[k] = q[ch];
+        k = ch;
+      }
+      q[k] = x;
+    }
+    return r;
+  }
+};
+}  // namespace
+
+static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) {
+  if (key_lo != 0 || key_hi != kMaxKeys) {
+    set_err("priorityqueue aggregations need the full key range (the queue order depends on every key)");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  hipStream_t s = c->stream;
+  const size_t N = B->n_bm;
+  const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
+  OutCtx oc;
+  CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, false));
+  c->pending_src = {id};
+  c->mark(0);
+  // one task per union key (an empty aggregate has none: new RoaringBitmap())
+  launch_plan_wide(s, N ? 0 : 1, B->key_off.as<uint32_t>(), N ? (uint32_t)N : 0xFFFFFFFFu, 0, kMaxKeys,
+                   c->by_key.as<Task>(), c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile);
+  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
+                 c->ntasks.as<uint32_t>());
+  c->mark(1);
+  if (N) {
+    uint32_t h_nt = 0;
+    HIPCHK(hipMemcpyAsync(&h_nt, c->ntasks.p, 4, hipMemcpyDeviceToHost, s));
+    CHK(c->scalar.ensure(64));
+    std::vector<unsigned long long> leaf(N);
+    DevBuf dsz;
+    CHK(dsz.ensure(8 * N));
+    HIPCHK(hipMemsetAsync(dsz.p, 0, 8 * N, s));
+    launch_pq_leaf_sizes(s, B->desc.as<CDesc>(), B->bm.as<uint32_t>(), B->payload.as<uint8_t>(), B->n_ctr,
+                         dsz.as<unsigned long long>());
+    HIPCHK(hipMemcpyAsync(leaf.data(), dsz.p, 8 * N, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const PQArgs pa{B->desc.as<CDesc>(), B->bm.as<uint32_t>(), B->payload.as<uint8_t>()};
+    const int grid = grid_for(h_nt, 65536);
+    // temps: one state (16 B) + one 8 KiB set per union key; freed slots are reused
+    const size_t st_bytes = ((size_t)16 * h_nt + 255) & ~(size_t)255;
+    std::vector<std::unique_ptr<DevBuf>> pool;
+    std::vector<int> free_slots;
+    auto alloc = [&](PQRef* out) -> int {
+      int k;
+      if (!free_slots.empty()) {
+        k = free_slots.back();
+        free_slots.pop_back();
+      } else {
+        pool.emplace_back(new DevBuf());
+        k = (int)pool.size() - 1;
+        CHK(pool[k]->ensure(st_bytes + (size_t)8192 * h_nt));
+      }
+      uint8_t* p = pool[k]->as<uint8_t>();
+      *out = PQRef{-1 - k, reinterpret_cast<PQState*>(p), reinterpret_cast<uint64_t*>(p + st_bytes)};
+      return RBG_OK;
+    };
+    auto release = [&](const PQRef& r) {
+      if (r.leaf < 0) free_slots.push_back(-1 - r.leaf);
+    };
+    auto as_arg = [](PQRef r) {
+      if (r.leaf < 0) r.leaf = -1;
+      return r;
+    };
+    unsigned long long h_size = 0;
+    auto step = [&](int pop, const PQRef& a, const PQRef& b, const PQRef& o, int64_t* size) -> int {
+      HIPCHK(hipMemsetAsync(c->scalar.p, 0, 8, s));
+      launch_pq_step(s, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), pa, pop, as_arg(a), as_arg(b), as_arg(o),
+                     c->scalar.as<unsigned long long>());
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(&h_size, c->scalar.p, 8, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      *size = 8 + (int64_t)h_size;
+      return RBG_OK;
+    };
+    std::vector<int64_t> sizes(N);
+    std::vector<PQRef> node(N);
+    for (size_t k = 0; k < N; k++) {
+      sizes[k] = 8 + (int64_t)leaf[k];
+      node[k] = PQRef{(int32_t)k, nullptr, nullptr};
+    }
+    auto cmp = [&](int a, int b) { return (int)(int32_t)(uint32_t)(uint64_t)(sizes[a] - sizes[b]); };
+    IntHeap<decltype(cmp)> pq(cmp);
+    for (size_t k = 0; k < N; k++) pq.add((int)k);
+    if (op == RBG_WIDE_PQ_OR) {  // :758-781
+      std::vector<char> istmp(N, 0);
+      while (pq.q.size() > 1) {
+        const int x1 = pq.poll(), x2 = pq.poll();
+        if (istmp[x2] && istmp[x1]) {  // lazyorfromlazyinputs(buffer[x1], buffer[x2])
+          CHK(step(PQ_LFL, node[x1], node[x2], node[x1], &sizes[x1]));
+          release(node[x2]);
+          pq.add(x1);
+        } else if (istmp[x2]) {  // buffer[x2].lazyor(buffer[x1])
+          CHK(step(PQ_LIOR, node[x2], node[x1], node[x2], &sizes[x2]));
+          pq.add(x2);
+        } else if (istmp[x1]) {  // buffer[x1].lazyor(buffer[x2])
+          CHK(step(PQ_LIOR, node[x1], node[x2], node[x1], &sizes[x1]));
+          pq.add(x1);
+        } else {  // RoaringBitmap.lazyor(buffer[x1], buffer[x2])
+          PQRef t;
+          CHK(alloc(&t));
+          CHK(step(PQ_LOR, node[x1], node[x2], t, &sizes[x1]));
+          node[x1] = t;
+          istmp[x1] = 1;
+          pq.add(x1);
+        }
+      }
+    } else {  // :799-811: pq.add(RoaringBitmap.xor(x1, x2))
+      while (pq.q.size() > 1) {
+        const int x1 = pq.poll(), x2 = pq.poll();
+        PQRef t;
+        CHK(alloc(&t));
+        int64_t sz;
+        CHK(step(PQ_XOR, node[x1], node[x2], t, &sz));
+        release(node[x1]);
+        release(node[x2]);
+        node.push_back(t);
+        sizes.push_back(sz);
+        pq.add((int)node.size() - 1);
+      }
+    }
+    const PQRef root = node[pq.poll()];
+    c->mark(2);
+    launch_pq_final(s, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), pa, op == RBG_WIDE_PQ_OR ? 1 : 0,
+                    as_arg(root), oc);
+    HIPCHK(hipGetLastError());
+    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
+    HIPCHK(hipStreamSynchronize(s));  // the temps are freed on return
+  } else {
+    c->mark(2);
+    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
+  }
+  c->last = 1;
+  c->mark(3);
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
+
 // FastAggregation dispatch (RB/FastAggregation.java:26-101,653-666,823-836)
 // start_override >= 0: naive_and starts from that input (key-range shards pass the
 // input with the fewest containers over the WHOLE universe, RB/FastAggregation.java:333-339)
@@ -726,9 +901,10 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
   }
   key_lo = std::max(0, key_lo);
   key_hi = std::min(kMaxKeys, key_hi);
+  *host_card_valid = false;
+  if (!card_only && (op == RBG_WIDE_PQ_OR || op == RBG_WIDE_PQ_XOR)) return ctx_pq(c, op, B, id, key_lo, key_hi);
   hipStream_t s = c->stream;
   const size_t N = B->n_bm;
-  *host_card_valid = false;
   int mode = WIDE_OR, plan_mode = 0;
   uint32_t start_bm = 0, chain = 0;
   const uint32_t* order = nullptr;
@@ -1089,7 +1265,7 @@ int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, 
 }
 
 int rbg_wide(int op, const uint8_t* const* bufs, const size_t* lens, const int32_t* ids, size_t n, rbg_buffer* out) {
-  if (!out || op < 0 || op > RBG_WIDE_HORIZONTAL_XOR) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!out || op < 0 || op > RBG_WIDE_PQ_XOR) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};

@@ -38,6 +38,43 @@ struct WideArgs {
   uint32_t chain;         // chain modes: kChain* flags
 };
 
+// priority-queue aggregations (pq.hip): one step of the queue combines two nodes
+// (an input bitmap of the batch, or an intermediate temp) over every union key.
+//   PQ_XOR  RoaringBitmap.xor(x1, x2)                 (priorityqueue_xor)
+//   PQ_LOR  RoaringBitmap.lazyor(x1, x2), static      (priorityqueue_or, two inputs)
+//   PQ_LIOR x1.lazyor(x2), in place on the temp x1    (one temp)
+//   PQ_LFL  RoaringBitmap.lazyorfromlazyinputs(x1, x2) (two temps)
+enum PQOp : int { PQ_XOR = 0, PQ_LOR = 1, PQ_LIOR = 2, PQ_LFL = 3 };
+// container kinds of a node: DK_A / DK_B (exact) / DK_R, and a lazy bitmap (card -1 in the reference)
+enum PQKind : int { PK_A = 0, PK_BE = 1, PK_R = 2, PK_BL = 3 };
+struct __align__(16) PQState {  // per key of a temp
+  uint32_t card;
+  uint16_t nruns;
+  uint8_t kind;     // PQKind
+  uint8_t present;  // the temp holds this key
+  int32_t src;      // >= 0: an unchanged clone of this input container (desc index); else `set`
+  uint32_t pad;
+};
+struct PQRef {
+  int32_t leaf;    // >= 0: input bitmap `leaf` of the batch; -1: a temp
+  PQState* st;     // temp: one state per task
+  uint64_t* set;   // temp: one 8 KiB bitmap (1024 words) per task
+};
+struct PQArgs {
+  const CDesc* desc;
+  const uint32_t* bm;
+  const uint8_t* payload;
+};
+// sizes[bm] += 2 + getSizeInBytes over the batch's containers (sizes zeroed by the caller)
+void launch_pq_leaf_sizes(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
+                          unsigned long long* sizes);
+// out = op(a, b); *size += 2 + getSizeInBytes of each of out's containers
+void launch_pq_step(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, PQArgs args, int op, PQRef a,
+                    PQRef b, PQRef out, unsigned long long* size);
+// the root node as the op's result records (repair: priorityqueue_or's repairAfterLazy)
+void launch_pq_final(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, PQArgs args, int repair,
+                     PQRef root, OutCtx oc);
+
 // bit-sliced index (bsi.hip); ops in the order of BitmapSliceIndex.Operation
 // (bsi/src/main/java/org/roaringbitmap/bsi/BitmapSliceIndex.java:23-38)
 // BSI_ALL: compareUsingMinMax's "all" (BSI/:516: ebM, or and(ebM, foundSet));

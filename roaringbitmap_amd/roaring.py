@@ -307,14 +307,18 @@ class FastAggregation:
 
     @staticmethod
     def priorityqueue_or(*args):
+        """priorityqueue_or(Iterator) :677-727 and priorityqueue_or(RoaringBitmap...) :737-781: a
+        queue of whole bitmaps by getLongSizeInBytes, lazy unions, repairAfterLazy at the end"""
         if len(args) == 1 and isinstance(args[0], Iterator):
-            return _wide("or", list(args[0]))
+            return _wide("priorityqueue_or", list(args[0]))
         bms = list(args[0]) if len(args) == 1 and isinstance(args[0], (list, tuple)) else list(args)
-        return _wide("or", bms)
+        return _wide("priorityqueue_or", bms)
 
     @staticmethod
     def priorityqueue_xor(*bitmaps):
-        return _wide("xor", list(bitmaps))
+        """priorityqueue_xor(RoaringBitmap...) :794-812: RoaringBitmap.xor of the two smallest"""
+        bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
+        return _wide("priorityqueue_xor", bms)
 
 
 class ParallelAggregation:

@@ -1,13 +1,17 @@
-"""ParallelAggregation, BufferFastAggregation.or(Mutable...), horizontal_or / horizontal_xor on
-the GPU, byte-exact against the oracle's restatements (tests/test_aggregation_oracle.py pins
+"""ParallelAggregation, BufferFastAggregation.or(Mutable...), horizontal_or / horizontal_xor and
+priorityqueue_or / priorityqueue_xor on the GPU, byte-exact against the oracle's restatements (tests/test_aggregation_oracle.py pins
 those to the reference's tests).
 
 Inputs mix every container family of tests/_gen.py at few keys so that many keys hold
 2..15 containers (the lazyIOR chain of ParallelAggregation.or, RB/ParallelAggregation.java:
 200-206) and some hold 16+ (its lazy-bitmap branch :208-214), plus equal-cardinality
 array / run containers at one key, whose chain order comes from the heap's tie order
-(horizontal_*, RB/FastAggregation.java:124-289).
+(horizontal_*, RB/FastAggregation.java:124-289).  priorityqueue_* (:677-812) pair whole
+bitmaps by getLongSizeInBytes, so their result types depend on the whole queue: equal-size
+inputs exercise the heap's tie order, and run / bitmap / array mixes the lazy algebra
+(lazyor, in-place lazyor, lazyorfromlazyinputs) and the final repairAfterLazy.
 """
+import os
 import numpy as np
 import pytest
 
@@ -17,7 +21,9 @@ from _fmt import A, R, encode
 
 pytestmark = pytest.mark.gpu
 
-OPS = ["parallel_or", "parallel_xor", "buffer_or_mutable", "horizontal_or", "horizontal_xor"]
+OPS = ["parallel_or", "parallel_xor", "buffer_or_mutable", "horizontal_or", "horizontal_xor", "priorityqueue_or",
+       "priorityqueue_xor"]
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
 def _wide(op, bufs):
@@ -93,3 +99,49 @@ def test_host_api_names(gpu):
     assert rb.FastAggregation.horizontal_or(*bms).serialize() == O.wide("horizontal_or", bufs)
     assert rb.FastAggregation.horizontal_or(iter(bms)).serialize() == O.wide("or", bufs)
     assert rb.FastAggregation.horizontal_xor(*bms).serialize() == O.wide("horizontal_xor", bufs)
+    assert rb.FastAggregation.priorityqueue_or(*bms).serialize() == O.wide("priorityqueue_or", bufs)
+    assert rb.FastAggregation.priorityqueue_or(iter(bms)).serialize() == O.wide("priorityqueue_or", bufs)
+    assert rb.FastAggregation.priorityqueue_xor(*bms).serialize() == O.wide("priorityqueue_xor", bufs)
+    assert rb.FastAggregation.priorityqueue_or().serialize() == O.wide("priorityqueue_or", [])
+    assert rb.FastAggregation.priorityqueue_xor().serialize() == O.wide("priorityqueue_xor", [])
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_priorityqueue_equal_sizes_and_lazy_mix(gpu, seed):
+    """Equal getLongSizeInBytes (tie order of the heap), temps meeting temps
+    (lazyorfromlazyinputs), full run containers and bitmap + array chains."""
+    rng = np.random.default_rng(500 + seed)
+    bufs = []
+    for i in range(11):
+        ctrs = [(k, A, np.sort(rng.choice(65536, 300, replace=False)).astype(np.uint16)) for k in (0, 1)]
+        if i % 3 == 0:
+            ctrs.append((2, R, np.arange(0, 65536).astype(np.uint16)))  # full run
+        elif i % 3 == 1:
+            s = int(rng.integers(0, 30000))
+            ctrs.append((2, R, np.arange(s, s + 20000, dtype=np.uint16)))
+        else:
+            ctrs.append((2, A, np.sort(rng.choice(65536, 5000, replace=False)).astype(np.uint16)))
+        ctrs.append((3 + i % 4, A, np.array([i, 100 + i], dtype=np.uint16)))
+        bufs.append(encode(ctrs))
+    for op in ("priorityqueue_or", "priorityqueue_xor"):
+        assert _wide(op, bufs) == O.wide(op, bufs), op
+
+
+def _realdata(ds):
+    z = np.load(os.path.join(GOLD, "realdata", ds + ".npz"))
+    v, o = z["values"], z["offsets"]
+    return [v[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+
+
+@pytest.mark.parametrize("run_opt", [False, True])
+def test_priorityqueue_realdata(gpu, run_opt):
+    """RealDataBenchmarkWideOrPqTest datasets: byte parity with the queue restatement and the
+    known wide-OR cardinality."""
+    import json
+    known = json.load(open(os.path.join(GOLD, "known_answers.json")))["values"]
+    for ds in ["census1881", "wikileaks-noquotes_srt"]:
+        bufs = [O.from_values(s, run_opt) for s in _realdata(ds)]
+        got = _wide("priorityqueue_or", bufs)
+        assert got == O.wide("priorityqueue_or", bufs), ds
+        assert len(O.to_values(got)) == known[ds]["wide_or"]
+        assert _wide("priorityqueue_xor", bufs) == O.wide("priorityqueue_xor", bufs), ds
