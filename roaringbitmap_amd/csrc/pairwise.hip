@@ -265,6 +265,13 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
     return;
   }
   PRIO_OUT();
+#if RBG_EXP_NOCOMPACT
+  {  // experiment: no compaction and no payload store (wrong bytes, timing only)
+    const int c = (int)uni((uint32_t)wave_sum_i(cnt));
+    w_place(t, c > 0, oc.scratch + (size_t)t * kSlotBytes, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, oc);
+    return;
+  }
+#endif
   // the map is dead: compact the kept values over it, then 16 B stores.  Vectors
   // j and j+1 share one scan (16-bit count fields); every value is written, the
   // dropped ones to a per-lane dummy just past the kept ones (u16 index ctot + l),
@@ -523,6 +530,13 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
     return;
   }
   uint32_t len;
+#if RBG_EXP_NOSTAGE
+  if (kind != DK_B) {  // experiment: A / R results not staged (wrong bytes, timing only)
+    w_place(t, true, oc.scratch + (size_t)t * kSlotBytes, false, lds, kind == DK_A ? 2u * c : 6u, (uint32_t)c, tk.key,
+            kind, oc);
+    return;
+  }
+#endif
   if (kind == DK_A) len = w_stage(DK_A, x, c, lds);
   else len = 2u + 4u * (uint32_t)w_stage_runs(x, lds);
   STAMP(7);
@@ -549,9 +563,46 @@ __device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
 // and bitmap-class tasks share the launch: separate kernels per class were
 // measured 15 % slower on the C2 mix (tail + an extra dependent index load).
 // MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
+#if RBG_EXP_LOADONLY
+// experiment: every operand payload read (16 B per lane per vector, all in flight), no compute
+__device__ __forceinline__ uint32_t exp_read(const uint8_t* slot, int kind, uint32_t card, uint32_t nr) {
+  const uint32_t bytes = kind == DK_A ? 2 * card : kind == DK_B ? 8192 : 4 + 4 * nr;
+  const uint32_t nvec = (bytes + 15) >> 4;
+  const uint4* p = reinterpret_cast<const uint4*>(slot) + lane_id();
+  uint32_t acc = 0;
+  uint4 v[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) v[j] = (64 * j + lane_id() < (int)nvec) ? p[64 * j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 8; j++) acc ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
+  return acc;
+}
+#endif
+
 template <int OP, int MODE>
 __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
                                          const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+#if RBG_EXP_LOADONLY
+  if (MODE == 1) {
+    uint32_t a = tk.kind_a != kAbsent ? exp_read(pa + tk.slot_a, tk.kind_a, tk.card_a, tk.nruns_a) : 0;
+    uint32_t b = tk.kind_b != kAbsent ? exp_read(pb + tk.slot_b, tk.kind_b, tk.card_b, tk.nruns_b) : 0;
+    const int c = wave_sum_i((int)((a ^ b) & 1));
+    if (lane_id() == 0) task_card[t] = (uint32_t)c;
+    return;
+  }
+  if (MODE == 0) {  // reads + a 4 KiB store per task (about the C2 AND's output bytes)
+    uint32_t a = tk.kind_a != kAbsent ? exp_read(pa + tk.slot_a, tk.kind_a, tk.card_a, tk.nruns_a) : 0;
+    uint32_t b = tk.kind_b != kAbsent ? exp_read(pb + tk.slot_b, tk.kind_b, tk.card_b, tk.nruns_b) : 0;
+#ifndef RBG_EXP_DST
+#define RBG_EXP_DST ((size_t)t * kSlotBytes)
+#endif
+    uint4* dst = reinterpret_cast<uint4*>(oc.scratch + RBG_EXP_DST) + lane_id();
+#pragma unroll
+    for (int j = 0; j < RBG_EXP_LOADONLY_STV; j++) dst[64 * j] = make_uint4(a, b, a ^ b, j);
+    if (lane_id() == 0) task_card[t] = a;
+    return;
+  }
+#endif
   PRIO_HI();
   if (pair_class(OP, tk.kind_a, tk.kind_b) == 1)
     filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
@@ -573,6 +624,38 @@ __global__ __launch_bounds__(256, RBG_PW_BLOCKS) void k_pair_wave(const PTask* _
   uint32_t t = uni(blockIdx.x * kWaves + w);
   if (t >= nt) return;
   PTask cur = load_task(tasks, t);
+#if RBG_EXP_LOADONLY == 2
+  if (MODE == 0) {  // experiment: reads + 4 KiB stores, the next task's reads issued before this task's stores
+    auto issue = [&](const PTask& tk, uint4* va, uint4* vb) {
+      const uint32_t ba = tk.kind_a == kAbsent ? 0 : tk.kind_a == DK_A ? 2 * tk.card_a : tk.kind_a == DK_B ? 8192 : 4 + 4 * tk.nruns_a;
+      const uint32_t bb = tk.kind_b == kAbsent ? 0 : tk.kind_b == DK_A ? 2 * tk.card_b : tk.kind_b == DK_B ? 8192 : 4 + 4 * tk.nruns_b;
+      const uint4* p = reinterpret_cast<const uint4*>(pa + tk.slot_a) + lane_id();
+      const uint4* q = reinterpret_cast<const uint4*>(pb + tk.slot_b) + lane_id();
+#pragma unroll
+      for (int j = 0; j < 8; j++) va[j] = (64 * j + lane_id() < (int)((ba + 15) >> 4)) ? p[64 * j] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < 8; j++) vb[j] = (64 * j + lane_id() < (int)((bb + 15) >> 4)) ? q[64 * j] : make_uint4(0, 0, 0, 0);
+    };
+    uint4 va[8], vb[8];
+    issue(cur, va, vb);
+    for (;;) {
+      const uint32_t tn = t + stride;
+      uint32_t a = 0, b = 0;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        a ^= va[j].x ^ va[j].y ^ va[j].z ^ va[j].w;
+        b ^= vb[j].x ^ vb[j].y ^ vb[j].z ^ vb[j].w;
+      }
+      if (tn < nt) issue(load_task(tasks, tn), va, vb);
+      uint4* dst = reinterpret_cast<uint4*>(oc.scratch + (size_t)t * kSlotBytes) + lane_id();
+#pragma unroll
+      for (int j = 0; j < 4; j++) dst[64 * j] = make_uint4(a, b, a ^ b, j);
+      if (tn >= nt) break;
+      t = tn;
+    }
+    return;
+  }
+#endif
 #if RBG_STAMPS
   StampAcc sacc = {};
   const uint64_t t_kernel = __builtin_amdgcn_s_memtime();
