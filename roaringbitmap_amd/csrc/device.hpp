@@ -305,18 +305,22 @@ __device__ __forceinline__ void store_bitmap_owned(uint8_t* words, const uint64_
 }
 
 // OR the sorted u16 values of an array container into an LDS bitmap
-// (cooperative over the workgroup; vals is 16 B aligned, reads stay in the slot).
+// (cooperative over the workgroup).  vals is 2 B aligned: 16 B slots, or the packed
+// arrays of a C3 synthetic batch; the 16 B vectors covering it are read and the
+// values outside [vals, vals + card) are skipped.
 template <int MODE = 0>  // 0: or, 1: xor
 __device__ __forceinline__ void lds_scatter_array(uint32_t* lds, const uint16_t* vals, int card) {
-  const int nvec = (card + 7) >> 3;
-  const uint4* v4 = reinterpret_cast<const uint4*>(vals);
+  const uintptr_t a = reinterpret_cast<uintptr_t>(vals);
+  const int lo = (int)((a & 15) >> 1);  // values of the first vector before vals
+  const int nvec = (lo + card + 7) >> 3;
+  const uint4* v4 = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
   for (int i = threadIdx.x; i < nvec; i += NT) {
     const uint4 v = v4[i];
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    const int base = i * 8;
+    const int base = i * 8 - lo;
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      if (base + j < card) {
+      if ((unsigned)(base + j) < (unsigned)card) {
         const uint32_t x = (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFF;
         if (MODE == 0) atomicOr(&lds[x >> 5], 1u << (x & 31));
         else atomicXor(&lds[x >> 5], 1u << (x & 31));

@@ -94,6 +94,8 @@ struct DevBuf {
 struct Batch {
   bool live = false;
   bool key_major = false;  // containers sorted by (key, input); else by (input, key)
+  bool packed = false;     // array payloads packed at 2 B granularity (C3 uniform synthetic
+                           // batches): wide ops and fetches only
   size_t n_bm = 0, n_ctr = 0;
   DevBuf keys, desc, bm, key_off, bm_off, payload;
   size_t payload_bytes = 0;
@@ -562,8 +564,8 @@ static int operand(Batch* b, size_t i, const uint16_t** keys, const CDesc** desc
     set_err("bitmap index out of range");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
-  if (b->n_bm != 1 || !b->key_major) {
-    set_err("pairwise operands must be single-bitmap key-major batches");
+  if (b->n_bm != 1 || !b->key_major || b->packed) {
+    set_err("pairwise operands must be single-bitmap key-major batches with slot-aligned payloads");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   *keys = b->keys.as<uint16_t>();
@@ -1048,7 +1050,7 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
                    int32_t min_value, int32_t max_value, int want_sum) {
   Batch* B;
   CHK(get_batch(c, id, &B));
-  if (!B->key_major || nbits < 0 || nbits + 2 > kBsiMaxInputs || B->n_bm != (size_t)(1 + nbits + (has_found ? 1 : 0)) ||
+  if (!B->key_major || B->packed || nbits < 0 || nbits + 2 > kBsiMaxInputs || B->n_bm != (size_t)(1 + nbits + (has_found ? 1 : 0)) ||
       op < 0 || op > BSI_SUM_ONLY || (op == BSI_SUM_ONLY && !has_found)) {
     set_err("bsi: batch must hold ebM, nbits slices and the optional foundSet; bad op");
     return RBG_ERR_ILLEGAL_ARGUMENT;
@@ -1302,6 +1304,10 @@ int rbg_wide_card(int op, const uint8_t* const* bufs, const size_t* lens, size_t
 static int ctx_batch_card(Ctx* c, int32_t id) {
   Batch* B;
   CHK(get_batch(c, id, &B));
+  if (B->packed) {
+    set_err("batched andCardinality needs slot-aligned payloads");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
   if (B->n_bm % 2 != 0) {
     set_err("batched andCardinality needs an even number of bitmaps");
     return RBG_ERR_ILLEGAL_ARGUMENT;
@@ -1974,6 +1980,7 @@ static int synth_c3(Ctx* c, int kind, uint64_t seed, size_t n, int key_lo, int k
     launch_synth_c3u(s, seed, (uint32_t)n, key_lo, nkeys, nullptr, kb, b.desc.as<CDesc>(), b.keys.as<uint16_t>(),
                      b.bm.as<uint32_t>(), b.payload.as<uint8_t>(), 1);
     b.n_kind[DK_A] = (int64_t)C;
+    b.packed = true;
   } else {
     b.payload_bytes = 8192 * C;
     CHK(b.payload.ensure(b.payload_bytes + 64));
@@ -2148,6 +2155,10 @@ static int copy_dev(DevBuf& dst, const DevBuf& src, hipStream_t s) {
 static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answers) {
   Batch* a;
   CHK(get_batch(c, id, &a));
+  if (a->packed) {
+    set_err("runOptimize needs slot-aligned payloads (not a packed synthetic batch)");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
   hipStream_t s = c->stream;
   const size_t C = a->n_ctr, n = a->n_bm;
   DevBuf info, size, part, flags;

@@ -32,7 +32,7 @@ struct WideArgs {
   const uint8_t* payload; // arena
   const uint8_t* skip;    // naive_and: per input bitmap, 1 = skip (identity with the start)
   uint32_t start_bm;      // naive_and: input bitmap the chain starts from
-  uint32_t all_array;     // every container is an array (slots padded with their last value)
+  uint32_t all_array;     // every container is an array: a key segment is one contiguous u16 value stream
   uint32_t slot32;        // every slot offset / 16 fits 32 bits (payload < 64 GiB)
   const uint32_t* order;  // chain modes: container index at chain position j of a key segment (null: input order)
   uint32_t chain;         // chain modes: kChain* flags

@@ -22,7 +22,9 @@ __device__ __forceinline__ uint64_t bernoulli_word(uint64_t seed, uint32_t thr) 
 // ===========================================================================
 // C3 uniform: one workgroup per key, n containers (one per bitmap) per key
 // ===========================================================================
-__device__ __forceinline__ uint32_t c3u_slot_bytes(uint32_t card) { return (2 * card + 15) & ~15u; }
+// C3 uniform arrays are packed back to back (2 B granularity, as in the portable
+// format): no slot padding, so a key segment streams exactly its payload bytes
+__device__ __forceinline__ uint32_t c3u_slot_bytes(uint32_t card) { return 2 * card; }
 
 __global__ __launch_bounds__(256) void k_synth_c3u_sizes(uint64_t seed, uint32_t n, int key_lo,
                                                          unsigned long long* __restrict__ key_bytes) {
@@ -68,7 +70,6 @@ __global__ __launch_bounds__(256) void k_synth_c3u_fill(uint64_t seed, uint32_t 
       const uint64_t h = splitmix64(seed ^ 0x5EEDULL ^ ((uint64_t)i << 20) ^ ((uint64_t)k << 40));
       uint16_t x = 0;
       for (uint32_t j = 0; j < card; j++) v[j] = x = (uint16_t)(j * step + (uint32_t)(splitmix64(h + j) % step));
-      for (uint32_t j = card; j < (uint32_t)sz / 2; j++) v[j] = x;  // slot padding repeats the last value
     }
     running += (uint64_t)tot;
   }

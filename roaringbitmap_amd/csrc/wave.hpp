@@ -130,24 +130,29 @@ constexpr int kVecRound = 4;  // 16 B vectors per lane loaded per round
 #ifndef RBG_SCATTER_MERGE
 #define RBG_SCATTER_MERGE 0
 #endif
+// Branch-free: one LDS atomic per value, 4 VALU (word index, address, valid bit,
+// bit mask).  Values whose bit in `vm` is clear get a zero mask (the valid bits are
+// formed once per vector).  An average array has about one value per map word, so
+// merging same-word neighbours saved few atomics but cost divergent branches.
+template <int MODE>  // MODE 0 or, 1 xor
+__device__ __forceinline__ void scatter_vec_mask(uint32_t* lds, const uint4 v, uint32_t vm) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint32_t wi = w[i >> 1];
+    uint32_t* p = lds + ((i & 1) ? bfe_hi_word(wi) : bfe_lo_word(wi));
+    const uint32_t m = ((vm >> i) & 1u) << (((i & 1) ? (wi >> 16) : wi) & 31u);
+    if (MODE == 0) atomicOr(p, m);
+    else atomicXor(p, m);
+  }
+}
+
 template <int MODE, bool MERGE = (RBG_SCATTER_MERGE != 0)>  // MODE 0 or, 1 xor
 __device__ __forceinline__ void scatter_vec(uint32_t* lds, const uint4 v, int base, int card) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
   if (!MERGE) {
-    // Branch-free: one LDS atomic per value, 4 VALU (word index, address, valid
-    // bit, bit mask).  Values past the card get a zero mask (the valid bits are
-    // formed once per vector).  An average array has about one value per map word,
-    // so merging same-word neighbours saved few atomics but cost divergent branches.
     const int rem = card - base;
-    const uint32_t vm = rem >= 8 ? 0xFFu : (1u << max(rem, 0)) - 1u;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const uint32_t wi = w[i >> 1];
-      uint32_t* p = lds + ((i & 1) ? bfe_hi_word(wi) : bfe_lo_word(wi));
-      const uint32_t m = ((vm >> i) & 1u) << (((i & 1) ? (wi >> 16) : wi) & 31u);
-      if (MODE == 0) atomicOr(p, m);
-      else atomicXor(p, m);
-    }
+    scatter_vec_mask<MODE>(lds, v, rem >= 8 ? 0xFFu : (1u << max(rem, 0)) - 1u);
     return;
   }
   uint32_t cur = 0xFFFFFFFFu, mask = 0;

@@ -12,15 +12,18 @@
 namespace rbg {
 
 // Thread-serial OR/XOR of a small array container into LDS (16 B vector loads).
+// vals is 2 B aligned (see lds_scatter_array).
 template <int MODE>
 __device__ __forceinline__ void thread_scatter_array(uint32_t* lds, const uint16_t* vals, int card) {
-  const uint4* v4 = reinterpret_cast<const uint4*>(vals);
-  for (int base = 0; base < card; base += 8) {
-    const uint4 v = v4[base >> 3];
+  const uintptr_t a = reinterpret_cast<uintptr_t>(vals);
+  const int lo = (int)((a & 15) >> 1);
+  const uint4* v4 = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+  for (int base = -lo; base < card; base += 8) {
+    const uint4 v = v4[(base + lo) >> 3];
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      if (base + j < card) {
+      if ((unsigned)(base + j) < (unsigned)card) {
         const uint32_t x = (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFF;
         if (MODE == 0) atomicOr(&lds[x >> 5], 1u << (x & 31));
         else atomicXor(&lds[x >> 5], 1u << (x & 31));
@@ -97,10 +100,18 @@ __device__ __forceinline__ void accumulate_segment(const CDesc* desc, const uint
   for (int i = 0; i < 4; i++) r[i] = MODE == 0 ? (r[i] | x[i]) : (r[i] ^ x[i]);
 }
 
-// OR a stream of u16 values (16 B vectors, every value valid) into the LDS
-// bitmap: four vectors per thread in flight per round.
-__device__ __forceinline__ void stream_or_values(uint32_t* acc, const uint4* v4, uint32_t nvec) {
+// OR the u16 value stream [b0, b1) (2 B aligned byte addresses) into the LDS bitmap:
+// the 16 B vectors covering it, four per thread in flight per round.  Only the first
+// and the last vector hold values outside the stream (masked).
+__device__ __forceinline__ void stream_or_values(uint32_t* acc, const uint8_t* b0, const uint8_t* b1) {
   constexpr int U = 4;
+  const uintptr_t a0 = reinterpret_cast<uintptr_t>(b0);
+  const uint4* v4 = reinterpret_cast<const uint4*>(a0 & ~(uintptr_t)15);
+  const uint32_t lo = (uint32_t)((a0 & 15) >> 1);
+  const uint32_t hi = lo + (uint32_t)((b1 - b0) >> 1);  // values [lo, hi) of the vectors are the stream
+  const uint32_t nvec = (hi + 7) >> 3;
+  const uint32_t first_m = (0xFFu << lo) & 0xFFu;
+  const uint32_t last_m = (hi & 7) ? (1u << (hi & 7)) - 1u : 0xFFu;
   for (uint32_t j0 = 0; j0 < nvec; j0 += U * NT) {
     uint4 v[U];
 #pragma unroll
@@ -109,8 +120,10 @@ __device__ __forceinline__ void stream_or_values(uint32_t* acc, const uint4* v4,
       v[u] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
-    for (int u = 0; u < U; u++)
-      if (j0 + u * NT + threadIdx.x < nvec) scatter_vec<0>(acc, v[u], 0, 8);
+    for (int u = 0; u < U; u++) {
+      const uint32_t k = j0 + u * NT + threadIdx.x;
+      if (k < nvec) scatter_vec_mask<0>(acc, v[u], (k == 0 ? first_m : 0xFFu) & (k == nvec - 1 ? last_m : 0xFFu));
+    }
   }
 }
 
@@ -172,17 +185,16 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         c = (int)d.card;
         kind = by_card(c);
       } else if (A.all_array) {
-        // every slot of the segment is an array padded with its last value, and
-        // the slots are contiguous: the segment is one u16 value stream
+        // every slot of the segment is an array and the slots are contiguous (16 B
+        // slots padded with their last value, or the packed arrays of a C3 synthetic
+        // batch): the segment is one u16 value stream
         __syncthreads();
         lds_clear(acc);
 #pragma unroll
         for (int i = 0; i < 4; i++) r[i] = 0;
         const CDesc d0 = A.desc[s], d1 = A.desc[s + n - 1];
-        const uint4* v4 = reinterpret_cast<const uint4*>(A.payload + d0.slot);
-        const uint32_t nvec = (uint32_t)((d1.slot + ((2 * d1.card + 15) & ~15u) - d0.slot) >> 4);
         __syncthreads();
-        stream_or_values(acc, v4, nvec);
+        stream_or_values(acc, A.payload + d0.slot, A.payload + d1.slot + 2 * (uint64_t)d1.card);
         __syncthreads();
         lds_read_owned(acc, r);
         c = block_card(r, sh);
