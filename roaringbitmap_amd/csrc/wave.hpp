@@ -30,9 +30,11 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #endif
 // wave-uniform copy (value of the first active lane, in an SGPR)
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+// (readfirstlane returns int: each half goes through uint32_t, or a low half with bit 31
+// set would sign-extend over the high half)
 __device__ __forceinline__ uint64_t uni64(uint64_t x) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
-         (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
 // Bit-field helpers for map probes.  Written as v_bfe_u32 directly: the compiler
