@@ -505,6 +505,18 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
     w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
   STAMP(1);
   PRIO_LO();
+#if RBG_EXP_BB
+  if (MODE == 0) {  // experiment: every bitmap-class result stored as a bitmap, no count / typing
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+    w_store_bitmap(slot, x);
+#if RBG_EXP_BB == 1
+    w_place(t, true, slot, false, lds, 8192, 1, tk.key, DK_B, oc);
+#else
+    if (l == 0) task_card[t] = (uint32_t)x.w[0];
+#endif
+    return;
+  }
+#endif
   const int c = w_card(x);
   if (MODE == 1) {
     if (l == 0) task_card[t] = (uint32_t)c;
