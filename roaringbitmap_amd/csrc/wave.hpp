@@ -630,24 +630,34 @@ __device__ __forceinline__ void w_map_pre(int kind, int card, int nruns, const W
   wsync();
 }
 
+// A bitmap payload (8 KiB, 16 B aligned) copied into the wave's LDS map by LDS-DMA:
+// eight global_load_lds_dwordx4, 1 KiB each (lane l's 16 B land at base + 16 l, the
+// map's own layout), all in flight at once and no VGPRs.  (Loaded through registers,
+// the copy was serialised by the register allocator in the pairwise kernels -- one
+// 4-VGPR buffer, a full memory round trip per 1 KiB -- whenever the kernel ran at its
+// 128-VGPR cap.)  Earlier LDS reads of the map are drained first; the DMA is waited
+// for with vmcnt(0) (it also retires any older global load or store of the wave).
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+typedef __attribute__((address_space(1))) void* global_void_ptr;
+__device__ __forceinline__ void w_bitmap_to_lds_dma(const uint8_t* slot, uint32_t* lds) {
+  const uint4* g = reinterpret_cast<const uint4*>(slot) + lane_id();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    __builtin_amdgcn_global_load_lds((global_void_ptr)(g + 64 * i), (lds_void_ptr)(lds + 256 * i), 16, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // The same map built from a container streamed from memory.
 __device__ __forceinline__ void w_map_lds(int kind, int card, const uint8_t* slot, uint32_t* lds) {
-  const int l = lane_id();
-  uint4* q = reinterpret_cast<uint4*>(lds) + l;
   wsync();
   if (kind == DK_B) {
-    const uint4* g = reinterpret_cast<const uint4*>(slot) + l;
-#pragma unroll
-    for (int h = 0; h < 8; h += 4) {
-      uint4 v[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) v[i] = g[64 * (h + i)];
-#pragma unroll
-      for (int i = 0; i < 4; i++) q[64 * (h + i)] = v[i];
-    }
+    w_bitmap_to_lds_dma(slot, lds);
     wsync();
     return;
   }
+  const int l = lane_id();
+  uint4* q = reinterpret_cast<uint4*>(lds) + l;
   w_clear_lds(lds);
   wsync();
   if (kind == DK_A) {

@@ -201,3 +201,53 @@ def test_run_or_run(gpu, na, nb):
         assert got == O.pairwise("or", bx, by)
         assert rb.RoaringBitmap.orCardinality(rb.RoaringBitmap(bx), rb.RoaringBitmap(by)) == \
             O.pairwise_card("or", bx, by)
+
+
+def _split_cases(rng):
+    """R AND R operand pairs whose run lists together exceed one wave's LDS
+    (2558 < na + nb <= 5116): the two-window run-domain path, its junction at
+    32767 / 32768, and its fallbacks (a window that does not fit, a result that is
+    not R)."""
+    lo_hi = lambda n1, n2: np.concatenate([_run_vals(rng, n1, 0, 32768), _run_vals(rng, n2, 32768, 65536)])
+    a, b = _run_vals(rng, 2000), _run_vals(rng, 1900)
+    cases = [("spread", a, b), ("spread_same", a, a)]
+    # one run of each operand spans 32767 / 32768: the result run is split and merged
+    cross_a = np.union1d(_run_vals(rng, 1100, 0, 32000), np.arange(32100, 33000))
+    cross_a = np.union1d(cross_a, _run_vals(rng, 1100, 33100, 65536))
+    cross_b = np.union1d(_run_vals(rng, 1100, 0, 32000), np.arange(32500, 34000))
+    cross_b = np.union1d(cross_b, _run_vals(rng, 1100, 34100, 65536))
+    cases.append(("junction", cross_a, cross_b))
+    cases.append(("junction_exact", np.union1d(lo_hi(1200, 1200), [32767, 32768]),
+                  np.union1d(lo_hi(1100, 1100), [32767, 32768])))
+    # only A crosses; B has a run ending at 32767 and one starting at 32769
+    b_edge = np.union1d(lo_hi(1100, 1100), np.concatenate([np.arange(32700, 32768), np.arange(32769, 32800)]))
+    cases.append(("cross_a_only", cross_a, b_edge))
+    # the result ends window 0 at 32767 without a junction
+    cases.append(("end_at_32767", np.union1d(lo_hi(1200, 1200), np.arange(32600, 32768)),
+                  np.union1d(lo_hi(1200, 1200), np.arange(32650, 32768))))
+    # every run in the low half: window 0 does not fit, bitmap path
+    cases.append(("low_half", _run_vals(rng, 1500, 0, 32768), _run_vals(rng, 1500, 0, 32768)))
+    # interleaved short runs: the intersection has > 2047 runs (bitmap result) ...
+    s3 = np.arange(0, 65536 - 3, 26)
+    cases.append(("many_result_runs", np.unique(np.concatenate([s3, s3 + 1, s3 + 2])),
+                  np.unique(np.concatenate([s3 + 1, s3 + 2, s3 + 3]))))
+    # ... or single values (array result by EFF)
+    s2 = np.arange(0, 65536 - 2, 40)
+    cases.append(("array_result", np.unique(np.concatenate([s2, s2 + 1])), np.unique(np.concatenate([s2 + 1, s2 + 2]))))
+    cases.append(("disjoint", a, np.setdiff1d(np.arange(65536), a)))
+    return cases
+
+
+def test_run_and_run_split_windows(gpu):
+    """R AND R above the one-window LDS capacity (RB/RunContainer.java and(RunContainer)):
+    byte-identical AND / andCardinality / intersects."""
+    import roaringbitmap_amd as rb
+    from _fmt import R, encode
+    rng = np.random.default_rng(2558)
+    for label, x, y in _split_cases(rng):
+        bx = encode([(5, R, x), (9, R, y), (11, R, x)])
+        by = encode([(5, R, y), (9, R, x), (11, R, x)])
+        got = rb.RoaringBitmap.and_(rb.RoaringBitmap(bx), rb.RoaringBitmap(by)).serialize()
+        assert got == O.pairwise("and", bx, by), label
+        for op in ("and", "intersects"):
+            assert gpu_card(op, bx, by) == O.pairwise_card(op, bx, by), (label, op)
