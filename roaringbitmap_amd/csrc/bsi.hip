@@ -500,23 +500,33 @@ __global__ __launch_bounds__(256, RBG_BSI_WAVES) void k_bsi_reg(const Task* __re
   // this unit's key inputs: lane i holds input i (0 = ebM, 1 + x = bA[x], nb + 1 = foundSet);
   // the next unit's row is requested while this unit runs
   BsiIn e = lane < kBsiKin ? table[(wi / kBsiUnits) * kBsiKin + lane] : BsiIn{0, 0, -1};
+  // every bitmap slice word of a unit requested at once (slots through readlane); slice
+  // x's bit in the returned mask says it was loaded.  The next unit's words are
+  // requested as soon as this unit's slice registers are dead (after the circuit and
+  // the sum shares), so they are in flight during this unit's result store and count
+  // rows.
+  uint64_t sl[kBsiRegSlices];
+  auto request_slices = [&](const BsiIn& r, uint64_t unit) -> uint64_t {
+    const int wq = (int)((unit % kBsiUnits) * kUnitWords) + tid;
+    const uint32_t lo = (uint32_t)r.slot, hi = (uint32_t)(r.slot >> 32);
+    const bool bmp = r.didx >= 0 && (r.card_kind >> 24) == DK_B && (r.card_kind & 0xFFFFFF) != 65536;
+    const uint64_t m = __ballot(bmp && lane >= 1 && lane <= nb) >> 1;  // slice x at bit x
+#pragma unroll
+    for (int x = 0; x < kBsiRegSlices; x++) {
+      const uint64_t slot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, 1 + x) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 1 + x) << 32);
+      sl[x] = ((m >> x) & 1) ? reinterpret_cast<const uint64_t*>(A.payload + slot)[wq] : 0;
+    }
+    return m;
+  };
+  uint64_t bmask = request_slices(e, wi);
   for (;;) {
     const uint32_t t = (uint32_t)(wi / kBsiUnits), u = (uint32_t)(wi % kBsiUnits);
     const uint64_t wn = wi + gridDim.x;
     BsiIn en{0, 0, -1};
     if (wn < nunits && lane < kBsiKin) en = table[(wn / kBsiUnits) * kBsiKin + lane];
     const int w = (int)(u * kUnitWords) + tid;  // this thread's container word
-    // 1. every bitmap slice word of the unit requested at once (slots through readlane)
-    uint64_t sl[kBsiRegSlices];
     const uint32_t lo = (uint32_t)e.slot, hi = (uint32_t)(e.slot >> 32);
-    const bool bmp = e.didx >= 0 && (e.card_kind >> 24) == DK_B && (e.card_kind & 0xFFFFFF) != 65536;
-    const uint64_t bmask = __ballot(bmp && lane >= 1 && lane <= nb) >> 1;  // slice x at bit x
-#pragma unroll
-    for (int x = 0; x < kBsiRegSlices; x++) {
-      const uint64_t slot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, 1 + x) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 1 + x) << 32);
-      sl[x] = ((bmask >> x) & 1) ? reinterpret_cast<const uint64_t*>(A.payload + slot)[w] : 0;
-    }
     auto input_word = [&](int i) -> uint64_t {
       const uint64_t slot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, i) |
                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, i) << 32);
@@ -584,6 +594,9 @@ __global__ __launch_bounds__(256, RBG_BSI_WAVES) void k_bsi_reg(const Task* __re
       for (int x = 0; x < kBsiRegSlices; x++)
         if (x < nb) rec1(sl[x] & res, kRowSum + x, rows);
     }
+    // the slice registers are dead: the next unit's bitmap slices are requested now
+    uint64_t bmask_n = 0;
+    if (wn < nunits) bmask_n = request_slices(en, wn);
     // this unit's result words to the task's scratch slot (the container itself when
     // it is a bitmap, else the input k_bsi_defer stages it from)
     reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[w] = res;
@@ -598,6 +611,7 @@ __global__ __launch_bounds__(256, RBG_BSI_WAVES) void k_bsi_reg(const Task* __re
     if (wn >= nunits) break;
     wi = wn;
     e = en;
+    bmask = bmask_n;
   }
 }
 
