@@ -573,8 +573,7 @@ __device__ __forceinline__ uint32_t wave_and_card(const CDesc& x, const CDesc& y
     }
     wave_sync();
   }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  return c;
+  return (uint32_t)wave_sum_i((int)c);  // DPP reduction (no LDS permutes)
 }
 
 // Batched andCardinality, planned: one thread per pair aligns the (few) keys of
@@ -658,12 +657,12 @@ __device__ __forceinline__ void small_pair_load(const PairItem& it, const uint8_
 }
 __device__ __forceinline__ uint32_t small_arrays_and_card(const uint4 va, uint32_t ca, const uint4 vb, uint32_t cb,
                                                          uint32_t* lds, int lane) {
-  uint4* l4 = reinterpret_cast<uint4*>(lds);
-#pragma unroll
-  for (int i = 0; i < 8; i++) l4[64 * i + lane] = make_uint4(0, 0, 0, 0);
-  wave_sync();
+  // the map is all zero on entry and is left all zero: the words the scatter touched
+  // are cleared after the probe (at most 8 stores per lane instead of an 8 KiB clear)
   const bool a_map = ca >= cb;
-  scatter_vec<0, true>(lds, a_map ? va : vb, 8 * lane, (int)(a_map ? ca : cb));
+  const uint4 mv = a_map ? va : vb;
+  const int mcard = (int)(a_map ? ca : cb);
+  scatter_vec<0, true>(lds, mv, 8 * lane, mcard);
   wave_sync();
   const uint4 v = a_map ? vb : va;
   const int card = (int)(a_map ? cb : ca);
@@ -675,8 +674,19 @@ __device__ __forceinline__ uint32_t small_arrays_and_card(const uint4 va, uint32
     c += (8 * lane + i < card) ? ((lds[x >> 5] >> (x & 31)) & 1u) : 0u;
   }
   wave_sync();
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  return c;
+  const uint32_t mw[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+  for (int i = 0; i < 8; i++)
+    if (8 * lane + i < mcard) lds[((mw[i >> 1] >> ((i & 1) * 16)) & 0xFFFF) >> 5] = 0;
+  return (uint32_t)wave_sum_i((int)c);  // DPP reduction (no LDS permutes)
+}
+// the whole 8 KiB map cleared (k_pair_items: at the start, and after a key that took
+// the general path, which leaves the map dirty)
+__device__ __forceinline__ void clear_map(uint32_t* lds, int lane) {
+  uint4* l4 = reinterpret_cast<uint4*>(lds);
+#pragma unroll
+  for (int i = 0; i < 8; i++) l4[64 * i + lane] = make_uint4(0, 0, 0, 0);
+  wave_sync();
 }
 
 // one wave per matched key (resident grid), software-pipelined: while an item is
@@ -695,6 +705,7 @@ __global__ __launch_bounds__(256) void k_pair_items(const PairItem* __restrict__
   uint4 va, vb;
   bool pre = small_pair(cur);
   if (pre) small_pair_load(cur, payload, lane, va, vb);
+  clear_map(lds[w], lane);
   for (;;) {
     const uint64_t in = i + stride, in2 = in + stride;
     PairItem nxt2;
@@ -708,6 +719,7 @@ __global__ __launch_bounds__(256) void k_pair_items(const PairItem* __restrict__
     } else {
       const CDesc da{cur.slot_a, cur.card_a, 0, cur.kind_a, 0}, db{cur.slot_b, cur.card_b, 0, cur.kind_b, 0};
       c = wave_and_card(da, db, payload, lds[w], lane);
+      clear_map(lds[w], lane);
     }
     if (lane == 0 && c) atomicAdd(reinterpret_cast<uint32_t*>(out) + cur.pair, c);
     if (in >= n) break;
