@@ -583,16 +583,17 @@ __device__ __forceinline__ uint32_t wave_and_card(const CDesc& x, const CDesc& y
 constexpr uint32_t kSmallPairKeys = 64;
 
 // count (emit = false) or write (emit = true) the matched keys of pair p
+// off (EMIT): this pair's exclusive offsets, items | large pairs << 32
 template <bool EMIT>
 __device__ __forceinline__ uint64_t pair_matches(uint64_t p, const uint32_t* bm_off, const uint16_t* keys,
-                                                 const CDesc* desc, const uint64_t* off, PairItem* items,
+                                                 const CDesc* desc, uint64_t off, PairItem* items,
                                                  uint32_t* large) {
   const uint32_t a0 = bm_off[2 * p], a1 = bm_off[2 * p + 1], b1 = bm_off[2 * p + 2];
   if ((a1 - a0) + (b1 - a1) > kSmallPairKeys) {
-    if (EMIT) large[off[p] >> 32] = (uint32_t)p;
+    if (EMIT) large[off >> 32] = (uint32_t)p;
     return 1ull << 32;
   }
-  uint64_t q = EMIT ? (off[p] & 0xFFFFFFFFull) : 0;
+  uint64_t q = EMIT ? (off & 0xFFFFFFFFull) : 0;
   uint32_t ia = a0, ib = a1, m = 0;
   uint32_t ka = ia < a1 ? keys[ia] : 0, kb = ib < b1 ? keys[ib] : 0;
   while (ia < a1 && ib < b1) {
@@ -615,20 +616,88 @@ __device__ __forceinline__ uint64_t pair_matches(uint64_t p, const uint32_t* bm_
   return m;
 }
 
+// Plan of the items, per workgroup of 256 pairs: k_pairs_count writes each
+// workgroup's total (items | large pairs << 32: at most 16,384 | 256), one small
+// scan turns the totals into workgroup offsets, and k_pairs_emit aligns its pairs
+// again, scans their counts inside the workgroup and writes the items in pair order.
+// (A scan over the 1 M per-pair counts cost three launches over 8 MB.)
+__device__ __forceinline__ uint64_t block_sum_packed(uint64_t v, uint64_t* sh4, uint64_t* excl) {
+  // v = items | large << 32 with small parts: two DPP int scans
+  const int li = (int)(uint32_t)v, ll = (int)(v >> 32);
+  const int si = dpp_incl_scan(li), sl = dpp_incl_scan(ll);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) sh4[w] = (uint32_t)si | ((uint64_t)(uint32_t)sl << 32);
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    pre += i < w ? sh4[i] : 0;
+    tot += sh4[i];
+  }
+  *excl = pre + ((uint64_t)(uint32_t)(si - li) | ((uint64_t)(uint32_t)(sl - ll) << 32));
+  return tot;
+}
+
 __global__ __launch_bounds__(256) void k_pairs_count(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
-                                                     const uint16_t* __restrict__ keys, uint64_t* __restrict__ cnt) {
+                                                     const uint16_t* __restrict__ keys, uint64_t* __restrict__ blk) {
+  __shared__ uint64_t sh4[4];
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < n_pairs) cnt[p] = pair_matches<false>(p, bm_off, keys, nullptr, nullptr, nullptr, nullptr);
+  const uint64_t v = p < n_pairs ? pair_matches<false>(p, bm_off, keys, nullptr, 0, nullptr, nullptr) : 0;
+  uint64_t ex;
+  const uint64_t tot = block_sum_packed(v, sh4, &ex);
+  if (threadIdx.x == 0) blk[blockIdx.x] = tot;
+}
+
+// exclusive scan of the workgroup totals in place (one workgroup of 1024 threads,
+// four per thread per round); *tot = items | large << 32
+__global__ __launch_bounds__(1024) void k_pairs_scan(uint64_t* __restrict__ blk, uint64_t nblk,
+                                                    uint64_t* __restrict__ tot) {
+  __shared__ uint64_t sw[16];
+  uint64_t carry = 0;
+  for (uint64_t b0 = 0; b0 < nblk; b0 += 4 * 1024) {
+    const uint64_t i0 = b0 + 4 * (uint64_t)threadIdx.x;
+    uint64_t v[4], s = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      v[j] = i0 + j < nblk ? blk[i0 + j] : 0;
+      s += v[j];
+    }
+    const int li = (int)(uint32_t)s, ll = (int)(s >> 32);
+    const int si = dpp_incl_scan(li), sl = dpp_incl_scan(ll);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 63) sw[w] = (uint32_t)si | ((uint64_t)(uint32_t)sl << 32);
+    __syncthreads();
+    uint64_t pre = 0, all = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      pre += i < w ? sw[i] : 0;
+      all += sw[i];
+    }
+    uint64_t run = carry + pre + ((uint64_t)(uint32_t)(si - li) | ((uint64_t)(uint32_t)(sl - ll) << 32));
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      if (i0 + j < nblk) blk[i0 + j] = run;
+      run += v[j];
+    }
+    carry += all;
+  }
+  if (threadIdx.x == 0) *tot = carry;
 }
 
 __global__ __launch_bounds__(256) void k_pairs_emit(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
                                                     const uint16_t* __restrict__ keys, const CDesc* __restrict__ desc,
-                                                    const uint64_t* __restrict__ off, PairItem* __restrict__ items,
+                                                    const uint64_t* __restrict__ blk, PairItem* __restrict__ items,
                                                     uint32_t* __restrict__ large, int32_t* __restrict__ out) {
+  __shared__ uint64_t sh4[4];
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n_pairs) return;
+  const bool ok = p < n_pairs;
+  const uint64_t v = ok ? pair_matches<false>(p, bm_off, keys, nullptr, 0, nullptr, nullptr) : 0;
+  uint64_t ex;
+  block_sum_packed(v, sh4, &ex);
+  if (!ok) return;
   out[p] = 0;
-  pair_matches<true>(p, bm_off, keys, desc, off, items, large);
+  if (v) pair_matches<true>(p, bm_off, keys, desc, blk[blockIdx.x] + ex, items, large);
 }
 
 __device__ __forceinline__ PairItem load_item(const PairItem* items, uint64_t i) {
@@ -767,8 +836,9 @@ void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_o
                            uint64_t* tot, PairItem* items, uint32_t* large) {
   if (n_pairs == 0) return;
   const unsigned g = (unsigned)((n_pairs + 255) / 256);
+  (void)part;
   hipLaunchKernelGGL(k_pairs_count, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, cnt);
-  launch_exclusive_scan(s, cnt, cnt, n_pairs, part, tot);
+  hipLaunchKernelGGL(k_pairs_scan, dim3(1), dim3(1024), 0, s, cnt, (uint64_t)g, tot);
   hipLaunchKernelGGL(k_pairs_emit, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, desc, (const uint64_t*)cnt, items,
                      large, out);
   hipLaunchKernelGGL(k_pair_items, dim3(resident_grid((const void*)&k_pair_items)), dim3(256), 0, s,
