@@ -760,58 +760,54 @@ __device__ __forceinline__ void clear_map(uint32_t* lds, int lane) {
 
 // one wave per matched key (resident grid), software-pipelined: while an item is
 // counted, the next item's payload vectors (small arrays) are already in flight and
-// the record after that is loaded through the scalar cache; sums wrap like Java ints
+// the record after that is loaded through the scalar cache; sums wrap like Java ints.
+// Then the pairs of more than kSmallPairKeys keys, one wave each merging the two key
+// arrays itself (in the same launch: a separate one cost ~5 us even with none).
 __global__ __launch_bounds__(256) void k_pair_items(const PairItem* __restrict__ items, const uint64_t* __restrict__ tot,
-                                                    const uint8_t* __restrict__ payload, int32_t* __restrict__ out) {
+                                                    const uint8_t* __restrict__ payload, int32_t* __restrict__ out,
+                                                    const uint32_t* __restrict__ large,
+                                                    const uint32_t* __restrict__ bm_off,
+                                                    const CDesc* __restrict__ desc) {
   __shared__ __align__(16) uint32_t lds[4][2048];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t n = *tot & 0xFFFFFFFFull;
+  const uint64_t n = *tot & 0xFFFFFFFFull, n_large = *tot >> 32;
   const uint64_t stride = (uint64_t)gridDim.x * 4;
-  uint64_t i = (uint64_t)blockIdx.x * 4 + w;
-  if (i >= n) return;
-  PairItem cur = load_item(items, i), nxt;
-  if (i + stride < n) nxt = load_item(items, i + stride);
-  uint4 va, vb;
-  bool pre = small_pair(cur);
-  if (pre) small_pair_load(cur, payload, lane, va, vb);
-  clear_map(lds[w], lane);
-  for (;;) {
-    const uint64_t in = i + stride, in2 = in + stride;
-    PairItem nxt2;
-    if (in2 < n) nxt2 = load_item(items, in2);
-    uint4 na, nb;
-    const bool npre = in < n && small_pair(nxt);
-    if (npre) small_pair_load(nxt, payload, lane, na, nb);  // in flight while this item is counted
-    uint32_t c;
-    if (pre) {
-      c = small_arrays_and_card(va, cur.card_a, vb, cur.card_b, lds[w], lane);
-    } else {
-      const CDesc da{cur.slot_a, cur.card_a, 0, cur.kind_a, 0}, db{cur.slot_b, cur.card_b, 0, cur.kind_b, 0};
-      c = wave_and_card(da, db, payload, lds[w], lane);
-      clear_map(lds[w], lane);
+  const uint64_t wid = (uint64_t)blockIdx.x * 4 + w;
+  uint64_t i = wid;
+  if (i < n) {
+    PairItem cur = load_item(items, i), nxt;
+    if (i + stride < n) nxt = load_item(items, i + stride);
+    uint4 va, vb;
+    bool pre = small_pair(cur);
+    if (pre) small_pair_load(cur, payload, lane, va, vb);
+    clear_map(lds[w], lane);
+    for (;;) {
+      const uint64_t in = i + stride, in2 = in + stride;
+      PairItem nxt2;
+      if (in2 < n) nxt2 = load_item(items, in2);
+      uint4 na, nb;
+      const bool npre = in < n && small_pair(nxt);
+      if (npre) small_pair_load(nxt, payload, lane, na, nb);  // in flight while this item is counted
+      uint32_t c;
+      if (pre) {
+        c = small_arrays_and_card(va, cur.card_a, vb, cur.card_b, lds[w], lane);
+      } else {
+        const CDesc da{cur.slot_a, cur.card_a, 0, cur.kind_a, 0}, db{cur.slot_b, cur.card_b, 0, cur.kind_b, 0};
+        c = wave_and_card(da, db, payload, lds[w], lane);
+        clear_map(lds[w], lane);
+      }
+      if (lane == 0 && c) atomicAdd(reinterpret_cast<uint32_t*>(out) + cur.pair, c);
+      if (in >= n) break;
+      i = in;
+      cur = nxt;
+      nxt = nxt2;
+      pre = npre;
+      va = na;
+      vb = nb;
     }
-    if (lane == 0 && c) atomicAdd(reinterpret_cast<uint32_t*>(out) + cur.pair, c);
-    if (in >= n) break;
-    i = in;
-    cur = nxt;
-    nxt = nxt2;
-    pre = npre;
-    va = na;
-    vb = nb;
   }
-}
-
-__global__ __launch_bounds__(256) void k_batch_and_card_large(const uint32_t* __restrict__ large,
-                                                              const uint64_t* __restrict__ tot,
-                                                              const uint32_t* __restrict__ bm_off,
-                                                              const CDesc* __restrict__ desc,
-                                                              const uint8_t* __restrict__ payload,
-                                                              int32_t* __restrict__ out) {
-  __shared__ __align__(16) uint32_t lds[4][2048];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t n = *tot >> 32;
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + w; i < n; i += (uint64_t)gridDim.x * 4) {
-    const uint32_t p = large[i];
+  for (uint64_t j = wid; j < n_large; j += stride) {
+    const uint32_t p = large[j];
     uint32_t ia = bm_off[2 * p], a1 = bm_off[2 * p + 1];
     uint32_t ib = a1, b1 = bm_off[2 * p + 2];
     uint32_t sum = 0;
@@ -842,9 +838,7 @@ void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_o
   hipLaunchKernelGGL(k_pairs_emit, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, desc, (const uint64_t*)cnt, items,
                      large, out);
   hipLaunchKernelGGL(k_pair_items, dim3(resident_grid((const void*)&k_pair_items)), dim3(256), 0, s,
-                     (const PairItem*)items, (const uint64_t*)tot, payload, out);
-  hipLaunchKernelGGL(k_batch_and_card_large, dim3(1024), dim3(256), 0, s, (const uint32_t*)large,
-                     (const uint64_t*)tot, bm_off, desc, payload, out);
+                     (const PairItem*)items, (const uint64_t*)tot, payload, out, (const uint32_t*)large, bm_off, desc);
 }
 
 // upper bound of the items of a batch: sum over small pairs of min(keys of a, keys of b)
