@@ -1325,7 +1325,7 @@ static int ctx_batch_card(Ctx* c, int32_t id) {
     B->pair_items_cap = batch_pair_items_cap(B->h_bm_nctr.data(), np);
     B->pair_cap_known = true;
   }
-  CHK(c->pc_cnt.ensure(8 * std::max<size_t>(np, 1)));
+  CHK(c->pc_cnt.ensure(8 * ((np + 255) / 256) + std::max<size_t>(np, 1) + 16));  // workgroup totals + a count byte per pair
   CHK(c->pc_part.ensure(8 * (scan_parts(std::max<size_t>(np, 1)) + 1)));
   CHK(c->pc_items.ensure(sizeof(PairItem) * std::max<uint64_t>(B->pair_items_cap, 1)));
   CHK(c->pc_large.ensure(4 * std::max<size_t>(np, 1)));

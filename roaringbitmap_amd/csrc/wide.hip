@@ -638,11 +638,16 @@ __device__ __forceinline__ uint64_t block_sum_packed(uint64_t v, uint64_t* sh4, 
   return tot;
 }
 
+// pc[p]: the pair's matched keys (<= 32 for a small pair), 0xFF for a large pair
+__device__ __forceinline__ uint64_t unpack_pc(uint8_t c) { return c == 0xFF ? 1ull << 32 : (uint64_t)c; }
+
 __global__ __launch_bounds__(256) void k_pairs_count(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
-                                                     const uint16_t* __restrict__ keys, uint64_t* __restrict__ blk) {
+                                                     const uint16_t* __restrict__ keys, uint64_t* __restrict__ blk,
+                                                     uint8_t* __restrict__ pc) {
   __shared__ uint64_t sh4[4];
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t v = p < n_pairs ? pair_matches<false>(p, bm_off, keys, nullptr, 0, nullptr, nullptr) : 0;
+  if (p < n_pairs) pc[p] = (v >> 32) ? (uint8_t)0xFF : (uint8_t)v;
   uint64_t ex;
   const uint64_t tot = block_sum_packed(v, sh4, &ex);
   if (threadIdx.x == 0) blk[blockIdx.x] = tot;
@@ -687,12 +692,13 @@ __global__ __launch_bounds__(1024) void k_pairs_scan(uint64_t* __restrict__ blk,
 
 __global__ __launch_bounds__(256) void k_pairs_emit(uint64_t n_pairs, const uint32_t* __restrict__ bm_off,
                                                     const uint16_t* __restrict__ keys, const CDesc* __restrict__ desc,
-                                                    const uint64_t* __restrict__ blk, PairItem* __restrict__ items,
-                                                    uint32_t* __restrict__ large, int32_t* __restrict__ out) {
+                                                    const uint64_t* __restrict__ blk, const uint8_t* __restrict__ pc,
+                                                    PairItem* __restrict__ items, uint32_t* __restrict__ large,
+                                                    int32_t* __restrict__ out) {
   __shared__ uint64_t sh4[4];
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool ok = p < n_pairs;
-  const uint64_t v = ok ? pair_matches<false>(p, bm_off, keys, nullptr, 0, nullptr, nullptr) : 0;
+  const uint64_t v = ok ? unpack_pc(pc[p]) : 0;  // only pairs with matches are aligned again
   uint64_t ex;
   block_sum_packed(v, sh4, &ex);
   if (!ok) return;
@@ -832,11 +838,13 @@ void launch_batch_and_card(hipStream_t s, uint64_t n_pairs, const uint32_t* bm_o
                            uint64_t* tot, PairItem* items, uint32_t* large) {
   if (n_pairs == 0) return;
   const unsigned g = (unsigned)((n_pairs + 255) / 256);
+  // cnt holds the workgroup totals (g u64), then one count byte per pair
+  uint8_t* pc = reinterpret_cast<uint8_t*>(cnt + g);
   (void)part;
-  hipLaunchKernelGGL(k_pairs_count, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, cnt);
+  hipLaunchKernelGGL(k_pairs_count, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, cnt, pc);
   hipLaunchKernelGGL(k_pairs_scan, dim3(1), dim3(1024), 0, s, cnt, (uint64_t)g, tot);
-  hipLaunchKernelGGL(k_pairs_emit, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, desc, (const uint64_t*)cnt, items,
-                     large, out);
+  hipLaunchKernelGGL(k_pairs_emit, dim3(g), dim3(256), 0, s, n_pairs, bm_off, keys, desc, (const uint64_t*)cnt,
+                     (const uint8_t*)pc, items, large, out);
   hipLaunchKernelGGL(k_pair_items, dim3(resident_grid((const void*)&k_pair_items)), dim3(256), 0, s,
                      (const PairItem*)items, (const uint64_t*)tot, payload, out, (const uint32_t*)large, bm_off, desc);
 }
