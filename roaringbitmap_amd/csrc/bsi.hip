@@ -448,22 +448,32 @@ struct BsiIn {
   uint32_t card_kind;  // card | kind << 24
   int32_t didx;        // desc index, -1 when the key has no container of this input
 };
+// One wave per key (4 keys per workgroup): lane j takes the key segment's container
+// j, so the segment is read in one round instead of a serial walk per thread.
 __global__ __launch_bounds__(256) void k_bsi_table(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                                    WideArgs A, BsiIn* __restrict__ table) {
+  __shared__ unsigned long long present[4];
   const uint32_t nt = *n_tasks;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nt) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t t = blockIdx.x * 4 + w;
+  if (t >= nt) return;  // wave-uniform
   const Task tk = tasks[t];
   BsiIn* row = table + (size_t)t * kBsiKin;
-  for (int i = 0; i < kBsiKin; i++) row[i] = BsiIn{0, 0, -1};
-  for (uint32_t j = 0; j < (uint32_t)tk.b; j++) {
+  if (lane == 0) present[w] = 0;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  for (uint32_t j = (uint32_t)lane; j < (uint32_t)tk.b; j += 64) {
     const uint32_t p = (uint32_t)tk.a + j;
     const uint32_t b = A.bm[p];
     if (b < (uint32_t)kBsiKin) {
       const CDesc d = A.desc[p];
       row[b] = BsiIn{d.slot, d.card | ((uint32_t)d.kind << 24), (int32_t)p};
+      atomicOr(&present[w], 1ull << b);
     }
   }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (lane < kBsiKin && !((present[w] >> lane) & 1)) row[lane] = BsiIn{0, 0, -1};  // the key has no container of input lane
 }
 
 // Word w of a key's input from its table entry: a full container needs no memory
@@ -615,49 +625,57 @@ __global__ __launch_bounds__(256, RBG_BSI_WAVES) void k_bsi_reg(const Task* __re
   }
 }
 
-// Types of the keys k_bsi_reg computed, one THREAD per key (64-thread blocks): the
-// key's counts (the units' partials added) and input types are first staged in LDS
-// -- every load independent, all in flight together -- then the reference's type
-// rule of every step is replayed from them with branch-free selects, and the result
-// record written.  A bitmap result is already in the scratch slot; array / run
+// Types of the keys k_bsi_reg computed, one THREAD per key (64 keys per 256-thread
+// block): the keys' counts (the units' partials added) and input types are first
+// staged in LDS by all four waves -- every load independent -- then the reference's
+// type rule of every step is replayed from them with branch-free selects, 16 keys per
+// wave (the replay is a serial chain per key: spread over four times the waves it
+// ends sooner), and the result record written.  A bitmap result is already in the scratch slot; array / run
 // results (staged from it) and keys whose replay needs a run count go to
 // k_bsi_defer.  Sums: per slice one wave reduction, one atomic.
 struct LdsCounts {
   const int* col;  // this lane's column of the staged counts (row stride 64)
   __device__ __forceinline__ int operator()(int r) const { return col[r * 64]; }
 };
-__global__ __launch_bounds__(64) void k_bsi_types(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
-                                                  WideArgs A, BsiArgs P, OutCtx oc,
-                                                  unsigned long long* __restrict__ sums, const int* __restrict__ cnts,
-                                                  const TB* __restrict__ kin, size_t tstride,
-                                                  uint32_t* __restrict__ defer) {
+__global__ __launch_bounds__(256) void k_bsi_types(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                   WideArgs A, BsiArgs P, OutCtx oc,
+                                                   unsigned long long* __restrict__ sums, const int* __restrict__ cnts,
+                                                   const TB* __restrict__ kin, size_t tstride,
+                                                   uint32_t* __restrict__ defer) {
   __shared__ int lc[kBsiRows * 64];
   __shared__ TB lk[kBsiKin * 64];
   const uint32_t nt = *n_tasks;
   const int nb = P.nbits;
   const bool two = P.op == BSI_RANGE;
-  const int lane = threadIdx.x;
-  const uint32_t t = blockIdx.x * 64 + lane;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t ts = blockIdx.x * 64 + lane;  // staging: lane = key of the block
   if (uni(blockIdx.x * 64) >= nt) return;
-  const bool live = t < nt;
-  const uint32_t tt = live ? t : 0;
-#pragma unroll 8
-  for (int r = 0; r < kBsiRows; r++) {
+  const uint32_t tt = ts < nt ? ts : 0;
+  // the block's four waves stage the 64 keys' rows (every fourth row each: four times
+  // the loads in flight of a lone wave)
+#pragma unroll 4
+  for (int r = wv; r < kBsiRows; r += 4) {
     int c = 0;
 #pragma unroll
     for (int u = 0; u < kBsiUnits; u++) c += cnts[((size_t)r * kBsiUnits + u) * tstride + tt];
     lc[r * 64 + lane] = c;
   }
-#pragma unroll 8
-  for (int i = 0; i < kBsiKin; i++) lk[i * 64 + lane] = kin[(size_t)i * tstride + tt];
-  const LdsCounts tv{lc + lane};
-  const TB ebmT = lk[kBsiRegSlices * 64 + lane];
-  const TB fixT = lk[(kBsiRegSlices + 1) * 64 + lane];
+#pragma unroll 4
+  for (int i = wv; i < kBsiKin; i += 4) lk[i * 64 + lane] = kin[(size_t)i * tstride + tt];
+  __syncthreads();
+  // replay: 16 keys per wave, all four waves (the type chain is serial per key, so
+  // four times the waves of a key-per-lane replay finish about four times sooner)
+  const int kl = 16 * wv + (lane & 15);
+  const uint32_t tk_ = blockIdx.x * 64 + kl;
+  const bool live2 = lane < 16 && tk_ < nt;
+  const LdsCounts tv{lc + kl};
+  const TB ebmT = lk[kBsiRegSlices * 64 + kl];
+  const TB fixT = lk[(kBsiRegSlices + 1) * 64 + kl];
   int slow = 0;
   CircuitT z0{tb_absent(), tb_absent(), ebmT, 0, 0, tv(kRowEbm)}, z1 = z0;
 #pragma unroll 1
   for (int i = nb - 1; i >= 0; i--) {
-    const TB sT = lk[i * 64 + lane];
+    const TB sT = lk[i * 64 + kl];
     types_step((P.pred0 >> i) & 1, sT, z0, step_row(i, 0), tv, slow);
     if (two) types_step((P.pred1 >> i) & 1, sT, z1, step_row(i, 1), tv, slow);
   }
@@ -669,17 +687,25 @@ __global__ __launch_bounds__(64) void k_bsi_types(const Task* __restrict__ tasks
   } else {
     rt = types_finish(P.op, fixT, z0, kRowFin, kRowFin + 1, tv, slow);
   }
-  const bool ok = live && !slow;
-  if (sums) {
+  const bool ok = live2 && !slow;
+  if (sums) {  // per slice: a wave sum, the block's four added in LDS, one atomic per block
+    __shared__ int bs[kBsiRegSlices + 1][4];
     const bool add = ok && rt.card > 0;
     for (int x = 0; x < nb; x++) {
       const int c = wave_sum(add ? tv(kRowSum + x) : 0);
-      if (lane == 0 && c) atomicAdd(&sums[x], (unsigned long long)(uint32_t)c);
+      if (lane == 0) bs[x][wv] = c;
     }
     const int cc = wave_sum(add ? rt.card : 0);
-    if (lane == 0 && cc) atomicAdd(&sums[kBsiMaxInputs], (unsigned long long)(uint32_t)cc);
+    if (lane == 0) bs[kBsiRegSlices][wv] = cc;
+    __syncthreads();
+    if (threadIdx.x <= (unsigned)kBsiRegSlices && ((int)threadIdx.x < nb || threadIdx.x == kBsiRegSlices)) {
+      const int x = threadIdx.x;
+      const int c = bs[x][0] + bs[x][1] + bs[x][2] + bs[x][3];
+      if (c) atomicAdd(&sums[x == kBsiRegSlices ? kBsiMaxInputs : x], (unsigned long long)(uint32_t)c);
+    }
   }
-  if (!live) return;
+  if (!live2) return;
+  const uint32_t t = tk_;
   if (slow) {  // a step's type needs its run count: k_bsi_defer redoes this key
     defer[1 + atomicAdd(defer, 1u)] = t | 0x80000000u;
     return;
@@ -739,14 +765,14 @@ void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, 
                 unsigned long long* sums, BsiScratch* sc) {
   if (p.op <= BSI_RANGE && p.nbits <= kBsiRegSlices && sc) {
     (void)hipMemsetAsync(sc->defer, 0, 4, s);
-    hipLaunchKernelGGL(k_bsi_table, dim3((unsigned)((sc->stride + 255) / 256)), dim3(256), 0, s, tasks, nt, args,
+    hipLaunchKernelGGL(k_bsi_table, dim3((unsigned)((sc->stride + 3) / 4)), dim3(256), 0, s, tasks, nt, args,
                        reinterpret_cast<BsiIn*>(sc->table));
     const int g = std::max(1, std::min(grid * kBsiUnits, resident_grid((const void*)&k_bsi_reg)));
     hipLaunchKernelGGL(k_bsi_reg, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc, sums != nullptr,
                        reinterpret_cast<const BsiIn*>(sc->table), sc->cnts,
                        reinterpret_cast<TB*>(sc->kin), sc->stride);
     const int g2 = (int)((sc->stride + 63) / 64);
-    hipLaunchKernelGGL(k_bsi_types, dim3(g2), dim3(64), 0, s, tasks, nt, args, p, oc, sums, sc->cnts,
+    hipLaunchKernelGGL(k_bsi_types, dim3(g2), dim3(256), 0, s, tasks, nt, args, p, oc, sums, sc->cnts,
                        reinterpret_cast<const TB*>(sc->kin), sc->stride, sc->defer);
     const int g3 = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_defer)));
     hipLaunchKernelGGL(k_bsi_defer, dim3(g3), dim3(256), 0, s, tasks, sc->defer, args, p, oc, sums);
