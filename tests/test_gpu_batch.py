@@ -67,3 +67,29 @@ def test_batch_and_card_large_and_mixed_pairs(gpu):
     got = rb.batch_and_cardinality([(rb.RoaringBitmap(a), rb.RoaringBitmap(b)) for a, b in pairs])
     exp = np.array([O.pairwise_card("and", a, b) for a, b in pairs], dtype=np.int32)
     np.testing.assert_array_equal(got, exp)
+
+
+def test_batch_and_card_threshold_pairs(gpu):
+    """Pairs at the small-pair bound (64 keys in all): 32 + 32 identical keys give the most
+    matched keys a small pair can have (32, one count byte); 33 + 32 keys go the large
+    path; many such pairs span several plan workgroups (256 pairs each)."""
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(6464)
+    pairs = []
+    for i in range(700):
+        m = i % 5
+        if m == 0:
+            ka = kb = np.arange(32) * 3
+        elif m == 1:
+            ka, kb = np.arange(33) * 2, np.arange(32) * 2
+        elif m == 2:
+            ka, kb = np.arange(40), np.arange(24) + 16
+        elif m == 3:
+            ka, kb = np.sort(rng.choice(100, size=31, replace=False)), np.sort(rng.choice(100, size=33, replace=False))
+        else:
+            ka, kb = np.array([7]), np.array([7])
+        pairs.append((_gen.bitmap(rng, ka, modes=["a_tiny", "a_small"], p_present=1.0),
+                      _gen.bitmap(rng, kb, modes=["a_tiny", "a_small"], p_present=1.0)))
+    got = rb.batch_and_cardinality([(rb.RoaringBitmap(a), rb.RoaringBitmap(b)) for a, b in pairs])
+    exp = np.array([O.pairwise_card("and", a, b) for a, b in pairs], dtype=np.int32)
+    np.testing.assert_array_equal(got, exp)
