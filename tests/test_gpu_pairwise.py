@@ -251,3 +251,30 @@ def test_run_and_run_split_windows(gpu):
         assert got == O.pairwise("and", bx, by), label
         for op in ("and", "intersects"):
             assert gpu_card(op, bx, by) == O.pairwise_card(op, bx, by), (label, op)
+
+
+@pytest.mark.parametrize("nruns", [3000, 9000, 32768])
+def test_many_run_inputs_all_ops(gpu, nruns):
+    """Input run containers with far more than 2047 runs (the deserializer accepts up to
+    32768: alternating bits) against arrays, bitmaps and run containers, every op and
+    cardinality: the run lists stream past the per-lane vectors and the R maps / bitmap
+    materialisation take them whole."""
+    from _fmt import A, B, R, encode
+    rng = np.random.default_rng(nruns)
+    if nruns == 32768:
+        many = np.arange(0, 65536, 2)
+    else:
+        many = _run_vals(rng, nruns)
+    others = [
+        (A, np.sort(rng.choice(65536, size=3000, replace=False))),
+        (A, np.sort(rng.choice(65536, size=40, replace=False))),
+        (B, np.sort(rng.choice(65536, size=30000, replace=False))),
+        (R, _run_vals(rng, 700)),
+        (R, _run_vals(rng, 2500)),
+        (R, np.arange(1, 65536, 2)),
+    ]
+    for kind, vals in others:
+        x = encode([(2, R, many), (4, kind, vals), (6, R, many)])
+        y = encode([(2, kind, vals), (4, R, many), (5, kind, vals)])
+        check_all(x, y, f"R{nruns} x {kind}")
+        check_all(y, x, f"{kind} x R{nruns}")
