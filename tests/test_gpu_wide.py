@@ -153,3 +153,38 @@ def test_buffer_fast_aggregation_dispatch(gpu, n):
         assert B.and_(buf, *bms).serialize() == ws
         with pytest.raises(rb.IllegalArgumentException):
             B.and_(np.zeros(10, dtype=np.int64), *bms)
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 11])
+def test_wide_many_run_inputs(gpu, n):
+    """Wide ops over inputs whose run containers hold 2,500 - 32,768 runs (beyond any
+    per-lane staging), mixed with arrays and bitmaps on the same keys: naive_or's single
+    input pass-through (R -> EFF), the lazy OR, the naive_xor chain replay with runs,
+    workShyAnd / naive_and."""
+    from _fmt import A, B, R, encode
+    rng = np.random.default_rng(900 + n)
+
+    def runs(k):
+        seg = 65536 // k
+        st = np.arange(k) * seg + rng.integers(0, max(1, seg // 2), k)
+        return np.unique(np.concatenate([np.arange(s, min(s + 1 + int(rng.integers(0, max(1, seg // 2))), 65536))
+                                         for s in st]))
+    bufs = []
+    for i in range(n):
+        ctrs = []
+        for key in (1, 3, 8):
+            m = (i + key) % 4
+            if m == 0:
+                ctrs.append((key, R, np.arange(i % 2, 65536, 2)))  # 32,768 runs
+            elif m == 1:
+                ctrs.append((key, R, runs(2500 + 1000 * i)))
+            elif m == 2:
+                ctrs.append((key, A, np.sort(rng.choice(65536, size=2000, replace=False))))
+            else:
+                ctrs.append((key, B, np.sort(rng.choice(65536, size=20000, replace=False))))
+        bufs.append(encode(ctrs))
+    for op in ["or", "xor", "and", "and_iter", "naive_and"]:
+        _cmp(op, bufs, list(range(n)))
+    _cmp("workshy_and", bufs)
+    for op in ["and", "or"]:
+        assert gpu_wide_card(op, bufs) == O.wide_card(op, bufs), op
