@@ -437,7 +437,28 @@ def main():
     eng.profile(0)
     ph_avg = [x / max(n_ops, 1) for x in ph]
 
+    # the headline's cross-rank reduction first: the extras below cannot lose it
+    t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device=cdev)
+    if dist is not None:
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        tsum = t.clone()
+        dist.all_reduce(tsum[1:], op=dist.ReduceOp.SUM)
+        wall_max, total_in = float(tmax[0]), float(tsum[1])
+    else:
+        wall_max, total_in = wall, float(in_bytes)
+
     extra = {}
+
+    def run_extra(name, fn):
+        # an extra that raises (on every rank alike) is reported in its entry instead of
+        # ending the run without the headline line
+        try:
+            extra[name] = fn()
+        except Exception as e:  # noqa: BLE001
+            print(f"bench: extra {name} failed: {e!r}", file=sys.stderr)
+            extra[name] = {"error": repr(e)}
+
     # RoaringBitmap.andCardinality on the same pair: the same input bytes,
     # no result containers
     for _ in range(args.warmup):
@@ -461,33 +482,23 @@ def main():
                      "achieved_GBps": round(in_bytes / (card_kern / 1e3) / 1e9, 1),
                      "frac": round(in_bytes / (card_kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": _pmc_traffic("k_pair_wave_card")}}
+    ks = max(3, args.steps // 4)
     if args.c3_n > 0:
         for kind, name in ((1, "c3_uniform_or"), (2, "c3_clustered_or")):
-            extra[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev)
+            run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, 1, cdev))
         # FastAggregation.and (N > 10: workShyAnd): per key the chain stops once the
         # intersection is empty, so it reads far less than the algorithmic input bytes
         for kind, name in ((1, "c3_uniform_and"), (2, "c3_clustered_and")):
-            extra[name] = c3_wide_or(eng, kind, args.c3_n, rank, world, dist, max(3, args.steps // 4), 1, cdev,
-                                     op="and")
+            run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, 1, cdev,
+                                                         op="and"))
     if args.c4_pairs > 0:
-        extra["c4_batch_and_card"] = c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, max(3, args.steps // 4),
-                                                       1, cdev)
+        run_extra("c4_batch_and_card", lambda: c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, ks, 1, cdev))
     if args.c5_rows > 0:
-        extra["c5_bsi_range_sum"] = c5_bsi(eng, args.c5_rows, rank, world, dist, max(3, args.steps // 4), 1, cdev)
+        run_extra("c5_bsi_range_sum", lambda: c5_bsi(eng, args.c5_rows, rank, world, dist, ks, 1, cdev))
 
     if args.c3_n > 0 or args.c4_pairs > 0 or args.c5_rows > 0:
-        extra["run_optimize_c2"] = run_optimize_c2(eng, a, sa, max(3, args.steps // 4))
-        extra["decode_c2"] = decode_c2(eng, a, max(3, args.steps // 4))
-
-    t = torch.tensor([wall, float(in_bytes)], dtype=torch.float64, device=cdev)
-    if dist is not None:
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum[1:], op=dist.ReduceOp.SUM)
-        wall_max, total_in = float(tmax[0]), float(tsum[1])
-    else:
-        wall_max, total_in = wall, float(in_bytes)
+        run_extra("run_optimize_c2", lambda: run_optimize_c2(eng, a, sa, ks))
+        run_extra("decode_c2", lambda: decode_c2(eng, a, ks))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
