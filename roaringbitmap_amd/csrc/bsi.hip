@@ -257,9 +257,6 @@ __global__ __launch_bounds__(256) void k_bsi(const Task* __restrict__ tasks, con
 //    the reference's type rule of every step (see there).
 // A key whose replay needs a run count (EFF) is redone by k_bsi_defer with the
 // streamed form; array / run results are staged there from the bits.
-#ifndef RBG_BSI_WAVES
-#define RBG_BSI_WAVES 4  // waves per SIMD k_bsi_reg is compiled for
-#endif
 constexpr int kBsiRegSlices = 32;
 constexpr int kBsiUnits = 4;                // units per key
 constexpr int kUnitWords = 1024 / kBsiUnits;  // container words per unit = threads per workgroup
@@ -490,7 +487,7 @@ __device__ __forceinline__ uint64_t in_word(uint64_t slot, uint32_t card_kind, i
 // compare ops (BSI_EQ .. BSI_RANGE) with nbits <= kBsiRegSlices.  cnts: per count row,
 // kBsiUnits partial rows of one int per task; kin: kBsiKin rows of one input type per
 // task (slices, ebM, the fixed found set); both transposed with row stride `tstride`.
-__global__ __launch_bounds__(256, RBG_BSI_WAVES) void k_bsi_reg(const Task* __restrict__ tasks,
+__global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tasks,
                                                                 const uint32_t* __restrict__ n_tasks,
                                                  WideArgs A, BsiArgs P, OutCtx oc, bool want_sum,
                                                  const BsiIn* __restrict__ table, int* __restrict__ cnts,

@@ -42,7 +42,7 @@ static void set_err(const std::string& s) { g_err = s; }
 
 constexpr size_t kSlack = 256;  // every device buffer carries read slack (group_copy)
 constexpr int kMaxKeys = 65536;
-constexpr size_t kLbHeader = 256;  // look-back state: ticket @0, error @64, result card @96, tile ticket @128
+constexpr size_t kLbHeader = 256;  // look-back state: error @64, result card @96, fused pairwise totals @192
 constexpr size_t kMaxTiles = 128;  // tile statuses follow the 65536 task statuses
 
 // RBG_DEBUG_SYNC=1: synchronise and report after every pipeline stage (debugging aid)
@@ -138,6 +138,7 @@ struct Ctx {
   int bsi_nbits = 0;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw,
       scalar, scratch;
+  DevBuf pw_state;  // fused pairwise placement state (kernels.hpp)
   size_t result_cap = 0;
   OutCtx pending{};         // output state of the last materialising op
   std::vector<int32_t> pending_src;  // batches the pending result's pass-through records point into
@@ -193,6 +194,7 @@ static int ctx_init(Ctx* c, int device) {
   HIPCHK(hipMemset(c->wg_epoch.p, 0, 8 * 256));
   CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + 2 * kMaxTiles)));
   CHK(c->recs.ensure(sizeof(ORec) * kMaxKeys));
+  CHK(c->pw_state.ensure(kPwStateBytes));
   CHK(c->kind_by_out.ensure(kMaxKeys));
   CHK(c->scalar.ensure(64));
   CHK(c->info.ensure(sizeof(ResultInfo)));
@@ -512,9 +514,7 @@ static int grid_for(size_t tasks, size_t cap = 4096) {
 static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc, bool card_only) {
   uint8_t* lb = c->lb.as<uint8_t>();
   *oc = OutCtx{};
-  oc->ticket = reinterpret_cast<uint32_t*>(lb);
   oc->err = reinterpret_cast<uint32_t*>(lb + 64);
-  oc->tile_ticket = reinterpret_cast<uint32_t*>(lb + 128);
   oc->status = reinterpret_cast<uint64_t*>(lb + kLbHeader);
   oc->tile_status = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * kMaxKeys);
   oc->tile_card = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * (kMaxKeys + kMaxTiles));
@@ -594,25 +594,42 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   }
   OutCtx oc;
   CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only));
+  PwOut po{};
+  PwTail tail{};
+  uint8_t* st = card_only ? nullptr : c->pw_state.as<uint8_t>();
+  if (!card_only) {  // placed and serialized inside the compute launch (pairwise.hip)
+    po.state = st;
+    po.scratch = oc.scratch;
+    tail.payload = oc.out + oc.payload_base;
+    tail.scratch = oc.scratch;
+    tail.out = oc.out;
+    tail.payload_base = oc.payload_base;
+    tail.err = oc.err;
+    tail.info = c->info.as<ResultInfo>();
+    tail.card = reinterpret_cast<unsigned long long*>(oc.err) + kCardWord;
+    // the fetch paths (k_shard_table, k_emit) read the records and place words
+    oc.recs = reinterpret_cast<ORec*>(st + kPwRecOff);
+    oc.tpos = reinterpret_cast<uint64_t*>(st + kPwPlaceOff);
+    c->pending = oc;
+  }
   c->pending_src = {ia, ib};
   c->mark(0);
   dbg(s, "memset");
   launch_plan_pairwise(s, plan_op, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), B->key_off.as<uint32_t>(),
                        db, B->payload.as<uint8_t>(), c->wg_epoch.as<uint64_t>(), next_epoch(c), c->tasks.as<PTask>(),
-                       c->ntasks.as<uint32_t>(), c->zlb, c->ztile, oc.err);
-  dbg(s, "compact");
+                       c->ntasks.as<uint32_t>(), c->zlb, c->ztile, oc.err, st, tail);
+  dbg(s, "plan");
   c->mark(1);
   const int grid = grid_for((ub + 3) / 4, 16384);  // 4 waves (tasks) per workgroup, clamped to the resident grid
   launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(),
-                  A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), oc, c->task_card.as<uint32_t>());
+                  A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), po, c->task_card.as<uint32_t>());
   dbg(s, "pairwise");
   c->mark(2);
   if (card_only) {
     launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>(), oc.err);
     c->last = 2;
   } else {
-    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
-    dbg(s, "header");
+    c->serialized = true;
     c->last = 1;
   }
   c->mark(3);
@@ -1128,13 +1145,17 @@ static int ctx_bsi_sums(Ctx* c, int64_t* out2) {
 static int ctx_info(Ctx* c, ResultInfo* ri) {
   HIPCHK(hipMemcpyAsync(ri, c->info.p, sizeof(ResultInfo), hipMemcpyDeviceToHost, c->stream));
   uint64_t card = 0;
-  if (c->last == 1)  // materialised result: k_place accumulated its cardinality
+  uint32_t err = 0;
+  if (c->last == 1)  // materialised result: k_place / the pairwise placer accumulated its cardinality
     HIPCHK(hipMemcpyAsync(&card, c->lb.as<uint8_t>() + 64 + 8 * kCardWord, 8, hipMemcpyDeviceToHost, c->stream));
+  if (c->last == 1 || c->last == 2)  // spin timeouts of any kernel of the op
+    HIPCHK(hipMemcpyAsync(&err, c->lb.as<uint8_t>() + 64, 4, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   if (c->last == 1) {
     ri->long_card = (int64_t)card;
     ri->card32 = (uint32_t)card;
   }
+  ri->err |= err;
   if ((c->last == 1 || c->last == 2) && ri->err) {
     set_err("a look-back spin of the op's plan or placement timed out: the result is invalid");
     return RBG_ERR_DEVICE;
@@ -1852,6 +1873,8 @@ static int ctx_fetch_shard_device(Ctx* c, int64_t total_containers, int has_run,
     set_err("fetch_shard: the global bitmap has an offset table; offsets_dst is required");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
+  ResultInfo ri;
+  CHK(ctx_info(c, &ri));  // a plan or placement whose spin timed out left an invalid result (RBG_ERR_DEVICE)
   const uint64_t off0 = header_size((size_t)total_containers, has_run != 0) + (uint64_t)payload_base;
   if (off0 > 0xFFFFFFFFull) {
     set_err("fetch_shard: payload offsets exceed 32 bits");
@@ -1861,8 +1884,6 @@ static int ctx_fetch_shard_device(Ctx* c, int64_t total_containers, int has_run,
   if (c->serialized) {
     // already serialized (possibly because an operand batch was released since): copy the
     // payload region rather than re-reading the operands' pass-through containers
-    ResultInfo ri;
-    CHK(ctx_info(c, &ri));
     if (ri.payload)
       HIPCHK(hipMemcpyAsync(payload_dst, c->result.as<uint8_t>() + c->pending.payload_base, ri.payload,
                             hipMemcpyDeviceToDevice, c->stream));

@@ -11,6 +11,8 @@
 //             totals) -- the result is now materialised on the device
 //   serialize (on fetch only): payload copies into the portable layout, then
 //             descriptors, offset table, run flags and cookie in front of it
+// (wide / BSI / priority-queue ops; the pairwise kernel places and serializes its
+// result inside its own launch, pairwise.hip)
 #include <algorithm>
 #include <mutex>
 #include <unordered_map>
@@ -71,11 +73,6 @@ __device__ __forceinline__ uint32_t ser_len_of(const CDesc& d, const uint8_t* pa
   if (d.kind == DK_A) return 2 * d.card;
   if (d.kind == DK_B) return 8192;
   return 2 + 4 * (uint32_t)(*reinterpret_cast<const uint16_t*>(payload + d.slot + 2));
-}
-
-__device__ __forceinline__ uint64_t header_bytes(uint32_t size, uint32_t has_run) {
-  if (has_run) return (size < 4) ? 4 + (size + 7) / 8 + 4ull * size : 4 + (size + 7) / 8 + 8ull * size;
-  return 8 + 8ull * size;
 }
 
 // Shape of the materialised result (container count, run flag, byte sizes)
@@ -412,7 +409,8 @@ __global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ n_tas
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     const ORec r = oc.recs[t];
     if (!r.keep) continue;
-    group_copy<NT>(dst + r.off, reinterpret_cast<const uint8_t*>(r.src), r.ser_len, threadIdx.x);
+    const uint64_t off = oc.tpos ? place_off(oc.tpos[t]) : r.off;
+    group_copy<NT>(dst + off, reinterpret_cast<const uint8_t*>(r.src), r.ser_len, threadIdx.x);
   }
 }
 
@@ -426,13 +424,16 @@ __global__ __launch_bounds__(256) void k_shard_table(const uint32_t* __restrict_
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
     const ORec r = oc.recs[t];
     if (!r.keep) continue;
+    // fused pairwise results: (index, offset) are in the place words
+    const uint32_t idx = oc.tpos ? place_idx(oc.tpos[t]) : r.idx;
+    const uint64_t roff = oc.tpos ? place_off(oc.tpos[t]) : r.off;
     const uint32_t d = (uint32_t)r.key | ((r.card - 1) << 16);
-    for (int k = 0; k < 4; k++) desc[4ull * r.idx + k] = (uint8_t)(d >> (8 * k));
+    for (int k = 0; k < 4; k++) desc[4ull * idx + k] = (uint8_t)(d >> (8 * k));
     if (offs) {
-      const uint32_t o = (uint32_t)(off0 + r.off);
-      for (int k = 0; k < 4; k++) offs[4ull * r.idx + k] = (uint8_t)(o >> (8 * k));
+      const uint32_t o = (uint32_t)(off0 + roff);
+      for (int k = 0; k < 4; k++) offs[4ull * idx + k] = (uint8_t)(o >> (8 * k));
     }
-    if (runb) runb[r.idx] = r.kind == DK_R ? 1 : 0;
+    if (runb) runb[idx] = r.kind == DK_R ? 1 : 0;
   }
 }
 

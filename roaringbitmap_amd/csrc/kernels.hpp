@@ -102,13 +102,43 @@ void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t
 void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
                     uint32_t* n_tasks);
 // pairwise.hip: plan (key alignment + descriptor resolution) and the wave-per-key compute
+// Fused pairwise placement state (one buffer, so the compute kernel holds one pointer for
+// all of it): a header (PwTail, written by the plan kernel; the totals word), then per task
+// the size words, the place words and the records.  Word formats: device.hpp.
+struct PwTail {
+  uint8_t* payload;       // result payload region (out + payload_base)
+  uint8_t* scratch;       // one kSlotBytes slot per task
+  uint8_t* out;           // result buffer: serialized bitmap at out + payload_base - header
+  uint64_t payload_base;
+  uint32_t* err;          // the op's error word (spin timeouts)
+  ResultInfo* info;       // result shape, written by the placer
+  unsigned long long* card;  // 64-bit result cardinality
+};
+constexpr size_t kPwHeader = 256;          // PwTail @0, totals word @128
+constexpr size_t kPwMaxTasks = 65536;
+constexpr size_t kPwSizeOff = kPwHeader;
+constexpr size_t kPwPlaceOff = kPwSizeOff + 8 * kPwMaxTasks;
+constexpr size_t kPwRecOff = kPwPlaceOff + 8 * kPwMaxTasks;
+constexpr size_t kPwStateBytes = kPwRecOff + sizeof(ORec) * kPwMaxTasks;
+// The compute kernel's output arguments: the state and the task slots; the rest is read
+// from the state header where it is used (kernel arguments held across the task loop
+// cost SGPRs, which the compiler spilled through VGPRs to scratch).
+struct PwOut {
+  uint8_t* state;    // kPwStateBytes
+  uint8_t* scratch;  // one kSlotBytes slot per task
+};
 // plan + compaction in one launch: tasks[] in key order, *n_tasks.  wg_epoch: 256 u64
 // (zeroed once per context), epoch: unique per op of the context.
+// state (materialising ops, or null): the fused placement state; its header gets `tail`,
+// its size / place words are zeroed.
 void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
                           const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_epoch, uint32_t epoch,
-                          PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile, uint32_t* err);
+                          PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile, uint32_t* err,
+                          uint8_t* state, PwTail tail);
+// mode 0: materialise, place and serialize the result in one launch (the serialized bitmap
+// starts at tail.out + info->start); mode 1: andCardinality into task_card
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
-                     const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card);
+                     const uint8_t* pa, const uint8_t* pb, PwOut po, uint32_t* task_card);
 // diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
 void debug_stamps(uint64_t* out20, bool reset);
 // diagnostic build (-DRBG_BSI_STAMPS=1): per-phase clock totals of k_bsi_reg

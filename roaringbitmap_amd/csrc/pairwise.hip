@@ -1,31 +1,31 @@
 // Pairwise static ops (RB/RoaringBitmap.java and :377, or :860, xor :1071,
-// andNot :444, andCardinality :413) on the MI355X.  RB/ = reference
-// RoaringBitmap/src/main/java/org/roaringbitmap/.
+// andNot :444, andCardinality :413) on the MI355X, ending at the serialized result
+// (RB/RoaringArray.java:896-940).  RB/ = reference RoaringBitmap/src/main/java/org/roaringbitmap/.
 //
 //   k_plan_pairwise : one thread per key: key alignment of the two operands
 //                     (the advanceUntil walks, here O(1) lookups in each batch's
-//                     key CSR) and resolution of both operands' descriptors into
-//                     a 32 B task record
-//   k_compact       : dense task list (kernels.hip)
+//                     key CSR), resolution of both operands' descriptors into a
+//                     32 B task record, and compaction into the dense task list
 //   k_pair_wave     : one wavefront per task over a resident grid; the next
 //                     task's record is fetched with scalar loads while the
-//                     current one runs, and both operand payloads are requested
-//                     before either is consumed
+//                     current one runs.  Materialising ops (MODE 0) also place
+//                     and serialize their result inside the same launch:
+//                       - every task publishes its result's size (a self-validating
+//                         8-byte word) as soon as it is written to the task's slot;
+//                       - one extra workgroup (the placer) scans the size words in
+//                         task order, 4,096 tasks per step, and publishes each task's
+//                         output index and payload offset (again one 8-byte word);
+//                       - between its tasks, each compute wave copies its own earlier
+//                         results whose place is published to their final offset in
+//                         the portable layout, so the copies overlap the compute;
+//                       - once every size is in, the placer writes cookie, run flags
+//                         and totals, and each wave the descriptors and offsets of its
+//                         own results.
+//                     The launch leaves the serialized bitmap in the result buffer.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
-// RBG_PW5=1: five 4-wave workgroups per CU (20 waves) instead of four.  Needs
-// <= 8 KiB of LDS per wave (R AND R in the run domain then takes na + nb <= 2048
-// runs) and <= 96 VGPRs, which the non-hoisted lane index gives.
-#ifndef RBG_PW5
-#define RBG_PW5 0
-#endif
-#if RBG_PW5
-#define RBG_OPAQUE_LANE 1
-#define RBG_WAVE_LDS 2048
-#define RBG_PW_BLOCKS 5
-#endif
 #include "kernels.hpp"
 #include "wave.hpp"
 
@@ -63,17 +63,28 @@ __device__ __forceinline__ int pair_class(int op, int ka, int kb) {
 // publishes its task count tagged with this op's epoch, sums the counts of the
 // workgroups before it (one per thread, waiting for the epoch), and writes its
 // tasks straight into the dense task list -- plan and compaction in one launch.
+// state (materialising ops): the fused placement's header gets `tail` (block 0) and its
+// per-task size / place words are zeroed here.
 __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* __restrict__ koa,
                                                        const CDesc* __restrict__ da, const uint8_t* __restrict__ pa,
                                                        const uint32_t* __restrict__ kob,
                                                        const CDesc* __restrict__ db, const uint8_t* __restrict__ pb,
                                                        uint64_t* __restrict__ wg_epoch, uint32_t epoch,
                                                        PTask* __restrict__ tasks, uint32_t* __restrict__ n_tasks,
-                                                       uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
+                                                       uint64_t* zlb, uint64_t* ztile, uint32_t* err,
+                                                       uint8_t* __restrict__ state, PwTail tail) {
   __shared__ int wt[4];
   __shared__ int wb[4];
   plan_zero(zlb, ztile);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (state) {
+    reinterpret_cast<uint64_t*>(state + kPwSizeOff)[k] = 0;
+    reinterpret_cast<uint64_t*>(state + kPwPlaceOff)[k] = 0;
+    if (k == 0) {
+      *reinterpret_cast<PwTail*>(state) = tail;
+      reinterpret_cast<uint64_t*>(state)[16] = 0;  // totals word
+    }
+  }
   PTask t;
   resolve(koa, da, pa, k, t.slot_a, t.card_a, t.kind_a, t.nruns_a);
   resolve(kob, db, pb, k, t.slot_b, t.card_b, t.kind_b, t.nruns_b);
@@ -122,11 +133,8 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* _
 constexpr int kWaves = 4;  // waves per workgroup
 // u32 words of LDS per wave: the 8 KiB bitmap map / staging area, plus room for
 // the run lists of run-domain R AND R (4 waves x 10 KiB x 4 workgroups = 160 KiB)
-#ifndef RBG_WAVE_LDS
-#define RBG_WAVE_LDS 2560
-#endif
-constexpr int kWaveLds = RBG_WAVE_LDS;
-static_assert(kWaveLds >= 2048, "the 8 KiB bitmap map / staging area");
+constexpr int kWaveLds = 2560;
+static_assert(kWaveLds >= 2048 + 32, "the 8 KiB bitmap map / staging area; the placer's run flags and partials");
 
 // Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
 // pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
@@ -156,45 +164,36 @@ struct StampAcc {
   } while (0)
 #endif
 
-// Wave priority (RBG_PRIO, default 1): a task runs at priority 3 until its
-// operand loads have been consumed, then drops to 0, so waves that are issuing
-// loads win instruction arbitration over waves in their compute / output phases
-// and more of the CU's memory requests are in flight (C2 AND -1 %, andCardinality
-// -2.5 %).  RBG_PRIO=2 also raises the output phase to 2 (no further change).
-#ifndef RBG_PRIO
-#define RBG_PRIO 1
-#endif
-#if RBG_PRIO
-#define PRIO_HI() __builtin_amdgcn_s_setprio(3)
-#define PRIO_LO() __builtin_amdgcn_s_setprio(0)
-#if RBG_PRIO == 2
-#define PRIO_OUT() __builtin_amdgcn_s_setprio(2)
-#else
-#define PRIO_OUT() \
-  do {            \
-  } while (0)
-#endif
-#else
-#define PRIO_OUT() \
-  do {            \
-  } while (0)
-#define PRIO_HI() \
-  do {            \
-  } while (0)
-#define PRIO_LO() \
-  do {            \
-  } while (0)
-#endif
+// Wave priority: a task runs at priority 3 until its operand loads have been
+// consumed, then drops to 0, so waves that are issuing loads win instruction
+// arbitration over waves in their compute / output phases and more of the CU's
+// memory requests are in flight (C2 AND -1 %, andCardinality -2.5 %).
+__device__ __forceinline__ void prio_hi() { __builtin_amdgcn_s_setprio(3); }
+__device__ __forceinline__ void prio_lo() { __builtin_amdgcn_s_setprio(0); }
+
+// the fused placement state (kernels.hpp)
+__device__ __forceinline__ uint64_t* size_words(const PwOut& po) {
+  return reinterpret_cast<uint64_t*>(po.state + kPwSizeOff);
+}
+__device__ __forceinline__ uint64_t* place_words(const PwOut& po) {
+  return reinterpret_cast<uint64_t*>(po.state + kPwPlaceOff);
+}
+__device__ __forceinline__ ORec* recs_of(const PwOut& po) { return reinterpret_cast<ORec*>(po.state + kPwRecOff); }
+__device__ __forceinline__ uint64_t* totals_word(const PwOut& po) { return reinterpret_cast<uint64_t*>(po.state) + 16; }
+__device__ __forceinline__ const PwTail& tail_of(const PwOut& po) { return *reinterpret_cast<const PwTail*>(po.state); }
+__device__ __forceinline__ uint8_t* scratch_of(const PwOut& po) { return po.scratch; }
+__device__ __forceinline__ uint8_t* payload_of(const PwOut& po) { return tail_of(po).payload; }
 
 // Records one task's output.  Staged results (LDS) are copied to the task's
 // scratch slot (arena slot layout); results already in the slot or pass-through
-// containers are referenced in place.  k_place and the serializer follow.
+// containers are referenced in place.  The record (source, length, type) stays with
+// the wave; the size word (keep, run, cardinality, length) goes to the placer.
 __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
-                                        uint32_t len, uint32_t card, uint32_t key, int kind, const OutCtx& oc) {
+                                        uint32_t len, uint32_t card, uint32_t key, int kind, const PwOut& po) {
   const int l = lane_id();
   uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
   if (keep && staged) {
-    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+    uint8_t* slot = scratch_of(po) + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
     copy_lds_to_global<64>(slot, lds, len, l);
     srcaddr = reinterpret_cast<uint64_t>(slot);
   }
@@ -208,7 +207,9 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
     r.key = (uint16_t)key;
     r.kind = (uint8_t)kind;
     r.keep = keep ? 1 : 0;
-    oc.recs[t] = r;
+    recs_of(po)[t] = r;
+    __hip_atomic_store(size_words(po) + t, size_word(keep, keep && kind == DK_R, card, keep ? len : 0), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -220,7 +221,7 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
 // -- go straight to the task's scratch slot.
 template <int OP, int MODE>
 __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard, const uint8_t* pslot, int mkind,
-                                            int mcard, const uint8_t* mslot, const OutCtx& oc, uint32_t* task_card,
+                                            int mcard, const uint8_t* mslot, const PwOut& po, uint32_t* task_card,
                                             uint32_t* lds SACC_PARAM) {
   STAMP_DECL
   // the array's values are requested first, so their memory latency overlaps the
@@ -232,7 +233,7 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
 #pragma unroll
   for (int j = 0; j < 8; j++) v[j] = (64 * j + l < nvec) ? pv[64 * j] : make_uint4(0, 0, 0, 0);
   w_map_lds(mkind, mcard, mslot, lds);
-  PRIO_LO();
+  prio_lo();
   STAMP(4);
   uint32_t hit[8];
   int cnt = 0;
@@ -264,14 +265,6 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
     if (l == 0) task_card[t] = (uint32_t)c;
     return;
   }
-  PRIO_OUT();
-#if RBG_EXP_NOCOMPACT
-  {  // experiment: no compaction and no payload store (wrong bytes, timing only)
-    const int c = (int)uni((uint32_t)wave_sum_i(cnt));
-    w_place(t, c > 0, oc.scratch + (size_t)t * kSlotBytes, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, oc);
-    return;
-  }
-#endif
   // the map is dead: compact the kept values over it, then 16 B stores.  Vectors
   // j and j+1 share one scan (16-bit count fields); every value is written, the
   // dropped ones to a per-lane dummy just past the kept ones (u16 index ctot + l),
@@ -308,23 +301,20 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
   }
   const int c = (int)ctot;
   wsync();
-  uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+  uint8_t* slot = scratch_of(po) + (size_t)t * kSlotBytes;
   const uint4* sv = reinterpret_cast<const uint4*>(lds);
   uint4* dv = reinterpret_cast<uint4*>(slot);
-#if RBG_EXP_NOSTORE
-  if (c == 0x7FFFFFFF)  // experiment: (almost) never store the filter output
-#endif
   for (int k = l; k < (2 * c + 15) >> 4; k += 64) dv[k] = sv[k];  // the slot has room for the rounded tail
   STAMP(5);
   // empty results are dropped (RB/RoaringBitmap.java:389,456)
-  w_place(t, c > 0, slot, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, oc);
+  w_place(t, c > 0, slot, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, po);
   STAMP(6);
 }
 
 // Filter-class task (pass-through clone, or a filter), one wave, wave-uniform branches.
 template <int OP, int MODE>
 __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+                                                  const PwOut& po, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
   const int ka = tk.kind_a, kb = tk.kind_b;
   if (ka == kAbsent || kb == kAbsent) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
     if (MODE == 0) {
@@ -334,7 +324,7 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
       const uint32_t nr = from_a ? tk.nruns_a : tk.nruns_b;
       const uint8_t* src = (from_a ? pa + tk.slot_a : pb + tk.slot_b) + (kind == DK_R ? 2 : 0);
       const uint32_t len = kind == DK_A ? 2 * card : kind == DK_B ? 8192u : 2 + 4 * nr;
-      w_place(t, true, src, false, lds, len, card, tk.key, kind, oc);
+      w_place(t, true, src, false, lds, len, card, tk.key, kind, po);
     }
     return;
   }
@@ -343,9 +333,9 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
   const uint8_t* sb = pb + tk.slot_b;
   // filter the array (A & A: the smaller one; A \ x: c1) through a map of the other operand
   if (ka == DK_A && (OP == OP_ANDNOT || kb != DK_A || ca <= cb))
-    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, oc, task_card, lds SACC_ARG);
+    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, po, task_card, lds SACC_ARG);
   else
-    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, oc, task_card, lds SACC_ARG);
+    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, po, task_card, lds SACC_ARG);
 }
 
 // R AND R in the run domain (RB/RunContainer.java and(RunContainer)): the
@@ -441,7 +431,7 @@ __device__ __forceinline__ void runs_to_lds2(const uint8_t* sa, int na, uint32_t
 
 template <int MODE>
 __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                            const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
+                                            const PwOut& po, uint32_t* task_card, uint32_t* lds) {
   const int na = tk.nruns_a, nb = tk.nruns_b;
   if (na + nb + 2 > kWaveLds) return false;
   const int l = lane_id();
@@ -451,7 +441,7 @@ __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const u
     lds[na] = kRunSentinel;
     lds[na + 1 + nb] = kRunSentinel;
   }
-  PRIO_LO();
+  prio_lo();
   wsync();
   const int d0 = (l * (na + nb)) >> 6, d1 = ((l + 1) * (na + nb)) >> 6;
   int cnt = 0, card = 0;
@@ -462,18 +452,18 @@ __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const u
     return true;
   }
   if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389)
-    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
+    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, po);
     return true;
   }
   int nr;
   const int off = wave_excl(cnt, &nr);
   nr = (int)uni((uint32_t)nr);
   if (eff(c, nr) != DK_R) return false;
-  uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+  uint8_t* slot = scratch_of(po) + (size_t)t * kSlotBytes;
   int cnt2 = 0, card2 = 0;
   rr_merge<true>(lds, na, nb, d0, d1, cnt2, card2, reinterpret_cast<uint32_t*>(slot + 4) + off);
   if (l == 0) *reinterpret_cast<uint16_t*>(slot + 2) = (uint16_t)nr;
-  w_place(t, true, slot + 2, false, lds, 2u + 4u * (uint32_t)nr, (uint32_t)c, tk.key, DK_R, oc);
+  w_place(t, true, slot + 2, false, lds, 2u + 4u * (uint32_t)nr, (uint32_t)c, tk.key, DK_R, po);
   return true;
 }
 
@@ -482,77 +472,41 @@ __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const u
 // staged in LDS).  One wave, wave-uniform branches.
 template <int OP, int MODE>
 __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
-  const int l = lane_id();
+                                                  const PwOut& po, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
   const int ka = tk.kind_a, kb = tk.kind_b;
   const int ca = (int)tk.card_a, cb = (int)tk.card_b;
-#if !RBG_NO_RR_RUNS
-  if (OP == OP_AND && ka == DK_R && kb == DK_R && rr_and_task<MODE>(t, tk, pa, pb, oc, task_card, lds)) return;
-#endif
+  if (OP == OP_AND && ka == DK_R && kb == DK_R && rr_and_task<MODE>(t, tk, pa, pb, po, task_card, lds)) return;
   STAMP_DECL
   WCtr x;
-#if RBG_BPRE
-  WPre xb;
-  const uint8_t* sb = pb + tk.slot_b;
-  if (kb == DK_B) w_prefetch(sb, 512, xb);
-#endif
   w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, (uint8_t)ka, 0}, pa, lds, x);
   STAMP(0);
-#if RBG_BPRE
-  if (kb == DK_B) w_combine_pre<OP>(DK_B, cb, 0, xb, sb, lds, x);
-  else
-#endif
-    w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
+  w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
   STAMP(1);
-  PRIO_LO();
-#if RBG_EXP_BB
-  if (MODE == 0) {  // experiment: every bitmap-class result stored as a bitmap, no count / typing
-    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
-    w_store_bitmap(slot, x);
-#if RBG_EXP_BB == 1
-    w_place(t, true, slot, false, lds, 8192, 1, tk.key, DK_B, oc);
-#else
-    if (l == 0) task_card[t] = (uint32_t)x.w[0];
-#endif
-    return;
-  }
-#endif
+  prio_lo();
   const int c = w_card(x);
   if (MODE == 1) {
-    if (l == 0) task_card[t] = (uint32_t)c;
+    if (lane_id() == 0) task_card[t] = (uint32_t)c;
     return;
   }
-  PRIO_OUT();
   if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389,456,1084)
-    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
+    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, po);
     return;
   }
   const bool use_eff = pairwise_needs_runs(OP, ka, ca, kb, cb);
   const int kind = use_eff ? eff(c, w_runs(x)) : pairwise_kind(OP, ka, kb, c);
   STAMP(2);
   if (kind == DK_B) {
-    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
-#if RBG_EXP_NOSTORE
-    if (x.w[0] == 0x123456789ULL) w_store_bitmap(slot, x);  // experiment: (almost) never store
-#else
+    uint8_t* slot = scratch_of(po) + (size_t)t * kSlotBytes;
     w_store_bitmap(slot, x);
-#endif
-    w_place(t, true, slot, false, lds, 8192, (uint32_t)c, tk.key, DK_B, oc);
+    w_place(t, true, slot, false, lds, 8192, (uint32_t)c, tk.key, DK_B, po);
     STAMP(3);
     return;
   }
   uint32_t len;
-#if RBG_EXP_NOSTAGE
-  if (kind != DK_B) {  // experiment: A / R results not staged (wrong bytes, timing only)
-    w_place(t, true, oc.scratch + (size_t)t * kSlotBytes, false, lds, kind == DK_A ? 2u * c : 6u, (uint32_t)c, tk.key,
-            kind, oc);
-    return;
-  }
-#endif
   if (kind == DK_A) len = w_stage(DK_A, x, c, lds);
   else len = 2u + 4u * (uint32_t)w_stage_runs(x, lds);
   STAMP(7);
-  w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, oc);
+  w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, po);
   STAMP(8);
 }
 
@@ -569,105 +523,320 @@ __device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
   return r.p;
 }
 
+template <int OP, int MODE>
+__device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
+                                         const PwOut& po, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+  prio_hi();
+  if (pair_class(OP, tk.kind_a, tk.kind_b) == 1)
+    filter_class_task<OP, MODE>(t, tk, pa, pb, po, task_card, lds SACC_ARG);
+  else
+    bitmap_class_task<OP, MODE>(t, tk, pa, pb, po, task_card, lds SACC_ARG);
+}
+
+// ===========================================================================
+// fused placement and serialization (MODE 0)
+// ===========================================================================
+constexpr uint32_t kSpinLimit = 1u << 22;  // bounded spins: a timeout sets the op's error word
+constexpr int kPlaceChunk = 4096;          // tasks per placer step (16 per thread)
+
+// 8-byte word written by another CU, polled with an `sc1` load (bypasses this CU's L1)
+__device__ __forceinline__ uint64_t poll_word(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave-uniform wait for a self-validating word; 0 on timeout (the error word is set)
+__device__ __forceinline__ uint64_t w_wait_word(const uint64_t* p, uint32_t* err) {
+  for (uint32_t spins = 0;; spins++) {
+    const uint64_t v = uni64(poll_word(p));
+    if (v & kGranuleValid) return v;
+    if (spins > kSpinLimit) {
+      if (lane_id() == 0) atomicOr(err, 1u);
+      return 0;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// n bytes from src to dst (even addresses, n even), one wave: the 16 B-aligned body of
+// the destination is written as 16 B vectors assembled from dword loads (alignbyte
+// for a source 2 bytes off dword alignment), 8 vectors per lane in flight; the
+// unaligned head and tail go as u16.  Reads up to 4 bytes past the end of src (slots
+// and payload arenas carry slack).  The pointers come from memory (records, the state
+// header), so they are generic to the compiler: the accesses go through explicitly
+// global-address-space types (no flat instructions, which also count against lgkmcnt).
+typedef __attribute__((address_space(1))) uint16_t g_u16;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+__device__ __forceinline__ void w_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  const int l = lane_id();
+  const uintptr_t d = reinterpret_cast<uintptr_t>(dst);
+  uint32_t head = (uint32_t)((16 - (d & 15)) & 15);
+  if (head > n) head = n;
+  const g_u16* s16 = (const g_u16*)src;
+  g_u16* d16 = (g_u16*)dst;
+  if (l < (int)(head >> 1)) d16[l] = s16[l];
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src + head);
+  g_u32x4* dv = (g_u32x4*)(dst + head);
+  const uint32_t nvec = (n - head) >> 4;
+  if ((s & 15) == 0) {
+    const g_u32x4* sv = (const g_u32x4*)s;
+    for (uint32_t i0 = 0; i0 < nvec; i0 += 512) {
+      u32x4 v[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t i = i0 + 64 * k + l;
+        if (i < nvec) v[k] = sv[i];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t i = i0 + 64 * k + l;
+        if (i < nvec) dv[i] = v[k];
+      }
+    }
+  } else {
+    const uint32_t sh = (uint32_t)(s & 3);  // 0 or 2
+    const g_u32* sw = (const g_u32*)(s & ~(uintptr_t)3);
+    for (uint32_t i0 = 0; i0 < nvec; i0 += 512) {
+      uint32_t a[8][5];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t i = i0 + 64 * k + l;
+#pragma unroll
+        for (int j = 0; j < 5; j++) a[k][j] = i < nvec ? sw[4 * i + j] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t i = i0 + 64 * k + l;
+        u32x4 o;
+        o.x = __builtin_amdgcn_alignbyte(a[k][1], a[k][0], sh);
+        o.y = __builtin_amdgcn_alignbyte(a[k][2], a[k][1], sh);
+        o.z = __builtin_amdgcn_alignbyte(a[k][3], a[k][2], sh);
+        o.w = __builtin_amdgcn_alignbyte(a[k][4], a[k][3], sh);
+        if (i < nvec) dv[i] = o;
+      }
+    }
+  }
+  const uint32_t done = head + (nvec << 4);
+  for (uint32_t i = (done >> 1) + l; i < (n >> 1); i += 64) d16[i] = s16[i];
+}
+
+// Task t's result (this wave's own record: source and length) to its final place
+// (place word: payload offset).
+__device__ __forceinline__ void w_emit(uint32_t t, uint64_t pw, const PwOut& po) {
+  const ORec& r = recs_of(po)[t];
+  if (!uni(r.keep)) return;
+  w_copy(payload_of(po) + place_off(pw), reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
+}
+
+// Own tasks tc, tc + stride, ... below `end` whose place is published go to their
+// final place; returns the first one still waiting.
+__device__ __forceinline__ uint32_t emit_ready(uint32_t tc, uint32_t end, uint32_t stride, const PwOut& po) {
+  while (tc < end) {
+    const uint64_t pw = uni64(poll_word(place_words(po) + tc));
+    if (!(pw & kGranuleValid)) break;
+    w_emit(tc, pw, po);
+    tc += stride;
+  }
+  return tc;
+}
+
+// The placer (one workgroup): scans the size words in task order, kPlaceChunk tasks
+// per step, and publishes every task's place word (output index, payload offset: the
+// exclusive prefix of the kept results -- RB/RoaringArray.java:896-940 writes the
+// payloads in container order).  A dropped task gets the place of the next kept one.
+// After the last step it writes the cookie, the run-flag bitset, the totals and the
+// result shape; the totals word releases the waves' descriptor / offset writes.
+__device__ void pw_placer(uint32_t nt, const PwOut& po, uint32_t* lds) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  uint32_t* rbits = lds;      // bit i: output container i is a run container
+  uint32_t* sh = lds + 2048;  // per-wave partials
+  const uint64_t* sizes = size_words(po);
+  uint64_t* places = place_words(po);
+  for (int i = tid; i < 2048; i += 256) rbits[i] = 0;
+  __syncthreads();
+  uint32_t n_out = 0, any_run = 0, err = 0;
+  uint64_t off_base = 0, card = 0;
+  for (uint32_t c0 = 0; c0 < nt; c0 += kPlaceChunk) {
+    const uint32_t tb = c0 + 16 * tid;
+    uint64_t s[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = 0;
+    // every size word of the thread's 16 tasks requested at once, re-polled until all are in
+    for (uint32_t spins = 0;; spins++) {
+#pragma unroll
+      for (int i = 0; i < 16; i++)
+        if (tb + i < nt && !(s[i] & kGranuleValid)) s[i] = poll_word(sizes + tb + i);
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < 16; i++) ok = ok && (tb + i >= nt || (s[i] & kGranuleValid));
+      if (ok || err) break;  // after one timeout the placer no longer waits (the result is invalid)
+      if (spins > kSpinLimit) {
+        err = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    uint32_t cnt = 0, bytes = 0, run = 0, cd = 0;  // per thread: <= 16 x 131074 bytes, <= 16 x 65536 values
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const bool keep = tb + i < nt && ((s[i] >> 62) & 1);
+      cnt += keep ? 1u : 0u;
+      bytes += keep ? (uint32_t)(s[i] & 0xFFFFFF) : 0u;
+      run |= keep ? (uint32_t)((s[i] >> 61) & 1) : 0u;
+      cd += keep ? (uint32_t)((s[i] >> 24) & 0x1FFFF) : 0u;
+    }
+    int wc, wb;
+    const int pc = wave_excl((int)cnt, &wc);
+    const int pb = wave_excl((int)bytes, &wb);  // a wave's bytes < 2^28
+    const int wcard = wave_sum_i((int)cd);      // a wave's values <= 2^26
+    const int wr = __any(run) ? 1 : 0;
+    if (lane == 0) {
+      sh[w] = (uint32_t)wc;
+      sh[4 + w] = (uint32_t)wb;
+      sh[8 + w] = (uint32_t)wcard;
+      sh[12 + w] = (uint32_t)wr;
+    }
+    __syncthreads();
+    uint32_t pre_c = 0, pre_b = 0, tot_c = 0, tot_r = 0;
+    uint64_t tot_b = 0, tot_card = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (i < w) {
+        pre_c += sh[i];
+        pre_b += sh[4 + i];
+      }
+      tot_c += sh[i];
+      tot_b += sh[4 + i];
+      tot_card += sh[8 + i];
+      tot_r |= sh[12 + i];
+    }
+    __syncthreads();  // sh is rewritten by the next step
+    uint32_t idx = n_out + pre_c + (uint32_t)pc;
+    uint64_t off = off_base + pre_b + (uint32_t)pb;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      if (tb + i < nt) {
+        __hip_atomic_store(places + tb + i, place_word(idx, off), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((s[i] >> 62) & 1) {
+          if ((s[i] >> 61) & 1) atomicOr(&rbits[idx >> 5], 1u << (idx & 31));
+          idx++;
+          off += s[i] & 0xFFFFFF;
+        }
+      }
+    }
+    n_out += tot_c;
+    off_base += tot_b;
+    card += tot_card;
+    any_run |= tot_r;
+  }
+  const PwTail& tl = tail_of(po);
+  if (__any(err)) {
+    if (lane == 0) atomicOr(tl.err, 1u);
+  }
+  __syncthreads();  // rbits complete
+  const uint64_t H = header_bytes(n_out, any_run);
+  const uint64_t start = tl.payload_base - H;
+  uint8_t* base = tl.out + start;
+  if (any_run) {  // run-flag bitset (RB/RoaringArray.java:905-913)
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rbits);
+    for (uint32_t b = tid; b < (n_out + 7) / 8; b += 256) base[4 + b] = rb[b];
+  }
+  if (tid == 0) {
+    uint32_t cookie[2];
+    int nb;
+    if (any_run) {  // RB/RoaringArray.java:900-904
+      cookie[0] = 12347u | ((n_out - 1) << 16);
+      nb = 4;
+    } else {  // :914-917
+      cookie[0] = 12346u;
+      cookie[1] = n_out;
+      nb = 8;
+    }
+    const uint8_t* cb = reinterpret_cast<const uint8_t*>(cookie);
+    for (int i = 0; i < nb; i++) base[i] = cb[i];
+    ResultInfo ri;
+    ri.n_out = n_out;
+    ri.has_run = any_run;
+    ri.header = H;
+    ri.payload = off_base;
+    ri.total = H + off_base;
+    ri.long_card = (int64_t)card;
+    ri.card32 = (uint32_t)card;
+    ri.any = n_out > 0;
+    ri.start = start;
+    ri.err = 0;
+    ri.pad = 0;
+    *tl.info = ri;
+    *tl.card = card;
+    __hip_atomic_store(totals_word(po), kGranuleValid | ((uint64_t)any_run << 62) | n_out, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// End of a compute wave (MODE 0): its remaining results to their places, then -- once
+// the totals are in -- the descriptors (key, card - 1) and offsets of its kept results
+// (RB/RoaringArray.java:918-933).  Lane j takes the wave's j-th task.
+__device__ __forceinline__ void pw_finish(uint32_t tc, uint32_t nt, uint32_t stride, const PwOut& po) {
+  uint32_t* err = tail_of(po).err;
+  while (tc < nt) {
+    const uint64_t pw = w_wait_word(place_words(po) + tc, err);
+    if (!pw) return;
+    w_emit(tc, pw, po);
+    tc += stride;
+  }
+  const uint64_t fin = w_wait_word(totals_word(po), err);
+  if (!fin) return;
+  const uint32_t size = (uint32_t)(fin & 0x1FFFF);
+  const bool has_run = (fin >> 62) & 1;
+  const uint64_t H = header_bytes(size, has_run);
+  uint8_t* base = payload_of(po) - H;
+  const uint64_t desc_base = has_run ? 4 + (size + 7) / 8 : 8;
+  const bool offsets = !has_run || size >= 4;
+  const uint64_t off_base = desc_base + 4ull * size;  // both tables are 4 B aligned (payload - 8 or 4 x size)
+  const ORec* recs = recs_of(po);
+  const uint64_t* places = place_words(po);
+  const uint32_t t0 = uni(blockIdx.x * kWaves + (threadIdx.x >> 6));  // recomputed: not held across the task loop
+  for (uint32_t j0 = 0; t0 + (uint64_t)j0 * stride < nt; j0 += 64) {
+    const uint64_t t = t0 + (uint64_t)(j0 + lane_id()) * stride;
+    if (t < nt) {
+      const ORec& r = recs[t];
+      if (r.keep) {
+        const uint64_t pw = poll_word(places + t);
+        const uint32_t idx = place_idx(pw);
+        *(g_u32*)(base + desc_base + 4ull * idx) = (uint32_t)r.key | ((r.card - 1) << 16);
+        if (offsets) *(g_u32*)(base + off_base + 4ull * idx) = (uint32_t)(H + place_off(pw));
+      }
+    }
+  }
+}
+
 // One wave per task, static stride over a resident grid (a contended ticket
 // counter costs ~12 ns per task chip-wide, a workgroup per task pays a dispatch
 // each).  The next task's record is loaded while this one runs.  Filter-class
 // and bitmap-class tasks share the launch: separate kernels per class were
 // measured 15 % slower on the C2 mix (tail + an extra dependent index load).
-// MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
-#if RBG_EXP_LOADONLY
-// experiment: every operand payload read (16 B per lane per vector, all in flight), no compute
-__device__ __forceinline__ uint32_t exp_read(const uint8_t* slot, int kind, uint32_t card, uint32_t nr) {
-  const uint32_t bytes = kind == DK_A ? 2 * card : kind == DK_B ? 8192 : 4 + 4 * nr;
-  const uint32_t nvec = (bytes + 15) >> 4;
-  const uint4* p = reinterpret_cast<const uint4*>(slot) + lane_id();
-  uint32_t acc = 0;
-  uint4 v[8];
-#pragma unroll
-  for (int j = 0; j < 8; j++) v[j] = (64 * j + lane_id() < (int)nvec) ? p[64 * j] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-  for (int j = 0; j < 8; j++) acc ^= v[j].x ^ v[j].y ^ v[j].z ^ v[j].w;
-  return acc;
-}
-#endif
-
+// MODE 0: materialise, place and serialize the result; the last workgroup is the
+// placer (the grid must be resident: every spin waits on a wave that is running).
+// MODE 1: andCardinality only (task_card[t]).
 template <int OP, int MODE>
-__device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                         const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
-#if RBG_EXP_LOADONLY
-  if (MODE == 1) {
-    uint32_t a = tk.kind_a != kAbsent ? exp_read(pa + tk.slot_a, tk.kind_a, tk.card_a, tk.nruns_a) : 0;
-    uint32_t b = tk.kind_b != kAbsent ? exp_read(pb + tk.slot_b, tk.kind_b, tk.card_b, tk.nruns_b) : 0;
-    const int c = wave_sum_i((int)((a ^ b) & 1));
-    if (lane_id() == 0) task_card[t] = (uint32_t)c;
-    return;
-  }
-  if (MODE == 0) {  // reads + a 4 KiB store per task (about the C2 AND's output bytes)
-    uint32_t a = tk.kind_a != kAbsent ? exp_read(pa + tk.slot_a, tk.kind_a, tk.card_a, tk.nruns_a) : 0;
-    uint32_t b = tk.kind_b != kAbsent ? exp_read(pb + tk.slot_b, tk.kind_b, tk.card_b, tk.nruns_b) : 0;
-#ifndef RBG_EXP_DST
-#define RBG_EXP_DST ((size_t)t * kSlotBytes)
-#endif
-    uint4* dst = reinterpret_cast<uint4*>(oc.scratch + RBG_EXP_DST) + lane_id();
-#pragma unroll
-    for (int j = 0; j < RBG_EXP_LOADONLY_STV; j++) dst[64 * j] = make_uint4(a, b, a ^ b, j);
-    if (lane_id() == 0) task_card[t] = a;
-    return;
-  }
-#endif
-  PRIO_HI();
-  if (pair_class(OP, tk.kind_a, tk.kind_b) == 1)
-    filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
-  else
-    bitmap_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
-}
-template <int OP, int MODE>
-#ifndef RBG_PW_BLOCKS
-#define RBG_PW_BLOCKS 4
-#endif
-__global__ __launch_bounds__(256, RBG_PW_BLOCKS) void k_pair_wave(const PTask* __restrict__ tasks,
+__global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
                                                       const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
-                                                      const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card) {
+                                                      const uint8_t* pb, PwOut po, uint32_t* __restrict__ task_card) {
   __shared__ __align__(16) uint32_t lds_all[kWaves][kWaveLds];
+  const uint32_t nt = uni(*n_tasks);
+  if (MODE == 0 && blockIdx.x == gridDim.x - 1) {
+    pw_placer(nt, po, &lds_all[0][0]);
+    return;
+  }
   const int w = threadIdx.x >> 6;
   uint32_t* lds = lds_all[w];
-  const uint32_t nt = uni(*n_tasks);
-  const uint32_t stride = gridDim.x * kWaves;
-  uint32_t t = uni(blockIdx.x * kWaves + w);
-  if (t >= nt) return;
+  const uint32_t stride = (MODE == 0 ? gridDim.x - 1 : gridDim.x) * kWaves;
+  const uint32_t t0 = uni(blockIdx.x * kWaves + w);
+  if (t0 >= nt) return;
+  uint32_t t = t0;
+  uint32_t tc = t0;  // MODE 0: the first own task whose result is not yet in its place
   PTask cur = load_task(tasks, t);
-#if RBG_EXP_LOADONLY == 2
-  if (MODE == 0) {  // experiment: reads + 4 KiB stores, the next task's reads issued before this task's stores
-    auto issue = [&](const PTask& tk, uint4* va, uint4* vb) {
-      const uint32_t ba = tk.kind_a == kAbsent ? 0 : tk.kind_a == DK_A ? 2 * tk.card_a : tk.kind_a == DK_B ? 8192 : 4 + 4 * tk.nruns_a;
-      const uint32_t bb = tk.kind_b == kAbsent ? 0 : tk.kind_b == DK_A ? 2 * tk.card_b : tk.kind_b == DK_B ? 8192 : 4 + 4 * tk.nruns_b;
-      const uint4* p = reinterpret_cast<const uint4*>(pa + tk.slot_a) + lane_id();
-      const uint4* q = reinterpret_cast<const uint4*>(pb + tk.slot_b) + lane_id();
-#pragma unroll
-      for (int j = 0; j < 8; j++) va[j] = (64 * j + lane_id() < (int)((ba + 15) >> 4)) ? p[64 * j] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < 8; j++) vb[j] = (64 * j + lane_id() < (int)((bb + 15) >> 4)) ? q[64 * j] : make_uint4(0, 0, 0, 0);
-    };
-    uint4 va[8], vb[8];
-    issue(cur, va, vb);
-    for (;;) {
-      const uint32_t tn = t + stride;
-      uint32_t a = 0, b = 0;
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        a ^= va[j].x ^ va[j].y ^ va[j].z ^ va[j].w;
-        b ^= vb[j].x ^ vb[j].y ^ vb[j].z ^ vb[j].w;
-      }
-      if (tn < nt) issue(load_task(tasks, tn), va, vb);
-      uint4* dst = reinterpret_cast<uint4*>(oc.scratch + (size_t)t * kSlotBytes) + lane_id();
-#pragma unroll
-      for (int j = 0; j < 4; j++) dst[64 * j] = make_uint4(a, b, a ^ b, j);
-      if (tn >= nt) break;
-      t = tn;
-    }
-    return;
-  }
-#endif
 #if RBG_STAMPS
   StampAcc sacc = {};
   const uint64_t t_kernel = __builtin_amdgcn_s_memtime();
@@ -681,14 +850,16 @@ __global__ __launch_bounds__(256, RBG_PW_BLOCKS) void k_pair_wave(const PTask* _
     const uint64_t t_in = __builtin_amdgcn_s_memtime();
     sacc.v[10] += 1;
 #endif
-    any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
+    any_task<OP, MODE>(t, cur, pa, pb, po, task_card, lds SACC_ARG);
 #if RBG_STAMPS
     sacc.v[11] += __builtin_amdgcn_s_memtime() - t_in;
 #endif
+    if (MODE == 0) tc = emit_ready(tc, min(tn, nt), stride, po);
     if (tn >= nt) break;
     t = tn;
     cur = nxt;
   }
+  if (MODE == 0) pw_finish(tc, nt, stride, po);
 #if RBG_STAMPS
   const uint64_t life = __builtin_amdgcn_s_memtime() - t_kernel;
   sacc.v[9] += life;
@@ -712,14 +883,11 @@ __global__ __launch_bounds__(256, RBG_PW_BLOCKS) void k_pair_wave(const PTask* _
 
 template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                      const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
-  const void* k = (const void*)&k_pair_wave<OP, MODE>;
-#ifndef RBG_GRID_MULT
-#define RBG_GRID_MULT 1
-#endif
-  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(std::max(1, std::min(grid, RBG_GRID_MULT * resident_grid(k)))),
-                     dim3(256), 0, s,
-                     tasks, nt, pa, pb, oc, task_card);
+                      const uint8_t* pb, PwOut po, uint32_t* task_card) {
+  const int res = resident_grid((const void*)&k_pair_wave<OP, MODE>);
+  // MODE 0: the compute workgroups plus the placer, all resident
+  const int g = MODE == 0 ? std::max(1, std::min(grid, res - 1)) + 1 : std::max(1, std::min(grid, res));
+  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, po, task_card);
 }
 
 #if RBG_STAMPS
@@ -747,15 +915,17 @@ void debug_stamps(uint64_t* out20, bool) {
 
 void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
                           const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_epoch, uint32_t epoch,
-                          PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
+                          PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile, uint32_t* err,
+                          uint8_t* state, PwTail tail) {
   hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, koa, da, pa, kob, db, pb, wg_epoch, epoch, tasks,
-                     n_tasks, zlb, ztile, err);
+                     n_tasks, zlb, ztile, err, state, tail);
 }
 
-void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
-#define RBG_LPW(O)                                                                    \
-  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card);   \
-  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card);
+void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
+                     const uint8_t* pb, PwOut po, uint32_t* task_card) {
+#define RBG_LPW(O)                                                           \
+  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, po, task_card); \
+  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, po, task_card);
   switch (op) {
     case OP_AND: RBG_LPW(OP_AND) break;
     case OP_OR: RBG_LPW(OP_OR) break;

@@ -13,21 +13,7 @@ namespace rbg {
 
 constexpr int WL = 64;  // lanes per wave
 
-#ifndef RBG_OPAQUE_LANE
-#define RBG_OPAQUE_LANE 0
-#endif
-#if RBG_OPAQUE_LANE
-// Lane index the compiler cannot hoist: every use recomputes it (2 VALU), so
-// lane-derived addresses are rebuilt per task instead of being held in VGPRs for
-// the whole kernel.
-__device__ __forceinline__ int lane_id() {
-  int v;
-  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(v));
-  return v;
-}
-#else
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
-#endif
 // wave-uniform copy (value of the first active lane, in an SGPR)
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
 // (readfirstlane returns int: each half goes through uint32_t, or a low half with bit 31
@@ -124,14 +110,9 @@ __device__ __forceinline__ void w_clear_lds(uint32_t* lds) {
 // OR/XOR the values of an array container (<= 4096 values, 16 B aligned slot)
 // into the wave's LDS bitmap.  All of a lane's 16 B vectors are loaded before
 // the first LDS atomic so the loads overlap (one memory latency per container).
-// RBG_SCATTER_MERGE=1 keeps the older variant that merges the bits of
-// consecutive values sharing a 32-bit word into one atomic.
 constexpr int kVecRound = 4;  // 16 B vectors per lane loaded per round
 
 // OR/XOR the 8 values of one 16 B vector (values base..base+7, those < card).
-#ifndef RBG_SCATTER_MERGE
-#define RBG_SCATTER_MERGE 0
-#endif
 // Branch-free: one LDS atomic per value, 4 VALU (word index, address, valid bit,
 // bit mask).  Values whose bit in `vm` is clear get a zero mask (the valid bits are
 // formed once per vector).  An average array has about one value per map word, so
@@ -149,14 +130,18 @@ __device__ __forceinline__ void scatter_vec_mask(uint32_t* lds, const uint4 v, u
   }
 }
 
-template <int MODE, bool MERGE = (RBG_SCATTER_MERGE != 0)>  // MODE 0 or, 1 xor
+template <int MODE>  // MODE 0 or, 1 xor
 __device__ __forceinline__ void scatter_vec(uint32_t* lds, const uint4 v, int base, int card) {
+  const int rem = card - base;
+  scatter_vec_mask<MODE>(lds, v, rem >= 8 ? 0xFFu : (1u << max(rem, 0)) - 1u);
+}
+
+// Same-word merging variant: the bits of consecutive values that share a 32-bit map
+// word go out in one atomic (branches on the word change).  The batched
+// andCardinality's small arrays keep it (C4 0.156 ms against 0.181 branch-free).
+template <int MODE>  // MODE 0 or, 1 xor
+__device__ __forceinline__ void scatter_vec_merged(uint32_t* lds, const uint4 v, int base, int card) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  if (!MERGE) {
-    const int rem = card - base;
-    scatter_vec_mask<MODE>(lds, v, rem >= 8 ? 0xFFu : (1u << max(rem, 0)) - 1u);
-    return;
-  }
   uint32_t cur = 0xFFFFFFFFu, mask = 0;
 #pragma unroll
   for (int i = 0; i < 8; i++) {
@@ -470,14 +455,10 @@ __device__ __forceinline__ void w_store_bitmap(uint8_t* p, const WCtr& x) {
   for (int i = 0; i < 8; i++) {
     const uint4 v = make_uint4((uint32_t)x.w[2 * i], (uint32_t)(x.w[2 * i] >> 32), (uint32_t)x.w[2 * i + 1],
                                (uint32_t)(x.w[2 * i + 1] >> 32));
-#if RBG_NO_NT
-    q[64 * i] = v;
-#else
     // streaming (nontemporal) stores: results are read back only by later kernels
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 nv = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(nv, reinterpret_cast<u32x4*>(q + 64 * i));
-#endif
   }
 }
 
@@ -854,51 +835,6 @@ __device__ __forceinline__ uint64_t lb_pack(uint64_t st, uint64_t run, uint64_t 
   return (st << 62) | (run << 61) | (cnt << 44) | bytes;
 }
 
-
-// Called by ALL lanes of ONE wave with identical (wave-uniform) arguments; the
-// spin loop is wave-uniform and single-exit.  Publishes this task's aggregate,
-// walks back to an inclusive predecessor, publishes the inclusive value and
-// returns the exclusive prefix.  The spin is bounded; on timeout *err is set
-// (the result is then invalid, nothing hangs).
-__device__ __forceinline__ Prefix lookback(uint64_t* status, uint32_t t, uint32_t cnt, uint64_t bytes, uint32_t run,
-                                           uint32_t* err) {
-  const bool leader = (threadIdx.x & 63) == 0;
-  t = uni(t);
-  uint64_t acc_cnt = 0, acc_bytes = 0, acc_run = 0;
-  if (leader)
-    __hip_atomic_store(status + t, lb_pack(t == 0 ? 2 : 1, run, cnt, bytes), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  if (t != 0) {
-    uint32_t j = t - 1;
-    uint32_t spins = 0;
-    bool done = false, timed_out = false;
-    while (!done) {
-      const uint64_t s = uni64(__hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      const uint32_t st = (uint32_t)(s >> 62);
-      if (st == 0) {
-        spins++;
-        if (spins > (1u << 22)) {
-          timed_out = true;
-          done = true;
-        } else {
-          __builtin_amdgcn_s_sleep(1);
-        }
-      } else {
-        acc_run |= (s >> 61) & 1;
-        acc_cnt += (s >> 44) & 0x1FFFF;
-        acc_bytes += s & ((1ULL << 44) - 1);
-        if (st == 2 || j == 0) done = true;
-        else j--;
-      }
-    }
-    if (leader) {
-      if (timed_out) atomicOr(err, 1u);
-      __hip_atomic_store(status + t, lb_pack(2, run | acc_run, cnt + acc_cnt, bytes + acc_bytes), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  return Prefix{(uint32_t)acc_cnt, acc_bytes};
-}
 
 // ---------------------------------------------------------------------------
 // workgroup-per-task result records (wide / BSI kernels)

@@ -37,10 +37,7 @@ constexpr int kSmallArray = 64;  // arrays up to this size are scattered by one 
 // Accumulate (OR or XOR, no run containers for XOR) every container of a key
 // segment: small arrays lane-serial, large arrays / runs cooperatively into LDS,
 // bitmaps into registers.
-#ifndef RBG_BGROUP
-#define RBG_BGROUP 2  // 4 costs the all-array path registers (C3 uniform -8%)
-#endif
-constexpr int kBGroup = RBG_BGROUP;
+constexpr int kBGroup = 2;  // bitmaps loaded together (4 costs the all-array path registers: C3 uniform -8 %)
 
 template <int MODE>
 __device__ __forceinline__ void accumulate_segment(const CDesc* desc, const uint8_t* payload, uint32_t s, uint32_t n,
@@ -737,7 +734,7 @@ __device__ __forceinline__ uint32_t small_arrays_and_card(const uint4 va, uint32
   const bool a_map = ca >= cb;
   const uint4 mv = a_map ? va : vb;
   const int mcard = (int)(a_map ? ca : cb);
-  scatter_vec<0, true>(lds, mv, 8 * lane, mcard);
+  scatter_vec_merged<0>(lds, mv, 8 * lane, mcard);
   wave_sync();
   const uint4 v = a_map ? vb : va;
   const int card = (int)(a_map ? cb : ca);

@@ -305,7 +305,9 @@ def assemble(fill, lay, rank=0, group=None, fill_device="cuda", comm_device="cud
     world = len(lay.n)
     if r == 0:
         out = torch.empty(lay.nbytes, dtype=torch.uint8, device=comm_device)
-        runb = torch.zeros(lay.total, dtype=torch.uint8, device=comm_device) if lay.has_run else None
+        # every byte is written: rank 0's slice by its fill, the others' by their receives
+        # (a zero fill here would run on torch's stream, unordered with the engine's writes)
+        runb = torch.empty(lay.total, dtype=torch.uint8, device=comm_device) if lay.has_run else None
         mine = views(out, runb, 0)
         if torch.device(fill_device) == torch.device(comm_device):
             do_fill(mine)
