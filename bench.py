@@ -273,31 +273,72 @@ def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
             "sum_count": list(sc), "min_max": [mn, mx]}
 
 
+def _median_of(fn, target_s):
+    """BASELINE.md §2 protocol (the JMH settings of jmh/build.gradle.kts:53-58): 5 warmup + 5
+    measured iterations, median.  One iteration runs fn(reps) with reps sized so that it takes
+    about target_s; returns (seconds per single run, reps)."""
+    t1 = max(fn(1), 1e-6)
+    reps = max(1, int(round(target_s / t1)))
+    for _ in range(5):
+        fn(reps)
+    times = sorted(fn(reps) for _ in range(5))
+    return times[2] / reps, reps
+
+
 def cpu_baselines(eng, a, b, in_bytes, budget_s):
-    """CPU legs on this host (rank 0, N=1): the oracle's C++ restatement of the reference
-    (the JVM reference cannot run here: no JDK), 1 thread with FastAggregation / RoaringBitmap
-    semantics and `threads` workers with ParallelAggregation's key-parallel semantics
-    (RB/ParallelAggregation.java:171-173), on bounded samples of the C2 and C3 workloads."""
+    """CPU legs on this host (rank 0, N=1), one per BASELINE.json config, with the BASELINE.md §2
+    protocol (5 warmup + 5 measured iterations, median).  The reference JVM path is probed for
+    (`java` on PATH); this image has none, so every leg is the oracle's C++ restatement of the
+    reference: FastAggregation / RoaringBitmap semantics on one thread, and ParallelAggregation's
+    key-parallel semantics (RB/ParallelAggregation.java:171-173) on cores - 1 workers, the
+    ForkJoin common pool's default parallelism.  Each leg runs on a bounded sample of its
+    workload (stated per leg)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import shutil
+
+    import numpy as np
+
     import _oracle as O  # CPU baseline leg only
     info = _cpu_info()
-    threads = max(1, min(16, info["affinity"] or 1))
-    per_leg = budget_s / 6.0
+    java = shutil.which("java")
+    threads = max(1, (info["affinity"] or 1) - 1)
+    n_legs = 12
+    target = budget_s / (n_legs * 11.0)  # 11 iterations per leg (calibration + 5 + 5)
+    legs = {}
+
+    def leg(name, fn, nbytes, thr, what, **kw):
+        sec, reps = _median_of(fn, target)
+        legs[name] = {"GBps": round(nbytes / sec / 1e9, 3), "ms": round(sec * 1e3, 3), "threads": thr,
+                      "reps_per_iter": reps, "what": what, **kw}
+
+    def algo_bytes(bufs):
+        n = p = 0
+        for x in bufs:
+            st = O.stats(x)
+            n += st["array"] + st["bitmap"] + st["run"]
+            p += st["payload"]
+        return p + 4 * n
+
+    # C1: census1881 (200 bitmaps, bitmapOf + runOptimize as RealDataBenchmarkState), FastAggregation.or
+    # and the pairwise and / andCardinality loops k = 0..198 of the jmh realdata benchmarks
+    z = np.load(os.path.join(ROOT, "tests", "golden", "realdata", "census1881.npz"))
+    vals, offs = z["values"], z["offsets"]
+    c1 = [O.from_values(vals[offs[i]:offs[i + 1]], True) for i in range(len(offs) - 1)]
+    c1_bytes = algo_bytes(c1)
+    pairs = [x for k in range(len(c1) - 1) for x in (c1[k], c1[k + 1])]
+    leg("c1_census_or_1t", lambda r: O.time_wide("or", c1, r), c1_bytes, 1,
+        "FastAggregation.or of the 200 census1881 bitmaps (runOptimize'd)")
+    leg("c1_census_and_1t", lambda r: O.time_pairs("and", pairs, 1, r), algo_bytes(pairs), 1,
+        "RoaringBitmap.and(b[k], b[k+1]).getCardinality(), k = 0..198 (census1881)")
+    leg("c1_census_andcard_1t", lambda r: O.time_pairs("and_card", pairs, 1, r), algo_bytes(pairs), 1,
+        "RoaringBitmap.andCardinality(b[k], b[k+1]), k = 0..198 (census1881)")
+    # C2: the headline pair itself
     xa = eng.batch_fetch(a).serialize()
     xb = eng.batch_fetch(b).serialize()
-
-    def timed(fn):
-        t1 = fn(1)
-        reps = max(1, int(math.ceil(per_leg / max(t1, 1e-3))))
-        return reps, fn(reps)
-
-    legs = {}
-    reps, t = timed(lambda r: O.time_pairwise("and", xa, xb, r))
-    legs["c2_and_1t"] = {"GBps": round(in_bytes * reps / t / 1e9, 3), "threads": 1, "reps": reps, "s": round(t, 2),
-                         "what": "RoaringBitmap.and(x1, x2) on the full C2 pair"}
-    reps, t = timed(lambda r: O.time_and_parallel(xa, xb, threads, r))
-    legs["c2_and_mt"] = {"GBps": round(in_bytes * reps / t / 1e9, 3), "threads": threads, "reps": reps,
-                         "s": round(t, 2), "what": f"key-parallel RoaringBitmap.and over {threads} key ranges"}
+    leg("c2_and_1t", lambda r: O.time_pairwise("and", xa, xb, r), in_bytes, 1,
+        "RoaringBitmap.and(x1, x2) on the full C2 pair")
+    leg("c2_and_mt", lambda r: O.time_and_parallel(xa, xb, threads, r), in_bytes, threads,
+        f"key-parallel RoaringBitmap.and over {threads} key ranges, full C2 pair")
     # C3: all 10,000 bitmaps restricted to a key sample (uniform: 128 keys; clustered: 512 keys)
     for kind, name, keys in ((1, "uniform", 128), (2, "clustered", 512)):
         sb = eng.synth(kind, 0xC3000000, 10000, 0, keys)
@@ -305,20 +346,42 @@ def cpu_baselines(eng, a, b, in_bytes, budget_s):
         sbytes = st["payload_bytes"] + 4 * st["containers"]
         bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
         eng.release(sb)
-        reps, t = timed(lambda r: O.time_wide("or", bufs, r))
-        legs[f"c3_{name}_or_1t"] = {"GBps": round(sbytes * reps / t / 1e9, 3), "threads": 1, "reps": reps,
-                                    "s": round(t, 2),
-                                    "what": f"FastAggregation.or of 10,000 C3 {name} bitmaps, keys [0, {keys})"}
-        reps, t = timed(lambda r: O.time_wide_parallel("or", bufs, threads, r))
-        legs[f"c3_{name}_or_mt"] = {"GBps": round(sbytes * reps / t / 1e9, 3), "threads": threads, "reps": reps,
-                                    "s": round(t, 2),
-                                    "what": f"ParallelAggregation.or (key groups over {threads} workers), same sample"}
+        leg(f"c3_{name}_or_1t", lambda r: O.time_wide("or", bufs, r), sbytes, 1,
+            f"FastAggregation.or of 10,000 C3 {name} bitmaps, keys [0, {keys})")
+        leg(f"c3_{name}_or_mt", lambda r: O.time_wide_parallel("or", bufs, threads, r), sbytes, threads,
+            f"ParallelAggregation.or (key groups over {threads} workers), same sample")
         del bufs
+    # C4: the first 65,536 of the million pairs (same generator, seed 0xC4)
+    n4 = 65536
+    sb = eng.synth(3, 0xC4, n4)
+    matched, _ = eng.pair_bytes(sb)
+    bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
+    eng.release(sb)
+    leg("c4_andcard_1t", lambda r: O.time_pairs("and_card", bufs, 1, r), matched, 1,
+        f"loop of RoaringBitmap.andCardinality over {n4} C4 pairs (seed 0xC4)", pairs_per_s=None)
+    legs["c4_andcard_1t"]["pairs_per_s"] = round(n4 / (legs["c4_andcard_1t"]["ms"] / 1e3), 1)
+    leg("c4_andcard_mt", lambda r: O.time_pairs("and_card", bufs, threads, r), matched, threads,
+        f"the same loop split over {threads} workers")
+    legs["c4_andcard_mt"]["pairs_per_s"] = round(n4 / (legs["c4_andcard_mt"]["ms"] / 1e3), 1)
+    del bufs
+    # C5: the 10^9-row column's first 16 keys (1,048,576 rows), ebM + 31 slices
+    sb = eng.synth(4, 0xC5, 16 * 65536, 0, 16)
+    st = eng.batch_stats(sb)
+    sbytes = st["payload_bytes"] + 4 * st["containers"]
+    bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
+    eng.release(sb)
+    lo, hi = 1 << 29, 1 << 30
+    leg("c5_bsi_range_sum_1t", lambda r: O.time_bsi_range_sum(bufs[0], bufs[1:], lo, hi, r)[0], sbytes, 1,
+        "RoaringBitmapSliceIndex.compare(RANGE, 2^29, 2^30) + sum, rows [0, 2^20) (16 keys x 31 slices)")
+    legs["c5_bsi_range_sum_1t"]["rows_per_s"] = round(16 * 65536 / (legs["c5_bsi_range_sum_1t"]["ms"] / 1e3), 1)
+    del bufs
     best = legs["c2_and_mt"]
     return {"value": best["GBps"], "unit": "GB/s", "cores": best["threads"], "kind": "port",
-            "sample": f"full C2 pair (same bytes as the GPU step), {best['reps']} x key-parallel RoaringBitmap.and on "
-                      f"{best['threads']} threads of the C++ restatement oracle/rbcpu -- C++ restatement, not the "
-                      f"reference JVM (no JDK on this image)",
+            "sample": f"full C2 pair (same bytes as the GPU step): key-parallel RoaringBitmap.and on {best['threads']} "
+                      f"threads (cores - 1, the ForkJoin common-pool default) of the C++ restatement oracle/rbcpu, "
+                      f"median of 5 after 5 warmup iterations -- C++ restatement, not the reference JVM "
+                      f"(java on this host: {java})",
+            "java": java, "protocol": "5 warmup + 5 measured iterations, median (BASELINE.md §2)",
             "host": info, "legs": legs}
 
 

@@ -290,4 +290,76 @@ double rbo_time_and_parallel(const uint8_t* a, size_t an, const uint8_t* b, size
   return now_s() - t0;
 }
 
+// C1 / C4 legs: a loop of RoaringBitmap.and(x1, x2).getCardinality() (op 0, :377-401) or
+// RoaringBitmap.andCardinality (op 4, :413-434) over the pairs (bufs[2i], bufs[2i+1]),
+// split into `threads` contiguous ranges; seconds for `reps` passes (inputs parsed outside
+// the clock).
+double rbo_time_pairs(int op, const uint8_t* const* bufs, const size_t* lens, size_t n_pairs, int threads, int reps) {
+  std::vector<Bitmap> bms;
+  std::vector<const Bitmap*> ptrs;
+  if (load_many(bufs, lens, 2 * n_pairs, &bms, &ptrs)) return -1.0;
+  const int T = std::max(1, threads);
+  std::vector<int64_t> sinks(T, 0);
+  double t0 = now_s();
+  for (int r = 0; r < reps; r++) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      th.emplace_back([&, t]() {
+        const size_t lo = n_pairs * t / T, hi = n_pairs * (t + 1) / T;
+        int64_t s = 0;
+        for (size_t i = lo; i < hi; i++)
+          s += op == 4 ? op_and_card(bms[2 * i], bms[2 * i + 1]) : op_and(bms[2 * i], bms[2 * i + 1]).long_card();
+        sinks[t] += s;
+      });
+    for (auto& x : th) x.join();
+  }
+  const double dt = now_s() - t0;
+  volatile int64_t sink = 0;
+  for (int64_t v : sinks) sink += v;
+  return dt;
+}
+
+// C5 leg: RoaringBitmapSliceIndex.compare(RANGE, lo, hi, null) + sum(result) on the heap
+// BSI (bsi/src/main/java/org/roaringbitmap/bsi/RoaringBitmapSliceIndex.java): the O'Neil
+// circuit oNeilCompare (:432-468) for GE lo and LE hi, their and (:508-511), then
+// sum = sum over slices of (1 << x) * andCardinality(bA[x], found) (:581-592).  bufs[0] = ebM,
+// bufs[1..nbits] = bA; single thread, as the heap BSI is; seconds for `reps` queries.
+static Bitmap oneil(const Bitmap& ebm, const std::vector<Bitmap>& ba, bool ge, uint32_t predicate) {
+  Bitmap gt, lt, eq = ebm;
+  for (int i = (int)ba.size() - 1; i >= 0; i--) {
+    if ((predicate >> i) & 1) {
+      lt = op_or(lt, op_andnot(eq, ba[i]));
+      eq = op_and(eq, ba[i]);
+    } else {
+      gt = op_or(gt, op_and(eq, ba[i]));
+      eq = op_andnot(eq, ba[i]);
+    }
+  }
+  eq = op_and(ebm, eq);                  // fixedFoundSet = ebM
+  return ge ? op_or(gt, eq) : op_or(lt, eq);
+}
+double rbo_time_bsi_range_sum(const uint8_t* const* bufs, const size_t* lens, int nbits, uint32_t lo, uint32_t hi,
+                              int reps, int64_t* out2) {
+  std::vector<Bitmap> bms;
+  std::vector<const Bitmap*> ptrs;
+  if (load_many(bufs, lens, (size_t)nbits + 1, &bms, &ptrs)) return -1.0;
+  const Bitmap& ebm = bms[0];
+  std::vector<Bitmap> ba(bms.begin() + 1, bms.end());
+  int64_t sum = 0, count = 0;
+  double t0 = now_s();
+  for (int r = 0; r < reps; r++) {
+    const Bitmap found = op_and(oneil(ebm, ba, true, lo), oneil(ebm, ba, false, hi));
+    count = found.long_card();
+    uint64_t s = 0;
+    for (int x = 0; x < nbits; x++) s += (uint64_t)((int64_t)(int32_t)(1u << x) * (int64_t)op_and_card(ba[x], found));
+    sum = (int64_t)s;
+  }
+  const double dt = now_s() - t0;
+  if (out2) {
+    out2[0] = sum;
+    out2[1] = count;
+  }
+  return dt;
+}
+
 }  // extern "C"

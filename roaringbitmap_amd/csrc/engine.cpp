@@ -194,7 +194,6 @@ static int ctx_init(Ctx* c, int device) {
   HIPCHK(hipMemset(c->wg_epoch.p, 0, 8 * 256));
   CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + 2 * kMaxTiles)));
   CHK(c->recs.ensure(sizeof(ORec) * kMaxKeys));
-  CHK(c->pw_state.ensure(kPwStateBytes));
   CHK(c->kind_by_out.ensure(kMaxKeys));
   CHK(c->scalar.ensure(64));
   CHK(c->info.ensure(sizeof(ResultInfo)));
@@ -511,7 +510,8 @@ static int grid_for(size_t tasks, size_t cap = 4096) {
 // Output state of a materialising op: per-task records + scratch slots (the
 // device-resident result), and the portable-format buffer the serialization
 // writes into on fetch.  Card-only ops need no output state.
-static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc, bool card_only) {
+static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc, bool card_only,
+                          bool task_slots = true) {
   uint8_t* lb = c->lb.as<uint8_t>();
   *oc = OutCtx{};
   oc->err = reinterpret_cast<uint32_t*>(lb + 64);
@@ -530,13 +530,13 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   const uint64_t P0 = header_reserve(max_tasks);
   CHK(c->result.ensure(P0 + max_payload + 64));
   c->result_cap = P0 + max_payload;
-  CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1) + 64));
+  if (task_slots) CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1) + 64));
   // the look-back header and tile statuses are zeroed by the op's plan kernel
   c->zlb = reinterpret_cast<uint64_t*>(lb);
   c->ztile = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * kMaxKeys);
   oc->out = c->result.as<uint8_t>();
   oc->payload_base = P0;
-  oc->scratch = c->scratch.as<uint8_t>();
+  oc->scratch = task_slots ? c->scratch.as<uint8_t>() : nullptr;
   c->pending = *oc;
   c->pending_ub = max_tasks;
   return RBG_OK;
@@ -593,15 +593,15 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     default: ub = std::min<size_t>((size_t)na + nb, kMaxKeys); break;
   }
   OutCtx oc;
-  CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only));
+  // the fused placement keeps its task slots in its own state buffer
+  CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only, false));
+  if (!card_only) CHK(c->pw_state.ensure(kPwScratchOff + (size_t)kSlotBytes * std::max<size_t>(ub, 1) + 64));
   PwOut po{};
   PwTail tail{};
   uint8_t* st = card_only ? nullptr : c->pw_state.as<uint8_t>();
   if (!card_only) {  // placed and serialized inside the compute launch (pairwise.hip)
     po.state = st;
-    po.scratch = oc.scratch;
     tail.payload = oc.out + oc.payload_base;
-    tail.scratch = oc.scratch;
     tail.out = oc.out;
     tail.payload_base = oc.payload_base;
     tail.err = oc.err;
@@ -629,6 +629,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>(), oc.err);
     c->last = 2;
   } else {
+    launch_pairwise_emit(s, c->ntasks.as<uint32_t>(), po);
     c->serialized = true;
     c->last = 1;
   }

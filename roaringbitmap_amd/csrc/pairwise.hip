@@ -80,9 +80,12 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* _
   if (state) {
     reinterpret_cast<uint64_t*>(state + kPwSizeOff)[k] = 0;
     reinterpret_cast<uint64_t*>(state + kPwPlaceOff)[k] = 0;
-    if (k == 0) {
-      *reinterpret_cast<PwTail*>(state) = tail;
-      reinterpret_cast<uint64_t*>(state)[16] = 0;  // totals word
+    state[kPwCopiedOff + k] = 0;
+    if (blockIdx.x == 0) {  // header: tail, totals / card / done words, chunk words, run-flag bitset
+      if (threadIdx.x == 0) *reinterpret_cast<PwTail*>(state) = tail;
+      if (threadIdx.x < 3) reinterpret_cast<uint64_t*>(state + kPwTotalsOff)[threadIdx.x] = 0;
+      if (threadIdx.x < kPwMaxChunks) reinterpret_cast<uint64_t*>(state + kPwChunkOff)[threadIdx.x] = 0;
+      for (uint32_t i = threadIdx.x; i < 1024; i += 256) reinterpret_cast<uint64_t*>(state + kPwRunBitsOff)[i] = 0;
     }
   }
   PTask t;
@@ -179,9 +182,11 @@ __device__ __forceinline__ uint64_t* place_words(const PwOut& po) {
   return reinterpret_cast<uint64_t*>(po.state + kPwPlaceOff);
 }
 __device__ __forceinline__ ORec* recs_of(const PwOut& po) { return reinterpret_cast<ORec*>(po.state + kPwRecOff); }
-__device__ __forceinline__ uint64_t* totals_word(const PwOut& po) { return reinterpret_cast<uint64_t*>(po.state) + 16; }
+__device__ __forceinline__ uint64_t* totals_word(const PwOut& po) {
+  return reinterpret_cast<uint64_t*>(po.state + kPwTotalsOff);
+}
 __device__ __forceinline__ const PwTail& tail_of(const PwOut& po) { return *reinterpret_cast<const PwTail*>(po.state); }
-__device__ __forceinline__ uint8_t* scratch_of(const PwOut& po) { return po.scratch; }
+__device__ __forceinline__ uint8_t* scratch_of(const PwOut& po) { return po.state + kPwScratchOff; }
 __device__ __forceinline__ uint8_t* payload_of(const PwOut& po) { return tail_of(po).payload; }
 
 // Records one task's output.  Staged results (LDS) are copied to the task's
@@ -536,7 +541,6 @@ __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint
 // ===========================================================================
 // fused placement and serialization (MODE 0)
 // ===========================================================================
-constexpr uint32_t kSpinLimit = 1u << 22;  // bounded spins: a timeout sets the op's error word
 constexpr int kPlaceChunk = 4096;          // tasks per placer step (16 per thread)
 
 // 8-byte word written by another CU, polled with an `sc1` load (bypasses this CU's L1)
@@ -544,83 +548,148 @@ __device__ __forceinline__ uint64_t poll_word(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave-uniform wait for a self-validating word; 0 on timeout (the error word is set)
-__device__ __forceinline__ uint64_t w_wait_word(const uint64_t* p, uint32_t* err) {
-  for (uint32_t spins = 0;; spins++) {
-    const uint64_t v = uni64(poll_word(p));
-    if (v & kGranuleValid) return v;
-    if (spins > kSpinLimit) {
-      if (lane_id() == 0) atomicOr(err, 1u);
-      return 0;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
+// Spin deadlines on the 100 MHz constant clock: a spin that outlives one has waited for a
+// wave that cannot come (the op's error word is set and nothing hangs).
+constexpr uint64_t kSpinTicks = 200000000;  // 2 s
+__device__ __forceinline__ uint64_t spin_deadline() { return __builtin_amdgcn_s_memrealtime() + kSpinTicks; }
+__device__ __forceinline__ bool spin_expired(uint64_t deadline) { return __builtin_amdgcn_s_memrealtime() > deadline; }
 
-// n bytes from src to dst (even addresses, n even), one wave: the 16 B-aligned body of
-// the destination is written as 16 B vectors assembled from dword loads (alignbyte
-// for a source 2 bytes off dword alignment), 8 vectors per lane in flight; the
-// unaligned head and tail go as u16.  Reads up to 4 bytes past the end of src (slots
-// and payload arenas carry slack).  The pointers come from memory (records, the state
-// header), so they are generic to the compiler: the accesses go through explicitly
-// global-address-space types (no flat instructions, which also count against lgkmcnt).
+// n bytes from src to dst (even addresses, n even), one wave.  The destination body is
+// written as aligned 16 B vectors; each is the 16 bytes at `shift` (the source's offset
+// from 16 B alignment at that point) inside two consecutive aligned source vectors: lane l
+// loads aligned source vector i, takes vector i + 1 from lane l + 1 (a DPP lane shift;
+// lane 63 from the next group's lane 0) and funnel-shifts the pair (alignbyte).  So every
+// load and store is a coalesced 16 B access, 8 per lane in flight.  The unaligned head and
+// tail go as u16.  Reads up to 16 bytes past the end of src (slots and payload arenas carry
+// slack).  The pointers come from memory (records, the state header), so they are generic
+// to the compiler: the accesses go through global-address-space types (flat instructions
+// would also count against lgkmcnt).
 typedef __attribute__((address_space(1))) uint16_t g_u16;
 typedef __attribute__((address_space(1))) uint32_t g_u32;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
-__device__ __forceinline__ void w_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
-  const int l = lane_id();
-  const uintptr_t d = reinterpret_cast<uintptr_t>(dst);
-  uint32_t head = (uint32_t)((16 - (d & 15)) & 15);
-  if (head > n) head = n;
-  const g_u16* s16 = (const g_u16*)src;
-  g_u16* d16 = (g_u16*)dst;
-  if (l < (int)(head >> 1)) d16[l] = s16[l];
-  const uintptr_t s = reinterpret_cast<uintptr_t>(src + head);
-  g_u32x4* dv = (g_u32x4*)(dst + head);
-  const uint32_t nvec = (n - head) >> 4;
-  if ((s & 15) == 0) {
-    const g_u32x4* sv = (const g_u32x4*)s;
-    for (uint32_t i0 = 0; i0 < nvec; i0 += 512) {
-      u32x4 v[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t i = i0 + 64 * k + l;
-        if (i < nvec) v[k] = sv[i];
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t i = i0 + 64 * k + l;
-        if (i < nvec) dv[i] = v[k];
-      }
-    }
+
+__device__ __forceinline__ u32x4 next_lane_vec(u32x4 v) {
+  u32x4 r;
+  r.x = from_next_lane(v.x);
+  r.y = from_next_lane(v.y);
+  r.z = from_next_lane(v.z);
+  r.w = from_next_lane(v.w);
+  return r;
+}
+__device__ __forceinline__ u32x4 lane0_vec(u32x4 v) {
+  u32x4 r;
+  r.x = lane0u(v.x);
+  r.y = lane0u(v.y);
+  r.z = lane0u(v.z);
+  r.w = lane0u(v.w);
+  return r;
+}
+// the 16 bytes at byte offset 4q + r (q wave-uniform, r in {0, 2}) of the 32-byte pair (a, b)
+__device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t q, uint32_t r) {
+  u32x4 o;
+  if (q == 0) {
+    o.x = __builtin_amdgcn_alignbyte(a.y, a.x, r);
+    o.y = __builtin_amdgcn_alignbyte(a.z, a.y, r);
+    o.z = __builtin_amdgcn_alignbyte(a.w, a.z, r);
+    o.w = __builtin_amdgcn_alignbyte(b.x, a.w, r);
+  } else if (q == 1) {
+    o.x = __builtin_amdgcn_alignbyte(a.z, a.y, r);
+    o.y = __builtin_amdgcn_alignbyte(a.w, a.z, r);
+    o.z = __builtin_amdgcn_alignbyte(b.x, a.w, r);
+    o.w = __builtin_amdgcn_alignbyte(b.y, b.x, r);
+  } else if (q == 2) {
+    o.x = __builtin_amdgcn_alignbyte(a.w, a.z, r);
+    o.y = __builtin_amdgcn_alignbyte(b.x, a.w, r);
+    o.z = __builtin_amdgcn_alignbyte(b.y, b.x, r);
+    o.w = __builtin_amdgcn_alignbyte(b.z, b.y, r);
   } else {
-    const uint32_t sh = (uint32_t)(s & 3);  // 0 or 2
-    const g_u32* sw = (const g_u32*)(s & ~(uintptr_t)3);
-    for (uint32_t i0 = 0; i0 < nvec; i0 += 512) {
-      uint32_t a[8][5];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t i = i0 + 64 * k + l;
-#pragma unroll
-        for (int j = 0; j < 5; j++) a[k][j] = i < nvec ? sw[4 * i + j] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t i = i0 + 64 * k + l;
-        u32x4 o;
-        o.x = __builtin_amdgcn_alignbyte(a[k][1], a[k][0], sh);
-        o.y = __builtin_amdgcn_alignbyte(a[k][2], a[k][1], sh);
-        o.z = __builtin_amdgcn_alignbyte(a[k][3], a[k][2], sh);
-        o.w = __builtin_amdgcn_alignbyte(a[k][4], a[k][3], sh);
-        if (i < nvec) dv[i] = o;
-      }
-    }
+    o.x = __builtin_amdgcn_alignbyte(b.x, a.w, r);
+    o.y = __builtin_amdgcn_alignbyte(b.y, b.x, r);
+    o.z = __builtin_amdgcn_alignbyte(b.z, b.y, r);
+    o.w = __builtin_amdgcn_alignbyte(b.w, b.z, r);
   }
-  const uint32_t done = head + (nvec << 4);
-  for (uint32_t i = (done >> 1) + l; i < (n >> 1); i += 64) d16[i] = s16[i];
+  return o;
 }
 
+struct CopyJob {
+  const g_u16* s16;
+  g_u16* d16;
+  const g_u32x4* sv;  // aligned source vectors
+  g_u32x4* dv;        // aligned destination body
+  uint32_t n, head, nvec, shift;
+};
+// the unaligned head (u16 by the first lanes) and the body's geometry
+__device__ __forceinline__ CopyJob copy_begin(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  const int l = lane_id();
+  CopyJob j;
+  const uintptr_t d = reinterpret_cast<uintptr_t>(dst);
+  j.head = (uint32_t)((16 - (d & 15)) & 15);
+  if (j.head > n) j.head = n;
+  j.n = n;
+  j.s16 = (const g_u16*)src;
+  j.d16 = (g_u16*)dst;
+  if (l < (int)(j.head >> 1)) j.d16[l] = j.s16[l];
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src + j.head);
+  j.shift = (uint32_t)(s & 15);  // even
+  j.sv = (const g_u32x4*)(s - j.shift);
+  j.dv = (g_u32x4*)(dst + j.head);
+  j.nvec = (n - j.head) >> 4;
+  return j;
+}
+// pass i0 (512 body vectors): every source vector the pass needs, requested at once (one
+// past the body too: the partner of the last one; lane 63 of the last group also needs
+// aligned vector i0 + 512 -- the one past the body when this is the last pass: it still
+// holds tail bytes or slack)
+__device__ __forceinline__ void copy_load(const CopyJob& j, uint32_t i0, u32x4 a[8], u32x4& last) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t i = i0 + 64 * k + l;
+    if (i <= j.nvec && (j.shift != 0 || i < j.nvec)) a[k] = j.sv[i];
+    else a[k] = u32x4{0, 0, 0, 0};
+  }
+  last = u32x4{0, 0, 0, 0};
+  if (j.shift != 0 && l == 63 && i0 + 511 < j.nvec) last = j.sv[i0 + 512];
+}
+__device__ __forceinline__ void copy_store(const CopyJob& j, uint32_t i0, const u32x4 a[8], const u32x4& last) {
+  const int l = lane_id();
+  if (j.shift == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t i = i0 + 64 * k + l;
+      if (i < j.nvec) j.dv[i] = a[k];
+    }
+    return;
+  }
+  const uint32_t q = j.shift >> 2, r = j.shift & 3;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t i = i0 + 64 * k + l;
+    u32x4 b = next_lane_vec(a[k]);
+    if (k < 7) {
+      const u32x4 nx = lane0_vec(a[k < 7 ? k + 1 : 7]);
+      if (l == 63) b = nx;
+    } else if (l == 63) {
+      b = last;
+    }
+    const u32x4 o = funnel16(a[k], b, q, r);
+    if (i < j.nvec) j.dv[i] = o;
+  }
+}
+__device__ __forceinline__ void copy_tail(const CopyJob& j) {
+  const uint32_t done = j.head + (j.nvec << 4);
+  for (uint32_t i = (done >> 1) + lane_id(); i < (j.n >> 1); i += 64) j.d16[i] = j.s16[i];
+}
+__device__ __forceinline__ void w_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  const CopyJob j = copy_begin(dst, src, n);
+  for (uint32_t i0 = 0; i0 < j.nvec; i0 += 512) {
+    u32x4 a[8], last;
+    copy_load(j, i0, a, last);
+    copy_store(j, i0, a, last);
+  }
+  copy_tail(j);
+}
 // Task t's result (this wave's own record: source and length) to its final place
 // (place word: payload offset).
 __device__ __forceinline__ void w_emit(uint32_t t, uint64_t pw, const PwOut& po) {
@@ -636,46 +705,78 @@ __device__ __forceinline__ uint32_t emit_ready(uint32_t tc, uint32_t end, uint32
     const uint64_t pw = uni64(poll_word(place_words(po) + tc));
     if (!(pw & kGranuleValid)) break;
     w_emit(tc, pw, po);
+    if (lane_id() == 0) po.state[kPwCopiedOff + tc] = 1;
     tc += stride;
   }
   return tc;
 }
 
-// The placer (one workgroup): scans the size words in task order, kPlaceChunk tasks
-// per step, and publishes every task's place word (output index, payload offset: the
-// exclusive prefix of the kept results -- RB/RoaringArray.java:896-940 writes the
-// payloads in container order).  A dropped task gets the place of the next kept one.
-// After the last step it writes the cookie, the run-flag bitset, the totals and the
-// result shape; the totals word releases the waves' descriptor / offset writes.
-__device__ void pw_placer(uint32_t nt, const PwOut& po, uint32_t* lds) {
+// The placers (kPlacers workgroups): chunk c of kPlaceChunk tasks is placed by placer
+// c % kPlacers.  A placer waits for the chunk's size words, scans them (keep count,
+// payload bytes, run flag, cardinality), takes the inclusive prefix of chunk c - 1 from
+// its chunk word (a decoupled look-back over chunks: the only serial link is one 8-byte
+// hand-off per chunk), publishes chunk c's inclusive prefix, then every task's place word
+// (output index, payload offset: the exclusive prefix of the kept results --
+// RB/RoaringArray.java:896-940 writes the payloads in container order; a dropped task
+// gets the place of the next kept one), its run flags and cardinality.  The placer of the
+// last chunk waits for the others to finish and writes cookie, run-flag bitset, totals
+// and result shape; the totals word releases the waves' descriptor / offset writes.
+constexpr int kPlacers = 4;
+// chunk word: valid | has_run << 62 | containers (17 b) << 45 | payload bytes (45 b)
+__device__ __forceinline__ uint64_t chunk_word(uint32_t run, uint32_t cnt, uint64_t bytes) {
+  return kGranuleValid | ((uint64_t)run << 62) | ((uint64_t)cnt << 45) | bytes;
+}
+
+__device__ void pw_placer(uint32_t nt, const PwOut& po, uint32_t* lds, uint32_t placer) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  uint32_t* rbits = lds;      // bit i: output container i is a run container
-  uint32_t* sh = lds + 2048;  // per-wave partials
+  uint32_t* sh = lds;  // per-wave partials, the chunk's prefix
   const uint64_t* sizes = size_words(po);
   uint64_t* places = place_words(po);
-  for (int i = tid; i < 2048; i += 256) rbits[i] = 0;
-  __syncthreads();
-  uint32_t n_out = 0, any_run = 0, err = 0;
-  uint64_t off_base = 0, card = 0;
-  for (uint32_t c0 = 0; c0 < nt; c0 += kPlaceChunk) {
+  uint64_t* chunks = reinterpret_cast<uint64_t*>(po.state + kPwChunkOff);
+  uint32_t* rbits = reinterpret_cast<uint32_t*>(po.state + kPwRunBitsOff);
+  unsigned long long* card_acc = reinterpret_cast<unsigned long long*>(po.state + kPwCardOff);
+  uint32_t* done = reinterpret_cast<uint32_t*>(po.state + kPwDoneOff);
+  const uint32_t nchunks = (nt + kPlaceChunk - 1) / kPlaceChunk;
+  const uint32_t last_chunk = nchunks ? nchunks - 1 : 0;  // nt == 0: placer 0 writes the empty result
+  uint32_t err = 0;
+  uint64_t prev = 0;  // inclusive prefix word of the chunk before the current one
+  for (uint32_t c = placer; c < nchunks; c += kPlacers) {
+    const uint32_t c0 = c * kPlaceChunk;
     const uint32_t tb = c0 + 16 * tid;
     uint64_t s[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) s[i] = 0;
-    // every size word of the thread's 16 tasks requested at once, re-polled until all are in
-    for (uint32_t spins = 0;; spins++) {
-#pragma unroll
-      for (int i = 0; i < 16; i++)
-        if (tb + i < nt && !(s[i] & kGranuleValid)) s[i] = poll_word(sizes + tb + i);
-      bool ok = true;
-#pragma unroll
-      for (int i = 0; i < 16; i++) ok = ok && (tb + i >= nt || (s[i] & kGranuleValid));
-      if (ok || err) break;  // after one timeout the placer no longer waits (the result is invalid)
-      if (spins > kSpinLimit) {
-        err = 1;
-        break;
+    // The chunk's last task is about the last of its round to be placed by its wave: one
+    // thread waits for that word first (polls ~1 us apart), then every size word of each
+    // thread's 16 tasks is requested at once and re-polled until all are in.
+    if (tid == 0 && !err) {
+      const uint32_t last = min(c0 + kPlaceChunk, nt) - 1;
+      const uint64_t deadline = spin_deadline();
+      while (!(poll_word(sizes + last) & kGranuleValid)) {
+        if (spin_expired(deadline)) {
+          err = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(32);
       }
-      __builtin_amdgcn_s_sleep(2);
+    }
+    __syncthreads();
+    {
+      const uint64_t deadline = spin_deadline();
+      for (;;) {
+#pragma unroll
+        for (int i = 0; i < 16; i++)
+          if (tb + i < nt && !(s[i] & kGranuleValid)) s[i] = poll_word(sizes + tb + i);
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < 16; i++) ok = ok && (tb + i >= nt || (s[i] & kGranuleValid));
+        if (ok || err) break;  // after one timeout the placer no longer waits (the result is invalid)
+        if (spin_expired(deadline)) {
+          err = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(16);
+      }
     }
     uint32_t cnt = 0, bytes = 0, run = 0, cd = 0;  // per thread: <= 16 x 131074 bytes, <= 16 x 65536 values
 #pragma unroll
@@ -711,38 +812,85 @@ __device__ void pw_placer(uint32_t nt, const PwOut& po, uint32_t* lds) {
       tot_card += sh[8 + i];
       tot_r |= sh[12 + i];
     }
-    __syncthreads();  // sh is rewritten by the next step
-    uint32_t idx = n_out + pre_c + (uint32_t)pc;
-    uint64_t off = off_base + pre_b + (uint32_t)pb;
+    // look-back: chunk c - 1's inclusive prefix, then chunk c's published at once
+    if (tid == 0) {
+      if (c == 0) {
+        prev = kGranuleValid;
+      } else {
+        const uint64_t deadline = spin_deadline();
+        while (!((prev = poll_word(chunks + c - 1)) & kGranuleValid)) {
+          if (err || spin_expired(deadline)) {
+            err = 1;
+            prev = kGranuleValid;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      const uint64_t incl = chunk_word((uint32_t)((prev >> 62) & 1) | tot_r,
+                                       (uint32_t)((prev >> 45) & 0x1FFFF) + tot_c,
+                                       (prev & ((1ull << 45) - 1)) + tot_b);
+      __hip_atomic_store(chunks + c, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sh[16] = (uint32_t)prev;
+      sh[17] = (uint32_t)(prev >> 32);
+    }
+    __syncthreads();
+    prev = ((uint64_t)sh[17] << 32) | sh[16];
+    uint32_t idx = (uint32_t)((prev >> 45) & 0x1FFFF) + pre_c + (uint32_t)pc;
+    uint64_t off = (prev & ((1ull << 45) - 1)) + pre_b + (uint32_t)pb;
 #pragma unroll
     for (int i = 0; i < 16; i++) {
       if (tb + i < nt) {
         __hip_atomic_store(places + tb + i, place_word(idx, off), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if ((s[i] >> 62) & 1) {
-          if ((s[i] >> 61) & 1) atomicOr(&rbits[idx >> 5], 1u << (idx & 31));
+          if ((s[i] >> 61) & 1) __hip_atomic_fetch_or(rbits + (idx >> 5), 1u << (idx & 31), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT);
           idx++;
           off += s[i] & 0xFFFFFF;
         }
       }
     }
-    n_out += tot_c;
-    off_base += tot_b;
-    card += tot_card;
-    any_run |= tot_r;
+    if (tid == 0)
+      __hip_atomic_fetch_add(card_acc, (unsigned long long)tot_card, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // this chunk's flag and cardinality atomics are done before it counts as done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0 && c != last_chunk)
+      __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // sh is rewritten by the next chunk
   }
   const PwTail& tl = tail_of(po);
   if (__any(err)) {
     if (lane == 0) atomicOr(tl.err, 1u);
   }
-  __syncthreads();  // rbits complete
+  if (placer != last_chunk % kPlacers) return;
+  // the last chunk's placer: every other chunk's flags and cardinality are in
+  if (tid == 0 && nchunks > 1) {
+    const uint64_t deadline = spin_deadline();
+    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nchunks - 1) {
+      if (spin_expired(deadline)) {
+        atomicOr(tl.err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  const uint64_t fin = nchunks ? poll_word(chunks + last_chunk) : kGranuleValid;
+  const uint32_t n_out = (uint32_t)((fin >> 45) & 0x1FFFF);
+  const uint32_t any_run = (uint32_t)((fin >> 62) & 1);
+  const uint64_t pay = fin & ((1ull << 45) - 1);
   const uint64_t H = header_bytes(n_out, any_run);
   const uint64_t start = tl.payload_base - H;
   uint8_t* base = tl.out + start;
   if (any_run) {  // run-flag bitset (RB/RoaringArray.java:905-913)
-    const uint8_t* rb = reinterpret_cast<const uint8_t*>(rbits);
-    for (uint32_t b = tid; b < (n_out + 7) / 8; b += 256) base[4 + b] = rb[b];
+    for (uint32_t b = tid; b < (n_out + 7) / 8; b += 256) {
+      const uint32_t wv = __hip_atomic_load(rbits + (b >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      base[4 + b] = (uint8_t)(wv >> (8 * (b & 3)));
+    }
   }
   if (tid == 0) {
+    const unsigned long long card = __hip_atomic_load(card_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t cookie[2];
     int nb;
     if (any_run) {  // RB/RoaringArray.java:900-904
@@ -759,8 +907,8 @@ __device__ void pw_placer(uint32_t nt, const PwOut& po, uint32_t* lds) {
     ri.n_out = n_out;
     ri.has_run = any_run;
     ri.header = H;
-    ri.payload = off_base;
-    ri.total = H + off_base;
+    ri.payload = pay;
+    ri.total = H + pay;
     ri.long_card = (int64_t)card;
     ri.card32 = (uint32_t)card;
     ri.any = n_out > 0;
@@ -774,39 +922,36 @@ __device__ void pw_placer(uint32_t nt, const PwOut& po, uint32_t* lds) {
   }
 }
 
-// End of a compute wave (MODE 0): its remaining results to their places, then -- once
-// the totals are in -- the descriptors (key, card - 1) and offsets of its kept results
-// (RB/RoaringArray.java:918-933).  Lane j takes the wave's j-th task.
-__device__ __forceinline__ void pw_finish(uint32_t tc, uint32_t nt, uint32_t stride, const PwOut& po) {
-  uint32_t* err = tail_of(po).err;
-  while (tc < nt) {
-    const uint64_t pw = w_wait_word(place_words(po) + tc, err);
-    if (!pw) return;
-    w_emit(tc, pw, po);
-    tc += stride;
-  }
-  const uint64_t fin = w_wait_word(totals_word(po), err);
-  if (!fin) return;
+// After the compute launch (MODE 0): every task whose result was not copied to its place
+// while the compute ran (its place was published after its wave's last task), and the
+// descriptors (key, card - 1) and offsets of every kept result (RB/RoaringArray.java:918-933).
+// One wave per task over a resident grid; the place words, records and totals are final.
+__global__ __launch_bounds__(256) void k_pair_emit(const uint32_t* __restrict__ n_tasks, uint8_t* pstate) {
+  const PwOut po{pstate};
+  const uint32_t nt = *n_tasks;
+  const uint64_t fin = *totals_word(po);
+  if (!(fin & kGranuleValid)) return;  // the placer timed out: the op's error word is set
   const uint32_t size = (uint32_t)(fin & 0x1FFFF);
   const bool has_run = (fin >> 62) & 1;
   const uint64_t H = header_bytes(size, has_run);
-  uint8_t* base = payload_of(po) - H;
+  uint8_t* payload = payload_of(po);
+  uint8_t* base = payload - H;
   const uint64_t desc_base = has_run ? 4 + (size + 7) / 8 : 8;
   const bool offsets = !has_run || size >= 4;
   const uint64_t off_base = desc_base + 4ull * size;  // both tables are 4 B aligned (payload - 8 or 4 x size)
   const ORec* recs = recs_of(po);
   const uint64_t* places = place_words(po);
-  const uint32_t t0 = uni(blockIdx.x * kWaves + (threadIdx.x >> 6));  // recomputed: not held across the task loop
-  for (uint32_t j0 = 0; t0 + (uint64_t)j0 * stride < nt; j0 += 64) {
-    const uint64_t t = t0 + (uint64_t)(j0 + lane_id()) * stride;
-    if (t < nt) {
-      const ORec& r = recs[t];
-      if (r.keep) {
-        const uint64_t pw = poll_word(places + t);
-        const uint32_t idx = place_idx(pw);
-        *(g_u32*)(base + desc_base + 4ull * idx) = (uint32_t)r.key | ((r.card - 1) << 16);
-        if (offsets) *(g_u32*)(base + off_base + 4ull * idx) = (uint32_t)(H + place_off(pw));
-      }
+  const uint32_t nw = gridDim.x * kWaves;
+  for (uint32_t t = uni(blockIdx.x * kWaves + (threadIdx.x >> 6)); t < nt; t += nw) {
+    const ORec& r = recs[t];
+    if (!uni(r.keep)) continue;
+    const uint64_t pw = uni64(places[t]);
+    if (!uni(po.state[kPwCopiedOff + t]))
+      w_copy(payload + place_off(pw), reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
+    if (lane_id() == 0) {
+      const uint32_t idx = place_idx(pw);
+      *(g_u32*)(base + desc_base + 4ull * idx) = (uint32_t)r.key | ((r.card - 1) << 16);
+      if (offsets) *(g_u32*)(base + off_base + 4ull * idx) = (uint32_t)(H + place_off(pw));
     }
   }
 }
@@ -822,16 +967,18 @@ __device__ __forceinline__ void pw_finish(uint32_t tc, uint32_t nt, uint32_t str
 template <int OP, int MODE>
 __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
                                                       const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
-                                                      const uint8_t* pb, PwOut po, uint32_t* __restrict__ task_card) {
+                                                      const uint8_t* pb, uint8_t* pstate,
+                                                      uint32_t* __restrict__ task_card) {
+  const PwOut po{pstate};  // a plain pointer argument: inferred global (as a struct member it was not)
   __shared__ __align__(16) uint32_t lds_all[kWaves][kWaveLds];
   const uint32_t nt = uni(*n_tasks);
-  if (MODE == 0 && blockIdx.x == gridDim.x - 1) {
-    pw_placer(nt, po, &lds_all[0][0]);
+  if (MODE == 0 && blockIdx.x >= gridDim.x - kPlacers) {
+    pw_placer(nt, po, &lds_all[0][0], blockIdx.x - (gridDim.x - kPlacers));
     return;
   }
   const int w = threadIdx.x >> 6;
   uint32_t* lds = lds_all[w];
-  const uint32_t stride = (MODE == 0 ? gridDim.x - 1 : gridDim.x) * kWaves;
+  const uint32_t stride = (MODE == 0 ? gridDim.x - kPlacers : gridDim.x) * kWaves;
   const uint32_t t0 = uni(blockIdx.x * kWaves + w);
   if (t0 >= nt) return;
   uint32_t t = t0;
@@ -859,7 +1006,6 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
     t = tn;
     cur = nxt;
   }
-  if (MODE == 0) pw_finish(tc, nt, stride, po);
 #if RBG_STAMPS
   const uint64_t life = __builtin_amdgcn_s_memtime() - t_kernel;
   sacc.v[9] += life;
@@ -885,9 +1031,9 @@ template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
                       const uint8_t* pb, PwOut po, uint32_t* task_card) {
   const int res = resident_grid((const void*)&k_pair_wave<OP, MODE>);
-  // MODE 0: the compute workgroups plus the placer, all resident
-  const int g = MODE == 0 ? std::max(1, std::min(grid, res - 1)) + 1 : std::max(1, std::min(grid, res));
-  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, po, task_card);
+  // MODE 0: the compute workgroups plus the placers, all resident
+  const int g = MODE == 0 ? std::max(1, std::min(grid, res - kPlacers)) + kPlacers : std::max(1, std::min(grid, res));
+  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, po.state, task_card);
 }
 
 #if RBG_STAMPS
@@ -912,6 +1058,11 @@ void debug_stamps(uint64_t* out20, bool) {
   for (int i = 0; i < 20; i++) out20[i] = 0;
 }
 #endif
+
+void launch_pairwise_emit(hipStream_t s, const uint32_t* nt, PwOut po) {
+  hipLaunchKernelGGL(k_pair_emit, dim3(std::max(1, resident_grid((const void*)&k_pair_emit))), dim3(256), 0, s, nt,
+                     po.state);
+}
 
 void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
                           const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_epoch, uint32_t epoch,

@@ -59,6 +59,13 @@ def lib():
         L.rbo_time_and_parallel.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
                                             ctypes.c_int, ctypes.c_int]
         L.rbo_time_and_parallel.restype = ctypes.c_double
+        L.rbo_time_pairs.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                     ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
+        L.rbo_time_pairs.restype = ctypes.c_double
+        L.rbo_time_bsi_range_sum.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                             ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int64)]
+        L.rbo_time_bsi_range_sum.restype = ctypes.c_double
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -188,6 +195,22 @@ def time_wide_parallel(op, bufs, threads, reps):
 def time_and_parallel(a, b, threads, reps):
     """Key-parallel RoaringBitmap.and over `threads` key ranges; seconds for reps runs."""
     return lib().rbo_time_and_parallel(a, len(a), b, len(b), threads, reps)
+
+
+def time_pairs(op, bufs, threads, reps):
+    """Loop of RoaringBitmap.and(...).getCardinality() (op "and") or andCardinality (op "and_card")
+    over the pairs (bufs[2i], bufs[2i+1]) on `threads` workers; seconds for reps passes."""
+    arr, lens = _bufs(bufs)
+    return lib().rbo_time_pairs({"and": 0, "and_card": 4}[op], arr, lens, len(bufs) // 2, threads, reps)
+
+
+def time_bsi_range_sum(ebm, slices, lo, hi, reps):
+    """RoaringBitmapSliceIndex.compare(RANGE, lo, hi, null) + sum on the heap BSI (one thread);
+    -> (seconds for reps queries, (sum, count))."""
+    arr, lens = _bufs([ebm] + list(slices))
+    out = (ctypes.c_int64 * 2)()
+    t = lib().rbo_time_bsi_range_sum(arr, lens, len(slices), lo, hi, reps, out)
+    return t, (int(out[0]), int(out[1]))
 
 
 def long_size(buf) -> int:
