@@ -2,25 +2,22 @@
 """Benchmark: pairwise AND of two full 2^32-universe bitmaps (BASELINE.json configs[1], "C2").
 
 One step = RoaringBitmap.and(x1, x2) over a device-resident C2 pair (65,536 mixed
-array/bitmap/run containers each, generated on the GPU), producing the
-device-resident result: every result container computed, typed and written to
-its slot, and the container table compacted (the counterpart of the Java result
-object; the reference's and() does not serialize either).  Key plan, container
-kernel and result placement are all inside the step.  The on-device portable
-serialization of the result (RoaringBitmap.serialize) is timed separately and
-reported in extra.serialize_ms.
+array/bitmap/run containers each, generated on the GPU), ending at the device-resident
+serialized result: key plan, container kernel, result placement and the
+portable serialization (RB/RoaringArray.java:896-940) are all inside the step.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per
 GPU; each rank owns an independent C2 pair (weak scaling, no data-path collective);
 barrier + synchronize bracket the timed loop and the max time over ranks is used.
+At N > 1, extra.c2_and_key_sharded also runs ONE C2 pair split into key ranges over
+the ranks (strong scaling), its result assembled on GPU 0.
 
 Prints ONE JSON line (rank 0).  Extra fields:
   roofline     - dominant kernel (container compute) achieved algorithmic GB/s vs
                  the 8 TB/s HBM peak, timed with HIP events on the engine's stream
   cpu_baseline - the CPU oracle (C++ restatement of the reference, not the JVM: no JDK here) on
-                 this host: key-parallel RoaringBitmap.and on the same C2 pair (value), plus
-                 legs for 1 thread and for C3 wide OR samples (FastAggregation 1 thread,
-                 ParallelAggregation key-parallel), host nproc / CPU model
+                 this host, legs for C1-C5 (BASELINE.md §2 protocol: 5 warmup + 5 measured
+                 iterations, median; ParallelAggregation legs on cores - 1 workers)
   extra        - per-phase times, container mix, result size, C3 (whole sharded op with the
                  result assembled on GPU 0), C4, C5, runOptimize, decode
 
@@ -86,10 +83,8 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
     from roaringbitmap_amd import shard
     from roaringbitmap_amd.engine import synth_key_bytes
     seed = 0xC3000000
-    if kind == 1:
-        ranges = [((65536 * r) // world, (65536 * (r + 1)) // world) for r in range(world)]  # uniform: equal keys
-    else:
-        ranges = shard.key_ranges(synth_key_bytes(kind, seed, n), world)
+    # equal algorithmic input bytes per rank, for uniform and clustered alike
+    ranges = shard.key_ranges(synth_key_bytes(kind, seed, n), world) if world > 1 else [(0, 65536)]
     lo, hi = ranges[rank]
     b = eng.synth(kind, seed, n, lo, hi)
     st = eng.batch_stats(b)
@@ -152,6 +147,52 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
                                {"kernel": "k_wide<AND_SHY>", "kernel_ms": round(kern_ms, 4),
                                 "note": "per key the chain stops at an empty intersection: the bytes read are far "
                                         "below input_bytes, so no roofline fraction is claimed"})}
+
+
+def c2_key_sharded(eng, rank, world, dist, steps, warmup, cdev, in_bytes):
+    """ONE C2 pair's RoaringBitmap.and split into key ranges over the ranks (strong
+    scaling): every rank holds the pair (seeds 0xC2A0 / 0xC2B0) and computes its key range
+    (rbg_ctx_pairwise_range), the shard layout is all-gathered and rank 0's GPU receives every
+    slice straight into its place (shard.assemble).  Equal key ranges: C2 draws each key's
+    container kinds independently, so equal key counts carry equal expected bytes."""
+    import hashlib
+
+    import torch
+    from roaringbitmap_amd import shard
+    a = eng.synth(0, 0xC2A0)
+    b = eng.synth(0, 0xC2B0)
+    lo, hi = (65536 * rank) // world, (65536 * (rank + 1)) // world
+    dev = torch.device("cuda", torch.cuda.current_device())
+    comm = dev if cdev == "cuda" else torch.device("cpu")
+    fill = shard.engine_fill(eng)
+
+    def step():
+        eng.pairwise("and", a, b, key_lo=lo, key_hi=hi)
+        rs = eng.result_stats()
+        lay = shard.exchange_layout(rs["containers"], rs["payload_bytes"], rs["has_run"], device=comm)
+        return shard.assemble(fill, lay, rank, fill_device=dev, comm_device=comm, sync=eng.sync), lay
+
+    for _ in range(warmup):
+        out, lay = step()
+    torch.cuda.synchronize()
+    sha = hashlib.sha256(bytes(out.cpu().numpy().tobytes())).hexdigest()[:16] if rank == 0 else None
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out, lay = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64, device=comm)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    eng.release(a)
+    eng.release(b)
+    ms = float(t[0]) / steps * 1e3
+    return {"workload": f"C2 RoaringBitmap.and of ONE pair, key-range sharded over {world} GPUs, result assembled "
+                        f"on GPU 0", "input_GBps": round(in_bytes / (ms / 1e3) / 1e9, 1), "ms_per_step": round(ms, 4),
+            "input_bytes": int(in_bytes), "result_serialized_bytes": int(lay.nbytes), "result_sha16": sha,
+            "rank0_keys": [lo, hi], "scaling": "strong"}
 
 
 def c4_batch_and_card(eng, n_pairs, rank, world, dist, steps, warmup, cdev):
@@ -454,10 +495,17 @@ def main():
     eng.pairwise("and", a, b)
     rs = eng.result_stats()
     out_bytes = rs["payload_bytes"] + 4 * rs["containers"]
+    import hashlib
+    rs["sha16"] = hashlib.sha256(eng.fetch().serialize()).hexdigest()[:16]  # of the serialized result
 
     stream = torch.cuda.ExternalStream(eng.stream_ptr)
-    for _ in range(args.warmup):
+
+    def c2_step():  # RoaringBitmap.and(x1, x2) -> the device-resident serialized result
         eng.pairwise("and", a, b)
+        eng.serialize()
+
+    for _ in range(args.warmup):
+        c2_step()
     eng.sync()
 
     def barrier():
@@ -471,14 +519,14 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        eng.pairwise("and", a, b)
+        c2_step()
     ev1.record(stream)
     eng.sync()
     barrier()
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
 
-    # on-device portable serialization of the result (not part of and(); reported beside it)
+    # the serialization's own device time (events around it, on the engine's stream)
     ser_ms = 0.0
     for _ in range(args.steps):
         eng.pairwise("and", a, b)
@@ -491,8 +539,8 @@ def main():
         ser_ms += e0.elapsed_time(e1)
     ser_ms /= args.steps
 
-    # per-phase device time of the same op (separate pass: HIP events between phases, on the
-    # engine's stream)
+    # per-phase device time of the op before serialization (separate pass: HIP events between
+    # phases, on the engine's stream)
     eng.profile(args.steps)
     for _ in range(args.steps):
         eng.pairwise("and", a, b)
@@ -514,8 +562,13 @@ def main():
     extra = {}
 
     def run_extra(name, fn):
-        # an extra that raises (on every rank alike) is reported in its entry instead of
-        # ending the run without the headline line
+        # One GPU: an extra that raises is reported in its entry instead of ending the run
+        # without the headline line.  Several ranks: it propagates -- a rank that stopped
+        # inside an extra's collectives or point-to-point assembly would leave the others
+        # blocked there; failing fast lets torch.distributed.run end the whole group.
+        if world > 1:
+            extra[name] = fn()
+            return
         try:
             extra[name] = fn()
         except Exception as e:  # noqa: BLE001
@@ -546,6 +599,8 @@ def main():
                      "frac": round(in_bytes / (card_kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": _pmc_traffic("k_pair_wave_card")}}
     ks = max(3, args.steps // 4)
+    if world > 1:  # the engine's own key split of one pair, beside the weak-scaling headline
+        run_extra("c2_and_key_sharded", lambda: c2_key_sharded(eng, rank, world, dist, ks, 1, cdev, in_bytes))
     if args.c3_n > 0:
         for kind, name in ((1, "c3_uniform_or"), (2, "c3_clustered_or")):
             run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, 1, cdev))
@@ -596,9 +651,7 @@ def main():
                 "input_bytes_per_step": int(in_bytes), "output_bytes_per_step": int(out_bytes),
                 "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
                 "phase_ms": {"plan": round(ph_avg[0], 4), "compute": round(ph_avg[1], 4),
-                             "place": round(ph_avg[2], 4)},
-                "serialize_ms": round(ser_ms, 4),
-                "value_incl_serialize": round(total_in / (step_s + ser_ms / 1e3) / 1e9, 2),
+                             "place": round(ph_avg[2], 4), "serialize": round(ser_ms, 4)},
                 "elements_per_s": round((sa["cardinality"] + sb["cardinality"]) * world / step_s, 1),
                 "operand_mix": {k: [sa[k], sb[k]] for k in ["array", "bitmap", "run"]},
                 "result": rs,

@@ -207,6 +207,10 @@ int rbg_ctx_batch_fetch_range(rbg_ctx* ctx, int32_t batch, size_t first, size_t 
  * container table, the counterpart of the Java result object); it is turned into
  * the portable format only by rbg_ctx_serialize / rbg_ctx_fetch. */
 int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
+/* rbg_ctx_pairwise restricted to keys [key_lo, key_hi): one key-range shard of the op (each
+ * key's result depends on that key's containers only, RB/RoaringBitmap.java:382-399); the
+ * shards of a partition are assembled with rbg_ctx_fetch_shard(_device). */
+int rbg_ctx_pairwise_range(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib, int key_lo, int key_hi);
 /* Enqueue a cardinality op; the int32 lands in device memory, read by rbg_ctx_card. */
 int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
 /* Enqueue a wide op over every bitmap of a batch, restricted to keys [key_lo, key_hi)

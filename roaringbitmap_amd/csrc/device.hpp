@@ -99,32 +99,14 @@ constexpr int kCardWord = 4;
 struct OutCtx {
   uint8_t* out;
   uint64_t payload_base;
-  uint64_t* status;  // per-task words: k_place's totals word status[n_tasks-1]; the fused
-                     // pairwise placement's size words (zeroed by the plan)
+  uint64_t* status;  // per-task look-back words (also the totals word status[n_tasks-1])
   uint32_t* err;
   ORec* recs;
   uint8_t* scratch;  // one kSlotBytes slot per task
   uint64_t* tile_status;  // scan placement: per-tile look-back words
   uint64_t* tile_card;    // scan placement: per-tile result cardinality
-  // fused pairwise placement (pairwise.hip): per-task final (index, payload offset) words;
-  // null elsewhere
-  uint64_t* tpos;
+  uint8_t* kind_by_out;   // k_place: R / not R per output container (run flags of the serialization)
 };
-
-// Fused pairwise placement words (8-byte granules: each is written by one `sc1` store
-// and validates itself, so no ordering is needed around it):
-//   size word  status[t]: valid | keep | run | card (17 b) << 24 | serialized length (24 b)
-//   place word tpos[t]  : valid | output index (17 b) << 44 | payload offset (44 b)
-//   totals word         : valid | has_run << 62 | container count
-constexpr uint64_t kGranuleValid = 1ull << 63;
-__host__ __device__ inline uint64_t size_word(bool keep, bool run, uint32_t card, uint32_t len) {
-  return kGranuleValid | ((uint64_t)keep << 62) | ((uint64_t)run << 61) | ((uint64_t)card << 24) | (uint64_t)len;
-}
-__host__ __device__ inline uint64_t place_word(uint32_t idx, uint64_t off) {
-  return kGranuleValid | ((uint64_t)idx << 44) | off;
-}
-__host__ __device__ inline uint32_t place_idx(uint64_t w) { return (uint32_t)((w >> 44) & 0x1FFFF); }
-__host__ __device__ inline uint64_t place_off(uint64_t w) { return w & ((1ull << 44) - 1); }
 
 // Portable-format header bytes for `size` containers (RB/RoaringArray.java:781-790)
 __host__ __device__ inline uint64_t header_bytes(uint32_t size, uint32_t has_run) {

@@ -138,7 +138,6 @@ struct Ctx {
   int bsi_nbits = 0;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw,
       scalar, scratch;
-  DevBuf pw_state;  // fused pairwise placement state (kernels.hpp)
   size_t result_cap = 0;
   OutCtx pending{};         // output state of the last materialising op
   std::vector<int32_t> pending_src;  // batches the pending result's pass-through records point into
@@ -510,8 +509,7 @@ static int grid_for(size_t tasks, size_t cap = 4096) {
 // Output state of a materialising op: per-task records + scratch slots (the
 // device-resident result), and the portable-format buffer the serialization
 // writes into on fetch.  Card-only ops need no output state.
-static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc, bool card_only,
-                          bool task_slots = true) {
+static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* oc, bool card_only) {
   uint8_t* lb = c->lb.as<uint8_t>();
   *oc = OutCtx{};
   oc->err = reinterpret_cast<uint32_t*>(lb + 64);
@@ -530,13 +528,14 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   const uint64_t P0 = header_reserve(max_tasks);
   CHK(c->result.ensure(P0 + max_payload + 64));
   c->result_cap = P0 + max_payload;
-  if (task_slots) CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1) + 64));
+  CHK(c->scratch.ensure((size_t)kSlotBytes * std::max<size_t>(max_tasks, 1) + 64));
   // the look-back header and tile statuses are zeroed by the op's plan kernel
   c->zlb = reinterpret_cast<uint64_t*>(lb);
   c->ztile = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * kMaxKeys);
   oc->out = c->result.as<uint8_t>();
   oc->payload_base = P0;
-  oc->scratch = task_slots ? c->scratch.as<uint8_t>() : nullptr;
+  oc->scratch = c->scratch.as<uint8_t>();
+  oc->kind_by_out = c->kind_by_out.as<uint8_t>();
   c->pending = *oc;
   c->pending_ub = max_tasks;
   return RBG_OK;
@@ -550,8 +549,7 @@ static int ctx_serialize(Ctx* c) {
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   if (c->serialized) return RBG_OK;
-  launch_serialize(c->stream, grid_for((c->pending_ub + 255) / 256, 256), c->ntasks.as<uint32_t>(), c->pending,
-                   c->kind_by_out.as<uint8_t>());
+  launch_serialize(c->stream, c->ntasks.as<uint32_t>(), c->pending);
   HIPCHK(hipGetLastError());
   c->serialized = true;
   return RBG_OK;
@@ -574,8 +572,11 @@ static int operand(Batch* b, size_t i, const uint16_t** keys, const CDesc** desc
   return RBG_OK;
 }
 
-static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only) {
+static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only, int key_lo = 0,
+                        int key_hi = kMaxKeys) {
   if (op < 0 || op > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
+  key_lo = std::max(0, key_lo);
+  key_hi = std::min(kMaxKeys, key_hi);
   Batch *A, *B;
   CHK(get_batch(c, ia, &A));
   CHK(get_batch(c, ib, &B));
@@ -593,44 +594,25 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     default: ub = std::min<size_t>((size_t)na + nb, kMaxKeys); break;
   }
   OutCtx oc;
-  // the fused placement keeps its task slots in its own state buffer
-  CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only, false));
-  if (!card_only) CHK(c->pw_state.ensure(kPwScratchOff + (size_t)kSlotBytes * std::max<size_t>(ub, 1) + 64));
-  PwOut po{};
-  PwTail tail{};
-  uint8_t* st = card_only ? nullptr : c->pw_state.as<uint8_t>();
-  if (!card_only) {  // placed and serialized inside the compute launch (pairwise.hip)
-    po.state = st;
-    tail.payload = oc.out + oc.payload_base;
-    tail.out = oc.out;
-    tail.payload_base = oc.payload_base;
-    tail.err = oc.err;
-    tail.info = c->info.as<ResultInfo>();
-    tail.card = reinterpret_cast<unsigned long long*>(oc.err) + kCardWord;
-    // the fetch paths (k_shard_table, k_emit) read the records and place words
-    oc.recs = reinterpret_cast<ORec*>(st + kPwRecOff);
-    oc.tpos = reinterpret_cast<uint64_t*>(st + kPwPlaceOff);
-    c->pending = oc;
-  }
+  CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only));
   c->pending_src = {ia, ib};
   c->mark(0);
   dbg(s, "memset");
-  launch_plan_pairwise(s, plan_op, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), B->key_off.as<uint32_t>(),
-                       db, B->payload.as<uint8_t>(), c->wg_epoch.as<uint64_t>(), next_epoch(c), c->tasks.as<PTask>(),
-                       c->ntasks.as<uint32_t>(), c->zlb, c->ztile, oc.err, st, tail);
+  launch_plan_pairwise(s, plan_op, key_lo, key_hi, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(),
+                       B->key_off.as<uint32_t>(), db, B->payload.as<uint8_t>(), c->wg_epoch.as<uint64_t>(),
+                       next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), c->zlb, c->ztile, oc.err);
   dbg(s, "plan");
   c->mark(1);
   const int grid = grid_for((ub + 3) / 4, 16384);  // 4 waves (tasks) per workgroup, clamped to the resident grid
   launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(),
-                  A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), po, c->task_card.as<uint32_t>());
+                  A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), oc, c->task_card.as<uint32_t>());
   dbg(s, "pairwise");
   c->mark(2);
   if (card_only) {
     launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>(), oc.err);
     c->last = 2;
   } else {
-    launch_pairwise_emit(s, c->ntasks.as<uint32_t>(), po);
-    c->serialized = true;
+    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
     c->last = 1;
   }
   c->mark(3);
@@ -1673,6 +1655,11 @@ extern "C" {
 int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
   HIPCHK(hipSetDevice(ctx->c.device));
   return ctx_pairwise(&ctx->c, op, a, ia, b, ib, false);
+}
+int rbg_ctx_pairwise_range(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib, int key_lo, int key_hi) {
+  if (!ctx || key_lo > key_hi) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_pairwise(&ctx->c, op, a, ia, b, ib, false, key_lo, key_hi);
 }
 int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
   HIPCHK(hipSetDevice(ctx->c.device));

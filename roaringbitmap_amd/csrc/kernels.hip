@@ -9,10 +9,9 @@
 //             in the task's scratch slot (arena slot layout) + a task record
 //   place   : tile scan over the task records (container index, payload offset,
 //             totals) -- the result is now materialised on the device
-//   serialize (on fetch only): payload copies into the portable layout, then
-//             descriptors, offset table, run flags and cookie in front of it
-// (wide / BSI / priority-queue ops; the pairwise kernel places and serializes its
-// result inside its own launch, pairwise.hip)
+//   serialize: payload copies into the portable layout, descriptors, offset
+//             table, run flags and cookie in front of it (one launch)
+
 #include <algorithm>
 #include <mutex>
 #include <unordered_map>
@@ -94,7 +93,8 @@ __device__ __forceinline__ void write_info(ResultInfo* info, const OutCtx& oc, u
 }
 
 // ===========================================================================
-// header (RB/RoaringArray.java:896-940): descriptors, offsets, run flags, cookie
+// serialization (RB/RoaringArray.java:896-940), after k_place: one launch writes the
+// whole portable bitmap in front of / into the payload region
 // ===========================================================================
 __device__ __forceinline__ void totals(const OutCtx& oc, uint32_t nt, uint32_t* n_out, uint32_t* has_run,
                                        uint64_t* payload) {
@@ -110,9 +110,14 @@ __device__ __forceinline__ void totals(const OutCtx& oc, uint32_t nt, uint32_t* 
   *payload = s & ((1ULL << 44) - 1);
 }
 
-
-__global__ __launch_bounds__(256) void k_header(const uint32_t* __restrict__ n_tasks, OutCtx oc,
-                                                uint8_t* __restrict__ kind_by_out, ResultInfo* __restrict__ info) {
+// One wave per task record (grid-stride): a kept result's payload bytes go to their offset
+// (w_copy: aligned 16 B loads and stores, the source's misalignment funnel-shifted in
+// registers), and lane 0 writes its descriptor (key, card - 1) and offset-table entry --
+// both tables are 4 B aligned (they end at payload_base).  Threads below the flag-byte
+// count pack the run-flag bitset from k_place's kind-by-output bytes; thread 0 writes the
+// cookie.
+__global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ n_tasks, OutCtx oc,
+                                                   const uint8_t* __restrict__ kind_by_out) {
   const uint32_t nt = *n_tasks;
   uint32_t size, has_run;
   uint64_t payload;
@@ -122,58 +127,43 @@ __global__ __launch_bounds__(256) void k_header(const uint32_t* __restrict__ n_t
   const uint64_t desc_base = has_run ? 4 + (size + 7) / 8 : 8;
   const bool offsets = !has_run || size >= 4;
   const uint64_t off_base = desc_base + 4ull * size;
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
-    const ORec r = oc.recs[t];
-    if (!r.keep) continue;
-    const uint32_t d = (uint32_t)r.key | ((r.card - 1) << 16);
-    uint8_t* pd = base + desc_base + 4ull * r.idx;
-    pd[0] = (uint8_t)d;
-    pd[1] = (uint8_t)(d >> 8);
-    pd[2] = (uint8_t)(d >> 16);
-    pd[3] = (uint8_t)(d >> 24);
-    if (offsets) {
-      const uint32_t o = (uint32_t)(H + r.off);
-      uint8_t* po = base + off_base + 4ull * r.idx;
-      po[0] = (uint8_t)o;
-      po[1] = (uint8_t)(o >> 8);
-      po[2] = (uint8_t)(o >> 16);
-      po[3] = (uint8_t)(o >> 24);
+  const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (has_run) {
+    for (uint32_t b = gid; b < (size + 7) / 8; b += gridDim.x * blockDim.x) {
+      uint8_t v = 0;
+      for (int k = 0; k < 8; k++) {
+        const uint32_t i = 8 * b + k;
+        if (i < size && kind_by_out[i] == DK_R) v |= (uint8_t)(1u << k);
+      }
+      base[4 + b] = v;
     }
-    kind_by_out[r.idx] = r.kind;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (gid == 0) {
     uint32_t cookie[2];
     int nb;
-    if (has_run) {
+    if (has_run) {  // RB/RoaringArray.java:900-904
       cookie[0] = 12347u | ((size - 1) << 16);
       nb = 4;
-    } else {
+    } else {  // :914-917
       cookie[0] = 12346u;
       cookie[1] = size;
       nb = 8;
     }
     const uint8_t* cb = reinterpret_cast<const uint8_t*>(cookie);
     for (int i = 0; i < nb; i++) base[i] = cb[i];
-    (void)info;  // written by k_place
   }
-}
-
-// run-flag bytes: bit i%8 of byte i/8 set iff output container i is a run container
-__global__ __launch_bounds__(256) void k_runflags(const uint32_t* __restrict__ n_tasks, OutCtx oc,
-                                                  const uint8_t* __restrict__ kind_by_out) {
-  uint32_t size, has_run;
-  uint64_t payload;
-  totals(oc, *n_tasks, &size, &has_run, &payload);
-  if (!has_run) return;
-  uint8_t* base = oc.out + oc.payload_base - header_bytes(size, has_run);
-  const uint32_t nbytes = (size + 7) / 8;
-  for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < nbytes; b += gridDim.x * blockDim.x) {
-    uint8_t v = 0;
-    for (int k = 0; k < 8; k++) {
-      const uint32_t i = 8 * b + k;
-      if (i < size && kind_by_out[i] == DK_R) v |= (uint8_t)(1u << k);
+  uint8_t* pay = oc.out + oc.payload_base;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
+    const ORec& r = oc.recs[t];
+    if (!uni(r.keep)) continue;
+    const uint64_t off = uni64(r.off);
+    w_copy(pay + off, reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
+    if (lane_id() == 0) {
+      const uint32_t idx = r.idx;
+      *(g_u32*)(base + desc_base + 4ull * idx) = (uint32_t)r.key | ((r.card - 1) << 16);
+      if (offsets) *(g_u32*)(base + off_base + 4ull * idx) = (uint32_t)(H + off);
     }
-    base[4 + b] = v;
   }
 }
 
@@ -381,6 +371,7 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
     if (t0 + i < nt) {
       oc.recs[t0 + i].idx = idx;
       oc.recs[t0 + i].off = off;
+      if (keep[i] && oc.kind_by_out) oc.kind_by_out[idx] = run[i] ? DK_R : DK_A;  // (the run flags need only R / not R)
     }
     idx += keep[i];
     off += len[i];
@@ -402,15 +393,15 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
   }
 }
 
-// payload copies of the scan placement: one workgroup per task (grid-stride)
-// dst: the payload region (oc.out + oc.payload_base, or a key shard's place in a global bitmap)
+// payload copies of the scan placement (key-shard fetch): one wave per task (grid-stride)
+// dst: the payload region (a key shard's place in a global bitmap)
 __global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ n_tasks, OutCtx oc, uint8_t* __restrict__ dst) {
   const uint32_t nt = *n_tasks;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    const ORec r = oc.recs[t];
-    if (!r.keep) continue;
-    const uint64_t off = oc.tpos ? place_off(oc.tpos[t]) : r.off;
-    group_copy<NT>(dst + off, reinterpret_cast<const uint8_t*>(r.src), r.ser_len, threadIdx.x);
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
+    const ORec& r = oc.recs[t];
+    if (!uni(r.keep)) continue;
+    w_copy(dst + uni64(r.off), reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
   }
 }
 
@@ -424,9 +415,8 @@ __global__ __launch_bounds__(256) void k_shard_table(const uint32_t* __restrict_
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
     const ORec r = oc.recs[t];
     if (!r.keep) continue;
-    // fused pairwise results: (index, offset) are in the place words
-    const uint32_t idx = oc.tpos ? place_idx(oc.tpos[t]) : r.idx;
-    const uint64_t roff = oc.tpos ? place_off(oc.tpos[t]) : r.off;
+    const uint32_t idx = r.idx;
+    const uint64_t roff = r.off;
     const uint32_t d = (uint32_t)r.key | ((r.card - 1) << 16);
     for (int k = 0; k < 4; k++) desc[4ull * idx + k] = (uint8_t)(d >> (8 * k));
     if (offs) {
@@ -482,14 +472,15 @@ void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, cons
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info) {
   hipLaunchKernelGGL(k_place, dim3(64), dim3(256), 0, s, nt, oc, info);
 }
-void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out) {
-  hipLaunchKernelGGL(k_emit, dim3(4096), dim3(256), 0, s, nt, oc, oc.out + oc.payload_base);
-  hipLaunchKernelGGL(k_header, dim3(grid), dim3(256), 0, s, nt, oc, kind_by_out, (ResultInfo*)nullptr);
-  hipLaunchKernelGGL(k_runflags, dim3(32), dim3(256), 0, s, nt, oc, (const uint8_t*)kind_by_out);
+void launch_serialize(hipStream_t s, const uint32_t* nt, OutCtx oc) {
+  hipLaunchKernelGGL(k_serialize, dim3(std::max(1, resident_grid((const void*)&k_serialize))), dim3(256), 0, s, nt, oc,
+                     (const uint8_t*)oc.kind_by_out);
 }
 void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* payload_dst, uint64_t off0,
                             uint8_t* desc, uint8_t* offs, uint8_t* runb) {
-  if (payload_dst) hipLaunchKernelGGL(k_emit, dim3(4096), dim3(256), 0, s, nt, oc, payload_dst);
+  if (payload_dst)
+    hipLaunchKernelGGL(k_emit, dim3(std::max(1, resident_grid((const void*)&k_emit))), dim3(256), 0, s, nt, oc,
+                       payload_dst);
   hipLaunchKernelGGL(k_shard_table, dim3(grid), dim3(256), 0, s, nt, oc, off0, desc, offs, runb);
 }
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info,

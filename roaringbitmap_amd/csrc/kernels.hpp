@@ -102,52 +102,15 @@ void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t
 void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, const uint32_t* wg_count, Task* tasks,
                     uint32_t* n_tasks);
 // pairwise.hip: plan (key alignment + descriptor resolution) and the wave-per-key compute
-// Fused pairwise placement state (one buffer, so the compute kernel holds one pointer for
-// all of it): a header (PwTail, written by the plan kernel; the totals word), then per task
-// the size words, the place words and the records.  Word formats: device.hpp.
-struct PwTail {
-  uint8_t* payload;       // result payload region (out + payload_base)
-  uint8_t* out;           // result buffer: serialized bitmap at out + payload_base - header
-  uint64_t payload_base;
-  uint32_t* err;          // the op's error word (spin timeouts)
-  ResultInfo* info;       // result shape, written by the placer
-  unsigned long long* card;  // 64-bit result cardinality
-};
-// header: PwTail @0, totals word @128, cardinality accumulator @136, chunks-done counter @144,
-// per-chunk inclusive-prefix words @1024 (kPwMaxChunks), run-flag bitset @8192 (8 KiB)
-constexpr size_t kPwHeader = 16384;
-constexpr size_t kPwTotalsOff = 128, kPwCardOff = 136, kPwDoneOff = 144, kPwChunkOff = 1024, kPwRunBitsOff = 8192;
-constexpr int kPwMaxChunks = 64;
-constexpr size_t kPwMaxTasks = 65536;
-constexpr size_t kPwSizeOff = kPwHeader;
-constexpr size_t kPwPlaceOff = kPwSizeOff + 8 * kPwMaxTasks;
-constexpr size_t kPwRecOff = kPwPlaceOff + 8 * kPwMaxTasks;
-constexpr size_t kPwCopiedOff = kPwRecOff + sizeof(ORec) * kPwMaxTasks;  // per task: 1 = already in its place
-constexpr size_t kPwScratchOff = kPwCopiedOff + kPwMaxTasks;             // one kSlotBytes slot per task
-constexpr size_t kPwStateBytes = kPwScratchOff + (size_t)kSlotBytes * kPwMaxTasks + 64;
-// The compute kernel's only output argument: the task slots and everything else are at
-// fixed offsets from it, or read from the state header where they are used (kernel
-// arguments held across the task loop cost SGPRs, which the compiler spilled through
-// VGPRs to scratch -- and a pointer reloaded from there is generic, so its stores went out
-// as flat instructions that also count against lgkmcnt).
-struct PwOut {
-  uint8_t* state;  // kPwStateBytes
-};
 // plan + compaction in one launch: tasks[] in key order, *n_tasks.  wg_epoch: 256 u64
-// (zeroed once per context), epoch: unique per op of the context.
-// state (materialising ops, or null): the fused placement state; its header gets `tail`,
-// its size / place words are zeroed.
-void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
-                          const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_epoch, uint32_t epoch,
-                          PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile, uint32_t* err,
-                          uint8_t* state, PwTail tail);
-// mode 0: materialise and place the result, copying results into the serialized layout as
-// their places are published (the serialized bitmap starts at tail.out + info->start once
-// launch_pairwise_emit has run); mode 1: andCardinality into task_card
+// (zeroed once per context), epoch: unique per op of the context; only keys in [key_lo, key_hi).
+void launch_plan_pairwise(hipStream_t s, int op, int key_lo, int key_hi, const uint32_t* koa, const CDesc* da,
+                          const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb,
+                          uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, uint64_t* zlb,
+                          uint64_t* ztile, uint32_t* err);
+// mode 0: materialise results (task slots + records); mode 1: andCardinality into task_card
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
-                     const uint8_t* pa, const uint8_t* pb, PwOut po, uint32_t* task_card);
-// after a mode-0 launch: the results not yet in their place, and every descriptor / offset
-void launch_pairwise_emit(hipStream_t s, const uint32_t* nt, PwOut po);
+                     const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card);
 // diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
 void debug_stamps(uint64_t* out20, bool reset);
 // diagnostic build (-DRBG_BSI_STAMPS=1): per-phase clock totals of k_bsi_reg
@@ -159,7 +122,7 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
 // portable serialization (payload copies, descriptors, offsets, run flags,
 // cookie) runs only when the result is fetched
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info);
-void launch_serialize(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* kind_by_out);
+void launch_serialize(hipStream_t s, const uint32_t* nt, OutCtx oc);
 // key shard of a global bitmap: payloads into payload_dst, 4 B descriptors into desc, global
 // offsets (off0 + local offset) into offs (nullable), one run-flag byte per container into runb (nullable)
 void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* payload_dst, uint64_t off0,

@@ -1,6 +1,6 @@
 // Pairwise static ops (RB/RoaringBitmap.java and :377, or :860, xor :1071,
-// andNot :444, andCardinality :413) on the MI355X, ending at the serialized result
-// (RB/RoaringArray.java:896-940).  RB/ = reference RoaringBitmap/src/main/java/org/roaringbitmap/.
+// andNot :444, andCardinality :413) on the MI355X.  RB/ = reference
+// RoaringBitmap/src/main/java/org/roaringbitmap/.
 //
 //   k_plan_pairwise : one thread per key: key alignment of the two operands
 //                     (the advanceUntil walks, here O(1) lookups in each batch's
@@ -8,20 +8,9 @@
 //                     32 B task record, and compaction into the dense task list
 //   k_pair_wave     : one wavefront per task over a resident grid; the next
 //                     task's record is fetched with scalar loads while the
-//                     current one runs.  Materialising ops (MODE 0) also place
-//                     and serialize their result inside the same launch:
-//                       - every task publishes its result's size (a self-validating
-//                         8-byte word) as soon as it is written to the task's slot;
-//                       - one extra workgroup (the placer) scans the size words in
-//                         task order, 4,096 tasks per step, and publishes each task's
-//                         output index and payload offset (again one 8-byte word);
-//                       - between its tasks, each compute wave copies its own earlier
-//                         results whose place is published to their final offset in
-//                         the portable layout, so the copies overlap the compute;
-//                       - once every size is in, the placer writes cookie, run flags
-//                         and totals, and each wave the descriptors and offsets of its
-//                         own results.
-//                     The launch leaves the serialized bitmap in the result buffer.
+//                     current one runs, and both operand payloads are requested
+//                     before either is consumed
+// Placement and serialization follow in kernels.hip (k_place, k_serialize).
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -62,32 +51,20 @@ __device__ __forceinline__ int pair_class(int op, int ka, int kb) {
 // One thread per key, 256 workgroups of 256 keys, all resident.  Each workgroup
 // publishes its task count tagged with this op's epoch, sums the counts of the
 // workgroups before it (one per thread, waiting for the epoch), and writes its
-// tasks straight into the dense task list -- plan and compaction in one launch.
-// state (materialising ops): the fused placement's header gets `tail` (block 0) and its
-// per-task size / place words are zeroed here.
-__global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* __restrict__ koa,
+// tasks straight into the dense task list -- plan and compaction in one launch.  Keys
+// outside [key_lo, key_hi) give no task (a key-range shard of the op: every key's result
+// depends on that key's containers only, RB/RoaringBitmap.java:382-399).
+__global__ __launch_bounds__(256) void k_plan_pairwise(int op, int key_lo, int key_hi, const uint32_t* __restrict__ koa,
                                                        const CDesc* __restrict__ da, const uint8_t* __restrict__ pa,
                                                        const uint32_t* __restrict__ kob,
                                                        const CDesc* __restrict__ db, const uint8_t* __restrict__ pb,
                                                        uint64_t* __restrict__ wg_epoch, uint32_t epoch,
                                                        PTask* __restrict__ tasks, uint32_t* __restrict__ n_tasks,
-                                                       uint64_t* zlb, uint64_t* ztile, uint32_t* err,
-                                                       uint8_t* __restrict__ state, PwTail tail) {
+                                                       uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
   __shared__ int wt[4];
   __shared__ int wb[4];
   plan_zero(zlb, ztile);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (state) {
-    reinterpret_cast<uint64_t*>(state + kPwSizeOff)[k] = 0;
-    reinterpret_cast<uint64_t*>(state + kPwPlaceOff)[k] = 0;
-    state[kPwCopiedOff + k] = 0;
-    if (blockIdx.x == 0) {  // header: tail, totals / card / done words, chunk words, run-flag bitset
-      if (threadIdx.x == 0) *reinterpret_cast<PwTail*>(state) = tail;
-      if (threadIdx.x < 3) reinterpret_cast<uint64_t*>(state + kPwTotalsOff)[threadIdx.x] = 0;
-      if (threadIdx.x < kPwMaxChunks) reinterpret_cast<uint64_t*>(state + kPwChunkOff)[threadIdx.x] = 0;
-      for (uint32_t i = threadIdx.x; i < 1024; i += 256) reinterpret_cast<uint64_t*>(state + kPwRunBitsOff)[i] = 0;
-    }
-  }
   PTask t;
   resolve(koa, da, pa, k, t.slot_a, t.card_a, t.kind_a, t.nruns_a);
   resolve(kob, db, pb, k, t.slot_b, t.card_b, t.kind_b, t.nruns_b);
@@ -100,6 +77,7 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, const uint32_t* _
     case OP_ANDNOT: f = ia; break;
     default: f = ia && ib; break;  // AND and andCardinality
   }
+  if ((int)k < key_lo || (int)k >= key_hi) f = 0;
   int tot;
   const int lane_pre = wave_excl(f, &tot);
   if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = tot;
@@ -137,7 +115,7 @@ constexpr int kWaves = 4;  // waves per workgroup
 // u32 words of LDS per wave: the 8 KiB bitmap map / staging area, plus room for
 // the run lists of run-domain R AND R (4 waves x 10 KiB x 4 workgroups = 160 KiB)
 constexpr int kWaveLds = 2560;
-static_assert(kWaveLds >= 2048 + 32, "the 8 KiB bitmap map / staging area; the placer's run flags and partials");
+static_assert(kWaveLds >= 2048, "the 8 KiB bitmap map / staging area");
 
 // Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
 // pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
@@ -174,31 +152,15 @@ struct StampAcc {
 __device__ __forceinline__ void prio_hi() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ void prio_lo() { __builtin_amdgcn_s_setprio(0); }
 
-// the fused placement state (kernels.hpp)
-__device__ __forceinline__ uint64_t* size_words(const PwOut& po) {
-  return reinterpret_cast<uint64_t*>(po.state + kPwSizeOff);
-}
-__device__ __forceinline__ uint64_t* place_words(const PwOut& po) {
-  return reinterpret_cast<uint64_t*>(po.state + kPwPlaceOff);
-}
-__device__ __forceinline__ ORec* recs_of(const PwOut& po) { return reinterpret_cast<ORec*>(po.state + kPwRecOff); }
-__device__ __forceinline__ uint64_t* totals_word(const PwOut& po) {
-  return reinterpret_cast<uint64_t*>(po.state + kPwTotalsOff);
-}
-__device__ __forceinline__ const PwTail& tail_of(const PwOut& po) { return *reinterpret_cast<const PwTail*>(po.state); }
-__device__ __forceinline__ uint8_t* scratch_of(const PwOut& po) { return po.state + kPwScratchOff; }
-__device__ __forceinline__ uint8_t* payload_of(const PwOut& po) { return tail_of(po).payload; }
-
 // Records one task's output.  Staged results (LDS) are copied to the task's
 // scratch slot (arena slot layout); results already in the slot or pass-through
-// containers are referenced in place.  The record (source, length, type) stays with
-// the wave; the size word (keep, run, cardinality, length) goes to the placer.
+// containers are referenced in place.  k_place and the serializer follow.
 __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
-                                        uint32_t len, uint32_t card, uint32_t key, int kind, const PwOut& po) {
+                                        uint32_t len, uint32_t card, uint32_t key, int kind, const OutCtx& oc) {
   const int l = lane_id();
   uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
   if (keep && staged) {
-    uint8_t* slot = scratch_of(po) + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
     copy_lds_to_global<64>(slot, lds, len, l);
     srcaddr = reinterpret_cast<uint64_t>(slot);
   }
@@ -212,9 +174,7 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
     r.key = (uint16_t)key;
     r.kind = (uint8_t)kind;
     r.keep = keep ? 1 : 0;
-    recs_of(po)[t] = r;
-    __hip_atomic_store(size_words(po) + t, size_word(keep, keep && kind == DK_R, card, keep ? len : 0), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    oc.recs[t] = r;
   }
 }
 
@@ -226,7 +186,7 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
 // -- go straight to the task's scratch slot.
 template <int OP, int MODE>
 __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard, const uint8_t* pslot, int mkind,
-                                            int mcard, const uint8_t* mslot, const PwOut& po, uint32_t* task_card,
+                                            int mcard, const uint8_t* mslot, const OutCtx& oc, uint32_t* task_card,
                                             uint32_t* lds SACC_PARAM) {
   STAMP_DECL
   // the array's values are requested first, so their memory latency overlaps the
@@ -306,20 +266,20 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
   }
   const int c = (int)ctot;
   wsync();
-  uint8_t* slot = scratch_of(po) + (size_t)t * kSlotBytes;
+  uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
   const uint4* sv = reinterpret_cast<const uint4*>(lds);
   uint4* dv = reinterpret_cast<uint4*>(slot);
   for (int k = l; k < (2 * c + 15) >> 4; k += 64) dv[k] = sv[k];  // the slot has room for the rounded tail
   STAMP(5);
   // empty results are dropped (RB/RoaringBitmap.java:389,456)
-  w_place(t, c > 0, slot, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, po);
+  w_place(t, c > 0, slot, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, oc);
   STAMP(6);
 }
 
 // Filter-class task (pass-through clone, or a filter), one wave, wave-uniform branches.
 template <int OP, int MODE>
 __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                                  const PwOut& po, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
   const int ka = tk.kind_a, kb = tk.kind_b;
   if (ka == kAbsent || kb == kAbsent) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
     if (MODE == 0) {
@@ -329,7 +289,7 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
       const uint32_t nr = from_a ? tk.nruns_a : tk.nruns_b;
       const uint8_t* src = (from_a ? pa + tk.slot_a : pb + tk.slot_b) + (kind == DK_R ? 2 : 0);
       const uint32_t len = kind == DK_A ? 2 * card : kind == DK_B ? 8192u : 2 + 4 * nr;
-      w_place(t, true, src, false, lds, len, card, tk.key, kind, po);
+      w_place(t, true, src, false, lds, len, card, tk.key, kind, oc);
     }
     return;
   }
@@ -338,9 +298,9 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
   const uint8_t* sb = pb + tk.slot_b;
   // filter the array (A & A: the smaller one; A \ x: c1) through a map of the other operand
   if (ka == DK_A && (OP == OP_ANDNOT || kb != DK_A || ca <= cb))
-    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, po, task_card, lds SACC_ARG);
+    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, oc, task_card, lds SACC_ARG);
   else
-    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, po, task_card, lds SACC_ARG);
+    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, oc, task_card, lds SACC_ARG);
 }
 
 // R AND R in the run domain (RB/RunContainer.java and(RunContainer)): the
@@ -436,7 +396,7 @@ __device__ __forceinline__ void runs_to_lds2(const uint8_t* sa, int na, uint32_t
 
 template <int MODE>
 __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                            const PwOut& po, uint32_t* task_card, uint32_t* lds) {
+                                            const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
   const int na = tk.nruns_a, nb = tk.nruns_b;
   if (na + nb + 2 > kWaveLds) return false;
   const int l = lane_id();
@@ -457,18 +417,18 @@ __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const u
     return true;
   }
   if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389)
-    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, po);
+    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
     return true;
   }
   int nr;
   const int off = wave_excl(cnt, &nr);
   nr = (int)uni((uint32_t)nr);
   if (eff(c, nr) != DK_R) return false;
-  uint8_t* slot = scratch_of(po) + (size_t)t * kSlotBytes;
+  uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
   int cnt2 = 0, card2 = 0;
   rr_merge<true>(lds, na, nb, d0, d1, cnt2, card2, reinterpret_cast<uint32_t*>(slot + 4) + off);
   if (l == 0) *reinterpret_cast<uint16_t*>(slot + 2) = (uint16_t)nr;
-  w_place(t, true, slot + 2, false, lds, 2u + 4u * (uint32_t)nr, (uint32_t)c, tk.key, DK_R, po);
+  w_place(t, true, slot + 2, false, lds, 2u + 4u * (uint32_t)nr, (uint32_t)c, tk.key, DK_R, oc);
   return true;
 }
 
@@ -477,10 +437,10 @@ __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const u
 // staged in LDS).  One wave, wave-uniform branches.
 template <int OP, int MODE>
 __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                                  const PwOut& po, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
   const int ka = tk.kind_a, kb = tk.kind_b;
   const int ca = (int)tk.card_a, cb = (int)tk.card_b;
-  if (OP == OP_AND && ka == DK_R && kb == DK_R && rr_and_task<MODE>(t, tk, pa, pb, po, task_card, lds)) return;
+  if (OP == OP_AND && ka == DK_R && kb == DK_R && rr_and_task<MODE>(t, tk, pa, pb, oc, task_card, lds)) return;
   STAMP_DECL
   WCtr x;
   w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, (uint8_t)ka, 0}, pa, lds, x);
@@ -494,16 +454,16 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
     return;
   }
   if (c == 0) {  // empty results are dropped (RB/RoaringBitmap.java:389,456,1084)
-    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, po);
+    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
     return;
   }
   const bool use_eff = pairwise_needs_runs(OP, ka, ca, kb, cb);
   const int kind = use_eff ? eff(c, w_runs(x)) : pairwise_kind(OP, ka, kb, c);
   STAMP(2);
   if (kind == DK_B) {
-    uint8_t* slot = scratch_of(po) + (size_t)t * kSlotBytes;
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
     w_store_bitmap(slot, x);
-    w_place(t, true, slot, false, lds, 8192, (uint32_t)c, tk.key, DK_B, po);
+    w_place(t, true, slot, false, lds, 8192, (uint32_t)c, tk.key, DK_B, oc);
     STAMP(3);
     return;
   }
@@ -511,7 +471,7 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
   if (kind == DK_A) len = w_stage(DK_A, x, c, lds);
   else len = 2u + 4u * (uint32_t)w_stage_runs(x, lds);
   STAMP(7);
-  w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, po);
+  w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, oc);
   STAMP(8);
 }
 
@@ -530,430 +490,12 @@ __device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
 
 template <int OP, int MODE>
 __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                         const PwOut& po, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+                                         const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
   prio_hi();
   if (pair_class(OP, tk.kind_a, tk.kind_b) == 1)
-    filter_class_task<OP, MODE>(t, tk, pa, pb, po, task_card, lds SACC_ARG);
+    filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
   else
-    bitmap_class_task<OP, MODE>(t, tk, pa, pb, po, task_card, lds SACC_ARG);
-}
-
-// ===========================================================================
-// fused placement and serialization (MODE 0)
-// ===========================================================================
-constexpr int kPlaceChunk = 4096;          // tasks per placer step (16 per thread)
-
-// 8-byte word written by another CU, polled with an `sc1` load (bypasses this CU's L1)
-__device__ __forceinline__ uint64_t poll_word(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Spin deadlines on the 100 MHz constant clock: a spin that outlives one has waited for a
-// wave that cannot come (the op's error word is set and nothing hangs).
-constexpr uint64_t kSpinTicks = 200000000;  // 2 s
-__device__ __forceinline__ uint64_t spin_deadline() { return __builtin_amdgcn_s_memrealtime() + kSpinTicks; }
-__device__ __forceinline__ bool spin_expired(uint64_t deadline) { return __builtin_amdgcn_s_memrealtime() > deadline; }
-
-// n bytes from src to dst (even addresses, n even), one wave.  The destination body is
-// written as aligned 16 B vectors; each is the 16 bytes at `shift` (the source's offset
-// from 16 B alignment at that point) inside two consecutive aligned source vectors: lane l
-// loads aligned source vector i, takes vector i + 1 from lane l + 1 (a DPP lane shift;
-// lane 63 from the next group's lane 0) and funnel-shifts the pair (alignbyte).  So every
-// load and store is a coalesced 16 B access, 8 per lane in flight.  The unaligned head and
-// tail go as u16.  Reads up to 16 bytes past the end of src (slots and payload arenas carry
-// slack).  The pointers come from memory (records, the state header), so they are generic
-// to the compiler: the accesses go through global-address-space types (flat instructions
-// would also count against lgkmcnt).
-typedef __attribute__((address_space(1))) uint16_t g_u16;
-typedef __attribute__((address_space(1))) uint32_t g_u32;
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) u32x4 g_u32x4;
-
-__device__ __forceinline__ u32x4 next_lane_vec(u32x4 v) {
-  u32x4 r;
-  r.x = from_next_lane(v.x);
-  r.y = from_next_lane(v.y);
-  r.z = from_next_lane(v.z);
-  r.w = from_next_lane(v.w);
-  return r;
-}
-__device__ __forceinline__ u32x4 lane0_vec(u32x4 v) {
-  u32x4 r;
-  r.x = lane0u(v.x);
-  r.y = lane0u(v.y);
-  r.z = lane0u(v.z);
-  r.w = lane0u(v.w);
-  return r;
-}
-// the 16 bytes at byte offset 4q + r (q wave-uniform, r in {0, 2}) of the 32-byte pair (a, b)
-__device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t q, uint32_t r) {
-  u32x4 o;
-  if (q == 0) {
-    o.x = __builtin_amdgcn_alignbyte(a.y, a.x, r);
-    o.y = __builtin_amdgcn_alignbyte(a.z, a.y, r);
-    o.z = __builtin_amdgcn_alignbyte(a.w, a.z, r);
-    o.w = __builtin_amdgcn_alignbyte(b.x, a.w, r);
-  } else if (q == 1) {
-    o.x = __builtin_amdgcn_alignbyte(a.z, a.y, r);
-    o.y = __builtin_amdgcn_alignbyte(a.w, a.z, r);
-    o.z = __builtin_amdgcn_alignbyte(b.x, a.w, r);
-    o.w = __builtin_amdgcn_alignbyte(b.y, b.x, r);
-  } else if (q == 2) {
-    o.x = __builtin_amdgcn_alignbyte(a.w, a.z, r);
-    o.y = __builtin_amdgcn_alignbyte(b.x, a.w, r);
-    o.z = __builtin_amdgcn_alignbyte(b.y, b.x, r);
-    o.w = __builtin_amdgcn_alignbyte(b.z, b.y, r);
-  } else {
-    o.x = __builtin_amdgcn_alignbyte(b.x, a.w, r);
-    o.y = __builtin_amdgcn_alignbyte(b.y, b.x, r);
-    o.z = __builtin_amdgcn_alignbyte(b.z, b.y, r);
-    o.w = __builtin_amdgcn_alignbyte(b.w, b.z, r);
-  }
-  return o;
-}
-
-struct CopyJob {
-  const g_u16* s16;
-  g_u16* d16;
-  const g_u32x4* sv;  // aligned source vectors
-  g_u32x4* dv;        // aligned destination body
-  uint32_t n, head, nvec, shift;
-};
-// the unaligned head (u16 by the first lanes) and the body's geometry
-__device__ __forceinline__ CopyJob copy_begin(uint8_t* dst, const uint8_t* src, uint32_t n) {
-  const int l = lane_id();
-  CopyJob j;
-  const uintptr_t d = reinterpret_cast<uintptr_t>(dst);
-  j.head = (uint32_t)((16 - (d & 15)) & 15);
-  if (j.head > n) j.head = n;
-  j.n = n;
-  j.s16 = (const g_u16*)src;
-  j.d16 = (g_u16*)dst;
-  if (l < (int)(j.head >> 1)) j.d16[l] = j.s16[l];
-  const uintptr_t s = reinterpret_cast<uintptr_t>(src + j.head);
-  j.shift = (uint32_t)(s & 15);  // even
-  j.sv = (const g_u32x4*)(s - j.shift);
-  j.dv = (g_u32x4*)(dst + j.head);
-  j.nvec = (n - j.head) >> 4;
-  return j;
-}
-// pass i0 (512 body vectors): every source vector the pass needs, requested at once (one
-// past the body too: the partner of the last one; lane 63 of the last group also needs
-// aligned vector i0 + 512 -- the one past the body when this is the last pass: it still
-// holds tail bytes or slack)
-__device__ __forceinline__ void copy_load(const CopyJob& j, uint32_t i0, u32x4 a[8], u32x4& last) {
-  const int l = lane_id();
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t i = i0 + 64 * k + l;
-    if (i <= j.nvec && (j.shift != 0 || i < j.nvec)) a[k] = j.sv[i];
-    else a[k] = u32x4{0, 0, 0, 0};
-  }
-  last = u32x4{0, 0, 0, 0};
-  if (j.shift != 0 && l == 63 && i0 + 511 < j.nvec) last = j.sv[i0 + 512];
-}
-__device__ __forceinline__ void copy_store(const CopyJob& j, uint32_t i0, const u32x4 a[8], const u32x4& last) {
-  const int l = lane_id();
-  if (j.shift == 0) {
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint32_t i = i0 + 64 * k + l;
-      if (i < j.nvec) j.dv[i] = a[k];
-    }
-    return;
-  }
-  const uint32_t q = j.shift >> 2, r = j.shift & 3;
-#pragma unroll
-  for (int k = 0; k < 8; k++) {
-    const uint32_t i = i0 + 64 * k + l;
-    u32x4 b = next_lane_vec(a[k]);
-    if (k < 7) {
-      const u32x4 nx = lane0_vec(a[k < 7 ? k + 1 : 7]);
-      if (l == 63) b = nx;
-    } else if (l == 63) {
-      b = last;
-    }
-    const u32x4 o = funnel16(a[k], b, q, r);
-    if (i < j.nvec) j.dv[i] = o;
-  }
-}
-__device__ __forceinline__ void copy_tail(const CopyJob& j) {
-  const uint32_t done = j.head + (j.nvec << 4);
-  for (uint32_t i = (done >> 1) + lane_id(); i < (j.n >> 1); i += 64) j.d16[i] = j.s16[i];
-}
-__device__ __forceinline__ void w_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
-  const CopyJob j = copy_begin(dst, src, n);
-  for (uint32_t i0 = 0; i0 < j.nvec; i0 += 512) {
-    u32x4 a[8], last;
-    copy_load(j, i0, a, last);
-    copy_store(j, i0, a, last);
-  }
-  copy_tail(j);
-}
-// Task t's result (this wave's own record: source and length) to its final place
-// (place word: payload offset).
-__device__ __forceinline__ void w_emit(uint32_t t, uint64_t pw, const PwOut& po) {
-  const ORec& r = recs_of(po)[t];
-  if (!uni(r.keep)) return;
-  w_copy(payload_of(po) + place_off(pw), reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
-}
-
-// Own tasks tc, tc + stride, ... below `end` whose place is published go to their
-// final place; returns the first one still waiting.
-__device__ __forceinline__ uint32_t emit_ready(uint32_t tc, uint32_t end, uint32_t stride, const PwOut& po) {
-  while (tc < end) {
-    const uint64_t pw = uni64(poll_word(place_words(po) + tc));
-    if (!(pw & kGranuleValid)) break;
-    w_emit(tc, pw, po);
-    if (lane_id() == 0) po.state[kPwCopiedOff + tc] = 1;
-    tc += stride;
-  }
-  return tc;
-}
-
-// The placers (kPlacers workgroups): chunk c of kPlaceChunk tasks is placed by placer
-// c % kPlacers.  A placer waits for the chunk's size words, scans them (keep count,
-// payload bytes, run flag, cardinality), takes the inclusive prefix of chunk c - 1 from
-// its chunk word (a decoupled look-back over chunks: the only serial link is one 8-byte
-// hand-off per chunk), publishes chunk c's inclusive prefix, then every task's place word
-// (output index, payload offset: the exclusive prefix of the kept results --
-// RB/RoaringArray.java:896-940 writes the payloads in container order; a dropped task
-// gets the place of the next kept one), its run flags and cardinality.  The placer of the
-// last chunk waits for the others to finish and writes cookie, run-flag bitset, totals
-// and result shape; the totals word releases the waves' descriptor / offset writes.
-constexpr int kPlacers = 4;
-// chunk word: valid | has_run << 62 | containers (17 b) << 45 | payload bytes (45 b)
-__device__ __forceinline__ uint64_t chunk_word(uint32_t run, uint32_t cnt, uint64_t bytes) {
-  return kGranuleValid | ((uint64_t)run << 62) | ((uint64_t)cnt << 45) | bytes;
-}
-
-__device__ void pw_placer(uint32_t nt, const PwOut& po, uint32_t* lds, uint32_t placer) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  uint32_t* sh = lds;  // per-wave partials, the chunk's prefix
-  const uint64_t* sizes = size_words(po);
-  uint64_t* places = place_words(po);
-  uint64_t* chunks = reinterpret_cast<uint64_t*>(po.state + kPwChunkOff);
-  uint32_t* rbits = reinterpret_cast<uint32_t*>(po.state + kPwRunBitsOff);
-  unsigned long long* card_acc = reinterpret_cast<unsigned long long*>(po.state + kPwCardOff);
-  uint32_t* done = reinterpret_cast<uint32_t*>(po.state + kPwDoneOff);
-  const uint32_t nchunks = (nt + kPlaceChunk - 1) / kPlaceChunk;
-  const uint32_t last_chunk = nchunks ? nchunks - 1 : 0;  // nt == 0: placer 0 writes the empty result
-  uint32_t err = 0;
-  uint64_t prev = 0;  // inclusive prefix word of the chunk before the current one
-  for (uint32_t c = placer; c < nchunks; c += kPlacers) {
-    const uint32_t c0 = c * kPlaceChunk;
-    const uint32_t tb = c0 + 16 * tid;
-    uint64_t s[16];
-#pragma unroll
-    for (int i = 0; i < 16; i++) s[i] = 0;
-    // The chunk's last task is about the last of its round to be placed by its wave: one
-    // thread waits for that word first (polls ~1 us apart), then every size word of each
-    // thread's 16 tasks is requested at once and re-polled until all are in.
-    if (tid == 0 && !err) {
-      const uint32_t last = min(c0 + kPlaceChunk, nt) - 1;
-      const uint64_t deadline = spin_deadline();
-      while (!(poll_word(sizes + last) & kGranuleValid)) {
-        if (spin_expired(deadline)) {
-          err = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(32);
-      }
-    }
-    __syncthreads();
-    {
-      const uint64_t deadline = spin_deadline();
-      for (;;) {
-#pragma unroll
-        for (int i = 0; i < 16; i++)
-          if (tb + i < nt && !(s[i] & kGranuleValid)) s[i] = poll_word(sizes + tb + i);
-        bool ok = true;
-#pragma unroll
-        for (int i = 0; i < 16; i++) ok = ok && (tb + i >= nt || (s[i] & kGranuleValid));
-        if (ok || err) break;  // after one timeout the placer no longer waits (the result is invalid)
-        if (spin_expired(deadline)) {
-          err = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(16);
-      }
-    }
-    uint32_t cnt = 0, bytes = 0, run = 0, cd = 0;  // per thread: <= 16 x 131074 bytes, <= 16 x 65536 values
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const bool keep = tb + i < nt && ((s[i] >> 62) & 1);
-      cnt += keep ? 1u : 0u;
-      bytes += keep ? (uint32_t)(s[i] & 0xFFFFFF) : 0u;
-      run |= keep ? (uint32_t)((s[i] >> 61) & 1) : 0u;
-      cd += keep ? (uint32_t)((s[i] >> 24) & 0x1FFFF) : 0u;
-    }
-    int wc, wb;
-    const int pc = wave_excl((int)cnt, &wc);
-    const int pb = wave_excl((int)bytes, &wb);  // a wave's bytes < 2^28
-    const int wcard = wave_sum_i((int)cd);      // a wave's values <= 2^26
-    const int wr = __any(run) ? 1 : 0;
-    if (lane == 0) {
-      sh[w] = (uint32_t)wc;
-      sh[4 + w] = (uint32_t)wb;
-      sh[8 + w] = (uint32_t)wcard;
-      sh[12 + w] = (uint32_t)wr;
-    }
-    __syncthreads();
-    uint32_t pre_c = 0, pre_b = 0, tot_c = 0, tot_r = 0;
-    uint64_t tot_b = 0, tot_card = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if (i < w) {
-        pre_c += sh[i];
-        pre_b += sh[4 + i];
-      }
-      tot_c += sh[i];
-      tot_b += sh[4 + i];
-      tot_card += sh[8 + i];
-      tot_r |= sh[12 + i];
-    }
-    // look-back: chunk c - 1's inclusive prefix, then chunk c's published at once
-    if (tid == 0) {
-      if (c == 0) {
-        prev = kGranuleValid;
-      } else {
-        const uint64_t deadline = spin_deadline();
-        while (!((prev = poll_word(chunks + c - 1)) & kGranuleValid)) {
-          if (err || spin_expired(deadline)) {
-            err = 1;
-            prev = kGranuleValid;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(2);
-        }
-      }
-      const uint64_t incl = chunk_word((uint32_t)((prev >> 62) & 1) | tot_r,
-                                       (uint32_t)((prev >> 45) & 0x1FFFF) + tot_c,
-                                       (prev & ((1ull << 45) - 1)) + tot_b);
-      __hip_atomic_store(chunks + c, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      sh[16] = (uint32_t)prev;
-      sh[17] = (uint32_t)(prev >> 32);
-    }
-    __syncthreads();
-    prev = ((uint64_t)sh[17] << 32) | sh[16];
-    uint32_t idx = (uint32_t)((prev >> 45) & 0x1FFFF) + pre_c + (uint32_t)pc;
-    uint64_t off = (prev & ((1ull << 45) - 1)) + pre_b + (uint32_t)pb;
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      if (tb + i < nt) {
-        __hip_atomic_store(places + tb + i, place_word(idx, off), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((s[i] >> 62) & 1) {
-          if ((s[i] >> 61) & 1) __hip_atomic_fetch_or(rbits + (idx >> 5), 1u << (idx & 31), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT);
-          idx++;
-          off += s[i] & 0xFFFFFF;
-        }
-      }
-    }
-    if (tid == 0)
-      __hip_atomic_fetch_add(card_acc, (unsigned long long)tot_card, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // this chunk's flag and cardinality atomics are done before it counts as done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0 && c != last_chunk)
-      __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();  // sh is rewritten by the next chunk
-  }
-  const PwTail& tl = tail_of(po);
-  if (__any(err)) {
-    if (lane == 0) atomicOr(tl.err, 1u);
-  }
-  if (placer != last_chunk % kPlacers) return;
-  // the last chunk's placer: every other chunk's flags and cardinality are in
-  if (tid == 0 && nchunks > 1) {
-    const uint64_t deadline = spin_deadline();
-    while (__hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < nchunks - 1) {
-      if (spin_expired(deadline)) {
-        atomicOr(tl.err, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-  }
-  __syncthreads();
-  const uint64_t fin = nchunks ? poll_word(chunks + last_chunk) : kGranuleValid;
-  const uint32_t n_out = (uint32_t)((fin >> 45) & 0x1FFFF);
-  const uint32_t any_run = (uint32_t)((fin >> 62) & 1);
-  const uint64_t pay = fin & ((1ull << 45) - 1);
-  const uint64_t H = header_bytes(n_out, any_run);
-  const uint64_t start = tl.payload_base - H;
-  uint8_t* base = tl.out + start;
-  if (any_run) {  // run-flag bitset (RB/RoaringArray.java:905-913)
-    for (uint32_t b = tid; b < (n_out + 7) / 8; b += 256) {
-      const uint32_t wv = __hip_atomic_load(rbits + (b >> 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      base[4 + b] = (uint8_t)(wv >> (8 * (b & 3)));
-    }
-  }
-  if (tid == 0) {
-    const unsigned long long card = __hip_atomic_load(card_acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t cookie[2];
-    int nb;
-    if (any_run) {  // RB/RoaringArray.java:900-904
-      cookie[0] = 12347u | ((n_out - 1) << 16);
-      nb = 4;
-    } else {  // :914-917
-      cookie[0] = 12346u;
-      cookie[1] = n_out;
-      nb = 8;
-    }
-    const uint8_t* cb = reinterpret_cast<const uint8_t*>(cookie);
-    for (int i = 0; i < nb; i++) base[i] = cb[i];
-    ResultInfo ri;
-    ri.n_out = n_out;
-    ri.has_run = any_run;
-    ri.header = H;
-    ri.payload = pay;
-    ri.total = H + pay;
-    ri.long_card = (int64_t)card;
-    ri.card32 = (uint32_t)card;
-    ri.any = n_out > 0;
-    ri.start = start;
-    ri.err = 0;
-    ri.pad = 0;
-    *tl.info = ri;
-    *tl.card = card;
-    __hip_atomic_store(totals_word(po), kGranuleValid | ((uint64_t)any_run << 62) | n_out, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// After the compute launch (MODE 0): every task whose result was not copied to its place
-// while the compute ran (its place was published after its wave's last task), and the
-// descriptors (key, card - 1) and offsets of every kept result (RB/RoaringArray.java:918-933).
-// One wave per task over a resident grid; the place words, records and totals are final.
-__global__ __launch_bounds__(256) void k_pair_emit(const uint32_t* __restrict__ n_tasks, uint8_t* pstate) {
-  const PwOut po{pstate};
-  const uint32_t nt = *n_tasks;
-  const uint64_t fin = *totals_word(po);
-  if (!(fin & kGranuleValid)) return;  // the placer timed out: the op's error word is set
-  const uint32_t size = (uint32_t)(fin & 0x1FFFF);
-  const bool has_run = (fin >> 62) & 1;
-  const uint64_t H = header_bytes(size, has_run);
-  uint8_t* payload = payload_of(po);
-  uint8_t* base = payload - H;
-  const uint64_t desc_base = has_run ? 4 + (size + 7) / 8 : 8;
-  const bool offsets = !has_run || size >= 4;
-  const uint64_t off_base = desc_base + 4ull * size;  // both tables are 4 B aligned (payload - 8 or 4 x size)
-  const ORec* recs = recs_of(po);
-  const uint64_t* places = place_words(po);
-  const uint32_t nw = gridDim.x * kWaves;
-  for (uint32_t t = uni(blockIdx.x * kWaves + (threadIdx.x >> 6)); t < nt; t += nw) {
-    const ORec& r = recs[t];
-    if (!uni(r.keep)) continue;
-    const uint64_t pw = uni64(places[t]);
-    if (!uni(po.state[kPwCopiedOff + t]))
-      w_copy(payload + place_off(pw), reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
-    if (lane_id() == 0) {
-      const uint32_t idx = place_idx(pw);
-      *(g_u32*)(base + desc_base + 4ull * idx) = (uint32_t)r.key | ((r.card - 1) << 16);
-      if (offsets) *(g_u32*)(base + off_base + 4ull * idx) = (uint32_t)(H + place_off(pw));
-    }
-  }
+    bitmap_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
 }
 
 // One wave per task, static stride over a resident grid (a contended ticket
@@ -961,28 +503,19 @@ __global__ __launch_bounds__(256) void k_pair_emit(const uint32_t* __restrict__ 
 // each).  The next task's record is loaded while this one runs.  Filter-class
 // and bitmap-class tasks share the launch: separate kernels per class were
 // measured 15 % slower on the C2 mix (tail + an extra dependent index load).
-// MODE 0: materialise, place and serialize the result; the last workgroup is the
-// placer (the grid must be resident: every spin waits on a wave that is running).
-// MODE 1: andCardinality only (task_card[t]).
+// MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
 template <int OP, int MODE>
 __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
                                                       const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
-                                                      const uint8_t* pb, uint8_t* pstate,
-                                                      uint32_t* __restrict__ task_card) {
-  const PwOut po{pstate};  // a plain pointer argument: inferred global (as a struct member it was not)
+                                                      const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card) {
   __shared__ __align__(16) uint32_t lds_all[kWaves][kWaveLds];
   const uint32_t nt = uni(*n_tasks);
-  if (MODE == 0 && blockIdx.x >= gridDim.x - kPlacers) {
-    pw_placer(nt, po, &lds_all[0][0], blockIdx.x - (gridDim.x - kPlacers));
-    return;
-  }
   const int w = threadIdx.x >> 6;
   uint32_t* lds = lds_all[w];
-  const uint32_t stride = (MODE == 0 ? gridDim.x - kPlacers : gridDim.x) * kWaves;
+  const uint32_t stride = gridDim.x * kWaves;
   const uint32_t t0 = uni(blockIdx.x * kWaves + w);
   if (t0 >= nt) return;
   uint32_t t = t0;
-  uint32_t tc = t0;  // MODE 0: the first own task whose result is not yet in its place
   PTask cur = load_task(tasks, t);
 #if RBG_STAMPS
   StampAcc sacc = {};
@@ -997,11 +530,10 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
     const uint64_t t_in = __builtin_amdgcn_s_memtime();
     sacc.v[10] += 1;
 #endif
-    any_task<OP, MODE>(t, cur, pa, pb, po, task_card, lds SACC_ARG);
+    any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
 #if RBG_STAMPS
     sacc.v[11] += __builtin_amdgcn_s_memtime() - t_in;
 #endif
-    if (MODE == 0) tc = emit_ready(tc, min(tn, nt), stride, po);
     if (tn >= nt) break;
     t = tn;
     cur = nxt;
@@ -1029,11 +561,9 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 
 template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                      const uint8_t* pb, PwOut po, uint32_t* task_card) {
-  const int res = resident_grid((const void*)&k_pair_wave<OP, MODE>);
-  // MODE 0: the compute workgroups plus the placers, all resident
-  const int g = MODE == 0 ? std::max(1, std::min(grid, res - kPlacers)) + kPlacers : std::max(1, std::min(grid, res));
-  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, po.state, task_card);
+                      const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
+  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE>)));
+  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card);
 }
 
 #if RBG_STAMPS
@@ -1059,24 +589,19 @@ void debug_stamps(uint64_t* out20, bool) {
 }
 #endif
 
-void launch_pairwise_emit(hipStream_t s, const uint32_t* nt, PwOut po) {
-  hipLaunchKernelGGL(k_pair_emit, dim3(std::max(1, resident_grid((const void*)&k_pair_emit))), dim3(256), 0, s, nt,
-                     po.state);
-}
-
-void launch_plan_pairwise(hipStream_t s, int op, const uint32_t* koa, const CDesc* da, const uint8_t* pa,
-                          const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_epoch, uint32_t epoch,
-                          PTask* tasks, uint32_t* n_tasks, uint64_t* zlb, uint64_t* ztile, uint32_t* err,
-                          uint8_t* state, PwTail tail) {
-  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, koa, da, pa, kob, db, pb, wg_epoch, epoch, tasks,
-                     n_tasks, zlb, ztile, err, state, tail);
+void launch_plan_pairwise(hipStream_t s, int op, int key_lo, int key_hi, const uint32_t* koa, const CDesc* da,
+                          const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb,
+                          uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, uint64_t* zlb,
+                          uint64_t* ztile, uint32_t* err) {
+  hipLaunchKernelGGL(k_plan_pairwise, dim3(256), dim3(256), 0, s, op, key_lo, key_hi, koa, da, pa, kob, db, pb, wg_epoch,
+                     epoch, tasks, n_tasks, zlb, ztile, err);
 }
 
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                     const uint8_t* pb, PwOut po, uint32_t* task_card) {
+                     const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
 #define RBG_LPW(O)                                                           \
-  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, po, task_card); \
-  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, po, task_card);
+  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card); \
+  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card);
   switch (op) {
     case OP_AND: RBG_LPW(OP_AND) break;
     case OP_OR: RBG_LPW(OP_OR) break;

@@ -836,6 +836,142 @@ __device__ __forceinline__ uint64_t lb_pack(uint64_t st, uint64_t run, uint64_t 
 }
 
 
+// n bytes from src to dst (even addresses, n even), one wave.  The destination body is
+// written as aligned 16 B vectors; each is the 16 bytes at `shift` (the source's offset
+// from 16 B alignment at that point) inside two consecutive aligned source vectors: lane l
+// loads aligned source vector i, takes vector i + 1 from lane l + 1 (a DPP lane shift;
+// lane 63 from the next group's lane 0) and funnel-shifts the pair (alignbyte).  So every
+// load and store is a coalesced 16 B access, 8 per lane in flight.  The unaligned head and
+// tail go as u16.  Reads up to 16 bytes past the end of src (slots and payload arenas carry
+// slack).  The pointers come from memory (records, the state header), so they are generic
+// to the compiler: the accesses go through global-address-space types (flat instructions
+// would also count against lgkmcnt).
+typedef __attribute__((address_space(1))) uint16_t g_u16;
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+__device__ __forceinline__ u32x4 next_lane_vec(u32x4 v) {
+  u32x4 r;
+  r.x = from_next_lane(v.x);
+  r.y = from_next_lane(v.y);
+  r.z = from_next_lane(v.z);
+  r.w = from_next_lane(v.w);
+  return r;
+}
+__device__ __forceinline__ u32x4 lane0_vec(u32x4 v) {
+  u32x4 r;
+  r.x = lane0u(v.x);
+  r.y = lane0u(v.y);
+  r.z = lane0u(v.z);
+  r.w = lane0u(v.w);
+  return r;
+}
+// the 16 bytes at byte offset 4q + r (q wave-uniform, r in {0, 2}) of the 32-byte pair (a, b)
+__device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t q, uint32_t r) {
+  u32x4 o;
+  if (q == 0) {
+    o.x = __builtin_amdgcn_alignbyte(a.y, a.x, r);
+    o.y = __builtin_amdgcn_alignbyte(a.z, a.y, r);
+    o.z = __builtin_amdgcn_alignbyte(a.w, a.z, r);
+    o.w = __builtin_amdgcn_alignbyte(b.x, a.w, r);
+  } else if (q == 1) {
+    o.x = __builtin_amdgcn_alignbyte(a.z, a.y, r);
+    o.y = __builtin_amdgcn_alignbyte(a.w, a.z, r);
+    o.z = __builtin_amdgcn_alignbyte(b.x, a.w, r);
+    o.w = __builtin_amdgcn_alignbyte(b.y, b.x, r);
+  } else if (q == 2) {
+    o.x = __builtin_amdgcn_alignbyte(a.w, a.z, r);
+    o.y = __builtin_amdgcn_alignbyte(b.x, a.w, r);
+    o.z = __builtin_amdgcn_alignbyte(b.y, b.x, r);
+    o.w = __builtin_amdgcn_alignbyte(b.z, b.y, r);
+  } else {
+    o.x = __builtin_amdgcn_alignbyte(b.x, a.w, r);
+    o.y = __builtin_amdgcn_alignbyte(b.y, b.x, r);
+    o.z = __builtin_amdgcn_alignbyte(b.z, b.y, r);
+    o.w = __builtin_amdgcn_alignbyte(b.w, b.z, r);
+  }
+  return o;
+}
+
+struct CopyJob {
+  const g_u16* s16;
+  g_u16* d16;
+  const g_u32x4* sv;  // aligned source vectors
+  g_u32x4* dv;        // aligned destination body
+  uint32_t n, head, nvec, shift;
+};
+// the unaligned head (u16 by the first lanes) and the body's geometry
+__device__ __forceinline__ CopyJob copy_begin(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  const int l = lane_id();
+  CopyJob j;
+  const uintptr_t d = reinterpret_cast<uintptr_t>(dst);
+  j.head = (uint32_t)((16 - (d & 15)) & 15);
+  if (j.head > n) j.head = n;
+  j.n = n;
+  j.s16 = (const g_u16*)src;
+  j.d16 = (g_u16*)dst;
+  if (l < (int)(j.head >> 1)) j.d16[l] = j.s16[l];
+  const uintptr_t s = reinterpret_cast<uintptr_t>(src + j.head);
+  j.shift = (uint32_t)(s & 15);  // even
+  j.sv = (const g_u32x4*)(s - j.shift);
+  j.dv = (g_u32x4*)(dst + j.head);
+  j.nvec = (n - j.head) >> 4;
+  return j;
+}
+// pass i0 (512 body vectors): every source vector the pass needs, requested at once (one
+// past the body too: the partner of the last one; lane 63 of the last group also needs
+// aligned vector i0 + 512 -- the one past the body when this is the last pass: it still
+// holds tail bytes or slack)
+__device__ __forceinline__ void copy_load(const CopyJob& j, uint32_t i0, u32x4 a[8], u32x4& last) {
+  const int l = lane_id();
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t i = i0 + 64 * k + l;
+    if (i <= j.nvec && (j.shift != 0 || i < j.nvec)) a[k] = j.sv[i];
+    else a[k] = u32x4{0, 0, 0, 0};
+  }
+  last = u32x4{0, 0, 0, 0};
+  if (j.shift != 0 && l == 63 && i0 + 511 < j.nvec) last = j.sv[i0 + 512];
+}
+__device__ __forceinline__ void copy_store(const CopyJob& j, uint32_t i0, const u32x4 a[8], const u32x4& last) {
+  const int l = lane_id();
+  if (j.shift == 0) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint32_t i = i0 + 64 * k + l;
+      if (i < j.nvec) j.dv[i] = a[k];
+    }
+    return;
+  }
+  const uint32_t q = j.shift >> 2, r = j.shift & 3;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint32_t i = i0 + 64 * k + l;
+    u32x4 b = next_lane_vec(a[k]);
+    if (k < 7) {
+      const u32x4 nx = lane0_vec(a[k < 7 ? k + 1 : 7]);
+      if (l == 63) b = nx;
+    } else if (l == 63) {
+      b = last;
+    }
+    const u32x4 o = funnel16(a[k], b, q, r);
+    if (i < j.nvec) j.dv[i] = o;
+  }
+}
+__device__ __forceinline__ void copy_tail(const CopyJob& j) {
+  const uint32_t done = j.head + (j.nvec << 4);
+  for (uint32_t i = (done >> 1) + lane_id(); i < (j.n >> 1); i += 64) j.d16[i] = j.s16[i];
+}
+__device__ __forceinline__ void w_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  const CopyJob j = copy_begin(dst, src, n);
+  for (uint32_t i0 = 0; i0 < j.nvec; i0 += 512) {
+    u32x4 a[8], last;
+    copy_load(j, i0, a, last);
+    copy_store(j, i0, a, last);
+  }
+  copy_tail(j);
+}
 // ---------------------------------------------------------------------------
 // workgroup-per-task result records (wide / BSI kernels)
 // ---------------------------------------------------------------------------

@@ -94,8 +94,13 @@ class Engine:
         return [RoaringBitmap(take(outs[k])) for k in range(count)]
 
     # ---- ops (asynchronous) -------------------------------------------------------
-    def pairwise(self, op, a, b, ia=0, ib=0):
-        check(lib().rbg_ctx_pairwise(self._ctx, _lib.OP[op], int(a), int(ia), int(b), int(ib)))
+    def pairwise(self, op, a, b, ia=0, ib=0, key_lo=0, key_hi=65536):
+        """A pairwise op; key_lo / key_hi restrict it to one key-range shard (shard.py assembles shards)."""
+        if key_lo == 0 and key_hi == 65536:
+            check(lib().rbg_ctx_pairwise(self._ctx, _lib.OP[op], int(a), int(ia), int(b), int(ib)))
+        else:
+            check(lib().rbg_ctx_pairwise_range(self._ctx, _lib.OP[op], int(a), int(ia), int(b), int(ib), int(key_lo),
+                                               int(key_hi)))
 
     def and_cardinality(self, a, b, ia=0, ib=0):
         check(lib().rbg_ctx_pairwise_card(self._ctx, 0, int(a), int(ia), int(b), int(ib)))

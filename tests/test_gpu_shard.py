@@ -60,6 +60,25 @@ def test_engine_key_shards(gpu, world):
     assert shard.concat_serialized(parts) == O.wide("and", small, list(range(len(small))))
 
 
+@pytest.mark.parametrize("world", [2, 5])
+def test_pairwise_key_shards(gpu, world):
+    """rbg_ctx_pairwise_range: each rank's key slice of a pairwise op (RB/RoaringBitmap.java:382-399
+    on that slice), concatenated, equals the oracle's whole result -- run containers on both sides."""
+    rng = np.random.default_rng(900 + world)
+    keys = np.sort(rng.choice(4096, size=60, replace=False))
+    a = _gen.bitmap(rng, keys, p_present=0.9)
+    b = _gen.bitmap(rng, keys, p_present=0.9)
+    e = _engine()
+    ba, bb = e.load([a]), e.load([b])
+    ranges = shard.key_ranges(_key_bytes([a, b]), world)
+    for op in ["and", "or", "xor", "andnot"]:
+        parts = []
+        for lo, hi in ranges:
+            e.pairwise(op, ba, bb, key_lo=lo, key_hi=hi)
+            parts.append(e.fetch().serialize())
+        assert shard.concat_serialized(parts) == O.pairwise(op, a, b), op
+
+
 @pytest.mark.parametrize("kind", [1, 2])
 def test_c3_synthetic_matches_oracle(gpu, kind):
     """C3 batches generated on the device: wide or/and/xor == oracle over the fetched bitmaps."""

@@ -71,6 +71,53 @@ def test_two_rank_engine_assembly(gpu, kind, op):
     assert res == ref
 
 
+def _pair_worker(rank, world, port, outdir, op):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from roaringbitmap_amd import Engine, shard
+        e = Engine(0)
+        # a mixed pair over ~200 keys with run containers on both sides (RB/RoaringBitmap.java:382-399)
+        rng = np.random.default_rng(11)
+        import roaringbitmap_amd as rb
+        va = np.concatenate([rng.integers(0, 200 << 16, 300000), np.arange(5 << 16, 9 << 16)])
+        vb = np.concatenate([rng.integers(0, 200 << 16, 300000), np.arange(7 << 16, (7 << 16) + 40000)])
+        xa = rb.RoaringBitmap.from_values(va, run_optimize=True).serialize()
+        xb = rb.RoaringBitmap.from_values(vb, run_optimize=True).serialize()
+        a, b = e.load([xa]), e.load([xb])
+        lo, hi = [(0, 77), (77, 65536)][rank]
+        e.pairwise(op, a, b, key_lo=lo, key_hi=hi)
+        rs = e.result_stats()
+        lay = shard.exchange_layout(rs["containers"], rs["payload_bytes"], rs["has_run"], device="cpu")
+        out = shard.assemble(shard.engine_fill(e), lay, rank, fill_device=torch.device("cuda", 0),
+                             comm_device="cpu", sync=e.sync)
+        if rank == 0:
+            e.pairwise(op, a, b)
+            ref = e.fetch().serialize()
+            with open(os.path.join(outdir, "res.bin"), "wb") as f:
+                f.write(bytes(out.numpy().tobytes()))
+            with open(os.path.join(outdir, "ref.bin"), "wb") as f:
+                f.write(ref)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("op", ["and", "or", "xor", "andnot"])
+def test_two_rank_pairwise_assembly(gpu, op):
+    """A pairwise op split into two key ranges over two processes, assembled on rank 0, equals
+    the unsharded result byte for byte."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_pair_worker, args=(2, _free_port(), d, op), nprocs=2, join=True)
+        res = open(os.path.join(d, "res.bin"), "rb").read()
+        ref = open(os.path.join(d, "ref.bin"), "rb").read()
+    assert res == ref
+
+
 def _bench(gpus):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo", "--steps", "2",
            "--warmup", "1", "--c3-n", "64", "--c4-pairs", "2000", "--c5-rows", "2000000", "--no-cpu-baseline"]
@@ -82,6 +129,8 @@ def _bench(gpus):
 def test_bench_two_ranks_rehearsal(gpu):
     one, two = _bench(1), _bench(2)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
+    # the key-sharded C2 AND assembles the same bytes as the one-GPU headline (same pair)
+    assert two["extra"]["c2_and_key_sharded"]["result_sha16"] == one["extra"]["result"]["sha16"]
     for w in ("c3_uniform_or", "c3_clustered_or", "c3_uniform_and"):
         assert two["extra"][w]["result_serialized_bytes"] == one["extra"][w]["result_serialized_bytes"], w
         assert two["extra"][w]["output_bytes"] == one["extra"][w]["output_bytes"], w
