@@ -716,46 +716,50 @@ static int horizontal_order(Ctx* c, Batch* B) {
 }
 
 // FastAggregation.priorityqueue_or / priorityqueue_xor (RB/FastAggregation.java:677-812).
-// The reference keeps a java.util.PriorityQueue of bitmap indices ordered by
-// (int)(sizes[a] - sizes[b]) over getLongSizeInBytes; the queue is replayed here with
-// the heap's own tie order, and every step is one device pass over the union keys
-// (pq.hip, launch_pq_step) whose result size is read back to order the queue.
+// The reference keeps a java.util.PriorityQueue of bitmaps ordered by
+// (int)(sizes[a] - sizes[b]) over getLongSizeInBytes.  The host adds the inputs and plans
+// the first step; the queue then runs on the device (pq.hip): N - 1 step launches, each
+// planning the next, with no host read-back in between.
 namespace {
-template <class Cmp>
-struct IntHeap {  // java.util.PriorityQueue with a comparator (OpenJDK siftUp / siftDown)
-  std::vector<int> q;
-  Cmp cmp;
-  explicit IntHeap(Cmp c) : cmp(c) {}
-  void add(int x) {
-    size_t k = q.size();
-    q.push_back(x);
+// host side of the queue for the first step (same operations as pq.hip's PQWave)
+struct PQHost {
+  std::vector<PQEnt>& heap;
+  std::vector<int32_t>& nodes;
+  std::vector<uint8_t>& tmp;
+  std::vector<int32_t>& slots;
+  void add(PQStep& c, PQEnt x) {  // OpenJDK PriorityQueue.siftUp
+    int k = c.heap_n++;
     while (k > 0) {
-      const size_t p = (k - 1) >> 1;
-      if (cmp(x, q[p]) >= 0) break;
-      q[k] = q[p];
+      const int p = (k - 1) >> 1;
+      if (pq_cmp(x.size, heap[p].size) >= 0) break;
+      heap[k] = heap[p];
       k = p;
     }
-    q[k] = x;
+    heap[k] = x;
   }
-  int poll() {
-    const int r = q[0];
-    const int x = q.back();
-    q.pop_back();
-    const size_t n = q.size();
-    if (n) {
-      size_t k = 0;
-      const size_t half = n >> 1;
-      while (k < half) {
-        size_t ch = 2 * k + 1;
-        if (ch + 1 < n && cmp(q[ch], q[ch + 1]) > 0) ch++;
-        if (cmp(x, q[ch]) <= 0) break;
-        q[k] = q[ch];
-        k = ch;
-      }
-      q[k] = x;
+  PQEnt poll(PQStep& c) {  // PriorityQueue.poll + siftDown
+    const PQEnt r = heap[0];
+    const int n = --c.heap_n;
+    if (n == 0) return r;
+    const PQEnt x = heap[n];
+    int k = 0;
+    const int half = n >> 1;
+    while (k < half) {
+      int ch = 2 * k + 1;
+      if (ch + 1 < n && pq_cmp(heap[ch].size, heap[ch + 1].size) > 0) ch++;
+      if (pq_cmp(x.size, heap[ch].size) <= 0) break;
+      heap[k] = heap[ch];
+      k = ch;
     }
+    heap[k] = x;
     return r;
   }
+  int32_t node(int i) { return nodes[i]; }
+  void set_node(int i, int32_t v) { nodes[i] = v; }
+  bool istmp(int i) { return tmp[i] != 0; }
+  void set_istmp(int i) { tmp[i] = 1; }
+  int slot_pop(PQStep& c) { return slots[--c.slot_top]; }
+  void slot_push(PQStep& c, int s) { slots[c.slot_top++] = s; }
 };
 }  // namespace
 
@@ -777,112 +781,100 @@ static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) 
   launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
                  c->ntasks.as<uint32_t>());
   c->mark(1);
-  if (N) {
-    uint32_t h_nt = 0;
-    HIPCHK(hipMemcpyAsync(&h_nt, c->ntasks.p, 4, hipMemcpyDeviceToHost, s));
-    CHK(c->scalar.ensure(64));
-    std::vector<unsigned long long> leaf(N);
-    DevBuf dsz;
-    CHK(dsz.ensure(8 * N));
-    HIPCHK(hipMemsetAsync(dsz.p, 0, 8 * N, s));
-    launch_pq_leaf_sizes(s, B->desc.as<CDesc>(), B->bm.as<uint32_t>(), B->payload.as<uint8_t>(), B->n_ctr,
-                         dsz.as<unsigned long long>());
-    HIPCHK(hipMemcpyAsync(leaf.data(), dsz.p, 8 * N, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    const PQArgs pa{B->desc.as<CDesc>(), B->bm.as<uint32_t>(), B->payload.as<uint8_t>()};
-    const int grid = grid_for(h_nt, 65536);
-    // temps: one state (16 B) + one 8 KiB set per union key; freed slots are reused
-    const size_t st_bytes = ((size_t)16 * h_nt + 255) & ~(size_t)255;
-    std::vector<std::unique_ptr<DevBuf>> pool;
-    std::vector<int> free_slots;
-    auto alloc = [&](PQRef* out) -> int {
-      int k;
-      if (!free_slots.empty()) {
-        k = free_slots.back();
-        free_slots.pop_back();
-      } else {
-        pool.emplace_back(new DevBuf());
-        k = (int)pool.size() - 1;
-        CHK(pool[k]->ensure(st_bytes + (size_t)8192 * h_nt));
-      }
-      uint8_t* p = pool[k]->as<uint8_t>();
-      *out = PQRef{-1 - k, reinterpret_cast<PQState*>(p), reinterpret_cast<uint64_t*>(p + st_bytes)};
-      return RBG_OK;
-    };
-    auto release = [&](const PQRef& r) {
-      if (r.leaf < 0) free_slots.push_back(-1 - r.leaf);
-    };
-    auto as_arg = [](PQRef r) {
-      if (r.leaf < 0) r.leaf = -1;
-      return r;
-    };
-    unsigned long long h_size = 0;
-    auto step = [&](int pop, const PQRef& a, const PQRef& b, const PQRef& o, int64_t* size) -> int {
-      HIPCHK(hipMemsetAsync(c->scalar.p, 0, 8, s));
-      launch_pq_step(s, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), pa, pop, as_arg(a), as_arg(b), as_arg(o),
-                     c->scalar.as<unsigned long long>());
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipMemcpyAsync(&h_size, c->scalar.p, 8, hipMemcpyDeviceToHost, s));
-      HIPCHK(hipStreamSynchronize(s));
-      *size = 8 + (int64_t)h_size;
-      return RBG_OK;
-    };
-    std::vector<int64_t> sizes(N);
-    std::vector<PQRef> node(N);
-    for (size_t k = 0; k < N; k++) {
-      sizes[k] = 8 + (int64_t)leaf[k];
-      node[k] = PQRef{(int32_t)k, nullptr, nullptr};
-    }
-    auto cmp = [&](int a, int b) { return (int)(int32_t)(uint32_t)(uint64_t)(sizes[a] - sizes[b]); };
-    IntHeap<decltype(cmp)> pq(cmp);
-    for (size_t k = 0; k < N; k++) pq.add((int)k);
-    if (op == RBG_WIDE_PQ_OR) {  // :758-781
-      std::vector<char> istmp(N, 0);
-      while (pq.q.size() > 1) {
-        const int x1 = pq.poll(), x2 = pq.poll();
-        if (istmp[x2] && istmp[x1]) {  // lazyorfromlazyinputs(buffer[x1], buffer[x2])
-          CHK(step(PQ_LFL, node[x1], node[x2], node[x1], &sizes[x1]));
-          release(node[x2]);
-          pq.add(x1);
-        } else if (istmp[x2]) {  // buffer[x2].lazyor(buffer[x1])
-          CHK(step(PQ_LIOR, node[x2], node[x1], node[x2], &sizes[x2]));
-          pq.add(x2);
-        } else if (istmp[x1]) {  // buffer[x1].lazyor(buffer[x2])
-          CHK(step(PQ_LIOR, node[x1], node[x2], node[x1], &sizes[x1]));
-          pq.add(x1);
-        } else {  // RoaringBitmap.lazyor(buffer[x1], buffer[x2])
-          PQRef t;
-          CHK(alloc(&t));
-          CHK(step(PQ_LOR, node[x1], node[x2], t, &sizes[x1]));
-          node[x1] = t;
-          istmp[x1] = 1;
-          pq.add(x1);
-        }
-      }
-    } else {  // :799-811: pq.add(RoaringBitmap.xor(x1, x2))
-      while (pq.q.size() > 1) {
-        const int x1 = pq.poll(), x2 = pq.poll();
-        PQRef t;
-        CHK(alloc(&t));
-        int64_t sz;
-        CHK(step(PQ_XOR, node[x1], node[x2], t, &sz));
-        release(node[x1]);
-        release(node[x2]);
-        node.push_back(t);
-        sizes.push_back(sz);
-        pq.add((int)node.size() - 1);
-      }
-    }
-    const PQRef root = node[pq.poll()];
+  if (!N) {
     c->mark(2);
-    launch_pq_final(s, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), pa, op == RBG_WIDE_PQ_OR ? 1 : 0,
-                    as_arg(root), oc);
+    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
+    c->last = 1;
+    c->mark(3);
     HIPCHK(hipGetLastError());
-    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
-    HIPCHK(hipStreamSynchronize(s));  // the temps are freed on return
-  } else {
-    c->mark(2);
-    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
+    return RBG_OK;
+  }
+  uint32_t h_nt = 0;
+  HIPCHK(hipMemcpyAsync(&h_nt, c->ntasks.p, 4, hipMemcpyDeviceToHost, s));
+  std::vector<unsigned long long> leaf(N);
+  DevBuf dsz;
+  CHK(dsz.ensure(8 * N));
+  HIPCHK(hipMemsetAsync(dsz.p, 0, 8 * N, s));
+  launch_pq_leaf_sizes(s, B->desc.as<CDesc>(), B->bm.as<uint32_t>(), B->payload.as<uint8_t>(), B->n_ctr,
+                       dsz.as<unsigned long long>());
+  HIPCHK(hipMemcpyAsync(leaf.data(), dsz.p, 8 * N, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+
+  // Temps: at most N/2 + 1 are live at once (every priorityqueue_or temp starts from two
+  // inputs; a priorityqueue_xor step allocates one while its operands are still queued).
+  // Each has one 16 B state per union key; containers that are not input clones live in
+  // 8 KiB arena blocks owned by exactly one temp key, and live temps cover disjoint
+  // inputs, so 2 x the batch's containers bounds the blocks in use (one step's fresh
+  // blocks come off the stack before its freed ones go back).
+  const size_t n_slots = N / 2 + 2;
+  const size_t stride = std::max<uint32_t>(h_nt, 1);
+  const size_t st_bytes = n_slots * stride * sizeof(PQState);
+  size_t n_blk = 2 * B->n_ctr + 64;
+  size_t free_b = 0, total_b = 0;
+  HIPCHK(hipMemGetInfo(&free_b, &total_b));
+  const size_t budget = free_b / 10 * 9;
+  if (st_bytes > budget / 2) {
+    set_err("priorityqueue: " + std::to_string(n_slots) + " temps x " + std::to_string(stride) +
+            " union keys need " + std::to_string(st_bytes >> 20) + " MiB of temp state (more than half the free "
+            "device memory); use FastAggregation.or / xor");
+    return RBG_ERR_OUT_OF_MEMORY;
+  }
+  n_blk = std::max<size_t>(1, std::min(n_blk, (budget - st_bytes) / 8192));
+  // host: add every input, plan the first step
+  std::vector<PQEnt> heap(N);
+  std::vector<int32_t> nodes(2 * N);
+  std::vector<uint8_t> tmp(2 * N, 0);
+  std::vector<int32_t> slots(n_slots);
+  for (size_t k = 0; k < N; k++) nodes[k] = (int32_t)k;
+  for (size_t k = 0; k < n_slots; k++) slots[k] = (int32_t)(n_slots - 1 - k);
+  PQCtl ctl{};
+  ctl.step.or_mode = op == RBG_WIDE_PQ_OR;
+  ctl.step.n_nodes = (int32_t)N;
+  ctl.step.slot_top = (int32_t)n_slots;
+  ctl.step.rel1 = ctl.step.rel2 = -1;
+  ctl.free_top = (int32_t)n_blk;
+  PQHost hm{heap, nodes, tmp, slots};
+  for (size_t k = 0; k < N; k++) hm.add(ctl.step, PQEnt{8 + (int64_t)leaf[k], (int32_t)k, 0});
+  pq_plan(hm, ctl.step);
+  std::vector<int32_t> stack(n_blk);
+  for (size_t k = 0; k < n_blk; k++) stack[k] = (int32_t)k;
+  // device copies
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t o_heap = al(sizeof(PQCtl)), o_node = o_heap + al(16 * N), o_tmp = o_node + al(8 * N),
+               o_slots = o_tmp + al(2 * N), o_stack = o_slots + al(4 * n_slots), o_freed = o_stack + al(4 * n_blk),
+               o_end = o_freed + al(8 * stride);
+  DevBuf meta, states, arena;
+  CHK(meta.ensure(o_end));
+  CHK(states.ensure(st_bytes));
+  CHK(arena.ensure(n_blk * 8192));
+  uint8_t* mb = meta.as<uint8_t>();
+  HIPCHK(hipMemcpyAsync(mb, &ctl, sizeof(ctl), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(mb + o_heap, heap.data(), 16 * N, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(mb + o_node, nodes.data(), 8 * N, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(mb + o_tmp, tmp.data(), 2 * N, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(mb + o_slots, slots.data(), 4 * n_slots, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(mb + o_stack, stack.data(), 4 * n_blk, hipMemcpyHostToDevice, s));
+  const PQDev D{reinterpret_cast<PQCtl*>(mb), reinterpret_cast<PQEnt*>(mb + o_heap),
+                reinterpret_cast<int32_t*>(mb + o_node), mb + o_tmp, reinterpret_cast<int32_t*>(mb + o_slots),
+                states.as<PQState>(), stride, arena.as<uint64_t>(), reinterpret_cast<int32_t*>(mb + o_stack),
+                reinterpret_cast<int32_t*>(mb + o_freed)};
+  const PQArgs pa{B->desc.as<CDesc>(), B->bm.as<uint32_t>(), B->payload.as<uint8_t>()};
+  const int grid = grid_for(h_nt, 65536);
+  for (size_t k = 0; k + 1 < N; k++) {
+    launch_pq_step(s, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), pa, D);
+    if ((k & 1023) == 1023) HIPCHK(hipGetLastError());
+  }
+  c->mark(2);
+  launch_pq_final(s, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), pa, op == RBG_WIDE_PQ_OR ? 1 : 0, D, oc);
+  HIPCHK(hipGetLastError());
+  launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
+  PQCtl done{};
+  HIPCHK(hipMemcpyAsync(&done, mb, sizeof(done), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));  // the temps are freed on return
+  if (done.err || !done.step.final_step) {
+    set_err(done.err ? "priorityqueue: the temp block arena (" + std::to_string(n_blk) + " x 8 KiB) ran out"
+                     : std::string("priorityqueue: the device queue did not finish"));
+    return done.err ? RBG_ERR_OUT_OF_MEMORY : RBG_ERR_DEVICE;
   }
   c->last = 1;
   c->mark(3);

@@ -38,8 +38,10 @@ struct WideArgs {
   uint32_t chain;         // chain modes: kChain* flags
 };
 
-// priority-queue aggregations (pq.hip): one step of the queue combines two nodes
-// (an input bitmap of the batch, or an intermediate temp) over every union key.
+// priority-queue aggregations (pq.hip): the size-ordered queue runs on the device.  Each
+// step launch combines two nodes (an input bitmap of the batch, or an intermediate temp)
+// over every union key; the launch's last workgroup folds the result size into the
+// queue and writes the next step, so the host only enqueues N - 1 launches.
 //   PQ_XOR  RoaringBitmap.xor(x1, x2)                 (priorityqueue_xor)
 //   PQ_LOR  RoaringBitmap.lazyor(x1, x2), static      (priorityqueue_or, two inputs)
 //   PQ_LIOR x1.lazyor(x2), in place on the temp x1    (one temp)
@@ -52,28 +54,121 @@ struct __align__(16) PQState {  // per key of a temp
   uint16_t nruns;
   uint8_t kind;     // PQKind
   uint8_t present;  // the temp holds this key
-  int32_t src;      // >= 0: an unchanged clone of this input container (desc index); else `set`
-  uint32_t pad;
+  int32_t src;      // >= 0: an unchanged clone of this input container (desc index)
+  int32_t blk;      // else: the 8 KiB block of the set arena holding the container
 };
-struct PQRef {
-  int32_t leaf;    // >= 0: input bitmap `leaf` of the batch; -1: a temp
-  PQState* st;     // temp: one state per task
-  uint64_t* set;   // temp: one 8 KiB bitmap (1024 words) per task
+// A queue entry: the node's getLongSizeInBytes is fixed while it is queued.
+struct PQEnt {
+  int64_t size;
+  int32_t node;
+  int32_t pad;
+};
+// The step the next launch runs, and the queue's scalar state.  Node references:
+// >= 0 input bitmap of the batch, < 0 temp slot -1 - ref.
+struct PQStep {
+  int32_t op, final_step, a, b, o;
+  int32_t target;      // node index whose size the step's result gives
+  int32_t rel1, rel2;  // temp slots freed after the step (-1: none)
+  int32_t heap_n, n_nodes, slot_top, or_mode;
+};
+struct PQCtl {
+  PQStep step;
+  int32_t free_top;  // block stack top (pops during a step)
+  uint32_t freed_n;  // blocks freed by the running step (pushed by its last workgroup)
+  uint32_t done;     // workgroups finished in the running step
+  uint32_t err;      // the block arena ran out
+  unsigned long long size;
+};
+struct PQDev {
+  PQCtl* ctl;
+  PQEnt* heap;        // java.util.PriorityQueue array order
+  int32_t* node;      // node index -> reference
+  uint8_t* istmp;     // priorityqueue_or: node holds a temp
+  int32_t* slots;     // free temp slots (stack)
+  PQState* states;    // temp slot s: states[s * stride + task]
+  uint64_t stride;
+  uint64_t* arena;    // 8 KiB blocks (1024 words)
+  int32_t* blk_stack; // free blocks
+  int32_t* freed;     // blocks freed by the running step
 };
 struct PQArgs {
   const CDesc* desc;
   const uint32_t* bm;
   const uint8_t* payload;
 };
+
+// The queue (RB/FastAggregation.java:758-781 / :799-811) after the host has added every
+// input: pq_finish folds a step's result size in, pq_plan polls the next pair.  M gives
+// the heap operations and node table: sequential on the host (the first step), a wave of
+// the scheduling workgroup on the device.
+template <class M>
+__host__ __device__ inline void pq_finish(M& m, PQStep& c, int64_t size) {
+  m.add(c, PQEnt{size, c.target, 0});
+  if (c.rel1 >= 0) m.slot_push(c, c.rel1);
+  if (c.rel2 >= 0) m.slot_push(c, c.rel2);
+}
+template <class M>
+__host__ __device__ inline void pq_plan(M& m, PQStep& c) {
+  if (c.heap_n <= 1) {
+    c.final_step = 1;
+    c.a = c.heap_n ? m.node(m.poll(c).node) : 0;
+    return;
+  }
+  const int x1 = m.poll(c).node;
+  const int x2 = m.poll(c).node;
+  c.rel1 = c.rel2 = -1;
+  if (c.or_mode) {
+    const bool t1 = m.istmp(x1), t2 = m.istmp(x2);
+    if (t1 && t2) {  // lazyorfromlazyinputs(buffer[x1], buffer[x2]) into x1's temp
+      c.op = PQ_LFL;
+      c.a = m.node(x1);
+      c.b = m.node(x2);
+      c.o = c.a;
+      c.target = x1;
+      c.rel1 = -1 - c.b;
+    } else if (t2) {  // buffer[x2].lazyor(buffer[x1])
+      c.op = PQ_LIOR;
+      c.a = m.node(x2);
+      c.b = m.node(x1);
+      c.o = c.a;
+      c.target = x2;
+    } else if (t1) {  // buffer[x1].lazyor(buffer[x2])
+      c.op = PQ_LIOR;
+      c.a = m.node(x1);
+      c.b = m.node(x2);
+      c.o = c.a;
+      c.target = x1;
+    } else {  // RoaringBitmap.lazyor(buffer[x1], buffer[x2]) into a new temp
+      c.op = PQ_LOR;
+      c.a = m.node(x1);
+      c.b = m.node(x2);
+      c.o = -1 - m.slot_pop(c);
+      m.set_node(x1, c.o);
+      m.set_istmp(x1);
+      c.target = x1;
+    }
+  } else {  // pq.add(RoaringBitmap.xor(x1, x2))
+    c.op = PQ_XOR;
+    c.a = m.node(x1);
+    c.b = m.node(x2);
+    c.o = -1 - m.slot_pop(c);
+    c.target = c.n_nodes++;
+    m.set_node(c.target, c.o);
+    if (c.a < 0) c.rel1 = -1 - c.a;
+    if (c.b < 0) c.rel2 = -1 - c.b;
+  }
+}
+// java.util.PriorityQueue's comparator over getLongSizeInBytes: (int)(sizes[a] - sizes[b])
+__host__ __device__ inline int pq_cmp(int64_t a, int64_t b) { return (int)(int32_t)(uint32_t)(uint64_t)(a - b); }
+
 // sizes[bm] += 2 + getSizeInBytes over the batch's containers (sizes zeroed by the caller)
 void launch_pq_leaf_sizes(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
                           unsigned long long* sizes);
-// out = op(a, b); *size += 2 + getSizeInBytes of each of out's containers
-void launch_pq_step(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, PQArgs args, int op, PQRef a,
-                    PQRef b, PQRef out, unsigned long long* size);
+// one step of the queue (the step record in D.ctl), then the next step's plan
+void launch_pq_step(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, PQArgs args, PQDev D);
 // the root node as the op's result records (repair: priorityqueue_or's repairAfterLazy)
 void launch_pq_final(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, PQArgs args, int repair,
-                     PQRef root, OutCtx oc);
+                     PQDev D, OutCtx oc);
 
 // bit-sliced index (bsi.hip); ops in the order of BitmapSliceIndex.Operation
 // (bsi/src/main/java/org/roaringbitmap/bsi/BitmapSliceIndex.java:23-38)

@@ -3,15 +3,24 @@
 //
 // The reference pairs whole bitmaps in a java.util.PriorityQueue ordered by
 // getLongSizeInBytes, so every step's operands depend on the sizes of earlier
-// intermediate results over all keys.  The host replays the queue (engine.cpp:
-// ctx_pq); each step here is one launch over the union keys of the batch (one
-// workgroup per key) that combines two nodes -- an input bitmap (leaf) or an
-// intermediate (temp) -- with the step's whole-bitmap op, keeps the per-key
-// result in a temp slot and adds its getSizeInBytes to the step's size word.
+// intermediate results over all keys.  The queue lives in device memory: the host
+// adds the inputs and plans the first step (engine.cpp: ctx_pq), then enqueues N - 1
+// launches of k_pq_step.  Each combines the two nodes its step record names -- an input
+// bitmap (leaf) or an intermediate (temp) -- over every union key (one workgroup per
+// key), keeps the per-key result in the output temp and adds its getSizeInBytes to the
+// step's size word; the launch's last workgroup folds that size into the queue and
+// polls the next pair (pq_finish / pq_plan, kernels.hpp) with one wave, reading the
+// heap a six-level subtree per round trip.  No host read-back between steps.
 //
 // Per key a temp holds a PQState (kind, cardinality, run count) and either the
-// index of the input container it is an unchanged clone of, or the container's
-// set as an 8 KiB bitmap.  Kinds follow the reference's lazy algebra
+// index of the input container it is an unchanged clone of, or an 8 KiB block of the
+// set arena holding the container as a bitmap.  Blocks move with the data: a step's
+// result reuses an operand temp's block at that key (every operand temp is consumed by
+// its step -- updated in place or released), a fresh block comes off the free stack only
+// where neither operand has one, and blocks left over go back after the step.  A temp
+// therefore holds blocks only for its own keys, so live blocks stay within the batch's
+// container count (live temps cover disjoint sets of inputs).
+// Kinds follow the reference's lazy algebra
 // (RB/Container.java:717-774 lazyIOR / lazyOR): a lazy bitmap (card -1 in the
 // reference) is kept apart from an exact one, because repairAfterLazy converts
 // only the lazy one (RB/BitmapContainer.java:1205-1215).
@@ -43,45 +52,58 @@ struct PQNode {
   int card;
   int nruns;
   int src;   // >= 0: desc index of the input container this one is a clone of
+  int blk;   // temp: set arena block (-1: none)
 };
 
-// Node of `ref` at task t (segment [s, s + n) of the key-major batch).  A leaf's
-// container is found by a workgroup-wide scan of the segment's input indices
-// (ascending); `found` is one int of LDS.  Contains barriers.
-__device__ __forceinline__ PQNode pq_load(const PQRef& ref, const PQArgs& A, uint32_t t, uint32_t s, uint32_t n,
-                                          int* found) {
-  PQNode x{0, PK_A, 0, 0, -1};
-  if (ref.leaf >= 0) {
-    if (threadIdx.x == 0) *found = -1;
-    lds_barrier();
-    for (uint32_t j = threadIdx.x; j < n; j += NT)
-      if (A.bm[s + j] == (uint32_t)ref.leaf) *found = (int)(s + j);
-    lds_barrier();
-    const int j = *found;
-    lds_barrier();
-    if (j >= 0) {
+__device__ __forceinline__ PQState* pq_states(const PQDev& D, int ref) {
+  return D.states + (uint64_t)(-1 - ref) * D.stride;
+}
+__device__ __forceinline__ uint8_t* pq_block(const PQDev& D, int blk) {
+  return reinterpret_cast<uint8_t*>(D.arena + (uint64_t)blk * 1024);
+}
+
+// Node `ref` at task t (segment [s, s + n) of the key-major batch).  A leaf's container
+// is found by a binary search of the segment's input indices (ascending, uniform loads).
+__device__ __forceinline__ PQNode pq_load(int ref, const PQDev& D, const PQArgs& A, uint32_t t, uint32_t s,
+                                          uint32_t n) {
+  PQNode x{0, PK_A, 0, 0, -1, -1};
+  if (ref >= 0) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (A.bm[s + mid] < (uint32_t)ref) lo = mid + 1;
+      else hi = mid;
+    }
+    if (lo < n && A.bm[s + lo] == (uint32_t)ref) {
+      const uint32_t j = s + lo;
       const CDesc d = A.desc[j];
       x.present = 1;
       x.kind = d.kind;  // DK_A / DK_B (= PK_BE) / DK_R
       x.card = (int)d.card;
       x.nruns = d.kind == DK_R ? *reinterpret_cast<const uint16_t*>(A.payload + d.slot + 2) : 0;
-      x.src = j;
+      x.src = (int)j;
     }
   } else {
-    const PQState st = ref.st[t];
+    const PQState st = pq_states(D, ref)[t];
     x.present = st.present;
     x.kind = st.kind;
     x.card = (int)st.card;
     x.nruns = st.nruns;
     x.src = st.src;
+    x.blk = st.present ? st.blk : -1;
   }
   return x;
 }
 
-__device__ __forceinline__ void pq_materialize(const PQNode& x, const PQRef& ref, const PQArgs& A, uint32_t t,
-                                               uint32_t* lds, int* q, uint64_t r[4]) {
-  if (x.src >= 0) materialize(A.desc[x.src], A.payload, lds, q, r);
-  else load_bitmap_owned(reinterpret_cast<const uint8_t*>(ref.set + (size_t)t * 1024), r);
+__device__ __forceinline__ void pq_materialize(const PQNode& x, const PQDev& D, const PQArgs& A, uint32_t* lds, int* q,
+                                               uint64_t r[4]) {
+  if (x.src >= 0) {
+    materialize(A.desc[x.src], A.payload, lds, q, r);
+  } else if (x.blk >= 0) {
+    load_bitmap_owned(pq_block(D, x.blk), r);
+  } else {  // the arena ran out in an earlier step (reported through ctl->err)
+    r[0] = r[1] = r[2] = r[3] = 0;
+  }
 }
 
 __device__ __forceinline__ int pq_size(int kind, int card, int nruns) {  // getSizeInBytes + the 2 B key
@@ -138,72 +160,259 @@ __device__ __forceinline__ int pq_kind(int op, const PQNode& a, const PQNode& b,
   return eff(*c, *nr);
 }
 
-// One step of the queue over every union key: out = op(a, b).  out may be a's temp
-// slot (the in-place RoaringBitmap.lazyor and lazyorfromlazyinputs).
+// ---- the queue on the device ----------------------------------------------------
+// Loads and stores of the queue go through the vector memory path (atomic loads and
+// stores, relaxed): the scheduling wave rereads entries it has just written.
+template <class T>
+__device__ __forceinline__ T pq_ld(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void pq_st(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int64_t rl64(int64_t v, int lane) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), lane);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// The queue operations run by one whole wave with uniform control flow; lane 0 stores.
+// The heap is java.util.PriorityQueue's array: siftUp / siftDown as OpenJDK, each
+// round trip fetching up to five levels of the path at once.
+struct PQWave {
+  const PQDev& D;
+  int lane;
+  __device__ void st_ent(int k, const PQEnt& e) {
+    if (lane == 0) {
+      pq_st(&D.heap[k].size, e.size);
+      pq_st(&D.heap[k].node, e.node);
+    }
+  }
+  __device__ PQEnt ld_ent(int k) { return PQEnt{pq_ld(&D.heap[k].size), pq_ld(&D.heap[k].node), 0}; }
+  __device__ void add(PQStep& c, PQEnt x) {
+    int k = c.heap_n++;
+    // ancestor L + 1 levels up of position k, one per lane
+    const int up = (k + 1) >> (lane + 1);
+    int64_t asz = 0;
+    int32_t and_ = 0;
+    if (lane < 31 && up >= 1) {
+      asz = pq_ld(&D.heap[up - 1].size);
+      and_ = pq_ld(&D.heap[up - 1].node);
+    }
+    for (int L = 0; k > 0; L++) {
+      const int64_t esz = rl64(asz, L);
+      const int32_t end = __builtin_amdgcn_readlane(and_, L);
+      if (pq_cmp(x.size, esz) >= 0) break;
+      st_ent(k, PQEnt{esz, end, 0});
+      k = (k - 1) >> 1;
+    }
+    st_ent(k, x);
+    __threadfence_block();
+  }
+  __device__ PQEnt poll(PQStep& c) {
+    const PQEnt r = ld_ent(0);
+    const int n = --c.heap_n;
+    if (n == 0) return r;
+    const PQEnt x = ld_ent(n);
+    // lane -> depth d (1..5) below the round trip's root, index j within that depth
+    const int d = 31 - __builtin_clz((unsigned)lane + 2);
+    const int j = lane + 2 - (1 << d);
+    const int half = n >> 1;
+    int k = 0;
+    bool done = k >= half;
+    while (!done) {
+      const int pos = ((k + 1) << d) - 1 + j;
+      int64_t sz = 0;
+      int32_t nd = 0;
+      if (d <= 5 && pos < n) {
+        sz = pq_ld(&D.heap[pos].size);
+        nd = pq_ld(&D.heap[pos].node);
+      }
+      int rel = 0;
+      for (int dd = 0; dd < 5; dd++) {
+        if (k >= half) {
+          done = true;
+          break;
+        }
+        int child = 2 * k + 1;
+        int cl = (2 << dd) - 2 + 2 * rel;
+        int64_t csz = rl64(sz, cl);
+        int32_t cnd = __builtin_amdgcn_readlane(nd, cl);
+        int nrel = 2 * rel;
+        if (child + 1 < n) {
+          const int64_t rsz = rl64(sz, cl + 1);
+          if (pq_cmp(csz, rsz) > 0) {
+            csz = rsz;
+            cnd = __builtin_amdgcn_readlane(nd, cl + 1);
+            child++;
+            nrel++;
+          }
+        }
+        if (pq_cmp(x.size, csz) <= 0) {
+          done = true;
+          break;
+        }
+        st_ent(k, PQEnt{csz, cnd, 0});
+        k = child;
+        rel = nrel;
+      }
+    }
+    st_ent(k, x);
+    __threadfence_block();
+    return r;
+  }
+  __device__ int32_t node(int i) { return pq_ld(&D.node[i]); }
+  __device__ void set_node(int i, int32_t v) {
+    if (lane == 0) pq_st(&D.node[i], v);
+    __threadfence_block();
+  }
+  __device__ bool istmp(int i) { return pq_ld(&D.istmp[i]) != 0; }
+  __device__ void set_istmp(int i) {
+    if (lane == 0) pq_st(&D.istmp[i], (uint8_t)1);
+    __threadfence_block();
+  }
+  __device__ int slot_pop(PQStep& c) { return pq_ld(&D.slots[--c.slot_top]); }
+  __device__ void slot_push(PQStep& c, int s) {
+    if (lane == 0) pq_st(&D.slots[c.slot_top], s);
+    c.slot_top++;
+    __threadfence_block();
+  }
+};
+
+// One step of the queue over every union key: out = op(a, b), the step record's operands.
+// out may be a's temp (the in-place x1.lazyor and lazyorfromlazyinputs).  The launch's
+// last workgroup returns the step's freed blocks to the stack and plans the next step.
 __global__ __launch_bounds__(256) void k_pq_step(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
-                                                 PQArgs A, int op, PQRef a_ref, PQRef b_ref, PQRef o_ref,
-                                                 unsigned long long* size) {
+                                                 PQArgs A, PQDev D) {
   __shared__ __align__(16) uint32_t lds[2048];
   __shared__ int q[257];
   __shared__ int sh[8];
-  __shared__ int found;
+  __shared__ int blk_sh;
+  __shared__ int last;
+  const int op = D.ctl->step.op;
+  const int a_ref = D.ctl->step.a, b_ref = D.ctl->step.b, o_ref = D.ctl->step.o;
+  PQState* const o_st = pq_states(D, o_ref);
   const uint32_t nt = *n_tasks;
   unsigned long long acc = 0;
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     const Task tk = tasks[t];
     const uint32_t s = (uint32_t)tk.a, n = (uint32_t)tk.b;
-    PQNode a = pq_load(a_ref, A, t, s, n, &found);
-    PQNode b = pq_load(b_ref, A, t, s, n, &found);
-    PQRef ar = a_ref, br = b_ref;
+    PQNode a = pq_load(a_ref, D, A, t, s, n);
+    PQNode b = pq_load(b_ref, D, A, t, s, n);
     // lazyorfromlazyinputs: a bitmap container goes first (RB/RoaringBitmap.java:782-788)
     if (op == PQ_LFL && a.present && b.present && (b.kind == PK_BE || b.kind == PK_BL) &&
         !(a.kind == PK_BE || a.kind == PK_BL)) {
       const PQNode x = a;
       a = b;
       b = x;
-      const PQRef y = ar;
-      ar = br;
-      br = y;
     }
     __syncthreads();  // every thread has read the states before the output state is written
-    PQState out{0, 0, 0, 0, -1, 0};
-    bool write_set = false, copy_set = false;
-    const PQRef* copy_from = nullptr;
+    PQState out{0, 0, 0, 0, -1, -1};
+    // every operand temp is consumed by the step, so its blocks are the result's to
+    // reuse; the ones not reused go back to the stack after the step
+    int spare0 = a.blk, spare1 = b.blk;
+    bool write_set = false;
     uint64_t r[4] = {0, 0, 0, 0};
     if (a.present && b.present) {
       uint64_t x[4];
-      pq_materialize(a, ar, A, t, lds, q, r);
-      pq_materialize(b, br, A, t, lds, q, x);
+      pq_materialize(a, D, A, lds, q, r);
+      pq_materialize(b, D, A, lds, q, x);
 #pragma unroll
       for (int i = 0; i < 4; i++) r[i] = op == PQ_XOR ? (r[i] ^ x[i]) : (r[i] | x[i]);
       int c, nr;
       const int kind = pq_kind(op, a, b, r, lds, sh, &c, &nr);
       if (kind >= 0) {
         if (kind == PK_R && nr == 0) nr = c == 65536 ? 1 : count_runs(r, lds, sh);
-        out = PQState{(uint32_t)c, (uint16_t)nr, (uint8_t)kind, 1, -1, 0};
+        out = PQState{(uint32_t)c, (uint16_t)nr, (uint8_t)kind, 1, -1, -1};
         write_set = true;
       }
     } else if (a.present || b.present) {
-      // unmatched key: a clone of the operand that holds it
+      // unmatched key: the operand's container moves over unchanged (a clone of an input
+      // container, or the temp's block itself)
       const PQNode& x = a.present ? a : b;
-      const PQRef& xr = a.present ? ar : br;
-      out = PQState{(uint32_t)x.card, (uint16_t)x.nruns, (uint8_t)x.kind, 1, x.src, 0};
-      if (x.src < 0 && xr.set != o_ref.set) {
-        copy_set = true;
-        copy_from = &xr;
+      out = PQState{(uint32_t)x.card, (uint16_t)x.nruns, (uint8_t)x.kind, 1, x.src, x.blk};
+      if (x.blk >= 0) {
+        if (spare0 == x.blk) spare0 = -1;
+        else spare1 = -1;
       }
     }
-    if (write_set) store_bitmap_owned(reinterpret_cast<uint8_t*>(o_ref.set + (size_t)t * 1024), r);
-    if (copy_set) {
-      load_bitmap_owned(reinterpret_cast<const uint8_t*>(copy_from->set + (size_t)t * 1024), r);
-      store_bitmap_owned(reinterpret_cast<uint8_t*>(o_ref.set + (size_t)t * 1024), r);
+    if (write_set) {
+      if (threadIdx.x == 0) {
+        int blk;
+        if (spare0 >= 0) {
+          blk = spare0;
+          spare0 = -1;
+        } else if (spare1 >= 0) {
+          blk = spare1;
+          spare1 = -1;
+        } else {
+          const int i = atomicSub(&D.ctl->free_top, 1) - 1;
+          blk = i >= 0 ? pq_ld(&D.blk_stack[i]) : -1;
+          if (blk < 0) atomicOr(&D.ctl->err, 1u);
+        }
+        blk_sh = blk;
+      }
+      lds_barrier();
+      out.blk = blk_sh;
+      if (out.blk >= 0) store_bitmap_owned(pq_block(D, out.blk), r);
     }
     if (threadIdx.x == 0) {
-      o_ref.st[t] = out;
+      if (spare0 >= 0) D.freed[atomicAdd(&D.ctl->freed_n, 1u)] = spare0;
+      if (spare1 >= 0) D.freed[atomicAdd(&D.ctl->freed_n, 1u)] = spare1;
+      o_st[t] = out;
       if (out.present) acc += (unsigned long long)pq_size(out.kind, (int)out.card, out.nruns);
     }
+    __syncthreads();  // blk_sh / lds reuse
   }
-  if (threadIdx.x == 0 && acc) atomicAdd(size, acc);
+  if (threadIdx.x == 0 && acc) atomicAdd(&D.ctl->size, acc);
+  // the last workgroup to finish schedules: every workgroup's freed entries and size are
+  // published (release) before its count, and acquired by the last one
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&D.ctl->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  const uint32_t fn = pq_ld(&D.ctl->freed_n);
+  const int top0 = max(0, (int)pq_ld(&D.ctl->free_top));
+  for (uint32_t j = threadIdx.x; j < fn; j += NT) D.blk_stack[top0 + j] = D.freed[j];
+  if (threadIdx.x >= 64) return;
+  PQWave m{D, (int)threadIdx.x};
+  PQStep c;
+  c.op = pq_ld(&D.ctl->step.op);
+  c.final_step = pq_ld(&D.ctl->step.final_step);
+  c.a = pq_ld(&D.ctl->step.a);
+  c.b = pq_ld(&D.ctl->step.b);
+  c.o = pq_ld(&D.ctl->step.o);
+  c.target = pq_ld(&D.ctl->step.target);
+  c.rel1 = pq_ld(&D.ctl->step.rel1);
+  c.rel2 = pq_ld(&D.ctl->step.rel2);
+  c.heap_n = pq_ld(&D.ctl->step.heap_n);
+  c.n_nodes = pq_ld(&D.ctl->step.n_nodes);
+  c.slot_top = pq_ld(&D.ctl->step.slot_top);
+  c.or_mode = pq_ld(&D.ctl->step.or_mode);
+  const unsigned long long size = pq_ld(&D.ctl->size);
+  pq_finish(m, c, 8 + (int64_t)size);
+  pq_plan(m, c);
+  if (threadIdx.x == 0) {
+    pq_st(&D.ctl->step.op, c.op);
+    pq_st(&D.ctl->step.final_step, c.final_step);
+    pq_st(&D.ctl->step.a, c.a);
+    pq_st(&D.ctl->step.b, c.b);
+    pq_st(&D.ctl->step.o, c.o);
+    pq_st(&D.ctl->step.target, c.target);
+    pq_st(&D.ctl->step.rel1, c.rel1);
+    pq_st(&D.ctl->step.rel2, c.rel2);
+    pq_st(&D.ctl->step.heap_n, c.heap_n);
+    pq_st(&D.ctl->step.n_nodes, c.n_nodes);
+    pq_st(&D.ctl->step.slot_top, c.slot_top);
+    pq_st(&D.ctl->free_top, top0 + (int)fn);
+    pq_st(&D.ctl->freed_n, 0u);
+    pq_st(&D.ctl->size, 0ull);
+    pq_st(&D.ctl->done, 0u);
+  }
 }
 
 // The root of the queue as the result: priorityqueue_or repairs it
@@ -211,18 +420,18 @@ __global__ __launch_bounds__(256) void k_pq_step(const Task* __restrict__ tasks,
 // toEfficientContainer, a lazy bitmap BY_CARD with 65536 -> RunContainer.full, an exact
 // bitmap kept); priorityqueue_xor returns it as is.
 __global__ __launch_bounds__(256) void k_pq_final(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
-                                                  PQArgs A, int repair, PQRef root, OutCtx oc) {
+                                                  PQArgs A, int repair, PQDev D, OutCtx oc) {
   __shared__ __align__(16) uint32_t acc[2048];
   __shared__ __align__(16) uint32_t tmp[2048];
   __shared__ int q[257];
   __shared__ int sh[8];
-  __shared__ int found;
   __shared__ Prefix shp;
+  const int root = D.ctl->step.a;
   const uint32_t nt = *n_tasks;
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     __syncthreads();
     const Task tk = tasks[t];
-    const PQNode x = pq_load(root, A, t, (uint32_t)tk.a, (uint32_t)tk.b, &found);
+    const PQNode x = pq_load(root, D, A, t, (uint32_t)tk.a, (uint32_t)tk.b);
     if (!x.present) {
       wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
       continue;
@@ -238,7 +447,7 @@ __global__ __launch_bounds__(256) void k_pq_final(const Task* __restrict__ tasks
       materialize(d, A.payload, tmp, q, r);  // RunContainer.toEfficientContainer -> A / B
       kind = by_card(c);
     } else {
-      load_bitmap_owned(reinterpret_cast<const uint8_t*>(root.set + (size_t)t * 1024), r);
+      pq_materialize(x, D, A, tmp, q, r);
       if (!repair) kind = x.kind == PK_BL ? DK_B : x.kind;
       else if (x.kind == PK_BL) kind = c == 65536 ? DK_R : by_card(c);
       else if (x.kind == PK_R) kind = eff(c, x.nruns);
@@ -268,16 +477,15 @@ void launch_pq_leaf_sizes(hipStream_t s, const CDesc* desc, const uint32_t* bm, 
   hipLaunchKernelGGL(k_pq_leaf_sizes, dim3(g), dim3(256), 0, s, desc, bm, payload, n, sizes);
 }
 
-void launch_pq_step(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, PQArgs args, int op, PQRef a,
-                    PQRef b, PQRef out, unsigned long long* size) {
+void launch_pq_step(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, PQArgs args, PQDev D) {
   grid = std::max(1, std::min(grid, resident_grid((const void*)&k_pq_step)));
-  hipLaunchKernelGGL(k_pq_step, dim3(grid), dim3(256), 0, s, tasks, nt, args, op, a, b, out, size);
+  hipLaunchKernelGGL(k_pq_step, dim3(grid), dim3(256), 0, s, tasks, nt, args, D);
 }
 
 void launch_pq_final(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, PQArgs args, int repair,
-                     PQRef root, OutCtx oc) {
+                     PQDev D, OutCtx oc) {
   grid = std::max(1, std::min(grid, resident_grid((const void*)&k_pq_final)));
-  hipLaunchKernelGGL(k_pq_final, dim3(grid), dim3(256), 0, s, tasks, nt, args, repair, root, oc);
+  hipLaunchKernelGGL(k_pq_final, dim3(grid), dim3(256), 0, s, tasks, nt, args, repair, D, oc);
 }
 
 }  // namespace rbg

@@ -145,3 +145,18 @@ def test_priorityqueue_realdata(gpu, run_opt):
         assert got == O.wide("priorityqueue_or", bufs), ds
         assert len(O.to_values(got)) == known[ds]["wide_or"]
         assert _wide("priorityqueue_xor", bufs) == O.wide("priorityqueue_xor", bufs), ds
+
+
+@pytest.mark.parametrize("n", [600, 3000])
+def test_priorityqueue_many_bitmaps_wide_keys(gpu, n):
+    """Many small bitmaps spread over most of the 65,536 keys (C3-shaped key space): the
+    temps hold arena blocks only for their own keys, so the op completes (the dense
+    per-temp layout needed n/2 x keys x 8 KiB) and matches the queue restatement."""
+    rng = np.random.default_rng(n)
+    bufs = []
+    for i in range(n):
+        keys = np.sort(rng.choice(65536, 40, replace=False))
+        v = (keys[:, None].astype(np.int64) << 16) + rng.integers(0, 65536, (40, 6 if i % 5 else 3000))
+        bufs.append(O.from_values(v.ravel(), i % 7 == 0))
+    for op in ("priorityqueue_or", "priorityqueue_xor"):
+        assert _wide(op, bufs) == O.wide(op, bufs), op
