@@ -196,7 +196,7 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
   const uint4* pv = reinterpret_cast<const uint4*>(pslot) + l;
   uint4 v[8];
 #pragma unroll
-  for (int j = 0; j < 8; j++) v[j] = (64 * j + l < nvec) ? pv[64 * j] : make_uint4(0, 0, 0, 0);
+  for (int j = 0; j < 8; j++) v[j] = (64 * j + l < nvec) ? ld_in(pv + 64 * j) : make_uint4(0, 0, 0, 0);
   w_map_lds(mkind, mcard, mslot, lds);
   prio_lo();
   STAMP(4);
@@ -382,8 +382,8 @@ __device__ __forceinline__ void runs_to_lds2(const uint8_t* sa, int na, uint32_t
 #pragma unroll
     for (int j = 0; j < R; j++) {
       const int q = 64 * (j0 + j) + l;
-      va[j] = q < nva ? a4[q] : make_uint4(0, 0, 0, 0);
-      vb[j] = q < nvb ? b4[q] : make_uint4(0, 0, 0, 0);
+      va[j] = q < nva ? ld_in(a4 + q) : make_uint4(0, 0, 0, 0);
+      vb[j] = q < nvb ? ld_in(b4 + q) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < R; j++) {
@@ -441,6 +441,13 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
   const int ka = tk.kind_a, kb = tk.kind_b;
   const int ca = (int)tk.card_a, cb = (int)tk.card_b;
   if (OP == OP_AND && ka == DK_R && kb == DK_R && rr_and_task<MODE>(t, tk, pa, pb, oc, task_card, lds)) return;
+#if RBG_EXP_SKIP_HEAVY
+  if (OP == OP_AND && ka == DK_R && kb == DK_R) {
+    if (MODE == 1) { if (lane_id() == 0) task_card[t] = 0; }
+    else w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
+    return;
+  }
+#endif
   STAMP_DECL
   WCtr x;
   w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, (uint8_t)ka, 0}, pa, lds, x);

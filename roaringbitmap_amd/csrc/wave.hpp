@@ -23,6 +23,15 @@ __device__ __forceinline__ uint64_t uni64(uint64_t x) {
          (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 
+// Operand payload loads (16 B) are nontemporal: every input byte of an op is read once,
+// and keeping the inputs out of the caches leaves the Infinity Cache to the result
+// slots that the serializer reads back (C2 AND: compute -7 %, andCardinality -10 %).
+__device__ __forceinline__ uint4 ld_in(const uint4* p) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const v4u v = __builtin_nontemporal_load(reinterpret_cast<const v4u*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // Bit-field helpers for map probes.  Written as v_bfe_u32 directly: the compiler
 // otherwise turns a field extract into shift + mask (2 VALU instead of 1), and a
 // variable bit test into shift + shift + and.  The hardware reads only the low
@@ -79,7 +88,7 @@ __device__ __forceinline__ void w_load_bitmap(const uint8_t* p, WCtr& x) {
   const uint4* q = reinterpret_cast<const uint4*>(p) + lane_id();
 #pragma unroll
   for (int i = 0; i < 8; i++) {
-    const uint4 v = q[64 * i];
+    const uint4 v = ld_in(q + 64 * i);
     x.w[2 * i] = (uint64_t)v.x | ((uint64_t)v.y << 32);
     x.w[2 * i + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
   }
@@ -175,7 +184,7 @@ __device__ __forceinline__ void w_scatter_array(uint32_t* lds, const uint16_t* v
 #pragma unroll
     for (int j = 0; j < kVecRound; j++) {
       const int k = 64 * (j0 + j) + l;
-      v[j] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
+      v[j] = k < nvec ? ld_in(v4 + k) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < kVecRound; j++) {
@@ -218,7 +227,7 @@ __device__ __forceinline__ void w_toggle_runs(uint32_t* lds, const uint8_t* slot
 #pragma unroll
     for (int j = 0; j < kVecRound; j++) {
       const int k = 64 * (j0 + j) + l;
-      v[j] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
+      v[j] = k < nvec ? ld_in(v4 + k) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int j = 0; j < kVecRound; j++) {
@@ -317,7 +326,7 @@ __device__ __forceinline__ void w_combine(const CDesc& d, const uint8_t* payload
     const uint4* g = reinterpret_cast<const uint4*>(slot) + lane_id();
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      const uint4 v = g[64 * i];
+      const uint4 v = ld_in(g + 64 * i);
       x.w[2 * i] = w_op<OP>(x.w[2 * i], (uint64_t)v.x | ((uint64_t)v.y << 32));
       x.w[2 * i + 1] = w_op<OP>(x.w[2 * i + 1], (uint64_t)v.z | ((uint64_t)v.w << 32));
     }
@@ -625,7 +634,8 @@ __device__ __forceinline__ void w_bitmap_to_lds_dma(const uint8_t* slot, uint32_
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int i = 0; i < 8; i++)
-    __builtin_amdgcn_global_load_lds((global_void_ptr)(g + 64 * i), (lds_void_ptr)(lds + 256 * i), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((global_void_ptr)(g + 64 * i), (lds_void_ptr)(lds + 256 * i), 16, 0,
+                                     2 /* nt */);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -919,7 +929,8 @@ __device__ __forceinline__ CopyJob copy_begin(uint8_t* dst, const uint8_t* src, 
   j.nvec = (n - j.head) >> 4;
   return j;
 }
-// pass i0 (512 body vectors): every source vector the pass needs, requested at once (one
+// pass i0 (512 body vectors): every source vector the pass needs, requested at once
+// (nontemporal: each result byte is read once; serialize -10 % against default loads; one
 // past the body too: the partner of the last one; lane 63 of the last group also needs
 // aligned vector i0 + 512 -- the one past the body when this is the last pass: it still
 // holds tail bytes or slack)
@@ -928,7 +939,7 @@ __device__ __forceinline__ void copy_load(const CopyJob& j, uint32_t i0, u32x4 a
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const uint32_t i = i0 + 64 * k + l;
-    if (i <= j.nvec && (j.shift != 0 || i < j.nvec)) a[k] = j.sv[i];
+    if (i <= j.nvec && (j.shift != 0 || i < j.nvec)) a[k] = __builtin_nontemporal_load(j.sv + i);
     else a[k] = u32x4{0, 0, 0, 0};
   }
   last = u32x4{0, 0, 0, 0};

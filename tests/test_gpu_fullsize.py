@@ -195,4 +195,17 @@ def test_c5_full_size(eng):
     assert (mn, mx) == (vmin, vmax)
     assert (s, cnt) == (tot, tcnt)
     assert rs["cardinality"] == tcnt
+    # result bytes: for 6 keys (the first, the partial last one and 4 random), the full
+    # result's container equals tests/_bsi.py's compare(RANGE) over that key's ebM and 31
+    # slice containers (generated as a key slice and fetched), with the global min / max
+    import _bsi
+    got = eng.fetch().serialize()
+    nkeys = (rows + 65535) // 65536
+    keys = sorted({0, nkeys - 1, *np.random.default_rng(55).choice(nkeys, 4, replace=False).tolist()})
+    for k in keys:
+        sb = eng.synth(4, seed, rows, k, k + 1)
+        bms = [eng.batch_fetch(sb, i).serialize() for i in range(32)]
+        eng.release(sb)
+        exp = _bsi.BSI(bms[0], bms[1:], mn, mx).compare("RANGE", lo, hi)
+        _same(_fmt.sub_bitmap(got, [k]), exp, f"C5 key {k}")
     eng.release(b)
