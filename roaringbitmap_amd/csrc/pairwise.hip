@@ -441,13 +441,6 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
   const int ka = tk.kind_a, kb = tk.kind_b;
   const int ca = (int)tk.card_a, cb = (int)tk.card_b;
   if (OP == OP_AND && ka == DK_R && kb == DK_R && rr_and_task<MODE>(t, tk, pa, pb, oc, task_card, lds)) return;
-#if RBG_EXP_SKIP_HEAVY
-  if (OP == OP_AND && ka == DK_R && kb == DK_R) {
-    if (MODE == 1) { if (lane_id() == 0) task_card[t] = 0; }
-    else w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
-    return;
-  }
-#endif
   STAMP_DECL
   WCtr x;
   w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, (uint8_t)ka, 0}, pa, lds, x);

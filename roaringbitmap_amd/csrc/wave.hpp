@@ -464,10 +464,14 @@ __device__ __forceinline__ void w_store_bitmap(uint8_t* p, const WCtr& x) {
   for (int i = 0; i < 8; i++) {
     const uint4 v = make_uint4((uint32_t)x.w[2 * i], (uint32_t)(x.w[2 * i] >> 32), (uint32_t)x.w[2 * i + 1],
                                (uint32_t)(x.w[2 * i + 1] >> 32));
-    // streaming (nontemporal) stores: results are read back only by later kernels
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 nv = {v.x, v.y, v.z, v.w};
+#if RBG_B_PLAIN_STORE
+    *reinterpret_cast<u32x4*>(q + 64 * i) = nv;
+#else
+    // streaming (nontemporal) stores: results are read back only by later kernels
     __builtin_nontemporal_store(nv, reinterpret_cast<u32x4*>(q + 64 * i));
+#endif
   }
 }
 
@@ -904,6 +908,15 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t q, uint32_t
   return o;
 }
 
+// serialized-output stores (the final bytes: not read again by the op)
+__device__ __forceinline__ void st_out(g_u32x4* p, const u32x4& v) {
+#if RBG_SER_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 struct CopyJob {
   const g_u16* s16;
   g_u16* d16;
@@ -951,7 +964,7 @@ __device__ __forceinline__ void copy_store(const CopyJob& j, uint32_t i0, const 
 #pragma unroll
     for (int k = 0; k < 8; k++) {
       const uint32_t i = i0 + 64 * k + l;
-      if (i < j.nvec) j.dv[i] = a[k];
+      if (i < j.nvec) st_out(j.dv + i, a[k]);
     }
     return;
   }
@@ -967,7 +980,7 @@ __device__ __forceinline__ void copy_store(const CopyJob& j, uint32_t i0, const 
       b = last;
     }
     const u32x4 o = funnel16(a[k], b, q, r);
-    if (i < j.nvec) j.dv[i] = o;
+    if (i < j.nvec) st_out(j.dv + i, o);
   }
 }
 __device__ __forceinline__ void copy_tail(const CopyJob& j) {
