@@ -95,6 +95,8 @@ struct __align__(16) ORec {
 // the result's long cardinality is accumulated at ((u64*)OutCtx::err)[kCardWord]
 // (inside the zeroed look-back header, 32 B past the error word)
 constexpr int kCardWord = 4;
+// look-back tile statuses zeroed by every plan kernel (k_place's tiles)
+constexpr int kMaxTiles = 128;
 
 struct OutCtx {
   uint8_t* out;

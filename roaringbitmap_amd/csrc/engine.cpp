@@ -42,8 +42,8 @@ static void set_err(const std::string& s) { g_err = s; }
 
 constexpr size_t kSlack = 256;  // every device buffer carries read slack (group_copy)
 constexpr int kMaxKeys = 65536;
-constexpr size_t kLbHeader = 256;  // look-back state: error @64, result card @96, fused pairwise totals @192
-constexpr size_t kMaxTiles = 128;  // tile statuses follow the 65536 task statuses
+constexpr size_t kLbHeader = 256;  // look-back state: error @64, result card @96
+// tile statuses (kMaxTiles, device.hpp) follow the 65536 task statuses, tile cardinalities them
 
 // RBG_DEBUG_SYNC=1: synchronise and report after every pipeline stage (debugging aid)
 static bool debug_sync() {
@@ -143,6 +143,7 @@ struct Ctx {
   std::vector<int32_t> pending_src;  // batches the pending result's pass-through records point into
   size_t pending_ub = 0;
   bool serialized = false;  // pending result already in the portable layout
+  bool place_pending = false;  // the op's k_place not launched yet (serialization then places too)
   size_t n_cards = 0;
   int last = 0;  // 0 none, 1 serialized result, 2 cardinality, 3 batch cardinalities
   void* pinned = nullptr;
@@ -518,6 +519,7 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   oc->tile_card = reinterpret_cast<uint64_t*>(lb + kLbHeader + 8 * (kMaxKeys + kMaxTiles));
   oc->recs = c->recs.as<ORec>();
   c->serialized = false;
+  c->place_pending = false;
   c->pending_ub = 0;
   c->zlb = c->ztile = nullptr;
   c->pending_src.clear();
@@ -541,6 +543,21 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   return RBG_OK;
 }
 
+// Placement of a materialising op's result (k_place) is deferred until something needs it
+// (serialization, result statistics, a key-shard fetch): an op whose caller only wants the
+// result to exist on the device (a BSI query followed by its sum) does not pay for it.
+static void defer_place(Ctx* c) {
+  c->place_pending = true;
+  c->last = 1;
+}
+static int ensure_placed(Ctx* c) {
+  if (!c->place_pending) return RBG_OK;
+  launch_place(c->stream, c->ntasks.as<uint32_t>(), c->pending, c->info.as<ResultInfo>());
+  HIPCHK(hipGetLastError());
+  c->place_pending = false;
+  return RBG_OK;
+}
+
 // Portable serialization of the pending result (RB/RoaringArray.java:896-940),
 // on the device, once per result.
 static int ctx_serialize(Ctx* c) {
@@ -549,6 +566,7 @@ static int ctx_serialize(Ctx* c) {
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   if (c->serialized) return RBG_OK;
+  CHK(ensure_placed(c));
   launch_serialize(c->stream, c->ntasks.as<uint32_t>(), c->pending);
   HIPCHK(hipGetLastError());
   c->serialized = true;
@@ -612,8 +630,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>(), oc.err);
     c->last = 2;
   } else {
-    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
-    c->last = 1;
+    defer_place(c);
   }
   c->mark(3);
   HIPCHK(hipGetLastError());
@@ -1006,8 +1023,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
       launch_reduce_card(s, c->task_card.as<uint32_t>(), c->ntasks.as<uint32_t>(), c->info.as<ResultInfo>(), oc.err);
       c->last = 2;
     } else {
-      launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
-      c->last = 1;
+      defer_place(c);
     }
     c->mark(3);
     HIPCHK(hipGetLastError());
@@ -1087,8 +1103,7 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
   if (op == BSI_SUM_ONLY) {
     c->last = 0;
   } else {
-    launch_place(s, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>());
-    c->last = 1;
+    defer_place(c);
   }
   c->mark(3);
   HIPCHK(hipGetLastError());
@@ -1118,6 +1133,7 @@ static int ctx_bsi_sums(Ctx* c, int64_t* out2) {
 }
 
 static int ctx_info(Ctx* c, ResultInfo* ri) {
+  if (c->last == 1) CHK(ensure_placed(c));
   HIPCHK(hipMemcpyAsync(ri, c->info.p, sizeof(ResultInfo), hipMemcpyDeviceToHost, c->stream));
   uint64_t card = 0;
   uint32_t err = 0;

@@ -110,6 +110,21 @@ __device__ __forceinline__ void totals(const OutCtx& oc, uint32_t nt, uint32_t* 
   *payload = s & ((1ULL << 44) - 1);
 }
 
+__device__ __forceinline__ void write_cookie(uint8_t* base, uint32_t size, uint32_t has_run) {
+  uint32_t cookie[2];
+  int nb;
+  if (has_run) {  // RB/RoaringArray.java:900-904
+    cookie[0] = 12347u | ((size - 1) << 16);
+    nb = 4;
+  } else {  // :914-917
+    cookie[0] = 12346u;
+    cookie[1] = size;
+    nb = 8;
+  }
+  const uint8_t* cb = reinterpret_cast<const uint8_t*>(cookie);
+  for (int i = 0; i < nb; i++) base[i] = cb[i];
+}
+
 // One wave per task record (grid-stride): a kept result's payload bytes go to their offset
 // (w_copy: aligned 16 B loads and stores, the source's misalignment funnel-shifted in
 // registers), and lane 0 writes its descriptor (key, card - 1) and offset-table entry --
@@ -138,20 +153,7 @@ __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ 
       base[4 + b] = v;
     }
   }
-  if (gid == 0) {
-    uint32_t cookie[2];
-    int nb;
-    if (has_run) {  // RB/RoaringArray.java:900-904
-      cookie[0] = 12347u | ((size - 1) << 16);
-      nb = 4;
-    } else {  // :914-917
-      cookie[0] = 12346u;
-      cookie[1] = size;
-      nb = 8;
-    }
-    const uint8_t* cb = reinterpret_cast<const uint8_t*>(cookie);
-    for (int i = 0; i < nb; i++) base[i] = cb[i];
-  }
+  if (gid == 0) write_cookie(base, size, has_run);
   uint8_t* pay = oc.out + oc.payload_base;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
