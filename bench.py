@@ -274,27 +274,39 @@ def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
         dist.all_reduce(mm, op=dist.ReduceOp.MIN)  # the BSI's min / max are global
     mn, mx = int(mm[0]), -int(mm[1])
     lo, hi = 1 << 29, 1 << 30
+    # sum(found) stays on the device: (sum, count) copied into a device tensor on the engine
+    # stream and all-reduced from there (RCCL); no host read inside the step
+    ext = torch.cuda.ExternalStream(eng.stream_ptr)
+    sums = torch.zeros(2, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
 
     def step():
         eng.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=True)
-        sc = eng.bsi_sums()
+        ext.wait_stream(torch.cuda.current_stream())  # the last step's all-reduce has read `sums`
+        eng.bsi_sums_device(sums)
         if dist is not None:
-            t = torch.tensor(sc, dtype=torch.int64, device=cdev)
-            dist.all_reduce(t)
-            sc = (int(t[0]), int(t[1]))
-        return sc
+            torch.cuda.current_stream().wait_stream(ext)
+            if cdev == "cuda":
+                dist.all_reduce(sums)
+            else:  # gloo rehearsal: the collective runs on host memory
+                t = sums.cpu()
+                dist.all_reduce(t)
+                sums.copy_(t)
 
     for _ in range(warmup):
-        sc = step()
+        step()
+    torch.cuda.synchronize()
+    eng.sync()
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        sc = step()
+        step()
     eng.sync()
+    torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     wall = time.perf_counter() - t0
+    sc = (int(sums[0]), int(sums[1]))
     ein = st["payload_bytes"] + 4 * st["containers"]
     t = torch.tensor([wall, float(ein)], dtype=torch.float64, device=cdev)
     if dist is not None:
@@ -672,8 +684,9 @@ def _only(eng, args, rank, world, dist, cdev):
         a = eng.synth(0, 0xC2A0 + 0x10000 * rank)
         b = eng.synth(0, 0xC2B0 + 0x10000 * rank)
         for _ in range(args.warmup + steps):
-            if w == "c2":
+            if w == "c2":  # the headline step: the op and its serialization
                 eng.pairwise("and", a, b)
+                eng.serialize()
             else:
                 eng.and_cardinality(a, b)
         eng.sync()

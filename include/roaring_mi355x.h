@@ -235,6 +235,9 @@ int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2);
 int rbg_ctx_bsi(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
                 int32_t min_value, int32_t max_value, int want_sum);
 int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2);
+/* The same {sum, count} (two int64) copied to device memory dst2, enqueued on the context
+ * stream (no host synchronisation: the sum stays on the device, e.g. for an all-reduce). */
+int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2);
 /* Diagnostics: 20 per-phase shader-clock totals of the pairwise kernel (all zero unless the
  * library was built with -DRBG_STAMPS=1); reset != 0 clears them. */
 int rbg_debug_stamps(uint64_t* out20, int reset);

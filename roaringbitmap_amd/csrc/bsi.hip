@@ -125,10 +125,16 @@ __device__ __forceinline__ void oneil_finish(int op, const VB& fixed, const VB& 
   }
 }
 
+// Block 0 also zeroes the op's sum words (zsums, kBsiSumWords u64) and the defer count.
 __global__ __launch_bounds__(256) void k_plan_bsi(const uint32_t* __restrict__ key_off, const uint32_t* __restrict__ bm,
                                                   uint32_t need, Task* __restrict__ by_key, uint8_t* __restrict__ flag,
-                                                  uint32_t* __restrict__ wg_count, uint64_t* zlb, uint64_t* ztile) {
+                                                  uint32_t* __restrict__ wg_count, uint64_t* zlb, uint64_t* ztile,
+                                                  unsigned long long* zsums, uint32_t* zdefer) {
   plan_zero(zlb, ztile);
+  if (blockIdx.x == 0) {
+    if (zsums && threadIdx.x < (unsigned)kBsiSumWords) zsums[threadIdx.x] = 0;
+    if (zdefer && threadIdx.x == 0) zdefer[0] = 0;
+  }
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t s = key_off[k], n = key_off[k + 1] - s;
   // a key yields a result only where input `need` (ebM, or foundSet for sum alone) has a container
@@ -754,14 +760,35 @@ __global__ __launch_bounds__(256) void k_bsi_defer(const Task* __restrict__ task
 }
 
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
-                     uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile) {
-  hipLaunchKernelGGL(k_plan_bsi, dim3(256), dim3(256), 0, s, key_off, bm, need, by_key, flag, wg_count, zlb, ztile);
+                     uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile, unsigned long long* zsums,
+                     uint32_t* zdefer) {
+  hipLaunchKernelGGL(k_plan_bsi, dim3(256), dim3(256), 0, s, key_off, bm, need, by_key, flag, wg_count, zlb, ztile,
+                     zsums, zdefer);
+}
+
+// sum(foundSet) as Java longs (BSI/:581-592) from the per-slice counts, on the device:
+// sum = sum over x of (long) (1 << x) * andCardinality(bA[x], found), each andCardinality a
+// Java int (RB/RoaringBitmap.java:413-434); (0, 0) when the found set is empty.  Lane x
+// takes slice x; the result stays on the device (sums[kBsiSumOut], [kBsiSumOut + 1]).
+__global__ __launch_bounds__(64) void k_bsi_sum_final(unsigned long long* __restrict__ sums, int nbits) {
+  const int x = threadIdx.x;
+  const unsigned long long count = sums[kBsiMaxInputs];
+  unsigned long long v = 0;
+  if (x < nbits && count) {
+    const int64_t card = (int32_t)(uint32_t)sums[x];
+    const int64_t w = (int64_t)(int32_t)(1u << x);
+    v = (unsigned long long)(w * card);
+  }
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if (x == 0) {
+    sums[kBsiSumOut] = v;
+    sums[kBsiSumOut + 1] = count;
+  }
 }
 
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
                 unsigned long long* sums, BsiScratch* sc) {
   if (p.op <= BSI_RANGE && p.nbits <= kBsiRegSlices && sc) {
-    (void)hipMemsetAsync(sc->defer, 0, 4, s);
     hipLaunchKernelGGL(k_bsi_table, dim3((unsigned)((sc->stride + 3) / 4)), dim3(256), 0, s, tasks, nt, args,
                        reinterpret_cast<BsiIn*>(sc->table));
     const int g = std::max(1, std::min(grid * kBsiUnits, resident_grid((const void*)&k_bsi_reg)));
@@ -773,10 +800,11 @@ void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, 
                        reinterpret_cast<const TB*>(sc->kin), sc->stride, sc->defer);
     const int g3 = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_defer)));
     hipLaunchKernelGGL(k_bsi_defer, dim3(g3), dim3(256), 0, s, tasks, sc->defer, args, p, oc, sums);
-    return;
+  } else {
+    const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi)));
+    hipLaunchKernelGGL(k_bsi, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc, sums);
   }
-  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi)));
-  hipLaunchKernelGGL(k_bsi, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc, sums);
+  if (sums) hipLaunchKernelGGL(k_bsi_sum_final, dim3(1), dim3(64), 0, s, sums, p.nbits);
 }
 
 }  // namespace rbg

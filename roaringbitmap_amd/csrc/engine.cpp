@@ -611,19 +611,32 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     case OP_ANDNOT: ub = na; break;
     default: ub = std::min<size_t>((size_t)na + nb, kMaxKeys); break;
   }
+  // Dense key ranges (the op's task bound covers at least half of the range) skip the plan
+  // launch: the compute kernel takes key key_lo + t as task t and resolves it itself (one
+  // record and scratch slot per key of the range).  Sparse ones are planned and compacted
+  // first, so the kernel sees only keys with work.  RBG_PAIRWISE_PLAN=1 always plans.
+  static const bool force_plan = getenv("RBG_PAIRWISE_PLAN") != nullptr;
+  const size_t nkeys = key_hi > key_lo ? (size_t)(key_hi - key_lo) : 0;
+  const bool direct = nkeys > 0 && 2 * ub >= nkeys && !force_plan;
   OutCtx oc;
-  CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, card_only));
+  CHK(prepare_output(c, direct ? std::max(ub, nkeys) : ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub,
+                     &oc, card_only));
   c->pending_src = {ia, ib};
   c->mark(0);
-  dbg(s, "memset");
-  launch_plan_pairwise(s, plan_op, key_lo, key_hi, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(),
-                       B->key_off.as<uint32_t>(), db, B->payload.as<uint8_t>(), c->wg_epoch.as<uint64_t>(),
-                       next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), c->zlb, c->ztile, oc.err);
-  dbg(s, "plan");
+  PwDirect pd{A->key_off.as<uint32_t>(), da, B->key_off.as<uint32_t>(), db, key_lo, (uint32_t)nkeys,
+              c->ntasks.as<uint32_t>(), c->zlb, c->ztile};
+  if (!direct) {
+    launch_plan_pairwise(s, plan_op, key_lo, key_hi, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(),
+                         B->key_off.as<uint32_t>(), db, B->payload.as<uint8_t>(), c->wg_epoch.as<uint64_t>(),
+                         next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), c->zlb, c->ztile, oc.err);
+    dbg(s, "plan");
+  }
   c->mark(1);
-  const int grid = grid_for((ub + 3) / 4, 16384);  // 4 waves (tasks) per workgroup, clamped to the resident grid
+  // 4 waves (tasks) per workgroup, clamped to the resident grid
+  const int grid = grid_for(((direct ? nkeys : ub) + 3) / 4, 16384);
   launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(),
-                  A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), oc, c->task_card.as<uint32_t>());
+                  A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), oc, c->task_card.as<uint32_t>(),
+                  direct ? &pd : nullptr);
   dbg(s, "pairwise");
   c->mark(2);
   if (card_only) {
@@ -1064,8 +1077,7 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   hipStream_t s = c->stream;
-  CHK(c->bsi_sums.ensure(8 * (kBsiMaxInputs + 1)));
-  HIPCHK(hipMemsetAsync(c->bsi_sums.p, 0, 8 * (kBsiMaxInputs + 1), s));
+  CHK(c->bsi_sums.ensure(8 * kBsiSumWords));  // zeroed by the plan kernel
   c->bsi_nbits = nbits;
   int mode = op;
   if (op != BSI_SUM_ONLY) {
@@ -1078,17 +1090,6 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
   CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, op == BSI_SUM_ONLY));
   c->pending_src = {id};
   const uint32_t need = mode == -1 ? 0xFFFFFFFFu : (op == BSI_SUM_ONLY ? (uint32_t)(nbits + 1) : 0u);
-  c->mark(0);
-  launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
-                  c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile);
-  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
-                 c->ntasks.as<uint32_t>());
-  c->mark(1);
-  WideArgs wa{};
-  wa.desc = B->desc.as<CDesc>();
-  wa.bm = B->bm.as<uint32_t>();
-  wa.payload = B->payload.as<uint8_t>();
-  BsiArgs p{mode < 0 ? BSI_EQ : mode, nbits, has_found, (uint32_t)start, (uint32_t)end};
   BsiScratch sc{};
   if (mode >= 0 && mode <= BSI_RANGE) {
     CHK(c->bsi_defer.ensure(4 * (ub + 1)));
@@ -1097,6 +1098,18 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
     CHK(c->bsi_table.ensure((size_t)16 * 34 * ub));
     sc = BsiScratch{c->bsi_defer.as<uint32_t>(), c->bsi_cnts.as<int>(), c->bsi_kin.p, ub, c->bsi_table.p};
   }
+  c->mark(0);
+  launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
+                  c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile,
+                  c->bsi_sums.as<unsigned long long>(), sc.defer);
+  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
+                 c->ntasks.as<uint32_t>());
+  c->mark(1);
+  WideArgs wa{};
+  wa.desc = B->desc.as<CDesc>();
+  wa.bm = B->bm.as<uint32_t>();
+  wa.payload = B->payload.as<uint8_t>();
+  BsiArgs p{mode < 0 ? BSI_EQ : mode, nbits, has_found, (uint32_t)start, (uint32_t)end};
   launch_bsi(s, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, p, oc,
              want_sum ? c->bsi_sums.as<unsigned long long>() : nullptr, sc.defer ? &sc : nullptr);
   c->mark(2);
@@ -1110,25 +1123,14 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
   return RBG_OK;
 }
 
-// (sum, count) as Java longs from the device totals: each slice's andCardinality is a
-// Java int (RB/RoaringBitmap.java:413-434), weighted by (long) (1 << x)
+// (sum, count) of the last BSI call: k_bsi_sum_final's Java longs, read back
 static int ctx_bsi_sums(Ctx* c, int64_t* out2) {
-  unsigned long long h[kBsiMaxInputs + 1];
-  HIPCHK(hipMemcpyAsync(h, c->bsi_sums.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  const uint64_t count = h[kBsiMaxInputs];
-  if (count == 0) {
+  if (!c->bsi_sums.p) {
     out2[0] = out2[1] = 0;
     return RBG_OK;
   }
-  uint64_t sum = 0;
-  for (int x = 0; x < c->bsi_nbits; x++) {
-    const int64_t card = (int32_t)(uint32_t)h[x];
-    const int64_t w = (int64_t)(int32_t)(1u << x);
-    sum += (uint64_t)(w * card);
-  }
-  out2[0] = (int64_t)sum;
-  out2[1] = (int64_t)count;
+  HIPCHK(hipMemcpyAsync(out2, c->bsi_sums.as<uint64_t>() + kBsiSumOut, 16, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   return RBG_OK;
 }
 
@@ -1719,6 +1721,13 @@ int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2) {
   if (!out2) return RBG_ERR_ILLEGAL_ARGUMENT;
   HIPCHK(hipSetDevice(ctx->c.device));
   return ctx_bsi_sums(&ctx->c, out2);
+}
+int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2) {
+  if (!dst2 || !ctx->c.bsi_sums.p) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipSetDevice(ctx->c.device));
+  HIPCHK(hipMemcpyAsync(dst2, ctx->c.bsi_sums.as<uint64_t>() + kBsiSumOut, 16, hipMemcpyDeviceToDevice,
+                        ctx->c.stream));
+  return RBG_OK;
 }
 static int bsi_load(Ctx* c, const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* lens,
                     size_t nbits, const uint8_t* found, size_t found_len, int32_t* id) {

@@ -177,6 +177,10 @@ void launch_pq_final(hipStream_t s, int grid, const Task* tasks, const uint32_t*
 enum BsiOp : int { BSI_EQ = 0, BSI_NEQ = 1, BSI_LE = 2, BSI_LT = 3, BSI_GE = 4, BSI_GT = 5, BSI_RANGE = 6,
                    BSI_ALL = 7, BSI_SUM_ONLY = 8 };
 constexpr int kBsiMaxInputs = 34;  // ebM + up to 32 slices + foundSet
+// BSI sum words (u64): per-slice |bA[x] & found| at [x], the found count at [kBsiMaxInputs],
+// then sum(found) = (sum, count) as Java longs at [kBsiSumOut], [kBsiSumOut + 1]
+constexpr int kBsiSumOut = kBsiMaxInputs + 1;
+constexpr int kBsiSumWords = kBsiSumOut + 2;
 struct BsiArgs {
   int op;         // BsiOp
   int nbits;      // slices
@@ -204,8 +208,23 @@ void launch_plan_pairwise(hipStream_t s, int op, int key_lo, int key_hi, const u
                           uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, uint64_t* zlb,
                           uint64_t* ztile, uint32_t* err);
 // mode 0: materialise results (task slots + records); mode 1: andCardinality into task_card
+// Direct mode of the pairwise compute kernel (no plan launch): task t = key key_lo + t over
+// nkeys keys, resolved by the kernel through both operands' key CSR; it also writes the task
+// count (n_tasks_out) and zeroes the op's look-back state (zlb, ztile), as the plan would.
+struct PwDirect {
+  const uint32_t* koa;
+  const CDesc* da;
+  const uint32_t* kob;
+  const CDesc* db;
+  int key_lo;
+  uint32_t nkeys;
+  uint32_t* n_tasks_out;
+  uint64_t* zlb;
+  uint64_t* ztile;
+};
+// direct: null = tasks / nt from launch_plan_pairwise
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
-                     const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card);
+                     const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct);
 // diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
 void debug_stamps(uint64_t* out20, bool reset);
 // diagnostic build (-DRBG_BSI_STAMPS=1): per-phase clock totals of k_bsi_reg
@@ -231,9 +250,12 @@ struct GatherItem {
 };
 void launch_gather(hipStream_t s, const GatherItem* items, uint64_t n, const uint8_t* src, uint8_t* dst);
 
+// block 0 also zeroes zsums (kBsiSumWords u64) and zdefer[0] (either may be null)
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
-                     uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile);
-// sums: kBsiMaxInputs + 1 u64 (per-slice |bA[x] & found|, then the found count); null = no sum
+                     uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile, unsigned long long* zsums,
+                     uint32_t* zdefer);
+// sums: kBsiSumWords u64 (per-slice |bA[x] & found|, the found count, then the final (sum, count)
+// written by k_bsi_sum_final); null = no sum
 // scratch of the register-resident compare kernels (bsi.hip), per task of the op
 // (stride = task capacity; the tables are transposed, row-major over the tasks):
 // defer: 1 + stride u32, cnts: 128 x 4 rows of stride ints, kin: 34 rows of stride x 16 B.

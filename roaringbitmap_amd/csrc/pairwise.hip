@@ -488,6 +488,76 @@ __device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
   return r.p;
 }
 
+// ---------------------------------------------------------------------------
+// Direct mode: the compute kernel resolves its tasks itself (no plan launch).  Task t is key
+// key_lo + t; a wave resolves the keys of its next three tasks through the operands' key CSR
+// in a three-stage pipeline of scalar loads (key offsets of task t + 3S, descriptors of
+// t + 2S, run counts of t + S), all issued before task t runs, so no stage waits on the one
+// before it inside a task.  A key without a task (by the op's key rule,
+// RB/RoaringBitmap.java:382-400 and, :864-896 or, :1076-1113 xor, :449-471 andNot) gives an
+// empty record (or a zero count).
+typedef const __attribute__((address_space(4))) uint32_t* CU32p;
+typedef const __attribute__((address_space(4))) uint64_t* CU64p;
+__device__ __forceinline__ uint32_t sld32(const void* p) {
+  return *reinterpret_cast<CU32p>(reinterpret_cast<uintptr_t>(p));
+}
+__device__ __forceinline__ uint64_t sld64(const void* p) {
+  return *reinterpret_cast<CU64p>(reinterpret_cast<uintptr_t>(p));
+}
+struct KeyOff {
+  uint32_t a0, a1, b0, b1;
+};
+struct KeyDesc {
+  uint64_t slot_a, slot_b;
+  uint32_t card_a, card_b;
+  uint8_t kind_a, kind_b;
+};
+__device__ __forceinline__ KeyOff ld_keyoff(const PwDirect& d, uint32_t t) {
+  const uint32_t k = (uint32_t)d.key_lo + t;
+  return KeyOff{sld32(d.koa + k), sld32(d.koa + k + 1), sld32(d.kob + k), sld32(d.kob + k + 1)};
+}
+__device__ __forceinline__ void ld_one_desc(const CDesc* desc, uint32_t p0, uint32_t p1, uint64_t& slot, uint32_t& card,
+                                            uint8_t& kind) {
+  if (p1 > p0) {  // wave-uniform
+    const uint64_t lo = sld64(desc + p0);
+    const uint64_t hi = sld64(reinterpret_cast<const uint8_t*>(desc + p0) + 8);
+    slot = lo;
+    card = (uint32_t)hi;
+    kind = (uint8_t)(hi >> 48);  // CDesc: slot, card, key (u16), kind (u8)
+  } else {
+    slot = 0;
+    card = 0;
+    kind = kAbsent;
+  }
+}
+__device__ __forceinline__ KeyDesc ld_keydesc(const PwDirect& d, const KeyOff& o) {
+  KeyDesc r;
+  ld_one_desc(d.da, o.a0, o.a1, r.slot_a, r.card_a, r.kind_a);
+  ld_one_desc(d.db, o.b0, o.b1, r.slot_b, r.card_b, r.kind_b);
+  return r;
+}
+__device__ __forceinline__ PTask ld_ptask(const KeyDesc& kd, uint32_t key, const uint8_t* pa, const uint8_t* pb) {
+  PTask t;
+  t.slot_a = kd.slot_a;
+  t.slot_b = kd.slot_b;
+  t.card_a = kd.card_a;
+  t.card_b = kd.card_b;
+  t.key = (uint16_t)key;
+  t.kind_a = kd.kind_a;
+  t.kind_b = kd.kind_b;
+  t.nruns_a = kd.kind_a == DK_R ? (uint16_t)(sld32(pa + kd.slot_a) >> 16) : 0;  // slot: [u16 pad][u16 nruns]
+  t.nruns_b = kd.kind_b == DK_R ? (uint16_t)(sld32(pb + kd.slot_b) >> 16) : 0;
+  return t;
+}
+// does key k give a task of op OP (the plan kernel's rule)
+template <int OP>
+__device__ __forceinline__ bool has_task(const PTask& t) {
+  const bool ia = t.kind_a != kAbsent, ib = t.kind_b != kAbsent;
+  if (OP == OP_OR || OP == OP_XOR) return ia || ib;
+  if (OP == OP_ANDNOT) return ia;
+  return ia && ib;
+}
+
 template <int OP, int MODE>
 __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
                                          const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
@@ -504,18 +574,56 @@ __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint
 // and bitmap-class tasks share the launch: separate kernels per class were
 // measured 15 % slower on the C2 mix (tail + an extra dependent index load).
 // MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
-template <int OP, int MODE>
+template <int OP, int MODE, bool DIRECT>
 __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
                                                       const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
-                                                      const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card) {
+                                                      const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card,
+                                                      PwDirect dsrc) {
   __shared__ __align__(16) uint32_t lds_all[kWaves][kWaveLds];
-  const uint32_t nt = uni(*n_tasks);
+  if (DIRECT) {
+    // the plan kernel's other duties: the task count and the op's zeroed look-back state
+    plan_zero(dsrc.zlb, dsrc.ztile);
+    if (blockIdx.x == 0 && threadIdx.x == 0) dsrc.n_tasks_out[0] = dsrc.nkeys;
+  }
+  const uint32_t nt = DIRECT ? dsrc.nkeys : uni(*n_tasks);
   const int w = threadIdx.x >> 6;
   uint32_t* lds = lds_all[w];
   const uint32_t stride = gridDim.x * kWaves;
   const uint32_t t0 = uni(blockIdx.x * kWaves + w);
   if (t0 >= nt) return;
   uint32_t t = t0;
+  if (DIRECT) {
+#if RBG_STAMPS
+    StampAcc sacc = {};
+#endif
+    PTask cur = ld_ptask(ld_keydesc(dsrc, ld_keyoff(dsrc, t)), (uint32_t)dsrc.key_lo + t, pa, pb);
+    KeyDesc kd1{};
+    KeyOff ko2{};
+    if (t + stride < nt) kd1 = ld_keydesc(dsrc, ld_keyoff(dsrc, t + stride));
+    if (t + 2 * stride < nt) ko2 = ld_keyoff(dsrc, t + 2 * stride);
+    for (;;) {
+      const uint32_t tn = t + stride;
+      KeyOff ko3{};
+      KeyDesc kd2{};
+      PTask nxt;
+      if (tn + 2 * stride < nt) ko3 = ld_keyoff(dsrc, tn + 2 * stride);
+      if (tn + stride < nt) kd2 = ld_keydesc(dsrc, ko2);
+      if (tn < nt) nxt = ld_ptask(kd1, (uint32_t)dsrc.key_lo + tn, pa, pb);
+      if (has_task<OP>(cur)) {
+        any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
+      } else if (MODE == 1) {
+        if (lane_id() == 0) task_card[t] = 0;
+      } else {
+        w_place(t, false, nullptr, true, lds, 0, 0, cur.key, DK_A, oc);
+      }
+      if (tn >= nt) break;
+      t = tn;
+      cur = nxt;
+      kd1 = kd2;
+      ko2 = ko3;
+    }
+    return;
+  }
   PTask cur = load_task(tasks, t);
 #if RBG_STAMPS
   StampAcc sacc = {};
@@ -561,9 +669,16 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 
 template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                      const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
-  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE>)));
-  hipLaunchKernelGGL((k_pair_wave<OP, MODE>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card);
+                      const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct) {
+  if (direct) {
+    const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, true>)));
+    hipLaunchKernelGGL((k_pair_wave<OP, MODE, true>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
+                       *direct);
+    return;
+  }
+  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, false>)));
+  hipLaunchKernelGGL((k_pair_wave<OP, MODE, false>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
+                     PwDirect{});
 }
 
 #if RBG_STAMPS
@@ -598,10 +713,10 @@ void launch_plan_pairwise(hipStream_t s, int op, int key_lo, int key_hi, const u
 }
 
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                     const uint8_t* pb, OutCtx oc, uint32_t* task_card) {
-#define RBG_LPW(O)                                                           \
-  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card); \
-  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card);
+                     const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct) {
+#define RBG_LPW(O)                                                                   \
+  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card, direct); \
+  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card, direct);
   switch (op) {
     case OP_AND: RBG_LPW(OP_AND) break;
     case OP_OR: RBG_LPW(OP_OR) break;

@@ -152,6 +152,11 @@ class Engine:
         check(lib().rbg_ctx_bsi_sums(self._ctx, out))
         return int(out[0]), int(out[1])
 
+    def bsi_sums_device(self, dst):
+        """(sum, count) of the last BSI call into a device int64 tensor of two elements, enqueued on
+        the engine stream (no host synchronisation)."""
+        check(lib().rbg_ctx_bsi_sums_device(self._ctx, ctypes.c_void_p(dst.data_ptr())))
+
     def batch_counts(self, batch) -> np.ndarray:
         """containers per input bitmap of a batch"""
         n = self.batch_stats(batch)["bitmaps"]

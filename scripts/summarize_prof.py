@@ -3,6 +3,7 @@
 
 Writes
   profiles/<tag>/kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/<tag>/kernel_stats_<w>.csv  the same for workload w run alone (bench.py --only w)
   profiles/<tag>/bench_kt.json      the bench line printed under the kernel trace
   profiles/<tag>/pmc_summary.json   per-kernel mean counters over the --pmc passes
   profiles/pmc_traffic.json         HBM bytes per launch of each workload's dominant kernel, from
@@ -74,6 +75,10 @@ def main(tag):
     kt = os.path.join(src, "kt", "run_kernel_stats.csv")
     if os.path.exists(kt):
         kernel_stats(kt, os.path.join(dst, "kernel_stats.csv"))
+    for w in WORKLOADS:  # per-workload kernel traces (bench.py --only w)
+        p = os.path.join(src, f"ktw_{w}", "run_kernel_stats.csv")
+        if os.path.exists(p):
+            kernel_stats(p, os.path.join(dst, f"kernel_stats_{w}.csv"))
     if os.path.exists(os.path.join(src, "bench_kt.json")):
         shutil.copy(os.path.join(src, "bench_kt.json"), os.path.join(dst, "bench_kt.json"))
     summary = {}
