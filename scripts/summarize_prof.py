@@ -63,7 +63,8 @@ def counters(path):
 
 
 # workload (bench.py --only) -> (traffic key in pmc_traffic.json, dominant kernel)
-WORKLOADS = {"c2": ("k_pair_wave", "k_pair_wave<0, 0>"), "c2card": ("k_pair_wave_card", "k_pair_wave<0, 1>"),
+WORKLOADS = {"c2": ("k_pair_wave", "k_pair_wave<0, 0, true>"), "c2card": ("k_pair_wave_card", "k_pair_wave<0, 1, true>"),
+             "c2ser": ("k_serialize_c2", "k_serialize"),
              "c3u": ("k_wide<OR>_uniform", "k_wide<0>"), "c3c": ("k_wide<OR>_clustered", "k_wide<0>"),
              "c5": ("k_bsi_reg", "k_bsi_reg")}
 
@@ -75,7 +76,7 @@ def main(tag):
     kt = os.path.join(src, "kt", "run_kernel_stats.csv")
     if os.path.exists(kt):
         kernel_stats(kt, os.path.join(dst, "kernel_stats.csv"))
-    for w in WORKLOADS:  # per-workload kernel traces (bench.py --only w)
+    for w in [x for x in WORKLOADS if x != "c2ser"]:  # per-workload kernel traces (bench.py --only w)
         p = os.path.join(src, f"ktw_{w}", "run_kernel_stats.csv")
         if os.path.exists(p):
             kernel_stats(p, os.path.join(dst, f"kernel_stats_{w}.csv"))
@@ -95,7 +96,7 @@ def main(tag):
     tp = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     traffic = json.load(open(tp)) if os.path.exists(tp) else {}
     for w, (key, kern) in WORKLOADS.items():
-        d = summary.get(w, {}).get(kern, {})
+        d = summary.get(w if w != "c2ser" else "c2", {}).get(kern, {})
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             rd = 2.0 * d["FETCH_SIZE"]["mean"] * 1024
             wr = d["WRITE_SIZE"]["mean"] * 1024
