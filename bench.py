@@ -143,7 +143,13 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
             "result_serialized_bytes": int(total_bytes), "containers_in": st["containers"], "rank0_keys": [lo, hi],
             "roofline_rank0": ({"kernel": "k_wide<OR>", "achieved_GBps": round(ach, 1),
                                 "frac": round(ach / HBM_PEAK_GBS, 4), "kernel_ms": round(kern_ms, 4),
-                                "traffic": _pmc_traffic(tkey)} if op == "or" else
+                                "traffic": _pmc_traffic(tkey),
+                                # the bytes the counters saw (the algorithmic input counts 4 B descriptors
+                                # that the key-major packed kernel never reads)
+                                **({"counter_GBps": round(_pmc_traffic(tkey) / (kern_ms / 1e3) / 1e9, 1),
+                                    "counter_frac": round(_pmc_traffic(tkey) / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                                                          4)} if _pmc_traffic(tkey) and world == 1 else {})}
+                               if op == "or" else
                                {"kernel": "k_wide<AND_SHY>", "kernel_ms": round(kern_ms, 4),
                                 "note": "per key the chain stops at an empty intersection: the bytes read are far "
                                         "below input_bytes, so no roofline fraction is claimed"})}

@@ -786,6 +786,16 @@ __global__ __launch_bounds__(64) void k_bsi_sum_final(unsigned long long* __rest
   }
 }
 
+// (sum, count) to caller memory on the stream: one tiny kernel (a D2D hipMemcpyAsync goes
+// through a blit kernel at ~12 us)
+__global__ __launch_bounds__(64) void k_bsi_sums_out(const unsigned long long* __restrict__ sums,
+                                                     unsigned long long* __restrict__ dst) {
+  if (threadIdx.x < 2) dst[threadIdx.x] = sums[kBsiSumOut + threadIdx.x];
+}
+void launch_bsi_sums_out(hipStream_t s, const unsigned long long* sums, void* dst) {
+  hipLaunchKernelGGL(k_bsi_sums_out, dim3(1), dim3(64), 0, s, sums, reinterpret_cast<unsigned long long*>(dst));
+}
+
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
                 unsigned long long* sums, BsiScratch* sc) {
   if (p.op <= BSI_RANGE && p.nbits <= kBsiRegSlices && sc) {

@@ -1725,8 +1725,8 @@ int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2) {
 int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2) {
   if (!dst2 || !ctx->c.bsi_sums.p) return RBG_ERR_ILLEGAL_ARGUMENT;
   HIPCHK(hipSetDevice(ctx->c.device));
-  HIPCHK(hipMemcpyAsync(dst2, ctx->c.bsi_sums.as<uint64_t>() + kBsiSumOut, 16, hipMemcpyDeviceToDevice,
-                        ctx->c.stream));
+  launch_bsi_sums_out(ctx->c.stream, ctx->c.bsi_sums.as<unsigned long long>(), dst2);
+  HIPCHK(hipGetLastError());
   return RBG_OK;
 }
 static int bsi_load(Ctx* c, const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* lens,

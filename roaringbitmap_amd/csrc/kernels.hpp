@@ -267,6 +267,7 @@ struct BsiScratch {
   size_t stride;
   void* table;  // 34 x 16 B per task: each input's container of the key
 };
+void launch_bsi_sums_out(hipStream_t s, const unsigned long long* sums, void* dst);  // 2 x u64 at kBsiSumOut
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
                 unsigned long long* sums, BsiScratch* sc);
 

@@ -847,16 +847,19 @@ __device__ __forceinline__ uint64_t lb_pack(uint64_t st, uint64_t run, uint64_t 
 }
 
 
-// n bytes from src to dst (even addresses, n even), one wave.  The destination body is
+// n bytes from src to dst (any addresses), one wave.  The destination body is
 // written as aligned 16 B vectors; each is the 16 bytes at `shift` (the source's offset
 // from 16 B alignment at that point) inside two consecutive aligned source vectors: lane l
 // loads aligned source vector i, takes vector i + 1 from lane l + 1 (a DPP lane shift;
 // lane 63 from the next group's lane 0) and funnel-shifts the pair (alignbyte).  So every
 // load and store is a coalesced 16 B access, 8 per lane in flight.  The unaligned head and
-// tail go as u16.  Reads up to 16 bytes past the end of src (slots and payload arenas carry
+// tail (< 16 bytes each) go as u16, or as bytes when an address is odd: a key shard's payload
+// lands at an odd offset of the global bitmap whenever the header size is odd.  Reads up to 16 bytes past the end of src
+// (slots and payload arenas carry
 // slack).  The pointers come from memory (records, the state header), so they are generic
 // to the compiler: the accesses go through global-address-space types (flat instructions
 // would also count against lgkmcnt).
+typedef __attribute__((address_space(1))) uint8_t g_u8;
 typedef __attribute__((address_space(1))) uint16_t g_u16;
 typedef __attribute__((address_space(1))) uint32_t g_u32;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -878,7 +881,7 @@ __device__ __forceinline__ u32x4 lane0_vec(u32x4 v) {
   r.w = lane0u(v.w);
   return r;
 }
-// the 16 bytes at byte offset 4q + r (q wave-uniform, r in {0, 2}) of the 32-byte pair (a, b)
+// the 16 bytes at byte offset 4q + r (q, r wave-uniform, r < 4) of the 32-byte pair (a, b)
 __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t q, uint32_t r) {
   u32x4 o;
   if (q == 0) {
@@ -910,13 +913,13 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 a, u32x4 b, uint32_t q, uint32_t
 __device__ __forceinline__ void st_out(g_u32x4* p, const u32x4& v) { __builtin_nontemporal_store(v, p); }
 
 struct CopyJob {
-  const g_u16* s16;
-  g_u16* d16;
+  const g_u8* s8;
+  g_u8* d8;
   const g_u32x4* sv;  // aligned source vectors
   g_u32x4* dv;        // aligned destination body
   uint32_t n, head, nvec, shift;
 };
-// the unaligned head (u16 by the first lanes) and the body's geometry
+// the unaligned head (bytes, by the first lanes) and the body's geometry
 __device__ __forceinline__ CopyJob copy_begin(uint8_t* dst, const uint8_t* src, uint32_t n) {
   const int l = lane_id();
   CopyJob j;
@@ -924,11 +927,15 @@ __device__ __forceinline__ CopyJob copy_begin(uint8_t* dst, const uint8_t* src, 
   j.head = (uint32_t)((16 - (d & 15)) & 15);
   if (j.head > n) j.head = n;
   j.n = n;
-  j.s16 = (const g_u16*)src;
-  j.d16 = (g_u16*)dst;
-  if (l < (int)(j.head >> 1)) j.d16[l] = j.s16[l];
+  j.s8 = (const g_u8*)src;
+  j.d8 = (g_u8*)dst;
+  if (((d | reinterpret_cast<uintptr_t>(src)) & 1) == 0) {  // even addresses (every slot): u16
+    if (l < (int)(j.head >> 1)) ((g_u16*)j.d8)[l] = ((const g_u16*)j.s8)[l];
+  } else if (l < (int)j.head) {
+    j.d8[l] = j.s8[l];
+  }
   const uintptr_t s = reinterpret_cast<uintptr_t>(src + j.head);
-  j.shift = (uint32_t)(s & 15);  // even
+  j.shift = (uint32_t)(s & 15);
   j.sv = (const g_u32x4*)(s - j.shift);
   j.dv = (g_u32x4*)(dst + j.head);
   j.nvec = (n - j.head) >> 4;
@@ -976,8 +983,14 @@ __device__ __forceinline__ void copy_store(const CopyJob& j, uint32_t i0, const 
   }
 }
 __device__ __forceinline__ void copy_tail(const CopyJob& j) {
-  const uint32_t done = j.head + (j.nvec << 4);
-  for (uint32_t i = (done >> 1) + lane_id(); i < (j.n >> 1); i += 64) j.d16[i] = j.s16[i];
+  const uint32_t done = j.head + (j.nvec << 4);  // fewer than 16 bytes remain
+  if (((reinterpret_cast<uintptr_t>(j.d8) | reinterpret_cast<uintptr_t>(j.s8) | j.n) & 1) == 0) {
+    const uint32_t i = (done >> 1) + (uint32_t)lane_id();
+    if (i < (j.n >> 1)) ((g_u16*)j.d8)[i] = ((const g_u16*)j.s8)[i];
+  } else {
+    const uint32_t i = done + (uint32_t)lane_id();
+    if (i < j.n) j.d8[i] = j.s8[i];
+  }
 }
 __device__ __forceinline__ void w_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
   const CopyJob j = copy_begin(dst, src, n);

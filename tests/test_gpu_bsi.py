@@ -108,3 +108,12 @@ def test_c5_synthetic_bsi(gpu):
     assert e.fetch().serialize() == exp
     assert e.bsi_sums() == o.sum(exp)
     assert o.sum(exp)[0] == int(v[(v >= lo) & (v <= hi)].sum())
+    # the same (sum, count) copied to device memory on the engine stream (the bench's all-reduce input)
+    import torch
+    d = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    e.bsi_sums_device(d)
+    e.sync()
+    assert (int(d[0]), int(d[1])) == o.sum(exp)
+    # a compare without want_sum leaves (0, 0)
+    e.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=False)
+    assert e.bsi_sums() == (0, 0)

@@ -113,3 +113,33 @@ def test_c3_synthetic_matches_oracle(gpu, kind):
 def shard_key_bytes(kind, n):
     from roaringbitmap_amd.engine import synth_key_bytes
     return synth_key_bytes(kind, 0xC3000000, n)
+
+
+@pytest.mark.parametrize("case", ["wide_or", "run_and"])
+def test_same_device_assembly(gpu, case):
+    """shard.assemble with the fill and the output on the same GPU (the bench's RCCL path at rank 0):
+    the engine writes descriptors, offsets, run-flag bytes and payload straight into views of the
+    output tensor on its own stream.  run_and: a pairwise AND of run-container bitmaps, so the
+    result holds run containers and the run-flag bitset must survive (no zero fill racing the
+    engine's writes)."""
+    import torch
+    e = _engine()
+    if case == "wide_or":
+        batch = e.synth(1, 0xC3000000, 24, 0, 2048)
+        e.wide("or", batch)
+    else:
+        rng = np.random.default_rng(77)
+        keys = np.sort(rng.choice(65536, size=300, replace=False))
+        a = _gen.bitmap(rng, keys, modes=["r_few", "r_mid", "r_many", "a_mid", "b_mid"], p_present=0.95)
+        b = _gen.bitmap(rng, keys, modes=["r_few", "r_mid", "r_many", "a_mid", "b_mid"], p_present=0.95)
+        ba, bb = e.load([a]), e.load([b])
+        e.pairwise("and", ba, bb)
+    rs = e.result_stats()
+    lay = shard.GlobalLayout([[rs["containers"], rs["payload_bytes"], int(rs["has_run"])]])
+    out = shard.assemble(shard.engine_fill(e), lay, 0, fill_device="cuda:0", comm_device="cuda:0", sync=e.sync)
+    torch.cuda.synchronize()
+    got = bytes(out.cpu().numpy().tobytes())
+    assert got == e.fetch().serialize()
+    if case == "run_and":
+        assert rs["has_run"]
+        assert got == O.pairwise("and", a, b)
