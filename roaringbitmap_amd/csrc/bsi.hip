@@ -322,9 +322,10 @@ __device__ __forceinline__ void rec1(uint64_t z, int k, uint8_t* rows) {
   rows[k * kRowB + threadIdx.x] = (uint8_t)popc64(z);
 }
 // row sums of rows [0, nk), one thread per row (16 B reads, v_dot4 over the bytes),
-// written as this unit's partial counts: cnt[(row * kBsiUnits + unit) * stride].
+// written as this unit's partial counts: cnt[row], contiguous (one coalesced store per
+// wave; a transposed layout made each count a scattered 4 B write).
 // Begins and ends with a barrier.
-__device__ __forceinline__ void sum_rows_unit(const uint8_t* rows, int nk, int* cnt, size_t stride) {
+__device__ __forceinline__ void sum_rows_unit(const uint8_t* rows, int nk, int* cnt) {
   lds_barrier();
   const int r = threadIdx.x;
   if (r < nk) {
@@ -338,7 +339,7 @@ __device__ __forceinline__ void sum_rows_unit(const uint8_t* rows, int nk, int* 
       c = __builtin_amdgcn_udot4(x.z, 0x01010101u, c, false);
       c = __builtin_amdgcn_udot4(x.w, 0x01010101u, c, false);
     }
-    cnt[(size_t)r * kBsiUnits * stride] = (int)c;
+    cnt[r] = (int)c;
   }
   lds_barrier();
 }
@@ -490,9 +491,9 @@ __device__ __forceinline__ uint64_t in_word(uint64_t slot, uint32_t card_kind, i
   return mat_unit_word(A.desc[didx], A.payload, lds, q, w);
 }
 
-// compare ops (BSI_EQ .. BSI_RANGE) with nbits <= kBsiRegSlices.  cnts: per count row,
-// kBsiUnits partial rows of one int per task; kin: kBsiKin rows of one input type per
-// task (slices, ebM, the fixed found set); both transposed with row stride `tstride`.
+// compare ops (BSI_EQ .. BSI_RANGE) with nbits <= kBsiRegSlices.  cnts: per task and unit,
+// kBsiCnt partial counts (one per count row); kin: per task, kBsiKin input types (slices,
+// ebM, the fixed found set), contiguous.
 __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tasks,
                                                                 const uint32_t* __restrict__ n_tasks,
                                                  WideArgs A, BsiArgs P, OutCtx oc, bool want_sum,
@@ -613,12 +614,12 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
     // this unit's result words to the task's scratch slot (the container itself when
     // it is a bitmap, else the input k_bsi_defer stages it from)
     reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[w] = res;
-    sum_rows_unit(rows, want_sum ? kRowSum + nb : kRowSum, cnts + (size_t)u * tstride + t, tstride);
+    sum_rows_unit(rows, want_sum ? kRowSum + nb : kRowSum, cnts + ((size_t)t * kBsiUnits + u) * kBsiCnt);
     if (u == 0 && tid < kBsiKin) {  // the key's input types, for k_bsi_types
       const int i = tid == kBsiRegSlices ? 0 : tid == kBsiRegSlices + 1 ? (P.has_found ? nb + 1 : 0) : 1 + tid;
       const BsiIn x = table[(size_t)t * kBsiKin + (i < kBsiKin ? i : 0)];
       const bool present = x.didx >= 0 && (tid >= kBsiRegSlices || tid < nb);
-      kin[(size_t)tid * tstride + t] =
+      kin[(size_t)t * kBsiKin + tid] =
           present ? TB{(int)(x.card_kind >> 24), (int)(x.card_kind & 0xFFFFFF), x.didx, 0} : tb_absent();
     }
     if (wn >= nunits) break;
@@ -651,20 +652,31 @@ __global__ __launch_bounds__(256) void k_bsi_types(const Task* __restrict__ task
   const int nb = P.nbits;
   const bool two = P.op == BSI_RANGE;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t ts = blockIdx.x * 64 + lane;  // staging: lane = key of the block
   if (uni(blockIdx.x * 64) >= nt) return;
-  const uint32_t tt = ts < nt ? ts : 0;
-  // the block's four waves stage the 64 keys' rows (every fourth row each: four times
-  // the loads in flight of a lone wave)
+  // the block stages the 64 keys' counts: each key's units wrote their rows contiguously
+  // (cnts[(task * kBsiUnits + unit) * kBsiCnt + row]), so a half-block reads one key's
+  // rows coalesced (thread = row) and adds the units' partials
+  {
+    const int r = threadIdx.x & (kBsiCnt - 1), half = threadIdx.x >> 7;
+    static_assert(2 * kBsiCnt == NT, "two keys per block pass");
 #pragma unroll 4
-  for (int r = wv; r < kBsiRows; r += 4) {
-    int c = 0;
+    for (int j = half; j < 64; j += 2) {
+      const uint32_t tj = blockIdx.x * 64 + j;
+      if (r < kBsiRows && tj < nt) {
+        const int* row = cnts + (size_t)tj * kBsiUnits * kBsiCnt + r;
+        int c = 0;
 #pragma unroll
-    for (int u = 0; u < kBsiUnits; u++) c += cnts[((size_t)r * kBsiUnits + u) * tstride + tt];
-    lc[r * 64 + lane] = c;
+        for (int u = 0; u < kBsiUnits; u++) c += row[u * kBsiCnt];
+        lc[r * 64 + j] = c;
+      }
+    }
   }
-#pragma unroll 4
-  for (int i = wv; i < kBsiKin; i += 4) lk[i * 64 + lane] = kin[(size_t)i * tstride + tt];
+  // the 64 keys' input types: kBsiKin contiguous entries per key, read coalesced
+  for (int x = threadIdx.x; x < 64 * kBsiKin; x += NT) {
+    const int j = x / kBsiKin, i = x - j * kBsiKin;
+    const uint32_t tj = blockIdx.x * 64 + j;
+    if (tj < nt) lk[i * 64 + j] = kin[(size_t)tj * kBsiKin + i];
+  }
   __syncthreads();
   // replay: 16 keys per wave, all four waves (the type chain is serial per key, so
   // four times the waves of a key-per-lane replay finish about four times sooner)
