@@ -127,8 +127,8 @@ __device__ __forceinline__ void write_cookie(uint8_t* base, uint32_t size, uint3
 
 // One wave per task record (grid-stride): a kept result's payload bytes go to their offset
 // (w_copy: aligned 16 B loads and stores, the source's misalignment funnel-shifted in
-// registers), and lane 0 writes its descriptor (key, card - 1) and offset-table entry --
-// both tables are 4 B aligned (they end at payload_base).  Threads below the flag-byte
+// registers); one thread per record writes its descriptor (key, card - 1) and offset-table
+// entry -- both tables are 4 B aligned (they end at payload_base).  Threads below the flag-byte
 // count pack the run-flag bitset from k_place's kind-by-output bytes; thread 0 writes the
 // cookie.
 __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ n_tasks, OutCtx oc,
@@ -154,6 +154,15 @@ __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ 
     }
   }
   if (gid == 0) write_cookie(base, size, has_run);
+  // descriptors and offsets by thread (record i -> its output index): neighbouring threads
+  // write neighbouring entries, so the stores coalesce (written by each task's copying wave
+  // they were scattered 4 B stores: serialize 0.107 -> 0.105 ms)
+  for (uint32_t i = gid; i < nt; i += gridDim.x * blockDim.x) {
+    const ORec r = oc.recs[i];
+    if (!r.keep) continue;
+    *(g_u32*)(base + desc_base + 4ull * r.idx) = (uint32_t)r.key | ((r.card - 1) << 16);
+    if (offsets) *(g_u32*)(base + off_base + 4ull * r.idx) = (uint32_t)(H + r.off);
+  }
   uint8_t* pay = oc.out + oc.payload_base;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
   for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
@@ -161,11 +170,6 @@ __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ 
     if (!uni(r.keep)) continue;
     const uint64_t off = uni64(r.off);
     w_copy(pay + off, reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
-    if (lane_id() == 0) {
-      const uint32_t idx = r.idx;
-      *(g_u32*)(base + desc_base + 4ull * idx) = (uint32_t)r.key | ((r.card - 1) << 16);
-      if (offsets) *(g_u32*)(base + off_base + 4ull * idx) = (uint32_t)(H + off);
-    }
   }
 }
 
