@@ -654,28 +654,66 @@ __global__ __launch_bounds__(256) void k_bsi_types(const Task* __restrict__ task
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (uni(blockIdx.x * 64) >= nt) return;
   // the block stages the 64 keys' counts: each key's units wrote their rows contiguously
-  // (cnts[(task * kBsiUnits + unit) * kBsiCnt + row]), so a half-block reads one key's
-  // rows coalesced (thread = row) and adds the units' partials
+  // (cnts[(task * kBsiUnits + unit) * kBsiCnt + row]); a thread takes four rows of a key as
+  // 16 B, adds the units' partials, and every thread's loads are issued at once (one round
+  // trip for the block)
   {
-    const int r = threadIdx.x & (kBsiCnt - 1), half = threadIdx.x >> 7;
-    static_assert(2 * kBsiCnt == NT, "two keys per block pass");
-#pragma unroll 4
-    for (int j = half; j < 64; j += 2) {
-      const uint32_t tj = blockIdx.x * 64 + j;
-      if (r < kBsiRows && tj < nt) {
-        const int* row = cnts + (size_t)tj * kBsiUnits * kBsiCnt + r;
-        int c = 0;
+    constexpr int kQuads = (kBsiRows + 3) / 4;
+    constexpr int kIt = (64 * kQuads + NT - 1) / NT;
+    static_assert(kBsiCnt % 4 == 0 && 4 * kQuads <= kBsiCnt, "row quads");
+    int4 acc[kIt];
 #pragma unroll
-        for (int u = 0; u < kBsiUnits; u++) c += row[u * kBsiCnt];
-        lc[r * 64 + j] = c;
+    for (int it = 0; it < kIt; it++) {  // every load first
+      const int x = it * NT + (int)threadIdx.x;
+      const int j = x / kQuads, q = x - j * kQuads;
+      const uint32_t tj = blockIdx.x * 64 + j;
+      acc[it] = make_int4(0, 0, 0, 0);
+      if (x < 64 * kQuads && tj < nt) {
+        const int4* p = reinterpret_cast<const int4*>(cnts + (size_t)tj * kBsiUnits * kBsiCnt) + q;
+#pragma unroll
+        for (int u = 0; u < kBsiUnits; u++) {
+          const int4 v = p[u * (kBsiCnt / 4)];
+          acc[it].x += v.x;
+          acc[it].y += v.y;
+          acc[it].z += v.z;
+          acc[it].w += v.w;
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; it++) {
+      const int x = it * NT + (int)threadIdx.x;
+      const int j = x / kQuads, r = 4 * (x - j * kQuads);
+      if (x < 64 * kQuads) {
+        lc[r * 64 + j] = acc[it].x;
+        if (r + 1 < kBsiRows) lc[(r + 1) * 64 + j] = acc[it].y;
+        if (r + 2 < kBsiRows) lc[(r + 2) * 64 + j] = acc[it].z;
+        if (r + 3 < kBsiRows) lc[(r + 3) * 64 + j] = acc[it].w;
       }
     }
   }
-  // the 64 keys' input types: kBsiKin contiguous entries per key, read coalesced
-  for (int x = threadIdx.x; x < 64 * kBsiKin; x += NT) {
-    const int j = x / kBsiKin, i = x - j * kBsiKin;
-    const uint32_t tj = blockIdx.x * 64 + j;
-    if (tj < nt) lk[i * 64 + j] = kin[(size_t)tj * kBsiKin + i];
+  // the 64 keys' input types: kBsiKin contiguous entries per key, read coalesced, every load
+  // issued before the first LDS store
+  {
+    constexpr int kIt = (64 * kBsiKin + NT - 1) / NT;
+    static_assert(sizeof(TB) == sizeof(int4), "TB as 16 B");
+    int4 v[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; it++) {
+      const int x = it * NT + (int)threadIdx.x;
+      const int j = x / kBsiKin;
+      const uint32_t tj = blockIdx.x * 64 + j;
+      v[it] = make_int4(0, 0, 0, 0);
+      if (x < 64 * kBsiKin && tj < nt)
+        v[it] = reinterpret_cast<const int4*>(kin)[(size_t)tj * kBsiKin + (x - j * kBsiKin)];
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; it++) {
+      const int x = it * NT + (int)threadIdx.x;
+      const int j = x / kBsiKin;
+      if (x < 64 * kBsiKin && blockIdx.x * 64 + j < nt)
+        reinterpret_cast<int4*>(lk)[(x - j * kBsiKin) * 64 + j] = v[it];
+    }
   }
   __syncthreads();
   // replay: 16 keys per wave, all four waves (the type chain is serial per key, so
