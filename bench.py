@@ -201,6 +201,39 @@ def c2_key_sharded(eng, rank, world, dist, steps, warmup, cdev, in_bytes):
             "rank0_keys": [lo, hi], "scaling": "strong"}
 
 
+def c2_two_streams(eng, a, b, in_bytes, steps, warmup):
+    """The headline op (RoaringBitmap.and + serialization) as a stream of independent calls on two
+    engine contexts, alternating: each context has its own HIP stream and device state."""
+    import torch
+    from roaringbitmap_amd import Engine
+    e2 = Engine(torch.cuda.current_device())
+    try:
+        a2 = e2.synth(0, 0xC2A0 + 0x10000 * int(os.environ.get("RANK", "0")))
+        b2 = e2.synth(0, 0xC2B0 + 0x10000 * int(os.environ.get("RANK", "0")))
+        ctx = [(eng, a, b), (e2, a2, b2)]
+        for i in range(warmup * 2):
+            e, x, y = ctx[i % 2]
+            e.pairwise("and", x, y)
+            e.serialize()
+        eng.sync()
+        e2.sync()
+        t0 = time.perf_counter()
+        for i in range(2 * steps):
+            e, x, y = ctx[i % 2]
+            e.pairwise("and", x, y)
+            e.serialize()
+        eng.sync()
+        e2.sync()
+        dt = (time.perf_counter() - t0) / (2 * steps)
+        e2.release(a2)
+        e2.release(b2)
+    finally:
+        e2.close()
+    return {"workload": "C2 RoaringBitmap.and + serialization, independent calls alternating on two engine contexts "
+                        "(two HIP streams)", "ms_per_op": round(dt * 1e3, 4),
+            "input_GBps": round(in_bytes / dt / 1e9, 1)}
+
+
 def c4_batch_and_card(eng, n_pairs, rank, world, dist, steps, warmup, cdev):
     """C4: batched andCardinality of n_pairs small sparse pairs per rank (weak scaling)."""
     import torch
@@ -617,6 +650,10 @@ def main():
                      "frac": round(in_bytes / (card_kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": _pmc_traffic("k_pair_wave_card")}}
     ks = max(3, args.steps // 4)
+    # a stream of independent C2 ANDs issued alternately on two engine contexts (two HIP streams):
+    # one op's serialization overlaps the next op's compute (throughput of concurrent calls, as a
+    # server would issue them; the headline above is one call after another)
+    run_extra("c2_and_two_streams", lambda: c2_two_streams(eng, a, b, in_bytes, args.steps, args.warmup))
     if world > 1:  # the engine's own key split of one pair, beside the weak-scaling headline
         run_extra("c2_and_key_sharded", lambda: c2_key_sharded(eng, rank, world, dist, ks, 1, cdev, in_bytes))
     if args.c3_n > 0:
