@@ -19,7 +19,7 @@ if [[ " $PASSES " == *" kt "* ]]; then
 fi
 if [[ " $PASSES " == *" ktw "* ]]; then
   # each workload alone under the kernel trace: per-workload kernel_stats (bench.py --only W)
-  for W in c2 c2card c3u c3c c5; do
+  for W in c2 c2card c3u c3c c4 c5; do
     timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktw_$W -o run -- python3 bench.py --only $W --steps 10 --warmup 2 > $OUT/only_kt_$W.json 2> $OUT/ktw_$W.err || { echo "ktw $W failed"; tail $OUT/ktw_$W.err; exit 1; }
     echo "ktw $W done"
   done

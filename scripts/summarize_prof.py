@@ -64,7 +64,7 @@ def counters(path):
 
 # workload (bench.py --only) -> (traffic key in pmc_traffic.json, dominant kernel)
 WORKLOADS = {"c2": ("k_pair_wave", "k_pair_wave<0, 0, true>"), "c2card": ("k_pair_wave_card", "k_pair_wave<0, 1, true>"),
-             "c2ser": ("k_serialize_c2", "k_serialize"),
+             "c2ser": ("k_serialize_c2", "k_serialize"), "c4": ("k_pair_items", "k_pair_items"),
              "c3u": ("k_wide<OR>_uniform", "k_wide<0>"), "c3c": ("k_wide<OR>_clustered", "k_wide<0>"),
              "c5": ("k_bsi_reg", "k_bsi_reg")}
 
