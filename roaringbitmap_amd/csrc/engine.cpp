@@ -187,7 +187,9 @@ static int ctx_init(Ctx* c, int device) {
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   CHK(c->by_key.ensure(sizeof(PTask) * kMaxKeys));  // Task (wide) or PTask (pairwise) records
   CHK(c->flag.ensure(kMaxKeys));
-  CHK(c->tasks.ensure(sizeof(PTask) * kMaxKeys));
+  // (+ 32768: the pairwise direct mode lays its tasks out wave-major in regions of a multiple of
+  // 4 records, at most 4 per resident wave (<= 8192 waves) past the task count)
+  CHK(c->tasks.ensure(sizeof(PTask) * (kMaxKeys + 32768)));
   CHK(c->ntasks.ensure(64));
   CHK(c->wg_count.ensure(4 * 256));
   CHK(c->wg_epoch.ensure(8 * 256));

@@ -490,65 +490,9 @@ __device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
 
 // ---------------------------------------------------------------------------
 // Direct mode: the compute kernel resolves its tasks itself (no plan launch).  Task t is key
-// key_lo + t; a wave resolves the keys of its next three tasks through the operands' key CSR
-// in a three-stage pipeline of scalar loads (key offsets of task t + 3S, descriptors of
-// t + 2S, run counts of t + S), all issued before task t runs, so no stage waits on the one
-// before it inside a task.  A key without a task (by the op's key rule,
+// key_lo + t (see k_pair_wave).  A key without a task (by the op's key rule,
 // RB/RoaringBitmap.java:382-400 and, :864-896 or, :1076-1113 xor, :449-471 andNot) gives an
 // empty record (or a zero count).
-typedef const __attribute__((address_space(4))) uint32_t* CU32p;
-typedef const __attribute__((address_space(4))) uint64_t* CU64p;
-__device__ __forceinline__ uint32_t sld32(const void* p) {
-  return *reinterpret_cast<CU32p>(reinterpret_cast<uintptr_t>(p));
-}
-__device__ __forceinline__ uint64_t sld64(const void* p) {
-  return *reinterpret_cast<CU64p>(reinterpret_cast<uintptr_t>(p));
-}
-struct KeyOff {
-  uint32_t a0, a1, b0, b1;
-};
-struct KeyDesc {
-  uint64_t slot_a, slot_b;
-  uint32_t card_a, card_b;
-  uint8_t kind_a, kind_b;
-};
-__device__ __forceinline__ KeyOff ld_keyoff(const PwDirect& d, uint32_t t) {
-  const uint32_t k = (uint32_t)d.key_lo + t;
-  return KeyOff{sld32(d.koa + k), sld32(d.koa + k + 1), sld32(d.kob + k), sld32(d.kob + k + 1)};
-}
-__device__ __forceinline__ void ld_one_desc(const CDesc* desc, uint32_t p0, uint32_t p1, uint64_t& slot, uint32_t& card,
-                                            uint8_t& kind) {
-  if (p1 > p0) {  // wave-uniform
-    const uint64_t lo = sld64(desc + p0);
-    const uint64_t hi = sld64(reinterpret_cast<const uint8_t*>(desc + p0) + 8);
-    slot = lo;
-    card = (uint32_t)hi;
-    kind = (uint8_t)(hi >> 48);  // CDesc: slot, card, key (u16), kind (u8)
-  } else {
-    slot = 0;
-    card = 0;
-    kind = kAbsent;
-  }
-}
-__device__ __forceinline__ KeyDesc ld_keydesc(const PwDirect& d, const KeyOff& o) {
-  KeyDesc r;
-  ld_one_desc(d.da, o.a0, o.a1, r.slot_a, r.card_a, r.kind_a);
-  ld_one_desc(d.db, o.b0, o.b1, r.slot_b, r.card_b, r.kind_b);
-  return r;
-}
-__device__ __forceinline__ PTask ld_ptask(const KeyDesc& kd, uint32_t key, const uint8_t* pa, const uint8_t* pb) {
-  PTask t;
-  t.slot_a = kd.slot_a;
-  t.slot_b = kd.slot_b;
-  t.card_a = kd.card_a;
-  t.card_b = kd.card_b;
-  t.key = (uint16_t)key;
-  t.kind_a = kd.kind_a;
-  t.kind_b = kd.kind_b;
-  t.nruns_a = kd.kind_a == DK_R ? (uint16_t)(sld32(pa + kd.slot_a) >> 16) : 0;  // slot: [u16 pad][u16 nruns]
-  t.nruns_b = kd.kind_b == DK_R ? (uint16_t)(sld32(pb + kd.slot_b) >> 16) : 0;
-  return t;
-}
 // does key k give a task of op OP (the plan kernel's rule)
 template <int OP>
 __device__ __forceinline__ bool has_task(const PTask& t) {
@@ -596,31 +540,47 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 #if RBG_STAMPS
     StampAcc sacc = {};
 #endif
-    PTask cur = ld_ptask(ld_keydesc(dsrc, ld_keyoff(dsrc, t)), (uint32_t)dsrc.key_lo + t, pa, pb);
-    KeyDesc kd1{};
-    KeyOff ko2{};
-    if (t + stride < nt) kd1 = ld_keydesc(dsrc, ld_keyoff(dsrc, t + stride));
-    if (t + 2 * stride < nt) ko2 = ld_keyoff(dsrc, t + 2 * stride);
+    // The wave first resolves all of its tasks at once (lane k: task t0 + k * stride, vector
+    // loads through both key CSRs) into its own region of the task buffer, wave-major, then
+    // runs them with the planned form's one scalar record load per task.  (Resolving each
+    // task through a chain of scalar loads in the loop made every load's result wait at the
+    // loop head: SMEM returns out of order, so any use waits for all of them.)
+    // tasks of the first wave (the most), rounded to 4 records (128 B): no scalar-cache line
+    // holds records of two waves
+    const uint32_t per = (((nt + stride - 1) / stride) + 3) & ~3u;
+    PTask* mine = const_cast<PTask*>(tasks) + (size_t)t0 * per;
+    const int l = lane_id();
+    for (uint32_t k0 = 0; k0 < per; k0 += 64) {
+      const uint32_t k = k0 + (uint32_t)l, tk = t0 + k * stride;
+      if (k < per && tk < nt) {
+        const uint32_t key = (uint32_t)dsrc.key_lo + tk;
+        PTask r;
+        resolve(dsrc.koa, dsrc.da, pa, key, r.slot_a, r.card_a, r.kind_a, r.nruns_a);
+        resolve(dsrc.kob, dsrc.db, pb, key, r.slot_b, r.card_b, r.kind_b, r.nruns_b);
+        r.key = (uint16_t)key;
+        mine[k] = r;
+      }
+    }
+    // the records are read back through the scalar cache (a fresh line per wave region: no
+    // other wave writes it, and the scalar cache holds nothing of it yet)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores are in the L2 the scalar loads read
+    uint32_t k = 0;
+    PTask cur = load_task(mine, 0);
     for (;;) {
       const uint32_t tn = t + stride;
-      KeyOff ko3{};
-      KeyDesc kd2{};
       PTask nxt;
-      if (tn + 2 * stride < nt) ko3 = ld_keyoff(dsrc, tn + 2 * stride);
-      if (tn + stride < nt) kd2 = ld_keydesc(dsrc, ko2);
-      if (tn < nt) nxt = ld_ptask(kd1, (uint32_t)dsrc.key_lo + tn, pa, pb);
+      if (tn < nt) nxt = load_task(mine, k + 1);  // in flight while this task runs
       if (has_task<OP>(cur)) {
         any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
       } else if (MODE == 1) {
-        if (lane_id() == 0) task_card[t] = 0;
+        if (l == 0) task_card[t] = 0;
       } else {
         w_place(t, false, nullptr, true, lds, 0, 0, cur.key, DK_A, oc);
       }
       if (tn >= nt) break;
       t = tn;
+      k++;
       cur = nxt;
-      kd1 = kd2;
-      ko2 = ko3;
     }
     return;
   }
