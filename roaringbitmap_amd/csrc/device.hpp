@@ -108,6 +108,9 @@ struct OutCtx {
   uint64_t* tile_status;  // scan placement: per-tile look-back words
   uint64_t* tile_card;    // scan placement: per-tile result cardinality
   uint8_t* kind_by_out;   // k_place: R / not R per output container (run flags of the serialization)
+  // wide OR: a staged bitmap result of task t is written straight to payload offset 8192 t, its place
+  // whenever every earlier task kept an 8 KiB container (k_spec_fix moves the others to their slot)
+  uint32_t spec;
 };
 
 // Portable-format header bytes for `size` containers (RB/RoaringArray.java:781-790)

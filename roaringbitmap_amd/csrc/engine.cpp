@@ -569,6 +569,7 @@ static int ctx_serialize(Ctx* c) {
   }
   if (c->serialized) return RBG_OK;
   CHK(ensure_placed(c));
+  if (c->pending.spec) launch_spec_fix(c->stream, c->ntasks.as<uint32_t>(), c->pending);
   launch_serialize(c->stream, c->ntasks.as<uint32_t>(), c->pending);
   HIPCHK(hipGetLastError());
   c->serialized = true;
@@ -1009,6 +1010,9 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     OutCtx oc;
     // each result container is staged (<= 8194 B) or a clone of one input container
     CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, card_only));
+    // OR results are bitmaps whenever more than 4096 values survive: write those in place
+    // (8192 t < 8194 ub, inside the payload region)
+    if (!card_only && mode == WIDE_OR) oc.spec = c->pending.spec = 1;
     c->pending_src = {id};
     if (!skip.empty()) {
       CHK(c->skip.ensure(skip.size()));

@@ -169,7 +169,27 @@ __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ 
     const ORec& r = oc.recs[t];
     if (!uni(r.keep)) continue;
     const uint64_t off = uni64(r.off);
-    w_copy(pay + off, reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
+    const uint64_t src = uni64(r.src);
+    if (src == reinterpret_cast<uint64_t>(pay + off)) continue;  // written in place by the op (OutCtx::spec)
+    w_copy(pay + off, reinterpret_cast<const uint8_t*>(src), uni(r.ser_len));
+  }
+}
+
+// After k_place, before the serialization of a result written with OutCtx::spec: a bitmap
+// result written at 8192 t whose placement differs (an earlier task kept fewer bytes or
+// nothing) is moved to its scratch slot, so the serialization's copies into the payload
+// region never overwrite a source they have yet to read.  One wave per task (grid-stride).
+__global__ __launch_bounds__(256) void k_spec_fix(const uint32_t* __restrict__ n_tasks, OutCtx oc) {
+  const uint32_t nt = *n_tasks;
+  const uint8_t* pay = oc.out + oc.payload_base;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
+    const ORec& r = oc.recs[t];
+    const uint64_t at = 8192ull * t;
+    if (!uni(r.keep) || uni64(r.src) != reinterpret_cast<uint64_t>(pay + at) || uni64(r.off) == at) continue;
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+    w_copy(slot, pay + at, 8192);
+    if (lane_id() == 0) oc.recs[t].src = reinterpret_cast<uint64_t>(slot);
   }
 }
 
@@ -477,6 +497,9 @@ void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, cons
 
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info) {
   hipLaunchKernelGGL(k_place, dim3(64), dim3(256), 0, s, nt, oc, info);
+}
+void launch_spec_fix(hipStream_t s, const uint32_t* nt, OutCtx oc) {
+  hipLaunchKernelGGL(k_spec_fix, dim3(std::max(1, resident_grid((const void*)&k_spec_fix))), dim3(256), 0, s, nt, oc);
 }
 void launch_serialize(hipStream_t s, const uint32_t* nt, OutCtx oc) {
   hipLaunchKernelGGL(k_serialize, dim3(std::max(1, resident_grid((const void*)&k_serialize))), dim3(256), 0, s, nt, oc,

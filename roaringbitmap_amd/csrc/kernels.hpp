@@ -236,6 +236,7 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
 // portable serialization (payload copies, descriptors, offsets, run flags,
 // cookie) runs only when the result is fetched
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info);
+void launch_spec_fix(hipStream_t s, const uint32_t* nt, OutCtx oc);
 void launch_serialize(hipStream_t s, const uint32_t* nt, OutCtx oc);
 // key shard of a global bitmap: payloads into payload_dst, 4 B descriptors into desc, global
 // offsets (off0 + local offset) into offs (nullable), one run-flag byte per container into runb (nullable)

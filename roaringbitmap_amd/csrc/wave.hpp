@@ -1011,7 +1011,8 @@ __device__ __forceinline__ void wg_place(uint32_t t, bool keep, const uint8_t* s
   (void)shp;
   uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
   if (keep && staged) {
-    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+    uint8_t* slot = oc.spec && kind == DK_B ? oc.out + oc.payload_base + 8192ull * t
+                                            : oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
     copy_lds_to_global<NT>(slot, stage, len, threadIdx.x);
     srcaddr = reinterpret_cast<uint64_t>(slot);
   }

@@ -188,3 +188,28 @@ def test_wide_many_run_inputs(gpu, n):
     _cmp("workshy_and", bufs)
     for op in ["and", "or"]:
         assert gpu_wide_card(op, bufs) == O.wide_card(op, bufs), op
+
+
+@pytest.mark.parametrize("case", ["all_bitmaps", "array_first", "run_middle", "gap"])
+def test_wide_or_in_place_bitmaps(gpu, case):
+    """Wide OR writes a bitmap result of task t straight to payload offset 8192 t (OutCtx::spec);
+    it is in place only while every earlier key kept an 8 KiB container, else k_spec_fix moves it
+    to its slot before the serialization.  Byte-identical to the oracle in every case."""
+    rb = _rb()
+    rng = np.random.default_rng(7)
+    nk = 40
+    per = [[] for _ in range(6)]
+    for k in range(nk):
+        for i in range(6):
+            if case == "gap" and k == 17:
+                continue  # no input has key 17: no task for it, so the later bitmaps stay in place
+            if case == "array_first" and k == 0:
+                v = rng.choice(65536, 300, replace=False)  # a small array result for key 0
+            elif case == "run_middle" and k == 20:
+                s = int(rng.integers(0, 30000))
+                v = np.arange(s, s + 20000)  # one long run: a run container result
+            else:
+                v = rng.choice(65536, 2000, replace=False)  # six of these: ~11,000 values, a bitmap
+            per[i].append((k << 16) + v)
+    bufs = [rb.RoaringBitmap.from_values(np.concatenate(p), run_optimize=True).serialize() for p in per]
+    _cmp("or", bufs, list(range(6)))
