@@ -1012,7 +1012,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, card_only));
     // OR results are bitmaps whenever more than 4096 values survive: write those in place
     // (8192 t < 8194 ub, inside the payload region)
-    if (!card_only && mode == WIDE_OR) oc.spec = c->pending.spec = 1;
+    if (!card_only && (mode == WIDE_OR || mode == WIDE_LAZY_CHAIN)) oc.spec = c->pending.spec = 1;
     c->pending_src = {id};
     if (!skip.empty()) {
       CHK(c->skip.ensure(skip.size()));
