@@ -741,6 +741,9 @@ def _only(eng, args, rank, world, dist, cdev):
         res = {"only": w, **c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, steps, args.warmup, cdev)}
     elif w == "c5":
         res = {"only": w, **c5_bsi(eng, args.c5_rows, rank, world, dist, steps, args.warmup, cdev)}
+    elif w == "runopt":
+        a = eng.synth(0, 0xC2A0 + 0x10000 * rank)
+        res = {"only": w, **run_optimize_c2(eng, a, eng.batch_stats(a), steps)}
     else:
         raise SystemExit(f"unknown workload {w}")
     if rank == 0:

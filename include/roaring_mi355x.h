@@ -181,6 +181,8 @@ int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, s
  *           [0,64) each, card 16..512 (key_lo / key_hi ignored) */
 int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi,
                   int32_t* batch);
+/* Drops a batch.  Its device buffers (up to 2 GiB per context, none above 1 GiB) are kept for
+ * reuse by later batches of the context and freed with it (rbg_ctx_destroy). */
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch);
 /* RoaringBitmap.runOptimize() (RB/RoaringBitmap.java:2764-2774) applied on the device to
  * every bitmap of a batch; the result is a new batch (same bitmaps, keys and order).

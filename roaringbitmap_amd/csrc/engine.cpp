@@ -68,6 +68,23 @@ static void dbg(hipStream_t s, const char* what) {
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), cap(o.cap) {
+    o.p = nullptr;
+    o.cap = 0;
+  }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    if (this != &o) {
+      if (p) (void)hipFree(p);
+      p = o.p;
+      cap = o.cap;
+      o.p = nullptr;
+      o.cap = 0;
+    }
+    return *this;
+  }
   ~DevBuf() {
     if (p) (void)hipFree(p);
   }
@@ -135,6 +152,11 @@ struct Ctx {
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   DevBuf order;                     // horizontal_*: chain order of every key segment
+  DevBuf ro_info, ro_size, ro_part, ro_flags;  // runOptimize scratch (kept: no allocation per call)
+  // device buffers of released batches kept for the next batch of a similar size (hipMalloc /
+  // hipFree of a 0.36 GB payload cost more than runOptimize's kernels); bounded by kPoolMax
+  std::vector<DevBuf> pool;
+  size_t pool_bytes = 0;
   int bsi_nbits = 0;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw,
       scalar, scratch;
@@ -241,6 +263,41 @@ static int32_t new_batch(Ctx* c) {
     }
   c->batches.emplace_back(new Batch());
   return (int32_t)(c->batches.size() - 1);
+}
+
+constexpr size_t kPoolMax = 2ull << 30;    // bytes of released buffers a context keeps
+constexpr size_t kPoolMaxBuf = 1ull << 30;  // larger buffers are freed at once
+
+// a released batch buffer into the context's pool (the stream is idle: rbg_ctx_release syncs)
+static void pool_put(Ctx* c, DevBuf& b) {
+  if (!b.p) return;
+  if (b.cap > kPoolMaxBuf) {
+    b = DevBuf();
+    return;
+  }
+  while (!c->pool.empty() && c->pool_bytes + b.cap > kPoolMax) {  // oldest first
+    c->pool_bytes -= c->pool.front().cap;
+    c->pool.erase(c->pool.begin());
+  }
+  c->pool_bytes += b.cap;
+  c->pool.push_back(std::move(b));
+}
+
+// dst sized for `bytes`: the smallest pooled buffer that holds it (at most twice as large),
+// else a fresh allocation
+static int pool_take(Ctx* c, DevBuf& dst, size_t bytes) {
+  if (dst.p && dst.cap >= bytes) return RBG_OK;
+  size_t best = c->pool.size();
+  for (size_t i = 0; i < c->pool.size(); i++) {
+    const size_t cap = c->pool[i].cap;
+    if (cap >= bytes && cap <= 2 * bytes + (1u << 20) && (best == c->pool.size() || cap < c->pool[best].cap))
+      best = i;
+  }
+  if (best == c->pool.size()) return dst.ensure(bytes);
+  c->pool_bytes -= c->pool[best].cap;
+  dst = std::move(c->pool[best]);
+  c->pool.erase(c->pool.begin() + (std::ptrdiff_t)best);
+  return RBG_OK;
 }
 
 // drops the listed batches on scope exit
@@ -1509,6 +1566,7 @@ int rbg_ctx_release(rbg_ctx* ctx, int32_t batch) {
       std::find(c.pending_src.begin(), c.pending_src.end(), batch) != c.pending_src.end())
     CHK(ctx_serialize(&c));
   HIPCHK(hipStreamSynchronize(c.stream));
+  for (DevBuf* d : {&b->keys, &b->desc, &b->bm, &b->key_off, &b->bm_off, &b->payload}) pool_put(&c, *d);
   c.batches[batch].reset();
   return RBG_OK;
 }
@@ -2178,8 +2236,8 @@ static int synth_c5(Ctx* c, uint64_t seed, size_t rows, int key_lo, int key_hi, 
 // RoaringBitmap.runOptimize (RB/RoaringBitmap.java:2764-2774) over every bitmap of a
 // batch, into a new batch: plan (new kind + slot size per container), scan of the
 // slot sizes, write.  answers[i] = 1 iff bitmap i holds a run container afterwards.
-static int copy_dev(DevBuf& dst, const DevBuf& src, hipStream_t s) {
-  CHK(dst.ensure(src.cap));
+static int copy_dev(Ctx* c, DevBuf& dst, const DevBuf& src, hipStream_t s) {
+  CHK(pool_take(c, dst, src.cap));
   if (src.cap) HIPCHK(hipMemcpyAsync(dst.p, src.p, src.cap, hipMemcpyDeviceToDevice, s));
   return RBG_OK;
 }
@@ -2193,27 +2251,49 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
   }
   hipStream_t s = c->stream;
   const size_t C = a->n_ctr, n = a->n_bm;
-  DevBuf info, size, part, flags;
-  CHK(info.ensure(4 * C + 16));
-  CHK(size.ensure(8 * C + 16));
-  CHK(part.ensure(8 * (scan_parts(C) + 1)));
-  CHK(flags.ensure(4 * n + 16));
+  CHK(c->ro_info.ensure(4 * C + 16));
+  CHK(c->ro_size.ensure(8 * C + 16));
+  CHK(c->ro_part.ensure(8 * (scan_parts(C) + 1)));
+  CHK(c->ro_flags.ensure(4 * n + 16));
   CHK(c->scalar.ensure(64));
-  HIPCHK(hipMemsetAsync(flags.p, 0, 4 * n + 16, s));
+  // the new batch's buffers before any kernel: a conversion only happens when the new form is
+  // smaller, and its 16 B-rounded slot is no larger either, so the input's payload size bounds
+  // the output's -- plan, scan and write then run back to back with one host sync at the end
+  const int32_t bid = new_batch(c);
+  Batch& b = *c->batches[bid];
+  struct Drop {  // an error below frees the half-built batch
+    Ctx* c;
+    int32_t id;
+    bool keep = false;
+    ~Drop() {
+      if (!keep) c->batches[id].reset();
+    }
+  } drop{c, bid};
+  CHK(pool_take(c, b.desc, sizeof(CDesc) * C + 16));
+  CHK(pool_take(c, b.payload, a->payload_bytes + 64));
+  CHK(copy_dev(c, b.keys, a->keys, s));
+  CHK(copy_dev(c, b.bm, a->bm, s));
+  CHK(copy_dev(c, b.key_off, a->key_off, s));
+  CHK(copy_dev(c, b.bm_off, a->bm_off, s));
+  HIPCHK(hipMemsetAsync(c->ro_flags.p, 0, 4 * n + 16, s));
   HIPCHK(hipMemsetAsync(c->scalar.p, 0, 64, s));
   unsigned long long* tot = c->scalar.as<unsigned long long>();
-  launch_runopt_plan(s, a->desc.as<CDesc>(), a->bm.as<uint32_t>(), a->payload.as<uint8_t>(), C, info.as<uint32_t>(),
-                     size.as<uint64_t>(), flags.as<uint32_t>(), tot);
-  launch_exclusive_scan(s, size.as<uint64_t>(), size.as<uint64_t>(), C, part.as<uint64_t>(),
+  launch_runopt_plan(s, a->desc.as<CDesc>(), a->bm.as<uint32_t>(), a->payload.as<uint8_t>(), C,
+                     c->ro_info.as<uint32_t>(), c->ro_size.as<uint64_t>(), c->ro_flags.as<uint32_t>(), tot);
+  launch_exclusive_scan(s, c->ro_size.as<uint64_t>(), c->ro_size.as<uint64_t>(), C, c->ro_part.as<uint64_t>(),
                         reinterpret_cast<uint64_t*>(tot + 4));
+  launch_runopt_write(s, a->desc.as<CDesc>(), a->payload.as<uint8_t>(), C, c->ro_info.as<uint32_t>(),
+                      c->ro_size.as<uint64_t>(), b.desc.as<CDesc>(), b.payload.as<uint8_t>());
   HIPCHK(hipGetLastError());
   unsigned long long h[5] = {};
   std::vector<uint32_t> hf(n);
   HIPCHK(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s));
-  if (n) HIPCHK(hipMemcpyAsync(hf.data(), flags.p, 4 * n, hipMemcpyDeviceToHost, s));
+  if (n) HIPCHK(hipMemcpyAsync(hf.data(), c->ro_flags.p, 4 * n, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  const int32_t bid = new_batch(c);
-  Batch& b = *c->batches[bid];
+  if (h[4] > a->payload_bytes) {  // the bound above is a theorem; a violation is a device error
+    set_err("runOptimize: converted payload larger than its input");
+    return RBG_ERR_DEVICE;
+  }
   b.n_bm = n;
   b.n_ctr = C;
   b.key_major = a->key_major;
@@ -2233,17 +2313,8 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
     if (answers) answers[i] = hf[i] != 0;
   }
   b.ser_bytes = a->ser_bytes ? ser : 0;  // batches built on the device carry no serialized size
-  CHK(copy_dev(b.keys, a->keys, s));
-  CHK(copy_dev(b.bm, a->bm, s));
-  CHK(copy_dev(b.key_off, a->key_off, s));
-  CHK(copy_dev(b.bm_off, a->bm_off, s));
-  CHK(b.desc.ensure(sizeof(CDesc) * C + 16));
-  CHK(b.payload.ensure(b.payload_bytes + 64));
-  launch_runopt_write(s, a->desc.as<CDesc>(), a->payload.as<uint8_t>(), C, info.as<uint32_t>(), size.as<uint64_t>(),
-                      b.desc.as<CDesc>(), b.payload.as<uint8_t>());
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(s));  // the scratch buffers above are freed on return
   b.live = true;
+  drop.keep = true;
   *out_id = bid;
   return RBG_OK;
 }
