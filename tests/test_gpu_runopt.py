@@ -91,3 +91,30 @@ def test_bsi_run_optimize(gpu):
     assert bsi.runOptimized
     after = [bsi.ebM.serialize()] + [s.serialize() for s in bsi.bA]
     assert after == [O.run_optimize(b) for b in before]
+
+
+def test_run_optimize_reuses_released_buffers(gpu):
+    """A context keeps the device buffers of released batches for the next batch of a similar
+    size (engine.cpp pool_take / pool_put): back-to-back runOptimize + release cycles over
+    different inputs reuse them, and every result still equals the oracle's (no stale bytes of
+    an earlier batch leak into a later one)."""
+    from roaringbitmap_amd import Engine
+    rng = np.random.default_rng(990)
+    e = Engine(0)
+    try:
+        for cycle in range(6):
+            bufs = []
+            for i in range(8):
+                keys = np.sort(rng.choice(1 << 16, size=int(rng.integers(1, 30)), replace=False))
+                bufs.append(_gen.bitmap(rng, keys))
+            a = e.load(bufs)
+            o, answers = e.run_optimize(a)
+            got = e.batch_fetch_range(o)
+            for b, g, ans in zip(bufs, got, answers):
+                exp = O.run_optimize(b)
+                assert g.serialize() == exp, cycle
+                assert bool(ans) == _answer(exp)
+            e.release(o)
+            e.release(a)
+    finally:
+        e.close()
