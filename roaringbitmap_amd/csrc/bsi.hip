@@ -132,7 +132,8 @@ __global__ __launch_bounds__(256) void k_plan_bsi(const uint32_t* __restrict__ k
                                                   unsigned long long* zsums, uint32_t* zdefer) {
   plan_zero(zlb, ztile);
   if (blockIdx.x == 0) {
-    if (zsums && threadIdx.x < (unsigned)kBsiSumWords) zsums[threadIdx.x] = 0;
+    if (zsums)
+      for (int i = threadIdx.x; i < kBsiSumAll; i += blockDim.x) zsums[i] = 0;
     if (zdefer && threadIdx.x == 0) zdefer[0] = 0;
   }
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
@@ -754,7 +755,8 @@ __global__ __launch_bounds__(256) void k_bsi_types(const Task* __restrict__ task
     if (threadIdx.x <= (unsigned)kBsiRegSlices && ((int)threadIdx.x < nb || threadIdx.x == kBsiRegSlices)) {
       const int x = threadIdx.x;
       const int c = bs[x][0] + bs[x][1] + bs[x][2] + bs[x][3];
-      if (c) atomicAdd(&sums[x == kBsiRegSlices ? kBsiMaxInputs : x], (unsigned long long)(uint32_t)c);
+      unsigned long long* rep = sums + kBsiSumWords + 64 * (blockIdx.x % kBsiSumReps);
+      if (c) atomicAdd(&rep[x == kBsiRegSlices ? kBsiMaxInputs : x], (unsigned long long)(uint32_t)c);
     }
   }
   if (!live2) return;
@@ -822,10 +824,14 @@ void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm,
 // takes slice x; the result stays on the device (sums[kBsiSumOut], [kBsiSumOut + 1]).
 __global__ __launch_bounds__(64) void k_bsi_sum_final(unsigned long long* __restrict__ sums, int nbits) {
   const int x = threadIdx.x;
-  const unsigned long long count = sums[kBsiMaxInputs];
+  // lane x: word x summed over the base words and k_bsi_types' replicas
+  unsigned long long wx = x < kBsiSumWords ? sums[x] : 0;
+#pragma unroll
+  for (int r = 0; r < kBsiSumReps; r++) wx += sums[kBsiSumWords + 64 * r + x];
+  const unsigned long long count = __shfl(wx, kBsiMaxInputs, 64);
   unsigned long long v = 0;
   if (x < nbits && count) {
-    const int64_t card = (int32_t)(uint32_t)sums[x];
+    const int64_t card = (int32_t)(uint32_t)wx;
     const int64_t w = (int64_t)(int32_t)(1u << x);
     v = (unsigned long long)(w * card);
   }

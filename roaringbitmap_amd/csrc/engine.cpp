@@ -1140,7 +1140,7 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   hipStream_t s = c->stream;
-  CHK(c->bsi_sums.ensure(8 * kBsiSumWords));  // zeroed by the plan kernel
+  CHK(c->bsi_sums.ensure(8 * kBsiSumAll));  // zeroed by the plan kernel
   c->bsi_nbits = nbits;
   int mode = op;
   if (op != BSI_SUM_ONLY) {

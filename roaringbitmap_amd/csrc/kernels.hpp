@@ -181,6 +181,11 @@ constexpr int kBsiMaxInputs = 34;  // ebM + up to 32 slices + foundSet
 // then sum(found) = (sum, count) as Java longs at [kBsiSumOut], [kBsiSumOut + 1]
 constexpr int kBsiSumOut = kBsiMaxInputs + 1;
 constexpr int kBsiSumWords = kBsiSumOut + 2;
+// k_bsi_types adds its per-block sums into one of kBsiSumReps replicas of 64 words after
+// those (block b: replica b % kBsiSumReps), so no sum word takes more than a few dozen
+// atomics; k_bsi_sum_final adds the replicas.  All of it is zeroed by the plan kernel.
+constexpr int kBsiSumReps = 16;
+constexpr int kBsiSumAll = kBsiSumWords + 64 * kBsiSumReps;
 struct BsiArgs {
   int op;         // BsiOp
   int nbits;      // slices
