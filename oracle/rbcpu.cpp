@@ -489,7 +489,10 @@ static Ctr R_and_B(const Ctr& r, const Ctr& b) {  // :338-378
   if (ans.card > kArrayMax) return ans;
   return bitmap_to_array(ans);
 }
-static Ctr R_and_R(const Ctr& t, const Ctr& x) {  // :381-456 (no galloping: ENABLE_GALLOPING_AND=false)
+// The run merge of RB/RunContainer.java:381-456 (no galloping: ENABLE_GALLOPING_AND=false) before its
+// toEfficientContainer; the buffer package's MappeableRunContainer.and(MappeableRunContainer)
+// (RB/buffer/MappeableRunContainer.java:474-536) returns exactly this merge.
+static Ctr R_and_R_runs(const Ctr& t, const Ctr& x) {
   RunBuf ans(t.nruns() + x.nruns());
   if (t.empty()) return ans.build();
   int rp = 0, xp = 0;
@@ -523,8 +526,9 @@ static Ctr R_and_R(const Ctr& t, const Ctr& x) {  // :381-456 (no galloping: ENA
       ans.push(latest, earliest - latest - 1);
     }
   }
-  return to_efficient(ans.build());
+  return ans.build();
 }
+static Ctr R_and_R(const Ctr& t, const Ctr& x) { return to_efficient(R_and_R_runs(t, x)); }  // :381-456
 static int R_and_card_A(const Ctr& r, const Ctr& a) {  // :459-486
   if (r.nruns() == 0) return a.card;
   int rp = 0, ap = 0, c = 0;
@@ -653,7 +657,10 @@ static Ctr R_andnot_B(const Ctr& r, const Ctr& b) {  // :594-634
   if (ans.card > kArrayMax) return ans;
   return bitmap_to_array(ans);
 }
-static Ctr R_andnot_R(const Ctr& t, const Ctr& x) {  // :637-692
+// The run difference of RB/RunContainer.java:637-692 before its toEfficientContainer; the buffer
+// package's MappeableRunContainer.andNot(MappeableRunContainer) (RB/buffer/MappeableRunContainer.java:600-663)
+// returns exactly this.
+static Ctr R_andnot_R_runs(const Ctr& t, const Ctr& x) {
   RunBuf ans(t.nruns() + x.nruns());
   int rp = 0, xp = 0;
   const int tn = t.nruns(), xn = x.nruns();
@@ -682,8 +689,9 @@ static Ctr R_andnot_R(const Ctr& t, const Ctr& x) {  // :637-692
     rp++;
     for (; rp < tn; rp++) ans.push(t.vals[2 * rp], t.vals[2 * rp + 1]);
   }
-  return to_efficient(ans.build());
+  return ans.build();
 }
+static Ctr R_andnot_R(const Ctr& t, const Ctr& x) { return to_efficient(R_andnot_R_runs(t, x)); }  // :637-692
 // lazyorToRun + convertToLazyBitmapIfNeeded, RB/RunContainer.java:1769-1813, 861-875
 static Ctr R_lazyor_A(const Ctr& r, const Ctr& a) {
   if (r.full()) return run_full();
@@ -925,6 +933,19 @@ Ctr c_andnot(const Ctr& a, const Ctr& b) {
   }
 }
 
+// Buffer package (RB/buffer/): MappeableContainer.and / andNot dispatch like the heap containers and
+// type their results alike (MappeableArrayContainer.java:287-384, MappeableBitmapContainer.java:152-348,
+// MappeableRunContainer.java:398-663) -- except run AND run and run ANDNOT run, which return the
+// merged run container without toEfficientContainer (MappeableRunContainer.java:474-536, 600-663).
+Ctr c_and_buf(const Ctr& a, const Ctr& b) {
+  if (a.kind == RUN && b.kind == RUN) return R_and_R_runs(a, b);
+  return c_and(a, b);
+}
+Ctr c_andnot_buf(const Ctr& a, const Ctr& b) {
+  if (a.kind == RUN && b.kind == RUN) return R_andnot_R_runs(a, b);
+  return c_andnot(a, b);
+}
+
 Ctr c_or(const Ctr& a, const Ctr& b) {
   switch (a.kind) {
     case ARRAY:
@@ -1093,13 +1114,16 @@ std::vector<uint32_t> bitmap_values(const Bitmap& b) {
   return out;
 }
 
-Bitmap op_and(const Bitmap& x1, const Bitmap& x2) {
+// key loop of RoaringBitmap.and (RB/RoaringBitmap.java:377-401); ImmutableRoaringBitmap.and
+// (RB/buffer/ImmutableRoaringBitmap.java:299-325) is the same loop over Mappeable containers
+template <class F>
+static Bitmap and_like(const Bitmap& x1, const Bitmap& x2, F op) {
   Bitmap ans;
   size_t p1 = 0, p2 = 0;
   while (p1 < x1.size() && p2 < x2.size()) {
     uint16_t s1 = x1.keys[p1], s2 = x2.keys[p2];
     if (s1 == s2) {
-      Ctr c = c_and(x1.ctrs[p1], x2.ctrs[p2]);
+      Ctr c = op(x1.ctrs[p1], x2.ctrs[p2]);
       if (!c.empty()) { ans.keys.push_back(s1); ans.ctrs.push_back(std::move(c)); }
       p1++;
       p2++;
@@ -1111,6 +1135,8 @@ Bitmap op_and(const Bitmap& x1, const Bitmap& x2) {
   }
   return ans;
 }
+Bitmap op_and(const Bitmap& x1, const Bitmap& x2) { return and_like(x1, x2, c_and); }
+Bitmap op_and_buf(const Bitmap& x1, const Bitmap& x2) { return and_like(x1, x2, c_and_buf); }
 
 int32_t op_and_card(const Bitmap& x1, const Bitmap& x2) {
   uint32_t ans = 0;  // Java int accumulation wraps mod 2^32
@@ -1147,13 +1173,16 @@ bool op_intersects(const Bitmap& x1, const Bitmap& x2) {
   return false;
 }
 
-Bitmap op_andnot(const Bitmap& x1, const Bitmap& x2) {
+// key loop of RoaringBitmap.andNot (RB/RoaringBitmap.java:444-473); ImmutableRoaringBitmap.andNot
+// (RB/buffer/ImmutableRoaringBitmap.java:441-471) is the same loop over Mappeable containers
+template <class F>
+static Bitmap andnot_like(const Bitmap& x1, const Bitmap& x2, F op) {
   Bitmap ans;
   size_t p1 = 0, p2 = 0;
   while (p1 < x1.size() && p2 < x2.size()) {
     uint16_t s1 = x1.keys[p1], s2 = x2.keys[p2];
     if (s1 == s2) {
-      Ctr c = c_andnot(x1.ctrs[p1], x2.ctrs[p2]);
+      Ctr c = op(x1.ctrs[p1], x2.ctrs[p2]);
       if (!c.empty()) { ans.keys.push_back(s1); ans.ctrs.push_back(std::move(c)); }
       p1++;
       p2++;
@@ -1170,6 +1199,8 @@ Bitmap op_andnot(const Bitmap& x1, const Bitmap& x2) {
   }
   return ans;
 }
+Bitmap op_andnot(const Bitmap& x1, const Bitmap& x2) { return andnot_like(x1, x2, c_andnot); }
+Bitmap op_andnot_buf(const Bitmap& x1, const Bitmap& x2) { return andnot_like(x1, x2, c_andnot_buf); }
 
 template <class F>
 static Bitmap union_like(const Bitmap& x1, const Bitmap& x2, F op, bool drop_empty) {

@@ -69,6 +69,9 @@ Ctr c_or(const Ctr& a, const Ctr& b);                // RB/Container.java:822-82
 Ctr c_xor(const Ctr& a, const Ctr& b);               // RB/Container.java:964-971
 Ctr c_andnot(const Ctr& a, const Ctr& b);            // RB/Container.java:164-171
 int c_and_card(const Ctr& a, const Ctr& b);          // RB/Container.java:113-126
+// buffer package: run AND / ANDNOT run keep the merged run container (RB/buffer/MappeableRunContainer.java:474-536,600-663)
+Ctr c_and_buf(const Ctr& a, const Ctr& b);
+Ctr c_andnot_buf(const Ctr& a, const Ctr& b);
 bool c_intersects(const Ctr& a, const Ctr& b);
 // in-place variants used by the FastAggregation chains
 Ctr c_iand(const Ctr& a, const Ctr& b);              // RB/Container.java:459-466
@@ -99,6 +102,9 @@ int32_t op_or_card(const Bitmap& x1, const Bitmap& x2);   // :916-920
 int32_t op_xor_card(const Bitmap& x1, const Bitmap& x2);  // :931-933
 int32_t op_andnot_card(const Bitmap& x1, const Bitmap& x2); // :944-985
 bool op_intersects(const Bitmap& x1, const Bitmap& x2);   // :698-720
+// ImmutableRoaringBitmap.and / andNot, RB/buffer/ImmutableRoaringBitmap.java:299-325, 441-471
+Bitmap op_and_buf(const Bitmap& x1, const Bitmap& x2);
+Bitmap op_andnot_buf(const Bitmap& x1, const Bitmap& x2);
 
 // FastAggregation, RB/FastAggregation.java.  `ids` carries Java object
 // identity (naive_and skips `bitmaps[k] != smallest` by reference, :341):

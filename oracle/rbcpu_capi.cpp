@@ -47,7 +47,8 @@ extern "C" {
 
 void rbo_free(void* p) { std::free(p); }
 
-// op: 0 and, 1 or, 2 xor, 3 andNot   (RB/RoaringBitmap.java:377,860,1071,444)
+// op: 0 and, 1 or, 2 xor, 3 andNot   (RB/RoaringBitmap.java:377,860,1071,444);
+// 4 and, 5 andNot of the buffer package (ImmutableRoaringBitmap.and :299, andNot :441)
 int rbo_pairwise(int op, const uint8_t* a, size_t an, const uint8_t* b, size_t bn, uint8_t** out,
                  size_t* out_len) {
   Bitmap x, y;
@@ -59,6 +60,8 @@ int rbo_pairwise(int op, const uint8_t* a, size_t an, const uint8_t* b, size_t b
     case 1: return emit(op_or(x, y), out, out_len);
     case 2: return emit(op_xor(x, y), out, out_len);
     case 3: return emit(op_andnot(x, y), out, out_len);
+    case 4: return emit(op_and_buf(x, y), out, out_len);
+    case 5: return emit(op_andnot_buf(x, y), out, out_len);
   }
   return ERR_ARG;
 }

@@ -121,3 +121,124 @@ class BSI:
             shift = np.int64(np.int32(np.uint32(1) << np.uint32(x)))  # (long) (1 << x), Java int shift
             s += int(shift) * O.pairwise_card("and", self.ba[x], found)
         return int(np.int64(np.uint64(s % (1 << 64)))), count
+
+
+def _i32(x):
+    return int(np.int64(x).astype(np.int32))
+
+
+class BufferBSI(BSI):
+    """The buffer package's bit-sliced index, ImmutableBitSliceIndex / MutableBitSliceIndex:
+    bsi/src/main/java/org/roaringbitmap/bsi/buffer/BitSliceIndexBase.java (BBSI/ below).
+
+    Its compare dispatches differently from the heap one (BBSI/:422-453):
+      EQ    rangeEQ (BBSI/:351-375): the chain starts from and(ebM, foundSet), not from ebM
+      NEQ   rangeNEQ (BBSI/:384-387): andNot(ebM, rangeEQ(...)) -- ebM, not the found set
+      GE    owenGreatEqual (BBSI/:243-275): BufferFastAggregation.horizontal_or over spine ANDs
+      GT/LT/LE  oNeilCompare (BBSI/:190-234), tracking only the needed GT / LT
+      RANGE and(owenGreatEqual(start), oNeilCompare(LE, end)) (BBSI/:444-449)
+    and every pairwise step is ImmutableRoaringBitmap's (O "and_buf" / "andnot_buf": a run AND /
+    ANDNOT run keeps the merged run container, RB/buffer/MappeableRunContainer.java:474-536,600-663).
+    horizontal_or over ImmutableRoaringBitmaps (RB/buffer/BufferFastAggregation.java:187-235) is the
+    heap FastAggregation.horizontal_or loop (RB/FastAggregation.java:183-231) over the same container
+    pointers (compareTo: RB/buffer/ImmutableRoaringArray.java:242-247 = RB/RoaringArray.java:708-713),
+    lazyOR / lazyIOR dispatch (RB/buffer/MappeableContainer.java:639-696 = RB/Container.java:717-774)
+    and repairAfterLazy, so O.wide("horizontal_or") gives its bytes.  sum is BBSI/:521-532 = BSI/:581-592.
+    """
+
+    def _and(self, a, b):
+        return O.pairwise("and_buf", a, b)
+
+    def _andnot(self, a, b):
+        return O.pairwise("andnot_buf", a, b)
+
+    # BBSI/:455-519 (all = ebM.clone() or ImmutableRoaringBitmap.and(ebM, foundSet))
+    def _minmax(self, op, start, end, found):
+        if found is None:
+            return BSI._minmax(self, op, start, end, None)
+        r = BSI._minmax(self, op, start, end, None)
+        if r is self.ebm:
+            return self._and(self.ebm, found)
+        return r
+
+    # BBSI/:190-234
+    def _oneil_buf(self, op, predicate, found):
+        fixed = self.ebm if found is None else found
+        gt = EMPTY if op in ("GT", "GE") else None
+        lt = EMPTY if op in ("LT", "LE") else None
+        eq = self.ebm
+        for i in range(self.bit_count() - 1, -1, -1):
+            if (predicate >> i) & 1:
+                if lt is not None:
+                    lt = O.pairwise("or", lt, self._andnot(eq, self.ba[i]))
+                eq = self._and(eq, self.ba[i])
+            else:
+                if gt is not None:
+                    gt = O.pairwise("or", gt, self._and(eq, self.ba[i]))
+                eq = self._andnot(eq, self.ba[i])
+        if op not in ("LT", "GT"):
+            eq = self._and(fixed, eq)
+        if op == "EQ":
+            return eq
+        if op == "GT":
+            return self._and(gt, fixed)
+        if op == "LT":
+            return self._and(lt, fixed)
+        if op == "LE":
+            return O.pairwise("or", lt, eq)
+        if op == "GE":
+            return O.pairwise("or", gt, eq)
+        raise ValueError(op)
+
+    def owen_inputs(self, predicate):
+        """owenGreatEqual's orInputs (BBSI/:245-264) as (kind, w) in order: "slice" = bA[w] itself,
+        "and" = and(spine, bA[w]); Java int / long arithmetic of beGtrThan and leastSignifZero."""
+        b = _i32(predicate - 1)
+        nb = _i32(~b)
+        lsz = 64 if nb == 0 else ((nb & 0xFFFFFFFF) & -(nb & 0xFFFFFFFF)).bit_length() - 1
+        spine, out = False, []
+        for w in range(self.bit_count() - 1, lsz - 1, -1):
+            if (b & (1 << w)) == 0:
+                out.append(("and" if spine else "slice", w))
+            else:
+                spine = True
+        return out
+
+    # BBSI/:243-275
+    def _owen_ge(self, predicate, found):
+        b = _i32(predicate - 1)
+        nb = _i32(~b)
+        lsz = 64 if nb == 0 else ((nb & 0xFFFFFFFF) & -(nb & 0xFFFFFFFF)).bit_length() - 1
+        spine, inputs = None, []
+        for w in range(self.bit_count() - 1, lsz - 1, -1):
+            if (b & (1 << w)) == 0:
+                inputs.append(self.ba[w] if spine is None else self._and(spine, self.ba[w]))
+            else:
+                spine = self.ba[w] if spine is None else self._and(spine, self.ba[w])
+        res = O.wide("horizontal_or", inputs) if inputs else EMPTY
+        return res if found is None else self._and(res, found)
+
+    # BBSI/:351-375
+    def range_eq(self, found, predicate):
+        eq = self.ebm if found is None else self._and(self.ebm, found)
+        r = self._minmax("EQ", predicate, 0, found)
+        if r is not None:
+            return r
+        for i in range(self.bit_count() - 1, -1, -1):
+            eq = self._and(eq, self.ba[i]) if (predicate >> i) & 1 else self._andnot(eq, self.ba[i])
+        return eq
+
+    # BBSI/:422-453
+    def compare(self, op, start, end=0, found=None):
+        r = self._minmax(op, start, end, found)
+        if r is not None:
+            return r
+        if op == "EQ":
+            return self.range_eq(found, start)
+        if op == "NEQ":  # BBSI/:384-387
+            return self._andnot(self.ebm, self.range_eq(found, start))
+        if op == "GE":
+            return self._owen_ge(start, found)
+        if op == "RANGE":
+            return self._and(self._owen_ge(start, found), self._oneil_buf("LE", end, found))
+        return self._oneil_buf(op, start, found)
