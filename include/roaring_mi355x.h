@@ -121,6 +121,18 @@ enum { RBG_BSI_EQ = 0, RBG_BSI_NEQ = 1, RBG_BSI_LE = 2, RBG_BSI_LT = 3, RBG_BSI_
 int rbg_bsi_compare(int op, int32_t start, int32_t end, const uint8_t* ebm, size_t ebm_len,
                     const uint8_t* const* slices, const size_t* slice_lens, size_t nbits, int32_t min_value,
                     int32_t max_value, const uint8_t* found, size_t found_len, rbg_buffer* out);
+/* The buffer package's index, ImmutableBitSliceIndex / MutableBitSliceIndex
+ * (bsi/src/main/java/org/roaringbitmap/bsi/buffer/BitSliceIndexBase.java, BBSI/): the same fields,
+ * its own compare circuit and ImmutableRoaringBitmap's result types.
+ *   op RBG_BSI_EQ .. RBG_BSI_RANGE: compare(op, startOrValue, end, foundSet)   BBSI/:422-453
+ *       (rangeEQ / rangeLT / rangeLE / rangeGT / rangeGE / range are compare, BBSI/:351-408)
+ *   op RBG_BSI_RANGE_NEQ_DIRECT: rangeNEQ(foundSet, value) called directly      BBSI/:384-387
+ *       (it skips compare's NEQ shortcut of compareUsingMinMax, :500-503)
+ * sum(foundSet) of this index is rbg_bsi_sum (BBSI/:521-532 is RoaringBitmapSliceIndex.java:581-592). */
+#define RBG_BSI_RANGE_NEQ_DIRECT 7
+int rbg_bsi_compare_buffer(int op, int32_t start, int32_t end, const uint8_t* ebm, size_t ebm_len,
+                           const uint8_t* const* slices, const size_t* slice_lens, size_t nbits, int32_t min_value,
+                           int32_t max_value, const uint8_t* found, size_t found_len, rbg_buffer* out);
 /* sum(foundSet) -> Pair<Long, Long> (RoaringBitmapSliceIndex.java:581-592): out2 = {sum, count}. */
 int rbg_bsi_sum(const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* slice_lens,
                 size_t nbits, const uint8_t* found, size_t found_len, int64_t* out2);
@@ -237,6 +249,10 @@ int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2);
 int rbg_ctx_bsi(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
                 int32_t min_value, int32_t max_value, int want_sum);
 int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2);
+/* rbg_bsi_compare_buffer over a device-resident batch (op as there); synchronous (the result's
+ * run containers above 2047 runs have an arena whose size is checked after the op). */
+int rbg_ctx_bsi_buffer(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
+                       int32_t min_value, int32_t max_value);
 /* The same {sum, count} (two int64) copied to device memory dst2, enqueued on the context
  * stream (no host synchronisation: the sum stays on the device, e.g. for an all-reduce). */
 int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2);

@@ -10,8 +10,9 @@ from ._lib import (DeviceError, IllegalArgumentException, InvalidRoaringFormat, 
 from .engine import Engine  # noqa: F401
 from .roaring import (BufferFastAggregation, FastAggregation, ParallelAggregation, RoaringBitmap, batch_and_cardinality,  # noqa: F401
                       run_optimize_many)
-from .bsi import RoaringBitmapSliceIndex  # noqa: F401
+from .bsi import BitSliceIndexBase, ImmutableBitSliceIndex, MutableBitSliceIndex, RoaringBitmapSliceIndex  # noqa: F401
 
-__all__ = ["RoaringBitmap", "FastAggregation", "BufferFastAggregation", "ParallelAggregation", "RoaringBitmapSliceIndex", "Engine", "batch_and_cardinality", "run_optimize_many",
+__all__ = ["RoaringBitmap", "FastAggregation", "BufferFastAggregation", "ParallelAggregation", "RoaringBitmapSliceIndex", "ImmutableBitSliceIndex",
+           "MutableBitSliceIndex", "BitSliceIndexBase", "Engine", "batch_and_cardinality", "run_optimize_many",
            "InvalidRoaringFormat",
            "TruncatedInput", "IllegalArgumentException", "DeviceError", "RoaringError"]

@@ -40,7 +40,7 @@ EXPORTED = [
     "rbg_ctx_batch_counts", "rbg_synth_key_bytes", "rbg_ctx_pair_bytes", "rbg_debug_stamps",
     "rbg_bsi_compare", "rbg_bsi_sum", "rbg_ctx_bsi", "rbg_ctx_bsi_sums", "rbg_ctx_bsi_sums_device", "rbg_ctx_batch_minmax",
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
-    "rbg_ctx_fetch_shard_device",
+    "rbg_ctx_fetch_shard_device", "rbg_bsi_compare_buffer", "rbg_ctx_bsi_buffer",
 ]
 
 _lib = None
@@ -87,6 +87,8 @@ def _declare(L):
     L.rbg_ctx_batch_counts.argtypes = [vp, i32, P(ctypes.c_uint32), sz]
     L.rbg_bsi_compare.argtypes = [ctypes.c_int, i32, i32, u8p, sz, P(ctypes.c_char_p), P(sz), sz, i32, i32, u8p, sz,
                                   buf]
+    L.rbg_bsi_compare_buffer.argtypes = L.rbg_bsi_compare.argtypes
+    L.rbg_ctx_bsi_buffer.argtypes = [vp, i32, ctypes.c_int, ctypes.c_int, ctypes.c_int, i32, i32, i32, i32]
     L.rbg_bsi_sum.argtypes = [u8p, sz, P(ctypes.c_char_p), P(sz), sz, u8p, sz, P(ctypes.c_int64)]
     L.rbg_ctx_bsi.argtypes = [vp, i32, ctypes.c_int, ctypes.c_int, ctypes.c_int, i32, i32, i32, i32, ctypes.c_int]
     L.rbg_ctx_bsi_sums.argtypes = [vp, P(ctypes.c_int64)]

@@ -1,10 +1,13 @@
-"""Host-side mirror of RoaringBitmapSliceIndex's query path.
+"""Host-side mirror of the bit-sliced indexes' query path.
 
 Mirrors bsi/src/main/java/org/roaringbitmap/bsi/RoaringBitmapSliceIndex.java (BSI/):
 compare(Operation, startOrValue, end, foundSet) (BSI/:482-513) and
-sum(foundSet) (BSI/:581-592). Both run as one fused MI355X pass per key over the
-slices (csrc/bsi.hip), and the results are the reference's bytes, container types
-included. Construction (setValue) is host-side.
+sum(foundSet) (BSI/:581-592), and the buffer package's ImmutableBitSliceIndex /
+MutableBitSliceIndex (bsi/src/main/java/org/roaringbitmap/bsi/buffer/BitSliceIndexBase.java,
+BBSI/): compare (BBSI/:422-453), rangeEQ / rangeNEQ / rangeLT / rangeLE / rangeGT / rangeGE /
+range (BBSI/:351-408) and sum (BBSI/:521-532).  Every query runs on the MI355X
+(csrc/bsi.hip) and the results are the reference's bytes, container types included.
+Construction (setValue) is host-side.
 """
 import ctypes
 
@@ -87,3 +90,56 @@ class RoaringBitmapSliceIndex:
         out = (ctypes.c_int64 * 2)()
         check(lib().rbg_bsi_sum(e, len(e), arr, lens, len(self.bA), f, len(f) if f else 0, out))
         return int(out[0]), int(out[1])
+
+
+class BitSliceIndexBase(RoaringBitmapSliceIndex):
+    """The buffer package's index (BBSI/): the same fields, its own compare circuit
+    (owenGreatEqual for GE and RANGE's lower bound, rangeEQ from and(ebM, foundSet), rangeNEQ
+    against ebM) and ImmutableRoaringBitmap's result types (csrc/bsi.hip, k_bsi_buf)."""
+
+    RANGE_NEQ_DIRECT = 7  # RBG_BSI_RANGE_NEQ_DIRECT
+
+    def _compare(self, op, start, end, foundSet):
+        arr, lens = self._slices()
+        e = self.ebM.serialize()
+        f = foundSet.serialize() if foundSet is not None else None
+        out = _lib.rbg_buffer()
+        check(lib().rbg_bsi_compare_buffer(op, int(start), int(end), e, len(e), arr, lens, len(self.bA),
+                                           self.minValue, self.maxValue, f, len(f) if f else 0, ctypes.byref(out)))
+        return RoaringBitmap(take(out))
+
+    def compare(self, operation, startOrValue, end=0, foundSet=None):
+        """BBSI/:422-453 -> ImmutableRoaringBitmap (as RoaringBitmap bytes)"""
+        op = OPERATIONS.index(operation) if isinstance(operation, str) else int(operation)
+        return self._compare(op, startOrValue, end, foundSet)
+
+    def rangeEQ(self, foundSet, predicate):  # BBSI/:351-375 (== compare(EQ))
+        return self._compare(0, predicate, 0, foundSet)
+
+    def rangeNEQ(self, foundSet, predicate):  # BBSI/:384-387
+        return self._compare(self.RANGE_NEQ_DIRECT, predicate, 0, foundSet)
+
+    def rangeLT(self, foundSet, predicate):  # BBSI/:389-391
+        return self.compare("LT", predicate, 0, foundSet)
+
+    def rangeLE(self, foundSet, predicate):  # BBSI/:393-395
+        return self.compare("LE", predicate, 0, foundSet)
+
+    def rangeGT(self, foundSet, predicate):  # BBSI/:397-399
+        return self.compare("GT", predicate, 0, foundSet)
+
+    def rangeGE(self, foundSet, predicate):  # BBSI/:401-403
+        return self.compare("GE", predicate, 0, foundSet)
+
+    def range(self, foundSet, start, end):  # BBSI/:405-408
+        return self.compare("RANGE", start, end, foundSet)
+
+    def sum(self, foundSet):
+        """BBSI/:521-532 (the heap index's sum, BSI/:581-592); None or empty -> (0, 0)"""
+        if foundSet is None or foundSet.isEmpty():
+            return 0, 0
+        return RoaringBitmapSliceIndex.sum(self, foundSet)
+
+
+ImmutableBitSliceIndex = BitSliceIndexBase
+MutableBitSliceIndex = BitSliceIndexBase

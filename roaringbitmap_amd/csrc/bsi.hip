@@ -43,8 +43,11 @@ __device__ __forceinline__ void vb_absent(VB& z) {
   for (int i = 0; i < 4; i++) z.r[i] = 0;
 }
 
-// z = x OP y with the reference's result-type rule; x / y may alias z
-template <int OP>
+// z = x OP y with the reference's result-type rule; x / y may alias z.  BUF: the buffer
+// package's ImmutableRoaringBitmap.and / andNot (RB/buffer/ImmutableRoaringBitmap.java:299-325,
+// 441-471), whose run AND / ANDNOT run keep the merged run container, no toEfficientContainer
+// (RB/buffer/MappeableRunContainer.java:474-536, 600-663); every other pair types like the heap's.
+template <int OP, bool BUF = false>
 __device__ __forceinline__ void vb_op(const VB& x, const VB& y, VB& z, uint32_t* lds, int* sh) {
   if (OP == OPR_AND && (!x.present || !y.present)) {
     vb_absent(z);
@@ -74,8 +77,9 @@ __device__ __forceinline__ void vb_op(const VB& x, const VB& y, VB& z, uint32_t*
     vb_absent(z);
     return;
   }
-  const bool use_eff = pairwise_needs_runs(OP, x.kind, x.card, y.kind, y.card);
-  const int kind = use_eff ? eff(c, count_runs(r, lds, sh)) : pairwise_kind(OP, x.kind, y.kind, c);
+  const bool raw_run = BUF && (OP == OPR_AND || OP == OPR_ANDNOT) && x.kind == DK_R && y.kind == DK_R;
+  const bool use_eff = !raw_run && pairwise_needs_runs(OP, x.kind, x.card, y.kind, y.card);
+  const int kind = raw_run ? DK_R : use_eff ? eff(c, count_runs(r, lds, sh)) : pairwise_kind(OP, x.kind, y.kind, c);
 #pragma unroll
   for (int i = 0; i < 4; i++) z.r[i] = r[i];
   z.present = 1;
@@ -139,7 +143,7 @@ __global__ __launch_bounds__(256) void k_plan_bsi(const uint32_t* __restrict__ k
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t s = key_off[k], n = key_off[k + 1] - s;
   // a key yields a result only where input `need` (ebM, or foundSet for sum alone) has a container
-  int f = 0;
+  int f = need == 0xFFFFFFFEu && n > 0;  // 0xFFFFFFFE: any input (buffer package: every key of any input)
   for (uint32_t j = 0; j < n; j++) f |= bm[s + j] == need;
   flag[k] = (uint8_t)f;
   by_key[k] = Task{k, (int32_t)s, (int32_t)n, 0};
@@ -809,6 +813,360 @@ __global__ __launch_bounds__(256) void k_bsi_defer(const Task* __restrict__ task
     const uint32_t len = stage_container(kind, r, (int)card, acc, tmp, sh);
     wg_place(t, true, nullptr, true, tmp, len, card, tasks[t].key, kind, oc, nullptr);
   }
+}
+
+// ===========================================================================
+// Buffer-package BSI: BitSliceIndexBase.compare
+// (bsi/src/main/java/org/roaringbitmap/bsi/buffer/BitSliceIndexBase.java, BBSI/ below)
+// ===========================================================================
+// ImmutableBitSliceIndex / MutableBitSliceIndex run their own circuit (BBSI/:422-453), and
+// every pairwise step is ImmutableRoaringBitmap's (vb_op<OP, true>):
+//   EQ    rangeEQ  (BBSI/:351-375): from and(ebM, foundSet), then and / andNot per slice
+//   NEQ   rangeNEQ (BBSI/:384-387): andNot(ebM, rangeEQ(...)); rangeEQ's own min / max shortcut
+//         (the empty bitmap) is decided on the host and makes the op ebM's clone (BSI_ALL)
+//   GT / LT / LE  oNeilCompare (BBSI/:190-234): the heap circuit, tracking GT or LT only
+//   GE    owenGreatEqual (BBSI/:243-275): from the top slice down to beGtrThan's least
+//         significant zero, the 1 bits of beGtrThan = start - 1 AND their slice into a spine
+//         and the 0 bits make orInputs (the slice itself above the first 1 bit, else
+//         and(spine, slice)); BufferFastAggregation.horizontal_or unites them
+//         (RB/buffer/BufferFastAggregation.java:187-235), then and(result, foundSet)
+//   RANGE and(owenGreatEqual(start), oNeilCompare(LE, end)) (BBSI/:444-449)
+//   ALL   compareUsingMinMax's "all" (BBSI/:456): ebM.clone() or and(ebM, foundSet)
+// One workgroup per key, streamed like bsi_task_streamed.  horizontal_or's chain for a key
+// follows the poll order of its container-pointer queue (key, then larger cardinality first,
+// ties in heap order, which depends on every earlier key).  With three orInputs or more,
+// k_bsi_owen_pre first records every orInput's type per key and the host replays the queue
+// (engine.cpp: owen_order); the chain of a key then rebuilds each orInput's bits in that
+// order.  With two or fewer the order does not matter (lazyOR is symmetric) and the
+// orInputs are chained as the spine makes them.
+
+__device__ __forceinline__ int bsi_card(const uint64_t r[4], int* sh) {
+  int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
+  int u = 0;
+  block_sum2(c, u, sh);
+  return (int)uni((uint32_t)c);
+}
+
+// horizontal_or's per-key chain (RB/buffer/BufferFastAggregation.java:200-233): one container
+// is cloned; else x1.lazyOR(x2), lazyIOR of the rest, repairAfterLazy.  The state is the
+// container class of the running union (the machine of WIDE_LAZY_CHAIN in wide.hip):
+//   A + A: lazyor, a lazy bitmap once the cardinalities add past 1024
+//          (RB/buffer/MappeableArrayContainer.java:1167-1191)
+//   x + B, B + x: a bitmap (MappeableBitmapContainer lazyor / ilazyor)
+//   A + R, R + A: lazyorToRun, a lazy bitmap above 4096 runs (RB/buffer/MappeableRunContainer.java:1709-1750, 748-762)
+//   R + R: or / ior -> toEfficientContainer (:1911-1944)
+// and repairAfterLazy: bitmap -> BY_CARD, full -> R (RB/buffer/MappeableBitmapContainer.java:1639-1649),
+// run -> toEfficientContainer (RB/buffer/MappeableRunContainer.java:2037-2039).
+struct HChain {
+  VB acc;
+  int n, st, cur;
+};
+__device__ __forceinline__ void hchain_add(HChain& h, const VB& x, uint32_t* lds, int* sh) {
+  if (!x.present) return;
+  if (h.n == 0) {
+    h.acc = x;
+    h.n = 1;
+    h.st = x.kind;
+    h.cur = x.card;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) h.acc.r[i] |= x.r[i];
+  if (h.st == DK_B) {
+  } else if (h.st == DK_A && x.kind == DK_A) {
+    if (h.cur + x.card > 1024) h.st = DK_B;
+    else h.cur = bsi_card(h.acc.r, sh);
+  } else if (x.kind == DK_B) {
+    h.st = DK_B;
+  } else if (h.st == DK_R && x.kind == DK_R) {
+    const int cc = bsi_card(h.acc.r, sh);
+    h.st = eff(cc, count_runs(h.acc.r, lds, sh));
+    h.cur = cc;
+  } else {
+    h.st = count_runs(h.acc.r, lds, sh) > 4096 ? DK_B : DK_R;
+  }
+  h.n++;
+}
+__device__ __forceinline__ void hchain_finish(HChain& h, VB& out, uint32_t* lds, int* sh) {
+  if (h.n == 0) {
+    vb_absent(out);
+    return;
+  }
+  out = h.acc;
+  if (h.n == 1) return;  // x1.getContainer().clone()
+  const int c = bsi_card(out.r, sh);
+  out.kind = h.st == DK_B ? (c == 65536 ? DK_R : by_card(c)) : h.st == DK_R ? eff(c, count_runs(out.r, lds, sh)) : DK_A;
+  out.card = c;
+  out.src = -1;
+}
+
+// pos[input] = desc index of the key's container of each input (-1: none)
+__device__ __forceinline__ void bsi_positions(const Task& tk, const WideArgs& A, int* pos) {
+  const uint32_t s = uni((uint32_t)tk.a), n = uni((uint32_t)tk.b);
+  __syncthreads();
+  for (int j = threadIdx.x; j < kBsiMaxInputs; j += NT) pos[j] = -1;
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < n; j += NT) pos[A.bm[s + j]] = (int)(s + j);
+  __syncthreads();
+}
+
+// owenGreatEqual's orInputs of one key, top down (BBSI/:250-264): rec != null records each
+// orInput's type (k_bsi_owen_pre), else each is chained into h as it is made.
+__device__ __forceinline__ void owen_walk(const WideArgs& A, const BsiArgs& P, const int* pos, HChain& h, TB* rec,
+                                          uint32_t* acc, uint32_t* tmp, int* q, int* sh) {
+  VB spine, s, x;
+  vb_absent(spine);
+  bool spine_null = true;
+  int j = 0;
+  for (int w = P.nbits - 1; w >= 0; w--) {
+    const uint32_t bit = 1u << w;
+    const bool zero = (P.owen_zeros & bit) != 0;
+    if (!zero && !(P.owen_ones & bit)) continue;  // below leastSignifZero
+    if (!spine_null && !spine.present) {          // the spine lacks the key: every later AND does too
+      if (zero) {
+        if (rec && threadIdx.x == 0) rec[j] = tb_absent();
+        j++;
+      }
+      continue;
+    }
+    vb_load(pos[1 + w], A, tmp, q, s);
+    if (zero) {  // orInputs.add(lastSpineGate == null ? bA[w] : and(lastSpineGate, bA[w]))
+      if (spine_null) x = s;
+      else vb_op<OPR_AND, true>(spine, s, x, acc, sh);
+      if (rec) {
+        if (threadIdx.x == 0) rec[j] = x.present ? TB{x.kind, x.card, x.src, 0} : tb_absent();
+      } else {
+        hchain_add(h, x, acc, sh);
+      }
+      j++;
+    } else if (spine_null) {  // lastSpineGate = bA[w]
+      spine = s;
+      spine_null = false;
+    } else {  // lastSpineGate = and(lastSpineGate, bA[w])
+      vb_op<OPR_AND, true>(spine, s, spine, acc, sh);
+    }
+  }
+}
+
+// orInput j (top-down index) of a key, rebuilt for the chain: its bits are the AND of the spine
+// slices above it and its own slice (in any order); its type is k_bsi_owen_pre's record.
+__device__ __forceinline__ void owen_input(int j, const WideArgs& A, const BsiArgs& P, const int* pos, const TB& tb,
+                                           VB& x, uint32_t* tmp, int* q) {
+  uint32_t z = P.owen_zeros;
+  for (int k = 0; k < j; k++) z &= ~(1u << (31 - __builtin_clz(z)));
+  const int w = 31 - __builtin_clz(z);
+  const uint32_t above = P.owen_ones & ~((2u << w) - 1u);  // (w = 31: nothing above)
+  if (!above) {  // above the first 1 bit: the slice itself
+    vb_load(pos[1 + w], A, tmp, q, x);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) x.r[i] = ~0ull;
+  for (uint32_t m = above | (1u << w); m; m &= m - 1) {
+    const int v = __builtin_ctz(m);
+    uint64_t y[4];
+    materialize(A.desc[pos[1 + v]], A.payload, tmp, q, y);
+#pragma unroll
+    for (int i = 0; i < 4; i++) x.r[i] &= y[i];
+  }
+  x.present = 1;
+  x.kind = tb.kind;
+  x.card = tb.card;
+  x.src = -1;
+}
+
+// A run container of more than 2047 runs (only the buffer package's raw run AND / ANDNOT make
+// them) into the big-run arena: [u16 nruns][(start, length - 1) pairs], written from the bits.
+__device__ __forceinline__ void place_big_runs(uint32_t t, uint32_t key, const VB& res, int nr, const OutCtx& oc,
+                                               const BigRuns& big, uint32_t* lds, int* sh,
+                                               unsigned long long* sh64) {
+  const uint32_t len = 2u + 4u * (uint32_t)nr;
+  if (threadIdx.x == 0) {
+    unsigned long long off = atomicAdd(&big.used[0], (unsigned long long)((len + 15u) & ~15u));
+    if (off + len > big.cap) {
+      atomicOr(&big.used[1], 1ull);  // the host reruns the op with a larger arena
+      off = ~0ull;
+    }
+    *sh64 = off;
+  }
+  __syncthreads();
+  const unsigned long long off = *sh64;
+  __syncthreads();
+  if (off == ~0ull) {
+    wg_place(t, false, nullptr, true, nullptr, 0, 0, key, DK_A, oc, nullptr);
+    return;
+  }
+  uint16_t* dst = reinterpret_cast<uint16_t*>(big.base + off);
+  uint64_t s[4], e[4];
+  run_edges(res.r, lds, s, e);
+  int ps0, ps1, ns, pe0, pe1, ne;
+  block_scan_halves(popc64(s[0]) + popc64(s[1]), popc64(s[2]) + popc64(s[3]), ps0, ps1, ns, sh);
+  block_scan_halves(popc64(e[0]) + popc64(e[1]), popc64(e[2]) + popc64(e[3]), pe0, pe1, ne, sh);
+  const int th = threadIdx.x;
+  const int bases[4] = {(2 * th) * 64, (2 * th + 1) * 64, (512 + 2 * th) * 64, (513 + 2 * th) * 64};
+  const int sp[4] = {ps0, ps0 + popc64(s[0]), ps1, ps1 + popc64(s[2])};
+  const int ep[4] = {pe0, pe0 + popc64(e[0]), pe1, pe1 + popc64(e[2])};
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    uint64_t x = s[k];
+    for (int p = sp[k]; x; p++, x &= x - 1) dst[1 + 2 * p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
+    x = e[k];
+    for (int p = ep[k]; x; p++, x &= x - 1) dst[2 + 2 * p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
+  }
+  if (th == 0) dst[0] = (uint16_t)nr;
+  __syncthreads();
+  for (int p = th; p < nr; p += NT) dst[2 + 2 * p] = (uint16_t)(dst[2 + 2 * p] - dst[1 + 2 * p]);  // end -> length - 1
+  __syncthreads();
+  wg_place(t, true, big.base + off, false, nullptr, len, (uint32_t)res.card, key, DK_R, oc, nullptr);
+}
+
+__device__ __forceinline__ void place_buf(uint32_t t, uint32_t key, const VB& res, const WideArgs& A, const OutCtx& oc,
+                                          const BigRuns& big, uint32_t* acc, uint32_t* tmp, int* sh,
+                                          unsigned long long* sh64) {
+  if (!res.present) {
+    wg_place(t, false, nullptr, true, tmp, 0, 0, key, DK_A, oc, nullptr);
+    return;
+  }
+  if (res.src >= 0) {
+    wg_passthrough(t, A.desc[res.src], A.payload, oc, nullptr);
+    return;
+  }
+  if (res.kind == DK_R) {
+    const int nr = count_runs(res.r, acc, sh);
+    if (nr > 2047) {
+      place_big_runs(t, key, res, nr, oc, big, acc, sh, sh64);
+      return;
+    }
+  }
+  const uint32_t len = stage_container(res.kind, res.r, res.card, acc, tmp, sh);
+  wg_place(t, true, nullptr, true, tmp, len, (uint32_t)res.card, key, res.kind, oc, nullptr);
+}
+
+__device__ __forceinline__ void bsi_task_buffer(uint32_t t, const Task& tk, const WideArgs& A, const BsiArgs& P,
+                                                const OutCtx& oc, uint32_t* acc, uint32_t* tmp, int* q, int* sh,
+                                                int* pos, unsigned long long* sh64) {
+  const int nb = P.nbits;
+  bsi_positions(tk, A, pos);
+  VB ebm, fixed, res;
+  vb_load(pos[0], A, tmp, q, ebm);
+  if (P.has_found) vb_load(pos[P.found_input], A, tmp, q, fixed);
+  else fixed = ebm;
+  const int op = P.op;
+  if (op == BSI_ALL) {  // ebM.clone() / and(ebM, foundSet)
+    if (P.has_found) vb_op<OPR_AND, true>(ebm, fixed, res, acc, sh);
+    else res = ebm;
+  } else if (op == BSI_EQ || op == BSI_NEQ) {  // rangeEQ, BBSI/:351-375
+    VB eq, sl;
+    if (P.has_found) vb_op<OPR_AND, true>(ebm, fixed, eq, acc, sh);
+    else eq = ebm;
+    for (int i = nb - 1; i >= 0 && eq.present; i--) {  // an absent EQ stays absent
+      vb_load(pos[1 + i], A, tmp, q, sl);
+      if ((P.pred0 >> i) & 1) vb_op<OPR_AND, true>(eq, sl, eq, acc, sh);
+      else vb_op<OPR_ANDNOT, true>(eq, sl, eq, acc, sh);
+    }
+    if (op == BSI_EQ) res = eq;
+    else vb_op<OPR_ANDNOT, true>(ebm, eq, res, acc, sh);  // rangeNEQ: andNot(ebM, EQ)
+  } else {
+    const bool two = op == BSI_RANGE;
+    VB left;
+    if (op == BSI_GE || two) {  // owenGreatEqual, BBSI/:243-275
+      HChain h;
+      h.n = 0;
+      h.st = DK_A;
+      h.cur = 0;
+      vb_absent(h.acc);
+      if (P.owen_order) {
+        const uint8_t* ord = P.owen_order + (size_t)t * kOwenOrder;
+        const TB* tb = reinterpret_cast<const TB*>(P.owen_tb) + (size_t)t * 32;
+        const int cnt = (int)uni(ord[0]);
+        for (int k = 0; k < cnt; k++) {
+          const int j = (int)uni(ord[1 + k]);
+          VB x;
+          owen_input(j, A, P, pos, tb[j], x, tmp, q);
+          hchain_add(h, x, acc, sh);
+        }
+      } else {
+        owen_walk(A, P, pos, h, nullptr, acc, tmp, q, sh);
+      }
+      hchain_finish(h, left, acc, sh);
+      if (P.has_found) vb_op<OPR_AND, true>(left, fixed, left, acc, sh);  // and(result, foundSet)
+    }
+    if (op == BSI_GE) {
+      res = left;
+    } else {  // oNeilCompare (BBSI/:190-234): GT, LT, LE, or RANGE's LE(end)
+      const int oop = two ? BSI_LE : op;
+      const uint32_t pred = two ? P.pred1 : P.pred0;
+      VB gt, lt, eq, sl, tv;
+      vb_absent(gt);
+      vb_absent(lt);
+      eq = ebm;
+      for (int i = nb - 1; i >= 0 && eq.present; i--) {  // an absent EQ adds nothing more
+        vb_load(pos[1 + i], A, tmp, q, sl);
+        if ((pred >> i) & 1) {
+          if (oop != BSI_GT) {  // LT = or(LT, andNot(EQ, bA[i]))
+            vb_op<OPR_ANDNOT, true>(eq, sl, tv, acc, sh);
+            vb_op<OPR_OR>(lt, tv, lt, acc, sh);
+          }
+          vb_op<OPR_AND, true>(eq, sl, eq, acc, sh);
+        } else {
+          if (oop == BSI_GT) {  // GT = or(GT, and(EQ, bA[i]))
+            vb_op<OPR_AND, true>(eq, sl, tv, acc, sh);
+            vb_op<OPR_OR>(gt, tv, gt, acc, sh);
+          }
+          vb_op<OPR_ANDNOT, true>(eq, sl, eq, acc, sh);
+        }
+      }
+      if (oop == BSI_GT) {
+        vb_op<OPR_AND, true>(gt, fixed, res, acc, sh);
+      } else if (oop == BSI_LT) {
+        vb_op<OPR_AND, true>(lt, fixed, res, acc, sh);
+      } else {  // LE: or(LT, and(fixedFoundSet, EQ))
+        vb_op<OPR_AND, true>(fixed, eq, eq, acc, sh);
+        vb_op<OPR_OR>(lt, eq, res, acc, sh);
+      }
+      if (two) vb_op<OPR_AND, true>(left, res, res, acc, sh);  // and(left, right)
+    }
+  }
+  place_buf(t, tk.key, res, A, oc, P.big, acc, tmp, sh, sh64);
+}
+
+__global__ __launch_bounds__(256) void k_bsi_owen_pre(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                      WideArgs A, BsiArgs P) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int q[257];
+  __shared__ int sh[8];
+  __shared__ int pos[kBsiMaxInputs];
+  const uint32_t nt = *n_tasks;
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const Task tk = tasks[t];
+    bsi_positions(tk, A, pos);
+    HChain h;
+    h.n = 0;
+    owen_walk(A, P, pos, h, reinterpret_cast<TB*>(P.owen_tb) + (size_t)t * 32, acc, tmp, q, sh);
+    if (threadIdx.x == 0) P.task_keys[t] = tk.key;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_bsi_buf(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                 WideArgs A, BsiArgs P, OutCtx oc) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int q[257];
+  __shared__ int sh[8];
+  __shared__ int pos[kBsiMaxInputs];
+  __shared__ unsigned long long sh64;
+  const uint32_t nt = *n_tasks;
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) bsi_task_buffer(t, tasks[t], A, P, oc, acc, tmp, q, sh, pos, &sh64);
+}
+
+void launch_bsi_owen_pre(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p) {
+  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_owen_pre)));
+  hipLaunchKernelGGL(k_bsi_owen_pre, dim3(g), dim3(256), 0, s, tasks, nt, args, p);
+}
+void launch_bsi_buf(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc) {
+  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi_buf)));
+  hipLaunchKernelGGL(k_bsi_buf, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc);
 }
 
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,

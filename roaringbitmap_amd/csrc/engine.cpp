@@ -65,6 +65,10 @@ static void dbg(hipStream_t s, const char* what) {
   std::fflush(stderr);
 }  // look-back state: ticket @0, error word @64, statuses @256
 
+// On an out-of-memory hipMalloc, the device buffers every context keeps for reuse (Ctx::pool) are
+// freed and the allocation is retried once (defined after Ctx).
+static size_t release_pools_on(int device);
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -94,6 +98,11 @@ struct DevBuf {
     p = nullptr;
     cap = 0;
     hipError_t e = hipMalloc(&p, bytes + kSlack);
+    if (e == hipErrorOutOfMemory) {
+      int dev = 0;
+      (void)hipGetLastError();
+      if (hipGetDevice(&dev) == hipSuccess && release_pools_on(dev) > 0) e = hipMalloc(&p, bytes + kSlack);
+    }
     if (e != hipSuccess) {
       p = nullptr;
       set_err(std::string("hipMalloc(") + std::to_string(bytes) + ") failed: " + hipGetErrorString(e));
@@ -150,6 +159,9 @@ struct Ctx {
   uint64_t* ztile = nullptr;
   DevBuf bsi_defer, bsi_cnts, bsi_kin, bsi_table;  // scratch of the register-resident BSI kernels
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
+  // buffer-package BSI: owenGreatEqual's orInput types / task keys / chain order, and the arena of
+  // result run containers above 2047 runs (BigRuns; big_ctl = {bytes used, overflow})
+  DevBuf owen_tb, owen_keys, owen_ord, big, big_ctl;
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   DevBuf order;                     // horizontal_*: chain order of every key segment
   DevBuf ro_info, ro_size, ro_part, ro_flags;  // runOptimize scratch (kept: no allocation per call)
@@ -157,6 +169,9 @@ struct Ctx {
   // hipFree of a 0.36 GB payload cost more than runOptimize's kernels); bounded by kPoolMax
   std::vector<DevBuf> pool;
   size_t pool_bytes = 0;
+  std::mutex pool_mu;  // the pool may be emptied by another thread's out-of-memory allocation
+  ResultInfo last_ri{};   // the pending result's facts, once ctx_info has read them (fetch_shard_device)
+  bool ri_valid = false;
   int bsi_nbits = 0;
   DevBuf by_key, flag, tasks, ntasks, wg_count, lb, recs, kind_by_out, info, task_card, result, cards, skip, raw,
       scalar, scratch;
@@ -183,13 +198,39 @@ struct Ctx {
     if (prof_n < prof_cap) (void)hipEventRecord(prof_ev[4 * prof_n + phase], stream);
     if (phase == 3 && prof_n < prof_cap) prof_n++;
   }
-  ~Ctx() {
-    prof_free();
-    if (pinned) (void)hipHostFree(pinned);
-    batches.clear();
-    if (stream) (void)hipStreamDestroy(stream);
-  }
+  ~Ctx();
 };
+
+// every live context, for release_pools_on
+static std::mutex g_ctx_mu;
+static std::vector<Ctx*> g_ctxs;
+
+Ctx::~Ctx() {
+  {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    g_ctxs.erase(std::remove(g_ctxs.begin(), g_ctxs.end(), this), g_ctxs.end());
+  }
+  prof_free();
+  if (pinned) (void)hipHostFree(pinned);
+  batches.clear();
+  if (stream) (void)hipStreamDestroy(stream);
+}
+
+static size_t pool_clear(Ctx* c) {
+  std::lock_guard<std::mutex> g(c->pool_mu);
+  const size_t n = c->pool.size();
+  c->pool.clear();
+  c->pool_bytes = 0;
+  return n;
+}
+
+static size_t release_pools_on(int device) {
+  std::lock_guard<std::mutex> g(g_ctx_mu);
+  size_t n = 0;
+  for (Ctx* c : g_ctxs)
+    if (c->device == device) n += pool_clear(c);
+  return n;
+}
 
 static int ctx_init(Ctx* c, int device) {
   int n = 0;
@@ -206,6 +247,10 @@ static int ctx_init(Ctx* c, int device) {
     return RBG_ERR_DEVICE;
   }
   c->device = device;
+  {
+    std::lock_guard<std::mutex> g(g_ctx_mu);
+    g_ctxs.push_back(c);
+  }
   HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   CHK(c->by_key.ensure(sizeof(PTask) * kMaxKeys));  // Task (wide) or PTask (pairwise) records
   CHK(c->flag.ensure(kMaxKeys));
@@ -271,6 +316,7 @@ constexpr size_t kPoolMaxBuf = 1ull << 30;  // larger buffers are freed at once
 // a released batch buffer into the context's pool (the stream is idle: rbg_ctx_release syncs)
 static void pool_put(Ctx* c, DevBuf& b) {
   if (!b.p) return;
+  std::lock_guard<std::mutex> g(c->pool_mu);
   if (b.cap > kPoolMaxBuf) {
     b = DevBuf();
     return;
@@ -287,13 +333,17 @@ static void pool_put(Ctx* c, DevBuf& b) {
 // else a fresh allocation
 static int pool_take(Ctx* c, DevBuf& dst, size_t bytes) {
   if (dst.p && dst.cap >= bytes) return RBG_OK;
+  std::unique_lock<std::mutex> lk(c->pool_mu);
   size_t best = c->pool.size();
   for (size_t i = 0; i < c->pool.size(); i++) {
     const size_t cap = c->pool[i].cap;
     if (cap >= bytes && cap <= 2 * bytes + (1u << 20) && (best == c->pool.size() || cap < c->pool[best].cap))
       best = i;
   }
-  if (best == c->pool.size()) return dst.ensure(bytes);
+  if (best == c->pool.size()) {
+    lk.unlock();  // ensure may empty the pools (out of memory)
+    return dst.ensure(bytes);
+  }
   c->pool_bytes -= c->pool[best].cap;
   dst = std::move(c->pool[best]);
   c->pool.erase(c->pool.begin() + (std::ptrdiff_t)best);
@@ -579,6 +629,7 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   oc->recs = c->recs.as<ORec>();
   c->serialized = false;
   c->place_pending = false;
+  c->ri_valid = false;
   c->pending_ub = 0;
   c->zlb = c->ztile = nullptr;
   c->pending_src.clear();
@@ -901,6 +952,7 @@ static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) 
   const size_t st_bytes = n_slots * stride * sizeof(PQState);
   size_t n_blk = 2 * B->n_ctr + 64;
   size_t free_b = 0, total_b = 0;
+  pool_clear(c);  // pooled buffers would count as used
   HIPCHK(hipMemGetInfo(&free_b, &total_b));
   const size_t budget = free_b / 10 * 9;
   if (st_bytes > budget / 2) {
@@ -1186,6 +1238,175 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
   return RBG_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Buffer-package BSI: BitSliceIndexBase.compare (bsi/src/main/java/org/roaringbitmap/bsi/buffer/
+// BitSliceIndexBase.java, BBSI/ below), bsi.hip's k_bsi_buf
+// ---------------------------------------------------------------------------
+
+// horizontal_or's chain order for owenGreatEqual (BBSI/:266, RB/buffer/BufferFastAggregation.java:187-235):
+// the queue holds one container pointer per orInput bitmap (in orInputs order, top down,
+// BBSI/:247-264); each walks the keys where its orInput has a container, ordered by key, then
+// larger cardinality first (RB/buffer/MutableRoaringArray.java:476-481), ties in the heap's
+// order.  The poll order of a key's pointers is that key's chain: ord[t * kOwenOrder] = n,
+// then the n orInput indices.
+static int owen_order(Ctx* c, int M, uint32_t nt) {
+  hipStream_t s = c->stream;
+  std::vector<uint32_t> keys(nt);
+  std::vector<int32_t> tb((size_t)nt * 32 * 4);  // TB: kind, card, src, pad
+  if (nt) {
+    HIPCHK(hipMemcpyAsync(keys.data(), c->owen_keys.p, 4 * (size_t)nt, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(tb.data(), c->owen_tb.p, 16 * 32 * (size_t)nt, hipMemcpyDeviceToHost, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<std::vector<uint32_t>> lists(M);  // tasks (ascending keys) where orInput j has a container
+  for (uint32_t t = 0; t < nt; t++)
+    for (int j = 0; j < M; j++)
+      if (tb[((size_t)t * 32 + j) * 4 + 1] > 0) lists[j].push_back(t);
+  std::vector<uint8_t> ord((size_t)std::max<uint32_t>(nt, 1) * kOwenOrder, 0);
+  auto ptr = [&](uint32_t j, uint32_t i) {
+    const uint32_t t = lists[j][i];
+    return HPtr{j, i, keys[t], (uint32_t)tb[((size_t)t * 32 + j) * 4 + 1], t};
+  };
+  auto push = [&](const HPtr& x) {
+    uint8_t* o = ord.data() + (size_t)x.pos * kOwenOrder;
+    o[1 + o[0]++] = (uint8_t)x.bm;
+  };
+  JHeap pq;
+  for (int j = 0; j < M; j++)
+    if (!lists[j].empty()) pq.add(ptr((uint32_t)j, 0));
+  auto advance_add = [&](const HPtr& x) {
+    if (x.i + 1 < lists[x.bm].size()) pq.add(ptr(x.bm, x.i + 1));
+  };
+  while (!pq.q.empty()) {
+    const HPtr x1 = pq.poll();
+    push(x1);
+    if (pq.q.empty() || pq.q[0].key != x1.key) {
+      advance_add(x1);
+      continue;
+    }
+    const HPtr x2 = pq.poll();
+    push(x2);
+    while (!pq.q.empty() && pq.q[0].key == x1.key) {
+      const HPtr x = pq.poll();
+      push(x);
+      if (x.i + 1 < lists[x.bm].size()) pq.add(ptr(x.bm, x.i + 1));
+      else if (pq.q.empty()) break;
+    }
+    advance_add(x1);
+    advance_add(x2);
+  }
+  CHK(c->owen_ord.ensure(ord.size()));
+  HIPCHK(hipMemcpyAsync(c->owen_ord.p, ord.data(), ord.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // `ord` is a stack vector
+  return RBG_OK;
+}
+
+// op: RBG_BSI_* (compare) or RBG_BSI_RANGE_NEQ_DIRECT; the batch is [ebM, bA[0..nbits-1], foundSet?].
+// Synchronous: the big-run arena is checked after the op (and the op rerun with a larger arena).
+static int ctx_bsi_buffer(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t start, int32_t end,
+                          int32_t min_value, int32_t max_value) {
+  Batch* B;
+  CHK(get_batch(c, id, &B));
+  if (!B->key_major || B->packed || nbits < 0 || nbits + 2 > kBsiMaxInputs ||
+      B->n_bm != (size_t)(1 + nbits + (has_found ? 1 : 0)) || op < 0 || op > RBG_BSI_RANGE_NEQ_DIRECT) {
+    set_err("bsi: batch must hold ebM, nbits slices and the optional foundSet; bad op");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  hipStream_t s = c->stream;
+  // compareUsingMinMax (BBSI/:455-519, as the heap one) and the op's own dispatch (BBSI/:422-453)
+  int mode, nb_eff = nbits, found_eff = has_found;
+  if (op == RBG_BSI_RANGE_NEQ_DIRECT || op == BSI_NEQ) {
+    const int mm = op == BSI_NEQ ? bsi_minmax(BSI_NEQ, start, end, min_value, max_value) : 0;
+    if (mm) {
+      mode = mm == 1 ? BSI_ALL : -1;
+    } else {  // andNot(ebM, rangeEQ(foundSet, value)); rangeEQ checks compareUsingMinMax(EQ) itself
+      const int em = bsi_minmax(BSI_EQ, start, 0, min_value, max_value);
+      mode = BSI_NEQ;
+      if (em == 2) {  // andNot(ebM, empty): ebM's clone
+        mode = BSI_ALL;
+        found_eff = 0;
+      } else if (em == 1) {  // andNot(ebM, ebM.clone() or and(ebM, foundSet)): the chain without slices
+        nb_eff = 0;
+      }
+    }
+  } else {
+    const int mm = bsi_minmax(op, start, end, min_value, max_value);
+    mode = mm == 1 ? BSI_ALL : mm == 2 ? -1 : op;
+  }
+  // owenGreatEqual (BBSI/:245-264): beGtrThan = start - 1, leastSignifZero =
+  // Long.numberOfTrailingZeros(~beGtrThan) (64 when start - 1 == -1: no orInput at all)
+  uint32_t zeros = 0, ones = 0;
+  if (mode == BSI_GE || mode == BSI_RANGE) {
+    const int32_t b = (int32_t)((uint32_t)start - 1u);
+    const uint32_t nbx = ~(uint32_t)b;
+    const int lsz = nbx == 0 ? 64 : __builtin_ctz(nbx);
+    for (int w = nbits - 1; w >= lsz; w--) {
+      if ((((uint32_t)b >> w) & 1u) == 0) zeros |= 1u << w;
+      else ones |= 1u << w;
+    }
+  }
+  const int M = __builtin_popcount(zeros);
+  const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
+  if (!c->big_ctl.p) CHK(c->big_ctl.ensure(16));
+  if (!c->big.p) CHK(c->big.ensure(16ull << 20));
+  for (int attempt = 0;; attempt++) {
+    OutCtx oc;
+    CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser + c->big.cap, &oc, false));
+    c->pending_src = {id};
+    const uint32_t need = mode == -1 ? 0xFFFFFFFFu : 0xFFFFFFFEu;  // every key of any input
+    c->mark(0);
+    launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
+                    c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile, nullptr, nullptr);
+    launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
+                   c->ntasks.as<uint32_t>());
+    HIPCHK(hipMemsetAsync(c->big_ctl.p, 0, 16, s));
+    c->mark(1);
+    WideArgs wa{};
+    wa.desc = B->desc.as<CDesc>();
+    wa.bm = B->bm.as<uint32_t>();
+    wa.payload = B->payload.as<uint8_t>();
+    BsiArgs p{};
+    p.op = mode < 0 ? BSI_EQ : mode;
+    p.nbits = nb_eff;
+    p.has_found = found_eff;
+    p.pred0 = (uint32_t)start;
+    p.pred1 = (uint32_t)end;
+    p.buffer = 1;
+    p.found_input = nbits + 1;
+    p.owen_zeros = zeros;
+    p.owen_ones = ones;
+    p.big = BigRuns{c->big.as<uint8_t>(), c->big_ctl.as<unsigned long long>(), c->big.cap};
+    const int grid = grid_for(ub, 65536);
+    if (mode >= 0 && M >= 3) {  // the chain order needs horizontal_or's queue: every orInput's type first
+      CHK(c->owen_tb.ensure((size_t)16 * 32 * ub));
+      CHK(c->owen_keys.ensure(4 * ub));
+      p.owen_tb = c->owen_tb.p;
+      p.task_keys = c->owen_keys.as<uint32_t>();
+      launch_bsi_owen_pre(s, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, p);
+      HIPCHK(hipGetLastError());
+      uint32_t nt = 0;
+      HIPCHK(hipMemcpyAsync(&nt, c->ntasks.p, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      CHK(owen_order(c, M, nt));
+      p.owen_order = c->owen_ord.as<uint8_t>();
+    }
+    if (mode >= 0) launch_bsi_buf(s, grid, c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, p, oc);
+    c->mark(2);
+    defer_place(c);
+    c->mark(3);
+    HIPCHK(hipGetLastError());
+    unsigned long long used[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(used, c->big_ctl.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (!used[1]) return RBG_OK;
+    if (attempt) {
+      set_err("bsi: the run-container arena overflowed twice");
+      return RBG_ERR_DEVICE;
+    }
+    CHK(c->big.ensure(used[0] + (used[0] >> 3) + 4096));  // the first pass counted every reservation
+  }
+}
+
 // (sum, count) of the last BSI call: k_bsi_sum_final's Java longs, read back
 static int ctx_bsi_sums(Ctx* c, int64_t* out2) {
   if (!c->bsi_sums.p) {
@@ -1215,6 +1436,10 @@ static int ctx_info(Ctx* c, ResultInfo* ri) {
   if ((c->last == 1 || c->last == 2) && ri->err) {
     set_err("a look-back spin of the op's plan or placement timed out: the result is invalid");
     return RBG_ERR_DEVICE;
+  }
+  if (c->last == 1) {
+    c->last_ri = *ri;
+    c->ri_valid = true;
   }
   return RBG_OK;
 }
@@ -1787,7 +2012,7 @@ int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2) {
   return ctx_bsi_sums(&ctx->c, out2);
 }
 int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2) {
-  if (!dst2 || !ctx->c.bsi_sums.p) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!ctx || !dst2 || !ctx->c.bsi_sums.p) return RBG_ERR_ILLEGAL_ARGUMENT;
   HIPCHK(hipSetDevice(ctx->c.device));
   launch_bsi_sums_out(ctx->c.stream, ctx->c.bsi_sums.as<unsigned long long>(), dst2);
   HIPCHK(hipGetLastError());
@@ -1820,6 +2045,24 @@ int rbg_bsi_compare(int op, int32_t start, int32_t end, const uint8_t* ebm, size
   g.ids.push_back(id);
   CHK(ctx_bsi(c, id, op, (int)nbits, found ? 1 : 0, start, end, min_value, max_value, 0));
   return ctx_fetch(c, out);
+}
+int rbg_bsi_compare_buffer(int op, int32_t start, int32_t end, const uint8_t* ebm, size_t ebm_len,
+                           const uint8_t* const* slices, const size_t* slice_lens, size_t nbits, int32_t min_value,
+                           int32_t max_value, const uint8_t* found, size_t found_len, rbg_buffer* out) {
+  if (!out || op < 0 || op > RBG_BSI_RANGE_NEQ_DIRECT) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(bsi_load(c, ebm, ebm_len, slices, slice_lens, nbits, found, found_len, &id));
+  g.ids.push_back(id);
+  CHK(ctx_bsi_buffer(c, id, op, (int)nbits, found ? 1 : 0, start, end, min_value, max_value));
+  return ctx_fetch(c, out);
+}
+int rbg_ctx_bsi_buffer(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
+                       int32_t min_value, int32_t max_value) {
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_bsi_buffer(&ctx->c, batch, op, nbits, has_found, start, end, min_value, max_value);
 }
 int rbg_bsi_sum(const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* slice_lens,
                 size_t nbits, const uint8_t* found, size_t found_len, int64_t* out2) {
@@ -1942,8 +2185,16 @@ static int ctx_fetch_shard_device(Ctx* c, int64_t total_containers, int has_run,
     set_err("fetch_shard: the global bitmap has an offset table; offsets_dst is required");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
+  // the result's facts: read by the result_stats call that sized the global layout (which also
+  // reported a timed-out spin as RBG_ERR_DEVICE), so the fetch stays asynchronous; without one,
+  // ctx_info synchronises here
   ResultInfo ri;
-  CHK(ctx_info(c, &ri));  // a plan or placement whose spin timed out left an invalid result (RBG_ERR_DEVICE)
+  if (c->ri_valid) {
+    ri = c->last_ri;
+    CHK(ensure_placed(c));
+  } else {
+    CHK(ctx_info(c, &ri));
+  }
   const uint64_t off0 = header_size((size_t)total_containers, has_run != 0) + (uint64_t)payload_base;
   if (off0 > 0xFFFFFFFFull) {
     set_err("fetch_shard: payload offsets exceed 32 bits");

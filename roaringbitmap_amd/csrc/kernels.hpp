@@ -186,12 +186,34 @@ constexpr int kBsiSumWords = kBsiSumOut + 2;
 // atomics; k_bsi_sum_final adds the replicas.  All of it is zeroed by the plan kernel.
 constexpr int kBsiSumReps = 16;
 constexpr int kBsiSumAll = kBsiSumWords + 64 * kBsiSumReps;
+// Run containers of more than 2047 runs (8 KiB of runs) do not fit a result slot.  Only the buffer
+// package's run AND / ANDNOT run make them (no toEfficientContainer); such a result is written to
+// this arena (bump allocation; `overflow` set when `cap` is exceeded, `used` then tells the size
+// the op needs, and the host reruns it with a larger arena).
+struct BigRuns {
+  uint8_t* base;
+  unsigned long long* used;  // used[0] bytes reserved, used[1] overflow flag
+  uint64_t cap;
+};
+constexpr int kOwenOrder = 64;  // bytes per task of an owenGreatEqual chain order
 struct BsiArgs {
   int op;         // BsiOp
   int nbits;      // slices
   int has_found;  // input nbits+1 is the foundSet
   uint32_t pred0;  // predicate (RANGE: start)
   uint32_t pred1;  // RANGE: end
+  // buffer package (bsi/.../bsi/buffer/BitSliceIndexBase.java): its own compare circuit and
+  // ImmutableRoaringBitmap's pairwise types (bsi.hip, "Buffer-package BSI")
+  int buffer;
+  int found_input;      // input index of the found set (nbits + 1 of the batch; the buffer kernel may run
+                        // with nbits = 0 over the same batch)
+  uint32_t owen_zeros;  // GE / RANGE: slice positions of owenGreatEqual's orInputs (0 bits of start - 1)
+  uint32_t owen_ones;   //   and of its spine ANDs (1 bits), both within [leastSignifZero, nbits)
+  const uint8_t* owen_order;  // per task kOwenOrder bytes: [0] = n, [1 + k] = orInput of chain position k
+                              // (the horizontal_or queue's poll order); null: top-down order
+  void* owen_tb;              // per task 32 x 16 B: each orInput's (kind, card, src) (k_bsi_owen_pre)
+  uint32_t* task_keys;        // k_bsi_owen_pre: key of each task
+  BigRuns big;
 };
 
 // Workgroups of `kernel` (256 threads) that are resident on the whole device at
@@ -276,6 +298,10 @@ struct BsiScratch {
 void launch_bsi_sums_out(hipStream_t s, const unsigned long long* sums, void* dst);  // 2 x u64 at kBsiSumOut
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
                 unsigned long long* sums, BsiScratch* sc);
+// buffer-package compare (p.buffer): k_bsi_owen_pre writes the orInput types of owenGreatEqual per
+// task (p.owen_tb, p.task_keys) for the host's horizontal_or queue replay; k_bsi_buf runs the circuit
+void launch_bsi_owen_pre(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p);
+void launch_bsi_buf(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc);
 
 // batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch: per-pair key
 // alignment (count, scan, emit), then one wave per matched key; pairs of more than 64

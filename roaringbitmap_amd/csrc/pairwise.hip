@@ -631,7 +631,10 @@ template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
                       const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct) {
   if (direct) {
-    const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, true>)));
+    // Direct mode lays each wave's tasks out in a region of per = ceil(nt / stride) + 3 (rounded to 4)
+    // records, stride = 4 g waves: at most nt + 4 stride records.  The task buffer holds
+    // kMaxKeys + 32768 (engine.cpp: ctx_init), so stride <= 8192 waves: g <= 2048 workgroups.
+    const int g = std::max(1, std::min({grid, resident_grid((const void*)&k_pair_wave<OP, MODE, true>), 2048}));
     hipLaunchKernelGGL((k_pair_wave<OP, MODE, true>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
                        *direct);
     return;

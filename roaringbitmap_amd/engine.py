@@ -147,6 +147,14 @@ class Engine:
         check(lib().rbg_ctx_bsi(self._ctx, int(batch), code, int(nbits), int(bool(has_found)), int(start), int(end),
                                 int(min_value), int(max_value), int(bool(want_sum))))
 
+    def bsi_buffer(self, batch, op, nbits, start, end=0, min_value=0, max_value=0, has_found=False):
+        """The buffer package's BitSliceIndexBase.compare (bsi/.../bsi/buffer/BitSliceIndexBase.java:422-453;
+        op 7 = rangeNEQ called directly) over a key-major batch [ebM, bA[0..nbits-1], foundSet?]."""
+        from .bsi import OPERATIONS
+        code = OPERATIONS.index(op) if isinstance(op, str) else int(op)
+        check(lib().rbg_ctx_bsi_buffer(self._ctx, int(batch), code, int(nbits), int(bool(has_found)), int(start),
+                                       int(end), int(min_value), int(max_value)))
+
     def bsi_sums(self):
         out = (ctypes.c_int64 * 2)()
         check(lib().rbg_ctx_bsi_sums(self._ctx, out))

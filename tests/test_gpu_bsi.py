@@ -110,7 +110,7 @@ def test_c5_synthetic_bsi(gpu):
     assert o.sum(exp)[0] == int(v[(v >= lo) & (v <= hi)].sum())
     # the same (sum, count) copied to device memory on the engine stream (the bench's all-reduce input)
     import torch
-    d = torch.zeros(2, dtype=torch.int64, device="cuda:0")
+    d = torch.empty(2, dtype=torch.int64, device="cuda:0")  # no fill on torch's stream to race the engine's write
     e.bsi_sums_device(d)
     e.sync()
     assert (int(d[0]), int(d[1])) == o.sum(exp)

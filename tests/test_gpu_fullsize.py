@@ -209,3 +209,29 @@ def test_c5_full_size(eng):
         exp = _bsi.BSI(bms[0], bms[1:], mn, mx).compare("RANGE", lo, hi)
         _same(_fmt.sub_bitmap(got, [k]), exp, f"C5 key {k}")
     eng.release(b)
+
+
+def test_c5_buffer_full_size(eng):
+    """C5 at 10^9 rows through the buffer package's circuit (BitSliceIndexBase.compare(RANGE):
+    owenGreatEqual over horizontal_or and oNeilCompare(LE), bsi/.../bsi/buffer/BitSliceIndexBase.java:
+    243-275,190-234,444-449): the same set as the heap query (the closed form checked above), and
+    for 6 keys the result's container equals tests/_bsi.BufferBSI's over that key's inputs."""
+    import _bsi
+    rows, seed = 1_000_000_000, 0xC5
+    b = eng.synth(4, seed, rows)
+    mn, mx = eng.batch_minmax(b)
+    lo, hi = 1 << 29, 1 << 30
+    eng.bsi(b, "RANGE", 31, lo, hi, mn, mx)
+    heap_card = eng.result_stats()["cardinality"]
+    eng.bsi_buffer(b, "RANGE", 31, lo, hi, mn, mx)
+    assert eng.result_stats()["cardinality"] == heap_card
+    got = eng.fetch().serialize()
+    nkeys = (rows + 65535) // 65536
+    keys = sorted({0, nkeys - 1, *np.random.default_rng(56).choice(nkeys, 4, replace=False).tolist()})
+    for k in keys:
+        sb = eng.synth(4, seed, rows, k, k + 1)
+        bms = [eng.batch_fetch(sb, i).serialize() for i in range(32)]
+        eng.release(sb)
+        exp = _bsi.BufferBSI(bms[0], bms[1:], mn, mx).compare("RANGE", lo, hi)
+        _same(_fmt.sub_bitmap(got, [k]), exp, f"C5 buffer key {k}")
+    eng.release(b)

@@ -95,3 +95,22 @@ def test_fetch_range_equals_single(gpu):
     assert got == [O.roundtrip(x)[1] for x in bufs]
     assert [x.serialize() for x in e.batch_fetch_range(b, 3, 4)] == got[3:7]
     e.release(b)
+
+
+def test_pooled_buffers_released_when_memory_runs_out(gpu):
+    """A released batch's device buffers stay pooled in its context (engine.cpp: pool_put); an
+    allocation that runs out of device memory empties every context's pool and retries."""
+    import torch
+    e = _engine()
+    b = e.synth(0, 0xC2A0, 1)  # a C2 operand: ~0.36 GB of payload
+    e.release(b)  # its buffers go to the pool
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info(0)
+    hog = torch.empty(max(free - (200 << 20), 0), dtype=torch.uint8, device="cuda:0")  # ~200 MB left
+    try:
+        b2 = e.synth(0, 0xC2B0, 1)  # fits only once the pooled buffers are freed
+        assert e.batch_stats(b2)["containers"] == 65536
+        e.release(b2)
+    finally:
+        del hog
+        torch.cuda.empty_cache()
