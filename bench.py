@@ -7,10 +7,15 @@ serialized result: key plan, container kernel, result placeme
 portable serialization (RB/RoaringArray.java:896-940) are all inside the step.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per
-GPU; each rank owns an independent C2 pair (weak scaling, no data-path collective);
-barrier + synchronize bracket the timed loop and the max time over ranks is used.
-At N > 1, extra.c2_and_key_sharded also runs ONE C2 pair split into key ranges over
-the ranks (strong scaling), its result assembled on GPU 0.
+GPU.  At N > 1 the headline is ONE C2 pair's RoaringBitmap.and split into key ranges over
+the ranks (strong scaling): each rank computes its key range, the shard
+layout is all-gathered on the device (RCCL) and every rank writes its slice at its global
+place in its own HBM -- no host round trip inside the step (shard.DeviceShard).  The gather
+of the slices to GPU 0 is timed separately (extra.c2_strong.gather_ms) and the gathered
+bitmap's sha is checked against the whole-pair result.  At N = 1 the step is the whole
+pair's AND + serialization.  barrier + synchronize bracket the timed loop and the max
+time over ranks is used.  extra.c2_and_weak keeps the weak-scaling form (an independent
+pair per rank).
 
 Prints ONE JSON line (rank 0).  Extra fields:
   roofline     - dominant kernel (container compute) achieved algorithmic GB/s vs
@@ -25,6 +30,7 @@ Prints ONE JSON line (rank 0).  Extra fields:
 ranks; `--only W` runs one workload alone (per-workload rocprofv3 --pmc passes).
 """
 import argparse
+import hashlib
 import json
 import math
 import os
@@ -155,50 +161,43 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
                                         "below input_bytes, so no roofline fraction is claimed"})}
 
 
-def c2_key_sharded(eng, rank, world, dist, steps, warmup, cdev, in_bytes):
-    """ONE C2 pair's RoaringBitmap.and split into key ranges over the ranks (strong
-    scaling): every rank holds the pair (seeds 0xC2A0 / 0xC2B0) and computes its key range
-    (rbg_ctx_pairwise_range), the shard layout is all-gathered and rank 0's GPU receives every
-    slice straight into its place (shard.assemble).  Equal key ranges: C2 draws each key's
-    container kinds independently, so equal key counts carry equal expected bytes."""
-    import hashlib
-
+def c2_weak(rank, world, dist, steps, warmup, cdev):
+    """The weak-scaling form of the headline: every rank ANDs its own C2 pair (seeds offset by the
+    rank) with the serialization, no data-path collective; max time over ranks."""
     import torch
-    from roaringbitmap_amd import shard
-    a = eng.synth(0, 0xC2A0)
-    b = eng.synth(0, 0xC2B0)
-    lo, hi = (65536 * rank) // world, (65536 * (rank + 1)) // world
-    dev = torch.device("cuda", torch.cuda.current_device())
-    comm = dev if cdev == "cuda" else torch.device("cpu")
-    fill = shard.engine_fill(eng)
-
-    def step():
-        eng.pairwise("and", a, b, key_lo=lo, key_hi=hi)
-        rs = eng.result_stats()
-        lay = shard.exchange_layout(rs["containers"], rs["payload_bytes"], rs["has_run"], device=comm)
-        return shard.assemble(fill, lay, rank, fill_device=dev, comm_device=comm, sync=eng.sync), lay
-
-    for _ in range(warmup):
-        out, lay = step()
-    torch.cuda.synchronize()
-    sha = hashlib.sha256(bytes(out.cpu().numpy().tobytes())).hexdigest()[:16] if rank == 0 else None
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        out, lay = step()
-    torch.cuda.synchronize()
-    dist.barrier()
-    wall = time.perf_counter() - t0
-    t = torch.tensor([wall], dtype=torch.float64, device=comm)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    eng.release(a)
-    eng.release(b)
-    ms = float(t[0]) / steps * 1e3
-    return {"workload": f"C2 RoaringBitmap.and of ONE pair, key-range sharded over {world} GPUs, result assembled "
-                        f"on GPU 0", "input_GBps": round(in_bytes / (ms / 1e3) / 1e9, 1), "ms_per_step": round(ms, 4),
-            "input_bytes": int(in_bytes), "result_serialized_bytes": int(lay.nbytes), "result_sha16": sha,
-            "rank0_keys": [lo, hi], "scaling": "strong"}
+    from roaringbitmap_amd import Engine
+    e = Engine(torch.cuda.current_device())
+    try:
+        a = e.synth(0, 0xC2A0 + 0x10000 * rank)
+        b = e.synth(0, 0xC2B0 + 0x10000 * rank)
+        sa, sb = e.batch_stats(a), e.batch_stats(b)
+        in_bytes = sa["payload_bytes"] + sb["payload_bytes"] + 4 * (sa["containers"] + sb["containers"])
+        for _ in range(warmup):
+            e.pairwise("and", a, b)
+            e.serialize()
+        e.sync()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            e.pairwise("and", a, b)
+            e.serialize()
+        e.sync()
+        if dist is not None:
+            dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0, float(in_bytes)], dtype=torch.float64, device=cdev)
+        if dist is not None:
+            tm = t.clone()
+            dist.all_reduce(tm[:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+            t[0] = tm[0]
+        e.release(a)
+        e.release(b)
+    finally:
+        e.close()
+    step = float(t[0]) / steps
+    return {"workload": f"C2 RoaringBitmap.and + serialization, an independent pair per GPU ({world} GPUs)",
+            "input_GBps": round(float(t[1]) / step / 1e9, 1), "ms_per_step": round(step * 1e3, 4), "scaling": "weak"}
 
 
 def c2_two_streams(eng, a, b, in_bytes, steps, warmup):
@@ -537,8 +536,8 @@ def main():
         if dist is not None:
             dist.destroy_process_group()
         return
-    a = eng.synth(0, 0xC2A0 + 0x10000 * rank)
-    b = eng.synth(0, 0xC2B0 + 0x10000 * rank)
+    a = eng.synth(0, 0xC2A0)  # ONE pair: at N > 1 every rank holds it and computes its key range
+    b = eng.synth(0, 0xC2B0)
     sa, sb = eng.batch_stats(a), eng.batch_stats(b)
     # algorithmic bytes: AND reads the descriptors of both operands and the
     # payload of matched pairs (every key matches here); writes the result payload + 4 B/container
@@ -546,14 +545,23 @@ def main():
     eng.pairwise("and", a, b)
     rs = eng.result_stats()
     out_bytes = rs["payload_bytes"] + 4 * rs["containers"]
-    import hashlib
     rs["sha16"] = hashlib.sha256(eng.fetch().serialize()).hexdigest()[:16]  # of the serialized result
 
     stream = torch.cuda.ExternalStream(eng.stream_ptr)
+    strong = world > 1
+    if strong:
+        from roaringbitmap_amd import shard
+        key_lo, key_hi = (65536 * rank) // world, (65536 * (rank + 1)) // world
+        dshard = shard.DeviceShard(eng, rank, world, torch.device("cuda", local),
+                                   torch.device("cuda", local) if cdev == "cuda" else "cpu")
 
-    def c2_step():  # RoaringBitmap.and(x1, x2) -> the device-resident serialized result
-        eng.pairwise("and", a, b)
-        eng.serialize()
+        def c2_step():  # this rank's key range of ONE pair -> its slice at its global place in its HBM
+            eng.pairwise("and", a, b, key_lo=key_lo, key_hi=key_hi)
+            dshard.place()
+    else:
+        def c2_step():  # RoaringBitmap.and(x1, x2) -> the device-resident serialized result
+            eng.pairwise("and", a, b)
+            eng.serialize()
 
     for _ in range(args.warmup):
         c2_step()
@@ -576,6 +584,24 @@ def main():
     barrier()
     wall = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+
+    strong_info = None
+    if strong:  # the gather of the slices to GPU 0, timed apart; its bytes against the whole pair's
+        ks_g = max(2, args.steps // 4)
+        barrier()
+        tg = time.perf_counter()
+        for _ in range(ks_g):
+            out = dshard.gather()
+        barrier()
+        g_ms = (time.perf_counter() - tg) / ks_g * 1e3
+        got = hashlib.sha256(bytes(out.cpu().numpy().tobytes())).hexdigest()[:16] if rank == 0 else None
+        lay = dshard.layout()
+        strong_info = {"workload": f"C2 RoaringBitmap.and of ONE pair, key-range sharded over {world} GPUs; the step "
+                                   f"ends with every slice at its global place in its rank's HBM",
+                       "rank0_keys": [key_lo, key_hi], "gather_to_gpu0_ms": round(g_ms, 4),
+                       "result_serialized_bytes": int(lay.nbytes), "result_sha16": got,
+                       "sha_equals_whole_pair_result": (got == rs["sha16"]) if rank == 0 else None,
+                       "layout_exchange": "device all-gather (RCCL)" if cdev == "cuda" else "gloo (host)"}
 
     # the serialization's own device time (events around it, on the engine's stream)
     ser_ms = 0.0
@@ -604,11 +630,10 @@ def main():
     if dist is not None:
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        tsum = t.clone()
-        dist.all_reduce(tsum[1:], op=dist.ReduceOp.SUM)
-        wall_max, total_in = float(tmax[0]), float(tsum[1])
+        wall_max = float(tmax[0])
     else:
-        wall_max, total_in = wall, float(in_bytes)
+        wall_max = wall
+    total_in = float(in_bytes)  # one pair, whatever the number of GPUs (strong scaling)
 
     extra = {}
 
@@ -654,8 +679,9 @@ def main():
     # one op's serialization overlaps the next op's compute (throughput of concurrent calls, as a
     # server would issue them; the headline above is one call after another)
     run_extra("c2_and_two_streams", lambda: c2_two_streams(eng, a, b, in_bytes, args.steps, args.warmup))
-    if world > 1:  # the engine's own key split of one pair, beside the weak-scaling headline
-        run_extra("c2_and_key_sharded", lambda: c2_key_sharded(eng, rank, world, dist, ks, 1, cdev, in_bytes))
+    if strong:  # the weak-scaling form beside the key-sharded headline
+        extra["c2_strong"] = strong_info
+        run_extra("c2_and_weak", lambda: c2_weak(rank, world, dist, ks, 1, cdev))
     if args.c3_n > 0:
         for kind, name in ((1, "c3_uniform_or"), (2, "c3_clustered_or")):
             run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, 1, cdev))
@@ -690,13 +716,15 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(step_s * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic",
             "config": {"workload": "C2: RoaringBitmap.and(x1, x2), two full 2^32-universe bitmaps of 65536 "
                                    "mixed array/bitmap/run containers each (configs[1])",
-                       "per_rank": "one independent C2 pair per GPU", "parallelism": f"dp{world}"},
+                       "per_rank": "the pair's key range [65536 r / N, 65536 (r + 1) / N); slices placed in each "
+                                   "rank's HBM" if strong else "the whole pair",
+                       "parallelism": f"key-range sharding over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(),
                          "kernel": "k_pair_wave<AND> (container compute)",
@@ -707,10 +735,10 @@ def main():
                 "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
                 "phase_ms": {"plan": round(ph_avg[0], 4), "compute": round(ph_avg[1], 4),
                              "place": round(ph_avg[2], 4), "serialize": round(ser_ms, 4)},
-                "elements_per_s": round((sa["cardinality"] + sb["cardinality"]) * world / step_s, 1),
+                "elements_per_s": round((sa["cardinality"] + sb["cardinality"]) / step_s, 1),
                 "operand_mix": {k: [sa[k], sb[k]] for k in ["array", "bitmap", "run"]},
                 "result": rs,
-                "input_frac_of_peak": round(total_in / step_s / 1e9 / world / HBM_PEAK_GBS, 4),
+                "input_frac_of_peak_per_gpu": round(total_in / step_s / 1e9 / world / HBM_PEAK_GBS, 4),
                 **extra,
             },
         }

@@ -298,6 +298,18 @@ int rbg_ctx_fetch_shard(rbg_ctx* ctx, int64_t total_containers, int has_run,
  * global offset); the run-flag bytes are packed into the header by the assembler. */
 int rbg_ctx_fetch_shard_device(rbg_ctx* ctx, int64_t total_containers, int has_run, int64_t payload_base,
                                void* desc_dst, void* offsets_dst, void* runflag_dst, void* payload_dst);
+/* The layout exchange without host synchronisation (SURVEY §8(e) steps 1-2 on the device):
+ * rbg_ctx_result_layout_device writes the pending result's (containers, payload bytes, has_run) as
+ * three int64 into device memory dst3, enqueued on the context stream -- the input of a device
+ * all-gather (RCCL).  rbg_ctx_fetch_shard_device_dyn then reads the gathered layout from device
+ * memory (world x 3 int64, ranks in key-range order) and writes this rank's slice into `out`, a
+ * buffer laid out as the whole global bitmap (descriptors, offset-table entries and payload at
+ * their global places; rank 0 also the cookie), and one run byte per global container into runb
+ * (needed when any shard has run containers; packed into the header by the assembler).  `out`
+ * must hold header + all payload bytes of the global bitmap: 8 + 8 * 65536 + 8194 * 65536 bytes
+ * bound any layout. */
+int rbg_ctx_result_layout_device(rbg_ctx* ctx, void* dst3);
+int rbg_ctx_fetch_shard_device_dyn(rbg_ctx* ctx, const void* layout, int rank, int world, void* out, void* runb);
 
 #ifdef __cplusplus
 }

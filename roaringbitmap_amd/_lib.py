@@ -41,6 +41,7 @@ EXPORTED = [
     "rbg_bsi_compare", "rbg_bsi_sum", "rbg_ctx_bsi", "rbg_ctx_bsi_sums", "rbg_ctx_bsi_sums_device", "rbg_ctx_batch_minmax",
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
     "rbg_ctx_fetch_shard_device", "rbg_bsi_compare_buffer", "rbg_ctx_bsi_buffer",
+    "rbg_ctx_result_layout_device", "rbg_ctx_fetch_shard_device_dyn",
 ]
 
 _lib = None
@@ -108,6 +109,8 @@ def _declare(L):
     L.rbg_ctx_profile.argtypes = [vp, ctypes.c_int]
     L.rbg_ctx_profile_read.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_int)]
     L.rbg_ctx_fetch_shard_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp]
+    L.rbg_ctx_result_layout_device.argtypes = [vp, vp]
+    L.rbg_ctx_fetch_shard_device_dyn.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, vp, vp]
     L.rbg_ctx_fetch_shard.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, buf, buf,
                                       buf]
 

@@ -2216,6 +2216,41 @@ static int ctx_fetch_shard_device(Ctx* c, int64_t total_containers, int has_run,
   return RBG_OK;
 }
 
+int rbg_ctx_result_layout_device(rbg_ctx* ctx, void* dst3) {
+  if (!ctx || !dst3) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c = &ctx->c;
+  HIPCHK(hipSetDevice(c->device));
+  if (c->last != 1) {
+    set_err("no materialised result pending");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  CHK(ensure_placed(c));
+  launch_layout_out(c->stream, c->info.as<ResultInfo>(), reinterpret_cast<int64_t*>(dst3));
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
+int rbg_ctx_fetch_shard_device_dyn(rbg_ctx* ctx, const void* layout, int rank, int world, void* out, void* runb) {
+  if (!ctx || !layout || !out || world < 1 || world > 1024 || rank < 0 || rank >= world)
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c = &ctx->c;
+  HIPCHK(hipSetDevice(c->device));
+  if (c->last != 1) {
+    set_err("no materialised result pending");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  CHK(ensure_placed(c));
+  // an already serialized result's pass-through records may point into released operands: copy its
+  // payload region instead (like rbg_ctx_fetch_shard_device); not expected on the sharded path
+  if (c->serialized) {
+    set_err("fetch_shard_device_dyn: the result was already serialized; fetch it before releasing operands "
+            "or use rbg_ctx_fetch_shard_device");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  launch_serialize_shard_dyn(c->stream, grid_for((c->pending_ub + 255) / 256, 256), c->ntasks.as<uint32_t>(), c->pending,
+                             reinterpret_cast<const int64_t*>(layout), rank, world, (uint8_t*)out, (uint8_t*)runb, true);
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
 int rbg_ctx_fetch_shard_device(rbg_ctx* ctx, int64_t total_containers, int has_run, int64_t payload_base,
                                void* desc_dst, void* offsets_dst, void* runflag_dst, void* payload_dst) {
   if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;

@@ -453,6 +453,78 @@ __global__ __launch_bounds__(256) void k_shard_table(const uint32_t* __restrict_
   }
 }
 
+// The same placement with the global layout read from device memory (an all-gather's output:
+// world x {containers, payload bytes, has_run} int64, ranks in key-range order), so a sharded
+// op needs no host round trip between its compute and its slice's place in the global bitmap.
+// `out` is laid out as the whole global bitmap; this rank writes its descriptors, offset-table
+// entries and payload there, one run byte per container into runb, and rank 0 the cookie
+// (RB/RoaringArray.java:896-940; the run-flag bitset is packed once every rank's bytes are in).
+struct ShardGeo {
+  uint64_t total, first, base, header, desc_base, off_base;
+  uint32_t has_run, offsets;
+};
+__device__ __forceinline__ ShardGeo shard_geo(const int64_t* __restrict__ lay, int rank, int world) {
+  ShardGeo g{};
+  for (int i = 0; i < world; i++) {
+    const uint64_t n = (uint64_t)lay[3 * i], p = (uint64_t)lay[3 * i + 1];
+    g.total += n;
+    g.has_run |= lay[3 * i + 2] != 0;
+    if (i < rank) {
+      g.first += n;
+      g.base += p;
+    }
+  }
+  g.header = header_bytes((uint32_t)g.total, g.has_run);
+  g.desc_base = g.has_run ? 4 + (g.total + 7) / 8 : 8;
+  g.offsets = !g.has_run || g.total >= 4;
+  g.off_base = g.desc_base + 4 * g.total;
+  return g;
+}
+__global__ __launch_bounds__(256) void k_emit_dyn(const uint32_t* __restrict__ n_tasks, OutCtx oc,
+                                                  const int64_t* __restrict__ lay, int rank, int world,
+                                                  uint8_t* __restrict__ out) {
+  const ShardGeo g = shard_geo(lay, rank, world);
+  uint8_t* dst = out + g.header + g.base;
+  const uint32_t nt = *n_tasks;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
+    const ORec& r = oc.recs[t];
+    if (!uni(r.keep)) continue;
+    w_copy(dst + uni64(r.off), reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
+  }
+}
+__global__ __launch_bounds__(256) void k_shard_table_dyn(const uint32_t* __restrict__ n_tasks, OutCtx oc,
+                                                         const int64_t* __restrict__ lay, int rank, int world,
+                                                         uint8_t* __restrict__ out, uint8_t* __restrict__ runb) {
+  const ShardGeo g = shard_geo(lay, rank, world);
+  const uint32_t nt = *n_tasks;
+  if (rank == 0 && blockIdx.x == 0 && threadIdx.x < 8) {  // the cookie (RB/RoaringArray.java:900-901,918-921)
+    const uint32_t c0 = g.has_run ? 12347u | ((uint32_t)(g.total - 1) << 16) : 12346u;
+    const uint32_t w = threadIdx.x < 4 ? c0 : (uint32_t)g.total;
+    if (threadIdx.x < 4 || !g.has_run) out[threadIdx.x] = (uint8_t)(w >> (8 * (threadIdx.x & 3)));
+  }
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    const ORec r = oc.recs[t];
+    if (!r.keep) continue;
+    const uint64_t idx = g.first + r.idx;
+    const uint32_t d = (uint32_t)r.key | ((r.card - 1) << 16);
+    for (int k = 0; k < 4; k++) out[g.desc_base + 4 * idx + k] = (uint8_t)(d >> (8 * k));
+    if (g.offsets) {
+      const uint32_t o = (uint32_t)(g.header + g.base + r.off);
+      for (int k = 0; k < 4; k++) out[g.off_base + 4 * idx + k] = (uint8_t)(o >> (8 * k));
+    }
+    if (runb) runb[idx] = r.kind == DK_R ? 1 : 0;
+  }
+}
+// the pending result's (containers, payload bytes, has_run) as int64, from k_place's ResultInfo
+__global__ void k_layout_out(const ResultInfo* __restrict__ info, int64_t* __restrict__ dst) {
+  if (threadIdx.x == 0) {
+    dst[0] = (int64_t)info->n_out;
+    dst[1] = (int64_t)info->payload;
+    dst[2] = (int64_t)info->has_run;
+  }
+}
+
 // ===========================================================================
 // slot gather (batch fetch): one wave per slot, into a contiguous download buffer
 // ===========================================================================
@@ -511,6 +583,16 @@ void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx 
     hipLaunchKernelGGL(k_emit, dim3(std::max(1, resident_grid((const void*)&k_emit))), dim3(256), 0, s, nt, oc,
                        payload_dst);
   hipLaunchKernelGGL(k_shard_table, dim3(grid), dim3(256), 0, s, nt, oc, off0, desc, offs, runb);
+}
+void launch_serialize_shard_dyn(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, const int64_t* lay, int rank,
+                                int world, uint8_t* out, uint8_t* runb, bool emit) {
+  if (emit)
+    hipLaunchKernelGGL(k_emit_dyn, dim3(std::max(1, resident_grid((const void*)&k_emit_dyn))), dim3(256), 0, s, nt, oc,
+                       lay, rank, world, out);
+  hipLaunchKernelGGL(k_shard_table_dyn, dim3(grid), dim3(256), 0, s, nt, oc, lay, rank, world, out, runb);
+}
+void launch_layout_out(hipStream_t s, const ResultInfo* info, int64_t* dst) {
+  hipLaunchKernelGGL(k_layout_out, dim3(1), dim3(64), 0, s, info, dst);
 }
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info,
                         const uint32_t* err) {

@@ -269,6 +269,13 @@ void launch_serialize(hipStream_t s, const uint32_t* nt, OutCtx oc);
 // offsets (off0 + local offset) into offs (nullable), one run-flag byte per container into runb (nullable)
 void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* payload_dst, uint64_t off0,
                             uint8_t* desc, uint8_t* offs, uint8_t* runb);
+// the same with the global layout in device memory (lay: world x {containers, payload bytes, has_run}
+// int64); out is laid out as the whole global bitmap, runb one byte per global container (nullable);
+// rank 0 also writes the cookie.  emit = false: the payload is already in place.
+void launch_serialize_shard_dyn(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, const int64_t* lay, int rank,
+                                int world, uint8_t* out, uint8_t* runb, bool emit);
+// dst[0..2] = the pending result's (containers, payload bytes, has_run) from k_place's ResultInfo
+void launch_layout_out(hipStream_t s, const ResultInfo* info, int64_t* dst);
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info,
                         const uint32_t* err);
 void launch_batch_bytes(hipStream_t s, const CDesc* desc, uint64_t n, const uint8_t* payload, unsigned long long* out);

@@ -215,6 +215,19 @@ class Engine:
         check(lib().rbg_ctx_fetch_shard_device(self._ctx, int(total_containers), int(bool(has_run)), int(payload_base),
                                                ptr(desc), ptr(offsets), ptr(runflags), ptr(payload)))
 
+    def result_layout_device(self, dst3):
+        """Enqueue (containers, payload bytes, has_run) of the pending result into a device int64
+        tensor of 3 elements on the engine stream (the input of a device all-gather)."""
+        check(lib().rbg_ctx_result_layout_device(self._ctx, ctypes.c_void_p(dst3.data_ptr())))
+
+    def fetch_shard_device_dyn(self, layout, rank, world, out, runb=None):
+        """Enqueue this rank's slice of the global bitmap, placed by a device-resident layout
+        (world x 3 int64 tensor, key-range order), into `out` (a uint8 tensor laid out as the whole
+        global bitmap) and one run byte per global container into runb.  No host synchronisation."""
+        check(lib().rbg_ctx_fetch_shard_device_dyn(self._ctx, ctypes.c_void_p(layout.data_ptr()), int(rank),
+                                                   int(world), ctypes.c_void_p(out.data_ptr()),
+                                                   ctypes.c_void_p(runb.data_ptr()) if runb is not None else None))
+
     def fetch_shard(self, total_containers, has_run, first_container, payload_base):
         d, o, p = _lib.rbg_buffer(), _lib.rbg_buffer(), _lib.rbg_buffer()
         check(lib().rbg_ctx_fetch_shard(self._ctx, int(total_containers), int(has_run), int(first_container),

@@ -395,3 +395,96 @@ def engine_shard(engine, op, batch, key_lo, key_hi, ids=None):
             engine.wide(op, batch, key_lo, key_hi, ids)
         return engine.fetch().serialize()
     return fn
+
+
+# ---------------------------------------------------------------------------
+# device-resident layout exchange: no host synchronisation inside a sharded step
+# ---------------------------------------------------------------------------
+MAX_SERIALIZED = 8 + 8 * KEYS + 8194 * KEYS  # bounds any global bitmap (header + payload)
+
+
+class DeviceShard:
+    """One rank's part of a key-sharded op whose result stays in HBM (SURVEY §8(e) steps 1-2,
+    all on the device): after the engine's op on this rank's key range, `place()` writes the
+    result's (containers, payload bytes, has_run) into a device tensor on the engine stream
+    (rbg_ctx_result_layout_device), all-gathers it (RCCL on device memory; gloo through the
+    host), and writes this rank's descriptors, offset-table entries, run bytes and payload at
+    their global places in `out`, this rank's buffer laid out as the whole global bitmap
+    (rbg_ctx_fetch_shard_device_dyn).  No host round trip: the step is a chain of stream
+    dependencies.  `gather()` then assembles the global bitmap on rank 0 (point-to-point)."""
+
+    def __init__(self, engine, rank, world, device, comm_device, group=None):
+        import torch
+        self.eng, self.rank, self.world, self.group = engine, rank, world, group
+        self.dev, self.comm = torch.device(device), torch.device(comm_device)
+        self.lay_local = torch.zeros(3, dtype=torch.int64, device=self.dev)
+        self.lay_all = torch.zeros(3 * world, dtype=torch.int64, device=self.dev)
+        self.out = torch.empty(MAX_SERIALIZED, dtype=torch.uint8, device=self.dev)
+        self.runb = torch.empty(KEYS, dtype=torch.uint8, device=self.dev)
+        self.ext = torch.cuda.ExternalStream(engine.stream_ptr, device=self.dev)
+
+    def place(self):
+        import torch
+        self.eng.result_layout_device(self.lay_local)
+        if self.world > 1:
+            dist = _dist()
+            cur = torch.cuda.current_stream(self.dev)
+            cur.wait_stream(self.ext)  # the layout is written
+            if self.comm.type == "cuda":
+                dist.all_gather_into_tensor(self.lay_all, self.lay_local, group=self.group)
+            else:  # gloo rehearsal: the collective runs on host memory
+                parts = [torch.zeros(3, dtype=torch.int64) for _ in range(self.world)]
+                dist.all_gather(parts, self.lay_local.cpu(), group=self.group)
+                self.lay_all.copy_(torch.cat(parts))
+            self.ext.wait_stream(cur)  # the gathered layout is in place
+            lay = self.lay_all
+        else:
+            lay = self.lay_local
+        self.eng.fetch_shard_device_dyn(lay, self.rank, self.world, self.out, self.runb)
+
+    def layout(self):
+        """the last step's GlobalLayout (synchronises)"""
+        self.eng.sync()
+        a = (self.lay_all if self.world > 1 else self.lay_local).cpu().numpy()
+        return GlobalLayout(a.reshape(-1, 3))
+
+    def gather(self):
+        """Rank 0 receives every other rank's slice into its `out` (each rank's buffer has the
+        global layout, so every slice travels to the same place) and packs the run flags.
+        Returns the global bitmap (a uint8 tensor view) on rank 0, None elsewhere."""
+        import torch
+        lay = self.layout()
+        r = self.rank
+
+        def views(rr):
+            nr, f, b = int(lay.n[rr]), int(lay.first[rr]), int(lay.base[rr])
+            v = [self.out[lay.desc_base + 4 * f: lay.desc_base + 4 * (f + nr)]]
+            if lay.offsets:
+                v.append(self.out[lay.off_base + 4 * f: lay.off_base + 4 * (f + nr)])
+            if lay.has_run:
+                v.append(self.runb[f: f + nr])
+            v.append(self.out[lay.header + b: lay.header + b + int(lay.pay[rr])])
+            return [t for t in v if t.numel()]
+
+        on_dev = self.comm.type == "cuda"
+        if self.world > 1:
+            dist = _dist()
+            peer = (lambda x: x) if self.group is None else (lambda x: dist.get_global_rank(self.group, x))
+            if r == 0:
+                recv = [(t, rr) for rr in range(1, self.world) if int(lay.n[rr]) for t in views(rr)]
+                bufs = [(t if on_dev else torch.empty(t.numel(), dtype=torch.uint8), t, rr) for t, rr in recv]
+                for q in _p2p([(dist.irecv, b, peer(rr)) for b, _, rr in bufs], self.group) if bufs else []:
+                    q.wait()
+                if not on_dev:
+                    for b, t, _ in bufs:
+                        t.copy_(b)
+            elif int(lay.n[r]):
+                sends = [t if on_dev else t.cpu() for t in views(r)]
+                for q in _p2p([(dist.isend, t, peer(0)) for t in sends], self.group):
+                    q.wait()
+        if r != 0:
+            return None
+        if lay.has_run and lay.total:
+            self.out[4:4 + lay.flag_bytes] = _pack_flags(self.runb[:lay.total])
+        torch.cuda.synchronize(self.dev)
+        return self.out[:lay.nbytes]

@@ -143,3 +143,43 @@ def test_same_device_assembly(gpu, case):
     if case == "run_and":
         assert rs["has_run"]
         assert got == O.pairwise("and", a, b)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_device_layout_shards(gpu, world):
+    """The device-resident layout exchange (bench's N > 1 headline, shard.DeviceShard): each key
+    shard's (containers, payload bytes, has_run) written to device memory by
+    rbg_ctx_result_layout_device, then every shard placed by rbg_ctx_fetch_shard_device_dyn from
+    that device layout into one buffer laid out as the global bitmap; with the run flags packed,
+    the buffer equals the oracle's whole result (an empty shard included for world 8)."""
+    import torch
+    rng = np.random.default_rng(1200 + world)
+    keys = np.sort(rng.choice(3000, size=70, replace=False))
+    a = _gen.bitmap(rng, keys, p_present=0.9)
+    b = _gen.bitmap(rng, keys, p_present=0.9)
+    e = _engine()
+    ba, bb = e.load([a]), e.load([b])
+    ranges = shard.key_ranges(_key_bytes([a, b]), world)
+    if world == 8:
+        ranges[3] = (ranges[3][0], ranges[3][0])  # an empty key range
+        ranges[4] = (ranges[3][0], ranges[4][1])
+    dev = torch.device("cuda", 0)
+    for op in ["and", "or", "xor", "andnot"]:
+        lay = torch.zeros(3 * world, dtype=torch.int64, device=dev)
+        for r, (lo, hi) in enumerate(ranges):
+            e.pairwise(op, ba, bb, key_lo=lo, key_hi=hi)
+            e.result_layout_device(lay[3 * r: 3 * r + 3])
+        e.sync()
+        out = torch.zeros(shard.MAX_SERIALIZED, dtype=torch.uint8, device=dev)
+        runb = torch.zeros(shard.KEYS, dtype=torch.uint8, device=dev)
+        for r, (lo, hi) in enumerate(ranges):
+            e.pairwise(op, ba, bb, key_lo=lo, key_hi=hi)
+            e.fetch_shard_device_dyn(lay, r, world, out, runb)
+        e.sync()
+        gl = shard.GlobalLayout(lay.cpu().numpy().reshape(-1, 3))
+        if gl.has_run and gl.total:
+            out[4:4 + gl.flag_bytes] = shard._pack_flags(runb[:gl.total])
+        got = bytes(out[:gl.nbytes].cpu().numpy().tobytes())
+        assert got == O.pairwise(op, a, b), op
+    e.release(ba)
+    e.release(bb)

@@ -118,6 +118,52 @@ def test_two_rank_pairwise_assembly(gpu, op):
     assert res == ref
 
 
+def _dyn_worker(rank, world, port, outdir, op):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import roaringbitmap_amd as rb
+        from roaringbitmap_amd import Engine, shard
+        e = Engine(0)
+        rng = np.random.default_rng(12)
+        va = np.concatenate([rng.integers(0, 300 << 16, 400000), np.arange(5 << 16, 9 << 16)])
+        vb = np.concatenate([rng.integers(0, 300 << 16, 400000), np.arange(7 << 16, (7 << 16) + 40000)])
+        a = e.load([rb.RoaringBitmap.from_values(va, run_optimize=True).serialize()])
+        b = e.load([rb.RoaringBitmap.from_values(vb, run_optimize=True).serialize()])
+        lo, hi = [(0, 100), (100, 65536)][rank]
+        ds = shard.DeviceShard(e, rank, world, torch.device("cuda", 0), "cpu")
+        for _ in range(2):  # a repeated step reuses the buffers
+            e.pairwise(op, a, b, key_lo=lo, key_hi=hi)
+            ds.place()
+        out = ds.gather()
+        if rank == 0:
+            e.pairwise(op, a, b)
+            ref = e.fetch().serialize()
+            with open(os.path.join(outdir, "res.bin"), "wb") as f:
+                f.write(bytes(out.cpu().numpy().tobytes()))
+            with open(os.path.join(outdir, "ref.bin"), "wb") as f:
+                f.write(ref)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("op", ["and", "or"])
+def test_two_rank_device_layout(gpu, op):
+    """shard.DeviceShard (the bench's N > 1 headline step): the layout all-gathered from device
+    tensors, each rank's slice placed at its global offsets in its own buffer, gathered on rank 0:
+    equal to the unsharded result byte for byte."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dyn_worker, args=(2, _free_port(), d, op), nprocs=2, join=True)
+        res = open(os.path.join(d, "res.bin"), "rb").read()
+        ref = open(os.path.join(d, "ref.bin"), "rb").read()
+    assert res == ref
+
+
 def _bench(gpus):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(gpus), "--backend", "gloo", "--steps", "2",
            "--warmup", "1", "--c3-n", "64", "--c4-pairs", "2000", "--c5-rows", "2000000", "--no-cpu-baseline"]
@@ -129,8 +175,12 @@ def _bench(gpus):
 def test_bench_two_ranks_rehearsal(gpu):
     one, two = _bench(1), _bench(2)
     assert one["n_gpus"] == 1 and two["n_gpus"] == 2
-    # the key-sharded C2 AND assembles the same bytes as the one-GPU headline (same pair)
-    assert two["extra"]["c2_and_key_sharded"]["result_sha16"] == one["extra"]["result"]["sha16"]
+    # the N > 1 headline is the key-sharded C2 AND (strong scaling): its slices, gathered on GPU 0,
+    # are the same bytes as the one-GPU headline's result (same pair)
+    assert one["scaling"] == two["scaling"] == "strong"
+    assert two["extra"]["c2_strong"]["result_sha16"] == one["extra"]["result"]["sha16"]
+    assert two["extra"]["c2_strong"]["sha_equals_whole_pair_result"] is True
+    assert two["extra"]["c2_and_weak"]["scaling"] == "weak"
     for w in ("c3_uniform_or", "c3_clustered_or", "c3_uniform_and"):
         assert two["extra"][w]["result_serialized_bytes"] == one["extra"][w]["result_serialized_bytes"], w
         assert two["extra"][w]["output_bytes"] == one["extra"][w]["output_bytes"], w
