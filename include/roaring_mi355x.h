@@ -54,8 +54,9 @@ typedef struct rbg_buffer {
   size_t len;
 } rbg_buffer;
 
-/* pairwise ops: RB/RoaringBitmap.java and :377, or :860, xor :1071, andNot :444 */
-enum { RBG_AND = 0, RBG_OR = 1, RBG_XOR = 2, RBG_ANDNOT = 3 };
+/* pairwise ops: RB/RoaringBitmap.java and :377, or :860, xor :1071, andNot :444;
+ * RBG_OR_INPLACE: x1.or(x2) in place (:2481-2523), Container.ior's result types */
+enum { RBG_AND = 0, RBG_OR = 1, RBG_XOR = 2, RBG_ANDNOT = 3, RBG_OR_INPLACE = 4 };
 /* cardinality ops: andCardinality :413, orCardinality :916, xorCardinality :931,
  * andNotCardinality :944 (all Java int, wrapping mod 2^32), intersects :698 (0/1) */
 enum { RBG_CARD_AND = 0, RBG_CARD_OR = 1, RBG_CARD_XOR = 2, RBG_CARD_ANDNOT = 3, RBG_INTERSECTS = 4 };
@@ -90,6 +91,14 @@ enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
 /* static RoaringBitmap.and/or/xor/andNot(RoaringBitmap, RoaringBitmap) -> RoaringBitmap */
 int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len,
                  rbg_buffer* out);
+
+/* In-place instance ops x1.and(x2) / x1.or(x2) / x1.xor(x2) / x1.andNot(x2) (op RBG_AND..RBG_ANDNOT;
+ * RB/RoaringBitmap.java:1272-1296, 2481-2523, 3296-3348, 1346-1382): out = x1's bytes afterwards.
+ * same_object != 0 when x2 is x1 itself (and / or leave it unchanged, xor / andNot clear it).
+ * and / xor / andNot give the static ops' bytes (iand / ixor / iandNot type alike); or follows
+ * Container.ior, whose bitmap | array keeps a full bitmap. */
+int rbg_pairwise_inplace(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int same_object,
+                         rbg_buffer* out);
 
 /* static RoaringBitmap.{and,or,xor,andNot}Cardinality / intersects -> int */
 int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len,

@@ -386,13 +386,19 @@ static Ctr B_andnot_R(const Ctr& b, const Ctr& run) {  // :259-274
   if (r.card > kArrayMax) return r;
   return bitmap_to_array(r);
 }
-static Ctr B_or_A(const Ctr& b, const Ctr& a) {  // :1064-1085
+// BitmapContainer.ior(ArrayContainer) (RB/BitmapContainer.java:740-757): the bits set in place and
+// the bitmap returned as is -- a full result stays a bitmap (no RunContainer.full())
+static Ctr B_ior_A(const Ctr& b, const Ctr& a) {
   Ctr r = b;
   for (uint16_t v : a.vals) {
     uint64_t w = r.words[v >> 6], aft = w | (1ULL << (v & 63));
     r.words[v >> 6] = aft;
     if (w != aft) r.card++;
   }
+  return r;
+}
+static Ctr B_or_A(const Ctr& b, const Ctr& a) {  // :1064-1085
+  Ctr r = B_ior_A(b, a);
   if (r.full()) return run_full();
   return r;
 }
@@ -933,6 +939,15 @@ Ctr c_andnot(const Ctr& a, const Ctr& b) {
   }
 }
 
+// In-place OR of RoaringBitmap.or(RoaringBitmap) (RB/RoaringBitmap.java:2481-2523): Container.ior.  Its
+// result types are the static or's (A.ior(A) :726-746 = A.or(A); A.ior(B|R) = x.or(this) :748-756;
+// B.ior(B|R) :760-785 and R.ior(A|B|R) :1462-1550 end in the same types as or) except
+// BitmapContainer.ior(ArrayContainer), which keeps a full bitmap (B_ior_A).
+Ctr c_ior(const Ctr& a, const Ctr& b) {
+  if (a.kind == BITMAP && b.kind == ARRAY) return B_ior_A(a, b);
+  return c_or(a, b);
+}
+
 // Buffer package (RB/buffer/): MappeableContainer.and / andNot dispatch like the heap containers and
 // type their results alike (MappeableArrayContainer.java:287-384, MappeableBitmapContainer.java:152-348,
 // MappeableRunContainer.java:398-663) -- except run AND run and run ANDNOT run, which return the
@@ -1229,6 +1244,9 @@ static Bitmap union_like(const Bitmap& x1, const Bitmap& x2, F op, bool drop_emp
 }
 
 Bitmap op_or(const Bitmap& x1, const Bitmap& x2) { return union_like(x1, x2, c_or, false); }
+// x1.or(x2) in place (RB/RoaringBitmap.java:2481-2523): the same key loop (x2-only containers
+// cloned in, x1-only kept), Container.ior per matched key
+Bitmap op_ior(const Bitmap& x1, const Bitmap& x2) { return union_like(x1, x2, c_ior, false); }
 Bitmap op_xor(const Bitmap& x1, const Bitmap& x2) { return union_like(x1, x2, c_xor, true); }
 
 int32_t op_or_card(const Bitmap& x1, const Bitmap& x2) {  // :916-920 (int arithmetic)

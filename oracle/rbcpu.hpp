@@ -95,6 +95,8 @@ std::vector<uint32_t> bitmap_values(const Bitmap& b);
 // static pairwise ops, RB/RoaringBitmap.java
 Bitmap op_and(const Bitmap& x1, const Bitmap& x2);        // :377-401
 Bitmap op_or(const Bitmap& x1, const Bitmap& x2);         // :860-902
+Bitmap op_ior(const Bitmap& x1, const Bitmap& x2);        // x1.or(x2) in place, :2481-2523
+Ctr c_ior(const Ctr& a, const Ctr& b);                    // Container.ior
 Bitmap op_xor(const Bitmap& x1, const Bitmap& x2);        // :1071-1118
 Bitmap op_andnot(const Bitmap& x1, const Bitmap& x2);     // :444-473
 int32_t op_and_card(const Bitmap& x1, const Bitmap& x2);  // :413-434

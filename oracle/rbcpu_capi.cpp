@@ -48,7 +48,8 @@ extern "C" {
 void rbo_free(void* p) { std::free(p); }
 
 // op: 0 and, 1 or, 2 xor, 3 andNot   (RB/RoaringBitmap.java:377,860,1071,444);
-// 4 and, 5 andNot of the buffer package (ImmutableRoaringBitmap.and :299, andNot :441)
+// 4 and, 5 andNot of the buffer package (ImmutableRoaringBitmap.and :299, andNot :441);
+// 6 x1.or(x2) in place (RB/RoaringBitmap.java:2481)
 int rbo_pairwise(int op, const uint8_t* a, size_t an, const uint8_t* b, size_t bn, uint8_t** out,
                  size_t* out_len) {
   Bitmap x, y;
@@ -62,6 +63,7 @@ int rbo_pairwise(int op, const uint8_t* a, size_t an, const uint8_t* b, size_t b
     case 3: return emit(op_andnot(x, y), out, out_len);
     case 4: return emit(op_and_buf(x, y), out, out_len);
     case 5: return emit(op_andnot_buf(x, y), out, out_len);
+    case 6: return emit(op_ior(x, y), out, out_len);
   }
   return ERR_ARG;
 }

@@ -17,7 +17,7 @@ RBG_ERR_ILLEGAL_ARGUMENT = -3
 RBG_ERR_DEVICE = -4
 RBG_ERR_OUT_OF_MEMORY = -5
 
-OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3}
+OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "ior": 4}  # ior: x1.or(x2) in place (Container.ior types)
 CARD_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
 WIDE_OP = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5, "parallel_or": 6,
            "parallel_xor": 7, "buffer_or_mutable": 8, "horizontal_or": 9, "horizontal_xor": 10,
@@ -41,7 +41,7 @@ EXPORTED = [
     "rbg_bsi_compare", "rbg_bsi_sum", "rbg_ctx_bsi", "rbg_ctx_bsi_sums", "rbg_ctx_bsi_sums_device", "rbg_ctx_batch_minmax",
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
     "rbg_ctx_fetch_shard_device", "rbg_bsi_compare_buffer", "rbg_ctx_bsi_buffer",
-    "rbg_ctx_result_layout_device", "rbg_ctx_fetch_shard_device_dyn",
+    "rbg_ctx_result_layout_device", "rbg_ctx_fetch_shard_device_dyn", "rbg_pairwise_inplace",
 ]
 
 _lib = None
@@ -56,6 +56,7 @@ def _declare(L):
     vp = ctypes.c_void_p
     L.rbg_pairwise.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, buf]
     L.rbg_pairwise_card.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, P(i32)]
+    L.rbg_pairwise_inplace.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, ctypes.c_int, buf]
     L.rbg_wide.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), P(i32), sz, buf]
     L.rbg_wide_card.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), sz, P(i32)]
     L.rbg_batch_and_card.argtypes = [sz, P(ctypes.c_char_p), P(sz), P(ctypes.c_char_p), P(sz), P(i32)]

@@ -51,7 +51,43 @@ class RoaringBitmapSliceIndex:
         nbits = (len(bin(mx)) - 2) if values.size else 0
         ebm = RoaringBitmap.from_values(columns, run_optimize)
         ba = [RoaringBitmap.from_values(columns[(values >> i) & 1 == 1], run_optimize) for i in range(nbits)]
-        return cls(ebm, ba, mn, mx)
+        obj = cls(ebm, ba, mn, mx)
+        obj.runOptimized = bool(run_optimize)
+        return obj
+
+    def merge(self, otherBsi):
+        """BSI/:379-405 ("designed for distributed computing"; the two indexes hold disjoint
+        columns): slice-wise RoaringBitmap.or, runOptimize when either side was run-optimized
+        (one device pass over all slices), the existence bitmaps united in place (x1.or(x2),
+        Container.ior types) and min / max widened.  The buffer MutableBitSliceIndex.merge is the
+        same steps over MutableRoaringBitmap (bsi/.../buffer/MutableBitSliceIndex.java:270-298)."""
+        if otherBsi is None or otherBsi.ebM.isEmpty():
+            return
+        if RoaringBitmap.intersects(self.ebM, otherBsi.ebM):
+            raise IllegalArgumentException("merge can be used only in bsiA  bsiB  is null")
+        depth = max(self.bitCount(), otherBsi.bitCount())
+        new = []
+        for i in range(depth):
+            cur = self.bA[i] if i < len(self.bA) else RoaringBitmap()
+            other = otherBsi.bA[i] if i < len(otherBsi.bA) else RoaringBitmap()
+            new.append(RoaringBitmap.or_(cur, other))
+        if self.runOptimized or otherBsi.runOptimized:
+            run_optimize_many(new)
+        self.bA = new
+        self.ebM.or_(otherBsi.ebM)  # in place
+        self.runOptimized = self.runOptimized or otherBsi.runOptimized
+        self.maxValue = max(self.maxValue, otherBsi.maxValue)
+        self.minValue = min(self.minValue, otherBsi.minValue)
+
+    def getValue(self, columnId):
+        """BSI/ getValue(columnId) -> (value, exists), read from the serialized bitmaps on the host"""
+        if int(columnId) not in set(self.ebM.toArray().tolist()):
+            return 0, False
+        v = 0
+        for i, b in enumerate(self.bA):
+            if int(columnId) in set(b.toArray().tolist()):
+                v |= 1 << i
+        return v, True
 
     def runOptimize(self):
         """BSI/:141-150: runOptimize of ebM and of every slice (one device pass over all of them)."""

@@ -162,6 +162,7 @@ struct Ctx {
   // buffer-package BSI: owenGreatEqual's orInput types / task keys / chain order, and the arena of
   // result run containers above 2047 runs (BigRuns; big_ctl = {bytes used, overflow})
   DevBuf owen_tb, owen_keys, owen_ord, big, big_ctl;
+  DevBuf ones;  // 8192 bytes of 0xFF: the full bitmap container of an in-place OR (k_ior_fix)
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   DevBuf order;                     // horizontal_*: chain order of every key segment
   DevBuf ro_info, ro_size, ro_part, ro_flags;  // runOptimize scratch (kept: no allocation per call)
@@ -701,8 +702,24 @@ static int operand(Batch* b, size_t i, const uint16_t** keys, const CDesc** desc
   return RBG_OK;
 }
 
+// op RBG_OR_INPLACE: x1.or(x2) in place (RB/RoaringBitmap.java:2481-2523), the OR with Container.ior's
+// types (k_ior_fix)
 static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only, int key_lo = 0,
                         int key_hi = kMaxKeys) {
+  if (op == RBG_OR_INPLACE && !card_only) {
+    CHK(ctx_pairwise(c, OP_OR, ia, ma, ib, mb, false, key_lo, key_hi));
+    if (!c->ones.p) {
+      CHK(c->ones.ensure(8192));
+      HIPCHK(hipMemsetAsync(c->ones.p, 0xFF, 8192, c->stream));
+    }
+    Batch *A, *B;
+    CHK(get_batch(c, ia, &A));
+    CHK(get_batch(c, ib, &B));
+    launch_ior_fix(c->stream, c->ntasks.as<uint32_t>(), c->recs.as<ORec>(), A->key_off.as<uint32_t>(),
+                   A->desc.as<CDesc>(), B->key_off.as<uint32_t>(), B->desc.as<CDesc>(), c->ones.as<uint8_t>());
+    HIPCHK(hipGetLastError());
+    return RBG_OK;
+  }
   if (op < 0 || op > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
   key_lo = std::max(0, key_lo);
   key_hi = std::min(kMaxKeys, key_hi);
@@ -1529,7 +1546,7 @@ int rbg_set_devices(uint64_t mask) {
 }
 
 int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, rbg_buffer* out) {
-  if (!out || op < 0 || op > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!out || op < 0 || op > RBG_OR_INPLACE) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
@@ -1540,6 +1557,35 @@ int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_
   g.ids.push_back(ib);
   CHK(ctx_pairwise(c, op, ia, 0, ib, 0, false));
   return ctx_fetch(c, out);
+}
+
+static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out);
+int rbg_pairwise_inplace(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int same_object,
+                         rbg_buffer* out) {
+  if (!out || op < 0 || op > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (same_object) {
+    // x1.and(x1) / x1.or(x1) return at once (x1 unchanged); x1.xor(x1) / x1.andNot(x1) clear it
+    // (RB/RoaringBitmap.java:1271, 2482, 3297-3300, 1347-1350)
+    if (op == RBG_XOR || op == RBG_ANDNOT) {
+      static const uint8_t kEmpty[8] = {0x3A, 0x30, 0, 0, 0, 0, 0, 0};
+      uint8_t* p = (uint8_t*)std::malloc(8);
+      if (!p) return RBG_ERR_OUT_OF_MEMORY;
+      std::memcpy(p, kEmpty, 8);
+      out->data = p;
+      out->len = 8;
+      return RBG_OK;
+    }
+    Ctx* c;
+    CHK(tl_ctx(&c));
+    BatchGuard g{c, {}};
+    int32_t ia;
+    CHK(ctx_load(c, &a, &a_len, 1, &ia));  // validated like any input, then its own bytes back
+    g.ids.push_back(ia);
+    return ctx_batch_fetch(c, ia, 0, out);
+  }
+  // x1.and / xor / andNot(x2) in place type like the static ops (Container.iand / ixor / iandNot
+  // end in the same container types); x1.or(x2) is Container.ior's
+  return rbg_pairwise(op == RBG_OR ? RBG_OR_INPLACE : op, a, a_len, b, b_len, out);
 }
 
 int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int32_t* out) {

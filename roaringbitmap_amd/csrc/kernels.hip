@@ -516,6 +516,32 @@ __global__ __launch_bounds__(256) void k_shard_table_dyn(const uint32_t* __restr
     if (runb) runb[idx] = r.kind == DK_R ? 1 : 0;
   }
 }
+// x1.or(x2) in place (RB/RoaringBitmap.java:2481-2523): Container.ior types like the static or,
+// except BitmapContainer.ior(ArrayContainer) (RB/BitmapContainer.java:740-757), which keeps a full
+// result a bitmap: such keys' R.full records become an 8 KiB bitmap of ones.  Runs after the OR's
+// compute kernel, before placement.  koa / kob: the operands' key CSR (one container per key).
+__global__ __launch_bounds__(256) void k_ior_fix(const uint32_t* __restrict__ n_tasks, ORec* __restrict__ recs,
+                                                 const uint32_t* __restrict__ koa, const CDesc* __restrict__ da,
+                                                 const uint32_t* __restrict__ kob, const CDesc* __restrict__ db,
+                                                 const uint8_t* __restrict__ ones) {
+  const uint32_t nt = *n_tasks;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    const ORec r = recs[t];
+    if (!r.keep || r.kind != DK_R || r.card != 65536) continue;
+    const uint32_t ia = koa[r.key], ib = kob[r.key];
+    if (koa[r.key + 1] == ia || kob[r.key + 1] == ib) continue;
+    if (da[ia].kind == DK_B && db[ib].kind == DK_A) {
+      recs[t].kind = DK_B;
+      recs[t].src = reinterpret_cast<uint64_t>(ones);
+      recs[t].ser_len = 8192;
+    }
+  }
+}
+void launch_ior_fix(hipStream_t s, const uint32_t* nt, ORec* recs, const uint32_t* koa, const CDesc* da,
+                    const uint32_t* kob, const CDesc* db, const uint8_t* ones) {
+  hipLaunchKernelGGL(k_ior_fix, dim3(256), dim3(256), 0, s, nt, recs, koa, da, kob, db, ones);
+}
+
 // the pending result's (containers, payload bytes, has_run) as int64, from k_place's ResultInfo
 __global__ void k_layout_out(const ResultInfo* __restrict__ info, int64_t* __restrict__ dst) {
   if (threadIdx.x == 0) {

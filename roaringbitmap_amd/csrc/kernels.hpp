@@ -274,6 +274,10 @@ void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx 
 // rank 0 also writes the cookie.  emit = false: the payload is already in place.
 void launch_serialize_shard_dyn(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, const int64_t* lay, int rank,
                                 int world, uint8_t* out, uint8_t* runb, bool emit);
+// in-place OR's types after an OR (x1.or(x2), RB/RoaringBitmap.java:2481-2523): a full result of
+// bitmap x1 | array x2 stays a bitmap (ones: 8192 bytes of 0xFF)
+void launch_ior_fix(hipStream_t s, const uint32_t* nt, ORec* recs, const uint32_t* koa, const CDesc* da,
+                    const uint32_t* kob, const CDesc* db, const uint8_t* ones);
 // dst[0..2] = the pending result's (containers, payload bytes, has_run) from k_place's ResultInfo
 void launch_layout_out(hipStream_t s, const ResultInfo* info, int64_t* dst);
 void launch_reduce_card(hipStream_t s, const uint32_t* task_card, const uint32_t* nt, ResultInfo* info,

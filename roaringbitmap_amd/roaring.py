@@ -28,6 +28,51 @@ def _int32(x):
     return int(np.int64(x).astype(np.int32)) if -(1 << 63) <= x < (1 << 63) else int(x)
 
 
+class _StaticOrInPlace:
+    """Java overloads one name with a static op and an in-place instance op: RoaringBitmap.and(x1, x2)
+    (RB/RoaringBitmap.java:377) and x1.and(x2) (:1272).  On the class this is the static form; on an
+    instance with one argument it modifies the instance (with two, Java calls the static one)."""
+
+    def __init__(self, static, op):
+        self.static, self.op = static, op
+        self.__doc__ = static.__doc__
+
+    def __get__(self, obj, objtype=None):
+        if obj is None:
+            return self.static
+
+        def call(*args):
+            if len(args) != 1:
+                return self.static(*args)
+            obj._inplace(self.op, args[0])
+
+        call.__doc__ = self.static.__doc__
+        return call
+
+
+def _s_and(x1, x2):
+    """static and(x1, x2), RB/RoaringBitmap.java:377-401; x1.and(x2) in place :1272-1296"""
+    return RoaringBitmap._pair("and", x1, x2)
+
+
+def _s_or(*bitmaps):
+    """static or(x1, x2) (:860-902); any other arity is or(RoaringBitmap...) (:844) = FastAggregation.or;
+    x1.or(x2) in place :2481-2523 (Container.ior's types)"""
+    if len(bitmaps) == 2:
+        return RoaringBitmap._pair("or", bitmaps[0], bitmaps[1])
+    return FastAggregation.or_(*bitmaps)
+
+
+def _s_xor(x1, x2):
+    """static xor(x1, x2), :1071-1118; x1.xor(x2) in place :3296-3348"""
+    return RoaringBitmap._pair("xor", x1, x2)
+
+
+def _s_andnot(x1, x2):
+    """static andNot(x1, x2), :444-473; x1.andNot(x2) in place :1346-1382"""
+    return RoaringBitmap._pair("andnot", x1, x2)
+
+
 class RoaringBitmap:
     __slots__ = ("_buf", "_lcard")
 
@@ -133,27 +178,18 @@ class RoaringBitmap:
                                       ctypes.byref(out)))
         return out.value
 
-    @staticmethod
-    def and_(x1, x2):
-        """static and(x1, x2), RB/RoaringBitmap.java:377-401"""
-        return RoaringBitmap._pair("and", x1, x2)
+    and_ = _StaticOrInPlace(_s_and, "and")
+    or_ = _StaticOrInPlace(_s_or, "or")
+    xor = _StaticOrInPlace(_s_xor, "xor")
+    andNot = _StaticOrInPlace(_s_andnot, "andnot")
 
-    @staticmethod
-    def or_(*bitmaps):
-        """static or(x1, x2) (:860-902); any other arity is or(RoaringBitmap...) (:844) = FastAggregation.or"""
-        if len(bitmaps) == 2:
-            return RoaringBitmap._pair("or", bitmaps[0], bitmaps[1])
-        return FastAggregation.or_(*bitmaps)
-
-    @staticmethod
-    def xor(x1, x2):
-        """static xor(x1, x2), :1071-1118"""
-        return RoaringBitmap._pair("xor", x1, x2)
-
-    @staticmethod
-    def andNot(x1, x2):
-        """static andNot(x1, x2), :444-473"""
-        return RoaringBitmap._pair("andnot", x1, x2)
+    def _inplace(self, op, x2):
+        """x1.and / or / xor / andNot(x2) in place (rbg_pairwise_inplace); x2 may be x1 itself"""
+        b = _lib.rbg_buffer()
+        check(lib().rbg_pairwise_inplace(_lib.OP[op], self._buf, len(self._buf), x2._buf, len(x2._buf),
+                                         int(x2 is self), ctypes.byref(b)))
+        self._buf = take(b)
+        self._lcard = None
 
     @staticmethod
     def andCardinality(x1, x2) -> int:
@@ -181,8 +217,8 @@ class RoaringBitmap:
         return RoaringBitmap._card("intersects", x1, x2) != 0
 
 
-setattr(RoaringBitmap, "and", RoaringBitmap.and_)
-setattr(RoaringBitmap, "or", RoaringBitmap.or_)
+setattr(RoaringBitmap, "and", RoaringBitmap.__dict__["and_"])
+setattr(RoaringBitmap, "or", RoaringBitmap.__dict__["or_"])
 
 
 def _identity_ids(bitmaps):

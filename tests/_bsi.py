@@ -19,8 +19,9 @@ OPS = ("EQ", "NEQ", "LE", "LT", "GE", "GT", "RANGE")
 class BSI:
     """ebM, bA (slice 0 = least significant bit), minValue, maxValue."""
 
-    def __init__(self, ebm, slices, min_value, max_value):
+    def __init__(self, ebm, slices, min_value, max_value, run_optimized=False):
         self.ebm, self.ba, self.min, self.max = ebm, list(slices), int(min_value), int(max_value)
+        self.run_optimized = bool(run_optimized)
 
     @classmethod
     def from_columns(cls, columns, values, run_optimize=False):
@@ -43,7 +44,39 @@ class BSI:
         nbits = len(bin(mx)) - 2 if len(values) else 0
         ebm = O.from_values(columns, run_optimize)
         ba = [O.from_values(columns[(values >> i) & 1 == 1], run_optimize) for i in range(nbits)]
-        return cls(ebm, ba, mn, mx)
+        return cls(ebm, ba, mn, mx, run_optimize)
+
+    # BSI/:379-405 (the buffer MutableBitSliceIndex.merge, BBSI mutable :270-298, is the same steps over
+    # MutableRoaringBitmap.or (static types as the heap's), runOptimize and the in-place ebM.or)
+    def merge(self, other):
+        if other is None or O.stats(other.ebm)["card"] == 0:
+            return
+        if O.pairwise_card("intersects", self.ebm, other.ebm):
+            raise ValueError("merge can be used only in bsiA  bsiB  is null")
+        depth = max(self.bit_count(), other.bit_count())
+        new = []
+        for i in range(depth):
+            cur = self.ba[i] if i < len(self.ba) else EMPTY
+            oth = other.ba[i] if i < len(other.ba) else EMPTY
+            x = O.pairwise("or", cur, oth)  # RoaringBitmap.or(current, other)
+            if self.run_optimized or other.run_optimized:
+                x = O.run_optimize(x)
+            new.append(x)
+        self.ba = new
+        self.ebm = O.pairwise("ior", self.ebm, other.ebm)  # this.ebM.or(otherBsi.ebM), in place
+        self.run_optimized = self.run_optimized or other.run_optimized
+        self.max = max(self.max, other.max)
+        self.min = min(self.min, other.min)
+
+    def get_value(self, column):
+        """BSI/ getValue: (value, exists)"""
+        if column not in set(O.to_values(self.ebm).tolist()):
+            return 0, False
+        v = 0
+        for i, b in enumerate(self.ba):
+            if column in set(O.to_values(b).tolist()):
+                v |= 1 << i
+        return v, True
 
     def bit_count(self):
         return len(self.ba)

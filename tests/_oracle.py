@@ -89,7 +89,8 @@ def _check(st):
         raise OracleError(st)
 
 
-OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "and_buf": 4, "andnot_buf": 5}  # *_buf: ImmutableRoaringBitmap ops
+OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "and_buf": 4, "andnot_buf": 5,  # *_buf: ImmutableRoaringBitmap ops
+       "ior": 6}  # x1.or(x2) in place
 CARD_OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
 WIDE_OPS = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5,
             "parallel_or": 6, "parallel_xor": 7, "buffer_or_mutable": 8, "horizontal_or": 9, "horizontal_xor": 10,
