@@ -280,6 +280,47 @@ def decode_c2(eng, a, steps):
             "GBps": round(len(x) / dt / 1e9, 2)}
 
 
+def c2_oneshot(eng, a, b, steps):
+    """The drop-in path a JNI caller takes (rbg_pairwise, RB/RoaringBitmap.java:377 with
+    serialize / deserialize at the boundary, :3017-3019 / :1805-1811): the two serialized C2
+    operands from host memory to the serialized result in host memory, PCIe included.  Split:
+    the upload + device decode of both operands (one Engine.load of the pair), the op with its
+    serialization, and the download."""
+    import roaringbitmap_amd as rb
+    xa = eng.batch_fetch(a).serialize()
+    xb = eng.batch_fetch(b).serialize()
+    ra, rbm = rb.RoaringBitmap(xa), rb.RoaringBitmap(xb)
+    rb.RoaringBitmap.and_(ra, rbm)  # warm the one-shot context
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = rb.RoaringBitmap.and_(ra, rbm)
+    one = (time.perf_counter() - t0) / steps
+    ta = tb = top = tdn = 0.0
+    for _ in range(steps):
+        t1 = time.perf_counter()
+        la, lb = eng.load_pair(xa, xb)
+        t2 = time.perf_counter()
+        eng.pairwise("and", la, lb)
+        eng.serialize()
+        eng.sync()
+        t3 = time.perf_counter()
+        res = eng.fetch().serialize()
+        t4 = time.perf_counter()
+        eng.release(la)
+        eng.release(lb)
+        ta += t2 - t1
+        top += t3 - t2
+        tdn += t4 - t3
+    assert res == out.serialize()
+    n = float(steps)
+    return {"workload": "rbg_pairwise(AND) from host bytes to host bytes on the C2 pair (PCIe included)",
+            "ms_per_call": round(one * 1e3, 3), "input_MB": round((len(xa) + len(xb)) / 1e6, 1),
+            "output_MB": round(len(res) / 1e6, 1),
+            "split_ms": {"upload_decode_both": round(ta / n * 1e3, 3), "op_serialize": round(top / n * 1e3, 3),
+                         "download": round(tdn / n * 1e3, 3)},
+            "pcie_inclusive_input_GBps": round((len(xa) + len(xb)) / one / 1e9, 2)}
+
+
 def run_optimize_c2(eng, a, sa, steps):
     """RoaringBitmap.runOptimize of one C2 operand on the device (plan, scan, write into a new
     batch); wall time per call, new-batch allocation and the host read-back of the totals included."""
@@ -698,6 +739,8 @@ def main():
     if args.c3_n > 0 or args.c4_pairs > 0 or args.c5_rows > 0:
         run_extra("run_optimize_c2", lambda: run_optimize_c2(eng, a, sa, ks))
         run_extra("decode_c2", lambda: decode_c2(eng, a, ks))
+        if rank == 0:
+            run_extra("c2_and_oneshot", lambda: c2_oneshot(eng, a, b, max(3, ks // 2)))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

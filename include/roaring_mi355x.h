@@ -189,6 +189,9 @@ int rbg_ctx_sync(rbg_ctx* ctx);
 int rbg_ctx_profile(rbg_ctx* ctx, int max_ops);
 int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops);
 
+/* n serialized bitmaps in one upload, each decoded into a single-bitmap batch of its own
+ * (ids[i]): the operands of pairwise ops, staged and copied to the device together. */
+int rbg_ctx_load_separate(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* ids);
 /* Parse + upload n serialized bitmaps as one batch; returns a batch id >= 0. */
 int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n,
                  int32_t* batch);

@@ -42,6 +42,7 @@ EXPORTED = [
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
     "rbg_ctx_fetch_shard_device", "rbg_bsi_compare_buffer", "rbg_ctx_bsi_buffer",
     "rbg_ctx_result_layout_device", "rbg_ctx_fetch_shard_device_dyn", "rbg_pairwise_inplace",
+    "rbg_ctx_load_separate",
 ]
 
 _lib = None
@@ -75,6 +76,7 @@ def _declare(L):
     L.rbg_ctx_stream.restype = vp
     L.rbg_ctx_sync.argtypes = [vp]
     L.rbg_ctx_load.argtypes = [vp, P(ctypes.c_char_p), P(sz), sz, P(i32)]
+    L.rbg_ctx_load_separate.argtypes = [vp, P(ctypes.c_char_p), P(sz), sz, P(i32)]
     L.rbg_ctx_synth.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, sz, ctypes.c_int, ctypes.c_int, P(i32)]
     L.rbg_ctx_release.argtypes = [vp, i32]
     L.rbg_ctx_batch_stats.argtypes = [vp, i32, P(ctypes.c_int64)]

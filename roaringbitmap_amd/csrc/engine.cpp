@@ -455,27 +455,37 @@ static int stage_upload(Ctx* c, const uint8_t* const* bufs, const size_t* lens, 
   return st;
 }
 
-// key_major: containers sorted by (key, input) with a key CSR (operands of every op);
-// otherwise input order (bitmap-major, batched andCardinality)
-static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, bool key_major,
-                         int32_t* out_id) {
+// The serialized inputs at 16 B aligned offsets of one upload into c->raw: off[i] (host)
+static int ctx_upload_raw(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n,
+                          std::vector<uint64_t>* off) {
   if (n && (!bufs || !lens)) return RBG_ERR_ILLEGAL_ARGUMENT;
   for (size_t i = 0; i < n; i++)
     if (!bufs[i] && lens[i]) return RBG_ERR_ILLEGAL_ARGUMENT;
-  DecBufs& d = c->dec;
-  hipStream_t s = c->stream;
-  // inputs at 16 B aligned offsets of one upload
-  std::vector<uint64_t> meta(2 * n + 2, 0);  // in_off[n], in_len[n]
+  off->assign(n, 0);
   uint64_t raw_bytes = 0;
   for (size_t i = 0; i < n; i++) {
-    meta[i] = raw_bytes;
-    meta[n + i] = lens[i];
+    (*off)[i] = raw_bytes;
     raw_bytes = round16(raw_bytes + lens[i]);
   }
   CHK(c->raw.ensure(raw_bytes + 64));
   CHK(pinned_ensure(c, raw_bytes + 64));
-  CHK(stage_upload(c, bufs, lens, n, meta.data(), raw_bytes));
-  dbg(s, "load: host staging copy");
+  CHK(stage_upload(c, bufs, lens, n, off->data(), raw_bytes));
+  dbg(c->stream, "load: host staging copy");
+  return RBG_OK;
+}
+
+// Device decode of n uploaded inputs (c->raw at off[i], len[i] bytes) into one batch.
+// key_major: containers sorted by (key, input) with a key CSR (operands of every op);
+// otherwise input order (bitmap-major, batched andCardinality)
+static int ctx_decode_raw(Ctx* c, const uint64_t* off, const size_t* lens, size_t n, bool key_major,
+                          int32_t* out_id) {
+  DecBufs& d = c->dec;
+  hipStream_t s = c->stream;
+  std::vector<uint64_t> meta(2 * n + 2, 0);  // in_off[n], in_len[n]
+  for (size_t i = 0; i < n; i++) {
+    meta[i] = off[i];
+    meta[n + i] = lens[i];
+  }
   CHK(d.meta.ensure(8 * (2 * n + 2)));
   CHK(d.head.ensure(sizeof(DecHead) * n + 16));
   CHK(d.nctr.ensure(8 * n + 16));
@@ -598,8 +608,29 @@ static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens,
   return RBG_OK;
 }
 
+static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, bool key_major,
+                         int32_t* out_id) {
+  std::vector<uint64_t> off;
+  CHK(ctx_upload_raw(c, bufs, lens, n, &off));
+  return ctx_decode_raw(c, off.data(), lens, n, key_major, out_id);
+}
+
 static int ctx_load(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out_id) {
   return ctx_load_impl(c, bufs, lens, n, true, out_id);
+}
+
+// n serialized bitmaps in ONE upload, each decoded into a batch of its own (the operands of a
+// pairwise op: one staging pass and DMA for both); ids[i] = batch of bitmap i
+static int ctx_load_separate(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* ids) {
+  std::vector<uint64_t> off;
+  CHK(ctx_upload_raw(c, bufs, lens, n, &off));
+  BatchGuard g{c, {}};
+  for (size_t i = 0; i < n; i++) {
+    CHK(ctx_decode_raw(c, &off[i], &lens[i], 1, true, &ids[i]));
+    g.ids.push_back(ids[i]);
+  }
+  g.ids.clear();
+  return RBG_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1461,6 +1492,59 @@ static int ctx_info(Ctx* c, ResultInfo* ri) {
   return RBG_OK;
 }
 
+// Device -> host copy of a large result into caller (pageable) memory: 32 MiB groups DMA'd into
+// the context's pinned staging, each copied out by worker threads as soon as its event fires, so
+// the DMA of the next groups overlaps the host copies (the mirror of stage_upload).
+static int download_staged(Ctx* c, const uint8_t* dev, uint64_t bytes, uint8_t* dst) {
+  constexpr uint64_t kGroup = 32ull << 20;
+  hipStream_t s = c->stream;
+  if (bytes <= kGroup) {
+    HIPCHK(hipMemcpyAsync(dst, dev, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return RBG_OK;
+  }
+  CHK(pinned_ensure(c, bytes + 64));
+  uint8_t* pin = reinterpret_cast<uint8_t*>(c->pinned);
+  const uint32_t groups = (uint32_t)((bytes + kGroup - 1) / kGroup);
+  std::vector<hipEvent_t> ev(groups);
+  for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  int st = RBG_OK;
+  for (uint32_t g = 0; g < groups; g++) {
+    const uint64_t lo = (uint64_t)g * kGroup, hi = std::min<uint64_t>(bytes, lo + kGroup);
+    if (hipMemcpyAsync(pin + lo, dev + lo, hi - lo, hipMemcpyDeviceToHost, s) != hipSuccess ||
+        hipEventRecord(ev[g], s) != hipSuccess) {
+      set_err("device-to-host copy of the result failed");
+      st = RBG_ERR_DEVICE;
+      break;
+    }
+  }
+  if (st == RBG_OK) {
+    std::atomic<uint32_t> next{0};
+    std::atomic<int> bad{0};
+    const int nthr = (int)std::min<unsigned>(8, std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthr; t++)
+      th.emplace_back([&]() {
+        for (uint32_t g; (g = next.fetch_add(1)) < groups;) {
+          if (hipEventSynchronize(ev[g]) != hipSuccess) {
+            bad.store(1);
+            continue;
+          }
+          const uint64_t lo = (uint64_t)g * kGroup, hi = std::min<uint64_t>(bytes, lo + kGroup);
+          std::memcpy(dst + lo, pin + lo, hi - lo);
+        }
+      });
+    for (auto& x : th) x.join();
+    if (bad.load()) {
+      set_err("device-to-host copy of the result failed");
+      st = RBG_ERR_DEVICE;
+    }
+  }
+  (void)hipStreamSynchronize(s);
+  for (auto& e : ev) (void)hipEventDestroy(e);
+  return st;
+}
+
 static int ctx_fetch(Ctx* c, rbg_buffer* out) {
   if (c->last != 1) {
     set_err("no serialized result pending");
@@ -1471,8 +1555,11 @@ static int ctx_fetch(Ctx* c, rbg_buffer* out) {
   CHK(ctx_info(c, &ri));
   uint8_t* p = (uint8_t*)std::malloc(ri.total ? ri.total : 1);
   if (!p) return RBG_ERR_OUT_OF_MEMORY;
-  HIPCHK(hipMemcpyAsync(p, c->result.as<uint8_t>() + ri.start, ri.total, hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
+  const int st = download_staged(c, c->result.as<uint8_t>() + ri.start, ri.total, p);
+  if (st != RBG_OK) {
+    std::free(p);
+    return st;
+  }
   out->data = p;
   out->len = ri.total;
   return RBG_OK;
@@ -1550,12 +1637,12 @@ int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
-  int32_t ia, ib;
-  CHK(ctx_load(c, &a, &a_len, 1, &ia));
-  g.ids.push_back(ia);
-  CHK(ctx_load(c, &b, &b_len, 1, &ib));
-  g.ids.push_back(ib);
-  CHK(ctx_pairwise(c, op, ia, 0, ib, 0, false));
+  const uint8_t* bufs[2] = {a, b};
+  const size_t lens[2] = {a_len, b_len};
+  int32_t ids[2];
+  CHK(ctx_load_separate(c, bufs, lens, 2, ids));  // one upload for both operands
+  g.ids = {ids[0], ids[1]};
+  CHK(ctx_pairwise(c, op, ids[0], 0, ids[1], 0, false));
   return ctx_fetch(c, out);
 }
 
@@ -1821,6 +1908,11 @@ int rbg_ctx_sync(rbg_ctx* ctx) {
   HIPCHK(hipSetDevice(ctx->c.device));
   HIPCHK(hipStreamSynchronize(ctx->c.stream));
   return RBG_OK;
+}
+int rbg_ctx_load_separate(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* ids) {
+  if (!ctx || !ids) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HIPCHK(hipSetDevice(ctx->c.device));
+  return ctx_load_separate(&ctx->c, bufs, lens, n, ids);
 }
 int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* batch) {
   HIPCHK(hipSetDevice(ctx->c.device));

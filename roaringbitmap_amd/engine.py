@@ -65,6 +65,15 @@ class Engine:
         check(lib().rbg_ctx_load(self._ctx, arr, lens, len(bufs), ctypes.byref(out)))
         return out.value
 
+    def load_pair(self, *bitmaps):
+        """Upload several serialized bitmaps at once, each decoded into a batch of its own
+        (rbg_ctx_load_separate): the operands of pairwise ops.  -> list of batch ids."""
+        bufs = [b.serialize() if isinstance(b, RoaringBitmap) else bytes(b) for b in bitmaps]
+        arr, lens = _lib.buf_array(bufs)
+        ids = (ctypes.c_int32 * max(len(bufs), 1))()
+        check(lib().rbg_ctx_load_separate(self._ctx, arr, lens, len(bufs), ids))
+        return list(ids)[:len(bufs)]
+
     def synth(self, kind, seed, n=0, key_lo=0, key_hi=65536) -> int:
         out = ctypes.c_int32()
         check(lib().rbg_ctx_synth(self._ctx, int(kind), int(seed), int(n), int(key_lo), int(key_hi),
