@@ -221,6 +221,13 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
         const uint64_t word = l64[(i & 1) ? bfe_u32<22, 10>(wi) : bfe_u32<6, 10>(wi)];
         h |= ((uint32_t)(word >> (x & 63)) & 1u) << i;
       }
+#elif RBG_EXP_PROBE_LIN  // counter attribution only (wrong results): lane-linear, conflict-free probes
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const uint32_t wi = w[i >> 1];
+        const uint32_t word = lds[((i & 1) ? bfe_hi_word(wi) & 64u : bfe_lo_word(wi) & 64u) + l];
+        h |= bit_at(word, (i & 1) ? (wi >> 16) : wi) << i;
+      }
 #else
 #pragma unroll
       for (int i = 0; i < 8; i++) {

@@ -5,7 +5,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc_lds
+OUT=${PMC_OUT:-gpurun_out/pmc_lds}
 mkdir -p $OUT
 [ $# -eq 0 ] && set -- "A A and" "A B and" "A R and" "B B and" "B R and" "R R and" "M M and" "M M card" "A A or" "A R or" "M M or" "M M xor" "M M andnot"
 for c in "$@"; do
