@@ -129,6 +129,7 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
     for _ in range(steps):
         eng.wide(op, b, lo, hi)
     k, ph = eng.profile_read()
+    rd_bytes = eng.profile_bytes() / max(k, 1)  # workShyAnd: what the early-exit chains read per launch
     eng.profile(0)
     kern_ms = ph[1] / max(k, 1)
     t = torch.tensor([wall, float(in_bytes), float(out_bytes)], dtype=torch.float64, device=comm)
@@ -157,8 +158,12 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
                                                           4)} if _pmc_traffic(tkey) and world == 1 else {})}
                                if op == "or" else
                                {"kernel": "k_wide<AND_SHY>", "kernel_ms": round(kern_ms, 4),
-                                "note": "per key the chain stops at an empty intersection: the bytes read are far "
-                                        "below input_bytes, so no roofline fraction is claimed"})}
+                                # per key the chain stops at an empty intersection: the bytes it read
+                                # (payload + 4 B per container, counted by the kernel in the profiled
+                                # pass) are the algorithmic input of this launch, not input_bytes
+                                "bytes_read_per_launch": int(rd_bytes),
+                                "achieved_GBps": round((rd_bytes + out_bytes) / (kern_ms / 1e3) / 1e9, 1),
+                                "frac": round((rd_bytes + out_bytes) / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)})}
 
 
 def c2_weak(rank, world, dist, steps, warmup, cdev):

@@ -188,6 +188,10 @@ int rbg_ctx_sync(rbg_ctx* ctx);
  * assembly (finalize + emit / reduction), and resets the record. */
 int rbg_ctx_profile(rbg_ctx* ctx, int max_ops);
 int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops);
+/* Bytes read by the early-exit wide AND (workShyAnd stops reading a key's inputs once the
+ * intersection is empty: payload + 4 B per container it read) over the ops run since
+ * rbg_ctx_profile enabled profiling; the algorithmic input of that kernel. */
+int rbg_ctx_profile_bytes(rbg_ctx* ctx, int64_t* bytes);
 
 /* n serialized bitmaps in one upload, each decoded into a single-bitmap batch of its own
  * (ids[i]): the operands of pairwise ops, staged and copied to the device together. */

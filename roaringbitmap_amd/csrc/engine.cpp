@@ -190,6 +190,7 @@ struct Ctx {
   // compute, after finalize+emit); read back without per-op host syncs.
   std::vector<hipEvent_t> prof_ev;
   size_t prof_cap = 0, prof_n = 0;
+  DevBuf rd_ctr;  // while profiling: bytes the early-exit workShyAnd kernels read (rbg_ctx_profile_bytes)
   void prof_free() {
     for (hipEvent_t e : prof_ev) (void)hipEventDestroy(e);
     prof_ev.clear();
@@ -1191,6 +1192,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.slot32 = B->payload_bytes < (1ull << 36) ? 1u : 0u;
     wa.order = order;
     wa.chain = chain;
+    wa.rd_bytes = c->prof_cap > 0 && c->rd_ctr.p ? c->rd_ctr.as<unsigned long long>() : nullptr;
     c->mark(1);
     launch_wide(s, mode, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
                 c->task_card.as<uint32_t>());
@@ -1886,6 +1888,21 @@ int rbg_ctx_profile(rbg_ctx* ctx, int max_ops) {
   for (hipEvent_t& e : ctx->c.prof_ev) HIPCHK(hipEventCreate(&e));
   ctx->c.prof_cap = (size_t)max_ops;
   ctx->c.prof_n = 0;
+  CHK(ctx->c.rd_ctr.ensure(8));
+  HIPCHK(hipMemsetAsync(ctx->c.rd_ctr.p, 0, 8, ctx->c.stream));
+  return RBG_OK;
+}
+int rbg_ctx_profile_bytes(rbg_ctx* ctx, int64_t* bytes) {
+  if (!ctx || !bytes) {
+    set_err("profile_bytes: null argument");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  Ctx& c = ctx->c;
+  HIPCHK(hipSetDevice(c.device));
+  HIPCHK(hipStreamSynchronize(c.stream));
+  unsigned long long v = 0;
+  if (c.rd_ctr.p) HIPCHK(hipMemcpy(&v, c.rd_ctr.p, 8, hipMemcpyDeviceToHost));
+  *bytes = (int64_t)v;
   return RBG_OK;
 }
 int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops) {

@@ -36,6 +36,7 @@ struct WideArgs {
   uint32_t slot32;        // every slot offset / 16 fits 32 bits (payload < 64 GiB)
   const uint32_t* order;  // chain modes: container index at chain position j of a key segment (null: input order)
   uint32_t chain;         // chain modes: kChain* flags
+  unsigned long long* rd_bytes;  // workShyAnd: payload + 4 B per container it read, summed (null: not counted)
 };
 
 // priority-queue aggregations (pq.hip): the size-ordered queue runs on the device.  Each

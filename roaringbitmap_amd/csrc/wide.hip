@@ -390,9 +390,15 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
     } else if (MODE == WIDE_AND_SHY || MODE == WIDE_AND_SHY_CARD) {
 #pragma unroll
       for (int i = 0; i < 4; i++) r[i] = ~0ULL;
+      uint64_t rd = 0;  // bytes read (counted only when A.rd_bytes is set)
       for (uint32_t j = 0; j < n; j++) {
         uint64_t x[4];
-        materialize(A.desc[s + j], A.payload, tmp, q, x);
+        const CDesc d = A.desc[s + j];
+        materialize(d, A.payload, tmp, q, x);
+        if (A.rd_bytes)
+          rd += 4 + (d.kind == DK_A   ? 2ull * d.card
+                     : d.kind == DK_B ? 8192ull
+                                      : 2ull + 4ull * *reinterpret_cast<const uint16_t*>(A.payload + d.slot + 2));
 #pragma unroll
         for (int i = 0; i < 4; i++) r[i] &= x[i];
         if ((j & 3) == 3) {  // an empty intersection stays empty: stop reading inputs
@@ -400,6 +406,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
           if (!__syncthreads_or(nz)) break;
         }
       }
+      if (A.rd_bytes && threadIdx.x == 0) atomicAdd(A.rd_bytes, (unsigned long long)rd);
       c = block_card(r, sh);
       if (MODE == WIDE_AND_SHY_CARD) {
         if (threadIdx.x == 0) task_card[t] = (uint32_t)c;

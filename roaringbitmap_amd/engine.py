@@ -57,6 +57,12 @@ class Engine:
         check(lib().rbg_ctx_profile_read(self._ctx, ms, ctypes.byref(n)))
         return n.value, list(ms)
 
+    def profile_bytes(self) -> int:
+        """Bytes the early-exit wide AND (workShyAnd) read since profiling was enabled."""
+        v = ctypes.c_int64()
+        check(lib().rbg_ctx_profile_bytes(self._ctx, ctypes.byref(v)))
+        return v.value
+
     # ---- batches ------------------------------------------------------------
     def load(self, bitmaps) -> int:
         bufs = [b.serialize() if isinstance(b, RoaringBitmap) else bytes(b) for b in bitmaps]

@@ -213,3 +213,30 @@ def test_wide_or_in_place_bitmaps(gpu, case):
             per[i].append((k << 16) + v)
     bufs = [rb.RoaringBitmap.from_values(np.concatenate(p), run_optimize=True).serialize() for p in per]
     _cmp("or", bufs, list(range(6)))
+
+
+def test_workshy_bytes_read(gpu):
+    """rbg_ctx_profile_bytes (the bench's C3 AND roofline): payload + 4 B per container that the
+    early-exit workShyAnd read.  Identical inputs never empty, so every container is read;
+    pairwise-disjoint ones are empty after two inputs and the chain stops at its first check
+    (after four)."""
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+
+    def read(bufs):
+        b = e.load(bufs)
+        e.profile(1)
+        e.wide("workshy_and", b)
+        e.profile_read()
+        v = e.profile_bytes()
+        e.profile(0)
+        e.release(b)
+        return v
+
+    rng = np.random.default_rng(9)
+    base = _gen.bitmap(rng, np.arange(6), p_present=1.0)
+    st = O.stats(base)
+    assert read([base] * 12) == 12 * (st["payload"] + 4 * (st["array"] + st["bitmap"] + st["run"]))
+    disjoint = [O.from_values(np.concatenate([k * 65536 + 100 * i + np.arange(50) for k in range(6)]))
+                for i in range(12)]
+    assert read(disjoint) == 6 * 4 * (4 + 2 * 50)
