@@ -38,6 +38,7 @@ for f in sorted(glob.glob(os.path.join(src, "*", "run_counter_collection.csv")))
             "lds_conflict_pct_of_cu_time": 100 * c["SQ_LDS_BANK_CONFLICT"] / (cyc * 256),
             "lds_active_pct_of_cu_time": 100 * c["SQ_LDS_IDX_ACTIVE"] / (cyc * 256),
             "lds_insts_per_task": c["SQ_INSTS_LDS"] / N_TASKS,
+            "conflict_cycles_per_task": c["SQ_LDS_BANK_CONFLICT"] / N_TASKS,
             "waves_per_cu": 4 * c["SQ_WAVE_CYCLES"] / (cyc * 256),
             "occupancy_pct_of_16_resident": 100 * 4 * c["SQ_WAVE_CYCLES"] / (cyc * 256) / 16,
             "valu_insts_per_task": c["SQ_INSTS_VALU"] / N_TASKS,
