@@ -422,6 +422,7 @@ class DeviceShard:
         self.out = torch.empty(MAX_SERIALIZED, dtype=torch.uint8, device=self.dev)
         self.runb = torch.empty(KEYS, dtype=torch.uint8, device=self.dev)
         self.ext = torch.cuda.ExternalStream(engine.stream_ptr, device=self.dev)
+        torch.cuda.synchronize(self.dev)  # the zero fills (torch's stream) before any engine-stream write
 
     def place(self):
         import torch

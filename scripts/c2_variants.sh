@@ -16,7 +16,7 @@ for v in base $VARIANTS; do
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1]); e = d["extra"]
 print(sys.argv[1], "step", d["ms_per_step"], "phases", e["phase_ms"], "card", e["c2_and_cardinality"]["roofline"]["kernel_ms"],
-      "card_step", e["c2_and_cardinality"]["ms_per_step"], flush=True)
+      "card_step", e["c2_and_cardinality"]["ms_per_step"], "sha", e["result"].get("sha16"), flush=True)
 PY
 done
 done

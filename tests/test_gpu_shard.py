@@ -166,12 +166,14 @@ def test_device_layout_shards(gpu, world):
     dev = torch.device("cuda", 0)
     for op in ["and", "or", "xor", "andnot"]:
         lay = torch.zeros(3 * world, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)
         for r, (lo, hi) in enumerate(ranges):
             e.pairwise(op, ba, bb, key_lo=lo, key_hi=hi)
             e.result_layout_device(lay[3 * r: 3 * r + 3])
         e.sync()
         out = torch.zeros(shard.MAX_SERIALIZED, dtype=torch.uint8, device=dev)
         runb = torch.zeros(shard.KEYS, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize(dev)  # the fills (torch's stream) before the engine's writes (its own stream)
         for r, (lo, hi) in enumerate(ranges):
             e.pairwise(op, ba, bb, key_lo=lo, key_hi=hi)
             e.fetch_shard_device_dyn(lay, r, world, out, runb)
