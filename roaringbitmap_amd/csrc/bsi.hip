@@ -333,21 +333,24 @@ __device__ __forceinline__ void rec1(uint64_t z, int k, uint8_t* rows) {
 // threads' reads over the banks).
 constexpr int kQB = 64 * 4 + 16;
 constexpr int kGrpB = 4 * kQB;
-constexpr int kRowsBytes = ((kBsiRows + 3) / 4) * kGrpB;
+constexpr int kRowsBytes = ((kBsiRows + 4) / 4) * kGrpB;  // packed positions 1 .. kBsiRows
+// Row r is packed at position r + 1, so the two rows of a circuit step (1 + 2 (31 - i) + {0, 1})
+// share a group.  Rows are recorded in increasing order and done(r) is called once every row up
+// to r is recorded or skipped.
 struct RowRec {
   uint8_t* rows;
   uint32_t v;
-  __device__ __forceinline__ void rec(uint64_t z, int r) { v |= (uint32_t)popc64(z) << (8 * (r & 3)); }
+  __device__ __forceinline__ void rec(uint64_t z, int r) { v |= (uint32_t)popc64(z) << (8 * ((r + 1) & 3)); }
   __device__ __forceinline__ void put(int g) {
     *reinterpret_cast<uint32_t*>(rows + g * kGrpB + (threadIdx.x >> 6) * kQB + 4 * (threadIdx.x & 63)) = v;
     v = 0;
   }
   // row r is complete (recorded or skipped): a full group is stored
   __device__ __forceinline__ void done(int r) {
-    if ((r & 3) == 3) put(r >> 2);
+    if (((r + 1) & 3) == 3) put((r + 1) >> 2);
   }
   __device__ __forceinline__ void end(int r) {  // the group of the last row r, if not full
-    if ((r & 3) != 3) put(r >> 2);
+    if (((r + 1) & 3) != 3) put((r + 1) >> 2);
   }
 };
 #else
@@ -390,7 +393,7 @@ __device__ __forceinline__ void sum_rows_packed(const uint8_t* rows, int nk, int
   lds_barrier();
   const int g = threadIdx.x >> 2, k = threadIdx.x & 3;
   uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-  if (4 * g < nk) {
+  if (4 * g <= nk) {
     const uint4* v = reinterpret_cast<const uint4*>(rows + g * kGrpB + k * kQB);
 #pragma unroll
     for (int j = 0; j < 16; j++) {
@@ -414,8 +417,8 @@ __device__ __forceinline__ void sum_rows_packed(const uint8_t* rows, int nk, int
   c1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1, 0x4E, 0xF, 0xF, false);
   c2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c2, 0x4E, 0xF, 0xF, false);
   c3 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c3, 0x4E, 0xF, 0xF, false);
-  const int r = 4 * g + k;
-  if (r < nk) cnt[r] = (int)(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
+  const int r = 4 * g + k - 1;  // packed position 4 g + k holds row 4 g + k - 1
+  if (r >= 0 && r < nk) cnt[r] = (int)(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
   lds_barrier();
 }
 #endif
@@ -677,13 +680,17 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
     if (two) {  // RANGE = and(GE(start), LE(end)), BSI/:503-507
       const uint64_t left = bits_finish1(BSI_GE, fixed, ebm ^ lt0 ^ eq0, lt0, eq0, kRowFin, 0, rc);
       const uint64_t right = bits_finish1(BSI_LE, fixed, ebm ^ lt1 ^ eq1, lt1, eq1, kRowFin + 1, 0, rc);
+      rc.done(kRowFin);
+      rc.done(kRowFin + 1);
       res = left & right;
       rc.rec(res, kRowFin + 2);
     } else {
       res = bits_finish1(P.op, fixed, ebm ^ lt0 ^ eq0, lt0, eq0, kRowFin, kRowFin + 1, rc);
+      rc.done(kRowFin);
+      rc.done(kRowFin + 1);
     }
 #pragma unroll
-    for (int r = kRowFin; r < kRowSum; r++) rc.done(r);
+    for (int r = kRowFin + 2; r < kRowSum; r++) rc.done(r);
     // sum shares |bA[x] & result| (an absent result has no bits: all zero)
     if (want_sum) {
 #pragma unroll
@@ -692,6 +699,8 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
         rc.done(kRowSum + x);
       }
       rc.end(kRowSum + kBsiRegSlices - 1);
+    } else {
+      rc.end(kRowSum - 1);  // the group holding the finish rows
     }
     // the slice registers are dead: the next unit's bitmap slices are requested now
     uint64_t bmask_n = 0;
