@@ -326,43 +326,6 @@ __device__ __forceinline__ TB tb_op(const TB& x, const TB& y, int c, int& slow) 
 __device__ __forceinline__ void rec1(uint64_t z, int k, uint8_t* rows) {
   rows[k * kRowB + threadIdx.x] = (uint8_t)popc64(z);
 }
-#if RBG_BSI_PACK
-// Experiment: four count rows packed per thread in one u32 (a byte each), so a step costs a
-// shift-or and every fourth row one LDS store instead of one byte store per row.  Group g of
-// rows 4g..4g+3: wave w's 64 words at g * kGrpB + w * kQB (the pad spreads the summing
-// threads' reads over the banks).
-constexpr int kQB = 64 * 4 + 16;
-constexpr int kGrpB = 4 * kQB;
-constexpr int kRowsBytes = ((kBsiRows + 4) / 4) * kGrpB;  // packed positions 1 .. kBsiRows
-// Row r is packed at position r + 1, so the two rows of a circuit step (1 + 2 (31 - i) + {0, 1})
-// share a group.  Rows are recorded in increasing order and done(r) is called once every row up
-// to r is recorded or skipped.
-struct RowRec {
-  uint8_t* rows;
-  uint32_t v;
-  __device__ __forceinline__ void rec(uint64_t z, int r) { v |= (uint32_t)popc64(z) << (8 * ((r + 1) & 3)); }
-  __device__ __forceinline__ void put(int g) {
-    *reinterpret_cast<uint32_t*>(rows + g * kGrpB + (threadIdx.x >> 6) * kQB + 4 * (threadIdx.x & 63)) = v;
-    v = 0;
-  }
-  // row r is complete (recorded or skipped): a full group is stored
-  __device__ __forceinline__ void done(int r) {
-    if (((r + 1) & 3) == 3) put((r + 1) >> 2);
-  }
-  __device__ __forceinline__ void end(int r) {  // the group of the last row r, if not full
-    if (((r + 1) & 3) != 3) put((r + 1) >> 2);
-  }
-};
-#else
-constexpr int kRowsBytes = kBsiRows * kRowB;
-struct RowRec {
-  uint8_t* rows;
-  uint32_t v;
-  __device__ __forceinline__ void rec(uint64_t z, int r) { rec1(z, r, rows); }
-  __device__ __forceinline__ void done(int) {}
-  __device__ __forceinline__ void end(int) {}
-};
-#endif
 // row sums of rows [0, nk), one thread per row (16 B reads, v_dot4 over the bytes),
 // written as this unit's partial counts: cnt[row], contiguous (one coalesced store per
 // wave; a transposed layout made each count a scattered 4 B write).
@@ -385,43 +348,6 @@ __device__ __forceinline__ void sum_rows_unit(const uint8_t* rows, int nk, int* 
   }
   lds_barrier();
 }
-#if RBG_BSI_PACK
-// the packed rows' sums: four threads per group, each summing one wave's quarter for all four
-// rows (v_dot4 with a byte selector), added over the quad with DPP; lane k of the quad writes
-// row 4g + k
-__device__ __forceinline__ void sum_rows_packed(const uint8_t* rows, int nk, int* cnt) {
-  lds_barrier();
-  const int g = threadIdx.x >> 2, k = threadIdx.x & 3;
-  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-  if (4 * g <= nk) {
-    const uint4* v = reinterpret_cast<const uint4*>(rows + g * kGrpB + k * kQB);
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const uint4 x = v[j];
-      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-      for (int e = 0; e < 4; e++) {
-        c0 = __builtin_amdgcn_udot4(w[e], 0x00000001u, c0, false);
-        c1 = __builtin_amdgcn_udot4(w[e], 0x00000100u, c1, false);
-        c2 = __builtin_amdgcn_udot4(w[e], 0x00010000u, c2, false);
-        c3 = __builtin_amdgcn_udot4(w[e], 0x01000000u, c3, false);
-      }
-    }
-  }
-  // quad sums (every lane takes part: the DPP moves need the whole quad)
-  c0 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c0, 0xB1, 0xF, 0xF, false);
-  c1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1, 0xB1, 0xF, 0xF, false);
-  c2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c2, 0xB1, 0xF, 0xF, false);
-  c3 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c3, 0xB1, 0xF, 0xF, false);
-  c0 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c0, 0x4E, 0xF, 0xF, false);
-  c1 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c1, 0x4E, 0xF, 0xF, false);
-  c2 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c2, 0x4E, 0xF, 0xF, false);
-  c3 += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c3, 0x4E, 0xF, 0xF, false);
-  const int r = 4 * g + k - 1;  // packed position 4 g + k holds row 4 g + k - 1
-  if (r >= 0 && r < nk) cnt[r] = (int)(k == 0 ? c0 : k == 1 ? c1 : k == 2 ? c2 : c3);
-  lds_barrier();
-}
-#endif
 // Type replay of a step / finish, in the order of the bits.  c* are the exact
 // cardinalities of the bits (0 for an absent bitmap).
 struct CircuitT {
@@ -463,9 +389,9 @@ __device__ __forceinline__ TB types_finish(int op, const TB& fixed, CircuitT& z,
 }
 // the same on bits (this thread's word); counted: fixed & EQ (row re), NEQ / GT / LT (row ro)
 __device__ __forceinline__ uint64_t bits_finish1(int op, uint64_t fixed, uint64_t gt, uint64_t lt, uint64_t& eq, int re,
-                                                 int ro, RowRec& rows) {
+                                                 int ro, uint8_t* rows) {
   eq &= fixed;
-  rows.rec(eq, re);
+  rec1(eq, re, rows);
   uint64_t out;
   switch (op) {
     case BSI_EQ: return eq;
@@ -475,7 +401,7 @@ __device__ __forceinline__ uint64_t bits_finish1(int op, uint64_t fixed, uint64_
     case BSI_LE: return lt | eq;
     default: return gt | eq;  // GE
   }
-  rows.rec(out, ro);
+  rec1(out, ro, rows);
   return out;
 }
 
@@ -580,9 +506,8 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
                                                  TB* __restrict__ kin, size_t tstride) {
   // the 8 KiB scratch for array / run inputs aliases the count rows: inputs are
   // materialised before the circuit writes the rows, and after the last unit's sums
-  __shared__ __align__(16) uint8_t rows[kRowsBytes];
-  static_assert(kRowsBytes >= 8192, "scratch bitmap inside the rows");
-  RowRec rc{rows, 0};
+  __shared__ __align__(16) uint8_t rows[kBsiRows * kRowB];
+  static_assert(kBsiRows * kRowB >= 8192, "scratch bitmap inside the rows");
   uint32_t* tmp = reinterpret_cast<uint32_t*>(rows);
   __shared__ int q[257];
   const uint64_t nunits = (uint64_t)*n_tasks * kBsiUnits;
@@ -636,8 +561,7 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
     // 2. bits of the whole circuit; each thread's share of every count to LDS.  GT is
     // not tracked: GT, LT and EQ partition ebM, so GT = ebM ^ LT ^ EQ at the end.
     uint64_t eq0 = ebm, lt0 = 0, eq1 = ebm, lt1 = 0, res;
-    rc.rec(ebm, kRowEbm);  // |ebM| of the bits: the start of the derived cardinalities
-    rc.done(kRowEbm);
+    rec1(ebm, kRowEbm, rows);  // |ebM| of the bits: the start of the derived cardinalities
     // predicate bits i = 31 .. 0 as the top bit of running copies; the asm keeps the
     // compiler from precomputing 64 per-step flags (SGPR spills)
     uint32_t p0 = P.pred0, p1 = P.pred1;
@@ -650,57 +574,44 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
         // step's form with a scalar branch
         if ((int32_t)p0 < 0) {  // LT |= EQ & ~bA[i]; EQ &= bA[i]
           const uint64_t tv = eq0 & ~sl[i];
-          rc.rec(tv, step_row(i, 0));
+          rec1(tv, step_row(i, 0), rows);
           lt0 |= tv;
           eq0 ^= tv;
         } else {  // GT |= EQ & bA[i]; EQ &= ~bA[i]
           const uint64_t tv = eq0 & sl[i];
-          rc.rec(tv, step_row(i, 0));
+          rec1(tv, step_row(i, 0), rows);
           eq0 ^= tv;
         }
         if (two) {
           if ((int32_t)p1 < 0) {
             const uint64_t tw = eq1 & ~sl[i];
-            rc.rec(tw, step_row(i, 1));
+            rec1(tw, step_row(i, 1), rows);
             lt1 |= tw;
             eq1 ^= tw;
           } else {
             const uint64_t tw = eq1 & sl[i];
-            rc.rec(tw, step_row(i, 1));
+            rec1(tw, step_row(i, 1), rows);
             eq1 ^= tw;
           }
         }
       }
-      rc.done(step_row(i, 0));
-      rc.done(step_row(i, 1));
       p0 <<= 1;
       p1 <<= 1;
       live--;
     }
     if (two) {  // RANGE = and(GE(start), LE(end)), BSI/:503-507
-      const uint64_t left = bits_finish1(BSI_GE, fixed, ebm ^ lt0 ^ eq0, lt0, eq0, kRowFin, 0, rc);
-      const uint64_t right = bits_finish1(BSI_LE, fixed, ebm ^ lt1 ^ eq1, lt1, eq1, kRowFin + 1, 0, rc);
-      rc.done(kRowFin);
-      rc.done(kRowFin + 1);
+      const uint64_t left = bits_finish1(BSI_GE, fixed, ebm ^ lt0 ^ eq0, lt0, eq0, kRowFin, 0, rows);
+      const uint64_t right = bits_finish1(BSI_LE, fixed, ebm ^ lt1 ^ eq1, lt1, eq1, kRowFin + 1, 0, rows);
       res = left & right;
-      rc.rec(res, kRowFin + 2);
+      rec1(res, kRowFin + 2, rows);
     } else {
-      res = bits_finish1(P.op, fixed, ebm ^ lt0 ^ eq0, lt0, eq0, kRowFin, kRowFin + 1, rc);
-      rc.done(kRowFin);
-      rc.done(kRowFin + 1);
+      res = bits_finish1(P.op, fixed, ebm ^ lt0 ^ eq0, lt0, eq0, kRowFin, kRowFin + 1, rows);
     }
-#pragma unroll
-    for (int r = kRowFin + 2; r < kRowSum; r++) rc.done(r);
     // sum shares |bA[x] & result| (an absent result has no bits: all zero)
     if (want_sum) {
 #pragma unroll
-      for (int x = 0; x < kBsiRegSlices; x++) {
-        if (x < nb) rc.rec(sl[x] & res, kRowSum + x);
-        rc.done(kRowSum + x);
-      }
-      rc.end(kRowSum + kBsiRegSlices - 1);
-    } else {
-      rc.end(kRowSum - 1);  // the group holding the finish rows
+      for (int x = 0; x < kBsiRegSlices; x++)
+        if (x < nb) rec1(sl[x] & res, kRowSum + x, rows);
     }
     // the slice registers are dead: the next unit's bitmap slices are requested now
     uint64_t bmask_n = 0;
@@ -708,11 +619,7 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
     // this unit's result words to the task's scratch slot (the container itself when
     // it is a bitmap, else the input k_bsi_defer stages it from)
     reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[w] = res;
-#if RBG_BSI_PACK
-    sum_rows_packed(rows, want_sum ? kRowSum + nb : kRowSum, cnts + ((size_t)t * kBsiUnits + u) * kBsiCnt);
-#else
     sum_rows_unit(rows, want_sum ? kRowSum + nb : kRowSum, cnts + ((size_t)t * kBsiUnits + u) * kBsiCnt);
-#endif
     if (u == 0 && tid < kBsiKin) {  // the key's input types, for k_bsi_types
       const int i = tid == kBsiRegSlices ? 0 : tid == kBsiRegSlices + 1 ? (P.has_found ? nb + 1 : 0) : 1 + tid;
       const BsiIn x = table[(size_t)t * kBsiKin + (i < kBsiKin ? i : 0)];

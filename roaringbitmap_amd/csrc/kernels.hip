@@ -165,52 +165,6 @@ __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ 
   }
   uint8_t* pay = oc.out + oc.payload_base;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-#if RBG_SER2  // experiment: two records per wave per round, both payloads requested before either is stored
-  for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += 2 * nw) {
-    const uint32_t t2 = t + nw;
-    CopyJob j[2];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint32_t tt = h ? t2 : t;
-      bool need = tt < nt;
-      uint64_t off = 0, src = 0;
-      uint32_t len = 0;
-      if (need) {
-        const ORec& r = oc.recs[tt];
-        off = uni64(r.off);
-        src = uni64(r.src);
-        len = uni(r.ser_len);
-        need = uni(r.keep) && src != reinterpret_cast<uint64_t>(pay + off);
-      }
-      if (need) {
-        j[h] = copy_begin(pay + off, reinterpret_cast<const uint8_t*>(src), len);
-      } else {
-        j[h].n = j[h].head = j[h].nvec = j[h].shift = 0;
-        j[h].s8 = nullptr;
-        j[h].d8 = nullptr;
-        j[h].sv = nullptr;
-        j[h].dv = nullptr;
-      }
-    }
-    {
-      u32x4 a[8], la, b[8], lb;
-      copy_load(j[0], 0, a, la);
-      copy_load(j[1], 0, b, lb);
-      copy_store(j[0], 0, a, la);
-      copy_store(j[1], 0, b, lb);
-    }
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      for (uint32_t i0 = 512; i0 < j[h].nvec; i0 += 512) {
-        u32x4 a[8], la;
-        copy_load(j[h], i0, a, la);
-        copy_store(j[h], i0, a, la);
-      }
-      if (j[h].n) copy_tail(j[h]);
-    }
-  }
-  return;
-#endif
   for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
     const ORec& r = oc.recs[t];
     if (!uni(r.keep)) continue;

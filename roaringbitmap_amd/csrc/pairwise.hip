@@ -212,16 +212,7 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
       // hardware shift reads only the low 5 bits, so no masking); the tail of
       // the array is masked once per vector, not per value
       uint32_t h = 0;
-#if RBG_PROBE64
-      const uint64_t* l64 = reinterpret_cast<const uint64_t*>(lds);
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const uint32_t wi = w[i >> 1];
-        const uint32_t x = (i & 1) ? (wi >> 16) : wi;
-        const uint64_t word = l64[(i & 1) ? bfe_u32<22, 10>(wi) : bfe_u32<6, 10>(wi)];
-        h |= ((uint32_t)(word >> (x & 63)) & 1u) << i;
-      }
-#elif RBG_EXP_PROBE_LIN  // counter attribution only (wrong results): lane-linear, conflict-free probes
+#if RBG_EXP_PROBE_LIN  // counter attribution only (wrong results): lane-linear, conflict-free probes
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         const uint32_t wi = w[i >> 1];

@@ -47,12 +47,6 @@ __device__ __forceinline__ uint32_t bfe_hi_word(uint32_t w) {
   asm("v_bfe_u32 %0, %1, 21, 11" : "=v"(r) : "v"(w));
   return r;
 }
-template <int OFF, int W>
-__device__ __forceinline__ uint32_t bfe_u32(uint32_t w) {
-  uint32_t r;
-  asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(r) : "v"(w), "i"(OFF), "i"(W));
-  return r;
-}
 // bit (bit & 31) of word, as 0 / 1
 __device__ __forceinline__ uint32_t bit_at(uint32_t word, uint32_t bit) {
   uint32_t r;
@@ -135,19 +129,6 @@ constexpr int kVecRound = 4;  // 16 B vectors per lane loaded per round
 template <int MODE>  // MODE 0 or, 1 xor
 __device__ __forceinline__ void scatter_vec_mask(uint32_t* lds, const uint4 v, uint32_t vm) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#if RBG_SCATTER64
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    const uint32_t wi = w[i >> 1];
-    unsigned long long* p =
-        reinterpret_cast<unsigned long long*>(lds) + ((i & 1) ? bfe_u32<22, 10>(wi) : bfe_u32<6, 10>(wi));
-    const uint32_t x = (i & 1) ? (wi >> 16) : wi;
-    const unsigned long long m = (unsigned long long)((vm >> i) & 1u) << (x & 63);
-    if (MODE == 0) atomicOr(p, m);
-    else atomicXor(p, m);
-  }
-  return;
-#endif
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint32_t wi = w[i >> 1];
