@@ -146,6 +146,9 @@ int rbg_bsi_compare_buffer(int op, int32_t start, int32_t end, const uint8_t* eb
 int rbg_bsi_sum(const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* slice_lens,
                 size_t nbits, const uint8_t* found, size_t found_len, int64_t* out2);
 
+/* Releases an output.  Large results (>= 8 MiB, 2 MiB-aligned huge-page buffers) are kept for
+ * reuse by the next large result, at most two of them, so a caller's steady stream of big results
+ * does not fault and zero fresh pages every call. */
 void rbg_free(rbg_buffer* buf);
 
 /* Select the HIP devices the one-shot calls may use (bit i = device i).  Returns the

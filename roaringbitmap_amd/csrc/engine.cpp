@@ -14,7 +14,10 @@
 #include <string>
 #include <thread>
 #include <chrono>
+#include <unordered_map>
 #include <vector>
+
+#include <sys/mman.h>
 
 #include "../../include/roaring_mi355x.h"
 #include "format.hpp"
@@ -1547,6 +1550,33 @@ static int download_staged(Ctx* c, const uint8_t* dev, uint64_t bytes, uint8_t* 
   return st;
 }
 
+// Large result buffers (a serialized C2 AND result is 0.25 GB): 2 MiB-aligned with transparent
+// huge pages, so first touch faults once per 2 MiB instead of once per 4 KiB, and rbg_free keeps up
+// to two of them for the next large result (a fresh buffer's pages are faulted and zeroed by the
+// kernel on first touch: tens of ms for 0.25 GB, more than its PCIe download).
+static std::mutex g_out_mu;
+static std::unordered_map<void*, size_t> g_out_live;        // large buffers handed out -> capacity
+static std::vector<std::pair<void*, size_t>> g_out_cache;   // freed ones kept for reuse
+constexpr size_t kOutLarge = 8ull << 20, kOutCacheMax = 2, kOutAlign = 2ull << 20;
+static uint8_t* out_alloc(size_t n) {
+  if (n < kOutLarge) return (uint8_t*)std::malloc(n ? n : 1);
+  std::lock_guard<std::mutex> g(g_out_mu);
+  for (size_t i = 0; i < g_out_cache.size(); i++) {
+    const auto e = g_out_cache[i];
+    if (e.second >= n && e.second <= 2 * n + kOutAlign) {
+      g_out_cache.erase(g_out_cache.begin() + (std::ptrdiff_t)i);
+      g_out_live[e.first] = e.second;
+      return (uint8_t*)e.first;
+    }
+  }
+  const size_t cap = (n + kOutAlign - 1) & ~(kOutAlign - 1);
+  void* p = nullptr;
+  if (posix_memalign(&p, kOutAlign, cap) != 0) return nullptr;
+  (void)madvise(p, cap, MADV_HUGEPAGE);
+  g_out_live[p] = cap;
+  return (uint8_t*)p;
+}
+
 static int ctx_fetch(Ctx* c, rbg_buffer* out) {
   if (c->last != 1) {
     set_err("no serialized result pending");
@@ -1555,15 +1585,15 @@ static int ctx_fetch(Ctx* c, rbg_buffer* out) {
   CHK(ctx_serialize(c));
   ResultInfo ri;
   CHK(ctx_info(c, &ri));
-  uint8_t* p = (uint8_t*)std::malloc(ri.total ? ri.total : 1);
+  uint8_t* p = out_alloc(ri.total);
   if (!p) return RBG_ERR_OUT_OF_MEMORY;
-  const int st = download_staged(c, c->result.as<uint8_t>() + ri.start, ri.total, p);
-  if (st != RBG_OK) {
-    std::free(p);
-    return st;
-  }
   out->data = p;
   out->len = ri.total;
+  const int st = download_staged(c, c->result.as<uint8_t>() + ri.start, ri.total, p);
+  if (st != RBG_OK) {
+    rbg_free(out);
+    return st;
+  }
   return RBG_OK;
 }
 
@@ -1613,6 +1643,21 @@ const char* rbg_last_error(void) { return g_err.c_str(); }
 
 void rbg_free(rbg_buffer* buf) {
   if (!buf) return;
+  if (buf->data) {
+    std::lock_guard<std::mutex> g(g_out_mu);
+    const auto it = g_out_live.find(buf->data);
+    if (it != g_out_live.end()) {  // a large result buffer: kept for reuse (the oldest kept one freed)
+      g_out_cache.emplace_back(it->first, it->second);
+      g_out_live.erase(it);
+      if (g_out_cache.size() > kOutCacheMax) {
+        std::free(g_out_cache.front().first);
+        g_out_cache.erase(g_out_cache.begin());
+      }
+      buf->data = nullptr;
+      buf->len = 0;
+      return;
+    }
+  }
   std::free(buf->data);
   buf->data = nullptr;
   buf->len = 0;

@@ -151,6 +151,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
   __shared__ int sh[8];
   __shared__ Prefix shp;
   const uint32_t nt = *n_tasks;
+  uint64_t rd_total = 0;  // workShyAnd's bytes read over this workgroup's keys (A.rd_bytes)
   // static stride over a resident grid (no contended counter)
   uint32_t t = blockIdx.x - gridDim.x;
   while (true) {
@@ -406,7 +407,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
           if (!__syncthreads_or(nz)) break;
         }
       }
-      if (A.rd_bytes && threadIdx.x == 0) atomicAdd(A.rd_bytes, (unsigned long long)rd);
+      rd_total += rd;
       c = block_card(r, sh);
       if (MODE == WIDE_AND_SHY_CARD) {
         if (threadIdx.x == 0) task_card[t] = (uint32_t)c;
@@ -465,6 +466,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
     const uint32_t len = stage_container(kind, r, c, acc, tmp, sh);
     wg_place(t, true, nullptr, true, tmp, len, (uint32_t)c, tk.key, kind, oc, &shp);
   }
+  if (A.rd_bytes && threadIdx.x == 0 && rd_total) atomicAdd(A.rd_bytes, (unsigned long long)rd_total);
 }
 
 void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
