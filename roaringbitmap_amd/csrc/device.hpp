@@ -111,6 +111,9 @@ struct OutCtx {
   // wide OR: a staged bitmap result of task t is written straight to payload offset 8192 t, its place
   // whenever every earlier task kept an 8 KiB container (k_spec_fix moves the others to their slot)
   uint32_t spec;
+  // k_place also writes the result's (containers, payload bytes, has_run) here when set: the
+  // device layout of a key shard (rbg_ctx_result_layout_device) without a launch of its own
+  int64_t* layout_out;
 };
 
 // Portable-format header bytes for `size` containers (RB/RoaringArray.java:781-790)

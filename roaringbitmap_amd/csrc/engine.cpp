@@ -2424,8 +2424,14 @@ int rbg_ctx_result_layout_device(rbg_ctx* ctx, void* dst3) {
     set_err("no materialised result pending");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
-  CHK(ensure_placed(c));
-  launch_layout_out(c->stream, c->info.as<ResultInfo>(), reinterpret_cast<int64_t*>(dst3));
+  if (c->place_pending) {  // the placement writes the layout too (one launch fewer per sharded step)
+    OutCtx o = c->pending;
+    o.layout_out = reinterpret_cast<int64_t*>(dst3);
+    launch_place(c->stream, c->ntasks.as<uint32_t>(), o, c->info.as<ResultInfo>());
+    c->place_pending = false;
+  } else {
+    launch_layout_out(c->stream, c->info.as<ResultInfo>(), reinterpret_cast<int64_t*>(dst3));
+  }
   HIPCHK(hipGetLastError());
   return RBG_OK;
 }

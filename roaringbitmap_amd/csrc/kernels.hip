@@ -328,7 +328,10 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
   const uint32_t nt = *n_tasks;
   const uint32_t ntiles = (nt + kTile - 1) / kTile;
   if (nt == 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) write_info(info, oc, 0, 0, 0);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      write_info(info, oc, 0, 0, 0);
+      if (oc.layout_out) oc.layout_out[0] = oc.layout_out[1] = oc.layout_out[2] = 0;
+    }
     return;
   }
   const uint32_t tile = blockIdx.x;
@@ -415,6 +418,11 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
       const uint64_t incl = __hip_atomic_load(oc.tile_status + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(oc.status + nt - 1, incl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       write_info(info, oc, (uint32_t)((incl >> 44) & 0x1FFFF), (uint32_t)((incl >> 61) & 1), incl & ((1ULL << 44) - 1));
+      if (oc.layout_out) {
+        oc.layout_out[0] = (int64_t)((incl >> 44) & 0x1FFFF);
+        oc.layout_out[1] = (int64_t)(incl & ((1ULL << 44) - 1));
+        oc.layout_out[2] = (int64_t)((incl >> 61) & 1);
+      }
     }
   }
 }
@@ -480,22 +488,11 @@ __device__ __forceinline__ ShardGeo shard_geo(const int64_t* __restrict__ lay, i
   g.off_base = g.desc_base + 4 * g.total;
   return g;
 }
-__global__ __launch_bounds__(256) void k_emit_dyn(const uint32_t* __restrict__ n_tasks, OutCtx oc,
-                                                  const int64_t* __restrict__ lay, int rank, int world,
-                                                  uint8_t* __restrict__ out) {
-  const ShardGeo g = shard_geo(lay, rank, world);
-  uint8_t* dst = out + g.header + g.base;
-  const uint32_t nt = *n_tasks;
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
-    const ORec& r = oc.recs[t];
-    if (!uni(r.keep)) continue;
-    w_copy(dst + uni64(r.off), reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
-  }
-}
-__global__ __launch_bounds__(256) void k_shard_table_dyn(const uint32_t* __restrict__ n_tasks, OutCtx oc,
-                                                         const int64_t* __restrict__ lay, int rank, int world,
-                                                         uint8_t* __restrict__ out, uint8_t* __restrict__ runb) {
+// One launch: one wave per record copies its payload (when `emit`) and its lane 0 writes the
+// descriptor, offset-table entry and run byte; rank 0 also the cookie.
+__global__ __launch_bounds__(256) void k_shard_dyn(const uint32_t* __restrict__ n_tasks, OutCtx oc,
+                                                   const int64_t* __restrict__ lay, int rank, int world,
+                                                   uint8_t* __restrict__ out, uint8_t* __restrict__ runb, int emit) {
   const ShardGeo g = shard_geo(lay, rank, world);
   const uint32_t nt = *n_tasks;
   if (rank == 0 && blockIdx.x == 0 && threadIdx.x < 8) {  // the cookie (RB/RoaringArray.java:900-901,918-921)
@@ -503,17 +500,23 @@ __global__ __launch_bounds__(256) void k_shard_table_dyn(const uint32_t* __restr
     const uint32_t w = threadIdx.x < 4 ? c0 : (uint32_t)g.total;
     if (threadIdx.x < 4 || !g.has_run) out[threadIdx.x] = (uint8_t)(w >> (8 * (threadIdx.x & 3)));
   }
-  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
-    const ORec r = oc.recs[t];
-    if (!r.keep) continue;
-    const uint64_t idx = g.first + r.idx;
-    const uint32_t d = (uint32_t)r.key | ((r.card - 1) << 16);
-    for (int k = 0; k < 4; k++) out[g.desc_base + 4 * idx + k] = (uint8_t)(d >> (8 * k));
-    if (g.offsets) {
-      const uint32_t o = (uint32_t)(g.header + g.base + r.off);
-      for (int k = 0; k < 4; k++) out[g.off_base + 4 * idx + k] = (uint8_t)(o >> (8 * k));
+  uint8_t* dst = out + g.header + g.base;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
+    const ORec& r = oc.recs[t];
+    if (!uni(r.keep)) continue;
+    if (emit) w_copy(dst + uni64(r.off), reinterpret_cast<const uint8_t*>(uni64(r.src)), uni(r.ser_len));
+    const int l = lane_id();
+    if (l < 4) {
+      const uint64_t idx = g.first + r.idx;
+      const uint32_t d = (uint32_t)r.key | ((r.card - 1) << 16);
+      out[g.desc_base + 4 * idx + l] = (uint8_t)(d >> (8 * l));
+      if (g.offsets) {
+        const uint32_t o = (uint32_t)(g.header + g.base + r.off);
+        out[g.off_base + 4 * idx + l] = (uint8_t)(o >> (8 * l));
+      }
+      if (runb && l == 0) runb[idx] = r.kind == DK_R ? 1 : 0;
     }
-    if (runb) runb[idx] = r.kind == DK_R ? 1 : 0;
   }
 }
 // x1.or(x2) in place (RB/RoaringBitmap.java:2481-2523): Container.ior types like the static or,
@@ -612,10 +615,9 @@ void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx 
 }
 void launch_serialize_shard_dyn(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, const int64_t* lay, int rank,
                                 int world, uint8_t* out, uint8_t* runb, bool emit) {
-  if (emit)
-    hipLaunchKernelGGL(k_emit_dyn, dim3(std::max(1, resident_grid((const void*)&k_emit_dyn))), dim3(256), 0, s, nt, oc,
-                       lay, rank, world, out);
-  hipLaunchKernelGGL(k_shard_table_dyn, dim3(grid), dim3(256), 0, s, nt, oc, lay, rank, world, out, runb);
+  (void)grid;
+  hipLaunchKernelGGL(k_shard_dyn, dim3(std::max(1, resident_grid((const void*)&k_shard_dyn))), dim3(256), 0, s, nt, oc,
+                     lay, rank, world, out, runb, emit ? 1 : 0);
 }
 void launch_layout_out(hipStream_t s, const ResultInfo* info, int64_t* dst) {
   hipLaunchKernelGGL(k_layout_out, dim3(1), dim3(64), 0, s, info, dst);

@@ -65,15 +65,11 @@ __device__ __forceinline__ void accumulate_segment(const CDesc* desc, const uint
       uint64_t x[kBGroup][4];
 #pragma unroll
       for (int u = 0; u < kBGroup; u++)
-#if RBG_WIDE_NT
-        if (k + u < nb) {
+        if (k + u < nb) {  // nontemporal: each input byte is read once (C3 clustered 0.70 -> 0.78 of peak)
           const uint4* p = reinterpret_cast<const uint4*>(payload + ((uint64_t)bslot[k + u] << 4));
           u4_to_words(ld_in(p + threadIdx.x), x[u][0], x[u][1]);
           u4_to_words(ld_in(p + threadIdx.x + NT), x[u][2], x[u][3]);
         }
-#else
-        if (k + u < nb) load_bitmap_owned(payload + ((uint64_t)bslot[k + u] << 4), x[u]);
-#endif
 #pragma unroll
       for (int u = 0; u < kBGroup; u++)
         if (k + u < nb) {
@@ -122,11 +118,7 @@ __device__ __forceinline__ void stream_or_values(uint32_t* acc, const uint8_t* b
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t k = j0 + u * NT + threadIdx.x;
-#if RBG_WIDE_NT
-      v[u] = k < nvec ? ld_in(v4 + k) : make_uint4(0, 0, 0, 0);
-#else
-      v[u] = k < nvec ? v4[k] : make_uint4(0, 0, 0, 0);
-#endif
+      v[u] = k < nvec ? ld_in(v4 + k) : make_uint4(0, 0, 0, 0);  // nontemporal: read once
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
