@@ -737,13 +737,8 @@ __device__ __forceinline__ bool small_pair(const PairItem& it) {
 __device__ __forceinline__ void small_pair_load(const PairItem& it, const uint8_t* payload, int lane, uint4& va,
                                                 uint4& vb) {
   const uint32_t na = (it.card_a + 7) >> 3, nb = (it.card_b + 7) >> 3;
-#if RBG_C4_NT
-  va = (uint32_t)lane < na ? ld_in(reinterpret_cast<const uint4*>(payload + it.slot_a) + lane) : make_uint4(0, 0, 0, 0);
-  vb = (uint32_t)lane < nb ? ld_in(reinterpret_cast<const uint4*>(payload + it.slot_b) + lane) : make_uint4(0, 0, 0, 0);
-#else
   va = (uint32_t)lane < na ? reinterpret_cast<const uint4*>(payload + it.slot_a)[lane] : make_uint4(0, 0, 0, 0);
   vb = (uint32_t)lane < nb ? reinterpret_cast<const uint4*>(payload + it.slot_b)[lane] : make_uint4(0, 0, 0, 0);
-#endif
 }
 __device__ __forceinline__ uint32_t small_arrays_and_card(const uint4 va, uint32_t ca, const uint4 vb, uint32_t cb,
                                                          uint32_t* lds, int lane) {
