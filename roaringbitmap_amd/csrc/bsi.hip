@@ -619,11 +619,7 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
     if (wn < nunits) bmask_n = request_slices(en, wn);
     // this unit's result words to the task's scratch slot (the container itself when
     // it is a bitmap, else the input k_bsi_defer stages it from)
-#if RBG_BSI_NTST
-    __builtin_nontemporal_store(res, reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes) + w);
-#else
     reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[w] = res;
-#endif
     sum_rows_unit(rows, want_sum ? kRowSum + nb : kRowSum, cnts + ((size_t)t * kBsiUnits + u) * kBsiCnt);
     if (u == 0 && tid < kBsiKin) {  // the key's input types, for k_bsi_types
       const int i = tid == kBsiRegSlices ? 0 : tid == kBsiRegSlices + 1 ? (P.has_found ? nb + 1 : 0) : 1 + tid;
