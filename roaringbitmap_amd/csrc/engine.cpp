@@ -45,7 +45,7 @@ static void set_err(const std::string& s) { g_err = s; }
 
 constexpr size_t kSlack = 256;  // every device buffer carries read slack (group_copy)
 constexpr int kMaxKeys = 65536;
-constexpr size_t kLbHeader = 2048;  // look-back state: error @64, result card @96; claim counters @1024 (kDynOff)
+constexpr size_t kLbHeader = 256;  // look-back state: error @64, result card @96
 // tile statuses (kMaxTiles, device.hpp) follow the 65536 task statuses, tile cardinalities them
 
 // RBG_DEBUG_SYNC=1: synchronise and report after every pipeline stage (debugging aid)

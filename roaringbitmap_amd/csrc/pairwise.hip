@@ -593,78 +593,6 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
     }
     return;
   }
-#if RBG_DYN
-  // Experiment: per-XCD claim queues.  Task list segment x = [x seg, (x + 1) seg) is claimed in
-  // chunks of kDynChunk by the waves of XCD x (counter at the look-back header + 1024 + 128 x,
-  // zeroed by the plan kernel); a wave whose queue is exhausted reads all counters at once and
-  // claims from one with work left.  Each wave keeps one claim in flight.
-  {
-    constexpr uint32_t kDynChunk = 4;
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    uint32_t* dyn = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(oc.err) + (1024 - 64));
-    const uint32_t seg = (nt + 7) / 8;
-    uint32_t q = xcc & 7;
-    const int l = lane_id();
-    auto issue = [&]() -> uint32_t {
-      uint32_t v = 0;
-      if (l == 0) v = atomicAdd(dyn + 32 * q, kDynChunk);
-      return v;
-    };
-    // the chunk of claim v_lane0 on queue q, else another queue's; false once every queue is empty
-    auto resolve = [&](uint32_t v_lane0, uint32_t& lo, uint32_t& n) -> bool {
-      for (;;) {
-        const uint32_t v = uni(v_lane0);
-        const uint32_t s_lo = q * seg, s_hi = min(nt, s_lo + seg);
-        if (s_lo + v < s_hi) {
-          lo = s_lo + v;
-          n = min(kDynChunk, s_hi - lo);
-          return true;
-        }
-        // exhausted: read every queue's counter (one round trip), pick one with work left
-        uint32_t left = 0;
-        if (l < 8) {
-          const uint32_t c = __hip_atomic_load(dyn + 32 * l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const uint32_t a = (uint32_t)l * seg, b = min(nt, a + seg);
-          left = a + c < b ? 1u : 0u;
-        }
-        const uint64_t m = __ballot(left != 0);
-        if (m == 0) return false;
-        q = (uint32_t)__builtin_ctzll(m);
-        v_lane0 = issue();
-      }
-    };
-    uint32_t lo, n;
-    if (!resolve(issue(), lo, n)) return;
-    uint32_t pend = issue();
-    t = lo;
-    uint32_t left_in_chunk = n;
-    PTask cur = load_task(tasks, t);
-    for (;;) {
-      uint32_t tn = 0;
-      bool more = true;
-      if (left_in_chunk > 1) {
-        tn = t + 1;
-        left_in_chunk--;
-      } else {
-        uint32_t nlo, nn;
-        more = resolve(pend, nlo, nn);
-        if (more) {
-          tn = nlo;
-          left_in_chunk = nn;
-          pend = issue();
-        }
-      }
-      PTask nxt;
-      if (more) nxt = load_task(tasks, tn);
-      any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
-      if (!more) break;
-      t = tn;
-      cur = nxt;
-    }
-    return;
-  }
-#endif
   PTask cur = load_task(tasks, t);
 #if RBG_STAMPS
   StampAcc sacc = {};

@@ -448,8 +448,7 @@ __device__ __forceinline__ int lower_bound_u16(const uint16_t* keys, int n, uint
 // kernel; saves two memset launches per op).  Either pointer may be null.
 __device__ __forceinline__ void plan_zero(uint64_t* lb_header, uint64_t* tile_status) {
   if (blockIdx.x != 0) return;
-  if (lb_header)
-    for (uint32_t i = threadIdx.x; i < 256u; i += blockDim.x) lb_header[i] = 0;  // the 2 KiB header
+  if (lb_header && threadIdx.x < 32) lb_header[threadIdx.x] = 0;
   if (tile_status)
     for (uint32_t i = threadIdx.x; i < (uint32_t)kMaxTiles; i += blockDim.x) tile_status[i] = 0;
 }
