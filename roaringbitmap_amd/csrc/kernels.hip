@@ -267,7 +267,11 @@ __global__ __launch_bounds__(256) void k_batch_bytes(const CDesc* __restrict__ d
 // scan placement: tile scan of the task records (uniform tiles, so a decoupled
 // look-back over tiles never waits on a slow container), then the payload copy
 // ===========================================================================
+#if RBG_KTILE512
+constexpr int kTile = 512;  // experiment: tasks per workgroup tile (2 per thread), <= kMaxTiles tiles
+#else
 constexpr int kTile = 1024;  // tasks per workgroup tile (4 per thread)
+#endif
 
 // Look-back of tile t over all earlier tiles at once (t < 64): lane i reads the
 // status of tile t - 1 - i; the nearest inclusive status ends the window, and every
@@ -288,9 +292,10 @@ __device__ __forceinline__ Prefix lookback_wave(uint64_t* status, uint32_t t, ui
                                  : (2ull << 62);  // before tile 0: an empty inclusive prefix
       const uint32_t st = (uint32_t)(sv >> 62);
       const uint64_t incl = __ballot(st == 2);  // lane t-1-0 ... : the nearest inclusive is the lowest lane
-      const int k = __builtin_ctzll(incl);       // exists: lane t (tile -1) is always inclusive
+      // exists for t <= 64 (lane t, tile -1, is always inclusive); further back, wait for one
+      const int k = incl ? __builtin_ctzll(incl) : 64;
       const uint64_t window = k >= 63 ? ~0ull : ((2ull << k) - 1);
-      if ((__ballot(st == 0) & window) == 0) {
+      if (incl != 0 && (__ballot(st == 0) & window) == 0) {
         const bool in = lane <= k;
         uint64_t c = in ? (sv >> 44) & 0x1FFFF : 0, by = in ? sv & ((1ULL << 44) - 1) : 0;
         const uint32_t r = in ? (uint32_t)((sv >> 61) & 1) : 0u;
@@ -336,13 +341,14 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
   }
   const uint32_t tile = blockIdx.x;
   if (tile >= ntiles) return;
-  const uint32_t t0 = tile * kTile + 4 * threadIdx.x;
-  uint32_t keep[4], len[4], run[4];
+  constexpr int kPer = kTile / 256;  // records per thread
+  const uint32_t t0 = tile * kTile + kPer * threadIdx.x;
+  uint32_t keep[kPer], len[kPer], run[kPer];
   uint32_t c = 0, r = 0;
   unsigned long long b = 0;
-  uint32_t card = 0;  // <= 4 x 65536 per thread
+  uint32_t card = 0;  // <= kPer x 65536 per thread
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < kPer; i++) {
     keep[i] = len[i] = run[i] = 0;
     if (t0 + i < nt) {
       const ORec x = oc.recs[t0 + i];
@@ -377,7 +383,7 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
   __syncthreads();
   uint32_t oc_c = 0, tot_c = 0, tot_r = 0;
   unsigned long long oc_b = 0, tot_b = 0, tot_card = 0;
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < kPer; i++) {
     if (i < w) {
       oc_c += wsum[0][i];
       oc_b += wbytes[i];
@@ -396,7 +402,7 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
   uint32_t idx = shp.idx + oc_c + (uint32_t)pc;
   unsigned long long off = shp.off + oc_b + (sb - b);
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
+  for (int i = 0; i < kPer; i++) {
     if (t0 + i < nt) {
       oc.recs[t0 + i].idx = idx;
       oc.recs[t0 + i].off = off;
@@ -409,8 +415,8 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
     // every earlier tile is published (its status was read as aggregate or inclusive,
     // with acquire): sum the tile cardinalities
     unsigned long long cs = threadIdx.x == 0 ? tot_card : 0;
-    if (threadIdx.x < tile)
-      cs += __hip_atomic_load(oc.tile_card + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = threadIdx.x; i < tile; i += 64)
+      cs += __hip_atomic_load(oc.tile_card + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (int o = 32; o > 0; o >>= 1) cs += __shfl_xor(cs, o, 64);
     if (threadIdx.x == 0) {
       reinterpret_cast<unsigned long long*>(oc.err)[kCardWord] = cs;
@@ -597,7 +603,7 @@ void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, cons
 }
 
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info) {
-  hipLaunchKernelGGL(k_place, dim3(64), dim3(256), 0, s, nt, oc, info);
+  hipLaunchKernelGGL(k_place, dim3(65536 / kTile), dim3(256), 0, s, nt, oc, info);
 }
 void launch_spec_fix(hipStream_t s, const uint32_t* nt, OutCtx oc) {
   hipLaunchKernelGGL(k_spec_fix, dim3(std::max(1, resident_grid((const void*)&k_spec_fix))), dim3(256), 0, s, nt, oc);
