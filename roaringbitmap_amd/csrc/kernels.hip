@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
   __syncthreads();
   uint32_t oc_c = 0, tot_c = 0, tot_r = 0;
   unsigned long long oc_b = 0, tot_b = 0, tot_card = 0;
-  for (int i = 0; i < kPer; i++) {
+  for (int i = 0; i < 4; i++) {  // the workgroup's 4 waves
     if (i < w) {
       oc_c += wsum[0][i];
       oc_b += wbytes[i];
