@@ -267,11 +267,7 @@ __global__ __launch_bounds__(256) void k_batch_bytes(const CDesc* __restrict__ d
 // scan placement: tile scan of the task records (uniform tiles, so a decoupled
 // look-back over tiles never waits on a slow container), then the payload copy
 // ===========================================================================
-#if RBG_KTILE512
-constexpr int kTile = 512;  // experiment: tasks per workgroup tile (2 per thread), <= kMaxTiles tiles
-#else
-constexpr int kTile = 1024;  // tasks per workgroup tile (4 per thread)
-#endif
+constexpr int kTile = 1024;  // tasks per workgroup tile (4 per thread; 512-record tiles measured slower)
 
 // Look-back of tile t over all earlier tiles at once (t < 64): lane i reads the
 // status of tile t - 1 - i; the nearest inclusive status ends the window, and every

@@ -593,42 +593,6 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
     }
     return;
   }
-#if RBG_XW
-  // Experiment (planned form only): static task shares per XCD proportional to the XCDs' speeds
-  // measured on one box (mean wave end per XCD, C2 mix); blocks of 256 tasks, XCD x owning
-  // [S[x], S[x+1]) of each.  A wave's index within its XCD comes from a counter in the zeroed
-  // look-back header (bytes 128..159); every XCD holds gridDim.x / 8 workgroups.
-  if (gridDim.x % 8 == 0) {
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 7;
-    constexpr uint32_t kB = 256;
-    constexpr uint32_t S[9] = {0, 40, 77, 102, 125, 154, 176, 222, 256};
-    uint32_t* ctr = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(oc.err) + 64);
-    uint32_t jv = 0;
-    if (lane_id() == 0) jv = atomicAdd(ctr + xcc, 1u);
-    const uint32_t j = uni(jv);
-    const uint32_t nwx = (gridDim.x / 8) * kWaves;
-    if (j >= nwx) return;
-    const uint32_t lo = S[xcc], len = S[xcc + 1] - S[xcc];
-    auto task_of = [&](uint32_t k) -> uint32_t { return (k / len) * kB + lo + (k % len); };
-    uint32_t k = j;
-    t = task_of(k);
-    if (t >= nt) return;
-    PTask cur = load_task(tasks, t);
-    for (;;) {
-      const uint32_t kn = k + nwx, tn = task_of(kn);
-      PTask nxt;
-      if (tn < nt) nxt = load_task(tasks, tn);
-      any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
-      if (tn >= nt) break;
-      k = kn;
-      t = tn;
-      cur = nxt;
-    }
-    return;
-  }
-#endif
   PTask cur = load_task(tasks, t);
 #if RBG_STAMPS
   StampAcc sacc = {};
