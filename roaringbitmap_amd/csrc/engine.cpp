@@ -996,24 +996,33 @@ static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) 
   // Temps: at most N/2 + 1 are live at once (every priorityqueue_or temp starts from two
   // inputs; a priorityqueue_xor step allocates one while its operands are still queued).
   // Each has one 16 B state per union key; containers that are not input clones live in
-  // 8 KiB arena blocks owned by exactly one temp key, and live temps cover disjoint
-  // inputs, so 2 x the batch's containers bounds the blocks in use (one step's fresh
-  // blocks come off the stack before its freed ones go back).
+  // 8 KiB arena blocks from the key's own pool: floor(n_t / 2) blocks for a key held by
+  // n_t inputs (pq.hip), at most half the batch's containers in all.
   const size_t n_slots = N / 2 + 2;
   const size_t stride = std::max<uint32_t>(h_nt, 1);
   const size_t st_bytes = n_slots * stride * sizeof(PQState);
-  size_t n_blk = 2 * B->n_ctr + 64;
+  std::vector<Task> h_tasks(h_nt);
+  if (h_nt) HIPCHK(hipMemcpyAsync(h_tasks.data(), c->tasks.p, sizeof(Task) * h_nt, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<uint32_t> kbase(stride, 0);
+  std::vector<int32_t> ktop(stride, 0);
+  size_t n_blk = 0;
+  for (uint32_t t = 0; t < h_nt; t++) {
+    kbase[t] = (uint32_t)n_blk;
+    ktop[t] = h_tasks[t].b / 2;
+    n_blk += (size_t)ktop[t];
+  }
+  n_blk = std::max<size_t>(n_blk, 1);
   size_t free_b = 0, total_b = 0;
   pool_clear(c);  // pooled buffers would count as used
   HIPCHK(hipMemGetInfo(&free_b, &total_b));
   const size_t budget = free_b / 10 * 9;
-  if (st_bytes > budget / 2) {
-    set_err("priorityqueue: " + std::to_string(n_slots) + " temps x " + std::to_string(stride) +
-            " union keys need " + std::to_string(st_bytes >> 20) + " MiB of temp state (more than half the free "
-            "device memory); use FastAggregation.or / xor");
+  if (st_bytes + n_blk * 8192 > budget) {
+    set_err("priorityqueue: " + std::to_string(n_slots) + " temps x " + std::to_string(stride) + " union keys and " +
+            std::to_string(n_blk) + " 8 KiB blocks need " + std::to_string((st_bytes + n_blk * 8192) >> 20) +
+            " MiB of temp state (more than the free device memory); use FastAggregation.or / xor");
     return RBG_ERR_OUT_OF_MEMORY;
   }
-  n_blk = std::max<size_t>(1, std::min(n_blk, (budget - st_bytes) / 8192));
   // host: add every input, plan the first step
   std::vector<PQEnt> heap(N);
   std::vector<int32_t> nodes(2 * N);
@@ -1026,17 +1035,33 @@ static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) 
   ctl.step.n_nodes = (int32_t)N;
   ctl.step.slot_top = (int32_t)n_slots;
   ctl.step.rel1 = ctl.step.rel2 = -1;
-  ctl.free_top = (int32_t)n_blk;
   PQHost hm{heap, nodes, tmp, slots};
   for (size_t k = 0; k < N; k++) hm.add(ctl.step, PQEnt{8 + (int64_t)leaf[k], (int32_t)k, 0});
   pq_plan(hm, ctl.step);
+  // Block ids level-major: pool position j of key t is block lvl[j] + rank[t], with the keys
+  // ranked by pool size (largest first, stable), so level j holds the keys with more than j
+  // blocks contiguously.  Keys pop their positions 0, 1, ... in order, so the workgroups of
+  // neighbouring keys write neighbouring blocks (uniform data: one contiguous level per
+  // step instead of blocks a pool apart).
+  std::vector<uint32_t> order(h_nt);
+  for (uint32_t t = 0; t < h_nt; t++) order[t] = t;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return ktop[x] > ktop[y]; });
+  std::vector<uint32_t> rank(h_nt);
+  for (uint32_t i = 0; i < h_nt; i++) rank[order[i]] = i;
+  const int32_t max_cap = h_nt ? ktop[order[0]] : 0;
+  std::vector<size_t> lvl(max_cap + 1, 0);
+  for (int32_t j = 0, i = (int32_t)h_nt; j < max_cap; j++) {  // keys with more than j blocks: the first i
+    while (i > 0 && ktop[order[i - 1]] <= j) i--;
+    lvl[j + 1] = lvl[j] + (size_t)i;
+  }
   std::vector<int32_t> stack(n_blk);
-  for (size_t k = 0; k < n_blk; k++) stack[k] = (int32_t)k;
+  for (uint32_t t = 0; t < h_nt; t++)
+    for (int32_t i = 0; i < ktop[t]; i++) stack[kbase[t] + i] = (int32_t)(lvl[ktop[t] - 1 - i] + rank[t]);
   // device copies
   auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   const size_t o_heap = al(sizeof(PQCtl)), o_node = o_heap + al(16 * N), o_tmp = o_node + al(8 * N),
-               o_slots = o_tmp + al(2 * N), o_stack = o_slots + al(4 * n_slots), o_freed = o_stack + al(4 * n_blk),
-               o_end = o_freed + al(8 * stride);
+               o_slots = o_tmp + al(2 * N), o_stack = o_slots + al(4 * n_slots), o_base = o_stack + al(4 * n_blk),
+               o_top = o_base + al(4 * stride), o_end = o_top + al(4 * stride);
   DevBuf meta, states, arena;
   CHK(meta.ensure(o_end));
   CHK(states.ensure(st_bytes));
@@ -1048,10 +1073,12 @@ static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) 
   HIPCHK(hipMemcpyAsync(mb + o_tmp, tmp.data(), 2 * N, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(mb + o_slots, slots.data(), 4 * n_slots, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(mb + o_stack, stack.data(), 4 * n_blk, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(mb + o_base, kbase.data(), 4 * stride, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(mb + o_top, ktop.data(), 4 * stride, hipMemcpyHostToDevice, s));
   const PQDev D{reinterpret_cast<PQCtl*>(mb), reinterpret_cast<PQEnt*>(mb + o_heap),
                 reinterpret_cast<int32_t*>(mb + o_node), mb + o_tmp, reinterpret_cast<int32_t*>(mb + o_slots),
                 states.as<PQState>(), stride, arena.as<uint64_t>(), reinterpret_cast<int32_t*>(mb + o_stack),
-                reinterpret_cast<int32_t*>(mb + o_freed)};
+                reinterpret_cast<const uint32_t*>(mb + o_base), reinterpret_cast<int32_t*>(mb + o_top)};
   const PQArgs pa{B->desc.as<CDesc>(), B->bm.as<uint32_t>(), B->payload.as<uint8_t>()};
   const int grid = grid_for(h_nt, 65536);
   for (size_t k = 0; k + 1 < N; k++) {
@@ -1066,7 +1093,7 @@ static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) 
   HIPCHK(hipMemcpyAsync(&done, mb, sizeof(done), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));  // the temps are freed on return
   if (done.err || !done.step.final_step) {
-    set_err(done.err ? "priorityqueue: the temp block arena (" + std::to_string(n_blk) + " x 8 KiB) ran out"
+    set_err(done.err ? "priorityqueue: a key's block pool ran out (" + std::to_string(n_blk) + " x 8 KiB in all)"
                      : std::string("priorityqueue: the device queue did not finish"));
     return done.err ? RBG_ERR_OUT_OF_MEMORY : RBG_ERR_DEVICE;
   }

@@ -72,13 +72,22 @@ struct PQStep {
   int32_t rel1, rel2;  // temp slots freed after the step (-1: none)
   int32_t heap_n, n_nodes, slot_top, or_mode;
 };
+// A step's workgroups report in kPQGroups groups (blockIdx % kPQGroups), each counter and
+// size word in a cache line of its own: one contended address serialises its atomics
+// (~12 ns each), so a launch of G workgroups pays G / kPQGroups of them on the longest chain.
+constexpr int kPQGroups = 8;
+struct __align__(128) PQLine {
+  uint32_t done;  // workgroups of the group finished in the running step
+  uint32_t pad;
+  unsigned long long size;  // the group's share of the step's result size
+  uint8_t pad2[112];
+};
 struct PQCtl {
   PQStep step;
-  int32_t free_top;  // block stack top (pops during a step)
-  uint32_t freed_n;  // blocks freed by the running step (pushed by its last workgroup)
-  uint32_t done;     // workgroups finished in the running step
-  uint32_t err;      // the block arena ran out
-  unsigned long long size;
+  uint32_t done;  // groups finished in the running step
+  uint32_t err;   // a key's block pool ran out (cannot happen: see ctx_pq)
+  uint8_t pad[72];
+  PQLine grp[kPQGroups];
 };
 struct PQDev {
   PQCtl* ctl;
@@ -89,8 +98,11 @@ struct PQDev {
   PQState* states;    // temp slot s: states[s * stride + task]
   uint64_t stride;
   uint64_t* arena;    // 8 KiB blocks (1024 words)
-  int32_t* blk_stack; // free blocks
-  int32_t* freed;     // blocks freed by the running step
+  // Per key, a private pool of arena blocks: the free blocks of key t are
+  // kstack[kbase[t] .. kbase[t] + ktop[t]).  Only the workgroup of key t touches them.
+  int32_t* kstack;
+  const uint32_t* kbase;
+  int32_t* ktop;
 };
 struct PQArgs {
   const CDesc* desc;

@@ -16,10 +16,11 @@
 // index of the input container it is an unchanged clone of, or an 8 KiB block of the
 // set arena holding the container as a bitmap.  Blocks move with the data: a step's
 // result reuses an operand temp's block at that key (every operand temp is consumed by
-// its step -- updated in place or released), a fresh block comes off the free stack only
-// where neither operand has one, and blocks left over go back after the step.  A temp
-// therefore holds blocks only for its own keys, so live blocks stay within the batch's
-// container count (live temps cover disjoint sets of inputs).
+// its step -- updated in place or released), a fresh block comes off the key's own pool
+// only where neither operand has one, and blocks left over go back to it.  A block at key
+// t holds the combination of at least two of the key's input containers and live temps
+// cover disjoint sets of inputs, so a pool of floor(n_t / 2) blocks (n_t = the inputs
+// holding key t) never runs out, and no two workgroups share a pool (no atomics).
 // Kinds follow the reference's lazy algebra
 // (RB/Container.java:717-774 lazyIOR / lazyOR): a lazy bitmap (card -1 in the
 // reference) is kept apart from an exact one, because repairAfterLazy converts
@@ -30,13 +31,6 @@
 #include "wave.hpp"
 
 namespace rbg {
-
-__device__ __forceinline__ int block_card4(const uint64_t r[4], int* sh) {
-  int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
-  int u = 0;
-  block_sum2(c, u, sh);
-  return (int)uni((uint32_t)c);
-}
 
 // lazy OR of a run and an array container: RunContainer.lazyorToRun +
 // convertToLazyBitmapIfNeeded (RB/RunContainer.java:1769-1813, 861-875): a full
@@ -62,20 +56,53 @@ __device__ __forceinline__ uint8_t* pq_block(const PQDev& D, int blk) {
   return reinterpret_cast<uint8_t*>(D.arena + (uint64_t)blk * 1024);
 }
 
-// Node `ref` at task t (segment [s, s + n) of the key-major batch).  A leaf's container
-// is found by a binary search of the segment's input indices (ascending, uniform loads).
-__device__ __forceinline__ PQNode pq_load(int ref, const PQDev& D, const PQArgs& A, uint32_t t, uint32_t s,
-                                          uint32_t n) {
+// Positions of inputs ra and rb (< 0: a temp, not searched) in the segment's ascending
+// input indices bm[s, s + n), n when absent: a 64-way search by each wave (lane i samples
+// position lo + i * step; the samples below ref are a prefix, so their count brackets
+// it), one dependent load round per factor of 64 -- two rounds up to 4,096 inputs at the
+// key -- and both searches' loads issued together in each round.
+__device__ __forceinline__ void leaf_find2(const uint32_t* bm, uint32_t s, uint32_t n, int ra, int rb, uint32_t* at) {
+  const uint32_t lane = (uint32_t)lane_id();
+  const uint32_t ref[2] = {(uint32_t)ra, (uint32_t)rb};
+  uint32_t lo[2] = {0, 0}, hi[2] = {n, n};
+  bool done[2] = {ra < 0, rb < 0};
+  at[0] = at[1] = n;
+  while (!(done[0] && done[1])) {
+    uint32_t v[2], step[2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) {  // every load of the round first
+      step[i] = hi[i] - lo[i] <= 64 ? 1 : (hi[i] - lo[i] + 63) >> 6;
+      const uint32_t p = lo[i] + lane * step[i];
+      v[i] = !done[i] && p < hi[i] ? bm[s + p] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      if (done[i]) continue;
+      const uint32_t k = (uint32_t)__popcll(__ballot(v[i] < ref[i]));
+      if (step[i] == 1 || k == 0) {  // the lower bound is lo + k (k == 0: lane 0 sampled lo)
+        const uint32_t p = step[i] == 1 ? lo[i] + k : lo[i];
+        uint32_t x;
+        if (p < hi[i]) x = (uint32_t)__builtin_amdgcn_readlane((int)v[i], step[i] == 1 ? (int)k : 0);
+        else x = p < n ? bm[s + p] : 0xFFFFFFFFu;
+        at[i] = x == ref[i] ? p : n;
+        done[i] = true;
+      } else {
+        const uint32_t nlo = lo[i] + (k - 1) * step[i] + 1;
+        hi[i] = min(hi[i], lo[i] + k * step[i]);
+        lo[i] = nlo;
+      }
+    }
+  }
+}
+
+// Node `ref` at task t (segment [s, s + n) of the key-major batch); `pos`: a leaf's
+// position in the segment (leaf_find2).
+__device__ __forceinline__ PQNode pq_load(int ref, uint32_t pos, const PQDev& D, const PQArgs& A, uint32_t t,
+                                          uint32_t s, uint32_t n) {
   PQNode x{0, PK_A, 0, 0, -1, -1};
   if (ref >= 0) {
-    uint32_t lo = 0, hi = n;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (A.bm[s + mid] < (uint32_t)ref) lo = mid + 1;
-      else hi = mid;
-    }
-    if (lo < n && A.bm[s + lo] == (uint32_t)ref) {
-      const uint32_t j = s + lo;
+    if (pos < n) {
+      const uint32_t j = s + pos;
       const CDesc d = A.desc[j];
       x.present = 1;
       x.kind = d.kind;  // DK_A / DK_B (= PK_BE) / DK_R
@@ -95,6 +122,25 @@ __device__ __forceinline__ PQNode pq_load(int ref, const PQDev& D, const PQArgs&
   return x;
 }
 
+// a node's container into one wave's registers / combined into them (OR or XOR); `lds` is
+// the wave's 8 KiB bitmap
+__device__ __forceinline__ void w_pq_materialize(const PQNode& x, const PQDev& D, const PQArgs& A, uint32_t* lds,
+                                                 WCtr& r) {
+  if (x.src >= 0) w_materialize(A.desc[x.src], A.payload, lds, r);
+  else if (x.blk >= 0) w_load_bitmap(pq_block(D, x.blk), r);
+  else w_zero(r);  // a pool ran out in an earlier step (reported through ctl->err)
+}
+template <int OP>  // 1 or, 2 xor (wave.hpp w_op)
+__device__ __forceinline__ void w_pq_combine(const PQNode& x, const PQDev& D, const PQArgs& A, uint32_t* lds,
+                                             WCtr& r) {
+  if (x.src >= 0) {
+    w_combine<OP>(A.desc[x.src], A.payload, lds, r);
+  } else if (x.blk >= 0) {
+    const CDesc d{0, 0, 0, (uint8_t)DK_B, 0};
+    w_combine<OP>(d, pq_block(D, x.blk), lds, r);
+  }
+}
+
 __device__ __forceinline__ void pq_materialize(const PQNode& x, const PQDev& D, const PQArgs& A, uint32_t* lds, int* q,
                                                uint64_t r[4]) {
   if (x.src >= 0) {
@@ -111,17 +157,16 @@ __device__ __forceinline__ int pq_size(int kind, int card, int nruns) {  // getS
 }
 
 // The kind of one step's result where both operands hold the key.  `a` is the
-// receiver of the reference's call, `b` its argument; r is the union (OR) or the
-// symmetric difference (XOR).  *c / *nr: cardinality / runs of r as needed.
-__device__ __forceinline__ int pq_kind(int op, const PQNode& a, const PQNode& b, const uint64_t r[4], uint32_t* lds,
-                                       int* sh, int* c, int* nr) {
-  *c = block_card4(r, sh);
+// receiver of the reference's call, `b` its argument; x (one wave's registers) is the
+// union (OR) or the symmetric difference (XOR).  *c / *nr: cardinality / runs of x as needed.
+__device__ __forceinline__ int pq_kind(int op, const PQNode& a, const PQNode& b, const WCtr& x, int* c, int* nr) {
+  *c = w_card(x);
   *nr = 0;
   if (op == PQ_XOR) {  // RoaringBitmap.xor(x1, x2): the pairwise XOR types (App. A)
     if (*c == 0) return -1;  // dropped
     const int ka = a.kind == PK_BL ? DK_B : a.kind, kb = b.kind == PK_BL ? DK_B : b.kind;
     if (pairwise_needs_runs(OPR_XOR, ka, a.card, kb, b.card)) {
-      *nr = count_runs(r, lds, sh);
+      *nr = w_runs(x);
       return eff(*c, *nr);
     }
     return by_card(*c);
@@ -133,10 +178,10 @@ __device__ __forceinline__ int pq_kind(int op, const PQNode& a, const PQNode& b,
     if (a_bm || b_bm) return PK_BL;  // BitmapContainer.lazyor(A|B|R) / A|R lazyor(B): a lazy bitmap clone
     if (a.kind == PK_R && b.kind == PK_R) {  // RunContainer.or(RunContainer) (:1952-1986)
       if (a.card == 65536 || b.card == 65536) return PK_R;
-      *nr = count_runs(r, lds, sh);
+      *nr = w_runs(x);
       return eff(*c, *nr);
     }
-    *nr = count_runs(r, lds, sh);  // A|R, R|A: lazyorToRun
+    *nr = w_runs(x);  // A|R, R|A: lazyorToRun
     return pq_run_lazyor_kind((a.kind == PK_R ? a.card : b.card) == 65536, *c, *nr);
   }
   // Container.lazyIOR (RB/Container.java:717-740), receiver a.  lazyorfromlazyinputs
@@ -145,18 +190,18 @@ __device__ __forceinline__ int pq_kind(int op, const PQNode& a, const PQNode& b,
   if (a.kind == PK_A) {
     if (b.kind == PK_A) return a.card + b.card > 1024 ? PK_BL : PK_A;  // ArrayContainer.lazyor
     if (b_bm) return *c == 65536 ? PK_R : PK_BE;  // ior(BitmapContainer) = b.or(this), exact (:1064-1085)
-    *nr = count_runs(r, lds, sh);                 // b.lazyor(this)
+    *nr = w_runs(x);                 // b.lazyor(this)
     return pq_run_lazyor_kind(b.card == 65536, *c, *nr);
   }
   // a is a run container
   if (a.card == 65536) return PK_R;  // a full run container returns itself (RB/RunContainer.java:1198-1240,1500-1550)
   if (b_bm) return *c == 65536 ? PK_R : PK_BE;  // RunContainer.or(BitmapContainer), exact (:1932-1949)
   if (b.kind == PK_A) {
-    *nr = count_runs(r, lds, sh);  // ilazyorToRun
+    *nr = w_runs(x);  // ilazyorToRun
     return pq_run_lazyor_kind(false, *c, *nr);
   }
   if (b.card == 65536) return PK_R;  // RunContainer.or(RunContainer)
-  *nr = count_runs(r, lds, sh);
+  *nr = w_runs(x);
   return eff(*c, *nr);
 }
 
@@ -281,25 +326,38 @@ struct PQWave {
 };
 
 // One step of the queue over every union key: out = op(a, b), the step record's operands.
-// out may be a's temp (the in-place x1.lazyor and lazyorfromlazyinputs).  The launch's
-// last workgroup returns the step's freed blocks to the stack and plans the next step.
+// out may be a's temp (the in-place x1.lazyor and lazyorfromlazyinputs).  One wave per key
+// (grid-stride over the resident grid's waves; a key's chain of dependent loads -- task,
+// leaf search, descriptor, payload or block -- is latency, so the more keys in flight the
+// better: a wave per key keeps 4x the keys of a workgroup per key in flight per CU).  The
+// launch's last workgroup plans the next step.
 __global__ __launch_bounds__(256) void k_pq_step(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                                  PQArgs A, PQDev D) {
-  __shared__ __align__(16) uint32_t lds[2048];
-  __shared__ int q[257];
-  __shared__ int sh[8];
-  __shared__ int blk_sh;
+  __shared__ __align__(16) uint32_t lds_w[4][2048];
+  __shared__ unsigned long long acc_w[4];
   __shared__ int last;
+  const int wv = (int)(threadIdx.x >> 6), lane = lane_id();
+  uint32_t* lds = lds_w[wv];
   const int op = D.ctl->step.op;
   const int a_ref = D.ctl->step.a, b_ref = D.ctl->step.b, o_ref = D.ctl->step.o;
   PQState* const o_st = pq_states(D, o_ref);
   const uint32_t nt = *n_tasks;
   unsigned long long acc = 0;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+  for (uint32_t t = uni(blockIdx.x * 4 + (uint32_t)wv); t < nt; t += gridDim.x * 4) {
     const Task tk = tasks[t];
     const uint32_t s = (uint32_t)tk.a, n = (uint32_t)tk.b;
-    PQNode a = pq_load(a_ref, D, A, t, s, n);
-    PQNode b = pq_load(b_ref, D, A, t, s, n);
+    // lane 0: the key's pool top and its next free block, in flight during the search
+    int32_t pool_top = 0, pool_blk = -1;
+    uint32_t pool_base = 0;
+    if (lane == 0) {
+      pool_base = D.kbase[t];
+      pool_top = D.ktop[t];
+      if (pool_top > 0) pool_blk = D.kstack[pool_base + pool_top - 1];
+    }
+    uint32_t pos[2];
+    leaf_find2(A.bm, s, n, a_ref, b_ref, pos);
+    PQNode a = pq_load(a_ref, pos[0], D, A, t, s, n);
+    PQNode b = pq_load(b_ref, pos[1], D, A, t, s, n);
     // lazyorfromlazyinputs: a bitmap container goes first (RB/RoaringBitmap.java:782-788)
     if (op == PQ_LFL && a.present && b.present && (b.kind == PK_BE || b.kind == PK_BL) &&
         !(a.kind == PK_BE || a.kind == PK_BL)) {
@@ -307,23 +365,20 @@ __global__ __launch_bounds__(256) void k_pq_step(const Task* __restrict__ tasks,
       a = b;
       b = x;
     }
-    __syncthreads();  // every thread has read the states before the output state is written
     PQState out{0, 0, 0, 0, -1, -1};
     // every operand temp is consumed by the step, so its blocks are the result's to
-    // reuse; the ones not reused go back to the stack after the step
+    // reuse; the ones not reused go back to the key's pool
     int spare0 = a.blk, spare1 = b.blk;
     bool write_set = false;
-    uint64_t r[4] = {0, 0, 0, 0};
+    WCtr r;
     if (a.present && b.present) {
-      uint64_t x[4];
-      pq_materialize(a, D, A, lds, q, r);
-      pq_materialize(b, D, A, lds, q, x);
-#pragma unroll
-      for (int i = 0; i < 4; i++) r[i] = op == PQ_XOR ? (r[i] ^ x[i]) : (r[i] | x[i]);
+      w_pq_materialize(a, D, A, lds, r);
+      if (op == PQ_XOR) w_pq_combine<2>(b, D, A, lds, r);
+      else w_pq_combine<1>(b, D, A, lds, r);
       int c, nr;
-      const int kind = pq_kind(op, a, b, r, lds, sh, &c, &nr);
+      const int kind = pq_kind(op, a, b, r, &c, &nr);
       if (kind >= 0) {
-        if (kind == PK_R && nr == 0) nr = c == 65536 ? 1 : count_runs(r, lds, sh);
+        if (kind == PK_R && nr == 0) nr = c == 65536 ? 1 : w_runs(r);
         out = PQState{(uint32_t)c, (uint16_t)nr, (uint8_t)kind, 1, -1, -1};
         write_set = true;
       }
@@ -337,9 +392,11 @@ __global__ __launch_bounds__(256) void k_pq_step(const Task* __restrict__ tasks,
         else spare1 = -1;
       }
     }
-    if (write_set) {
-      if (threadIdx.x == 0) {
-        int blk;
+    int blk = -1;
+    if (lane == 0) {
+      // the key's own block pool (no other wave touches it during the step)
+      int top = pool_top;
+      if (write_set) {
         if (spare0 >= 0) {
           blk = spare0;
           spare0 = -1;
@@ -347,37 +404,43 @@ __global__ __launch_bounds__(256) void k_pq_step(const Task* __restrict__ tasks,
           blk = spare1;
           spare1 = -1;
         } else {
-          const int i = atomicSub(&D.ctl->free_top, 1) - 1;
-          blk = i >= 0 ? pq_ld(&D.blk_stack[i]) : -1;
+          blk = pool_blk;
+          top--;
           if (blk < 0) atomicOr(&D.ctl->err, 1u);
         }
-        blk_sh = blk;
       }
-      lds_barrier();
-      out.blk = blk_sh;
-      if (out.blk >= 0) store_bitmap_owned(pq_block(D, out.blk), r);
+      if (spare0 >= 0) D.kstack[pool_base + top++] = spare0;
+      if (spare1 >= 0) D.kstack[pool_base + top++] = spare1;
+      if (top != pool_top) D.ktop[t] = max(top, 0);
     }
-    if (threadIdx.x == 0) {
-      if (spare0 >= 0) D.freed[atomicAdd(&D.ctl->freed_n, 1u)] = spare0;
-      if (spare1 >= 0) D.freed[atomicAdd(&D.ctl->freed_n, 1u)] = spare1;
+    if (write_set) {
+      out.blk = __builtin_amdgcn_readfirstlane(blk);
+      if (out.blk >= 0) w_store_bitmap(pq_block(D, out.blk), r);
+    }
+    if (lane == 0) {  // the operand states were read above (their values are in registers)
       o_st[t] = out;
       if (out.present) acc += (unsigned long long)pq_size(out.kind, (int)out.card, out.nruns);
     }
-    __syncthreads();  // blk_sh / lds reuse
   }
-  if (threadIdx.x == 0 && acc) atomicAdd(&D.ctl->size, acc);
-  // the last workgroup to finish schedules: every workgroup's freed entries and size are
-  // published (release) before its count, and acquired by the last one
-  __threadfence();
+  if (lane == 0) acc_w[wv] = acc;
   __syncthreads();
-  if (threadIdx.x == 0)
-    last = __hip_atomic_fetch_add(&D.ctl->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  if (threadIdx.x == 0) acc = acc_w[0] + acc_w[1] + acc_w[2] + acc_w[3];
+  // the last workgroup to finish schedules: each workgroup adds its size to its group's
+  // word and counts in (release); the group's last one counts the group in; the last
+  // group's last workgroup acquires every size
+  const int g = (int)(blockIdx.x % kPQGroups);
+  const uint32_t n_groups = min(gridDim.x, (uint32_t)kPQGroups);
+  const uint32_t in_group = (gridDim.x - (uint32_t)g + kPQGroups - 1) / kPQGroups;
+  if (threadIdx.x == 0) {
+    if (acc) atomicAdd(&D.ctl->grp[g].size, acc);
+    bool l = __hip_atomic_fetch_add(&D.ctl->grp[g].done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+             in_group - 1;
+    if (l) l = __hip_atomic_fetch_add(&D.ctl->done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == n_groups - 1;
+    last = l;
+  }
   __syncthreads();
   if (!last) return;
   __threadfence();
-  const uint32_t fn = pq_ld(&D.ctl->freed_n);
-  const int top0 = max(0, (int)pq_ld(&D.ctl->free_top));
-  for (uint32_t j = threadIdx.x; j < fn; j += NT) D.blk_stack[top0 + j] = D.freed[j];
   if (threadIdx.x >= 64) return;
   PQWave m{D, (int)threadIdx.x};
   PQStep c;
@@ -393,7 +456,8 @@ __global__ __launch_bounds__(256) void k_pq_step(const Task* __restrict__ tasks,
   c.n_nodes = pq_ld(&D.ctl->step.n_nodes);
   c.slot_top = pq_ld(&D.ctl->step.slot_top);
   c.or_mode = pq_ld(&D.ctl->step.or_mode);
-  const unsigned long long size = pq_ld(&D.ctl->size);
+  unsigned long long size = 0;
+  for (int k = 0; k < kPQGroups; k++) size += pq_ld(&D.ctl->grp[k].size);
   pq_finish(m, c, 8 + (int64_t)size);
   pq_plan(m, c);
   if (threadIdx.x == 0) {
@@ -408,10 +472,11 @@ __global__ __launch_bounds__(256) void k_pq_step(const Task* __restrict__ tasks,
     pq_st(&D.ctl->step.heap_n, c.heap_n);
     pq_st(&D.ctl->step.n_nodes, c.n_nodes);
     pq_st(&D.ctl->step.slot_top, c.slot_top);
-    pq_st(&D.ctl->free_top, top0 + (int)fn);
-    pq_st(&D.ctl->freed_n, 0u);
-    pq_st(&D.ctl->size, 0ull);
     pq_st(&D.ctl->done, 0u);
+  }
+  if (threadIdx.x < (unsigned)kPQGroups) {
+    pq_st(&D.ctl->grp[threadIdx.x].size, 0ull);
+    pq_st(&D.ctl->grp[threadIdx.x].done, 0u);
   }
 }
 
@@ -431,7 +496,9 @@ __global__ __launch_bounds__(256) void k_pq_final(const Task* __restrict__ tasks
   for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
     __syncthreads();
     const Task tk = tasks[t];
-    const PQNode x = pq_load(root, D, A, t, (uint32_t)tk.a, (uint32_t)tk.b);
+    uint32_t pos[2];
+    leaf_find2(A.bm, (uint32_t)tk.a, (uint32_t)tk.b, root, -1, pos);
+    const PQNode x = pq_load(root, pos[0], D, A, t, (uint32_t)tk.a, (uint32_t)tk.b);
     if (!x.present) {
       wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
       continue;
