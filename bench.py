@@ -345,6 +345,35 @@ def c2_oneshot(eng, a, b, steps):
             "pcie_inclusive_input_GBps": round((len(xa) + len(xb)) / per_call / 1e9, 2)}
 
 
+def pq_or_clustered(eng, n, steps):
+    """FastAggregation.priorityqueue_or (RB/FastAggregation.java:737-781) of n C3-clustered
+    synthetic bitmaps, device-resident: the size-ordered queue runs on the device, N - 1 step
+    launches.  Latency-bound (a chain of dependent loads per key and a serial plan
+    per step), so it reports time per queue step, not a roofline."""
+    b = eng.synth(2, 0xC3000000, n)
+    try:
+        eng.wide("priorityqueue_or", b)
+        eng.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.wide("priorityqueue_or", b)
+            eng.sync()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        rs = eng.result_stats()
+        eng.wide("or", b)
+        eng.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.wide("or", b)
+            eng.sync()
+        naive_ms = (time.perf_counter() - t0) / steps * 1e3
+    finally:
+        eng.release(b)
+    return {"workload": f"FastAggregation.priorityqueue_or of {n} C3-clustered synthetic bitmaps (one GPU)",
+            "ms_per_op": round(ms, 3), "queue_steps": n - 1, "us_per_step": round(ms * 1e3 / max(n - 1, 1), 2),
+            "result_containers": rs["containers"], "naive_or_ms_same_input": round(naive_ms, 4)}
+
+
 def run_optimize_c2(eng, a, sa, steps):
     """RoaringBitmap.runOptimize of one C2 operand on the device (plan, scan, write into a new
     batch); wall time per call, new-batch allocation and the host read-back of the totals included."""
@@ -765,6 +794,7 @@ def main():
         run_extra("decode_c2", lambda: decode_c2(eng, a, ks))
         if rank == 0:
             run_extra("c2_and_oneshot", lambda: c2_oneshot(eng, a, b, max(3, ks // 2)))
+            run_extra("pq_or_clustered_1000", lambda: pq_or_clustered(eng, 1000, 2))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
