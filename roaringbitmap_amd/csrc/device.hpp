@@ -342,6 +342,35 @@ __device__ __forceinline__ void lds_scatter_array(uint32_t* lds, const uint16_t*
   }
 }
 
+// The same walk, returning how many of this thread's values hit a set bit (XOR: bits
+// turned off) / a clear bit (OR: bits newly set).  An array's values are distinct, so
+// the counts over the workgroup are exact: the set's new cardinality follows from the
+// old one by arithmetic (XOR: card + n - 2 * off; OR: card + new), with no pass over the
+// 8 KiB.
+template <int MODE>  // 0: or (counts new bits), 1: xor (counts bits turned off)
+__device__ __forceinline__ int lds_apply_array_count(uint32_t* lds, const uint16_t* vals, int card) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(vals);
+  const int lo = (int)((a & 15) >> 1);
+  const int nvec = (lo + card + 7) >> 3;
+  const uint4* v4 = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+  int cnt = 0;
+  for (int i = threadIdx.x; i < nvec; i += NT) {
+    const uint4 v = v4[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    const int base = i * 8 - lo;
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if ((unsigned)(base + j) < (unsigned)card) {
+        const uint32_t x = (w[j >> 1] >> ((j & 1) * 16)) & 0xFFFF;
+        const uint32_t m = 1u << (x & 31);
+        const uint32_t old = MODE == 0 ? atomicOr(&lds[x >> 5], m) : atomicXor(&lds[x >> 5], m);
+        cnt += MODE == 0 ? ((old & m) == 0) : ((old & m) != 0);
+      }
+    }
+  }
+  return cnt;
+}
+
 // OR one run [s, e] (inclusive) into LDS words, single thread.
 __device__ __forceinline__ void lds_or_run_serial(uint32_t* lds, int s, int e) {
   const int ws = s >> 5, we = e >> 5;

@@ -307,18 +307,56 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
       } else {
         int st = d0.kind, cur = (int)d0.card;
         bool bulk = (A.chain & kChainLimit16) && n >= 16;  // ParallelAggregation.or :208-214
-        if (bulk) {  // a lazy bitmap from the start
+        if (!bulk) {
+          // Without run containers the chain's type is that of the final union: a bitmap
+          // operand makes the state a (lazy) bitmap, repaired to BY_CARD; arrays alone stay
+          // an array while the union plus the next array holds at most 1024 values
+          // (ArrayContainer.lazyor), so an array end state has at most 1024 values and a
+          // bitmap end state is repaired to BY_CARD -- an array again below 4097.  Either
+          // way BY_CARD of the union (RunContainer.full at 65536), whatever the order.
+          int has_r = 0;
+          for (uint32_t j = threadIdx.x; j < n; j += NT) has_r |= A.desc[s + j].kind == DK_R;
+          if (!__syncthreads_or(has_r)) bulk = true;
+        }
+        if (bulk) {  // a lazy bitmap of the whole segment
           st = DK_B;
 #pragma unroll
           for (int i = 0; i < 4; i++) r[i] = 0;
-        } else {
+          __syncthreads();
+          lds_clear(acc);
+          accumulate_segment<0>(A.desc, A.payload, s, n, acc, q, big, nbig, bslot, A.slot32 != 0, r);
+        }
+        if (!bulk) {
           materialize(d0, A.payload, tmp, q, r);
+          bool in_lds = false;  // the running union lives in acc (array steps), not in r
           for (uint32_t j = 1; j < n; j++) {
             if (st == DK_B) {
               bulk = true;
               break;
             }
             const CDesc d = A.desc[A.order ? A.order[s + j] : s + j];
+            if (st == DK_A && d.kind == DK_A) {
+              // ArrayContainer.lazyor: the values OR-ed into the LDS set, the new ones
+              // counted (cur = |union|), no materialisation or popcount pass
+              if (!in_lds) {
+                lds_barrier();
+                lds_write_owned(acc, r);
+                lds_barrier();
+                in_lds = true;
+              }
+              int fresh = lds_apply_array_count<0>(acc, reinterpret_cast<const uint16_t*>(A.payload + d.slot),
+                                                   (int)d.card);
+              int unused = 0;
+              block_sum2(fresh, unused, sh);  // its barriers order this step's atomics before the next
+              if (cur + (int)d.card > 1024) st = DK_B;
+              else cur += fresh;
+              continue;
+            }
+            if (in_lds) {
+              lds_read_owned(acc, r);
+              lds_barrier();  // acc is scratch again (count_runs)
+              in_lds = false;
+            }
             uint64_t x[4];
             materialize(d, A.payload, tmp, q, x);
 #pragma unroll
@@ -336,11 +374,15 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
               st = count_runs(r, acc, sh) > 4096 ? DK_B : DK_R;
             }
           }
-        }
-        if (bulk) {
-          __syncthreads();
-          lds_clear(acc);
-          accumulate_segment<0>(A.desc, A.payload, s, n, acc, q, big, nbig, bslot, A.slot32 != 0, r);
+          if (in_lds) {
+            lds_read_owned(acc, r);
+            lds_barrier();
+          }
+          if (bulk) {
+            __syncthreads();
+            lds_clear(acc);
+            accumulate_segment<0>(A.desc, A.payload, s, n, acc, q, big, nbig, bslot, A.slot32 != 0, r);
+          }
         }
         c = block_card(r, sh);
         if (st == DK_B) kind = c == 65536 ? DK_R : by_card(c);  // BitmapContainer.repairAfterLazy
@@ -357,11 +399,51 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         wg_passthrough(t, d0, A.payload, oc, &shp);
         continue;
       }
+      // without run containers every step is BY_CARD (A / B ixor), so the type is BY_CARD of
+      // the final set, which the chain's order does not change (as naive_xor's fast path)
+      int has_r = 0;
+      for (uint32_t j = threadIdx.x; j < n; j += NT) has_r |= A.desc[s + j].kind == DK_R;
+      if (!__syncthreads_or(has_r)) {
+        __syncthreads();
+        lds_clear(acc);
+#pragma unroll
+        for (int i = 0; i < 4; i++) r[i] = 0;
+        accumulate_segment<1>(A.desc, A.payload, s, n, acc, q, big, nbig, bslot, A.slot32 != 0, r);
+        c = block_card(r, sh);
+        if (c == 0 && !(A.chain & kChainKeepEmpty)) {
+          wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
+          continue;
+        }
+        kind = by_card(c);
+      } else {
       materialize(d0, A.payload, tmp, q, r);
       int st_kind = d0.kind, st_card = (int)d0.card;
+      bool in_lds = false;  // the running set lives in acc (array steps), not in r
       for (uint32_t j = 1; j < n; j++) {
         const int idx = (int)(A.order ? A.order[s + j] : s + j);
         const CDesc d = A.desc[idx];
+        if (d.kind == DK_A && st_kind != DK_R) {
+          // A into A / B: BY_CARD, no run count.  The values are toggled in the LDS set
+          // and the ones that were present counted: |r ^ a| = |r| + |a| - 2 |r & a|
+          if (!in_lds) {
+            lds_barrier();
+            lds_write_owned(acc, r);
+            lds_barrier();
+            in_lds = true;
+          }
+          int off = lds_apply_array_count<1>(acc, reinterpret_cast<const uint16_t*>(A.payload + d.slot), (int)d.card);
+          int unused = 0;
+          block_sum2(off, unused, sh);  // its barriers order this step's atomics before the next
+          st_card += (int)d.card - 2 * off;
+          st_kind = by_card(st_card);
+          clone = -1;
+          continue;
+        }
+        if (in_lds) {
+          lds_read_owned(acc, r);
+          lds_barrier();  // acc is scratch again (count_runs)
+          in_lds = false;
+        }
         if (st_kind == DK_R && d.kind == DK_R && d.card == 0) continue;  // x empty: this.clone()
         uint64_t x[4];
         materialize(d, A.payload, tmp, q, x);
@@ -382,6 +464,10 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         st_card = cc;
         clone = -1;
       }
+      if (in_lds) {
+        lds_read_owned(acc, r);
+        lds_barrier();
+      }
       if (st_card == 0 && !(A.chain & kChainKeepEmpty)) {
         wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
         continue;
@@ -392,6 +478,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
       }
       c = st_card;
       kind = st_kind;
+      }
     } else if (MODE == WIDE_AND_SHY || MODE == WIDE_AND_SHY_CARD) {
 #pragma unroll
       for (int i = 0; i < 4; i++) r[i] = ~0ULL;

@@ -17,7 +17,7 @@ import pytest
 
 import _gen
 import _oracle as O
-from _fmt import A, R, encode
+from _fmt import A, B, R, encode
 
 pytestmark = pytest.mark.gpu
 
@@ -71,6 +71,36 @@ def test_horizontal_equal_cardinality_ties(gpu):
         bufs.append(encode([ctr, (1, A, np.array([i], dtype=np.uint16))]))
     for op in OPS:
         assert _wide(op, bufs) == O.wide(op, bufs), op
+
+
+def test_chains_without_runs(gpu):
+    """Keys without run containers take the order-free path of the chain modes (the type is
+    BY_CARD of the union / symmetric difference, RunContainer.full at 65536).  Key 0: arrays
+    whose cardinalities sum past 1024 over a union of at most 1024 values (ArrayContainer.
+    lazyor's 1024 threshold may or may not fire, the repaired type is the same); key 1: arrays
+    whose union passes 4096; key 2: arrays and a bitmap that fill the key; key 3: pairs of
+    identical arrays (XOR chains end empty: dropped by ParallelAggregation.xor, kept by
+    horizontal_xor); key 4: one bitmap among arrays."""
+    rng = np.random.default_rng(77)
+    pool = np.sort(rng.choice(65536, 900, replace=False)).astype(np.uint16)
+    odd = np.arange(1, 65536, 2, dtype=np.uint16)  # 8 arrays of 4,096 cover them
+    for n in (2, 3, 6, 17):
+        bufs = []
+        for i in range(n):
+            ctrs = [(0, A, np.sort(rng.choice(pool, 400, replace=False)).astype(np.uint16)),
+                    (1, A, np.sort(rng.choice(65536, 3000, replace=False)).astype(np.uint16))]
+            if i == 0:
+                ctrs.append((2, B, np.arange(0, 65536, 2, dtype=np.uint16)))  # the even values
+            else:
+                ctrs.append((2, A, odd[4096 * ((i - 1) % 8):4096 * ((i - 1) % 8 + 1)]))
+            ctrs.append((3, A, np.arange(100 + (i // 2) * 10, 110 + (i // 2) * 10, dtype=np.uint16)))
+            if i == n // 2:
+                ctrs.append((4, B, np.sort(rng.choice(65536, 5000, replace=False)).astype(np.uint16)))
+            else:
+                ctrs.append((4, A, np.sort(rng.choice(65536, 50, replace=False)).astype(np.uint16)))
+            bufs.append(encode(ctrs))
+        for op in OPS:
+            assert _wide(op, bufs) == O.wide(op, bufs), (op, n)
 
 
 def test_aggregations_c3_slices(gpu):
