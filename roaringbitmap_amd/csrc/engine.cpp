@@ -141,6 +141,7 @@ struct Batch {
   // host copy of the container table for fetches (batches are immutable once loaded):
   // h_desc in container order, h_pos[h_pos_off[i] .. h_pos_off[i+1]) = bitmap i's containers
   bool h_index = false;
+  bool h_chain_identity = false;  // horizontal_order found the batch order to be the chain order
   std::vector<CDesc> h_desc;
   std::vector<uint32_t> h_pos, h_pos_off;
 };
@@ -863,9 +864,53 @@ struct JHeap {  // java.util.PriorityQueue siftUp / siftDown (OpenJDK)
 };
 }  // namespace
 
-static int horizontal_order(Ctx* c, Batch* B) {
+// *identity: the chain order is the batch's own (no key needed sorting): no order table
+static int horizontal_order(Ctx* c, Batch* B, bool* identity) {
+  *identity = B->h_chain_identity;
+  if (*identity) return RBG_OK;
   CHK(batch_host_index(c, B));
   std::vector<uint32_t> order;
+  // Within a key the heap pops by larger cardinality first; only equal cardinalities pop in
+  // the heap's tie order, which depends on everything polled before.  The chain's order
+  // matters only at keys holding a run container (the wide kernel types run-free keys from
+  // the result alone, wide.hip), so unless such a key has two containers of equal
+  // cardinality the order is the per-key sort by cardinality and the replay is skipped.
+  if (B->key_major || B->n_bm == 1) {
+    const std::vector<CDesc>& D = B->h_desc;
+    const size_t n = B->n_ctr;
+    std::vector<std::pair<uint32_t, uint32_t>> rkeys;  // segments of keys holding a run container
+    std::vector<uint32_t> seg;
+    bool tie = false;
+    for (size_t p = 0; p < n && !tie;) {
+      size_t e = p;
+      bool has_r = false;
+      while (e < n && D[e].key == D[p].key) has_r |= D[e++].kind == DK_R;
+      if (has_r && e - p > 1) {
+        seg.resize(e - p);
+        for (size_t q = p; q < e; q++) seg[q - p] = D[q].card;
+        std::sort(seg.begin(), seg.end());
+        tie = std::adjacent_find(seg.begin(), seg.end()) != seg.end();
+        rkeys.emplace_back((uint32_t)p, (uint32_t)e);
+      }
+      p = e;
+    }
+    if (!tie && rkeys.empty()) {
+      *identity = B->h_chain_identity = true;
+      return RBG_OK;
+    }
+    if (!tie) {
+      order.resize(n);
+      for (size_t q = 0; q < n; q++) order[q] = (uint32_t)q;
+      for (const auto& pe : rkeys)
+        std::sort(order.begin() + pe.first, order.begin() + pe.second,
+                  [&](uint32_t x, uint32_t y) { return D[x].card > D[y].card; });
+      CHK(c->order.ensure(4 * std::max<size_t>(n, 1)));
+      if (n) HIPCHK(hipMemcpyAsync(c->order.p, order.data(), 4 * n, hipMemcpyHostToDevice, c->stream));
+      HIPCHK(hipStreamSynchronize(c->stream));  // `order` is a stack vector
+      return RBG_OK;
+    }
+    order.clear();
+  }
   order.reserve(B->n_ctr);
   auto ptr = [&](uint32_t bm, uint32_t i) {
     const uint32_t pos = B->h_pos[B->h_pos_off[bm] + i];
@@ -1183,8 +1228,9 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
       case RBG_WIDE_HORIZONTAL_XOR:
         mode = op == RBG_WIDE_HORIZONTAL_OR ? WIDE_LAZY_CHAIN : WIDE_XOR_CHAIN;
         chain = op == RBG_WIDE_HORIZONTAL_OR ? kChainN1Clone : kChainKeepEmpty;
-        CHK(horizontal_order(c, B));
-        order = c->order.as<uint32_t>();
+        bool identity;
+        CHK(horizontal_order(c, B, &identity));
+        order = identity ? nullptr : c->order.as<uint32_t>();
         break;
       default: return RBG_ERR_ILLEGAL_ARGUMENT;
     }
