@@ -345,13 +345,17 @@ def c2_oneshot(eng, a, b, steps):
             "pcie_inclusive_input_GBps": round((len(xa) + len(xb)) / per_call / 1e9, 2)}
 
 
-def pq_or_clustered(eng, n, steps):
-    """FastAggregation.priorityqueue_or (RB/FastAggregation.java:737-781) of n C3-clustered
-    synthetic bitmaps, device-resident: the size-ordered queue runs on the device, N - 1 step
-    launches.  Latency-bound (a chain of dependent loads per key and a serial plan
-    per step), so it reports time per queue step, not a roofline."""
-    b = eng.synth(2, 0xC3000000, n)
+def pq_or_queue(eng, rows, steps):
+    """FastAggregation.priorityqueue_or (RB/FastAggregation.java:737-781) over the 32 bitmaps of a
+    synthetic bit-sliced index of `rows` rows (C5's generator: ebM as full run containers, 31
+    slices of bitmaps), device-resident: the size-ordered queue runs on the device, one launch per
+    queue step (a batch without run containers skips the queue -- its bytes are
+    naive_or's -- so this input keeps the runs).  Latency-bound (a chain of dependent loads per
+    key and a serial plan per step): time per queue step, no roofline."""
+    b = eng.synth(4, 0xC5000000, rows)
     try:
+        st = eng.batch_stats(b)
+        n = st["bitmaps"]
         eng.wide("priorityqueue_or", b)
         eng.sync()
         t0 = time.perf_counter()
@@ -369,7 +373,8 @@ def pq_or_clustered(eng, n, steps):
         naive_ms = (time.perf_counter() - t0) / steps * 1e3
     finally:
         eng.release(b)
-    return {"workload": f"FastAggregation.priorityqueue_or of {n} C3-clustered synthetic bitmaps (one GPU)",
+    return {"workload": f"FastAggregation.priorityqueue_or of the {n} bitmaps of a {rows}-row synthetic BSI "
+                        f"({st['containers']} containers, {st['run']} runs; one GPU)",
             "ms_per_op": round(ms, 3), "queue_steps": n - 1, "us_per_step": round(ms * 1e3 / max(n - 1, 1), 2),
             "result_containers": rs["containers"], "naive_or_ms_same_input": round(naive_ms, 4)}
 
@@ -794,7 +799,7 @@ def main():
         run_extra("decode_c2", lambda: decode_c2(eng, a, ks))
         if rank == 0:
             run_extra("c2_and_oneshot", lambda: c2_oneshot(eng, a, b, max(3, ks // 2)))
-            run_extra("pq_or_clustered_1000", lambda: pq_or_clustered(eng, 1000, 2))
+            run_extra("pq_or_bsi_slices", lambda: pq_or_queue(eng, 10 ** 8, 3))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

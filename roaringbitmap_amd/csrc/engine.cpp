@@ -1162,7 +1162,16 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
   key_lo = std::max(0, key_lo);
   key_hi = std::min(kMaxKeys, key_hi);
   *host_card_valid = false;
-  if (!card_only && (op == RBG_WIDE_PQ_OR || op == RBG_WIDE_PQ_XOR)) return ctx_pq(c, op, B, id, key_lo, key_hi);
+  if (!card_only && (op == RBG_WIDE_PQ_OR || op == RBG_WIDE_PQ_XOR)) {
+    // Without run containers the queue's order cannot show in the bytes: every container of
+    // its algebra ends BY_CARD of its set (pq.hip: lazy bitmaps are repaired to BY_CARD or
+    // RunContainer.full; an exact bitmap only comes from an input bitmap, over 4096 values;
+    // an array from ArrayContainer.lazyor holds at most 1024; the pairwise XOR types are
+    // BY_CARD), and a key held by one input is that input's container, as in naive_or /
+    // naive_xor, which then give the same bytes.
+    if (B->n_kind[DK_R] != 0 || key_lo != 0 || key_hi != kMaxKeys) return ctx_pq(c, op, B, id, key_lo, key_hi);
+    op = op == RBG_WIDE_PQ_OR ? RBG_WIDE_OR : RBG_WIDE_XOR;
+  }
   hipStream_t s = c->stream;
   const size_t N = B->n_bm;
   int mode = WIDE_OR, plan_mode = 0;

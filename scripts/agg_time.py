@@ -1,6 +1,7 @@
 """Time every wide aggregation form on one synthetic C3-shaped batch (device-resident, synchronised).
 
-usage: python scripts/agg_time.py KIND N [REPS]   (KIND 1 uniform, 2 clustered)
+usage: python scripts/agg_time.py KIND N [REPS [SKIP_OPS [ro]]]   (KIND 1 uniform, 2 clustered;
+       ro: runOptimize the batch first)
 """
 import json
 import os
@@ -18,13 +19,18 @@ from roaringbitmap_amd.engine import Engine  # noqa: E402
 def main():
     kind, n = int(sys.argv[1]), int(sys.argv[2])
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
-    skip = set(sys.argv[4].split(",")) if len(sys.argv) > 4 else set()
+    skip = set(sys.argv[4].split(",")) if len(sys.argv) > 4 and sys.argv[4] else set()
+    ro = len(sys.argv) > 5 and sys.argv[5] == "ro"
     torch.cuda.init()
     eng = Engine(0)
     b = eng.synth(kind, 0xC3000000, n)
+    if ro:
+        b0 = b
+        b, _ = eng.run_optimize(b0)
+        eng.release(b0)
     st = eng.batch_stats(b)
-    print(json.dumps({"kind": kind, "n": n, "containers": st["containers"], "payload_bytes": st["payload_bytes"]}),
-          flush=True)
+    print(json.dumps({"kind": kind, "n": n, "run_optimized": ro, "containers": st["containers"], "runs": st["run"],
+                      "bitmaps": st["bitmap"], "payload_bytes": st["payload_bytes"]}), flush=True)
     for op in _lib.WIDE_OP:
         if op in skip:
             continue
