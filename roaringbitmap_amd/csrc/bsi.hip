@@ -269,6 +269,7 @@ __global__ __launch_bounds__(256) void k_bsi(const Task* __restrict__ tasks, con
 // A key whose replay needs a run count (EFF) is redone by k_bsi_defer with the
 // streamed form; array / run results are staged there from the bits.
 constexpr int kBsiRegSlices = 32;
+constexpr int kBsiCut = 10;  // compare without sum: slices [0, kBsiCut) wait for EQ to survive the rest
 constexpr int kBsiUnits = 4;                // units per key
 constexpr int kUnitWords = 1024 / kBsiUnits;  // container words per unit = threads per workgroup
 static_assert(kUnitWords == NT, "a unit is one 256-thread workgroup");
@@ -525,6 +526,10 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
   // the sum shares), so they are in flight during this unit's result store and count
   // rows.
   uint64_t sl[kBsiRegSlices];
+  // Without sum shares the slices below kBsiCut are requested only once EQ survives the ones
+  // above (see the circuit): xlo = the lowest slice requested up front.
+  const bool split = !want_sum && nb > kBsiCut;
+  const int xlo = split ? kBsiCut : 0;
   auto request_slices = [&](const BsiIn& r, uint64_t unit) -> uint64_t {
     const int wq = (int)((unit % kBsiUnits) * kUnitWords) + tid;
     const uint32_t lo = (uint32_t)r.slot, hi = (uint32_t)(r.slot >> 32);
@@ -535,7 +540,9 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
       const uint64_t slot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, 1 + x) |
                             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 1 + x) << 32);
       // nontemporal: every index word is read once (C5 step -1.8 %, alternating runs on one box)
-      sl[x] = ((m >> x) & 1) ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(A.payload + slot) + wq) : 0;
+      sl[x] = ((m >> x) & 1) && x >= xlo
+                  ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(A.payload + slot) + wq)
+                  : 0;
     }
     return m;
   };
@@ -569,6 +576,21 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
     int live = 32 - nb;  // steps i >= nb are skipped
 #pragma unroll
     for (int i = kBsiRegSlices - 1; i >= 0; i--) {
+      if (i == kBsiCut - 1 && split) {
+        // Where EQ is empty every remaining step counts 0 and changes no bit, so the low
+        // slices matter only if EQ survived the high ones somewhere in the unit.  (The
+        // reference's and(EQ, bA[i]) skips a key whose EQ holds no container, so it does
+        // not read the slice there either.)
+        if (__syncthreads_or((two ? (eq0 | eq1) : eq0) != 0)) {
+#pragma unroll
+          for (int x = 0; x < kBsiCut; x++) {
+            const uint64_t slot = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, 1 + x) |
+                                  ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 1 + x) << 32);
+            if ((bmask >> x) & 1)
+              sl[x] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(A.payload + slot) + w);
+          }
+        }
+      }
       asm volatile("" : "+s"(p0), "+s"(p1), "+s"(live));
       if (live <= 0) {
         // bit i of the predicate (the top bit of the opaque running copy) picks the

@@ -117,3 +117,10 @@ def test_c5_synthetic_bsi(gpu):
     # a compare without want_sum leaves (0, 0)
     e.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=False)
     assert e.bsi_sums() == (0, 0)
+    assert e.fetch().serialize() == exp
+    # without sum shares the low slices are read only where EQ survives the high ones: every op,
+    # with predicates whose EQ dies early, survives into the low slices, or matches exactly
+    for op in _bsi.OPS:
+        for a, z in ((lo, hi), (int(v[7]), int(v[7]) + 3), (int(v[11]) - 1, int(v[11]))):
+            e.bsi(b, op, 31, a, z, mn, mx)
+            assert e.fetch().serialize() == o.compare(op, a, z), (op, a, z)
