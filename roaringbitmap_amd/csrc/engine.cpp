@@ -1051,23 +1051,41 @@ static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) 
   HIPCHK(hipStreamSynchronize(s));
   std::vector<uint32_t> kbase(stride, 0);
   std::vector<int32_t> ktop(stride, 0);
-  size_t n_blk = 0;
-  for (uint32_t t = 0; t < h_nt; t++) {
-    kbase[t] = (uint32_t)n_blk;
-    ktop[t] = h_tasks[t].b / 2;
-    n_blk += (size_t)ktop[t];
-  }
-  n_blk = std::max<size_t>(n_blk, 1);
   size_t free_b = 0, total_b = 0;
   pool_clear(c);  // pooled buffers would count as used
   HIPCHK(hipMemGetInfo(&free_b, &total_b));
   const size_t budget = free_b / 10 * 9;
-  if (st_bytes + n_blk * 8192 > budget) {
-    set_err("priorityqueue: " + std::to_string(n_slots) + " temps x " + std::to_string(stride) + " union keys and " +
-            std::to_string(n_blk) + " 8 KiB blocks need " + std::to_string((st_bytes + n_blk * 8192) >> 20) +
-            " MiB of temp state (more than the free device memory); use FastAggregation.or / xor");
-    return RBG_ERR_OUT_OF_MEMORY;
+  // pools of floor(n_t / 2) blocks never run out; when they do not all fit, every pool is
+  // capped at the largest size that fits (a key that needs more ends the op with
+  // RBG_ERR_OUT_OF_MEMORY, as a full arena did)
+  auto pool_blocks = [&](int32_t cap) {
+    size_t n = 0;
+    for (uint32_t t = 0; t < h_nt; t++) n += (size_t)std::min(h_tasks[t].b / 2, cap);
+    return n;
+  };
+  int32_t cap = 0;
+  for (uint32_t t = 0; t < h_nt; t++) cap = std::max(cap, h_tasks[t].b / 2);
+  if (st_bytes + pool_blocks(cap) * 8192 > budget) {
+    int32_t lo = 0, hi = cap;  // the largest cap that fits
+    while (lo < hi) {
+      const int32_t mid = lo + (hi - lo + 1) / 2;
+      if (st_bytes + pool_blocks(mid) * 8192 <= budget) lo = mid;
+      else hi = mid - 1;
+    }
+    if (lo < 1 && cap >= 1) {
+      set_err("priorityqueue: " + std::to_string(n_slots) + " temps x " + std::to_string(stride) +
+              " union keys need more than the free device memory; use FastAggregation.or / xor");
+      return RBG_ERR_OUT_OF_MEMORY;
+    }
+    cap = lo;
   }
+  size_t n_blk = 0;
+  for (uint32_t t = 0; t < h_nt; t++) {
+    kbase[t] = (uint32_t)n_blk;
+    ktop[t] = std::min(h_tasks[t].b / 2, cap);
+    n_blk += (size_t)ktop[t];
+  }
+  n_blk = std::max<size_t>(n_blk, 1);
   // host: add every input, plan the first step
   std::vector<PQEnt> heap(N);
   std::vector<int32_t> nodes(2 * N);
