@@ -600,7 +600,7 @@ def main():
     ap.add_argument("--c3-n", type=int, default=10000, help="bitmaps of the C3 wide-OR workloads (0 = skip)")
     ap.add_argument("--c4-pairs", type=int, default=1000000, help="pairs of the C4 workload per GPU (0 = skip)")
     ap.add_argument("--c5-rows", type=int, default=1000000000, help="rows of the C5 BSI workload (0 = skip)")
-    ap.add_argument("--only", default="", help="profiling: run one workload alone (c2, c2card, c3u, c3c, c4, c5)")
+    ap.add_argument("--only", default="", help="profiling: run one workload alone (c2, c2card, c3u, c3c, c3u_and, c3c_and, c4, c5, runopt)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo to rehearse "
                                                        "several ranks on one GPU)")
     args = ap.parse_args()
@@ -867,6 +867,9 @@ def _only(eng, args, rank, world, dist, cdev):
     elif w in ("c3u", "c3c"):
         res = {"only": w, **c3_wide_or(eng, 1 if w == "c3u" else 2, args.c3_n, rank, world, dist, steps,
                                        args.warmup, cdev)}
+    elif w in ("c3u_and", "c3c_and"):
+        res = {"only": w, **c3_wide_or(eng, 1 if w == "c3u_and" else 2, args.c3_n, rank, world, dist, steps,
+                                       args.warmup, cdev, op="and")}
     elif w == "c4":
         res = {"only": w, **c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, steps, args.warmup, cdev)}
     elif w == "c5":
