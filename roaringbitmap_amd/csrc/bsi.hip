@@ -269,10 +269,9 @@ __global__ __launch_bounds__(256) void k_bsi(const Task* __restrict__ tasks, con
 // A key whose replay needs a run count (EFF) is redone by k_bsi_defer with the
 // streamed form; array / run results are staged there from the bits.
 constexpr int kBsiRegSlices = 32;
-#ifndef RBG_BSI_CUT
-#define RBG_BSI_CUT 13
-#endif
-constexpr int kBsiCut = RBG_BSI_CUT;  // compare without sum: slices [0, kBsiCut) wait for EQ to survive the rest
+// compare without sum: slices [0, kBsiCut) wait for EQ to survive the rest (13 measured
+// against 10 and 15, profiles/r04/experiments/bsi_cut_variants.txt)
+constexpr int kBsiCut = 13;
 constexpr int kBsiUnits = 4;                // units per key
 constexpr int kUnitWords = 1024 / kBsiUnits;  // container words per unit = threads per workgroup
 static_assert(kUnitWords == NT, "a unit is one 256-thread workgroup");
