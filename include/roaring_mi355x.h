@@ -84,7 +84,17 @@ enum { RBG_WIDE_AND = 0, RBG_WIDE_OR = 1, RBG_WIDE_XOR = 2, RBG_WIDE_AND_ITER = 
  * N - 1 dependent whole-bitmap steps, one device pass over the union keys each (full key
  * range only: the queue order depends on every key). */
        RBG_WIDE_PARALLEL_OR = 6, RBG_WIDE_PARALLEL_XOR = 7, RBG_WIDE_BUFFER_OR_MUTABLE = 8,
-       RBG_WIDE_HORIZONTAL_OR = 9, RBG_WIDE_HORIZONTAL_XOR = 10, RBG_WIDE_PQ_OR = 11, RBG_WIDE_PQ_XOR = 12 };
+       RBG_WIDE_HORIZONTAL_OR = 9, RBG_WIDE_HORIZONTAL_XOR = 10, RBG_WIDE_PQ_OR = 11, RBG_WIDE_PQ_XOR = 12,
+/* BufferFastAggregation's and chains, RB/buffer/BufferFastAggregation.java.  They chain the buffer
+ * package's in-place MutableRoaringBitmap.and (RB/buffer/MutableRoaringBitmap.java:886-910), whose
+ * run AND run keeps the merged run container (MappeableRunContainer.iand(R) = and(R), :1106-1108,
+ * :474-536) where the heap's converts it (RunContainer.and(R) ends in toEfficientContainer):
+ *   RBG_WIDE_BUFFER_AND         and(ImmutableRoaringBitmap...) / and(long[], ...) :28-56 (N>10 workShyAnd)
+ *   RBG_WIDE_BUFFER_NAIVE_AND   naive_and(ImmutableRoaringBitmap...) :347-369 (smallest first)
+ *   RBG_WIDE_BUFFER_AND_ITER    naive_and(Iterator) :383-396, naive_and(MutableRoaringBitmap...) :407-416
+ * A result container of more than 2047 runs is kept as such; these calls synchronise the stream
+ * (the run arena is checked after the op). */
+       RBG_WIDE_BUFFER_AND = 13, RBG_WIDE_BUFFER_NAIVE_AND = 14, RBG_WIDE_BUFFER_AND_ITER = 15 };
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
 
@@ -158,6 +168,12 @@ int rbg_set_devices(uint64_t mask);
 /* Human-readable message for the last error on this thread. */
 const char* rbg_last_error(void);
 int rbg_version(void);
+/* Result buffers of 8 MiB and more are kept for reuse after rbg_free (at most two, 1 GiB in all, so a
+ * repeated large fetch does not fault fresh pages); rbg_trim frees them. */
+void rbg_trim(void);
+/* Pooled device buffers freed to satisfy an out-of-memory allocation since the library loaded
+ * (first the calling context's pool, then the other contexts' on the device). */
+uint64_t rbg_pool_evictions(void);
 
 /* ---- host-side format utilities (construction, not the hot path) ----------------
  * RoaringBitmap.bitmapOf(int...) (RB/RoaringBitmap.java:566-570) optionally followed

@@ -1285,13 +1285,17 @@ int32_t op_andnot_card(const Bitmap& x1, const Bitmap& x2) {  // :944-985
 // ---------------------------------------------------------------------------
 // In-place bitmap ops used by the FastAggregation chains
 // ---------------------------------------------------------------------------
-static void ip_and(Bitmap& a, const Bitmap& x2) {  // RB/RoaringBitmap.java:1272-1296
+// RB/RoaringBitmap.java:1272-1296 (heap: Container.iand); the buffer package's
+// MutableRoaringBitmap.and(ImmutableRoaringBitmap) (RB/buffer/MutableRoaringBitmap.java:886-910) is the
+// same key loop over MappeableContainer.iand
+template <class F>
+static void ip_and_with(Bitmap& a, const Bitmap& x2, F iand) {
   size_t p1 = 0, p2 = 0, isz = 0;
   const size_t l1 = a.size(), l2 = x2.size();
   while (p1 < l1 && p2 < l2) {
     uint16_t s1 = a.keys[p1], s2 = x2.keys[p2];
     if (s1 == s2) {
-      Ctr c = c_iand(a.ctrs[p1], x2.ctrs[p2]);
+      Ctr c = iand(a.ctrs[p1], x2.ctrs[p2]);
       if (!c.empty()) { a.keys[isz] = s1; a.ctrs[isz] = std::move(c); isz++; }
       p1++;
       p2++;
@@ -1304,6 +1308,19 @@ static void ip_and(Bitmap& a, const Bitmap& x2) {  // RB/RoaringBitmap.java:1272
   a.keys.resize(isz);
   a.ctrs.resize(isz);
 }
+
+static void ip_and(Bitmap& a, const Bitmap& x2) { ip_and_with(a, x2, c_iand); }
+
+// MappeableContainer.iand: MappeableRunContainer.iand(R) = and(R) keeps the merged run container
+// (RB/buffer/MappeableRunContainer.java:1106-1108 -> :474-536, no toEfficientContainer); every other
+// pair types as the heap's c_iand (MappeableArrayContainer.iand :674-700 filters in place,
+// MappeableBitmapContainer.iand :572-677 as BitmapContainer.iand, MappeableRunContainer.iand(A|B)
+// :1095-1102 = and(A|B) :398-471 as RunContainer.and)
+static Ctr c_iand_buf(const Ctr& a, const Ctr& b) {
+  if (a.kind == RUN && b.kind == RUN) return R_and_R_runs(a, b);
+  return c_iand(a, b);
+}
+static void ip_and_buf(Bitmap& a, const Bitmap& x2) { ip_and_with(a, x2, c_iand_buf); }
 
 static void ip_xor(Bitmap& a, const Bitmap& x2) {  // RB/RoaringBitmap.java:3296-3348
   size_t p1 = 0, p2 = 0;
@@ -1384,6 +1401,38 @@ Bitmap fa_and_iter(const std::vector<const Bitmap*>& bms) {  // naive_and(Iterat
   Bitmap ans = *bms[0];
   for (size_t k = 1; k < bms.size() && !all_empty(ans); k++) ip_and(ans, *bms[k]);
   return ans;
+}
+
+// BufferFastAggregation.naive_and(ImmutableRoaringBitmap...) (RB/buffer/BufferFastAggregation.java:347-369):
+// smallest.toMutableRoaringBitmap(), then answer.and(bitmap) for every bitmap != smallest, with no
+// early exit on an empty answer (an empty answer stays empty: same bytes)
+Bitmap buf_naive_and(const std::vector<const Bitmap*>& bms, const int* ids) {
+  if (bms.empty()) return Bitmap();
+  size_t smallest = 0;
+  for (size_t i = 1; i < bms.size(); i++)
+    if (bms[i]->size() < bms[smallest]->size()) smallest = i;
+  Bitmap ans = *bms[smallest];
+  for (size_t k = 0; k < bms.size(); k++) {
+    bool same = ids ? (ids[k] == ids[smallest]) : (k == smallest);
+    if (!same) ip_and_buf(ans, *bms[k]);
+  }
+  return ans;
+}
+
+// naive_and(Iterator) :383-396 (first.toMutableRoaringBitmap()) and naive_and(MutableRoaringBitmap...)
+// :407-416 (bitmaps[0].clone()): the buffer in-place and chain from the first input
+Bitmap buf_and_iter(const std::vector<const Bitmap*>& bms) {
+  if (bms.empty()) return Bitmap();
+  Bitmap ans = *bms[0];
+  for (size_t k = 1; k < bms.size(); k++) ip_and_buf(ans, *bms[k]);
+  return ans;
+}
+
+// and(ImmutableRoaringBitmap...) / and(long[], ImmutableRoaringBitmap...) :28-56: workShyAnd above
+// 10 inputs (buffer workShyAnd :426-494 types as the heap's), else the buffer naive_and
+Bitmap buf_and(const std::vector<const Bitmap*>& bms, const int* ids) {
+  if (bms.size() > 10) return fa_workshy_and(bms);
+  return buf_naive_and(bms, ids);
 }
 
 // key-bitset intersection shared by workShyAnd / workShyAndCardinality

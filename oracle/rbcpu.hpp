@@ -129,6 +129,11 @@ Bitmap pa_xor(const std::vector<const Bitmap*>& bms);                // Parallel
 Ctr pa_or_key(const std::vector<const Ctr*>& cs);                    // :197-223
 Ctr pa_xor_key(const std::vector<const Ctr*>& cs);                   // :189-195
 Bitmap buf_or_mutable(const std::vector<const Bitmap*>& bms);        // BufferFastAggregation.naive_or(Mutable...)
+// BufferFastAggregation's and chains (RB/buffer/BufferFastAggregation.java:28-56,347-416): the in-place
+// MutableRoaringBitmap.and, whose run AND run keeps the merged run container
+Bitmap buf_and(const std::vector<const Bitmap*>& bms, const int* ids);        // and(Immutable...) :28-56
+Bitmap buf_naive_and(const std::vector<const Bitmap*>& bms, const int* ids);  // naive_and(Immutable...) :347-369
+Bitmap buf_and_iter(const std::vector<const Bitmap*>& bms);  // naive_and(Iterator) :383-396, (Mutable...) :407-416
 Bitmap fa_horizontal_or(const std::vector<const Bitmap*>& bms);      // FastAggregation.horizontal_or :124-231
 Bitmap fa_horizontal_xor(const std::vector<const Bitmap*>& bms);     // :243-289
 Bitmap fa_priorityqueue_or(const std::vector<const Bitmap*>& bms);   // :733-781

@@ -87,7 +87,8 @@ int rbo_pairwise_card(int op, const uint8_t* a, size_t an, const uint8_t* b, siz
 // op: 0 FastAggregation.and(varargs), 1 or, 2 xor, 3 and(Iterator), 4 naive_and, 5 workShyAnd,
 //     6 ParallelAggregation.or, 7 ParallelAggregation.xor, 8 BufferFastAggregation.or(Mutable...),
 //     9 FastAggregation.horizontal_or(varargs/List), 10 horizontal_xor, 11 priorityqueue_or,
-//     12 priorityqueue_xor
+//     12 priorityqueue_xor, 13 BufferFastAggregation.and(Immutable...), 14 BufferFastAggregation.naive_and
+//     (Immutable...), 15 BufferFastAggregation.naive_and(Iterator / Mutable...)
 int rbo_wide(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, const int* ids,
              uint8_t** out, size_t* out_len) {
   std::vector<Bitmap> bms;
@@ -108,6 +109,9 @@ int rbo_wide(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, c
     case 10: return emit(fa_horizontal_xor(ptrs), out, out_len);
     case 11: return emit(fa_priorityqueue_or(ptrs), out, out_len);
     case 12: return emit(fa_priorityqueue_xor(ptrs), out, out_len);
+    case 13: return emit(buf_and(ptrs, ids), out, out_len);
+    case 14: return emit(buf_naive_and(ptrs, ids), out, out_len);
+    case 15: return emit(buf_and_iter(ptrs), out, out_len);
   }
   return ERR_ARG;
 }

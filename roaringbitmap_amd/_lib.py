@@ -21,7 +21,8 @@ OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "ior": 4}  # ior: x1.or(x2) in p
 CARD_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
 WIDE_OP = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5, "parallel_or": 6,
            "parallel_xor": 7, "buffer_or_mutable": 8, "horizontal_or": 9, "horizontal_xor": 10,
-           "priorityqueue_or": 11, "priorityqueue_xor": 12}
+           "priorityqueue_or": 11, "priorityqueue_xor": 12, "buffer_and": 13, "buffer_naive_and": 14,
+           "buffer_and_iter": 15}
 WIDE_CARD_OP = {"and": 0, "or": 1}
 
 
@@ -31,7 +32,7 @@ class rbg_buffer(ctypes.Structure):
 
 EXPORTED = [
     "rbg_pairwise", "rbg_pairwise_card", "rbg_wide", "rbg_wide_card", "rbg_batch_and_card", "rbg_free",
-    "rbg_set_devices", "rbg_last_error", "rbg_version", "rbg_from_values", "rbg_run_optimize",
+    "rbg_set_devices", "rbg_last_error", "rbg_version", "rbg_trim", "rbg_pool_evictions", "rbg_from_values", "rbg_run_optimize",
     "rbg_to_values", "rbg_inspect", "rbg_ctx_create", "rbg_ctx_destroy", "rbg_ctx_stream", "rbg_ctx_sync",
     "rbg_ctx_load", "rbg_ctx_synth", "rbg_ctx_release", "rbg_ctx_batch_stats", "rbg_ctx_batch_fetch",
     "rbg_ctx_pairwise", "rbg_ctx_pairwise_range", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
@@ -56,6 +57,10 @@ def _declare(L):
     i32 = ctypes.c_int32
     vp = ctypes.c_void_p
     L.rbg_pairwise.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, buf]
+    L.rbg_trim.argtypes = []
+    L.rbg_trim.restype = None
+    L.rbg_pool_evictions.argtypes = []
+    L.rbg_pool_evictions.restype = ctypes.c_uint64
     L.rbg_pairwise_card.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, P(i32)]
     L.rbg_pairwise_inplace.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, ctypes.c_int, buf]
     L.rbg_wide.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), P(i32), sz, buf]

@@ -80,12 +80,13 @@ class RoaringBitmapSliceIndex:
         self.minValue = min(self.minValue, otherBsi.minValue)
 
     def getValue(self, columnId):
-        """BSI/ getValue(columnId) -> (value, exists), read from the serialized bitmaps on the host"""
-        if int(columnId) not in set(self.ebM.toArray().tolist()):
+        """BSI/:181-196 getValue(columnId) -> (value, exists): ebM.contains, then one contains per slice
+        (RoaringBitmap.contains on the serialized bitmaps, on the host)"""
+        if not self.ebM.contains(columnId):
             return 0, False
         v = 0
         for i, b in enumerate(self.bA):
-            if int(columnId) in set(b.toArray().tolist()):
+            if b.contains(columnId):
                 v |= 1 << i
         return v, True
 

@@ -1000,51 +1000,6 @@ __device__ __forceinline__ void owen_input(int j, const WideArgs& A, const BsiAr
   x.src = -1;
 }
 
-// A run container of more than 2047 runs (only the buffer package's raw run AND / ANDNOT make
-// them) into the big-run arena: [u16 nruns][(start, length - 1) pairs], written from the bits.
-__device__ __forceinline__ void place_big_runs(uint32_t t, uint32_t key, const VB& res, int nr, const OutCtx& oc,
-                                               const BigRuns& big, uint32_t* lds, int* sh,
-                                               unsigned long long* sh64) {
-  const uint32_t len = 2u + 4u * (uint32_t)nr;
-  if (threadIdx.x == 0) {
-    unsigned long long off = atomicAdd(&big.used[0], (unsigned long long)((len + 15u) & ~15u));
-    if (off + len > big.cap) {
-      atomicOr(&big.used[1], 1ull);  // the host reruns the op with a larger arena
-      off = ~0ull;
-    }
-    *sh64 = off;
-  }
-  __syncthreads();
-  const unsigned long long off = *sh64;
-  __syncthreads();
-  if (off == ~0ull) {
-    wg_place(t, false, nullptr, true, nullptr, 0, 0, key, DK_A, oc, nullptr);
-    return;
-  }
-  uint16_t* dst = reinterpret_cast<uint16_t*>(big.base + off);
-  uint64_t s[4], e[4];
-  run_edges(res.r, lds, s, e);
-  int ps0, ps1, ns, pe0, pe1, ne;
-  block_scan_halves(popc64(s[0]) + popc64(s[1]), popc64(s[2]) + popc64(s[3]), ps0, ps1, ns, sh);
-  block_scan_halves(popc64(e[0]) + popc64(e[1]), popc64(e[2]) + popc64(e[3]), pe0, pe1, ne, sh);
-  const int th = threadIdx.x;
-  const int bases[4] = {(2 * th) * 64, (2 * th + 1) * 64, (512 + 2 * th) * 64, (513 + 2 * th) * 64};
-  const int sp[4] = {ps0, ps0 + popc64(s[0]), ps1, ps1 + popc64(s[2])};
-  const int ep[4] = {pe0, pe0 + popc64(e[0]), pe1, pe1 + popc64(e[2])};
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    uint64_t x = s[k];
-    for (int p = sp[k]; x; p++, x &= x - 1) dst[1 + 2 * p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
-    x = e[k];
-    for (int p = ep[k]; x; p++, x &= x - 1) dst[2 + 2 * p] = (uint16_t)(bases[k] + __builtin_ctzll(x));
-  }
-  if (th == 0) dst[0] = (uint16_t)nr;
-  __syncthreads();
-  for (int p = th; p < nr; p += NT) dst[2 + 2 * p] = (uint16_t)(dst[2 + 2 * p] - dst[1 + 2 * p]);  // end -> length - 1
-  __syncthreads();
-  wg_place(t, true, big.base + off, false, nullptr, len, (uint32_t)res.card, key, DK_R, oc, nullptr);
-}
-
 __device__ __forceinline__ void place_buf(uint32_t t, uint32_t key, const VB& res, const WideArgs& A, const OutCtx& oc,
                                           const BigRuns& big, uint32_t* acc, uint32_t* tmp, int* sh,
                                           unsigned long long* sh64) {
@@ -1059,7 +1014,7 @@ __device__ __forceinline__ void place_buf(uint32_t t, uint32_t key, const VB& re
   if (res.kind == DK_R) {
     const int nr = count_runs(res.r, acc, sh);
     if (nr > 2047) {
-      place_big_runs(t, key, res, nr, oc, big, acc, sh, sh64);
+      place_big_runs(t, key, res.r, res.card, nr, oc, big, acc, sh, sh64);
       return;
     }
   }

@@ -11,6 +11,12 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+// The RBG_EXP_* variants make one access lane-linear to attribute LDS conflicts in counter runs; they
+// compute wrong results, so only a profiling build (scripts/build_variant.sh) may set them.
+#if (defined(RBG_EXP_PROBE_LIN) || defined(RBG_EXP_SCAT_LIN)) && !defined(RBG_PROFILING_BUILD)
+#error "RBG_EXP_* give wrong results: counter-attribution builds only (scripts/build_variant.sh)"
+#endif
+
 namespace rbg {
 
 constexpr int NT = 256;
@@ -116,6 +122,15 @@ struct OutCtx {
   int64_t* layout_out;
 };
 
+// Run containers of more than 2047 runs (8 KiB of runs) do not fit a result slot.  Only the buffer
+// package's run AND / ANDNOT run make them (no toEfficientContainer); such a result is written to
+// this arena (bump allocation; `overflow` set when `cap` is exceeded, `used` then tells the size
+// the op needs, and the host reruns it with a larger arena).
+struct BigRuns {
+  uint8_t* base;
+  unsigned long long* used;  // used[0] bytes reserved, used[1] overflow flag
+  uint64_t cap;
+};
 // Portable-format header bytes for `size` containers (RB/RoaringArray.java:781-790)
 __host__ __device__ inline uint64_t header_bytes(uint32_t size, uint32_t has_run) {
   if (has_run) return (size < 4) ? 4 + (size + 7) / 8 + 4ull * size : 4 + (size + 7) / 8 + 8ull * size;

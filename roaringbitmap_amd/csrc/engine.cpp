@@ -68,9 +68,11 @@ static void dbg(hipStream_t s, const char* what) {
   std::fflush(stderr);
 }  // look-back state: ticket @0, error word @64, statuses @256
 
-// On an out-of-memory hipMalloc, the device buffers every context keeps for reuse (Ctx::pool) are
-// freed and the allocation is retried once (defined after Ctx).
-static size_t release_pools_on(int device);
+// On an out-of-memory hipMalloc, the device buffers kept for reuse (Ctx::pool) are freed and the
+// allocation retried: first the pool of the context the calling thread works on, then, if that was
+// not enough, those of every other context on the device (defined after Ctx).  Every pooled buffer
+// freed this way is counted (rbg_pool_evictions), so memory pressure shows.
+static size_t release_pools_on(int device, int stage);
 
 struct DevBuf {
   void* p = nullptr;
@@ -104,7 +106,13 @@ struct DevBuf {
     if (e == hipErrorOutOfMemory) {
       int dev = 0;
       (void)hipGetLastError();
-      if (hipGetDevice(&dev) == hipSuccess && release_pools_on(dev) > 0) e = hipMalloc(&p, bytes + kSlack);
+      for (int stage = 0; stage < 2 && e == hipErrorOutOfMemory; stage++) {
+        if (hipGetDevice(&dev) != hipSuccess) break;
+        if (release_pools_on(dev, stage) > 0) {
+          e = hipMalloc(&p, bytes + kSlack);
+          if (e == hipErrorOutOfMemory) (void)hipGetLastError();
+        }
+      }
     }
     if (e != hipSuccess) {
       p = nullptr;
@@ -230,12 +238,29 @@ static size_t pool_clear(Ctx* c) {
   return n;
 }
 
-static size_t release_pools_on(int device) {
+// the context the calling thread works on (set by tl_ctx / enter), for release_pools_on's first stage
+static thread_local Ctx* t_cur_ctx = nullptr;
+static std::atomic<uint64_t> g_pool_evictions{0};
+
+static size_t release_pools_on(int device, int stage) {
   std::lock_guard<std::mutex> g(g_ctx_mu);
   size_t n = 0;
-  for (Ctx* c : g_ctxs)
-    if (c->device == device) n += pool_clear(c);
+  const bool own = t_cur_ctx && std::find(g_ctxs.begin(), g_ctxs.end(), t_cur_ctx) != g_ctxs.end();
+  if (stage == 0) {
+    if (own && t_cur_ctx->device == device) n = pool_clear(t_cur_ctx);
+  } else {
+    for (Ctx* c : g_ctxs)
+      if (c->device == device && !(own && c == t_cur_ctx)) n += pool_clear(c);
+  }
+  g_pool_evictions += n;
   return n;
+}
+
+// entry of a session call: the context's device, and the context out-of-memory retries empty first
+static int enter(Ctx* c) {
+  t_cur_ctx = c;
+  HIPCHK(hipSetDevice(c->device));
+  return RBG_OK;
 }
 
 static int ctx_init(Ctx* c, int device) {
@@ -1190,6 +1215,12 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     if (B->n_kind[DK_R] != 0 || key_lo != 0 || key_hi != kMaxKeys) return ctx_pq(c, op, B, id, key_lo, key_hi);
     op = op == RBG_WIDE_PQ_OR ? RBG_WIDE_OR : RBG_WIDE_XOR;
   }
+  // BufferFastAggregation's and chains: the heap forms' dispatch, with the buffer package's run AND run
+  bool buffer = false;
+  if (!card_only && op >= RBG_WIDE_BUFFER_AND && op <= RBG_WIDE_BUFFER_AND_ITER) {
+    buffer = true;
+    op = op == RBG_WIDE_BUFFER_AND ? RBG_WIDE_AND : op == RBG_WIDE_BUFFER_NAIVE_AND ? RBG_WIDE_NAIVE_AND : RBG_WIDE_AND_ITER;
+  }
   hipStream_t s = c->stream;
   const size_t N = B->n_bm;
   int mode = WIDE_OR, plan_mode = 0;
@@ -1266,11 +1297,18 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     // empty aggregate: empty bitmap (:329-331 for and; naive_or/xor of nothing)
     plan_mode = 2;
   }
-  {
+  // the buffer naive_and chain may keep run containers of more than 2047 runs: they go to the
+  // big-run arena, checked after the op (rerun once with the size the first pass reserved)
+  const bool big_runs = buffer && mode == WIDE_AND_NAIVE && N > 0;
+  if (big_runs) {
+    if (!c->big_ctl.p) CHK(c->big_ctl.ensure(16));
+    if (!c->big.p) CHK(c->big.ensure(16ull << 20));
+  }
+  for (int attempt = 0;; attempt++) {
     const size_t ub = std::min<size_t>(kMaxKeys, std::max<size_t>(B->n_ctr, 1));
     OutCtx oc;
     // each result container is staged (<= 8194 B) or a clone of one input container
-    CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser, &oc, card_only));
+    CHK(prepare_output(c, ub, (size_t)8194 * ub + B->max_ser + (big_runs ? c->big.cap : 0), &oc, card_only));
     // OR results are bitmaps whenever more than 4096 values survive: write those in place
     // (8192 t < 8194 ub, inside the payload region)
     if (!card_only && (mode == WIDE_OR || mode == WIDE_LAZY_CHAIN)) oc.spec = c->pending.spec = 1;
@@ -1285,7 +1323,7 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
                      c->by_key.as<Task>(), c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile);
     launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
                    c->ntasks.as<uint32_t>());
-    WideArgs wa;
+    WideArgs wa{};
     wa.desc = B->desc.as<CDesc>();
     wa.bm = B->bm.as<uint32_t>();
     wa.payload = B->payload.as<uint8_t>();
@@ -1296,6 +1334,11 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.order = order;
     wa.chain = chain;
     wa.rd_bytes = c->prof_cap > 0 && c->rd_ctr.p ? c->rd_ctr.as<unsigned long long>() : nullptr;
+    wa.buffer = buffer ? 1u : 0u;
+    if (big_runs) {
+      HIPCHK(hipMemsetAsync(c->big_ctl.p, 0, 16, s));
+      wa.big = BigRuns{c->big.as<uint8_t>(), c->big_ctl.as<unsigned long long>(), c->big.cap};
+    }
     c->mark(1);
     launch_wide(s, mode, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, oc,
                 c->task_card.as<uint32_t>());
@@ -1308,6 +1351,16 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     }
     c->mark(3);
     HIPCHK(hipGetLastError());
+    if (!big_runs) break;
+    unsigned long long used[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(used, c->big_ctl.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (!used[1]) break;
+    if (attempt) {
+      set_err("naive_and: the run-container arena overflowed twice");
+      return RBG_ERR_DEVICE;
+    }
+    CHK(c->big.ensure(used[0] + (used[0] >> 3) + 4096));  // the first pass counted every reservation
   }
   return RBG_OK;
 }
@@ -1657,7 +1710,13 @@ static int download_staged(Ctx* c, const uint8_t* dev, uint64_t bytes, uint8_t* 
 static std::mutex g_out_mu;
 static std::unordered_map<void*, size_t> g_out_live;        // large buffers handed out -> capacity
 static std::vector<std::pair<void*, size_t>> g_out_cache;   // freed ones kept for reuse
-constexpr size_t kOutLarge = 8ull << 20, kOutCacheMax = 2, kOutAlign = 2ull << 20;
+// The cache holds at most two buffers and 1 GiB; rbg_trim releases it.
+constexpr size_t kOutLarge = 8ull << 20, kOutCacheMax = 2, kOutCacheBytes = 1ull << 30, kOutAlign = 2ull << 20;
+static size_t out_cache_bytes() {
+  size_t b = 0;
+  for (const auto& e : g_out_cache) b += e.second;
+  return b;
+}
 static uint8_t* out_alloc(size_t n) {
   if (n < kOutLarge) return (uint8_t*)std::malloc(n ? n : 1);
   std::lock_guard<std::mutex> g(g_out_mu);
@@ -1722,7 +1781,7 @@ static int tl_ctx(Ctx** out) {
     tl.ctx = std::move(c);
     tl.device = dev;
   }
-  HIPCHK(hipSetDevice(tl.device));
+  CHK(enter(tl.ctx.get()));
   *out = tl.ctx.get();
   return RBG_OK;
 }
@@ -1739,6 +1798,14 @@ struct rbg_ctx {
 extern "C" {
 
 int rbg_version(void) { return 1; }
+
+void rbg_trim(void) {
+  std::lock_guard<std::mutex> g(g_out_mu);
+  for (const auto& e : g_out_cache) std::free(e.first);
+  g_out_cache.clear();
+}
+
+uint64_t rbg_pool_evictions(void) { return g_pool_evictions.load(); }
 const char* rbg_last_error(void) { return g_err.c_str(); }
 
 void rbg_free(rbg_buffer* buf) {
@@ -1749,7 +1816,7 @@ void rbg_free(rbg_buffer* buf) {
     if (it != g_out_live.end()) {  // a large result buffer: kept for reuse (the oldest kept one freed)
       g_out_cache.emplace_back(it->first, it->second);
       g_out_live.erase(it);
-      if (g_out_cache.size() > kOutCacheMax) {
+      while (g_out_cache.size() > kOutCacheMax || (!g_out_cache.empty() && out_cache_bytes() > kOutCacheBytes)) {
         std::free(g_out_cache.front().first);
         g_out_cache.erase(g_out_cache.begin());
       }
@@ -1809,13 +1876,20 @@ int rbg_pairwise_inplace(int op, const uint8_t* a, size_t a_len, const uint8_t* 
       out->len = 8;
       return RBG_OK;
     }
-    Ctx* c;
-    CHK(tl_ctx(&c));
-    BatchGuard g{c, {}};
-    int32_t ia;
-    CHK(ctx_load(c, &a, &a_len, 1, &ia));  // validated like any input, then its own bytes back
-    g.ids.push_back(ia);
-    return ctx_batch_fetch(c, ia, 0, out);
+    // x1 unchanged: validated on the host like any input, then its own bytes back (no device call)
+    HostBitmap hb;
+    std::string err;
+    const int st = parse(a, a_len, &hb, &err);
+    if (st) {
+      set_err(err);
+      return st;
+    }
+    uint8_t* p = out_alloc(hb.consumed);
+    if (!p) return RBG_ERR_OUT_OF_MEMORY;
+    std::memcpy(p, a, hb.consumed);
+    out->data = p;
+    out->len = hb.consumed;
+    return RBG_OK;
   }
   // x1.and / xor / andNot(x2) in place type like the static ops (Container.iand / ixor / iandNot
   // end in the same container types); x1.or(x2) is Container.ior's
@@ -1849,7 +1923,7 @@ int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, 
 }
 
 int rbg_wide(int op, const uint8_t* const* bufs, const size_t* lens, const int32_t* ids, size_t n, rbg_buffer* out) {
-  if (!out || op < 0 || op > RBG_WIDE_PQ_XOR) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!out || op < 0 || op > RBG_WIDE_BUFFER_AND_ITER) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
@@ -2025,7 +2099,7 @@ void rbg_ctx_destroy(rbg_ctx* ctx) {
 }
 void* rbg_ctx_stream(rbg_ctx* ctx) { return ctx ? (void*)ctx->c.stream : nullptr; }
 int rbg_ctx_profile(rbg_ctx* ctx, int max_ops) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   HIPCHK(hipStreamSynchronize(ctx->c.stream));
   ctx->c.prof_free();
   if (max_ops <= 0) return RBG_OK;
@@ -2043,7 +2117,7 @@ int rbg_ctx_profile_bytes(rbg_ctx* ctx, int64_t* bytes) {
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   Ctx& c = ctx->c;
-  HIPCHK(hipSetDevice(c.device));
+  CHK(enter(&c));
   HIPCHK(hipStreamSynchronize(c.stream));
   unsigned long long v = 0;
   if (c.rd_ctr.p) HIPCHK(hipMemcpy(&v, c.rd_ctr.p, 8, hipMemcpyDeviceToHost));
@@ -2052,7 +2126,7 @@ int rbg_ctx_profile_bytes(rbg_ctx* ctx, int64_t* bytes) {
 }
 int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops) {
   Ctx& c = ctx->c;
-  HIPCHK(hipSetDevice(c.device));
+  CHK(enter(&c));
   HIPCHK(hipStreamSynchronize(c.stream));
   ms3[0] = ms3[1] = ms3[2] = 0.0;
   for (size_t i = 0; i < c.prof_n; i++) {
@@ -2067,24 +2141,24 @@ int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops) {
   return RBG_OK;
 }
 int rbg_ctx_sync(rbg_ctx* ctx) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   HIPCHK(hipStreamSynchronize(ctx->c.stream));
   return RBG_OK;
 }
 int rbg_ctx_load_separate(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* ids) {
   if (!ctx || !ids) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_load_separate(&ctx->c, bufs, lens, n, ids);
 }
 int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* batch) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_load(&ctx->c, bufs, lens, n, batch);
 }
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch) {
   Ctx& c = ctx->c;
   Batch* b;
   CHK(get_batch(&c, batch, &b));
-  HIPCHK(hipSetDevice(c.device));
+  CHK(enter(&c));
   // A materialised result references pass-through containers inside its operand
   // batches (ORec::src) until it is serialized: serialize it before an operand goes.
   if (c.last == 1 && !c.serialized &&
@@ -2107,7 +2181,7 @@ int rbg_ctx_batch_stats(rbg_ctx* ctx, int32_t batch, int64_t* st) {
   st[6] = b->long_card;
   st[7] = b->ser_bytes;
   if (b->n_ctr) {
-    HIPCHK(hipSetDevice(ctx->c.device));
+    CHK(enter(&ctx->c));
     hipStream_t s = ctx->c.stream;
     HIPCHK(hipMemsetAsync(ctx->c.scalar.p, 0, 8, s));
     launch_batch_bytes(s, b->desc.as<CDesc>(), b->n_ctr, b->payload.as<uint8_t>(),
@@ -2123,12 +2197,12 @@ static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out);
 static int ctx_batch_fetch_range(Ctx* c, int32_t batch, size_t i0, size_t i1, rbg_buffer* outs);
 int rbg_ctx_batch_fetch(rbg_ctx* ctx, int32_t batch, size_t i, rbg_buffer* out) {
   if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_batch_fetch(&ctx->c, batch, i, out);
 }
 int rbg_ctx_batch_fetch_range(rbg_ctx* ctx, int32_t batch, size_t first, size_t count, rbg_buffer* outs) {
   if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_batch_fetch_range(&ctx->c, batch, first, first + count, outs);
 }
 }  // extern "C"
@@ -2252,16 +2326,16 @@ static int ctx_batch_fetch(Ctx* c, int32_t batch, size_t i, rbg_buffer* out) {
 
 extern "C" {
 int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_pairwise(&ctx->c, op, a, ia, b, ib, false);
 }
 int rbg_ctx_pairwise_range(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib, int key_lo, int key_hi) {
   if (!ctx || key_lo > key_hi) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_pairwise(&ctx->c, op, a, ia, b, ib, false, key_lo, key_hi);
 }
 int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   if (op != RBG_CARD_AND) {
     set_err("the session API computes andCardinality; derive the others from the input cardinalities");
     return RBG_ERR_ILLEGAL_ARGUMENT;
@@ -2269,14 +2343,14 @@ int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b,
   return ctx_pairwise(&ctx->c, OP_AND, a, ia, b, ib, true);
 }
 int rbg_ctx_wide(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, const int32_t* ids) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   int hc;
   bool hv;
   return ctx_wide(&ctx->c, op, batch, key_lo, key_hi, ids, false, &hc, &hv);
 }
 int rbg_ctx_wide_start(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi, const int32_t* ids,
                        int32_t start_bm) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   int hc;
   bool hv;
   return ctx_wide(&ctx->c, op, batch, key_lo, key_hi, ids, false, &hc, &hv, start_bm);
@@ -2303,17 +2377,17 @@ int rbg_synth_key_bytes(int kind, uint64_t seed, size_t n, uint64_t* out) {
 }
 int rbg_ctx_bsi(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
                 int32_t min_value, int32_t max_value, int want_sum) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_bsi(&ctx->c, batch, op, nbits, has_found, start, end, min_value, max_value, want_sum);
 }
 int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2) {
   if (!out2) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_bsi_sums(&ctx->c, out2);
 }
 int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2) {
   if (!ctx || !dst2 || !ctx->c.bsi_sums.p) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   launch_bsi_sums_out(ctx->c.stream, ctx->c.bsi_sums.as<unsigned long long>(), dst2);
   HIPCHK(hipGetLastError());
   return RBG_OK;
@@ -2361,7 +2435,7 @@ int rbg_bsi_compare_buffer(int op, int32_t start, int32_t end, const uint8_t* eb
 }
 int rbg_ctx_bsi_buffer(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_found, int32_t start, int32_t end,
                        int32_t min_value, int32_t max_value) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_bsi_buffer(&ctx->c, batch, op, nbits, has_found, start, end, min_value, max_value);
 }
 int rbg_bsi_sum(const uint8_t* ebm, size_t ebm_len, const uint8_t* const* slices, const size_t* slice_lens,
@@ -2393,7 +2467,7 @@ int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2) {
     set_err("needs a bitmap-major batch of pairs");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   HIPCHK(hipStreamSynchronize(ctx->c.stream));
   std::vector<CDesc> d(b->n_ctr);
   if (b->n_ctr) HIPCHK(hipMemcpy(d.data(), b->desc.p, sizeof(CDesc) * b->n_ctr, hipMemcpyDeviceToHost));
@@ -2419,7 +2493,7 @@ int rbg_ctx_pair_bytes(rbg_ctx* ctx, int32_t batch, int64_t* out2) {
   return RBG_OK;
 }
 int rbg_ctx_wide_card(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_hi) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   int hc;
   bool hv;
   CHK(ctx_wide(&ctx->c, op, batch, key_lo, key_hi, nullptr, true, &hc, &hv));
@@ -2433,25 +2507,25 @@ int rbg_ctx_wide_card(rbg_ctx* ctx, int op, int32_t batch, int key_lo, int key_h
   return RBG_OK;
 }
 int rbg_ctx_batch_and_card(rbg_ctx* ctx, int32_t batch) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_batch_card(&ctx->c, batch);
 }
 int rbg_ctx_card(rbg_ctx* ctx, int32_t* out) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   ResultInfo ri;
   CHK(ctx_info(&ctx->c, &ri));
   *out = (int32_t)ri.card32;
   return RBG_OK;
 }
 int rbg_ctx_cards(rbg_ctx* ctx, int32_t* out, size_t n) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   if (n > ctx->c.n_cards) return RBG_ERR_ILLEGAL_ARGUMENT;
   HIPCHK(hipMemcpyAsync(out, ctx->c.cards.p, 4 * n, hipMemcpyDeviceToHost, ctx->c.stream));
   HIPCHK(hipStreamSynchronize(ctx->c.stream));
   return RBG_OK;
 }
 int rbg_ctx_result_stats(rbg_ctx* ctx, int64_t* st) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   ResultInfo ri;
   CHK(ctx_info(&ctx->c, &ri));
   st[0] = ri.n_out;
@@ -2461,11 +2535,11 @@ int rbg_ctx_result_stats(rbg_ctx* ctx, int64_t* st) {
   return RBG_OK;
 }
 int rbg_ctx_serialize(rbg_ctx* ctx) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_serialize(&ctx->c);
 }
 int rbg_ctx_fetch(rbg_ctx* ctx, rbg_buffer* out) {
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_fetch(&ctx->c, out);
 }
 // Key-shard placement of the pending result inside a global portable bitmap of
@@ -2519,7 +2593,7 @@ static int ctx_fetch_shard_device(Ctx* c, int64_t total_containers, int has_run,
 int rbg_ctx_result_layout_device(rbg_ctx* ctx, void* dst3) {
   if (!ctx || !dst3) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c = &ctx->c;
-  HIPCHK(hipSetDevice(c->device));
+  CHK(enter(c));
   if (c->last != 1) {
     set_err("no materialised result pending");
     return RBG_ERR_ILLEGAL_ARGUMENT;
@@ -2539,7 +2613,7 @@ int rbg_ctx_fetch_shard_device_dyn(rbg_ctx* ctx, const void* layout, int rank, i
   if (!ctx || !layout || !out || world < 1 || world > 1024 || rank < 0 || rank >= world)
     return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c = &ctx->c;
-  HIPCHK(hipSetDevice(c->device));
+  CHK(enter(c));
   if (c->last != 1) {
     set_err("no materialised result pending");
     return RBG_ERR_ILLEGAL_ARGUMENT;
@@ -2560,7 +2634,7 @@ int rbg_ctx_fetch_shard_device_dyn(rbg_ctx* ctx, const void* layout, int rank, i
 int rbg_ctx_fetch_shard_device(rbg_ctx* ctx, int64_t total_containers, int has_run, int64_t payload_base,
                                void* desc_dst, void* offsets_dst, void* runflag_dst, void* payload_dst) {
   if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_fetch_shard_device(&ctx->c, total_containers, has_run, payload_base, desc_dst, offsets_dst, runflag_dst,
                                 payload_dst);
 }
@@ -2569,7 +2643,7 @@ int rbg_ctx_fetch_shard(rbg_ctx* ctx, int64_t total_containers, int has_run, int
                         int64_t payload_base, rbg_buffer* out_desc, rbg_buffer* out_offsets, rbg_buffer* out_payload) {
   if (!ctx || !out_desc || !out_offsets || !out_payload) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx& c = ctx->c;
-  HIPCHK(hipSetDevice(c.device));
+  CHK(enter(&c));
   (void)first_container;  // the shard's own buffers start at its first container
   ResultInfo ri;
   CHK(ctx_info(&c, &ri));
@@ -2935,7 +3009,7 @@ int rbg_run_optimize_many(const uint8_t* const* bufs, const size_t* lens, size_t
 
 int rbg_ctx_run_optimize(rbg_ctx* ctx, int32_t batch, int32_t* out_batch, uint8_t* answers) {
   if (!ctx || !out_batch) return RBG_ERR_ILLEGAL_ARGUMENT;
-  HIPCHK(hipSetDevice(ctx->c.device));
+  CHK(enter(&ctx->c));
   return ctx_run_optimize(&ctx->c, batch, out_batch, answers);
 }
 
@@ -2950,7 +3024,7 @@ int rbg_ctx_batch_minmax(rbg_ctx* ctx, int32_t batch, int32_t* out2) {
 
 int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, int key_hi, int32_t* batch) {
   Ctx* c = &ctx->c;
-  HIPCHK(hipSetDevice(c->device));
+  CHK(enter(c));
   if (kind == 4) return synth_c5(c, seed, n, key_lo, key_hi, batch);
   if (kind == 1 || kind == 2) return synth_c3(c, kind, seed, n, key_lo, key_hi, batch);
   if (kind == 3) return synth_c4(c, seed, n, batch);

@@ -15,7 +15,7 @@ enum WideMode : int {
   WIDE_XOR = 2,        // naive_xor
   WIDE_AND_SHY = 3,    // workShyAnd
   WIDE_AND_SHY_CARD = 4,  // workShyAndCardinality
-  WIDE_AND_NAIVE = 5,  // naive_and chain
+  WIDE_AND_NAIVE = 5,  // naive_and chain (WideArgs::buffer: BufferFastAggregation's)
   WIDE_LAZY_CHAIN = 6,  // lazyIOR chain + repairAfterLazy: ParallelAggregation.or, BufferFastAggregation.or(Mutable...),
                         // horizontal_or
   WIDE_XOR_CHAIN = 7,   // clone + ixor chain without restart: ParallelAggregation.xor, horizontal_xor
@@ -37,6 +37,8 @@ struct WideArgs {
   const uint32_t* order;  // chain modes: container index at chain position j of a key segment (null: input order)
   uint32_t chain;         // chain modes: kChain* flags
   unsigned long long* rd_bytes;  // workShyAnd: payload + 4 B per container it read, summed (null: not counted)
+  uint32_t buffer;        // naive_and: the buffer package's chain (MappeableRunContainer.iand(R) keeps the merged runs)
+  BigRuns big;            // naive_and (buffer): results of more than 2047 runs
 };
 
 // priority-queue aggregations (pq.hip): the size-ordered queue runs on the device.  Each
@@ -199,15 +201,6 @@ constexpr int kBsiSumWords = kBsiSumOut + 2;
 // atomics; k_bsi_sum_final adds the replicas.  All of it is zeroed by the plan kernel.
 constexpr int kBsiSumReps = 16;
 constexpr int kBsiSumAll = kBsiSumWords + 64 * kBsiSumReps;
-// Run containers of more than 2047 runs (8 KiB of runs) do not fit a result slot.  Only the buffer
-// package's run AND / ANDNOT run make them (no toEfficientContainer); such a result is written to
-// this arena (bump allocation; `overflow` set when `cap` is exceeded, `used` then tells the size
-// the op needs, and the host reruns it with a larger arena).
-struct BigRuns {
-  uint8_t* base;
-  unsigned long long* used;  // used[0] bytes reserved, used[1] overflow flag
-  uint64_t cap;
-};
 constexpr int kOwenOrder = 64;  // bytes per task of an owenGreatEqual chain order
 struct BsiArgs {
   int op;         // BsiOp

@@ -154,6 +154,7 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
   __shared__ uint32_t bslot[NT];
   __shared__ int sh[8];
   __shared__ Prefix shp;
+  __shared__ unsigned long long sh64;
   const uint32_t nt = *n_tasks;
   uint64_t rd_total = 0;  // workShyAnd's bytes read over this workgroup's keys (A.rd_bytes)
   // static stride over a resident grid (no contended counter)
@@ -539,8 +540,10 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
           empty = true;
           break;
         }
-        const bool need_r = st_kind == DK_R && d.kind == DK_R;  // R.iand(R) = R.and(R) -> EFF
-        st_kind = need_r ? eff(cc, count_runs(r, acc, sh)) : by_card(cc);
+        // R.iand(R) = R.and(R): toEfficientContainer on the heap (RB/RunContainer.java:381-456); the
+        // buffer package keeps the merged run container (RB/buffer/MappeableRunContainer.java:474-536)
+        const bool need_r = st_kind == DK_R && d.kind == DK_R;
+        st_kind = !need_r ? by_card(cc) : A.buffer ? DK_R : eff(cc, count_runs(r, acc, sh));
         c = cc;
       }
       if (empty) {
@@ -552,6 +555,13 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         continue;
       }
       kind = st_kind;
+      if (A.buffer && kind == DK_R) {
+        const int nr = count_runs(r, acc, sh);
+        if (nr > 2047) {  // more than a result slot holds
+          place_big_runs(t, tk.key, r, c, nr, oc, A.big, acc, sh, &sh64);
+          continue;
+        }
+      }
     }
 
     const uint32_t len = stage_container(kind, r, c, acc, tmp, sh);

@@ -151,6 +151,29 @@ class RoaringBitmap:
         raw = take(b)
         return np.frombuffer(raw, dtype=np.uint32).copy()
 
+    def contains(self, x) -> bool:
+        """RoaringBitmap.contains(int) (RB/RoaringBitmap.java:1693-1701): the key's container through
+        a binary search of the descriptor table (RoaringArray.getContainer), then the container's own
+        contains (ArrayContainer binary search, BitmapContainer bit test, RunContainer binary search
+        of the run starts), read straight from the serialized bytes."""
+        x = int(x) & 0xFFFFFFFF
+        key, low = x >> 16, x & 0xFFFF
+        ctr = _find_container(self._buf, key)
+        if ctr is None:
+            return False
+        kind, pay = ctr
+        if kind == 0:
+            i = int(np.searchsorted(pay, low))
+            return i < pay.size and int(pay[i]) == low
+        if kind == 1:
+            return bool((int(pay[low >> 6]) >> (low & 63)) & 1)
+        starts = pay[0::2]
+        i = int(np.searchsorted(starts, low, side="right")) - 1
+        return i >= 0 and low <= int(starts[i]) + int(pay[2 * i + 1])
+
+    def __contains__(self, x):
+        return self.contains(x)
+
     def __len__(self):
         return self.getLongCardinality()
 
@@ -185,6 +208,8 @@ class RoaringBitmap:
 
     def _inplace(self, op, x2):
         """x1.and / or / xor / andNot(x2) in place (rbg_pairwise_inplace); x2 may be x1 itself"""
+        if x2 is self and op in ("and", "or"):
+            return  # x1.and(x1) / x1.or(x1) return at once (RB/RoaringBitmap.java:1273, 2482)
         b = _lib.rbg_buffer()
         check(lib().rbg_pairwise_inplace(_lib.OP[op], self._buf, len(self._buf), x2._buf, len(x2._buf),
                                          int(x2 is self), ctypes.byref(b)))
@@ -219,6 +244,56 @@ class RoaringBitmap:
 
 setattr(RoaringBitmap, "and", RoaringBitmap.__dict__["and_"])
 setattr(RoaringBitmap, "or", RoaringBitmap.__dict__["or_"])
+
+
+def _find_container(buf, key):
+    """(kind, payload view) of `key`'s container in a portable serialized bitmap (RB/RoaringArray.java
+    :547-629 layout: cookie, run flags, (key, card - 1) descriptors, offsets unless a run bitmap of
+    fewer than 4 containers), or None.  kind 0 = array (u16 values), 1 = bitmap (u64 words), 2 = run
+    (u16 start, length - 1 pairs)."""
+    cookie = int.from_bytes(buf[0:4], "little")
+    if (cookie & 0xFFFF) == 12347:
+        size = (cookie >> 16) + 1
+        flags = buf[4:4 + (size + 7) // 8]
+        dpos = 4 + (size + 7) // 8
+        has_off = size >= 4
+    else:
+        size = int.from_bytes(buf[4:8], "little")
+        flags = None
+        dpos = 8
+        has_off = True
+    if size == 0:
+        return None
+    desc = np.frombuffer(buf, dtype="<u2", count=2 * size, offset=dpos)
+    keys = desc[0::2]
+    i = int(np.searchsorted(keys, key))
+    if i >= size or int(keys[i]) != key:
+        return None
+
+    def kind_of(j):
+        if flags is not None and (flags[j >> 3] >> (j & 7)) & 1:
+            return 2
+        return 1 if int(desc[2 * j + 1]) + 1 > 4096 else 0
+
+    def length(j, pos):
+        k = kind_of(j)
+        if k == 2:
+            return 2 + 4 * int.from_bytes(buf[pos:pos + 2], "little")
+        return 8192 if k == 1 else 2 * (int(desc[2 * j + 1]) + 1)
+
+    if has_off:
+        pos = int.from_bytes(buf[dpos + 4 * size + 4 * i:dpos + 4 * size + 4 * i + 4], "little")
+    else:  # no offset table: walk the (at most 3) payloads before it
+        pos = dpos + 4 * size
+        for j in range(i):
+            pos += length(j, pos)
+    k = kind_of(i)
+    if k == 0:
+        return 0, np.frombuffer(buf, dtype="<u2", count=int(desc[2 * i + 1]) + 1, offset=pos)
+    if k == 1:
+        return 1, np.frombuffer(buf, dtype="<u8", count=1024, offset=pos)
+    nr = int.from_bytes(buf[pos:pos + 2], "little")
+    return 2, np.frombuffer(buf, dtype="<u2", count=2 * nr, offset=pos + 2)
 
 
 def _identity_ids(bitmaps):
@@ -382,10 +457,15 @@ class BufferFastAggregation:
 
     An ImmutableRoaringBitmap is a mapped portable-format buffer, which is exactly
     what RoaringBitmap(serialized) holds, so every form takes the same objects.
-    The algorithms are FastAggregation's (buffer workShyAnd :426-494 is
-    FastAggregation.workShyAnd :356-414 over Mappeable containers; naive_or
-    :774-781 is naivelazyor + repairAfterLazy like :603-610; naive_xor :827-833
-    is the xor chain of :637-644).  The dispatch differs in three places:
+    The or / xor algorithms are FastAggregation's (naive_or :774-781 is naivelazyor +
+    repairAfterLazy like :603-610; naive_xor :827-833 is the xor chain of :637-644), and
+    buffer workShyAnd :426-494 is FastAggregation.workShyAnd :356-414 over Mappeable
+    containers.  The and chains are the buffer package's own: they run the in-place
+    MutableRoaringBitmap.and (RB/buffer/MutableRoaringBitmap.java:886-910), whose run AND run
+    keeps the merged run container (MappeableRunContainer.iand(R) = and(R), :1106-1108,
+    :474-536) where the heap chain's RunContainer.and(R) ends in toEfficientContainer.  So
+    these forms give other bytes than FastAggregation's whenever two run containers meet.
+    The dispatch also differs:
       - and(Iterator) :66-89 always runs workShyAnd (FastAggregation's runs
         naive_and, :26-28);
       - and(MutableRoaringBitmap...) :100-102 goes through convertToImmutable,
@@ -396,11 +476,19 @@ class BufferFastAggregation:
 
     @staticmethod
     def and_(*args):
-        """and(ImmutableRoaringBitmap...) :28-33, and(long[], ...) :43-58, and(Iterator) :66-89"""
+        """and(ImmutableRoaringBitmap...) :28-33, and(long[], ...) :43-58 (N > 10: workShyAnd, else the
+        buffer naive_and), and(Iterator) :66-89"""
         kind, buf, bms = _split_args(args)
         if kind == "iter":
             return _wide("workshy_and", bms) if bms else RoaringBitmap()
-        return FastAggregation.and_(*args)
+        if kind == "buffer" and len(bms) > 10:
+            if buf.size < 1024:
+                raise IllegalArgumentException("buffer should have at least 1024 elements.")
+            try:
+                return _wide("workshy_and", bms)
+            finally:
+                buf[...] = 0  # Arrays.fill(aggregationBuffer, 0L)
+        return _wide("buffer_and", bms, _identity_ids(bms))
 
     @staticmethod
     def and_mutable(*bitmaps):
@@ -409,13 +497,18 @@ class BufferFastAggregation:
 
     @staticmethod
     def naive_and(*args):
-        """naive_and(ImmutableRoaringBitmap...) :347-368 (smallest first), naive_and(Iterator) :383-396"""
-        return FastAggregation.naive_and(*args)
+        """naive_and(ImmutableRoaringBitmap...) :347-369 (smallest first, identity skip),
+        naive_and(Iterator) :383-396 (from the first)"""
+        kind, _, bms = _split_args(args)
+        if kind == "iter":
+            return _wide("buffer_and_iter", bms)
+        return _wide("buffer_naive_and", bms, _identity_ids(bms))
 
     @staticmethod
     def naive_and_mutable(*bitmaps):
         """naive_and(MutableRoaringBitmap...) :407-416: clone of the first, then the and chain"""
-        return _wide("and_iter", list(bitmaps))
+        bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
+        return _wide("buffer_and_iter", bms)
 
     @staticmethod
     def workShyAnd(buffer, *bitmaps):

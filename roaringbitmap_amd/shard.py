@@ -413,9 +413,12 @@ class DeviceShard:
     (rbg_ctx_fetch_shard_device_dyn).  No host round trip: the step is a chain of stream
     dependencies.  `gather()` then assembles the global bitmap on rank 0 (point-to-point)."""
 
-    def __init__(self, engine, rank, world, device, comm_device, group=None):
+    def __init__(self, engine, rank, world, device, comm_device, group=None, collective=None):
+        """collective: exchange the layout through the process group (default: when world > 1;
+        True at world 1 runs the all-gather path, stream waits included, on one rank)."""
         import torch
         self.eng, self.rank, self.world, self.group = engine, rank, world, group
+        self.collective = world > 1 if collective is None else bool(collective)
         self.dev, self.comm = torch.device(device), torch.device(comm_device)
         self.lay_local = torch.zeros(3, dtype=torch.int64, device=self.dev)
         self.lay_all = torch.zeros(3 * world, dtype=torch.int64, device=self.dev)
@@ -427,7 +430,7 @@ class DeviceShard:
     def place(self):
         import torch
         self.eng.result_layout_device(self.lay_local)
-        if self.world > 1:
+        if self.collective:
             dist = _dist()
             cur = torch.cuda.current_stream(self.dev)
             cur.wait_stream(self.ext)  # the layout is written
@@ -446,7 +449,7 @@ class DeviceShard:
     def layout(self):
         """the last step's GlobalLayout (synchronises)"""
         self.eng.sync()
-        a = (self.lay_all if self.world > 1 else self.lay_local).cpu().numpy()
+        a = (self.lay_all if self.collective else self.lay_local).cpu().numpy()
         return GlobalLayout(a.reshape(-1, 3))
 
     def gather(self):

@@ -3,7 +3,7 @@
 #   scripts/build_variant.sh NAME "-DRBG_EXP_X=1"  ->  roaringbitmap_amd/lib/variants/NAME.so
 # (load it with RBG_LIB=... ; the default library is untouched)
 set -e
-NAME=$1; FLAGS=$2
+NAME=$1; FLAGS="$2 -DRBG_PROFILING_BUILD=1"
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 C=$ROOT/roaringbitmap_amd/csrc
 OUT=$ROOT/roaringbitmap_amd/lib/variants/$NAME

@@ -94,7 +94,8 @@ OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "and_buf": 4, "andnot_buf": 5, 
 CARD_OPS = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
 WIDE_OPS = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5,
             "parallel_or": 6, "parallel_xor": 7, "buffer_or_mutable": 8, "horizontal_or": 9, "horizontal_xor": 10,
-            "priorityqueue_or": 11, "priorityqueue_xor": 12}
+            "priorityqueue_or": 11, "priorityqueue_xor": 12, "buffer_and": 13, "buffer_naive_and": 14,
+            "buffer_and_iter": 15}
 
 
 def pairwise(op, a: bytes, b: bytes) -> bytes:

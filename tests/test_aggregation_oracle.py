@@ -185,3 +185,50 @@ def test_chain_variants_agree_where_the_reference_says_so():
         assert O.wide("parallel_or", bms) == O.wide("buffer_or_mutable", bms)
     bms = [_gen.bitmap(rng, keys, p_present=1.0) for _ in range(16)]
     assert O.wide("parallel_or", bms) == O.wide("or", bms)
+
+
+def _rr_inputs(extra_arrays=False):
+    """Two run-container bitmaps whose run ANDs give one-value runs: keys 1 (1,000 runs of one value,
+    toEfficientContainer -> array), 2 (16,384 runs of one value -> bitmap, and more than 2,047 runs)
+    and 3 (a few long runs, which stay runs either way)."""
+    a = [(1, R, np.sort(np.concatenate([np.arange(0, 4000, 4), np.arange(1, 4000, 4)]))),
+         (2, R, np.sort(np.concatenate([np.arange(0, 65536, 4), np.arange(1, 65536, 4)]))),
+         (3, R, np.arange(100, 30000))]
+    b = [(1, R, np.sort(np.concatenate([np.arange(1, 4000, 4), np.arange(2, 4000, 4)]))),
+         (2, R, np.sort(np.concatenate([np.arange(1, 65536, 4), np.arange(2, 65536, 4)]))),
+         (3, R, np.arange(20000, 50000))]
+    if extra_arrays:
+        a.append((4, A, np.arange(0, 4000, 3)))
+        b.append((4, A, np.arange(0, 4000, 2)))
+    return encode(a), encode(b)
+
+
+def test_buffer_and_chain_keeps_merged_runs():
+    """BufferFastAggregation's and chains run MutableRoaringBitmap.and in place
+    (RB/buffer/MutableRoaringBitmap.java:886-910); MappeableRunContainer.iand(R) = and(R)
+    (RB/buffer/MappeableRunContainer.java:1106-1108, :474-536) keeps the merged run container,
+    where the heap's RunContainer.and(R) ends in toEfficientContainer (RB/RunContainer.java:381-456).
+    Same sets, other bytes."""
+    a, b = _rr_inputs(extra_arrays=True)
+    for heap_op, buf_op, ids in (("naive_and", "buffer_naive_and", [0, 1]), ("and", "buffer_and", [0, 1]),
+                                 ("and_iter", "buffer_and_iter", None)):
+        heap, buf = O.wide(heap_op, [a, b], ids), O.wide(buf_op, [a, b], ids)
+        assert heap != buf, buf_op
+        assert java_equals(heap, buf)  # RunContainer.equals compares sets: the reference's tests pass either way
+        dh, db = decode(heap), decode(buf)
+        assert [c[:3] for c in dh] == [(1, A, 1000), (2, B, 16384), (3, R, 10000), (4, A, 667)]
+        assert [c[:3] for c in db] == [(1, R, 1000), (2, R, 16384), (3, R, 10000), (4, A, 667)]
+    # the static ImmutableRoaringBitmap.and (RB/buffer/ImmutableRoaringBitmap.java:299-325) types alike
+    assert O.pairwise("and_buf", a, b) == O.wide("buffer_naive_and", [a, b], [0, 1])
+    # above 10 inputs and(Immutable...) is workShyAnd, which types as the heap's
+    many = [a, b] + [a] * 9
+    assert O.wide("buffer_and", many, list(range(11))) == O.wide("workshy_and", many)
+
+
+def test_buffer_and_chain_without_run_pairs_is_heap():
+    """Without a run AND run step the buffer chain's types are the heap chain's."""
+    rng = np.random.default_rng(5)
+    from _gen import bitmap
+    bufs = [bitmap(rng, np.arange(6), modes=["a_small", "b_dense", "b_mid"], p_present=1.0) for _ in range(4)]
+    assert O.wide("buffer_naive_and", bufs, [0, 1, 2, 3]) == O.wide("naive_and", bufs, [0, 1, 2, 3])
+    assert O.wide("buffer_and_iter", bufs) == O.wide("and_iter", bufs)

@@ -185,3 +185,57 @@ def test_bench_two_ranks_rehearsal(gpu):
         assert two["extra"][w]["result_serialized_bytes"] == one["extra"][w]["result_serialized_bytes"], w
         assert two["extra"][w]["output_bytes"] == one["extra"][w]["output_bytes"], w
     assert two["extra"]["c5_bsi_range_sum"]["sum_count"] == one["extra"]["c5_bsi_range_sum"]["sum_count"]
+
+
+def _rccl_worker(rank, world, port, outdir, op):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    # RCCL ("nccl" on ROCm) before any other GPU call of this process
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+    try:
+        import roaringbitmap_amd as rb
+        from roaringbitmap_amd import Engine, shard
+        e = Engine(0)
+        rng = np.random.default_rng(13)
+        va = np.concatenate([rng.integers(0, 300 << 16, 400000), np.arange(5 << 16, 9 << 16)])
+        vb = np.concatenate([rng.integers(0, 300 << 16, 400000), np.arange(7 << 16, (7 << 16) + 40000)])
+        a = e.load([rb.RoaringBitmap.from_values(va, run_optimize=True).serialize()])
+        b = e.load([rb.RoaringBitmap.from_values(vb, run_optimize=True).serialize()])
+        dev = torch.device("cuda", 0)
+        ds = shard.DeviceShard(e, rank, world, dev, dev, collective=True)
+        for _ in range(3):  # repeated steps reuse the buffers; every step waits on RCCL's stream
+            e.pairwise(op, a, b)
+            ds.place()
+        lay_local = ds.lay_local.cpu().tolist()
+        lay_all = ds.lay_all.cpu().tolist()
+        out = ds.gather()
+        e.pairwise(op, a, b)
+        ref = e.fetch().serialize()
+        with open(os.path.join(outdir, "res.bin"), "wb") as f:
+            f.write(bytes(out.cpu().numpy().tobytes()))
+        with open(os.path.join(outdir, "ref.bin"), "wb") as f:
+            f.write(ref)
+        with open(os.path.join(outdir, "lay.json"), "w") as f:
+            json.dump({"local": lay_local, "all": lay_all, "backend": dist.get_backend()}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("op", ["and", "or"])
+def test_rccl_device_layout_world1(gpu, op):
+    """The RCCL branch of shard.DeviceShard.place() on the one GPU of the box: a world-size-1 "nccl"
+    process group, the layout all-gathered with all_gather_into_tensor on device memory, ordered
+    against the engine stream by wait_stream both ways, then placed by rbg_ctx_fetch_shard_device_dyn:
+    the gathered bitmap equals the engine's whole-pair result byte for byte."""
+    import torch.multiprocessing as mp
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rccl_worker, args=(1, _free_port(), d, op), nprocs=1, join=True)
+        res = open(os.path.join(d, "res.bin"), "rb").read()
+        ref = open(os.path.join(d, "ref.bin"), "rb").read()
+        lay = json.load(open(os.path.join(d, "lay.json")))
+    assert lay["backend"] == "nccl"
+    assert lay["all"] == lay["local"] and lay["local"][0] > 0
+    assert res == ref

@@ -129,7 +129,8 @@ def test_buffer_fast_aggregation_dispatch(gpu, n):
     """RB/buffer/BufferFastAggregation.java: and(Iterator) :66-89 and and(Mutable...)
     :100-102 run workShyAnd for every N (FastAggregation's Iterator form runs
     naive_and); naive_and(Mutable...) :407-416 chains from the first bitmap; the
-    varargs forms dispatch like FastAggregation (workShyAnd above 10 inputs)."""
+    varargs forms dispatch like FastAggregation (workShyAnd above 10 inputs).  The and
+    chains are the buffer package's (run AND run keeps the merged runs)."""
     import roaringbitmap_amd as rb
     rng = np.random.default_rng(900 + n)
     bufs = [_gen.bitmap(rng, np.arange(8), p_present=0.85) for _ in range(n)]
@@ -139,10 +140,10 @@ def test_buffer_fast_aggregation_dispatch(gpu, n):
     ws = O.wide("workshy_and", bufs) if n else empty
     assert B.and_(iter(bms)).serialize() == ws
     assert B.and_mutable(*bms).serialize() == ws
-    assert getattr(B, "and")(*bms).serialize() == O.wide("and", bufs, list(range(n)))
-    assert B.naive_and(*bms).serialize() == O.wide("naive_and", bufs, list(range(n)))
-    assert B.naive_and(iter(bms)).serialize() == O.wide("and_iter", bufs)
-    assert B.naive_and_mutable(*bms).serialize() == O.wide("and_iter", bufs)
+    assert getattr(B, "and")(*bms).serialize() == O.wide("buffer_and", bufs, list(range(n)))
+    assert B.naive_and(*bms).serialize() == O.wide("buffer_naive_and", bufs, list(range(n)))
+    assert B.naive_and(iter(bms)).serialize() == O.wide("buffer_and_iter", bufs)
+    assert B.naive_and_mutable(*bms).serialize() == O.wide("buffer_and_iter", bufs)
     assert B.or_(*bms).serialize() == O.wide("or", bufs)
     assert B.or_(iter(bms)).serialize() == O.wide("or", bufs)
     assert B.xor(*bms).serialize() == O.wide("xor", bufs)
@@ -240,3 +241,38 @@ def test_workshy_bytes_read(gpu):
     disjoint = [O.from_values(np.concatenate([k * 65536 + 100 * i + np.arange(50) for k in range(6)]))
                 for i in range(12)]
     assert read(disjoint) == 6 * 4 * (4 + 2 * 50)
+
+
+@pytest.mark.parametrize("n", [2, 3, 6])
+def test_buffer_and_chain_run_pairs(gpu, n):
+    """BufferFastAggregation's and chains keep a run AND run result as the merged run container
+    (RB/buffer/MappeableRunContainer.java:474-536 via iand :1106-1108), including results of more
+    than 2,047 runs (16,384 one-value runs on key 2), where FastAggregation's heap chain converts
+    (RB/RunContainer.java:381-456): heap and buffer bytes differ, each byte-exact to its oracle."""
+    from _fmt import A, R, encode
+    rb = _rb()
+    rng = np.random.default_rng(40 + n)
+    bufs = []
+    for i in range(n):
+        ph = i % 2  # alternate {4k, 4k+1} and {4k+1, 4k+2}: every AND leaves the one-value runs {4k+1}
+        ctrs = [(1, R, np.sort(np.concatenate([np.arange(ph, 4000, 4), np.arange(1 + ph, 4000, 4)]))),
+                (2, R, np.sort(np.concatenate([np.arange(ph, 65536, 4), np.arange(1 + ph, 65536, 4)]))),
+                (3, R, np.arange(100 + 50 * i, 30000 + 1000 * i)),
+                (5, A, np.sort(rng.choice(65536, 3000, replace=False)))]
+        if i % 3 == 2:
+            ctrs.append((4, R, np.arange(0, 65536, 2)))  # 32,768 runs against the others' absence
+        bufs.append(encode(ctrs))
+    bms = [rb.RoaringBitmap(b) for b in bufs]
+    ids = list(range(n))
+    B = rb.BufferFastAggregation
+    for got, op, i in ((getattr(B, "and")(*bms), "buffer_and", ids), (B.naive_and(*bms), "buffer_naive_and", ids),
+                       (B.naive_and(iter(bms)), "buffer_and_iter", None),
+                       (B.naive_and_mutable(*bms), "buffer_and_iter", None)):
+        exp = O.wide(op, bufs, i)
+        assert got.serialize() == exp, op
+        assert exp != O.wide(op.replace("buffer_", ""), bufs, i)
+    kinds = [c[:2] for c in decode(B.naive_and(*bms).serialize())]
+    assert (2, R) in kinds and (1, R) in kinds
+    # FastAggregation's chains on the same inputs stay the heap's
+    _cmp("naive_and", bufs, ids)
+    _cmp("and_iter", bufs)

@@ -140,3 +140,59 @@ def test_illegal_argument_type():
     assert issubclass(IllegalArgumentException, ValueError)
     with pytest.raises(IllegalArgumentException):
         L.check(L.RBG_ERR_ILLEGAL_ARGUMENT)
+
+
+@pytest.mark.parametrize("n_keys", [1, 3, 4, 9])
+@pytest.mark.parametrize("run_opt", [False, True])
+def test_contains_reads_serialized_bytes(n_keys, run_opt):
+    """RoaringBitmap.contains (RB/RoaringBitmap.java:1693-1701) on the serialized bytes: every
+    container kind, run bitmaps below 4 containers (no offset table) and above, members and
+    non-members, against the value list."""
+    rng = np.random.default_rng(n_keys * 2 + run_opt)
+    vals = np.concatenate([bitmap_values(rng, m, n_keys) for m in ("a_small", "b_dense", "r_few")])
+    vals = np.unique(vals.astype(np.uint32))
+    rb = RoaringBitmap.from_values(vals, run_optimize=run_opt)
+    members = set(vals.tolist())
+    probes = np.concatenate([rng.choice(vals, 300), rng.integers(0, 1 << 32, 300, dtype=np.uint64),
+                             vals[:50] + 1, vals[-50:] - 1]).astype(np.uint32)
+    for x in probes.tolist():
+        assert rb.contains(x) == (x in members), x
+    assert not RoaringBitmap().contains(5)
+
+
+def test_bsi_get_value_uses_contains():
+    """BSI getValue (bsi/.../RoaringBitmapSliceIndex.java:181-196): ebM.contains, then valueAt."""
+    from roaringbitmap_amd import RoaringBitmapSliceIndex
+    rng = np.random.default_rng(3)
+    cols = np.unique(rng.integers(0, 1 << 20, 5000))
+    vals = rng.integers(0, 1 << 12, cols.size)
+    bsi = RoaringBitmapSliceIndex.from_columns(cols, vals, run_optimize=True)
+    for c, v in list(zip(cols.tolist(), vals.tolist()))[:200]:
+        assert bsi.getValue(c) == (v, True)
+    assert bsi.getValue(int(cols.max()) + 1) == (0, False)
+
+
+def test_inplace_same_object_needs_no_device():
+    """x1.and(x1) / x1.or(x1) return at once and x1.xor(x1) / x1.andNot(x1) clear it
+    (RB/RoaringBitmap.java:1273, 2482, 3297-3300, 1347-1350): no device call, so this runs without a
+    GPU.  The C ABI hands x1's own bytes back (validated; trailing bytes past the bitmap dropped)."""
+    from _fmt import R, encode
+    x = encode([(k, R, np.arange(10 * k, 10 * k + 500)) for k in range(5)])  # run bitmap, offset table
+    rb = RoaringBitmap(x)
+    rb.and_(rb)
+    assert rb.serialize() == x
+    rb.or_(rb)
+    assert rb.serialize() == x
+    for op in (0, 1):
+        out = L.rbg_buffer()
+        L.check(L.lib().rbg_pairwise_inplace(op, x + b"tail", len(x) + 4, x, len(x), 1, ctypes.byref(out)))
+        assert L.take(out) == x
+    for op in (2, 3):
+        out = L.rbg_buffer()
+        L.check(L.lib().rbg_pairwise_inplace(op, x, len(x), x, len(x), 1, ctypes.byref(out)))
+        assert L.take(out) == bytes.fromhex("3a30000000000000")
+    with pytest.raises(InvalidRoaringFormat):
+        out = L.rbg_buffer()
+        L.check(L.lib().rbg_pairwise_inplace(0, b"\x00" * 12, 12, x, len(x), 1, ctypes.byref(out)))
+    L.lib().rbg_trim()
+    assert L.lib().rbg_pool_evictions() == 0
