@@ -256,6 +256,11 @@ int rbg_ctx_batch_fetch_range(rbg_ctx* ctx, int32_t batch, size_t first, size_t 
  * container table, the counterpart of the Java result object); it is turned into
  * the portable format only by rbg_ctx_serialize / rbg_ctx_fetch. */
 int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
+/* rbg_ctx_pairwise followed by rbg_ctx_serialize (RoaringBitmap.and/or/xor/andNot, then serialize,
+ * RB/RoaringBitmap.java:377-473,3017-3019), as one pipeline: the key universe is cut into
+ * RBG_SER_PIPE (default 4) ranges and range r's placement and payload copies run on a second stream
+ * while range r + 1 computes.  The same bytes as the two calls. */
+int rbg_ctx_pairwise_serialized(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
 /* rbg_ctx_pairwise restricted to keys [key_lo, key_hi): one key-range shard of the op (each
  * key's result depends on that key's containers only, RB/RoaringBitmap.java:382-399); the
  * shards of a partition are assembled with rbg_ctx_fetch_shard(_device). */

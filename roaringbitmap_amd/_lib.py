@@ -35,7 +35,7 @@ EXPORTED = [
     "rbg_set_devices", "rbg_last_error", "rbg_version", "rbg_trim", "rbg_pool_evictions", "rbg_from_values", "rbg_run_optimize",
     "rbg_to_values", "rbg_inspect", "rbg_ctx_create", "rbg_ctx_destroy", "rbg_ctx_stream", "rbg_ctx_sync",
     "rbg_ctx_load", "rbg_ctx_synth", "rbg_ctx_release", "rbg_ctx_batch_stats", "rbg_ctx_batch_fetch",
-    "rbg_ctx_pairwise", "rbg_ctx_pairwise_range", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
+    "rbg_ctx_pairwise", "rbg_ctx_pairwise_serialized", "rbg_ctx_pairwise_range", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
     "rbg_ctx_batch_and_card", "rbg_ctx_card", "rbg_ctx_cards", "rbg_ctx_result_stats", "rbg_ctx_fetch",
     "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read", "rbg_ctx_profile_bytes", "rbg_ctx_serialize", "rbg_ctx_wide_start",
     "rbg_ctx_batch_counts", "rbg_synth_key_bytes", "rbg_ctx_pair_bytes", "rbg_debug_stamps",
@@ -88,6 +88,7 @@ def _declare(L):
     L.rbg_ctx_batch_fetch.argtypes = [vp, i32, sz, buf]
     L.rbg_ctx_batch_fetch_range.argtypes = [vp, i32, sz, sz, vp]
     L.rbg_ctx_pairwise.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz]
+    L.rbg_ctx_pairwise_serialized.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz]
     L.rbg_ctx_pairwise_range.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz, ctypes.c_int, ctypes.c_int]
     L.rbg_ctx_pairwise_card.argtypes = [vp, ctypes.c_int, i32, sz, i32, sz]
     L.rbg_ctx_wide.argtypes = [vp, ctypes.c_int, i32, ctypes.c_int, ctypes.c_int, P(i32)]

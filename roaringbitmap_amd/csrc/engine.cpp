@@ -159,6 +159,8 @@ struct DecBufs {  // scratch of the device decode (decode.hip), reused across lo
       size, cpart;
 };
 
+constexpr int kPipeMax = 16;  // key ranges of a pipelined pairwise op + serialization
+
 struct Ctx {
   int device = 0;
   DecBufs dec;
@@ -166,6 +168,10 @@ struct Ctx {
   uint32_t epoch = 0;
   DevBuf pc_cnt, pc_part, pc_items, pc_large;  // batched andCardinality scratch
   hipStream_t stream = nullptr;
+  // pipelined op + serialization (ctx_pairwise_ser): placement and payload copies of key range r
+  // run on stream2 while range r + 1 computes on stream
+  hipStream_t stream2 = nullptr;
+  hipEvent_t pipe_ev[kPipeMax + 1] = {};
   std::vector<std::unique_ptr<Batch>> batches;
   uint64_t* zlb = nullptr;    // look-back state the next plan kernel zeroes (null: none)
   uint64_t* ztile = nullptr;
@@ -227,6 +233,9 @@ Ctx::~Ctx() {
   prof_free();
   if (pinned) (void)hipHostFree(pinned);
   batches.clear();
+  for (hipEvent_t e : pipe_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (stream2) (void)hipStreamDestroy(stream2);
   if (stream) (void)hipStreamDestroy(stream);
 }
 
@@ -765,8 +774,75 @@ static int operand(Batch* b, size_t i, const uint16_t** keys, const CDesc** desc
 
 // op RBG_OR_INPLACE: x1.or(x2) in place (RB/RoaringBitmap.java:2481-2523), the OR with Container.ior's
 // types (k_ior_fix)
+// RoaringBitmap.and / or / xor / andNot + serialize of a dense key range as K key ranges in one
+// pipeline (ctx_pairwise with pipe_k > 1): range r's compute launch runs on the context stream; its
+// placement tiles (k_place: the look-back reads the tiles the earlier ranges published, so every record
+// gets its global output index and payload offset) and its payload copies (k_serialize part 2) run on
+// stream2 while range r + 1 computes.  The header (cookie, run flags, descriptors, offsets) follows the
+// last range; the context stream then waits for stream2.  Same records, same bytes as the op followed
+// by ctx_serialize: only the order of the launches differs.  Ranges are whole placement tiles.
+// RBG_PIPE_PW_WG / RBG_PIPE_COPY_WG: workgroups per CU of the compute / copy launches (defaults:
+// resident maximum, 1).
+static int pairwise_pipelined(Ctx* c, int op, int K, PwDirect pd, Batch* A, Batch* B, OutCtx oc) {
+  hipStream_t s = c->stream;
+  if (!c->stream2) {
+    HIPCHK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->pipe_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  hipStream_t s2 = c->stream2;
+  K = std::min(K, kPipeMax);
+  const uint32_t n = pd.nkeys;
+  // range bounds in whole tiles
+  const uint32_t tiles = (n + kPlaceTile - 1) / kPlaceTile;
+  K = (int)std::max<uint32_t>(1, std::min<uint32_t>((uint32_t)K, tiles));
+  const int pw_wg = getenv("RBG_PIPE_PW_WG") ? atoi(getenv("RBG_PIPE_PW_WG")) : 0;
+  const int cp_wg = getenv("RBG_PIPE_COPY_WG") ? atoi(getenv("RBG_PIPE_COPY_WG")) : 1;
+  int cus = 256;
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  c->mark(0);
+  c->mark(1);
+  // the first range's record -> the previous op's stream2 work (a pending header of the last
+  // pipelined op) is complete before this op reuses the records: stream waits for it at the end of
+  // every pipelined op, so nothing is needed here
+  uint32_t t_lo = 0;
+  for (int r = 0; r < K; r++) {
+    const uint32_t t_hi = r == K - 1 ? n : (uint32_t)(((uint64_t)tiles * (r + 1) / K) * kPlaceTile);
+    PwDirect d = pd;
+    d.key_lo = pd.key_lo + (int)t_lo;
+    d.nkeys = t_hi - t_lo;
+    if (r) d.zlb = d.ztile = nullptr;  // zeroed once, by the first range's launch
+    OutCtx o = oc;
+    o.recs = oc.recs + t_lo;
+    o.scratch = oc.scratch + (size_t)t_lo * kSlotBytes;
+    const int want = grid_for((d.nkeys + 3) / 4, 16384);
+    const int grid = pw_wg > 0 ? std::min(want, pw_wg * cus) : want;
+    launch_pairwise(s, op, 0, grid, c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), A->payload.as<uint8_t>(),
+                    B->payload.as<uint8_t>(), o, c->task_card.as<uint32_t>(), &d);
+    HIPCHK(hipEventRecord(c->pipe_ev[r], s));
+    HIPCHK(hipStreamWaitEvent(s2, c->pipe_ev[r], 0));
+    launch_place_tiles(s2, c->ntasks.as<uint32_t>(), oc, c->info.as<ResultInfo>(), t_lo, t_hi);
+    launch_serialize_part(s2, c->ntasks.as<uint32_t>(), oc, 2, t_lo, t_hi, cp_wg * cus);
+    t_lo = t_hi;
+  }
+  c->mark(2);
+  launch_serialize_part(s2, c->ntasks.as<uint32_t>(), oc, 1, 0, 0xFFFFFFFFu, 256);
+  HIPCHK(hipEventRecord(c->pipe_ev[kPipeMax], s2));
+  HIPCHK(hipStreamWaitEvent(s, c->pipe_ev[kPipeMax], 0));
+  c->place_pending = false;
+  c->serialized = true;
+  c->last = 1;
+  c->mark(3);
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
+
+// key ranges of a pipelined op + serialization (RBG_SER_PIPE, default 4; 1 = op, then serialization)
+static int pipe_ranges() {
+  const char* e = getenv("RBG_SER_PIPE");  // read per call (tests vary it)
+  return e ? std::max(1, atoi(e)) : 4;
+}
 static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only, int key_lo = 0,
-                        int key_hi = kMaxKeys) {
+                        int key_hi = kMaxKeys, int pipe_k = 0) {
   if (op == RBG_OR_INPLACE && !card_only) {
     CHK(ctx_pairwise(c, OP_OR, ia, ma, ib, mb, false, key_lo, key_hi));
     if (!c->ones.p) {
@@ -813,7 +889,8 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   c->pending_src = {ia, ib};
   c->mark(0);
   PwDirect pd{A->key_off.as<uint32_t>(), da, B->key_off.as<uint32_t>(), db, key_lo, (uint32_t)nkeys,
-              c->ntasks.as<uint32_t>(), c->zlb, c->ztile};
+              c->ntasks.as<uint32_t>(), c->zlb, c->ztile, (uint32_t)nkeys};
+  if (direct && pipe_k > 1 && !card_only) return pairwise_pipelined(c, op, pipe_k, pd, A, B, oc);
   if (!direct) {
     launch_plan_pairwise(s, plan_op, key_lo, key_hi, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(),
                          B->key_off.as<uint32_t>(), db, B->payload.as<uint8_t>(), c->wg_epoch.as<uint64_t>(),
@@ -1856,7 +1933,7 @@ int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_
   int32_t ids[2];
   CHK(ctx_load_separate(c, bufs, lens, 2, ids));  // one upload for both operands
   g.ids = {ids[0], ids[1]};
-  CHK(ctx_pairwise(c, op, ids[0], 0, ids[1], 0, false));
+  CHK(ctx_pairwise(c, op, ids[0], 0, ids[1], 0, false, 0, kMaxKeys, op == RBG_OR_INPLACE ? 0 : pipe_ranges()));
   return ctx_fetch(c, out);
 }
 
@@ -2328,6 +2405,13 @@ extern "C" {
 int rbg_ctx_pairwise(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
   CHK(enter(&ctx->c));
   return ctx_pairwise(&ctx->c, op, a, ia, b, ib, false);
+}
+int rbg_ctx_pairwise_serialized(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib) {
+  if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
+  CHK(enter(&ctx->c));
+  if (op < 0 || op > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
+  CHK(ctx_pairwise(&ctx->c, op, a, ia, b, ib, false, 0, kMaxKeys, pipe_ranges()));
+  return ctx_serialize(&ctx->c);  // no-op after the pipelined form
 }
 int rbg_ctx_pairwise_range(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib, int key_lo, int key_hi) {
   if (!ctx || key_lo > key_hi) return RBG_ERR_ILLEGAL_ARGUMENT;

@@ -131,8 +131,12 @@ __device__ __forceinline__ void write_cookie(uint8_t* base, uint32_t size, uint3
 // entry -- both tables are 4 B aligned (they end at payload_base).  Threads below the flag-byte
 // count pack the run-flag bitset from k_place's kind-by-output bytes; thread 0 writes the
 // cookie.
+//   PART bit 0: the header (cookie, run flags, descriptors, offsets) -- needs the placement of every record;
+//   PART bit 1: the payload copies of records [t_lo, t_hi) -- need only theirs (a key range of a pipelined op).
+template <int PART>
 __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ n_tasks, OutCtx oc,
-                                                   const uint8_t* __restrict__ kind_by_out) {
+                                                   const uint8_t* __restrict__ kind_by_out, uint32_t t_lo,
+                                                   uint32_t t_hi) {
   const uint32_t nt = *n_tasks;
   uint32_t size, has_run;
   uint64_t payload;
@@ -143,7 +147,7 @@ __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ 
   const bool offsets = !has_run || size >= 4;
   const uint64_t off_base = desc_base + 4ull * size;
   const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (has_run) {
+  if ((PART & 1) && has_run) {
     for (uint32_t b = gid; b < (size + 7) / 8; b += gridDim.x * blockDim.x) {
       uint8_t v = 0;
       for (int k = 0; k < 8; k++) {
@@ -153,19 +157,23 @@ __global__ __launch_bounds__(256) void k_serialize(const uint32_t* __restrict__ 
       base[4 + b] = v;
     }
   }
-  if (gid == 0) write_cookie(base, size, has_run);
-  // descriptors and offsets by thread (record i -> its output index): neighbouring threads
-  // write neighbouring entries, so the stores coalesce (written by each task's copying wave
-  // they were scattered 4 B stores: serialize 0.107 -> 0.105 ms)
-  for (uint32_t i = gid; i < nt; i += gridDim.x * blockDim.x) {
-    const ORec r = oc.recs[i];
-    if (!r.keep) continue;
-    *(g_u32*)(base + desc_base + 4ull * r.idx) = (uint32_t)r.key | ((r.card - 1) << 16);
-    if (offsets) *(g_u32*)(base + off_base + 4ull * r.idx) = (uint32_t)(H + r.off);
+  if (PART & 1) {
+    if (gid == 0) write_cookie(base, size, has_run);
+    // descriptors and offsets by thread (record i -> its output index): neighbouring threads
+    // write neighbouring entries, so the stores coalesce (written by each task's copying wave
+    // they were scattered 4 B stores: serialize 0.107 -> 0.105 ms)
+    for (uint32_t i = gid; i < nt; i += gridDim.x * blockDim.x) {
+      const ORec r = oc.recs[i];
+      if (!r.keep) continue;
+      *(g_u32*)(base + desc_base + 4ull * r.idx) = (uint32_t)r.key | ((r.card - 1) << 16);
+      if (offsets) *(g_u32*)(base + off_base + 4ull * r.idx) = (uint32_t)(H + r.off);
+    }
   }
+  if (!(PART & 2)) return;
   uint8_t* pay = oc.out + oc.payload_base;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t t = uni(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < nt; t += nw) {
+  const uint32_t te = min(nt, t_hi);
+  for (uint32_t t = uni(t_lo + blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)); t < te; t += nw) {
     const ORec& r = oc.recs[t];
     if (!uni(r.keep)) continue;
     const uint64_t off = uni64(r.off);
@@ -321,7 +329,10 @@ __device__ __forceinline__ Prefix lookback_wave(uint64_t* status, uint32_t t, ui
 // blockIdx order: counts, payload bytes and run flags scanned in the workgroup and
 // across tiles by lookback_wave; each tile's result cardinality goes to tile_card
 // before its status is published, and the last tile sums them.
-__global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_tasks, OutCtx oc, ResultInfo* __restrict__ info) {
+// tile_lo: the launch's first tile (a pipelined op places its key ranges one launch each, in order;
+// a tile's look-back reads the statuses the earlier launches published).
+__global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_tasks, OutCtx oc, ResultInfo* __restrict__ info,
+                                               uint32_t tile_lo) {
   __shared__ int wsum[3][4];
   __shared__ unsigned long long wbytes[4];
   __shared__ unsigned long long wcard[4];
@@ -329,13 +340,13 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
   const uint32_t nt = *n_tasks;
   const uint32_t ntiles = (nt + kTile - 1) / kTile;
   if (nt == 0) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && tile_lo == 0 && threadIdx.x == 0) {
       write_info(info, oc, 0, 0, 0);
       if (oc.layout_out) oc.layout_out[0] = oc.layout_out[1] = oc.layout_out[2] = 0;
     }
     return;
   }
-  const uint32_t tile = blockIdx.x;
+  const uint32_t tile = tile_lo + blockIdx.x;
   if (tile >= ntiles) return;
   constexpr int kPer = kTile / 256;  // records per thread
   const uint32_t t0 = tile * kTile + kPer * threadIdx.x;
@@ -599,14 +610,28 @@ void launch_compact(hipStream_t s, const uint8_t* flag, const Task* by_key, cons
 }
 
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info) {
-  hipLaunchKernelGGL(k_place, dim3(65536 / kTile), dim3(256), 0, s, nt, oc, info);
+  hipLaunchKernelGGL(k_place, dim3(65536 / kTile), dim3(256), 0, s, nt, oc, info, 0u);
+}
+void launch_place_tiles(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info, uint32_t t_lo, uint32_t t_hi) {
+  const uint32_t tl = t_lo / kTile, th = (t_hi + kTile - 1) / kTile;
+  if (th > tl) hipLaunchKernelGGL(k_place, dim3(th - tl), dim3(256), 0, s, nt, oc, info, tl);
 }
 void launch_spec_fix(hipStream_t s, const uint32_t* nt, OutCtx oc) {
   hipLaunchKernelGGL(k_spec_fix, dim3(std::max(1, resident_grid((const void*)&k_spec_fix))), dim3(256), 0, s, nt, oc);
 }
 void launch_serialize(hipStream_t s, const uint32_t* nt, OutCtx oc) {
-  hipLaunchKernelGGL(k_serialize, dim3(std::max(1, resident_grid((const void*)&k_serialize))), dim3(256), 0, s, nt, oc,
-                     (const uint8_t*)oc.kind_by_out);
+  hipLaunchKernelGGL(k_serialize<3>, dim3(std::max(1, resident_grid((const void*)&k_serialize<3>))), dim3(256), 0, s, nt,
+                     oc, (const uint8_t*)oc.kind_by_out, 0u, 0xFFFFFFFFu);
+}
+void launch_serialize_part(hipStream_t s, const uint32_t* nt, OutCtx oc, int part, uint32_t t_lo, uint32_t t_hi,
+                           int grid) {
+  if (part == 1) {
+    hipLaunchKernelGGL(k_serialize<1>, dim3(std::max(1, std::min(grid, 256))), dim3(256), 0, s, nt, oc,
+                       (const uint8_t*)oc.kind_by_out, t_lo, t_hi);
+  } else {
+    const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_serialize<2>)));
+    hipLaunchKernelGGL(k_serialize<2>, dim3(g), dim3(256), 0, s, nt, oc, (const uint8_t*)oc.kind_by_out, t_lo, t_hi);
+  }
 }
 void launch_serialize_shard(hipStream_t s, int grid, const uint32_t* nt, OutCtx oc, uint8_t* payload_dst, uint64_t off0,
                             uint8_t* desc, uint8_t* offs, uint8_t* runb) {

@@ -254,6 +254,7 @@ struct PwDirect {
   uint32_t* n_tasks_out;
   uint64_t* zlb;
   uint64_t* ztile;
+  uint32_t n_tasks_write;  // the task count block 0 writes to n_tasks_out (a pipelined op's total over its ranges)
 };
 // direct: null = tasks / nt from launch_plan_pairwise
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
@@ -269,6 +270,14 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
 // portable serialization (payload copies, descriptors, offsets, run flags,
 // cookie) runs only when the result is fetched
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info);
+// the placement tiles covering tasks [t_lo, t_hi) (t_lo a multiple of the 1,024-record tile), for a
+// pipelined op whose key ranges are placed one launch each, in order
+void launch_place_tiles(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info, uint32_t t_lo, uint32_t t_hi);
+constexpr uint32_t kPlaceTile = 1024;
+// one part of k_serialize: part 1 = the header (cookie, run flags, descriptors, offsets; every record
+// placed), part 2 = the payload copies of records [t_lo, t_hi); grid: workgroups to launch (clamped)
+void launch_serialize_part(hipStream_t s, const uint32_t* nt, OutCtx oc, int part, uint32_t t_lo, uint32_t t_hi,
+                           int grid);
 void launch_spec_fix(hipStream_t s, const uint32_t* nt, OutCtx oc);
 void launch_serialize(hipStream_t s, const uint32_t* nt, OutCtx oc);
 // key shard of a global bitmap: payloads into payload_dst, 4 B descriptors into desc, global

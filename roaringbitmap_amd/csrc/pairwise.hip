@@ -152,32 +152,6 @@ struct StampAcc {
 __device__ __forceinline__ void prio_hi() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ void prio_lo() { __builtin_amdgcn_s_setprio(0); }
 
-// Records one task's output.  Staged results (LDS) are copied to the task's
-// scratch slot (arena slot layout); results already in the slot or pass-through
-// containers are referenced in place.  k_place and the serializer follow.
-__device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
-                                        uint32_t len, uint32_t card, uint32_t key, int kind, const OutCtx& oc) {
-  const int l = lane_id();
-  uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
-  if (keep && staged) {
-    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
-    copy_lds_to_global<64>(slot, lds, len, l);
-    srcaddr = reinterpret_cast<uint64_t>(slot);
-  }
-  if (l == 0) {
-    ORec r;
-    r.off = 0;
-    r.src = srcaddr;
-    r.idx = 0;
-    r.card = card;
-    r.ser_len = len;
-    r.key = (uint16_t)key;
-    r.kind = (uint8_t)kind;
-    r.keep = keep ? 1 : 0;
-    oc.recs[t] = r;
-  }
-}
-
 // Filter path: AND with an array operand and ANDNOT of an array c1 always give an
 // array that is a subset of that array (App. A.1 / A.3; RB/ArrayContainer.java:
 // 184-271, RB/BitmapContainer.java:162-171, RB/RunContainer.java:305-334).  The
@@ -536,7 +510,7 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
   if (DIRECT) {
     // the plan kernel's other duties: the task count and the op's zeroed look-back state
     plan_zero(dsrc.zlb, dsrc.ztile);
-    if (blockIdx.x == 0 && threadIdx.x == 0) dsrc.n_tasks_out[0] = dsrc.nkeys;
+    if (blockIdx.x == 0 && threadIdx.x == 0) dsrc.n_tasks_out[0] = dsrc.n_tasks_write;
   }
   const uint32_t nt = DIRECT ? dsrc.nkeys : uni(*n_tasks);
   const int w = threadIdx.x >> 6;

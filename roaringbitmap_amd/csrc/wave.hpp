@@ -1081,6 +1081,32 @@ __device__ __forceinline__ void place_big_runs(uint32_t t, uint32_t key, const u
   wg_place(t, true, big.base + off, false, nullptr, len, (uint32_t)card, key, DK_R, oc, nullptr);
 }
 
+// Records one task's output (wave per task: pairwise, workShyAnd).  Staged results (LDS) are copied to the task's
+// scratch slot (arena slot layout); results already in the slot or pass-through
+// containers are referenced in place.  k_place and the serializer follow.
+__device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* src, bool staged, const uint32_t* lds,
+                                        uint32_t len, uint32_t card, uint32_t key, int kind, const OutCtx& oc) {
+  const int l = lane_id();
+  uint64_t srcaddr = reinterpret_cast<uint64_t>(src);
+  if (keep && staged) {
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes + (kind == DK_R ? 2 : 0);
+    copy_lds_to_global<64>(slot, lds, len, l);
+    srcaddr = reinterpret_cast<uint64_t>(slot);
+  }
+  if (l == 0) {
+    ORec r;
+    r.off = 0;
+    r.src = srcaddr;
+    r.idx = 0;
+    r.card = card;
+    r.ser_len = len;
+    r.key = (uint16_t)key;
+    r.kind = (uint8_t)kind;
+    r.keep = keep ? 1 : 0;
+    oc.recs[t] = r;
+  }
+}
+
 __device__ __forceinline__ void wg_passthrough(uint32_t t, const CDesc& d, const uint8_t* payload, const OutCtx& oc,
                                                Prefix* shp) {
   uint32_t len;

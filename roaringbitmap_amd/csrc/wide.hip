@@ -139,7 +139,7 @@ __device__ __forceinline__ int block_card(const uint64_t r[4], int* sh) {
 //   naive_or  (RB/FastAggregation.java:603-610): n == 1 -> clone + repairAfterLazy
 //             (A, B unchanged; R -> toEfficientContainer); n >= 2 -> lazy bitmap
 //             repaired: BY_CARD, 65536 -> R.full (RB/BitmapContainer.java:1205-1215)
-//   workShyAnd (:356-414): 0 dropped, <= 4096 A, 65536 R.full, else B
+//   workShyAnd (:356-414, k_shy_wave): 0 dropped, <= 4096 A, 65536 R.full, else B
 //   naive_and (:328-346): iand chain from the smallest input (RB/RoaringBitmap.java:1272-1296)
 //   naive_xor (:637-644): ixor chain with restart after an empty result
 //             (RB/RoaringBitmap.java:3296-3348)
@@ -156,7 +156,6 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
   __shared__ Prefix shp;
   __shared__ unsigned long long sh64;
   const uint32_t nt = *n_tasks;
-  uint64_t rd_total = 0;  // workShyAnd's bytes read over this workgroup's keys (A.rd_bytes)
   // static stride over a resident grid (no contended counter)
   uint32_t t = blockIdx.x - gridDim.x;
   while (true) {
@@ -480,36 +479,6 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
       c = st_card;
       kind = st_kind;
       }
-    } else if (MODE == WIDE_AND_SHY || MODE == WIDE_AND_SHY_CARD) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) r[i] = ~0ULL;
-      uint64_t rd = 0;  // bytes read (counted only when A.rd_bytes is set)
-      for (uint32_t j = 0; j < n; j++) {
-        uint64_t x[4];
-        const CDesc d = A.desc[s + j];
-        materialize(d, A.payload, tmp, q, x);
-        if (A.rd_bytes)
-          rd += 4 + (d.kind == DK_A   ? 2ull * d.card
-                     : d.kind == DK_B ? 8192ull
-                                      : 2ull + 4ull * *reinterpret_cast<const uint16_t*>(A.payload + d.slot + 2));
-#pragma unroll
-        for (int i = 0; i < 4; i++) r[i] &= x[i];
-        if ((j & 3) == 3) {  // an empty intersection stays empty: stop reading inputs
-          const int nz = (r[0] | r[1] | r[2] | r[3]) != 0;
-          if (!__syncthreads_or(nz)) break;
-        }
-      }
-      rd_total += rd;
-      c = block_card(r, sh);
-      if (MODE == WIDE_AND_SHY_CARD) {
-        if (threadIdx.x == 0) task_card[t] = (uint32_t)c;
-        continue;
-      }
-      if (c == 0) {
-        wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, &shp);
-        continue;
-      }
-      kind = c == 65536 ? DK_R : by_card(c);
     } else {  // WIDE_AND_NAIVE
       // start container: the one from input start_bm (segments are sorted by input index)
       int start = -1;
@@ -567,36 +536,269 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
     const uint32_t len = stage_container(kind, r, c, acc, tmp, sh);
     wg_place(t, true, nullptr, true, tmp, len, (uint32_t)c, tk.key, kind, oc, &shp);
   }
-  if (A.rd_bytes && threadIdx.x == 0 && rd_total) atomicAdd(A.rd_bytes, (unsigned long long)rd_total);
+}
+
+// ===========================================================================
+// FastAggregation.workShyAnd / workShyAndCardinality (RB/FastAggregation.java:356-414, :416-462):
+// one wave per common key.  The reference ANDs every container of the key into a lazy bitmap
+// (BitmapContainer.iand with cardinality -1) and repairs it at the end, so the result is typed by
+// its cardinality alone (BY_CARD, 65536 -> RunContainer.full) whatever the chain's order or
+// intermediate forms.  Here the running intersection is a sorted array, one value per lane, while
+// it holds at most 64 values (a uniform C3 key: ~15 values per input), and a register bitmap
+// (16 words per lane) otherwise; it is tested for emptiness after every input, and an empty one
+// ends the key's chain (an empty intersection stays empty).
+// ===========================================================================
+constexpr int kShyArr = 64;
+
+// values [0, card) of an array container at any 2 B alignment (packed batches), from the 16 B
+// vectors covering it: OR-scattered into the wave's LDS bitmap (MAP) or written to u16 st[idx]
+template <bool MAP>
+__device__ __forceinline__ void w_array_any(uint32_t* lds, const uint16_t* vals, int card) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(vals);
+  const int lo = (int)((a & 15) >> 1);
+  const uint4* v4 = reinterpret_cast<const uint4*>(a & ~(uintptr_t)15);
+  const int nvec = (card + lo + 7) >> 3;
+  const int l = lane_id();
+  uint16_t* st = reinterpret_cast<uint16_t*>(lds);
+#pragma unroll 1
+  for (int j0 = 0; 64 * j0 < nvec; j0 += kVecRound) {
+    uint4 v[kVecRound];
+#pragma unroll
+    for (int j = 0; j < kVecRound; j++) {
+      const int q = 64 * (j0 + j) + l;
+      v[j] = q < nvec ? ld_in(v4 + q) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < kVecRound; j++) {
+      const int base = 8 * (64 * (j0 + j) + l) - lo;  // value index of the vector's first element
+      uint32_t vm = 0;
+#pragma unroll
+      for (int i = 0; i < 8; i++) vm |= (uint32_t)((unsigned)(base + i) < (unsigned)card) << i;
+      if (MAP) {
+        scatter_vec_mask<0>(lds, v[j], vm);
+      } else {
+        const uint32_t w[4] = {v[j].x, v[j].y, v[j].z, v[j].w};
+#pragma unroll
+        for (int i = 0; i < 8; i++)
+          if ((vm >> i) & 1u) st[base + i] = (uint16_t)((w[i >> 1] >> ((i & 1) * 16)) & 0xFFFF);
+      }
+    }
+  }
+}
+
+// x &= the wave's LDS bitmap
+__device__ __forceinline__ void w_and_lds(const uint32_t* lds, WCtr& x) {
+  const uint4* q = reinterpret_cast<const uint4*>(lds) + lane_id();
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const uint4 v = q[64 * i];
+    x.w[2 * i] &= (uint64_t)v.x | ((uint64_t)v.y << 32);
+    x.w[2 * i + 1] &= (uint64_t)v.z | ((uint64_t)v.w << 32);
+  }
+}
+
+__device__ __forceinline__ bool w_any(const WCtr& x) {
+  uint64_t o = 0;
+#pragma unroll
+  for (int k = 0; k < 16; k++) o |= x.w[k];
+  return __any(o != 0);
+}
+
+// lane l < m holds value `val` of a sorted array: -> register bitmap
+__device__ __forceinline__ void w_array_regs_to_bitmap(uint32_t* lds, uint32_t val, int m, WCtr& x) {
+  wsync();
+  w_clear_lds(lds);
+  wsync();
+  if (lane_id() < m) atomicOr(&lds[val >> 5], 1u << (val & 31));
+  wsync();
+  w_read_lds(lds, x);
+}
+
+// sorted u16 st[0, m): is v one of them (lower bound)
+__device__ __forceinline__ uint32_t lds_contains(const uint16_t* st, int m, uint32_t v) {
+  int lo = 0, hi = m;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if ((uint32_t)st[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return (lo < m && (uint32_t)st[lo] == v) ? 1u : 0u;
+}
+
+// keep the lanes of `m` (ballot of the kept lanes): their values, still sorted, to lanes 0..popc - 1
+__device__ __forceinline__ uint32_t compact_lanes(uint16_t* st, uint64_t m, bool keep, uint32_t val, int cnt) {
+  wsync();
+  if (keep) st[__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = (uint16_t)val;
+  wsync();
+  return lane_id() < cnt ? (uint32_t)st[lane_id()] : 0u;
+}
+
+// 16 B descriptor through the scalar cache (wave-uniform address)
+__device__ __forceinline__ CDesc load_desc(const CDesc* desc, uint32_t i) {
+  typedef const __attribute__((address_space(4))) uint64_t* CU64;
+  const CU64 q = reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(desc + i));
+  union {
+    uint64_t u[2];
+    CDesc d;
+  } r;
+  r.u[0] = q[0];
+  r.u[1] = q[1];
+  return r.d;
+}
+
+template <int MODE>  // WIDE_AND_SHY or WIDE_AND_SHY_CARD
+__global__ __launch_bounds__(256) void k_shy_wave(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                  WideArgs A, OutCtx oc, uint32_t* __restrict__ task_card) {
+  __shared__ __align__(16) uint32_t lds_all[4][2048];
+  const int w = threadIdx.x >> 6, l = lane_id();
+  uint32_t* lds = lds_all[w];
+  uint16_t* st = reinterpret_cast<uint16_t*>(lds);
+  const uint32_t nt = uni(*n_tasks);
+  const uint32_t nw = gridDim.x * 4;
+  unsigned long long rd_total = 0;  // bytes read (A.rd_bytes): payload + 4 B per container consumed
+  for (uint32_t t = uni(blockIdx.x * 4 + (uint32_t)w); t < nt; t += nw) {
+    const uint32_t s = uni((uint32_t)tasks[t].a), n = uni((uint32_t)tasks[t].b), key = uni(tasks[t].key);
+    bool arr = false, empty = false;
+    int cnt = 0;
+    uint32_t val = 0;
+    WCtr x;
+    CDesc d = load_desc(A.desc, s);
+    for (uint32_t j = 0; j < n; j++) {
+      const CDesc dn = j + 1 < n ? load_desc(A.desc, s + j + 1) : d;  // in flight while d is used
+      const uint8_t* slot = A.payload + d.slot;
+      const uint16_t* v16 = reinterpret_cast<const uint16_t*>(slot);
+      if (A.rd_bytes)
+        rd_total += 4 + (d.kind == DK_A   ? 2ull * d.card
+                         : d.kind == DK_B ? 8192ull
+                                          : 2ull + 4ull * *reinterpret_cast<const uint16_t*>(slot + 2));
+      if (j == 0) {
+        if (d.kind == DK_A && d.card <= (uint32_t)kShyArr) {
+          arr = true;
+          cnt = (int)d.card;
+          val = l < cnt ? (uint32_t)v16[l] : 0u;
+        } else if (d.kind == DK_A) {
+          wsync();
+          w_clear_lds(lds);
+          wsync();
+          w_array_any<true>(lds, v16, (int)d.card);
+          wsync();
+          w_read_lds(lds, x);
+        } else {
+          w_materialize(d, A.payload, lds, x);
+        }
+      } else if (arr && d.kind != DK_R) {
+        uint32_t keep = 0;
+        if (d.kind == DK_B) {  // a bit test per value: one gathered word per lane
+          if (l < cnt) keep = (uint32_t)(reinterpret_cast<const uint64_t*>(slot)[val >> 6] >> (val & 63)) & 1u;
+        } else {  // the array staged in LDS, a binary search per value
+          const int m = (int)d.card;
+          wsync();
+          if (m <= kShyArr) {
+            if (l < m) st[l] = v16[l];
+          } else {
+            w_array_any<false>(lds, v16, m);
+          }
+          wsync();
+          if (l < cnt) keep = lds_contains(st, m, val);
+        }
+        const uint64_t km = __ballot(keep);
+        cnt = __popcll(km);
+        if (cnt == 0) {
+          empty = true;
+          break;
+        }
+        val = compact_lanes(st, km, keep != 0, val, cnt);
+      } else if (!arr && d.kind == DK_A && d.card <= (uint32_t)kShyArr) {
+        // bitmap AND a small array: a subset of the array, back to the array form
+        wsync();
+        w_write_lds(lds, x);
+        wsync();
+        const uint32_t v = l < (int)d.card ? (uint32_t)v16[l] : 0u;
+        const uint32_t keep = l < (int)d.card ? (lds[v >> 5] >> (v & 31)) & 1u : 0u;
+        const uint64_t km = __ballot(keep);
+        cnt = __popcll(km);
+        arr = true;
+        if (cnt == 0) {
+          empty = true;
+          break;
+        }
+        val = compact_lanes(st, km, keep != 0, v, cnt);
+      } else {
+        if (arr) {  // a run container: the running array as a bitmap first
+          w_array_regs_to_bitmap(lds, val, cnt, x);
+          arr = false;
+        }
+        if (d.kind == DK_A) {
+          wsync();
+          w_clear_lds(lds);
+          wsync();
+          w_array_any<true>(lds, v16, (int)d.card);
+          wsync();
+          w_and_lds(lds, x);
+        } else {
+          w_combine<0>(d, A.payload, lds, x);
+        }
+        if (!w_any(x)) {
+          empty = true;
+          break;
+        }
+      }
+      d = dn;
+    }
+    const int c = empty ? 0 : arr ? cnt : w_card(x);
+    if (MODE == WIDE_AND_SHY_CARD) {
+      if (l == 0) task_card[t] = (uint32_t)c;
+      continue;
+    }
+    if (c == 0) {  // dropped (:408)
+      w_place(t, false, nullptr, true, lds, 0, 0, key, DK_A, oc);
+      continue;
+    }
+    if (arr) {
+      wsync();
+      if (l < cnt) st[l] = (uint16_t)val;
+      wsync();
+      w_place(t, true, nullptr, true, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, oc);
+      continue;
+    }
+    const int kind = c == 65536 ? DK_R : by_card(c);  // BitmapContainer.repairAfterLazy
+    if (kind == DK_B) {
+      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+      w_store_bitmap(slot, x);
+      w_place(t, true, slot, false, lds, 8192, (uint32_t)c, key, DK_B, oc);
+      continue;
+    }
+    const uint32_t len = w_stage(kind, x, c, lds);
+    w_place(t, true, nullptr, true, lds, len, (uint32_t)c, key, kind, oc);
+  }
+  if (A.rd_bytes && l == 0 && rd_total) atomicAdd(A.rd_bytes, rd_total);
+}
+
+template <int MODE>
+static void launch_k_wide(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
+                          uint32_t* task_card) {
+  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_wide<MODE>)));
+  hipLaunchKernelGGL((k_wide<MODE>), dim3(g), dim3(256), 0, s, tasks, nt, args, oc, task_card);
+}
+template <int MODE>
+static void launch_k_shy(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
+                         uint32_t* task_card) {
+  // a wave per key: 4 keys per workgroup
+  const int g = std::max(1, std::min((grid + 3) / 4, resident_grid((const void*)&k_shy_wave<MODE>)));
+  hipLaunchKernelGGL((k_shy_wave<MODE>), dim3(g), dim3(256), 0, s, tasks, nt, args, oc, task_card);
 }
 
 void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
                  uint32_t* task_card) {
   switch (mode) {
-    case WIDE_OR:
-      hipLaunchKernelGGL((k_wide<WIDE_OR>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_OR>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
-      break;
-    case WIDE_OR_CARD:
-      hipLaunchKernelGGL((k_wide<WIDE_OR_CARD>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_OR_CARD>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
-      break;
-    case WIDE_XOR:
-      hipLaunchKernelGGL((k_wide<WIDE_XOR>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_XOR>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
-      break;
-    case WIDE_AND_SHY:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_AND_SHY>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
-      break;
-    case WIDE_AND_SHY_CARD:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_SHY_CARD>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_AND_SHY_CARD>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
-      break;
-    case WIDE_LAZY_CHAIN:
-      hipLaunchKernelGGL((k_wide<WIDE_LAZY_CHAIN>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_LAZY_CHAIN>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
-      break;
-    case WIDE_XOR_CHAIN:
-      hipLaunchKernelGGL((k_wide<WIDE_XOR_CHAIN>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_XOR_CHAIN>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
-      break;
-    default:
-      hipLaunchKernelGGL((k_wide<WIDE_AND_NAIVE>), dim3(std::max(1, std::min(grid, resident_grid((const void*)&k_wide<WIDE_AND_NAIVE>)))), dim3(256), 0, s, tasks, nt, args, oc, task_card);
-      break;
+    case WIDE_OR: launch_k_wide<WIDE_OR>(s, grid, tasks, nt, args, oc, task_card); break;
+    case WIDE_OR_CARD: launch_k_wide<WIDE_OR_CARD>(s, grid, tasks, nt, args, oc, task_card); break;
+    case WIDE_XOR: launch_k_wide<WIDE_XOR>(s, grid, tasks, nt, args, oc, task_card); break;
+    case WIDE_AND_SHY: launch_k_shy<WIDE_AND_SHY>(s, grid, tasks, nt, args, oc, task_card); break;
+    case WIDE_AND_SHY_CARD: launch_k_shy<WIDE_AND_SHY_CARD>(s, grid, tasks, nt, args, oc, task_card); break;
+    case WIDE_LAZY_CHAIN: launch_k_wide<WIDE_LAZY_CHAIN>(s, grid, tasks, nt, args, oc, task_card); break;
+    case WIDE_XOR_CHAIN: launch_k_wide<WIDE_XOR_CHAIN>(s, grid, tasks, nt, args, oc, task_card); break;
+    default: launch_k_wide<WIDE_AND_NAIVE>(s, grid, tasks, nt, args, oc, task_card); break;
   }
 }
 

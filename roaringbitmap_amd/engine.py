@@ -117,6 +117,11 @@ class Engine:
             check(lib().rbg_ctx_pairwise_range(self._ctx, _lib.OP[op], int(a), int(ia), int(b), int(ib), int(key_lo),
                                                int(key_hi)))
 
+    def pairwise_serialized(self, op, a, b, ia=0, ib=0):
+        """pairwise(op) + serialize() as one pipeline (rbg_ctx_pairwise_serialized): the result's
+        placement and payload copies for one key range overlap the next range's compute."""
+        check(lib().rbg_ctx_pairwise_serialized(self._ctx, _lib.OP[op], int(a), int(ia), int(b), int(ib)))
+
     def and_cardinality(self, a, b, ia=0, ib=0):
         check(lib().rbg_ctx_pairwise_card(self._ctx, 0, int(a), int(ia), int(b), int(ib)))
 

@@ -63,6 +63,28 @@ def c2(eng):
 
 @pytest.mark.parametrize("variant", ["raw", "runopt"])
 @pytest.mark.parametrize("op", ["and", "or", "xor", "andnot"])
+def test_c2_pipelined_serialization(eng, c2, variant, op, monkeypatch):
+    """rbg_ctx_pairwise_serialized (the bench's headline step): the op in K key ranges, each range's
+    placement and payload copies on a second stream while the next range computes.  For every K
+    (and thinned compute grids), the bytes equal the oracle's and the two-call form's."""
+    x, y, xa, xb = c2[variant]
+    exp = O.pairwise(op, xa, xb)
+    for k, pw in ((1, None), (2, None), (3, None), (4, None), (7, "3"), (16, None), (64, "2")):
+        monkeypatch.setenv("RBG_SER_PIPE", str(k))
+        if pw:
+            monkeypatch.setenv("RBG_PIPE_PW_WG", pw)
+        else:
+            monkeypatch.delenv("RBG_PIPE_PW_WG", raising=False)
+        for _ in range(2):  # back to back: the second op reuses the records the first one's stream2 read
+            eng.pairwise_serialized(op, x, y)
+        rs = eng.result_stats()
+        _same(eng.fetch().serialize(), exp, f"C2 {variant} {op} pipelined K={k}")
+        so = O.stats(exp)
+        assert rs["containers"] == so["array"] + so["bitmap"] + so["run"]
+
+
+@pytest.mark.parametrize("variant", ["raw", "runopt"])
+@pytest.mark.parametrize("op", ["and", "or", "xor", "andnot"])
 def test_c2_full_pair(eng, c2, variant, op):
     x, y, xa, xb = c2[variant]
     st = eng.batch_stats(x)

@@ -219,8 +219,8 @@ def test_wide_or_in_place_bitmaps(gpu, case):
 def test_workshy_bytes_read(gpu):
     """rbg_ctx_profile_bytes (the bench's C3 AND roofline): payload + 4 B per container that the
     early-exit workShyAnd read.  Identical inputs never empty, so every container is read;
-    pairwise-disjoint ones are empty after two inputs and the chain stops at its first check
-    (after four)."""
+    pairwise-disjoint ones are empty after two inputs, where the chain stops (it tests the
+    intersection after every input)."""
     from roaringbitmap_amd import Engine
     e = Engine(0)
 
@@ -240,7 +240,7 @@ def test_workshy_bytes_read(gpu):
     assert read([base] * 12) == 12 * (st["payload"] + 4 * (st["array"] + st["bitmap"] + st["run"]))
     disjoint = [O.from_values(np.concatenate([k * 65536 + 100 * i + np.arange(50) for k in range(6)]))
                 for i in range(12)]
-    assert read(disjoint) == 6 * 4 * (4 + 2 * 50)
+    assert read(disjoint) == 6 * 2 * (4 + 2 * 50)
 
 
 @pytest.mark.parametrize("n", [2, 3, 6])
@@ -276,3 +276,38 @@ def test_buffer_and_chain_run_pairs(gpu, n):
     # FastAggregation's chains on the same inputs stay the heap's
     _cmp("naive_and", bufs, ids)
     _cmp("and_iter", bufs)
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_workshy_forms(gpu, seed):
+    """FastAggregation.workShyAnd (RB/FastAggregation.java:356-414) per key, through every form of the
+    wave-per-key kernel's running intersection: small arrays kept in lanes (identical, partly
+    overlapping), array AND bitmap (bit gathers), array AND large array (LDS binary search), array
+    AND run (to a bitmap), run / bitmap AND small array (back to lanes), large arrays as bitmaps,
+    a full result (RunContainer.full), and chains that empty.  Bytes and cardinality vs the oracle."""
+    from _fmt import A, B, R, encode
+    rng = np.random.default_rng(300 + seed)
+    n = 12
+    base1 = np.sort(rng.choice(65536, 40, replace=False))
+    small = np.sort(rng.choice(5000, 30, replace=False))
+    big_sup = np.unique(np.concatenate([small, rng.choice(65536, 1970, replace=False)]))
+    mids = np.sort(rng.choice(65536, 3000, replace=False))
+    per = [[] for _ in range(n)]
+    for i in range(n):
+        per[i].append((0, A, small))
+        per[i].append((1, A, np.sort(rng.choice(base1, 36, replace=False))))
+        per[i].append((2, A, small) if i == 0 else (2, B, np.unique(np.concatenate([small, rng.choice(65536, 6000)]))))
+        per[i].append((3, R, np.arange(0, 5000)) if i == 0 else (3, A, np.sort(rng.choice(small, 28, replace=False)))
+                      if i == 1 else (3, A, small))
+        per[i].append((4, A, np.sort(rng.choice(mids, 2900, replace=False))))
+        per[i].append((5, R, np.arange(65536)))
+        per[i].append((6, A, small) if i % 2 == 0 else (6, R, np.arange(0, 6000)))
+        per[i].append((7, A, small) if i % 3 else (7, A, big_sup))
+        per[i].append((8, A, np.arange(100 * i, 100 * i + 50)))  # empty after two inputs
+        per[i].append((9, B, np.sort(rng.choice(65536, 20000, replace=False))))
+    bufs = [encode(p) for p in per]
+    _cmp("workshy_and", bufs)
+    _cmp("and", bufs, list(range(n)))  # N > 10: workShyAnd
+    assert gpu_wide_card("and", bufs) == O.wide_card("and", bufs)
+    kinds = {c[0]: c[1] for c in decode(O.wide("workshy_and", bufs))}
+    assert kinds[5] == R and kinds[0] == A and 8 not in kinds
