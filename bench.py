@@ -416,10 +416,11 @@ def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
     ext = torch.cuda.ExternalStream(eng.stream_ptr)
     sums = torch.zeros(2, dtype=torch.int64, device=torch.device("cuda", torch.cuda.current_device()))
 
+    eng.bsi_sums_target(sums)  # (sum, count) written into `sums` by the kernel that sums
+
     def step():
-        eng.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=True)
         ext.wait_stream(torch.cuda.current_stream())  # the last step's all-reduce has read `sums`
-        eng.bsi_sums_device(sums)
+        eng.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=True)
         if dist is not None:
             torch.cuda.current_stream().wait_stream(ext)
             if cdev == "cuda":
@@ -443,6 +444,7 @@ def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
     if dist is not None:
         dist.barrier()
     wall = time.perf_counter() - t0
+    eng.bsi_sums_target(None)
     sc = (int(sums[0]), int(sums[1]))
     ein = st["payload_bytes"] + 4 * st["containers"]
     t = torch.tensor([wall, float(ein)], dtype=torch.float64, device=cdev)

@@ -296,6 +296,9 @@ int rbg_ctx_bsi_buffer(rbg_ctx* ctx, int32_t batch, int op, int nbits, int has_f
 /* The same {sum, count} (two int64) copied to device memory dst2, enqueued on the context
  * stream (no host synchronisation: the sum stays on the device, e.g. for an all-reduce). */
 int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2);
+/* From now on every rbg_ctx_bsi with want_sum also writes its {sum, count} (two int64) to device
+ * memory dst2, in the kernel that computes them (no copy launch); null stops it. */
+int rbg_ctx_bsi_sums_target(rbg_ctx* ctx, void* dst2);
 /* Diagnostics: 20 per-phase shader-clock totals of the pairwise kernel (all zero unless the
  * library was built with -DRBG_STAMPS=1); reset != 0 clears them. */
 int rbg_debug_stamps(uint64_t* out20, int reset);

@@ -39,7 +39,7 @@ EXPORTED = [
     "rbg_ctx_batch_and_card", "rbg_ctx_card", "rbg_ctx_cards", "rbg_ctx_result_stats", "rbg_ctx_fetch",
     "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read", "rbg_ctx_profile_bytes", "rbg_ctx_serialize", "rbg_ctx_wide_start",
     "rbg_ctx_batch_counts", "rbg_synth_key_bytes", "rbg_ctx_pair_bytes", "rbg_debug_stamps",
-    "rbg_bsi_compare", "rbg_bsi_sum", "rbg_ctx_bsi", "rbg_ctx_bsi_sums", "rbg_ctx_bsi_sums_device", "rbg_ctx_batch_minmax",
+    "rbg_bsi_compare", "rbg_bsi_sum", "rbg_ctx_bsi", "rbg_ctx_bsi_sums", "rbg_ctx_bsi_sums_device", "rbg_ctx_bsi_sums_target", "rbg_ctx_batch_minmax",
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
     "rbg_ctx_fetch_shard_device", "rbg_bsi_compare_buffer", "rbg_ctx_bsi_buffer",
     "rbg_ctx_result_layout_device", "rbg_ctx_fetch_shard_device_dyn", "rbg_pairwise_inplace",
@@ -103,6 +103,7 @@ def _declare(L):
     L.rbg_ctx_bsi.argtypes = [vp, i32, ctypes.c_int, ctypes.c_int, ctypes.c_int, i32, i32, i32, i32, ctypes.c_int]
     L.rbg_ctx_bsi_sums.argtypes = [vp, P(ctypes.c_int64)]
     L.rbg_ctx_bsi_sums_device.argtypes = [vp, vp]
+    L.rbg_ctx_bsi_sums_target.argtypes = [vp, vp]
     L.rbg_ctx_batch_minmax.argtypes = [vp, i32, P(i32)]
     L.rbg_ctx_run_optimize.argtypes = [vp, i32, P(i32), P(ctypes.c_uint8)]
     L.rbg_run_optimize_many.argtypes = [vp, P(sz), sz, vp, P(ctypes.c_uint8)]

@@ -506,7 +506,16 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
                                                                 const uint32_t* __restrict__ n_tasks,
                                                  WideArgs A, BsiArgs P, OutCtx oc, bool want_sum,
                                                  const BsiIn* __restrict__ table, int* __restrict__ cnts,
-                                                 TB* __restrict__ kin, size_t tstride) {
+                                                 TB* __restrict__ kin, size_t tstride, BsiScratch z) {
+  if (blockIdx.x == 0 && z.table_ready) {  // the per-query zeroing of the (skipped) plan kernel
+    plan_zero(z.zlb, z.ztile);
+    if (z.zsums)
+      for (int i = threadIdx.x; i < kBsiSumAll; i += blockDim.x) z.zsums[i] = 0;
+    if (threadIdx.x == 0) {
+      if (z.defer) z.defer[0] = 0;
+      if (z.nt_dst) *z.nt_dst = *z.nt_src;
+    }
+  }
   // the 8 KiB scratch for array / run inputs aliases the count rows: inputs are
   // materialised before the circuit writes the rows, and after the last unit's sums
   __shared__ __align__(16) uint8_t rows[kBsiRows * kRowB];
@@ -1160,7 +1169,8 @@ void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm,
 // sum = sum over x of (long) (1 << x) * andCardinality(bA[x], found), each andCardinality a
 // Java int (RB/RoaringBitmap.java:413-434); (0, 0) when the found set is empty.  Lane x
 // takes slice x; the result stays on the device (sums[kBsiSumOut], [kBsiSumOut + 1]).
-__global__ __launch_bounds__(64) void k_bsi_sum_final(unsigned long long* __restrict__ sums, int nbits) {
+__global__ __launch_bounds__(64) void k_bsi_sum_final(unsigned long long* __restrict__ sums, int nbits,
+                                                      unsigned long long* __restrict__ dst) {
   const int x = threadIdx.x;
   // lane x: word x summed over the base words and k_bsi_types' replicas
   unsigned long long wx = x < kBsiSumWords ? sums[x] : 0;
@@ -1177,6 +1187,10 @@ __global__ __launch_bounds__(64) void k_bsi_sum_final(unsigned long long* __rest
   if (x == 0) {
     sums[kBsiSumOut] = v;
     sums[kBsiSumOut + 1] = count;
+    if (dst) {  // the caller's copy (rbg_ctx_bsi_sums_target), without a launch of its own
+      dst[0] = v;
+      dst[1] = count;
+    }
   }
 }
 
@@ -1190,15 +1204,19 @@ void launch_bsi_sums_out(hipStream_t s, const unsigned long long* sums, void* ds
   hipLaunchKernelGGL(k_bsi_sums_out, dim3(1), dim3(64), 0, s, sums, reinterpret_cast<unsigned long long*>(dst));
 }
 
+bool bsi_reg_path(int op, int nbits) { return op >= 0 && op <= BSI_RANGE && nbits <= kBsiRegSlices; }
+void launch_bsi_table(hipStream_t s, const Task* tasks, const uint32_t* nt, WideArgs args, void* table, size_t stride) {
+  hipLaunchKernelGGL(k_bsi_table, dim3((unsigned)((stride + 3) / 4)), dim3(256), 0, s, tasks, nt, args,
+                     reinterpret_cast<BsiIn*>(table));
+}
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
-                unsigned long long* sums, BsiScratch* sc) {
+                unsigned long long* sums, BsiScratch* sc, void* sums_dst) {
   if (p.op <= BSI_RANGE && p.nbits <= kBsiRegSlices && sc) {
-    hipLaunchKernelGGL(k_bsi_table, dim3((unsigned)((sc->stride + 3) / 4)), dim3(256), 0, s, tasks, nt, args,
-                       reinterpret_cast<BsiIn*>(sc->table));
+    if (!sc->table_ready) launch_bsi_table(s, tasks, nt, args, sc->table, sc->stride);
     const int g = std::max(1, std::min(grid * kBsiUnits, resident_grid((const void*)&k_bsi_reg)));
     hipLaunchKernelGGL(k_bsi_reg, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc, sums != nullptr,
                        reinterpret_cast<const BsiIn*>(sc->table), sc->cnts,
-                       reinterpret_cast<TB*>(sc->kin), sc->stride);
+                       reinterpret_cast<TB*>(sc->kin), sc->stride, *sc);
     const int g2 = (int)((sc->stride + 63) / 64);
     hipLaunchKernelGGL(k_bsi_types, dim3(g2), dim3(256), 0, s, tasks, nt, args, p, oc, sums, sc->cnts,
                        reinterpret_cast<const TB*>(sc->kin), sc->stride, sc->defer);
@@ -1208,7 +1226,9 @@ void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, 
     const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_bsi)));
     hipLaunchKernelGGL(k_bsi, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc, sums);
   }
-  if (sums) hipLaunchKernelGGL(k_bsi_sum_final, dim3(1), dim3(64), 0, s, sums, p.nbits);
+  if (sums)
+    hipLaunchKernelGGL(k_bsi_sum_final, dim3(1), dim3(64), 0, s, sums, p.nbits,
+                       reinterpret_cast<unsigned long long*>(sums_dst));
 }
 
 }  // namespace rbg

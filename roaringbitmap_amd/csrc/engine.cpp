@@ -145,6 +145,10 @@ struct Batch {
   size_t max_ser = 0;  // Σ serialized payload of containers larger than 8194 B (long run inputs)
   int32_t bsi_min = 0, bsi_max = 0;  // synthetic C5: min / max of the indexed values
   bool pair_cap_known = false;        // batched andCardinality: item capacity computed
+  // BSI compare over this batch (ebM = input 0): the task list (keys of ebM) and the per-key input
+  // table, planned by the first query and kept (ctx_bsi)
+  bool bsi_cached = false;
+  DevBuf bsi_tasks, bsi_nt, bsi_table;
   uint64_t pair_items_cap = 0;
   // host copy of the container table for fetches (batches are immutable once loaded):
   // h_desc in container order, h_pos[h_pos_off[i] .. h_pos_off[i+1]) = bitmap i's containers
@@ -177,6 +181,7 @@ struct Ctx {
   uint64_t* ztile = nullptr;
   DevBuf bsi_defer, bsi_cnts, bsi_kin, bsi_table;  // scratch of the register-resident BSI kernels
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
+  void* bsi_sums_dst = nullptr;  // rbg_ctx_bsi_sums_target: (sum, count) also written here by every sum
   // buffer-package BSI: owenGreatEqual's orInput types / task keys / chain order, and the arena of
   // result run containers above 2047 runs (BigRuns; big_ctl = {bytes used, overflow})
   DevBuf owen_tb, owen_keys, owen_ord, big, big_ctl;
@@ -1496,20 +1501,47 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
     CHK(c->bsi_table.ensure((size_t)16 * 34 * ub));
     sc = BsiScratch{c->bsi_defer.as<uint32_t>(), c->bsi_cnts.as<int>(), c->bsi_kin.p, ub, c->bsi_table.p};
   }
-  c->mark(0);
-  launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
-                  c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile,
-                  c->bsi_sums.as<unsigned long long>(), sc.defer);
-  launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), c->tasks.as<Task>(),
-                 c->ntasks.as<uint32_t>());
-  c->mark(1);
   WideArgs wa{};
   wa.desc = B->desc.as<CDesc>();
   wa.bm = B->bm.as<uint32_t>();
   wa.payload = B->payload.as<uint8_t>();
+  c->mark(0);
+  Task* tasks = c->tasks.as<Task>();
+  uint32_t* nt = c->ntasks.as<uint32_t>();
+  if (sc.defer && bsi_reg_path(mode, nbits)) {
+    // The task list (keys where ebM has a container) and the input table depend on the batch
+    // only: planned once per batch, kept with it (RoaringBitmapSliceIndex queries on one index,
+    // BSI/:482-513, re-walk the same keys every time).
+    if (!B->bsi_cached) {
+      CHK(B->bsi_tasks.ensure(sizeof(Task) * kMaxKeys));
+      CHK(B->bsi_nt.ensure(64));
+      CHK(B->bsi_table.ensure((size_t)16 * 34 * ub));
+      launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
+                      c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr);
+      launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(),
+                     B->bsi_tasks.as<Task>(), B->bsi_nt.as<uint32_t>());
+      launch_bsi_table(s, B->bsi_tasks.as<Task>(), B->bsi_nt.as<uint32_t>(), wa, B->bsi_table.p, ub);
+      B->bsi_cached = true;
+    }
+    tasks = B->bsi_tasks.as<Task>();
+    nt = B->bsi_nt.as<uint32_t>();
+    sc.table = B->bsi_table.p;
+    sc.table_ready = true;
+    sc.zlb = c->zlb;
+    sc.ztile = c->ztile;
+    sc.zsums = c->bsi_sums.as<unsigned long long>();
+    sc.nt_src = nt;
+    sc.nt_dst = c->ntasks.as<uint32_t>();
+  } else {
+    launch_plan_bsi(s, B->key_off.as<uint32_t>(), B->bm.as<uint32_t>(), need, c->by_key.as<Task>(),
+                    c->flag.as<uint8_t>(), c->wg_count.as<uint32_t>(), c->zlb, c->ztile,
+                    c->bsi_sums.as<unsigned long long>(), sc.defer);
+    launch_compact(s, c->flag.as<uint8_t>(), c->by_key.as<Task>(), c->wg_count.as<uint32_t>(), tasks, nt);
+  }
+  c->mark(1);
   BsiArgs p{mode < 0 ? BSI_EQ : mode, nbits, has_found, (uint32_t)start, (uint32_t)end};
-  launch_bsi(s, grid_for(ub, 65536), c->tasks.as<Task>(), c->ntasks.as<uint32_t>(), wa, p, oc,
-             want_sum ? c->bsi_sums.as<unsigned long long>() : nullptr, sc.defer ? &sc : nullptr);
+  launch_bsi(s, grid_for(ub, 65536), tasks, nt, wa, p, oc, want_sum ? c->bsi_sums.as<unsigned long long>() : nullptr,
+             sc.defer ? &sc : nullptr, want_sum ? c->bsi_sums_dst : nullptr);
   c->mark(2);
   if (op == BSI_SUM_ONLY) {
     c->last = 0;
@@ -2468,6 +2500,11 @@ int rbg_ctx_bsi_sums(rbg_ctx* ctx, int64_t* out2) {
   if (!out2) return RBG_ERR_ILLEGAL_ARGUMENT;
   CHK(enter(&ctx->c));
   return ctx_bsi_sums(&ctx->c, out2);
+}
+int rbg_ctx_bsi_sums_target(rbg_ctx* ctx, void* dst2) {
+  if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
+  ctx->c.bsi_sums_dst = dst2;
+  return RBG_OK;
 }
 int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2) {
   if (!ctx || !dst2 || !ctx->c.bsi_sums.p) return RBG_ERR_ILLEGAL_ARGUMENT;

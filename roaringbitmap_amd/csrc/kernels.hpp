@@ -320,10 +320,24 @@ struct BsiScratch {
   void* kin;
   size_t stride;
   void* table;  // 34 x 16 B per task: each input's container of the key
+  // The task list and the input table depend on the batch only: a batch keeps them across queries
+  // (table_ready: k_bsi_table skipped).  The zeroing the plan kernel does per query is then done by
+  // block 0 of k_bsi_reg (zlb / ztile: placement look-back, zsums: sum words, zdefer: defer count),
+  // and the batch's task count is copied to nt_dst (the context's, which k_place reads).
+  bool table_ready;
+  uint64_t* zlb;
+  uint64_t* ztile;
+  unsigned long long* zsums;
+  const uint32_t* nt_src;
+  uint32_t* nt_dst;
 };
+// true: compare `op` over `nbits` slices runs the register-resident kernels (k_bsi_table, k_bsi_reg, ...)
+bool bsi_reg_path(int op, int nbits);
+void launch_bsi_table(hipStream_t s, const Task* tasks, const uint32_t* nt, WideArgs args, void* table, size_t stride);
 void launch_bsi_sums_out(hipStream_t s, const unsigned long long* sums, void* dst);  // 2 x u64 at kBsiSumOut
+// sums_dst (nullable): (sum, count) also written there by the final sum kernel (two int64, device memory)
 void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc,
-                unsigned long long* sums, BsiScratch* sc);
+                unsigned long long* sums, BsiScratch* sc, void* sums_dst = nullptr);
 // buffer-package compare (p.buffer): k_bsi_owen_pre writes the orInput types of owenGreatEqual per
 // task (p.owen_tb, p.task_keys) for the host's horizontal_or queue replay; k_bsi_buf runs the circuit
 void launch_bsi_owen_pre(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p);

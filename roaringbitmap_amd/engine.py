@@ -185,6 +185,11 @@ class Engine:
         the engine stream (no host synchronisation)."""
         check(lib().rbg_ctx_bsi_sums_device(self._ctx, ctypes.c_void_p(dst.data_ptr())))
 
+    def bsi_sums_target(self, dst):
+        """From now on every BSI sum also writes its (sum, count) into the int64 device tensor `dst`
+        (two elements) from the kernel that computes it; None stops it (rbg_ctx_bsi_sums_target)."""
+        check(lib().rbg_ctx_bsi_sums_target(self._ctx, None if dst is None else ctypes.c_void_p(dst.data_ptr())))
+
     def batch_counts(self, batch) -> np.ndarray:
         """containers per input bitmap of a batch"""
         n = self.batch_stats(batch)["bitmaps"]

@@ -124,3 +124,21 @@ def test_c5_synthetic_bsi(gpu):
         for a, z in ((lo, hi), (int(v[7]), int(v[7]) + 3), (int(v[11]) - 1, int(v[11]))):
             e.bsi(b, op, 31, a, z, mn, mx)
             assert e.fetch().serialize() == o.compare(op, a, z), (op, a, z)
+    # the sums target (the bench's C5 step): every sum also lands in d, written by the summing kernel
+    d2 = torch.empty(2, dtype=torch.int64, device="cuda:0")
+    e.bsi_sums_target(d2)
+    e.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=True)
+    e.sync()
+    assert (int(d2[0]), int(d2[1])) == o.sum(exp)
+    e.bsi_sums_target(None)
+    # a second index on the same engine: each batch keeps its own task list and input table
+    b2 = e.synth(4, seed + 1, rows // 3)
+    mn2, mx2 = e.batch_minmax(b2)
+    o2 = _bsi.BSI(e.batch_fetch(b2, 0).serialize(), [e.batch_fetch(b2, i).serialize() for i in range(1, 32)], mn2, mx2)
+    for _ in range(2):
+        for bb, oo, m0, m1 in ((b, o, mn, mx), (b2, o2, mn2, mx2)):
+            e.bsi(bb, "GE", 31, lo, 0, m0, m1, want_sum=True)
+            ex = oo.compare("GE", lo, 0)
+            assert e.fetch().serialize() == ex
+            assert e.bsi_sums() == oo.sum(ex)
+    e.release(b2)
