@@ -145,6 +145,11 @@ struct Batch {
   size_t max_ser = 0;  // Σ serialized payload of containers larger than 8194 B (long run inputs)
   int32_t bsi_min = 0, bsi_max = 0;  // synthetic C5: min / max of the indexed values
   bool pair_cap_known = false;        // batched andCardinality: item capacity computed
+  // made by runOptimize: kinds / payload bytes / run flags still in ro_stats (device: 5 u64 totals,
+  // then a u32 run flag per bitmap at +64) until ensure_stats reads them
+  bool stats_pending = false;
+  DevBuf ro_stats;
+  std::vector<uint8_t> h_has_run;
   // BSI compare over this batch (ebM = input 0): the task list (keys of ebM) and the per-key input
   // table, planned by the first query and kept (ctx_bsi)
   bool bsi_cached = false;
@@ -336,13 +341,46 @@ static uint32_t next_epoch(Ctx* c) {
   return c->epoch;
 }
 
-static int get_batch(Ctx* c, int32_t id, Batch** out) {
+static int find_batch(Ctx* c, int32_t id, Batch** out) {
   if (id < 0 || (size_t)id >= c->batches.size() || !c->batches[id] || !c->batches[id]->live) {
     set_err("invalid batch id " + std::to_string(id));
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   *out = c->batches[id].get();
   return RBG_OK;
+}
+
+// A batch made by runOptimize on the device has its statistics (container kinds, payload bytes, the
+// per-bitmap run flags) in device memory until something on the host needs them: read them then.
+static int ensure_stats(Ctx* c, Batch* b) {
+  if (!b->stats_pending) return RBG_OK;
+  const size_t n = b->n_bm;
+  unsigned long long h[5] = {};
+  std::vector<uint32_t> hf(n);
+  HIPCHK(hipMemcpyAsync(h, b->ro_stats.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+  if (n) HIPCHK(hipMemcpyAsync(hf.data(), b->ro_stats.as<uint8_t>() + 64, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  b->stats_pending = false;
+  if (h[4] > b->payload_bytes) {  // payload_bytes holds the input's, a bound (a theorem; else a device error)
+    set_err("runOptimize: converted payload larger than its input");
+    return RBG_ERR_DEVICE;
+  }
+  for (int k = 0; k < 3; k++) b->n_kind[k] = (int64_t)h[k];
+  b->payload_bytes = h[4];
+  int64_t ser = (int64_t)h[3];
+  b->h_has_run.assign(n, 0);
+  for (size_t i = 0; i < n; i++) {
+    const size_t nc = b->h_bm_nctr.empty() ? 0 : b->h_bm_nctr[i];
+    ser += (int64_t)header_size(nc, hf[i] != 0);
+    b->h_has_run[i] = hf[i] != 0;
+  }
+  if (b->ser_bytes) b->ser_bytes = ser;  // batches built on the device carry no serialized size
+  return RBG_OK;
+}
+
+static int get_batch(Ctx* c, int32_t id, Batch** out) {
+  CHK(find_batch(c, id, out));
+  return ensure_stats(c, *out);
 }
 
 static int32_t new_batch(Ctx* c) {
@@ -358,7 +396,7 @@ static int32_t new_batch(Ctx* c) {
 constexpr size_t kPoolMax = 2ull << 30;    // bytes of released buffers a context keeps
 constexpr size_t kPoolMaxBuf = 1ull << 30;  // larger buffers are freed at once
 
-// a released batch buffer into the context's pool (the stream is idle: rbg_ctx_release syncs)
+// a released batch buffer into the context's pool (reused only by later work on the same stream)
 static void pool_put(Ctx* c, DevBuf& b) {
   if (!b.p) return;
   std::lock_guard<std::mutex> g(c->pool_mu);
@@ -2266,15 +2304,20 @@ int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, s
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch) {
   Ctx& c = ctx->c;
   Batch* b;
-  CHK(get_batch(&c, batch, &b));
+  CHK(find_batch(&c, batch, &b));  // no statistics read-back for a batch that goes
   CHK(enter(&c));
   // A materialised result references pass-through containers inside its operand
   // batches (ORec::src) until it is serialized: serialize it before an operand goes.
   if (c.last == 1 && !c.serialized &&
       std::find(c.pending_src.begin(), c.pending_src.end(), batch) != c.pending_src.end())
     CHK(ctx_serialize(&c));
-  HIPCHK(hipStreamSynchronize(c.stream));
-  for (DevBuf* d : {&b->keys, &b->desc, &b->bm, &b->key_off, &b->bm_off, &b->payload}) pool_put(&c, *d);
+  // No host sync: the buffers go to this context's pool, and whatever reuses them is enqueued on
+  // the same stream after every launch that reads them (a pipelined op's second stream is joined
+  // back into it at the op's end); a pooled buffer that is freed goes through hipFree, which waits
+  // for the device.
+  for (DevBuf* d : {&b->keys, &b->desc, &b->bm, &b->key_off, &b->bm_off, &b->payload, &b->ro_stats,
+                    &b->bsi_tasks, &b->bsi_nt, &b->bsi_table})
+    pool_put(&c, *d);
   c.batches[batch].reset();
   return RBG_OK;
 }
@@ -3041,8 +3084,6 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
   CHK(c->ro_info.ensure(4 * C + 16));
   CHK(c->ro_size.ensure(8 * C + 16));
   CHK(c->ro_part.ensure(8 * (scan_parts(C) + 1)));
-  CHK(c->ro_flags.ensure(4 * n + 16));
-  CHK(c->scalar.ensure(64));
   // the new batch's buffers before any kernel: a conversion only happens when the new form is
   // smaller, and its 16 B-rounded slot is no larger either, so the input's payload size bounds
   // the output's -- plan, scan and write then run back to back with one host sync at the end
@@ -3058,29 +3099,21 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
   } drop{c, bid};
   CHK(pool_take(c, b.desc, sizeof(CDesc) * C + 16));
   CHK(pool_take(c, b.payload, a->payload_bytes + 64));
+  CHK(pool_take(c, b.ro_stats, 64 + 4 * n + 16));
   CHK(copy_dev(c, b.keys, a->keys, s));
   CHK(copy_dev(c, b.bm, a->bm, s));
   CHK(copy_dev(c, b.key_off, a->key_off, s));
   CHK(copy_dev(c, b.bm_off, a->bm_off, s));
-  HIPCHK(hipMemsetAsync(c->ro_flags.p, 0, 4 * n + 16, s));
-  HIPCHK(hipMemsetAsync(c->scalar.p, 0, 64, s));
-  unsigned long long* tot = c->scalar.as<unsigned long long>();
+  HIPCHK(hipMemsetAsync(b.ro_stats.p, 0, 64 + 4 * n + 16, s));
+  unsigned long long* tot = b.ro_stats.as<unsigned long long>();
   launch_runopt_plan(s, a->desc.as<CDesc>(), a->bm.as<uint32_t>(), a->payload.as<uint8_t>(), C,
-                     c->ro_info.as<uint32_t>(), c->ro_size.as<uint64_t>(), c->ro_flags.as<uint32_t>(), tot);
+                     c->ro_info.as<uint32_t>(), c->ro_size.as<uint64_t>(), b.ro_stats.as<uint32_t>() + 16, tot);
   launch_exclusive_scan(s, c->ro_size.as<uint64_t>(), c->ro_size.as<uint64_t>(), C, c->ro_part.as<uint64_t>(),
                         reinterpret_cast<uint64_t*>(tot + 4));
   launch_runopt_write(s, a->desc.as<CDesc>(), a->payload.as<uint8_t>(), C, c->ro_info.as<uint32_t>(),
                       c->ro_size.as<uint64_t>(), b.desc.as<CDesc>(), b.payload.as<uint8_t>());
   HIPCHK(hipGetLastError());
-  unsigned long long h[5] = {};
-  std::vector<uint32_t> hf(n);
-  HIPCHK(hipMemcpyAsync(h, tot, sizeof(h), hipMemcpyDeviceToHost, s));
-  if (n) HIPCHK(hipMemcpyAsync(hf.data(), c->ro_flags.p, 4 * n, hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  if (h[4] > a->payload_bytes) {  // the bound above is a theorem; a violation is a device error
-    set_err("runOptimize: converted payload larger than its input");
-    return RBG_ERR_DEVICE;
-  }
+  // no host read-back here: the new batch's statistics stay on the device until needed (ensure_stats)
   b.n_bm = n;
   b.n_ctr = C;
   b.key_major = a->key_major;
@@ -3090,19 +3123,17 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
   b.long_card = a->long_card;
   b.bsi_min = a->bsi_min;
   b.bsi_max = a->bsi_max;
-  for (int k = 0; k < 3; k++) b.n_kind[k] = (int64_t)h[k];
-  b.payload_bytes = h[4];
+  b.payload_bytes = a->payload_bytes;  // a bound until ensure_stats reads the real size
   b.max_ser = 0;  // runOptimize leaves no container above 8194 serialized bytes
-  int64_t ser = (int64_t)h[3];
-  for (size_t i = 0; i < n; i++) {
-    const size_t nc = a->h_bm_nctr.empty() ? 0 : a->h_bm_nctr[i];
-    ser += (int64_t)header_size(nc, hf[i] != 0);
-    if (answers) answers[i] = hf[i] != 0;
-  }
-  b.ser_bytes = a->ser_bytes ? ser : 0;  // batches built on the device carry no serialized size
+  b.ser_bytes = a->ser_bytes ? 1 : 0;  // nonzero: computed by ensure_stats
+  b.stats_pending = true;
   b.live = true;
   drop.keep = true;
   *out_id = bid;
+  if (answers) {  // runOptimize's boolean per bitmap: the statistics now
+    CHK(ensure_stats(c, &b));
+    for (size_t i = 0; i < n; i++) answers[i] = b.h_has_run[i];
+  }
   return RBG_OK;
 }
 

@@ -145,11 +145,16 @@ class Engine:
         check(lib().rbg_ctx_pair_bytes(self._ctx, int(batch), out))
         return int(out[0]), int(out[1])
 
-    def run_optimize(self, batch):
+    def run_optimize(self, batch, answers=True):
         """RoaringBitmap.runOptimize (RB/RoaringBitmap.java:2764-2774) of every bitmap of a batch, on the
-        device -> (new batch id, [runOptimize's boolean per bitmap]).  Synchronous."""
-        n = self.batch_stats(batch)["bitmaps"]
+        device -> (new batch id, [runOptimize's boolean per bitmap]).  The booleans need a read-back
+        (synchronous); answers=False returns (id, None) with nothing read back: the new batch's
+        statistics stay on the device until a host-side use needs them."""
         out = ctypes.c_int32()
+        if not answers:
+            check(lib().rbg_ctx_run_optimize(self._ctx, int(batch), ctypes.byref(out), None))
+            return int(out.value), None
+        n = self.batch_stats(batch)["bitmaps"]
         ans = (ctypes.c_uint8 * max(n, 1))()
         check(lib().rbg_ctx_run_optimize(self._ctx, int(batch), ctypes.byref(out), ans))
         return int(out.value), [bool(x) for x in ans[:n]]

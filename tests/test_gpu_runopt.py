@@ -118,3 +118,31 @@ def test_run_optimize_reuses_released_buffers(gpu):
             e.release(a)
     finally:
         e.close()
+
+
+def test_engine_run_optimize_without_readback(gpu):
+    """runOptimize with no booleans asked for (the bench's timed loop): the new batch's statistics stay
+    on the device; the first host-side use reads them (kinds, payload bytes), an op uses the batch
+    before that, and releasing it needs no read-back.  Same bytes as the synchronous form."""
+    from roaringbitmap_amd import Engine
+    e = Engine(0)
+    a = e.synth(0, 0xC2A0)
+    b = e.synth(0, 0xC2B0)
+    src_a, src_b = e.batch_fetch(a).serialize(), e.batch_fetch(b).serialize()
+    for _ in range(3):  # released without read-back, buffers back to the pool and reused
+        o, none = e.run_optimize(a, answers=False)
+        assert none is None
+        e.release(o)
+    oa, _ = e.run_optimize(a, answers=False)
+    ob, _ = e.run_optimize(b, answers=False)
+    e.pairwise("and", oa, ob)  # an op on the pending batches (reads their statistics first)
+    exp_a, exp_b = O.run_optimize(src_a), O.run_optimize(src_b)
+    assert e.fetch().serialize() == O.pairwise("and", exp_a, exp_b)
+    st = e.batch_stats(oa)
+    ost = O.stats(exp_a)
+    assert (st["array"], st["bitmap"], st["run"]) == (ost["array"], ost["bitmap"], ost["run"])
+    assert e.batch_fetch(oa).serialize() == exp_a
+    oc, ans = e.run_optimize(oa)  # runOptimize of an optimized batch: nothing changes
+    assert e.batch_fetch(oc).serialize() == exp_a and ans == [_answer(exp_a)]
+    for x in (a, b, oa, ob, oc):
+        e.release(x)
