@@ -497,7 +497,7 @@ def cpu_baselines(eng, a, b, in_bytes, budget_s):
     info = _cpu_info()
     java = shutil.which("java")
     threads = max(1, (info["affinity"] or 1) - 1)
-    n_legs = 12
+    n_legs = 13
     target = budget_s / (n_legs * 11.0)  # 11 iterations per leg (calibration + 5 + 5)
     legs = {}
 
@@ -534,18 +534,30 @@ def cpu_baselines(eng, a, b, in_bytes, budget_s):
         "RoaringBitmap.and(x1, x2) on the full C2 pair")
     leg("c2_and_mt", lambda r: O.time_and_parallel(xa, xb, threads, r), in_bytes, threads,
         f"key-parallel RoaringBitmap.and over {threads} key ranges, full C2 pair")
-    # C3: all 10,000 bitmaps restricted to a key sample (uniform: 128 keys; clustered: 512 keys)
+    # C3: all 10,000 bitmaps restricted to a key sample (uniform: 128 keys; clustered: 512 keys) on one
+    # thread; ParallelAggregation.or over the whole clustered job (1.3 GB) and the uniform sample (the
+    # whole uniform job is 22 GB)
     for kind, name, keys in ((1, "uniform", 128), (2, "clustered", 512)):
         sb = eng.synth(kind, 0xC3000000, 10000, 0, keys)
         st = eng.batch_stats(sb)
         sbytes = st["payload_bytes"] + 4 * st["containers"]
         bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
         eng.release(sb)
-        leg(f"c3_{name}_or_1t", lambda r: O.time_wide("or", bufs, r), sbytes, 1,
+        leg(f"c3_{name}_or_1t_sample", lambda r: O.time_wide("or", bufs, r), sbytes, 1,
             f"FastAggregation.or of 10,000 C3 {name} bitmaps, keys [0, {keys})")
-        leg(f"c3_{name}_or_mt", lambda r: O.time_wide_parallel("or", bufs, threads, r), sbytes, threads,
-            f"ParallelAggregation.or (key groups over {threads} workers), same sample")
+        if kind == 1:
+            leg(f"c3_{name}_or_mt_sample", lambda r: O.time_wide_parallel("or", bufs, threads, r), sbytes, threads,
+                f"ParallelAggregation.or (key groups over {threads} workers), same sample")
         del bufs
+    sb = eng.synth(2, 0xC3000000, 10000)
+    st = eng.batch_stats(sb)
+    sbytes = st["payload_bytes"] + 4 * st["containers"]
+    bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
+    eng.release(sb)
+    leg("c3_clustered_or_mt", lambda r: O.time_wide_parallel("or", bufs, threads, r), sbytes, threads,
+        f"ParallelAggregation.or (key groups over {threads} workers) of the whole C3 clustered job "
+        f"(10,000 bitmaps, {sbytes / 1e9:.2f} GB)")
+    del bufs
     # C4: the first 65,536 of the million pairs (same generator, seed 0xC4)
     n4 = 65536
     sb = eng.synth(3, 0xC4, n4)
@@ -559,16 +571,31 @@ def cpu_baselines(eng, a, b, in_bytes, budget_s):
         f"the same loop split over {threads} workers")
     legs["c4_andcard_mt"]["pairs_per_s"] = round(n4 / (legs["c4_andcard_mt"]["ms"] / 1e3), 1)
     del bufs
-    # C5: the 10^9-row column's first 16 keys (1,048,576 rows), ebM + 31 slices
+    # C5: the 10^9-row column's first 16 keys (1,048,576 rows), ebM + 31 slices, on one thread; the
+    # whole column key-parallel
     sb = eng.synth(4, 0xC5, 16 * 65536, 0, 16)
     st = eng.batch_stats(sb)
     sbytes = st["payload_bytes"] + 4 * st["containers"]
     bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
     eng.release(sb)
     lo, hi = 1 << 29, 1 << 30
-    leg("c5_bsi_range_sum_1t", lambda r: O.time_bsi_range_sum(bufs[0], bufs[1:], lo, hi, r)[0], sbytes, 1,
+    leg("c5_bsi_range_sum_1t_sample", lambda r: O.time_bsi_range_sum(bufs[0], bufs[1:], lo, hi, r)[0], sbytes, 1,
         "RoaringBitmapSliceIndex.compare(RANGE, 2^29, 2^30) + sum, rows [0, 2^20) (16 keys x 31 slices)")
-    legs["c5_bsi_range_sum_1t"]["rows_per_s"] = round(16 * 65536 / (legs["c5_bsi_range_sum_1t"]["ms"] / 1e3), 1)
+    legs["c5_bsi_range_sum_1t_sample"]["rows_per_s"] = round(
+        16 * 65536 / (legs["c5_bsi_range_sum_1t_sample"]["ms"] / 1e3), 1)
+    del bufs
+    rows5 = 10 ** 9
+    sb = eng.synth(4, 0xC5, rows5)
+    st = eng.batch_stats(sb)
+    sbytes = st["payload_bytes"] + 4 * st["containers"]
+    bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
+    eng.release(sb)
+    leg("c5_bsi_range_sum_mt", lambda r: O.time_bsi_range_sum_parallel(bufs[0], bufs[1:], lo, hi, threads, r)[0],
+        sbytes, threads, f"the same query over all {rows5} rows ({st['containers']} containers), key ranges over "
+                         f"{threads} workers (per-key sums added before sum's int cast)")
+    legs["c5_bsi_range_sum_mt"]["rows_per_s"] = round(rows5 / (legs["c5_bsi_range_sum_mt"]["ms"] / 1e3), 1)
+    legs["c5_bsi_range_sum_mt"]["sum_count"] = list(O.time_bsi_range_sum_parallel(bufs[0], bufs[1:], lo, hi,
+                                                                                  threads, 1)[1])
     del bufs
     best = legs["c2_and_mt"]
     return {"value": best["GBps"], "unit": "GB/s", "cores": best["threads"], "kind": "port",

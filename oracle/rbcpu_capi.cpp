@@ -371,4 +371,62 @@ double rbo_time_bsi_range_sum(const uint8_t* const* bufs, const size_t* lens, in
   return dt;
 }
 
+// The same query key-parallel (compare and the per-slice andCardinality are per-key sums, BSI/:482-513,
+// 581-592): every bitmap is cut into `threads` contiguous key ranges outside the clock (ranges of equal
+// ebM container counts), each worker runs the circuit on its ranges, and the per-slice cardinalities are
+// added over the workers before sum's Java int cast.  Seconds for reps queries.
+double rbo_time_bsi_range_sum_parallel(const uint8_t* const* bufs, const size_t* lens, int nbits, uint32_t lo,
+                                       uint32_t hi, int threads, int reps, int64_t* out2) {
+  std::vector<Bitmap> bms;
+  std::vector<const Bitmap*> ptrs;
+  if (load_many(bufs, lens, (size_t)nbits + 1, &bms, &ptrs)) return -1.0;
+  const int T = std::max(1, threads);
+  const Bitmap& e0 = bms[0];
+  auto cut = [&](const Bitmap& b, uint32_t klo, uint32_t khi) {
+    Bitmap o;
+    for (size_t i = 0; i < b.size(); i++)
+      if (b.keys[i] >= klo && b.keys[i] < khi) {
+        o.keys.push_back(b.keys[i]);
+        o.ctrs.push_back(b.ctrs[i]);
+      }
+    return o;
+  };
+  std::vector<std::vector<Bitmap>> part(T);  // part[t] = [ebM, bA...] restricted to worker t's keys
+  for (int t = 0; t < T; t++) {
+    const size_t i0 = e0.size() * t / T, i1 = e0.size() * (t + 1) / T;
+    const uint32_t klo = i0 < e0.size() ? e0.keys[i0] : 65536u, khi = i1 < e0.size() ? e0.keys[i1] : 65536u;
+    for (const Bitmap& b : bms) part[t].push_back(cut(b, klo, khi));
+  }
+  std::vector<int64_t> cards((size_t)T * nbits), counts(T);
+  int64_t sum = 0, count = 0;
+  double t0 = now_s();
+  for (int r = 0; r < reps; r++) {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      th.emplace_back([&, t]() {
+        const Bitmap& ebm = part[t][0];
+        std::vector<Bitmap> ba(part[t].begin() + 1, part[t].end());
+        const Bitmap found = op_and(oneil(ebm, ba, true, lo), oneil(ebm, ba, false, hi));
+        counts[t] = found.long_card();
+        for (int x = 0; x < nbits; x++) cards[(size_t)t * nbits + x] = op_and_card(ba[x], found);
+      });
+    for (auto& x : th) x.join();
+    count = 0;
+    for (int t = 0; t < T; t++) count += counts[t];
+    uint64_t s = 0;
+    for (int x = 0; x < nbits; x++) {
+      int64_t c = 0;
+      for (int t = 0; t < T; t++) c += cards[(size_t)t * nbits + x];
+      s += (uint64_t)((int64_t)(int32_t)(1u << x) * (int64_t)(int32_t)(uint32_t)(uint64_t)c);
+    }
+    sum = (int64_t)s;
+  }
+  const double dt = now_s() - t0;
+  if (out2) {
+    out2[0] = sum;
+    out2[1] = count;
+  }
+  return dt;
+}
+
 }  // extern "C"

@@ -66,6 +66,10 @@ def lib():
                                              ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                              ctypes.POINTER(ctypes.c_int64)]
         L.rbo_time_bsi_range_sum.restype = ctypes.c_double
+        L.rbo_time_bsi_range_sum_parallel.argtypes = [ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                                      ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                                      ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+        L.rbo_time_bsi_range_sum_parallel.restype = ctypes.c_double
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -212,6 +216,15 @@ def time_bsi_range_sum(ebm, slices, lo, hi, reps):
     arr, lens = _bufs([ebm] + list(slices))
     out = (ctypes.c_int64 * 2)()
     t = lib().rbo_time_bsi_range_sum(arr, lens, len(slices), lo, hi, reps, out)
+    return t, (int(out[0]), int(out[1]))
+
+
+def time_bsi_range_sum_parallel(ebm, slices, lo, hi, threads, reps):
+    """The same query key-parallel over `threads` workers (per-key sums added before sum's int cast);
+    -> (seconds for reps queries, (sum, count))."""
+    arr, lens = _bufs([ebm] + list(slices))
+    out = (ctypes.c_int64 * 2)()
+    t = lib().rbo_time_bsi_range_sum_parallel(arr, lens, len(slices), lo, hi, threads, reps, out)
     return t, (int(out[0]), int(out[1]))
 
 

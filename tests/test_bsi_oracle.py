@@ -73,3 +73,19 @@ def test_oracle_matches_brute_force(seed):
         assert got == set(cols[m].tolist()), op
     found = O.from_values(cols[::3])
     assert b.sum(found) == (int(v[::3].sum()), len(cols[::3]))
+
+
+def test_parallel_range_sum_leg_matches_single_thread():
+    """The bench's key-parallel CPU leg (rbo_time_bsi_range_sum_parallel) gives the single-thread
+    compare(RANGE) + sum (BSI/:482-513, 581-592) for any worker count."""
+    rng = np.random.default_rng(8)
+    cols = np.unique(rng.integers(0, 40 << 16, 60000))
+    vals = rng.integers(0, 1 << 20, cols.size)
+    ebm = O.from_values(cols, True)
+    slices = [O.from_values(cols[(vals >> i) & 1 == 1], True) for i in range(20)]
+    lo, hi = 1 << 17, 3 << 18
+    _, one = O.time_bsi_range_sum(ebm, slices, lo, hi, 1)
+    m = (vals >= lo) & (vals <= hi)
+    assert one == (int(vals[m].sum()), int(m.sum()))
+    for t in (1, 2, 3, 7, 64):
+        assert O.time_bsi_range_sum_parallel(ebm, slices, lo, hi, t, 1)[1] == one
