@@ -120,6 +120,25 @@ static_assert(kWaveLds >= 2048, "the 8 KiB bitmap map / staging area");
 // Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
 // pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
 // their own; no result depends on them.
+// Diagnostic build only (-DRBG_WAVE_PROBE=1, scripts/xcd_probe.py): per wave of the direct-mode
+// kernel, its start / end on the constant 100 MHz clock (s_memrealtime) and on the shader clock
+// (s_memtime), its XCC_ID and task count: three plain 16 B stores at the wave's end -- nothing per
+// task, no atomics, so the kernel runs at production speed.
+#if RBG_WAVE_PROBE
+__device__ uint4 g_probe[3 * 16384];
+__device__ __forceinline__ void probe_store(uint64_t r0, uint64_t m0, uint32_t ntask) {
+  const uint64_t r1 = __builtin_amdgcn_s_memrealtime(), m1 = __builtin_amdgcn_s_memtime();
+  uint32_t xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  const uint32_t wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (lane_id() == 0 && wid < 16384) {
+    g_probe[3 * wid] = make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32));
+    g_probe[3 * wid + 1] = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)(m1 >> 32));
+    g_probe[3 * wid + 2] = make_uint4(xcc, ntask, 1u, 0u);
+  }
+}
+#endif
+
 #if RBG_STAMPS
 __device__ unsigned long long g_stamp[20];
 __device__ uint4 g_wave[16384];  // per wave: start, end (realtime), XCC_ID, HW_ID
@@ -547,6 +566,9 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
     // the records are read back through the scalar cache (a fresh line per wave region: no
     // other wave writes it, and the scalar cache holds nothing of it yet)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores are in the L2 the scalar loads read
+#if RBG_WAVE_PROBE
+    const uint64_t pr0 = __builtin_amdgcn_s_memrealtime(), pm0 = __builtin_amdgcn_s_memtime();
+#endif
     uint32_t k = 0;
     PTask cur = load_task(mine, 0);
     for (;;) {
@@ -565,6 +587,9 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
       k++;
       cur = nxt;
     }
+#if RBG_WAVE_PROBE
+    probe_store(pr0, pm0, k + 1);
+#endif
     return;
   }
   PTask cur = load_task(tasks, t);
@@ -627,7 +652,24 @@ static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_
                      PwDirect{});
 }
 
-#if RBG_STAMPS
+#if RBG_WAVE_PROBE
+void debug_stamps(uint64_t* out20, bool reset) {
+  (void)hipDeviceSynchronize();
+  for (int i = 0; i < 20; i++) out20[i] = 0;
+  if (const char* f = getenv("RBG_WAVE_DUMP")) {
+    static uint4 h[3 * 16384];
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_probe), sizeof(h), 0, hipMemcpyDeviceToHost);
+    if (FILE* fp = fopen(f, "ab")) {
+      fwrite(h, sizeof(h), 1, fp);
+      fclose(fp);
+    }
+  }
+  if (reset) {
+    static uint4 z[3 * 16384];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_probe), z, sizeof(z), 0, hipMemcpyHostToDevice);
+  }
+}
+#elif RBG_STAMPS
 void debug_stamps(uint64_t* out20, bool reset) {
   (void)hipDeviceSynchronize();
   (void)hipMemcpyFromSymbol(out20, HIP_SYMBOL(g_stamp), 20 * 8, 0, hipMemcpyDeviceToHost);
