@@ -95,6 +95,19 @@ enum { RBG_WIDE_AND = 0, RBG_WIDE_OR = 1, RBG_WIDE_XOR = 2, RBG_WIDE_AND_ITER = 
  * A result container of more than 2047 runs is kept as such; these calls synchronise the stream
  * (the run arena is checked after the op). */
        RBG_WIDE_BUFFER_AND = 13, RBG_WIDE_BUFFER_NAIVE_AND = 14, RBG_WIDE_BUFFER_AND_ITER = 15 };
+/* range-restricted aggregations, RB/RoaringBitmap.java: every input through selectRangeWithoutCopy
+ * (:3160-3214: keys outside [rangeStart >> 16, (rangeEnd - 1) >> 16] dropped, the first / last key's
+ * container cut by Container.remove -- A stays A, B becomes A at <= 4096 values, R stays R with its runs
+ * clipped -- and emptied ones dropped), then
+ *   RBG_RANGE_AND     and(Iterator, rangeStart, rangeEnd) :1308-1316 -> FastAggregation.and(Iterator)
+ *   RBG_RANGE_OR      or(Iterator, rangeStart, rangeEnd) :2536-2543 -> FastAggregation.or(Iterator)
+ *   RBG_RANGE_XOR     xor(Iterator, rangeStart, rangeEnd) :3359-3365 -> FastAggregation.xor(Iterator)
+ *   RBG_RANGE_ANDNOT  andNot(x1, x2, rangeStart, rangeEnd) :1396-1404 (n == 2)
+ * rangeSanityCheck (:204-213): rangeStart in [0, 2^32 - 1], rangeEnd in [0, 2^32], else
+ * RBG_ERR_ILLEGAL_ARGUMENT; rangeEnd <= rangeStart gives the empty bitmap. */
+enum { RBG_RANGE_AND = 0, RBG_RANGE_OR = 1, RBG_RANGE_XOR = 2, RBG_RANGE_ANDNOT = 3 };
+int rbg_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int64_t range_start,
+                 int64_t range_end, rbg_buffer* out);
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
 
@@ -231,6 +244,9 @@ int rbg_ctx_synth(rbg_ctx* ctx, int kind, uint64_t seed, size_t n, int key_lo, i
 /* Drops a batch.  Its device buffers (up to 2 GiB per context, none above 1 GiB) are kept for
  * reuse by later batches of the context and freed with it (rbg_ctx_destroy). */
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch);
+/* selectRangeWithoutCopy of every bitmap of a key-major batch into a new batch (the first step of the
+ * RBG_RANGE_* ops, on the device; synchronous: one read-back of the new batch's container counts). */
+int rbg_ctx_select_range(rbg_ctx* ctx, int32_t batch, int64_t range_start, int64_t range_end, int32_t* out_batch);
 /* RoaringBitmap.runOptimize() (RB/RoaringBitmap.java:2764-2774) applied on the device to
  * every bitmap of a batch; the result is a new batch (same bitmaps, keys and order).
  * answers (n bitmaps, nullable) receives runOptimize's boolean per bitmap.  Also backs

@@ -1435,6 +1435,88 @@ Bitmap buf_and(const std::vector<const Bitmap*>& bms, const int* ids) {
   return buf_naive_and(bms, ids);
 }
 
+// ---------------------------------------------------------------------------
+// Range-restricted aggregations (RB/RoaringBitmap.java:1308-1336 and, 1396-1423 andNot, 2536-2557 or,
+// 3359-3379 xor): every input through the private static selectRangeWithoutCopy (:3160-3214), then the
+// unrestricted op.
+// ---------------------------------------------------------------------------
+// Container.remove(begin, end): the values of [begin, end) removed.  ArrayContainer.remove / iremove
+// (RB/ArrayContainer.java:1039-1061, 759-780) stay arrays; BitmapContainer.remove / iremove
+// (RB/BitmapContainer.java:1166-1181, 788-802) become arrays at <= 4096 values; RunContainer.remove
+// = clone().iremove (RB/RunContainer.java:2032-2035, 1553-...) stays a run container, its runs clipped.
+// end == begin: unchanged (remove returns a clone, iremove this).
+static Ctr c_remove_range(const Ctr& c, int begin, int end) {
+  if (end == begin) return c;
+  if (c.kind == ARRAY) {
+    std::vector<uint16_t> v;
+    for (uint16_t x : c.vals)
+      if ((int)x < begin || (int)x >= end) v.push_back(x);
+    return make_array(std::move(v));
+  }
+  if (c.kind == BITMAP) {
+    Ctr b = c;
+    b.card -= card_in_range(b.words, begin, end);
+    reset_range(b.words, begin, end);
+    if (b.card <= kArrayMax) return bitmap_to_array(b);
+    return b;
+  }
+  std::vector<uint16_t> pairs;
+  for (int r = 0; r < c.nruns(); r++) {
+    const int s = c.vals[2 * r], e = s + c.vals[2 * r + 1];  // inclusive
+    if (s < begin) {
+      const int e1 = std::min(e, begin - 1);
+      pairs.push_back((uint16_t)s);
+      pairs.push_back((uint16_t)(e1 - s));
+    }
+    if (e >= end) {
+      const int s1 = std::max(s, end);
+      pairs.push_back((uint16_t)s1);
+      pairs.push_back((uint16_t)(e - s1));
+    }
+  }
+  const int n = (int)pairs.size() / 2;
+  return make_run(std::move(pairs), n);
+}
+
+// selectRangeWithoutCopy(RoaringBitmap, rangeStart, rangeEnd): the containers of the keys inside the
+// range as they are, the first key's container through remove(0, lbStart), the last key's through
+// remove(lbLast + 1, 65536) (one key: both), empty ones dropped
+Bitmap select_range(const Bitmap& b, uint64_t start, uint64_t end) {
+  Bitmap ans;
+  if (end <= start) return ans;
+  const int hbs = (int)(start >> 16), lbs = (int)(start & 0xFFFF);
+  const int hbl = (int)((end - 1) >> 16), lbl = (int)((end - 1) & 0xFFFF);
+  for (size_t i = 0; i < b.size(); i++) {
+    const int k = b.keys[i];
+    if (k < hbs || k > hbl) continue;
+    Ctr c = b.ctrs[i];
+    if (k == hbs) c = c_remove_range(c, 0, lbs);
+    if (k == hbl) c = c_remove_range(c, lbl + 1, 65536);
+    if (!c.empty()) {
+      ans.keys.push_back((uint16_t)k);
+      ans.ctrs.push_back(std::move(c));
+    }
+  }
+  return ans;
+}
+
+// op 0: and(Iterator, start, end) -> FastAggregation.and(Iterator) = naive_and(Iterator) (:304-313);
+// 1: or -> FastAggregation.or(Iterator) = naive_or; 2: xor -> FastAggregation.xor(Iterator) = naive_xor
+Bitmap range_aggregate(int op, const std::vector<const Bitmap*>& bms, uint64_t start, uint64_t end) {
+  std::vector<Bitmap> sel;
+  sel.reserve(bms.size());
+  for (const Bitmap* b : bms) sel.push_back(select_range(*b, start, end));
+  std::vector<const Bitmap*> ptrs;
+  for (const Bitmap& b : sel) ptrs.push_back(&b);
+  if (op == 0) return fa_and_iter(ptrs);
+  if (op == 1) return fa_or(ptrs);
+  return fa_xor(ptrs);
+}
+
+Bitmap op_andnot_range(const Bitmap& x1, const Bitmap& x2, uint64_t start, uint64_t end) {
+  return op_andnot(select_range(x1, start, end), select_range(x2, start, end));
+}
+
 // key-bitset intersection shared by workShyAnd / workShyAndCardinality
 static std::vector<uint16_t> common_keys(const std::vector<const Bitmap*>& bms) {
   std::vector<uint64_t> words(1024, 0);

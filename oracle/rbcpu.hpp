@@ -134,6 +134,10 @@ Bitmap buf_or_mutable(const std::vector<const Bitmap*>& bms);        // BufferFa
 Bitmap buf_and(const std::vector<const Bitmap*>& bms, const int* ids);        // and(Immutable...) :28-56
 Bitmap buf_naive_and(const std::vector<const Bitmap*>& bms, const int* ids);  // naive_and(Immutable...) :347-369
 Bitmap buf_and_iter(const std::vector<const Bitmap*>& bms);  // naive_and(Iterator) :383-396, (Mutable...) :407-416
+// range-restricted aggregations, RB/RoaringBitmap.java (selectRangeWithoutCopy, then the op)
+Bitmap select_range(const Bitmap& b, uint64_t start, uint64_t end);
+Bitmap range_aggregate(int op, const std::vector<const Bitmap*>& bms, uint64_t start, uint64_t end);  // 0 and 1 or 2 xor
+Bitmap op_andnot_range(const Bitmap& x1, const Bitmap& x2, uint64_t start, uint64_t end);  // :1396-1423
 Bitmap fa_horizontal_or(const std::vector<const Bitmap*>& bms);      // FastAggregation.horizontal_or :124-231
 Bitmap fa_horizontal_xor(const std::vector<const Bitmap*>& bms);     // :243-289
 Bitmap fa_priorityqueue_or(const std::vector<const Bitmap*>& bms);   // :733-781

@@ -116,6 +116,28 @@ int rbo_wide(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, c
   return ERR_ARG;
 }
 
+// RoaringBitmap.and / or / xor(Iterator, rangeStart, rangeEnd) (op 0 / 1 / 2) and andNot(x1, x2,
+// rangeStart, rangeEnd) (op 3, n == 2): RB/RoaringBitmap.java:1308-1336, 2536-2557, 3359-3379, 1396-1423.
+// rangeSanityCheck (:204-213) -> ERR_ARG.
+int rbo_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int64_t start, int64_t end,
+                 uint8_t** out, size_t* out_len) {
+  if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll) return ERR_ARG;
+  std::vector<Bitmap> bms;
+  std::vector<const Bitmap*> ptrs;
+  int st = load_many(bufs, lens, n, &bms, &ptrs);
+  if (st) return st;
+  if (op == 3) {
+    if (n != 2) return ERR_ARG;
+    return emit(op_andnot_range(bms[0], bms[1], (uint64_t)start, (uint64_t)end), out, out_len);
+  }
+  if (op == 4) {  // selectRangeWithoutCopy alone (n == 1)
+    if (n != 1) return ERR_ARG;
+    return emit(select_range(bms[0], (uint64_t)start, (uint64_t)end), out, out_len);
+  }
+  if (op < 0 || op > 2) return ERR_ARG;
+  return emit(range_aggregate(op, ptrs, (uint64_t)start, (uint64_t)end), out, out_len);
+}
+
 // RoaringBitmap.getLongSizeInBytes of a serialized bitmap (RB/RoaringBitmap.java:2212-2219)
 int64_t rbo_long_size(const uint8_t* a, size_t an) {
   Bitmap b;

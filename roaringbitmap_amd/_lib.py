@@ -24,6 +24,7 @@ WIDE_OP = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_
            "priorityqueue_or": 11, "priorityqueue_xor": 12, "buffer_and": 13, "buffer_naive_and": 14,
            "buffer_and_iter": 15}
 WIDE_CARD_OP = {"and": 0, "or": 1}
+RANGE_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3}
 
 
 class rbg_buffer(ctypes.Structure):
@@ -31,7 +32,7 @@ class rbg_buffer(ctypes.Structure):
 
 
 EXPORTED = [
-    "rbg_pairwise", "rbg_pairwise_card", "rbg_wide", "rbg_wide_card", "rbg_batch_and_card", "rbg_free",
+    "rbg_pairwise", "rbg_pairwise_card", "rbg_wide", "rbg_wide_card", "rbg_range_op", "rbg_ctx_select_range", "rbg_batch_and_card", "rbg_free",
     "rbg_set_devices", "rbg_last_error", "rbg_version", "rbg_trim", "rbg_pool_evictions", "rbg_from_values", "rbg_run_optimize",
     "rbg_to_values", "rbg_inspect", "rbg_ctx_create", "rbg_ctx_destroy", "rbg_ctx_stream", "rbg_ctx_sync",
     "rbg_ctx_load", "rbg_ctx_synth", "rbg_ctx_release", "rbg_ctx_batch_stats", "rbg_ctx_batch_fetch",
@@ -65,6 +66,8 @@ def _declare(L):
     L.rbg_pairwise_inplace.argtypes = [ctypes.c_int, u8p, sz, u8p, sz, ctypes.c_int, buf]
     L.rbg_wide.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), P(i32), sz, buf]
     L.rbg_wide_card.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), sz, P(i32)]
+    L.rbg_range_op.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), sz, ctypes.c_int64, ctypes.c_int64, buf]
+    L.rbg_ctx_select_range.argtypes = [vp, i32, ctypes.c_int64, ctypes.c_int64, P(i32)]
     L.rbg_batch_and_card.argtypes = [sz, P(ctypes.c_char_p), P(sz), P(ctypes.c_char_p), P(sz), P(i32)]
     L.rbg_free.argtypes = [buf]
     L.rbg_free.restype = None

@@ -194,6 +194,7 @@ struct Ctx {
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   DevBuf order;                     // horizontal_*: chain order of every key segment
   DevBuf ro_info, ro_size, ro_part, ro_flags;  // runOptimize scratch (kept: no allocation per call)
+  DevBuf rs_card, rs_keep, rs_bm;              // range selection scratch (with ro_info / ro_size / ro_part)
   // device buffers of released batches kept for the next batch of a similar size (hipMalloc /
   // hipFree of a 0.36 GB payload cost more than runOptimize's kernels); bounded by kPoolMax
   std::vector<DevBuf> pool;
@@ -2083,6 +2084,45 @@ int rbg_wide(int op, const uint8_t* const* bufs, const size_t* lens, const int32
   return ctx_fetch(c, out);
 }
 
+static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int32_t* out_id);
+
+int rbg_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int64_t range_start,
+                 int64_t range_end, rbg_buffer* out) {
+  if (!out || op < RBG_RANGE_AND || op > RBG_RANGE_ANDNOT || (op == RBG_RANGE_ANDNOT && n != 2))
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  if (op == RBG_RANGE_ANDNOT) {  // andNot(x1, x2, start, end): both operands selected, then andNot
+    int32_t ids[2], sel[2];
+    CHK(ctx_load_separate(c, bufs, lens, 2, ids));
+    g.ids = {ids[0], ids[1]};
+    for (int i = 0; i < 2; i++) {
+      CHK(ctx_select_range(c, ids[i], range_start, range_end, &sel[i]));
+      g.ids.push_back(sel[i]);
+    }
+    CHK(ctx_pairwise(c, OP_ANDNOT, sel[0], 0, sel[1], 0, false));
+    return ctx_fetch(c, out);
+  }
+  int32_t id, sel;
+  CHK(ctx_load(c, bufs, lens, n, &id));
+  g.ids.push_back(id);
+  CHK(ctx_select_range(c, id, range_start, range_end, &sel));
+  g.ids.push_back(sel);
+  // and -> FastAggregation.and(Iterator) = naive_and(Iterator); or / xor -> naive_or / naive_xor
+  const int wop = op == RBG_RANGE_AND ? RBG_WIDE_AND_ITER : op == RBG_RANGE_OR ? RBG_WIDE_OR : RBG_WIDE_XOR;
+  int hc;
+  bool hv;
+  CHK(ctx_wide(c, wop, sel, 0, 65536, nullptr, false, &hc, &hv));
+  return ctx_fetch(c, out);
+}
+
+int rbg_ctx_select_range(rbg_ctx* ctx, int32_t batch, int64_t range_start, int64_t range_end, int32_t* out_batch) {
+  if (!ctx || !out_batch) return RBG_ERR_ILLEGAL_ARGUMENT;
+  CHK(enter(&ctx->c));
+  return ctx_select_range(&ctx->c, batch, range_start, range_end, out_batch);
+}
+
 int rbg_wide_card(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out) {
   if (!out || op < 0 || op > 1) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
@@ -3134,6 +3174,91 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
     CHK(ensure_stats(c, &b));
     for (size_t i = 0; i < n; i++) answers[i] = b.h_has_run[i];
   }
+  return RBG_OK;
+}
+
+// selectRangeWithoutCopy (RB/RoaringBitmap.java:3160-3214) of every bitmap of a key-major batch into a
+// new batch, on the device (runopt.hip: k_rsel_plan, two scans, k_rsel_write, the key CSR); one host
+// read-back for the new batch's container counts.  rangeSanityCheck (:204-213) first.
+static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int32_t* out_id) {
+  if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll) {
+    set_err("rangeStart=" + std::to_string(start) + " should be in [0, 0xffffffff], rangeEnd=" + std::to_string(end) +
+            " in [0, 0xffffffff + 1]");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  Batch* a;
+  CHK(get_batch(c, id, &a));
+  if (!a->key_major || a->packed) {
+    set_err("range selection needs a key-major batch with slot-aligned payloads");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  hipStream_t s = c->stream;
+  const size_t C = a->n_ctr, n = a->n_bm;
+  RselArgs ra{1, 0, 0, 0};  // end <= start: no key is kept
+  if (end > start) {
+    ra.hbs = (int)(start >> 16);
+    ra.lbs = (int)(start & 0xFFFF);
+    ra.hbl = (int)((end - 1) >> 16);
+    ra.lbl = (int)((end - 1) & 0xFFFF);
+  }
+  CHK(c->ro_info.ensure(4 * C + 16));
+  CHK(c->ro_size.ensure(8 * C + 16));
+  CHK(c->ro_part.ensure(8 * (scan_parts(std::max<size_t>(C, 1)) + 1)));
+  CHK(c->rs_card.ensure(4 * C + 16));
+  CHK(c->rs_keep.ensure(8 * C + 16));
+  CHK(c->rs_bm.ensure(16 * n + 64 + 16));  // per bitmap: kept containers, cardinality; then the totals
+  const int32_t bid = new_batch(c);
+  Batch& b = *c->batches[bid];
+  BatchGuard guard{c, {bid}};  // dropped unless the selection completes
+  CHK(pool_take(c, b.desc, sizeof(CDesc) * C + 16));
+  CHK(pool_take(c, b.payload, a->payload_bytes + 64));
+  CHK(b.keys.ensure(2 * C + 16));
+  CHK(b.bm.ensure(4 * C + 16));
+  CHK(b.key_off.ensure(4 * (kMaxKeys + 1)));
+  CHK(b.bm_off.ensure(4 * (n + 1)));
+  unsigned long long* bm_cnt = c->rs_bm.as<unsigned long long>();
+  unsigned long long* bm_card = bm_cnt + n;
+  unsigned long long* tot = bm_cnt + 2 * n;  // #A, #B, #R, big bytes, then the two scan totals
+  HIPCHK(hipMemsetAsync(c->rs_bm.p, 0, 16 * n + 64, s));
+  launch_rsel_plan(s, a->desc.as<CDesc>(), a->bm.as<uint32_t>(), a->payload.as<uint8_t>(), C, ra,
+                   c->ro_info.as<uint32_t>(), c->rs_card.as<uint32_t>(), c->ro_size.as<uint64_t>(),
+                   c->rs_keep.as<uint64_t>(), bm_cnt, bm_card, tot);
+  launch_exclusive_scan(s, c->ro_size.as<uint64_t>(), c->ro_size.as<uint64_t>(), C, c->ro_part.as<uint64_t>(),
+                        reinterpret_cast<uint64_t*>(tot + 4));
+  launch_exclusive_scan(s, c->rs_keep.as<uint64_t>(), c->rs_keep.as<uint64_t>(), C, c->ro_part.as<uint64_t>(),
+                        reinterpret_cast<uint64_t*>(tot + 5));
+  launch_rsel_write(s, a->desc.as<CDesc>(), a->bm.as<uint32_t>(), a->payload.as<uint8_t>(), C, ra,
+                    c->ro_info.as<uint32_t>(), c->rs_card.as<uint32_t>(), c->ro_size.as<uint64_t>(),
+                    c->rs_keep.as<uint64_t>(), b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.bm.as<uint32_t>(),
+                    b.payload.as<uint8_t>());
+  HIPCHK(hipGetLastError());
+  std::vector<unsigned long long> h(2 * n + 8);
+  HIPCHK(hipMemcpyAsync(h.data(), c->rs_bm.p, 8 * (2 * n + 6), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const unsigned long long* t = h.data() + 2 * n;
+  const uint64_t C2 = t[5];
+  launch_dec_key_off(s, b.keys.as<uint16_t>(), C2, b.key_off.as<uint32_t>());
+  b.n_bm = n;
+  b.n_ctr = C2;
+  b.key_major = true;
+  for (int k = 0; k < 3; k++) b.n_kind[k] = (int64_t)t[k];
+  b.max_ser = t[3];
+  b.payload_bytes = t[4];
+  b.h_bm_off.assign(n + 1, 0);
+  b.h_bm_nctr.resize(n);
+  b.h_bm_card.resize(n);
+  for (size_t i = 0; i < n; i++) {
+    b.h_bm_nctr[i] = (uint32_t)h[i];
+    b.h_bm_off[i + 1] = b.h_bm_off[i] + (uint32_t)h[i];
+    b.h_bm_card[i] = (int64_t)h[n + i];
+    b.long_card += (int64_t)h[n + i];
+  }
+  HIPCHK(hipMemcpyAsync(b.bm_off.p, b.h_bm_off.data(), 4 * (n + 1), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));  // the host vector above goes out of scope
+  HIPCHK(hipGetLastError());
+  b.live = true;
+  guard.ids.clear();
+  *out_id = bid;
   return RBG_OK;
 }
 

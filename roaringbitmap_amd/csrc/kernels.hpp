@@ -390,6 +390,19 @@ void launch_runopt_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, co
 void launch_runopt_write(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, const uint32_t* info,
                          const uint64_t* off, CDesc* out_desc, uint8_t* out_payload);
 
+// runopt.hip: selectRangeWithoutCopy of every bitmap of a batch (range-restricted aggregations): the
+// range's first / last key and low bits (lbs..lbl kept on those keys)
+struct RselArgs {
+  int hbs, lbs, hbl, lbl;
+};
+void launch_rsel_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
+                      RselArgs ra, uint32_t* info, uint32_t* card, uint64_t* size, uint64_t* keep,
+                      unsigned long long* bm_cnt, unsigned long long* bm_card, unsigned long long* totals);
+void launch_rsel_write(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
+                       RselArgs ra, const uint32_t* info, const uint32_t* card, const uint64_t* off,
+                       const uint64_t* idx, CDesc* out_desc, uint16_t* out_keys, uint32_t* out_bm,
+                       uint8_t* out_payload);
+
 // decode.hip: portable-format decode on the device
 enum DecErr : uint32_t {
   DEC_OK = 0,

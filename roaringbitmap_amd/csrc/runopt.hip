@@ -264,4 +264,242 @@ void launch_runopt_write(hipStream_t s, const CDesc* desc, const uint8_t* payloa
                      out_payload);
 }
 
+// ---------------------------------------------------------------------------
+// selectRangeWithoutCopy (RB/RoaringBitmap.java:3160-3214) of every bitmap of a batch, into a new batch:
+// the input of the range-restricted aggregations and(Iterator, start, end) :1308-1316, or :2536-2543,
+// xor :3359-3365 and andNot(x1, x2, start, end) :1396-1404.  Keys outside [hbs, hbl] go; the first key
+// loses [0, lbs), the last (lbl, 65535] through Container.remove (A stays A, B becomes A at <= 4096
+// values, R stays R with its runs clipped: RB/ArrayContainer.java:1039-1061, RB/BitmapContainer.java:
+// 1166-1181, RB/RunContainer.java:2032-2035); a container left empty goes too.
+// ---------------------------------------------------------------------------
+// the bits of owned word k (chunk i, word j) inside [lo, hi]
+__device__ __forceinline__ uint64_t range_mask_word(int i, int j, int lo, int hi) {
+  const int w = 128 * i + 2 * lane_id() + j;
+  const int b0 = 64 * w, b1 = b0 + 63;
+  if (b1 < lo || b0 > hi) return 0;
+  uint64_t m = ~0ull;
+  if (lo > b0) m &= ~0ull << (lo - b0);
+  if (hi < b1) m &= ~0ull >> (b1 - hi);
+  return m;
+}
+
+// the cut [lo, hi] of container i (cut = false: the key lies inside the range, unchanged)
+__device__ __forceinline__ void rsel_bounds(const CDesc& d, const RselArgs& ra, bool* keep_key, bool* cut, int* lo,
+                                            int* hi) {
+  const int k = d.key;
+  *keep_key = k >= ra.hbs && k <= ra.hbl;
+  *lo = k == ra.hbs ? ra.lbs : 0;
+  *hi = k == ra.hbl ? ra.lbl : 65535;
+  *cut = *keep_key && (*lo > 0 || *hi < 65535);
+}
+
+// A: values [first, first + cnt) lie in [lo, hi] (the array is sorted)
+__device__ __forceinline__ void array_window(const uint16_t* v, int card, int lo, int hi, int* first, int* cnt) {
+  int below = 0, in = 0;
+  for (int x = lane_id(); x < card; x += 64) {
+    const int y = v[x];
+    below += y < lo;
+    in += y >= lo && y <= hi;
+  }
+  *first = (int)uni((uint32_t)wave_sum_i(below));
+  *cnt = (int)uni((uint32_t)wave_sum_i(in));
+}
+
+// R: runs overlapping [lo, hi] and their clipped cardinality
+__device__ __forceinline__ void run_window(const uint8_t* slot, int lo, int hi, int* nr_out, int* card_out) {
+  const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
+  const uint32_t* pr = reinterpret_cast<const uint32_t*>(slot + 4);
+  int c = 0, n = 0;
+  for (int r = lane_id(); r < nr; r += 64) {
+    const uint32_t p = pr[r];
+    const int s = (int)(p & 0xFFFF), e = s + (int)(p >> 16);
+    const int s1 = max(s, lo), e1 = min(e, hi);
+    if (s1 <= e1) {
+      n++;
+      c += e1 - s1 + 1;
+    }
+  }
+  *nr_out = (int)uni((uint32_t)wave_sum_i(n));
+  *card_out = (int)uni((uint32_t)wave_sum_i(c));
+}
+
+// info[i] = kind | keep << 2 | cut << 3; card[i], size[i] (new slot bytes), keep[i]; per bitmap kept
+// containers and cardinality; totals = {#A, #B, #R, serialized bytes of containers above 8194 B}
+__global__ __launch_bounds__(256) void k_rsel_plan(const CDesc* __restrict__ desc, const uint32_t* __restrict__ bm,
+                                                   const uint8_t* __restrict__ payload, uint64_t n, RselArgs ra,
+                                                   uint32_t* __restrict__ info, uint32_t* __restrict__ ncard,
+                                                   uint64_t* __restrict__ size, uint64_t* __restrict__ keepv,
+                                                   unsigned long long* __restrict__ bm_cnt,
+                                                   unsigned long long* __restrict__ bm_card,
+                                                   unsigned long long* __restrict__ totals) {
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  unsigned long long cnt[3] = {0, 0, 0}, big = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
+    const CDesc d = desc[i];
+    const uint8_t* slot = payload + d.slot;
+    bool keep_key, cut;
+    int lo, hi;
+    rsel_bounds(d, ra, &keep_key, &cut, &lo, &hi);
+    int kind = d.kind, card = keep_key ? (int)d.card : 0;
+    uint32_t len = 0;
+    if (keep_key && !cut) {
+      len = kind == DK_A ? 2u * card : kind == DK_B ? 8192u : 2u + 4u * *reinterpret_cast<const uint16_t*>(slot + 2);
+    } else if (cut && kind == DK_A) {
+      int first;
+      array_window(reinterpret_cast<const uint16_t*>(slot), card, lo, hi, &first, &card);
+      len = 2u * card;
+    } else if (cut && kind == DK_B) {
+      WCtr x;
+      w_load_bitmap(slot, x);
+#pragma unroll
+      for (int k = 0; k < 16; k++) x.w[k] &= range_mask_word(k >> 1, k & 1, lo, hi);
+      card = w_card(x);
+      kind = by_card(card);
+      len = kind == DK_A ? 2u * card : 8192u;
+    } else if (cut) {  // R
+      int nr;
+      run_window(slot, lo, hi, &nr, &card);
+      len = 2u + 4u * nr;
+    }
+    const bool keep = keep_key && card > 0;
+    if (lane_id() == 0) {
+      info[i] = (uint32_t)kind | (keep ? 4u : 0u) | (cut ? 8u : 0u);
+      ncard[i] = (uint32_t)card;
+      size[i] = keep ? slot_size_of(kind, len) : 0;
+      keepv[i] = keep ? 1 : 0;
+      if (keep) {
+        atomicAdd(&bm_cnt[bm[i]], 1ull);
+        atomicAdd(&bm_card[bm[i]], (unsigned long long)card);
+      }
+    }
+    if (keep) {
+      cnt[kind]++;
+      if (len > 8194) big += len;
+    }
+  }
+  __shared__ unsigned long long wsum[4][4];
+  if (lane_id() == 0) {
+    wsum[threadIdx.x >> 6][0] = cnt[0];
+    wsum[threadIdx.x >> 6][1] = cnt[1];
+    wsum[threadIdx.x >> 6][2] = cnt[2];
+    wsum[threadIdx.x >> 6][3] = big;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const unsigned long long v = wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] +
+                                 wsum[3][threadIdx.x];
+    if (v) atomicAdd(&totals[threadIdx.x], v);
+  }
+}
+
+// kept container i -> index idx[i], slot at off[i] of the new batch
+__global__ __launch_bounds__(256) void k_rsel_write(const CDesc* __restrict__ desc, const uint32_t* __restrict__ bm,
+                                                    const uint8_t* __restrict__ payload, uint64_t n, RselArgs ra,
+                                                    const uint32_t* __restrict__ info,
+                                                    const uint32_t* __restrict__ ncard,
+                                                    const uint64_t* __restrict__ off, const uint64_t* __restrict__ idx,
+                                                    CDesc* __restrict__ out_desc, uint16_t* __restrict__ out_keys,
+                                                    uint32_t* __restrict__ out_bm, uint8_t* __restrict__ out_payload) {
+  __shared__ __align__(16) uint32_t lds_all[4][2048];
+  uint32_t* lds = lds_all[threadIdx.x >> 6];
+  const int lane = lane_id();
+  const uint64_t nw = (uint64_t)gridDim.x * 4;
+  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
+    const uint32_t inf = info[i];
+    if (!(inf & 4)) continue;  // wave-uniform
+    const CDesc d = desc[i];
+    const int kind = (int)(inf & 3);
+    const uint32_t card = ncard[i];
+    const uint64_t j = idx[i], o = off[i];
+    const uint8_t* slot = payload + d.slot;
+    uint8_t* dst = out_payload + o;
+    if (!(inf & 8)) {  // inside the range: the slot as it is
+      const uint32_t len = kind == DK_A   ? 2u * card
+                           : kind == DK_B ? 8192u
+                                          : 2u + 4u * *reinterpret_cast<const uint16_t*>(slot + 2);
+      const uint32_t nvec = (uint32_t)(slot_size_of(kind, len) >> 4);
+      const uint4* sv = reinterpret_cast<const uint4*>(slot);
+      uint4* dv = reinterpret_cast<uint4*>(dst);
+      for (uint32_t q = lane; q < nvec; q += 64) dv[q] = sv[q];
+    } else {
+      bool keep_key, cut;
+      int lo, hi;
+      rsel_bounds(d, ra, &keep_key, &cut, &lo, &hi);
+      if (d.kind == DK_A) {  // the window of the sorted values, padded to 16 B with the last one
+        int first, cnt;
+        array_window(reinterpret_cast<const uint16_t*>(slot), (int)d.card, lo, hi, &first, &cnt);
+        const uint16_t* v = reinterpret_cast<const uint16_t*>(slot) + first;
+        uint16_t* w = reinterpret_cast<uint16_t*>(dst);
+        const int padded = (int)((2u * card + 15) & ~15u) / 2;
+        for (int x = lane; x < padded; x += 64) w[x] = v[min(x, (int)card - 1)];
+      } else if (d.kind == DK_B) {
+        WCtr x;
+        w_load_bitmap(slot, x);
+#pragma unroll
+        for (int k = 0; k < 16; k++) x.w[k] &= range_mask_word(k >> 1, k & 1, lo, hi);
+        if (kind == DK_B) {
+          w_store_bitmap(dst, x);
+        } else {
+          w_stage(DK_A, x, (int)card, lds);
+          uint16_t* st = reinterpret_cast<uint16_t*>(lds);
+          const uint32_t padded = (2u * card + 15) & ~15u;
+          const uint16_t last = st[card - 1];
+          for (uint32_t q = card + lane; q < padded / 2; q += 64) st[q] = last;
+          wsync();
+          copy_lds_to_global<64>(dst, lds, padded, lane);
+          wsync();
+        }
+      } else {  // R: the overlapping runs, clipped, in order
+        const int nr = *reinterpret_cast<const uint16_t*>(slot + 2);
+        const uint32_t* pr = reinterpret_cast<const uint32_t*>(slot + 4);
+        uint32_t* out = reinterpret_cast<uint32_t*>(dst + 4);
+        int base = 0;
+        for (int r0 = 0; r0 < nr; r0 += 64) {
+          const int r = r0 + lane;
+          uint32_t np = 0;
+          int ov = 0;
+          if (r < nr) {
+            const uint32_t p = pr[r];
+            const int s = (int)(p & 0xFFFF), e = s + (int)(p >> 16);
+            const int s1 = max(s, lo), e1 = min(e, hi);
+            ov = s1 <= e1;
+            np = (uint32_t)s1 | ((uint32_t)(e1 - s1) << 16);
+          }
+          int tot;
+          const int pos = base + wave_excl(ov, &tot);
+          if (ov) out[pos] = np;
+          base += tot;
+        }
+        if (lane == 0) {
+          reinterpret_cast<uint16_t*>(dst)[0] = 0;
+          reinterpret_cast<uint16_t*>(dst)[1] = (uint16_t)base;
+        }
+      }
+    }
+    if (lane == 0) {
+      out_desc[j] = CDesc{o, card, d.key, (uint8_t)kind, 0};
+      out_keys[j] = d.key;
+      out_bm[j] = bm[i];
+    }
+  }
+}
+
+void launch_rsel_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
+                      RselArgs ra, uint32_t* info, uint32_t* card, uint64_t* size, uint64_t* keep,
+                      unsigned long long* bm_cnt, unsigned long long* bm_card, unsigned long long* totals) {
+  if (!n) return;
+  const uint64_t g = std::min<uint64_t>((n + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_rsel_plan, dim3((unsigned)g), dim3(256), 0, s, desc, bm, payload, n, ra, info, card, size, keep,
+                     bm_cnt, bm_card, totals);
+}
+void launch_rsel_write(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
+                       RselArgs ra, const uint32_t* info, const uint32_t* card, const uint64_t* off,
+                       const uint64_t* idx, CDesc* out_desc, uint16_t* out_keys, uint32_t* out_bm,
+                       uint8_t* out_payload) {
+  if (!n) return;
+  const uint64_t g = std::min<uint64_t>((n + 3) / 4, 8192);
+  hipLaunchKernelGGL(k_rsel_write, dim3((unsigned)g), dim3(256), 0, s, desc, bm, payload, n, ra, info, card, off, idx,
+                     out_desc, out_keys, out_bm, out_payload);
+}
+
 }  // namespace rbg

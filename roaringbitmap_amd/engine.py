@@ -159,6 +159,13 @@ class Engine:
         check(lib().rbg_ctx_run_optimize(self._ctx, int(batch), ctypes.byref(out), ans))
         return int(out.value), [bool(x) for x in ans[:n]]
 
+    def select_range(self, batch, start, end):
+        """selectRangeWithoutCopy (RB/RoaringBitmap.java:3160-3214) of every bitmap of a batch, on the device
+        -> new batch id (rbg_ctx_select_range)."""
+        out = ctypes.c_int32()
+        check(lib().rbg_ctx_select_range(self._ctx, int(batch), int(start), int(end), ctypes.byref(out)))
+        return int(out.value)
+
     def batch_minmax(self, batch):
         out = (ctypes.c_int32 * 2)()
         check(lib().rbg_ctx_batch_minmax(self._ctx, int(batch), out))

@@ -50,26 +50,54 @@ class _StaticOrInPlace:
         return call
 
 
-def _s_and(x1, x2):
-    """static and(x1, x2), RB/RoaringBitmap.java:377-401; x1.and(x2) in place :1272-1296"""
+def _range_op(op, bitmaps, start, end):
+    """RB/RoaringBitmap.java range-restricted forms: every input through selectRangeWithoutCopy
+    (:3160-3214), then FastAggregation.and / or / xor(Iterator) or andNot (rbg_range_op)."""
+    bufs = [b._buf for b in bitmaps]
+    arr, lens = _lib.buf_array(bufs)
+    b = _lib.rbg_buffer()
+    check(lib().rbg_range_op(_lib.RANGE_OP[op], arr, lens, len(bufs), int(start), int(end), ctypes.byref(b)))
+    return RoaringBitmap(take(b))
+
+
+def _is_range(args):
+    return len(args) == 3 and isinstance(args[0], Iterator) and all(isinstance(x, (int, np.integer)) for x in args[1:])
+
+
+def _s_and(*args):
+    """static and(x1, x2), RB/RoaringBitmap.java:377-401; and(Iterator, rangeStart, rangeEnd) :1308-1316;
+    x1.and(x2) in place :1272-1296"""
+    if _is_range(args):
+        return _range_op("and", list(args[0]), args[1], args[2])
+    x1, x2 = args
     return RoaringBitmap._pair("and", x1, x2)
 
 
 def _s_or(*bitmaps):
-    """static or(x1, x2) (:860-902); any other arity is or(RoaringBitmap...) (:844) = FastAggregation.or;
-    x1.or(x2) in place :2481-2523 (Container.ior's types)"""
+    """static or(x1, x2) (:860-902); or(Iterator, rangeStart, rangeEnd) :2536-2543; any other arity is
+    or(RoaringBitmap...) (:844) = FastAggregation.or; x1.or(x2) in place :2481-2523 (Container.ior's types)"""
+    if _is_range(bitmaps):
+        return _range_op("or", list(bitmaps[0]), bitmaps[1], bitmaps[2])
     if len(bitmaps) == 2:
         return RoaringBitmap._pair("or", bitmaps[0], bitmaps[1])
     return FastAggregation.or_(*bitmaps)
 
 
-def _s_xor(x1, x2):
-    """static xor(x1, x2), :1071-1118; x1.xor(x2) in place :3296-3348"""
+def _s_xor(*args):
+    """static xor(x1, x2), :1071-1118; xor(Iterator, rangeStart, rangeEnd) :3359-3365; x1.xor(x2) in place
+    :3296-3348"""
+    if _is_range(args):
+        return _range_op("xor", list(args[0]), args[1], args[2])
+    x1, x2 = args
     return RoaringBitmap._pair("xor", x1, x2)
 
 
-def _s_andnot(x1, x2):
-    """static andNot(x1, x2), :444-473; x1.andNot(x2) in place :1346-1382"""
+def _s_andnot(*args):
+    """static andNot(x1, x2), :444-473; andNot(x1, x2, rangeStart, rangeEnd) :1396-1404; x1.andNot(x2) in
+    place :1346-1382"""
+    if len(args) == 4:
+        return _range_op("andnot", [args[0], args[1]], args[2], args[3])
+    x1, x2 = args
     return RoaringBitmap._pair("andnot", x1, x2)
 
 

@@ -4,7 +4,7 @@
 set -e
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_fullsize.py \
-  tests/test_gpu_wide.py tests/test_gpu_bsi.py tests/test_gpu_runopt.py > gpurun_out/r5_t2.log 2>&1
+  tests/test_gpu_wide.py tests/test_gpu_bsi.py tests/test_gpu_runopt.py tests/test_gpu_range.py > gpurun_out/r5_t2.log 2>&1
 timeout -k 10 300 python -u scripts/c2_pipe.py > gpurun_out/r5_pipe.txt 2>&1
 timeout -k 10 120 python -u bench.py --only c3u_and --steps 20 --warmup 3 > gpurun_out/r5_shy.txt 2>&1
 timeout -k 10 200 python -u bench.py --only c5 --steps 20 --warmup 3 > gpurun_out/r5_c5.txt 2>&1

@@ -70,6 +70,9 @@ def lib():
                                                       ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                                       ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
         L.rbo_time_bsi_range_sum_parallel.restype = ctypes.c_double
+        L.rbo_range_op.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                   ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64,
+                                   ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -226,6 +229,17 @@ def time_bsi_range_sum_parallel(ebm, slices, lo, hi, threads, reps):
     out = (ctypes.c_int64 * 2)()
     t = lib().rbo_time_bsi_range_sum_parallel(arr, lens, len(slices), lo, hi, threads, reps, out)
     return t, (int(out[0]), int(out[1]))
+
+
+def range_op(op, bufs, start, end) -> bytes:
+    """RoaringBitmap.and / or / xor(Iterator, start, end) ("and" / "or" / "xor") and andNot(x1, x2, start,
+    end) ("andnot", two inputs): RB/RoaringBitmap.java:1308-1336, 2536-2557, 3359-3379, 1396-1423."""
+    arr, lens = _bufs(bufs)
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_range_op({"and": 0, "or": 1, "xor": 2, "andnot": 3, "select": 4}[op], arr, lens, len(bufs), start, end,
+                              ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
 
 
 def long_size(buf) -> int:
