@@ -324,6 +324,36 @@ def _find_container(buf, key):
     return 2, np.frombuffer(buf, dtype="<u2", count=2 * nr, offset=pos + 2)
 
 
+def _keys_of(buf) -> np.ndarray:
+    """the container keys of a portable serialized bitmap (its descriptor table, RB/RoaringArray.java:547-588)"""
+    cookie = int.from_bytes(buf[0:4], "little")
+    if (cookie & 0xFFFF) == 12347:
+        size = (cookie >> 16) + 1
+        dpos = 4 + (size + 7) // 8
+    else:
+        size = int.from_bytes(buf[4:8], "little")
+        dpos = 8
+    return np.frombuffer(buf, dtype="<u2", count=2 * size, offset=dpos)[0::2].astype(np.int64)
+
+
+def _full_containers(keys) -> bytes:
+    """the portable bytes of a bitmap with a full run container (RunContainer.full(), one run 0..65535)
+    at each of the sorted `keys` (RB/RoaringArray.java:896-940 layout)"""
+    import struct
+    n = len(keys)
+    out = bytearray(struct.pack("<I", 12347 | ((n - 1) << 16)))
+    out += bytes([0xFF] * (n // 8)) + (bytes([(1 << (n % 8)) - 1]) if n % 8 else b"")
+    for k in keys:
+        out += struct.pack("<HH", k, 0xFFFF)
+    header = len(out) + (4 * n if n >= 4 else 0)
+    if n >= 4:
+        for i in range(n):
+            out += struct.pack("<I", header + 6 * i)
+    for _ in keys:
+        out += struct.pack("<HHH", 1, 0, 0xFFFF)
+    return bytes(out)
+
+
 def _identity_ids(bitmaps):
     seen = {}
     return [seen.setdefault(id(b), len(seen)) for b in bitmaps]
@@ -412,6 +442,33 @@ class FastAggregation:
         """workShyAnd(long[] buffer, RoaringBitmap...) :356-414"""
         bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
         return _wide("workshy_and", bms)
+
+    @staticmethod
+    def workAndMemoryShyAnd(buffer, *bitmaps):
+        """workAndMemoryShyAnd(long[] buffer, RoaringBitmap...) (RB/FastAggregation.java:522-576).
+
+        workShyAnd's algorithm (its results and types) with two observable differences, kept here:
+        the buffer length is checked (IllegalArgumentException below 1024), and the caller's buffer is
+        the key bitset, which it does not clear first -- a nonzero buffer contributes its bits as
+        keys of the first bitmap (:527-532); a key of those the first bitmap lacks is skipped by the
+        per-key getIndex (:561-564), so it behaves as a full container there.  Afterwards the buffer
+        holds what the reference leaves: all ones once any key survived the key intersection
+        (Arrays.fill(words, -1L) per key, :558), else the (all-zero) intersection."""
+        if buffer is None or len(buffer) < 1024:
+            raise IllegalArgumentException("buffer should have at least 1024 elements.")
+        bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
+        words = np.asarray(buffer[:1024]).astype(np.uint64)
+        garbage = np.nonzero(np.unpackbits(words.view(np.uint8), bitorder="little"))[0]
+        keys = set(garbage.tolist()) | set(_keys_of(bms[0]._buf).tolist())
+        for b in bms[1:]:
+            keys &= set(_keys_of(b._buf).tolist())
+        extra = sorted(set(garbage.tolist()) - set(_keys_of(bms[0]._buf).tolist()))
+        first = bms[0]
+        if extra:  # the first bitmap with full containers at the buffer's own keys (an identity for AND)
+            first = RoaringBitmap._pair("or", bms[0], RoaringBitmap(_full_containers(extra)))
+        out = _wide("workshy_and", [first] + bms[1:])
+        buffer[:1024] = -1 if keys else 0
+        return out
 
     @staticmethod
     def andCardinality(*args) -> int:

@@ -311,3 +311,37 @@ def test_workshy_forms(gpu, seed):
     assert gpu_wide_card("and", bufs) == O.wide_card("and", bufs)
     kinds = {c[0]: c[1] for c in decode(O.wide("workshy_and", bufs))}
     assert kinds[5] == R and kinds[0] == A and 8 not in kinds
+
+
+def test_work_and_memory_shy_and(gpu):
+    """FastAggregation.workAndMemoryShyAnd (RB/FastAggregation.java:522-576): workShyAnd's result with a
+    zeroed buffer; a nonzero buffer adds its bits to the first bitmap's keys (a key the first bitmap
+    lacks is skipped per bitmap, i.e. it acts as a full container); the buffer is left all ones once a
+    key survived the key intersection, else zero."""
+    from roaringbitmap_amd.roaring import _full_containers
+    rb = _rb()
+    rng = np.random.default_rng(21)
+    bufs = [_gen.bitmap(rng, np.arange(10), p_present=0.9) for _ in range(4)]
+    bms = [rb.RoaringBitmap(b) for b in bufs]
+    buf = np.zeros(1024, dtype=np.int64)
+    assert rb.FastAggregation.workAndMemoryShyAnd(buf, *bms).serialize() == O.wide("workshy_and", bufs)
+    assert (buf == -1).all()
+    # a dirty buffer: keys 20 and 3 set; key 20 is in no input, so it cannot survive (n > 1)
+    keys0 = set(O.to_values(bufs[0]) >> 16)
+    common = set.intersection(*[set((O.to_values(b) >> 16).tolist()) for b in bufs[1:]])
+    extra = sorted(k for k in common if k not in keys0)
+    buf = np.zeros(1024, dtype=np.int64)
+    for k in [20] + extra:
+        buf[k >> 6] |= np.int64(1) << np.int64(k & 63)
+    exp_first = O.pairwise("or", bufs[0], _full_containers(extra)) if extra else bufs[0]
+    got = rb.FastAggregation.workAndMemoryShyAnd(buf, *bms).serialize()
+    assert got == O.wide("workshy_and", [exp_first] + bufs[1:])
+    # one input and a dirty buffer: the buffer's keys become full run containers
+    buf = np.zeros(1024, dtype=np.int64)
+    buf[1] = 1  # key 64
+    got = rb.FastAggregation.workAndMemoryShyAnd(buf, bms[0]).serialize()
+    assert got == O.wide("workshy_and", [O.pairwise("or", bufs[0], _full_containers([64]))])
+    # disjoint keys: nothing survives, the buffer is left zero
+    a, b = rb.RoaringBitmap.bitmapOf(1, 2), rb.RoaringBitmap.bitmapOf(1 << 16)
+    buf = np.zeros(1024, dtype=np.int64)
+    assert rb.FastAggregation.workAndMemoryShyAnd(buf, a, b).isEmpty() and (buf == 0).all()

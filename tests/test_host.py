@@ -196,3 +196,10 @@ def test_inplace_same_object_needs_no_device():
         L.check(L.lib().rbg_pairwise_inplace(0, b"\x00" * 12, 12, x, len(x), 1, ctypes.byref(out)))
     L.lib().rbg_trim()
     assert L.lib().rbg_pool_evictions() == 0
+
+
+def test_work_and_memory_shy_and_buffer_check():
+    """FastAggregation.workAndMemoryShyAnd checks the buffer before anything (RB/FastAggregation.java:523-525)."""
+    x = RoaringBitmap.bitmapOf(1, 2, 3)
+    with pytest.raises(IllegalArgumentException):
+        FastAggregation.workAndMemoryShyAnd(np.zeros(100, dtype=np.int64), x, x)
