@@ -41,9 +41,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-# the one-GPU headline step: the op and its serialization as one pipeline (RBG_BENCH_PIPE=0: two calls)
-PIPELINED = os.environ.get("RBG_BENCH_PIPE", "1") != "0"
-PIPE_K = int(os.environ.get("RBG_SER_PIPE", "4"))  # the engine's default key ranges
+# the one-GPU headline step as rbg_ctx_pairwise_serialized (RBG_BENCH_PIPE=1; default: the op, then the
+# serialization -- measured faster than 2-16 pipelined key ranges)
+PIPELINED = os.environ.get("RBG_BENCH_PIPE", "0") != "0"
+PIPE_K = int(os.environ.get("RBG_SER_PIPE", "4"))  # key ranges when RBG_BENCH_PIPE=1
 METRIC = "wide-OR/pairwise-AND input GB/s + % of HBM peak at 1/2/4/8 MI355X"
 
 

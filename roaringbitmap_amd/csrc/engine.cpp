@@ -883,7 +883,7 @@ static int pairwise_pipelined(Ctx* c, int op, int K, PwDirect pd, Batch* A, Batc
 // key ranges of a pipelined op + serialization (RBG_SER_PIPE, default 4; 1 = op, then serialization)
 static int pipe_ranges() {
   const char* e = getenv("RBG_SER_PIPE");  // read per call (tests vary it)
-  return e ? std::max(1, atoi(e)) : 4;
+  return e ? std::max(1, atoi(e)) : 1;  // measured: 2-16 ranges are slower than the two calls
 }
 static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only, int key_lo = 0,
                         int key_hi = kMaxKeys, int pipe_k = 0) {
@@ -3106,11 +3106,6 @@ static int synth_c5(Ctx* c, uint64_t seed, size_t rows, int key_lo, int key_hi, 
 // RoaringBitmap.runOptimize (RB/RoaringBitmap.java:2764-2774) over every bitmap of a
 // batch, into a new batch: plan (new kind + slot size per container), scan of the
 // slot sizes, write.  answers[i] = 1 iff bitmap i holds a run container afterwards.
-static int copy_dev(Ctx* c, DevBuf& dst, const DevBuf& src, hipStream_t s) {
-  CHK(pool_take(c, dst, src.cap));
-  if (src.cap) HIPCHK(hipMemcpyAsync(dst.p, src.p, src.cap, hipMemcpyDeviceToDevice, s));
-  return RBG_OK;
-}
 
 static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answers) {
   Batch* a;
@@ -3140,18 +3135,21 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
   CHK(pool_take(c, b.desc, sizeof(CDesc) * C + 16));
   CHK(pool_take(c, b.payload, a->payload_bytes + 64));
   CHK(pool_take(c, b.ro_stats, 64 + 4 * n + 16));
-  CHK(copy_dev(c, b.keys, a->keys, s));
-  CHK(copy_dev(c, b.bm, a->bm, s));
-  CHK(copy_dev(c, b.key_off, a->key_off, s));
-  CHK(copy_dev(c, b.bm_off, a->bm_off, s));
+  CHK(pool_take(c, b.keys, a->keys.cap));
+  CHK(pool_take(c, b.bm, a->bm.cap));
+  CHK(pool_take(c, b.key_off, a->key_off.cap));
+  CHK(pool_take(c, b.bm_off, a->bm_off.cap));
   HIPCHK(hipMemsetAsync(b.ro_stats.p, 0, 64 + 4 * n + 16, s));
   unsigned long long* tot = b.ro_stats.as<unsigned long long>();
   launch_runopt_plan(s, a->desc.as<CDesc>(), a->bm.as<uint32_t>(), a->payload.as<uint8_t>(), C,
                      c->ro_info.as<uint32_t>(), c->ro_size.as<uint64_t>(), b.ro_stats.as<uint32_t>() + 16, tot);
   launch_exclusive_scan(s, c->ro_size.as<uint64_t>(), c->ro_size.as<uint64_t>(), C, c->ro_part.as<uint64_t>(),
                         reinterpret_cast<uint64_t*>(tot + 4));
+  const RoCopy cp{a->keys.as<uint16_t>(), b.keys.as<uint16_t>(), a->bm.as<uint32_t>(), b.bm.as<uint32_t>(),
+                  a->key_off.as<uint32_t>(), b.key_off.as<uint32_t>(), a->key_off.cap / 4,
+                  a->bm_off.as<uint32_t>(), b.bm_off.as<uint32_t>(), a->bm_off.cap / 4};
   launch_runopt_write(s, a->desc.as<CDesc>(), a->payload.as<uint8_t>(), C, c->ro_info.as<uint32_t>(),
-                      c->ro_size.as<uint64_t>(), b.desc.as<CDesc>(), b.payload.as<uint8_t>());
+                      c->ro_size.as<uint64_t>(), b.desc.as<CDesc>(), b.payload.as<uint8_t>(), cp);
   HIPCHK(hipGetLastError());
   // no host read-back here: the new batch's statistics stay on the device until needed (ensure_stats)
   b.n_bm = n;

@@ -387,8 +387,22 @@ void launch_exclusive_scan(hipStream_t s, const uint64_t* in, uint64_t* out, uin
 // where an R container results; totals = {#A, #B, #R, serialized payload bytes}
 void launch_runopt_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
                         uint32_t* info, uint64_t* size, uint32_t* bm_has_run, unsigned long long* totals);
+// the arrays the new batch shares with the input (keys, input index, key CSR, bitmap CSR), copied by
+// the write kernel
+struct RoCopy {
+  const uint16_t* keys;
+  uint16_t* out_keys;
+  const uint32_t* bm;
+  uint32_t* out_bm;
+  const uint32_t* koff;
+  uint32_t* out_koff;
+  uint64_t n_koff;
+  const uint32_t* boff;
+  uint32_t* out_boff;
+  uint64_t n_boff;
+};
 void launch_runopt_write(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, const uint32_t* info,
-                         const uint64_t* off, CDesc* out_desc, uint8_t* out_payload);
+                         const uint64_t* off, CDesc* out_desc, uint8_t* out_payload, RoCopy cp);
 
 // runopt.hip: selectRangeWithoutCopy of every bitmap of a batch (range-restricted aggregations): the
 // range's first / last key and low bits (lbs..lbl kept on those keys)

@@ -207,11 +207,22 @@ __global__ __launch_bounds__(256) void k_runopt_write(const CDesc* __restrict__ 
                                                          const uint8_t* __restrict__ payload, uint64_t n,
                                                          const uint32_t* __restrict__ info,
                                                          const uint64_t* __restrict__ off, CDesc* __restrict__ out_desc,
-                                                         uint8_t* __restrict__ out_payload) {
+                                                         uint8_t* __restrict__ out_payload, RoCopy cp) {
   __shared__ __align__(16) uint32_t lds_all[4][2048];
   uint32_t* lds = lds_all[threadIdx.x >> 6];
   const int lane = lane_id();
   const uint64_t nw = (uint64_t)gridDim.x * 4;
+  // the new batch's keys, input indices and both CSRs are the input's (runOptimize changes no key):
+  // copied here by every thread of the grid instead of four device-to-device copies
+  {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = g; i < n; i += gs) {
+      cp.out_keys[i] = cp.keys[i];
+      cp.out_bm[i] = cp.bm[i];
+    }
+    for (uint64_t i = g; i < cp.n_koff; i += gs) cp.out_koff[i] = cp.koff[i];
+    for (uint64_t i = g; i < cp.n_boff; i += gs) cp.out_boff[i] = cp.boff[i];
+  }
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
     const CDesc d = desc[i];
     const uint32_t inf = info[i];
@@ -257,11 +268,10 @@ void launch_runopt_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, co
 }
 
 void launch_runopt_write(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, const uint32_t* info,
-                         const uint64_t* off, CDesc* out_desc, uint8_t* out_payload) {
-  if (!n) return;
-  const uint64_t g = std::min<uint64_t>((n + 3) / 4, 8192);
+                         const uint64_t* off, CDesc* out_desc, uint8_t* out_payload, RoCopy cp) {
+  const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((n + 3) / 4, 8192));
   hipLaunchKernelGGL(k_runopt_write, dim3((unsigned)g), dim3(256), 0, s, desc, payload, n, info, off, out_desc,
-                     out_payload);
+                     out_payload, cp);
 }
 
 // ---------------------------------------------------------------------------
