@@ -111,6 +111,137 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, int key_lo, int k
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_tasks = base + cnt;
 }
 
+// ---------------------------------------------------------------------------
+// Balanced task order (dense key ranges).  A wave of the static-stride grid gets one task of every
+// block of S = waves tasks of the list; over a list in key order the families fall at random, so the
+// waves' work differs by the sum of ~16 random task costs (measured with the per-wave probe build,
+// scripts/xcd_probe.py: mean wave life ~165 us against a 227 us launch, equal over the XCDs).  Here
+// the plan sorts the tasks into kBalBins bins by an estimated cost (family, array size, run count),
+// heaviest first, so each block of S tasks holds similar costs and every wave draws one task of each
+// cost band; the kernel then walks its bands in a per-wave rotated order (wave w starts at band
+// w mod bands), so at any instant the waves run a mix of families.  Records and scratch slots stay
+// at key positions (key - key_lo; the plan writes the records of keys without a task), so placement
+// and serialization see key order as before.
+// ---------------------------------------------------------------------------
+constexpr int kBalBins = 32;
+
+// estimated per-task cost (arbitrary units, ~1 per 0.6 us of one wave) -> bin, heaviest first
+template <int OP>
+__device__ __forceinline__ int bal_bin(const PTask& t) {
+  const int ka = t.kind_a, kb = t.kind_b;
+  int c;
+  if (ka == kAbsent || kb == kAbsent) {
+    c = 2;  // a clone: its record only
+  } else if (pair_class(OP, ka, kb) == 1) {  // filter class: the array's values probed in a map of the other
+    const bool probe_a = ka == DK_A && (OP == OP_ANDNOT || kb != DK_A || t.card_a <= t.card_b);  // filter_class_task
+    const int arr = (int)(probe_a ? t.card_a : t.card_b);
+    const int mk = probe_a ? kb : ka;
+    const int mn = probe_a ? t.nruns_b : t.nruns_a;
+    c = 9 + arr / 800 + (mk == DK_R ? 4 + mn / 400 : mk == DK_B ? 3 : (int)(probe_a ? t.card_b : t.card_a) / 1600);
+  } else if (ka == DK_B && kb == DK_B) {
+    c = 24;
+  } else if (ka == DK_R && kb == DK_R) {
+    const int n = t.nruns_a + t.nruns_b;
+    c = n + 2 > 2560 ? 30 : 14 + n / 200;
+  } else {  // B with R, or any other bitmap-class pair (OR / XOR / ANDNOT of arrays and bitmaps)
+    const int n = ka == DK_R ? t.nruns_a : kb == DK_R ? t.nruns_b : 0;
+    c = 18 + n / 300;
+  }
+  return kBalBins - 1 - min(c, kBalBins - 1);
+}
+
+template <int OP, int MODE>
+__global__ __launch_bounds__(256) void k_plan_balanced(int key_lo, uint32_t nkeys, const uint32_t* __restrict__ koa,
+                                                       const CDesc* __restrict__ da, const uint8_t* __restrict__ pa,
+                                                       const uint32_t* __restrict__ kob,
+                                                       const CDesc* __restrict__ db, const uint8_t* __restrict__ pb,
+                                                       uint64_t* __restrict__ wg_bins, uint32_t epoch,
+                                                       PTask* __restrict__ tasks, uint32_t* __restrict__ n_tasks,
+                                                       OutCtx oc, uint32_t* __restrict__ task_card, uint64_t* zlb,
+                                                       uint64_t* ztile, uint32_t* err) {
+  __shared__ int hist[kBalBins];
+  __shared__ uint32_t cnt[256][kBalBins + 1];
+  __shared__ uint32_t base[kBalBins];
+  plan_zero(zlb, ztile);
+  if (threadIdx.x < kBalBins) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // key position in the range
+  PTask t;
+  bool has = false;
+  int bin = -1, rank = 0;
+  if (i < nkeys) {
+    const uint32_t k = (uint32_t)key_lo + i;
+    resolve(koa, da, pa, k, t.slot_a, t.card_a, t.kind_a, t.nruns_a);
+    resolve(kob, db, pb, k, t.slot_b, t.card_b, t.kind_b, t.nruns_b);
+    t.key = (uint16_t)k;
+    const bool ia = t.kind_a != kAbsent, ib = t.kind_b != kAbsent;
+    has = (OP == OP_OR || OP == OP_XOR) ? (ia || ib) : OP == OP_ANDNOT ? ia : (ia && ib);
+    if (has) {
+      bin = bal_bin<OP>(t);
+      rank = atomicAdd(&hist[bin], 1);
+    } else if (MODE == 1) {
+      task_card[i] = 0;
+    } else {  // no result container for this key (RB/RoaringBitmap.java:382-400): an empty record
+      ORec r;
+      r.off = 0;
+      r.src = 0;
+      r.idx = 0;
+      r.card = 0;
+      r.ser_len = 0;
+      r.key = (uint16_t)k;
+      r.kind = DK_A;
+      r.keep = 0;
+      oc.recs[i] = r;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kBalBins)
+    __hip_atomic_store(wg_bins + (size_t)blockIdx.x * kBalBins + threadIdx.x,
+                       ((uint64_t)epoch << 32) | (uint32_t)hist[threadIdx.x], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  // every workgroup's bins (all 256 are resident: one per 256 keys), one workgroup per thread
+  if (threadIdx.x < gridDim.x) {
+    for (int b = 0; b < kBalBins; b++) {
+      uint64_t v;
+      uint32_t spins = 0;
+      while (((v = __hip_atomic_load(wg_bins + (size_t)threadIdx.x * kBalBins + b, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT)) >> 32) != epoch) {
+        if (++spins > (1u << 22)) {
+          atomicOr(err, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      cnt[threadIdx.x][b] = (uint32_t)v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < kBalBins) {  // bin b: its total and this workgroup's offset in it
+    uint32_t tot = 0, pre = 0;
+    for (uint32_t j = 0; j < gridDim.x; j++) {
+      const uint32_t c = cnt[j][threadIdx.x];
+      tot += c;
+      pre += j < blockIdx.x ? c : 0;
+    }
+    cnt[0][threadIdx.x] = tot;  // (row 0 is not read again below)
+    base[threadIdx.x] = pre;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int b = 0; b < kBalBins; b++) {
+      base[b] += run;
+      run += cnt[0][b];
+    }
+    if (blockIdx.x == 0) {
+      n_tasks[0] = nkeys;  // records: one per key of the range
+      n_tasks[1] = run;    // the task list
+    }
+  }
+  __syncthreads();
+  if (has) tasks[base[bin] + rank] = t;
+}
+
 constexpr int kWaves = 4;  // waves per workgroup
 // u32 words of LDS per wave: the 8 KiB bitmap map / staging area, plus room for
 // the run lists of run-domain R AND R (4 waves x 10 KiB x 4 workgroups = 160 KiB)
@@ -520,24 +651,62 @@ __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint
 // and bitmap-class tasks share the launch: separate kernels per class were
 // measured 15 % slower on the C2 mix (tail + an extra dependent index load).
 // MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
-template <int OP, int MODE, bool DIRECT>
+// FORM 0: planned task list (key order); 1: direct (task t = key key_lo + t); 2: balanced (k_plan_balanced's
+// list, the bands walked in a per-wave rotated order, records at key positions)
+template <int OP, int MODE, int FORM>
 __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
                                                       const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
                                                       const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card,
                                                       PwDirect dsrc) {
   __shared__ __align__(16) uint32_t lds_all[kWaves][kWaveLds];
+  constexpr bool DIRECT = FORM == 1;
   if (DIRECT) {
     // the plan kernel's other duties: the task count and the op's zeroed look-back state
     plan_zero(dsrc.zlb, dsrc.ztile);
     if (blockIdx.x == 0 && threadIdx.x == 0) dsrc.n_tasks_out[0] = dsrc.n_tasks_write;
   }
-  const uint32_t nt = DIRECT ? dsrc.nkeys : uni(*n_tasks);
+  const uint32_t nt = DIRECT ? dsrc.nkeys : FORM == 2 ? uni(n_tasks[1]) : uni(*n_tasks);
   const int w = threadIdx.x >> 6;
   uint32_t* lds = lds_all[w];
   const uint32_t stride = gridDim.x * kWaves;
   const uint32_t t0 = uni(blockIdx.x * kWaves + w);
   if (t0 >= nt) return;
   uint32_t t = t0;
+  if (FORM == 2) {
+    // band b holds list positions [b S, (b + 1) S); this wave takes position t0 of each band, starting
+    // at band t0 mod nb (only the last band can be short)
+    const uint32_t nb = (nt + stride - 1) / stride;
+    const uint32_t b0 = t0 % nb;
+    auto pos_of = [&](uint32_t k) -> uint32_t {
+      const uint32_t b = b0 + k < nb ? b0 + k : b0 + k - nb;
+      return b * stride + t0;
+    };
+    uint32_t k = 0;
+    while (k < nb && pos_of(k) >= nt) k++;
+    if (k >= nb) return;
+#if RBG_WAVE_PROBE
+    const uint64_t pr0 = __builtin_amdgcn_s_memrealtime(), pm0 = __builtin_amdgcn_s_memtime();
+    uint32_t ntask = 0;
+#endif
+    PTask cur = load_task(tasks, pos_of(k));
+    for (;;) {
+      uint32_t kn = k + 1;
+      while (kn < nb && pos_of(kn) >= nt) kn++;
+      PTask nxt;
+      if (kn < nb) nxt = load_task(tasks, pos_of(kn));  // in flight while this task runs
+      any_task<OP, MODE>((uint32_t)cur.key - (uint32_t)dsrc.key_lo, cur, pa, pb, oc, task_card, lds SACC_ARG);
+#if RBG_WAVE_PROBE
+      ntask++;
+#endif
+      if (kn >= nb) break;
+      k = kn;
+      cur = nxt;
+    }
+#if RBG_WAVE_PROBE
+    probe_store(pr0, pm0, ntask);
+#endif
+    return;
+  }
   if (DIRECT) {
 #if RBG_STAMPS
     StampAcc sacc = {};
@@ -637,18 +806,24 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 
 template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                      const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct) {
+                      const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced) {
+  if (direct && balanced) {
+    const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, 2>)));
+    hipLaunchKernelGGL((k_pair_wave<OP, MODE, 2>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
+                       *direct);
+    return;
+  }
   if (direct) {
     // Direct mode lays each wave's tasks out in a region of per = ceil(nt / stride) + 3 (rounded to 4)
     // records, stride = 4 g waves: at most nt + 4 stride records.  The task buffer holds
     // kMaxKeys + 32768 (engine.cpp: ctx_init), so stride <= 8192 waves: g <= 2048 workgroups.
-    const int g = std::max(1, std::min({grid, resident_grid((const void*)&k_pair_wave<OP, MODE, true>), 2048}));
-    hipLaunchKernelGGL((k_pair_wave<OP, MODE, true>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
+    const int g = std::max(1, std::min({grid, resident_grid((const void*)&k_pair_wave<OP, MODE, 1>), 2048}));
+    hipLaunchKernelGGL((k_pair_wave<OP, MODE, 1>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
                        *direct);
     return;
   }
-  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, false>)));
-  hipLaunchKernelGGL((k_pair_wave<OP, MODE, false>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
+  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, 0>)));
+  hipLaunchKernelGGL((k_pair_wave<OP, MODE, 0>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
                      PwDirect{});
 }
 
@@ -692,6 +867,34 @@ void debug_stamps(uint64_t* out20, bool) {
 }
 #endif
 
+template <int OP, int MODE>
+static void launch_pb(hipStream_t s, int key_lo, uint32_t nkeys, const uint32_t* koa, const CDesc* da,
+                      const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_bins,
+                      uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint32_t* task_card, uint64_t* zlb,
+                      uint64_t* ztile, uint32_t* err) {
+  hipLaunchKernelGGL((k_plan_balanced<OP, MODE>), dim3((nkeys + 255) / 256), dim3(256), 0, s, key_lo, nkeys, koa, da,
+                     pa, kob, db, pb, wg_bins, epoch, tasks, n_tasks, oc, task_card, zlb, ztile, err);
+}
+void launch_plan_balanced(hipStream_t s, int op, int mode, int key_lo, uint32_t nkeys, const uint32_t* koa,
+                          const CDesc* da, const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb,
+                          uint64_t* wg_bins, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc,
+                          uint32_t* task_card, uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
+#define RBG_LPB(O)                                                                                              \
+  if (mode == 0)                                                                                                \
+    launch_pb<O, 0>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, wg_bins, epoch, tasks, n_tasks, oc, task_card, \
+                    zlb, ztile, err);                                                                           \
+  else                                                                                                          \
+    launch_pb<O, 1>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, wg_bins, epoch, tasks, n_tasks, oc, task_card, \
+                    zlb, ztile, err);
+  switch (op) {
+    case OP_AND: RBG_LPB(OP_AND) break;
+    case OP_OR: RBG_LPB(OP_OR) break;
+    case OP_XOR: RBG_LPB(OP_XOR) break;
+    default: RBG_LPB(OP_ANDNOT) break;
+  }
+#undef RBG_LPB
+}
+
 void launch_plan_pairwise(hipStream_t s, int op, int key_lo, int key_hi, const uint32_t* koa, const CDesc* da,
                           const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb,
                           uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, uint64_t* zlb,
@@ -701,10 +904,10 @@ void launch_plan_pairwise(hipStream_t s, int op, int key_lo, int key_hi, const u
 }
 
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                     const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct) {
-#define RBG_LPW(O)                                                                   \
-  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card, direct); \
-  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card, direct);
+                     const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced) {
+#define RBG_LPW(O)                                                                             \
+  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced); \
+  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced);
   switch (op) {
     case OP_AND: RBG_LPW(OP_AND) break;
     case OP_OR: RBG_LPW(OP_OR) break;

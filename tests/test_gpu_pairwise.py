@@ -303,3 +303,36 @@ def test_dense_key_range_direct_mode(gpu, seed):
     assert e.card() == O.pairwise_card("and", a, b)
     e.release(ba)
     e.release(bb)
+
+
+@pytest.mark.parametrize("balance", ["0", "1"])
+@pytest.mark.parametrize("seed", range(3))
+def test_dense_range_task_orders(gpu, seed, balance, monkeypatch):
+    """Dense key ranges in both task orders: key order (RBG_PW_BALANCE=0, the direct form) and binned by
+    estimated cost (k_plan_balanced: the task list out of key order, records still at key positions,
+    empty records / zero counts for keys without a task).  Every op, the key-range form and
+    andCardinality over a range that covers every key, against the oracle."""
+    from roaringbitmap_amd import Engine
+    monkeypatch.setenv("RBG_PW_BALANCE", balance)
+    rng = np.random.default_rng(4100 + seed)
+    n = int(rng.integers(300, 1500))
+    keys = np.arange(n)
+    a = _gen.bitmap(rng, keys, p_present=0.8)
+    b = _gen.bitmap(rng, keys, p_present=0.8)
+    e = Engine(0)
+    ba, bb = e.load([a]), e.load([b])
+    for op in OPS:
+        e.pairwise(op, ba, bb, key_lo=0, key_hi=n)
+        assert e.fetch().serialize() == O.pairwise(op, a, b), (seed, op)
+        lo, hi = n // 3, n // 3 + n // 2
+        e.pairwise(op, ba, bb, key_lo=lo, key_hi=hi)
+        rs = e.result_stats()
+        exp = O.pairwise(op, a, b)
+        want = sum(1 for c in decode(exp) if lo <= c[0] < hi)
+        assert rs["containers"] == want, (seed, op)
+    e.and_cardinality(ba, bb)
+    assert e.card() == O.pairwise_card("and", a, b)
+    e.release(ba)
+    e.release(bb)
+    for op in OPS:  # one-shot path (rbg_pairwise) with a dense pair
+        assert gpu_pair(op, a, b) == O.pairwise(op, a, b), (seed, op)
