@@ -174,7 +174,6 @@ struct Ctx {
   int device = 0;
   DecBufs dec;
   DevBuf wg_epoch;         // pairwise plan: per-workgroup task counts tagged with the op epoch
-  DevBuf wg_bins;          // balanced pairwise plan: per-workgroup cost-bin counts tagged with the op epoch
   uint32_t epoch = 0;
   DevBuf pc_cnt, pc_part, pc_items, pc_large;  // batched andCardinality scratch
   hipStream_t stream = nullptr;
@@ -946,16 +945,11 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   // RBG_PW_BALANCE=0: the direct form, tasks in key order)
   const char* bal_env = getenv("RBG_PW_BALANCE");
   const bool balanced = direct && (!bal_env || atoi(bal_env) != 0);
-  if (balanced) {
-    if (!c->wg_bins.p) {
-      CHK(c->wg_bins.ensure(8 * 256 * 32));
-      HIPCHK(hipMemsetAsync(c->wg_bins.p, 0, 8 * 256 * 32, s));
-    }
+  if (balanced)
     launch_plan_balanced(s, plan_op, card_only ? 1 : 0, key_lo, (uint32_t)nkeys, A->key_off.as<uint32_t>(), da,
                          A->payload.as<uint8_t>(), B->key_off.as<uint32_t>(), db, B->payload.as<uint8_t>(),
-                         c->wg_bins.as<uint64_t>(), next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc,
-                         c->task_card.as<uint32_t>(), c->zlb, c->ztile, oc.err);
-  }
+                         c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->task_card.as<uint32_t>(), c->zlb,
+                         c->ztile);
   c->mark(1);
   // 4 waves (tasks) per workgroup, clamped to the resident grid
   const int grid = grid_for(((direct ? nkeys : ub) + 3) / 4, 16384);

@@ -261,13 +261,13 @@ struct PwDirect {
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
                      const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct,
                      bool balanced = false);
-// dense key ranges: every key's task resolved and binned by estimated cost (heaviest first) into tasks[];
-// n_tasks[0] = nkeys (records, one per key: keys without a task get an empty record / a zero count),
-// n_tasks[1] = list length.  wg_bins: 256 x 32 u64 (zeroed once per context), epoch unique per op.
+// dense key ranges: every key's task resolved and ordered by estimated cost within its 256-key segment
+// (heaviest first, rotated by the segment index) into tasks[]; n_tasks[0] = n_tasks[1] = nkeys (records
+// and list positions, one per key: keys without a task are marked, with an empty record / a zero count)
 void launch_plan_balanced(hipStream_t s, int op, int mode, int key_lo, uint32_t nkeys, const uint32_t* koa,
                           const CDesc* da, const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb,
-                          uint64_t* wg_bins, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc,
-                          uint32_t* task_card, uint64_t* zlb, uint64_t* ztile, uint32_t* err);
+                          PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint32_t* task_card, uint64_t* zlb,
+                          uint64_t* ztile);
 // diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
 void debug_stamps(uint64_t* out20, bool reset);
 // diagnostic build (-DRBG_BSI_STAMPS=1): per-phase clock totals of k_bsi_reg

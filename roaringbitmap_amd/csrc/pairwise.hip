@@ -121,7 +121,9 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, int key_lo, int k
 // cost band; the kernel then walks its bands in a per-wave rotated order (wave w starts at band
 // w mod bands), so at any instant the waves run a mix of families.  Records and scratch slots stay
 // at key positions (key - key_lo; the plan writes the records of keys without a task), so placement
-// and serialization see key order as before.
+// and serialization see key order as before.  The binning is per workgroup of the plan (256 keys, a
+// counting sort in LDS, no cross-workgroup step: a global sort's inter-workgroup exchange cost 20 us);
+// the workgroups' key ranges hold the same family mix, so per-segment ranks are global cost bands.
 // ---------------------------------------------------------------------------
 constexpr int kBalBins = 32;
 
@@ -155,91 +157,66 @@ __global__ __launch_bounds__(256) void k_plan_balanced(int key_lo, uint32_t nkey
                                                        const CDesc* __restrict__ da, const uint8_t* __restrict__ pa,
                                                        const uint32_t* __restrict__ kob,
                                                        const CDesc* __restrict__ db, const uint8_t* __restrict__ pb,
-                                                       uint64_t* __restrict__ wg_bins, uint32_t epoch,
                                                        PTask* __restrict__ tasks, uint32_t* __restrict__ n_tasks,
                                                        OutCtx oc, uint32_t* __restrict__ task_card, uint64_t* zlb,
-                                                       uint64_t* ztile, uint32_t* err) {
+                                                       uint64_t* ztile) {
   __shared__ int hist[kBalBins];
-  __shared__ uint32_t cnt[256][kBalBins + 1];
-  __shared__ uint32_t base[kBalBins];
+  __shared__ int off[kBalBins];
   plan_zero(zlb, ztile);
   if (threadIdx.x < kBalBins) hist[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;  // key position in the range
   PTask t;
-  bool has = false;
-  int bin = -1, rank = 0;
+  int bin = kBalBins - 1, rank = 0;
   if (i < nkeys) {
     const uint32_t k = (uint32_t)key_lo + i;
     resolve(koa, da, pa, k, t.slot_a, t.card_a, t.kind_a, t.nruns_a);
     resolve(kob, db, pb, k, t.slot_b, t.card_b, t.kind_b, t.nruns_b);
     t.key = (uint16_t)k;
     const bool ia = t.kind_a != kAbsent, ib = t.kind_b != kAbsent;
-    has = (OP == OP_OR || OP == OP_XOR) ? (ia || ib) : OP == OP_ANDNOT ? ia : (ia && ib);
+    const bool has = (OP == OP_OR || OP == OP_XOR) ? (ia || ib) : OP == OP_ANDNOT ? ia : (ia && ib);
     if (has) {
       bin = bal_bin<OP>(t);
-      rank = atomicAdd(&hist[bin], 1);
-    } else if (MODE == 1) {
-      task_card[i] = 0;
-    } else {  // no result container for this key (RB/RoaringBitmap.java:382-400): an empty record
-      ORec r;
-      r.off = 0;
-      r.src = 0;
-      r.idx = 0;
-      r.card = 0;
-      r.ser_len = 0;
-      r.key = (uint16_t)k;
-      r.kind = DK_A;
-      r.keep = 0;
-      oc.recs[i] = r;
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x < kBalBins)
-    __hip_atomic_store(wg_bins + (size_t)blockIdx.x * kBalBins + threadIdx.x,
-                       ((uint64_t)epoch << 32) | (uint32_t)hist[threadIdx.x], __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  // every workgroup's bins (all 256 are resident: one per 256 keys), one workgroup per thread
-  if (threadIdx.x < gridDim.x) {
-    for (int b = 0; b < kBalBins; b++) {
-      uint64_t v;
-      uint32_t spins = 0;
-      while (((v = __hip_atomic_load(wg_bins + (size_t)threadIdx.x * kBalBins + b, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT)) >> 32) != epoch) {
-        if (++spins > (1u << 22)) {
-          atomicOr(err, 1u);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+    } else {  // no task: marked (both kinds absent) and skipped by the compute kernel
+      t.kind_a = t.kind_b = kAbsent;
+      if (MODE == 1) {
+        task_card[i] = 0;
+      } else {  // no result container for this key (RB/RoaringBitmap.java:382-400): an empty record
+        ORec r;
+        r.off = 0;
+        r.src = 0;
+        r.idx = 0;
+        r.card = 0;
+        r.ser_len = 0;
+        r.key = (uint16_t)k;
+        r.kind = DK_A;
+        r.keep = 0;
+        oc.recs[i] = r;
       }
-      cnt[threadIdx.x][b] = (uint32_t)v;
     }
+    rank = atomicAdd(&hist[bin], 1);
   }
   __syncthreads();
-  if (threadIdx.x < kBalBins) {  // bin b: its total and this workgroup's offset in it
-    uint32_t tot = 0, pre = 0;
-    for (uint32_t j = 0; j < gridDim.x; j++) {
-      const uint32_t c = cnt[j][threadIdx.x];
-      tot += c;
-      pre += j < blockIdx.x ? c : 0;
-    }
-    cnt[0][threadIdx.x] = tot;  // (row 0 is not read again below)
-    base[threadIdx.x] = pre;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t run = 0;
+  if (threadIdx.x == 0) {  // heaviest bin first
+    int run = 0;
     for (int b = 0; b < kBalBins; b++) {
-      base[b] += run;
-      run += cnt[0][b];
-    }
-    if (blockIdx.x == 0) {
-      n_tasks[0] = nkeys;  // records: one per key of the range
-      n_tasks[1] = run;    // the task list
+      off[b] = run;
+      run += hist[b];
     }
   }
   __syncthreads();
-  if (has) tasks[base[bin] + rank] = t;
+  if (i < nkeys) {
+    // this workgroup's segment [256 g, 256 g + m) holds its keys' tasks by cost rank r (0 = heaviest) at
+    // offset (r + g) mod m: a wave takes one offset of every 16th segment, so its tasks are ranks
+    // spaced 16 apart (every cost band of the segments) rather than one rank over and over
+    const uint32_t m = min(256u, nkeys - blockIdx.x * 256u);
+    const uint32_t r = (uint32_t)(off[bin] + rank);
+    tasks[blockIdx.x * 256u + (r + blockIdx.x) % m] = t;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    n_tasks[0] = nkeys;  // records: one per key of the range
+    n_tasks[1] = nkeys;  // list positions (keys without a task are marked)
+  }
 }
 
 constexpr int kWaves = 4;  // waves per workgroup
@@ -694,10 +671,12 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
       while (kn < nb && pos_of(kn) >= nt) kn++;
       PTask nxt;
       if (kn < nb) nxt = load_task(tasks, pos_of(kn));  // in flight while this task runs
-      any_task<OP, MODE>((uint32_t)cur.key - (uint32_t)dsrc.key_lo, cur, pa, pb, oc, task_card, lds SACC_ARG);
+      if (cur.kind_a != kAbsent || cur.kind_b != kAbsent) {  // marked: no task (the plan wrote its record)
+        any_task<OP, MODE>((uint32_t)cur.key - (uint32_t)dsrc.key_lo, cur, pa, pb, oc, task_card, lds SACC_ARG);
 #if RBG_WAVE_PROBE
-      ntask++;
+        ntask++;
 #endif
+      }
       if (kn >= nb) break;
       k = kn;
       cur = nxt;
@@ -869,23 +848,20 @@ void debug_stamps(uint64_t* out20, bool) {
 
 template <int OP, int MODE>
 static void launch_pb(hipStream_t s, int key_lo, uint32_t nkeys, const uint32_t* koa, const CDesc* da,
-                      const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb, uint64_t* wg_bins,
-                      uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint32_t* task_card, uint64_t* zlb,
-                      uint64_t* ztile, uint32_t* err) {
+                      const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb, PTask* tasks,
+                      uint32_t* n_tasks, OutCtx oc, uint32_t* task_card, uint64_t* zlb, uint64_t* ztile) {
   hipLaunchKernelGGL((k_plan_balanced<OP, MODE>), dim3((nkeys + 255) / 256), dim3(256), 0, s, key_lo, nkeys, koa, da,
-                     pa, kob, db, pb, wg_bins, epoch, tasks, n_tasks, oc, task_card, zlb, ztile, err);
+                     pa, kob, db, pb, tasks, n_tasks, oc, task_card, zlb, ztile);
 }
 void launch_plan_balanced(hipStream_t s, int op, int mode, int key_lo, uint32_t nkeys, const uint32_t* koa,
                           const CDesc* da, const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb,
-                          uint64_t* wg_bins, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc,
-                          uint32_t* task_card, uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
-#define RBG_LPB(O)                                                                                              \
-  if (mode == 0)                                                                                                \
-    launch_pb<O, 0>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, wg_bins, epoch, tasks, n_tasks, oc, task_card, \
-                    zlb, ztile, err);                                                                           \
-  else                                                                                                          \
-    launch_pb<O, 1>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, wg_bins, epoch, tasks, n_tasks, oc, task_card, \
-                    zlb, ztile, err);
+                          PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint32_t* task_card, uint64_t* zlb,
+                          uint64_t* ztile) {
+#define RBG_LPB(O)                                                                                               \
+  if (mode == 0)                                                                                                 \
+    launch_pb<O, 0>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, tasks, n_tasks, oc, task_card, zlb, ztile);     \
+  else                                                                                                           \
+    launch_pb<O, 1>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, tasks, n_tasks, oc, task_card, zlb, ztile);
   switch (op) {
     case OP_AND: RBG_LPB(OP_AND) break;
     case OP_OR: RBG_LPB(OP_OR) break;
