@@ -276,8 +276,30 @@ struct StampAcc {
 // consumed, then drops to 0, so waves that are issuing loads win instruction
 // arbitration over waves in their compute / output phases and more of the CU's
 // memory requests are in flight (C2 AND -1 %, andCardinality -2.5 %).
-__device__ __forceinline__ void prio_hi() { __builtin_amdgcn_s_setprio(3); }
-__device__ __forceinline__ void prio_lo() { __builtin_amdgcn_s_setprio(0); }
+// Experiment builds (RBG_PRIO_TIER, scripts/gpu_r5d.sh): the per-wave probe shows the workgroups of a
+// CU finishing in dispatch order (mean wave end 154 / 162 / 169 / 178 us for the 1st..4th workgroup of
+// a CU, round 5), the issue arbitration favouring the oldest waves at equal priority.  1: the compute
+// phase at the workgroup's dispatch tier (younger = higher), 2: no priorities, 3: tier / 2.
+#ifndef RBG_PRIO_TIER
+#define RBG_PRIO_TIER 0
+#endif
+__device__ __forceinline__ void prio_hi() {
+#if RBG_PRIO_TIER != 2
+  __builtin_amdgcn_s_setprio(3);
+#endif
+}
+__device__ __forceinline__ void prio_lo() {
+#if RBG_PRIO_TIER == 1 || RBG_PRIO_TIER == 3
+  uint32_t tier = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u) / gridDim.x);
+  if (RBG_PRIO_TIER == 3) tier >>= 1;
+  if (tier == 0) __builtin_amdgcn_s_setprio(0);
+  else if (tier == 1) __builtin_amdgcn_s_setprio(1);
+  else if (tier == 2) __builtin_amdgcn_s_setprio(2);
+  else __builtin_amdgcn_s_setprio(3);
+#elif RBG_PRIO_TIER == 0
+  __builtin_amdgcn_s_setprio(0);
+#endif
+}
 
 // Filter path: AND with an array operand and ANDNOT of an array c1 always give an
 // array that is a subset of that array (App. A.1 / A.3; RB/ArrayContainer.java:
