@@ -276,12 +276,13 @@ struct StampAcc {
 // consumed, then drops to 0, so waves that are issuing loads win instruction
 // arbitration over waves in their compute / output phases and more of the CU's
 // memory requests are in flight (C2 AND -1 %, andCardinality -2.5 %).
-// Experiment builds (RBG_PRIO_TIER, scripts/gpu_r5d.sh): the per-wave probe shows the workgroups of a
-// CU finishing in dispatch order (mean wave end 154 / 162 / 169 / 178 us for the 1st..4th workgroup of
-// a CU, round 5), the issue arbitration favouring the oldest waves at equal priority.  1: the compute
-// phase at the workgroup's dispatch tier (younger = higher), 2: no priorities, 3: tier / 2.
+// The per-wave probe shows the workgroups of a CU finishing in dispatch order (mean wave end 154 / 162 /
+// 169 / 178 us for the 1st..4th workgroup of a CU, round 5): the issue arbitration favours the oldest
+// waves at equal priority.  RBG_PRIO_TIER (scripts/gpu_r5d.sh): 0: compute phases at priority 0,
+// 1: at the workgroup's dispatch tier (younger = higher; reverses the order, the spread stays),
+// 2: no priorities, 3 (kept): tier / 2 -- with the balanced task order, the AND kernel 0.244 -> 0.233 ms.
 #ifndef RBG_PRIO_TIER
-#define RBG_PRIO_TIER 0
+#define RBG_PRIO_TIER 3
 #endif
 __device__ __forceinline__ void prio_hi() {
 #if RBG_PRIO_TIER != 2
