@@ -63,8 +63,9 @@ def counters(path):
 
 
 # workload (bench.py --only) -> (traffic key in pmc_traffic.json, dominant kernel)
-WORKLOADS = {"c2": ("k_pair_wave", "k_pair_wave<0, 0, true>"), "c2card": ("k_pair_wave_card", "k_pair_wave<0, 1, true>"),
-             "c2ser": ("k_serialize_c2", "k_serialize"), "c4": ("k_pair_items", "k_pair_items"),
+# (round 5: the dense pairwise ranges run the balanced form <OP, MODE, 2>; k_serialize<3> is the whole serialization)
+WORKLOADS = {"c2": ("k_pair_wave", "k_pair_wave<0, 0, 2>"), "c2card": ("k_pair_wave_card", "k_pair_wave<0, 1, 2>"),
+             "c2ser": ("k_serialize_c2", "k_serialize<3>"), "c4": ("k_pair_items", "k_pair_items"),
              "c3u": ("k_wide<OR>_uniform", "k_wide<0>"), "c3c": ("k_wide<OR>_clustered", "k_wide<0>"),
              "c5": ("k_bsi_reg", "k_bsi_reg")}
 
