@@ -55,8 +55,15 @@ typedef struct rbg_buffer {
 } rbg_buffer;
 
 /* pairwise ops: RB/RoaringBitmap.java and :377, or :860, xor :1071, andNot :444;
- * RBG_OR_INPLACE: x1.or(x2) in place (:2481-2523), Container.ior's result types */
-enum { RBG_AND = 0, RBG_OR = 1, RBG_XOR = 2, RBG_ANDNOT = 3, RBG_OR_INPLACE = 4 };
+ * RBG_OR_INPLACE: x1.or(x2) in place (:2481-2523), Container.ior's result types;
+ * RBG_AND_BUFFER / RBG_ANDNOT_BUFFER: the buffer package's static and / andNot,
+ * RB/buffer/ImmutableRoaringBitmap.java:299-325, 441-471 (= MutableRoaringBitmap.and / andNot
+ * static, RB/buffer/MutableRoaringBitmap.java:235-301): run AND / ANDNOT run keep the merged run
+ * container (RB/buffer/MappeableRunContainer.java:474-536, 600-663), results above 2047 runs
+ * included; every other container pair types like the heap's.  Synchronous (the run arena is checked).
+ * The buffer or / xor type like the heap's: RBG_OR / RBG_XOR. */
+enum { RBG_AND = 0, RBG_OR = 1, RBG_XOR = 2, RBG_ANDNOT = 3, RBG_OR_INPLACE = 4, RBG_AND_BUFFER = 5,
+       RBG_ANDNOT_BUFFER = 6 };
 /* cardinality ops: andCardinality :413, orCardinality :916, xorCardinality :931,
  * andNotCardinality :944 (all Java int, wrapping mod 2^32), intersects :698 (0/1) */
 enum { RBG_CARD_AND = 0, RBG_CARD_OR = 1, RBG_CARD_XOR = 2, RBG_CARD_ANDNOT = 3, RBG_INTERSECTS = 4 };

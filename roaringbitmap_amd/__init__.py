@@ -8,11 +8,11 @@ include/roaring_mi355x.h.
 from ._lib import (DeviceError, IllegalArgumentException, InvalidRoaringFormat, RoaringError,  # noqa: F401
                    TruncatedInput)
 from .engine import Engine  # noqa: F401
-from .roaring import (BufferFastAggregation, FastAggregation, ParallelAggregation, RoaringBitmap, batch_and_cardinality,  # noqa: F401
-                      run_optimize_many)
+from .roaring import (BufferFastAggregation, FastAggregation, ImmutableRoaringBitmap, MutableRoaringBitmap,  # noqa: F401
+                      ParallelAggregation, RoaringBitmap, batch_and_cardinality, run_optimize_many)
 from .bsi import BitSliceIndexBase, ImmutableBitSliceIndex, MutableBitSliceIndex, RoaringBitmapSliceIndex  # noqa: F401
 
-__all__ = ["RoaringBitmap", "FastAggregation", "BufferFastAggregation", "ParallelAggregation", "RoaringBitmapSliceIndex", "ImmutableBitSliceIndex",
+__all__ = ["RoaringBitmap", "ImmutableRoaringBitmap", "MutableRoaringBitmap", "FastAggregation", "BufferFastAggregation", "ParallelAggregation", "RoaringBitmapSliceIndex", "ImmutableBitSliceIndex",
            "MutableBitSliceIndex", "BitSliceIndexBase", "Engine", "batch_and_cardinality", "run_optimize_many",
            "InvalidRoaringFormat",
            "TruncatedInput", "IllegalArgumentException", "DeviceError", "RoaringError"]

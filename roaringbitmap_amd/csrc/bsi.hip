@@ -1158,6 +1158,71 @@ void launch_bsi_buf(hipStream_t s, int grid, const Task* tasks, const uint32_t* 
   hipLaunchKernelGGL(k_bsi_buf, dim3(g), dim3(256), 0, s, tasks, nt, args, p, oc);
 }
 
+// ImmutableRoaringBitmap.and / andNot (RB/buffer/ImmutableRoaringBitmap.java:299-325, 441-471) and
+// MutableRoaringBitmap's static and / andNot (RB/buffer/MutableRoaringBitmap.java:235-301): per key
+// c1.and(c2) / c1.andNot(c2) with the buffer package's container types -- vb_op<OP, true>, the
+// buffer BSI's step: run AND / ANDNOT run keep the merged run container (more than 2047 runs go to
+// the big-run arena), every other pair types like the heap's.  One workgroup per task of the
+// pairwise plan (k_plan_pairwise: AND = keys of both, ANDNOT = keys of x1); an x1 container with
+// no x2 counterpart is appended as is (appendCopy, :460-469).
+__device__ __forceinline__ void pb_load(uint64_t slot, uint32_t card, uint16_t key, uint8_t kind, int src,
+                                        const uint8_t* payload, uint32_t* tmp, int* q, VB& z) {
+  if (kind == kAbsent) {
+    vb_absent(z);
+    return;
+  }
+  materialize(CDesc{slot, card, key, kind, 0}, payload, tmp, q, z.r);
+  z.present = 1;
+  z.kind = kind;
+  z.card = (int)card;
+  z.src = src;
+}
+
+template <int OP>
+__global__ __launch_bounds__(256) void k_pair_buf(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                  const uint8_t* pa, const uint8_t* pb, OutCtx oc, BigRuns big) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int q[257];
+  __shared__ int sh[8];
+  __shared__ unsigned long long sh64;
+  const uint32_t nt = *n_tasks;
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const PTask tk = tasks[t];
+    VB x, y, z;
+    pb_load(tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0, pa, tmp, q, x);
+    pb_load(tk.slot_b, tk.card_b, tk.key, tk.kind_b, 1, pb, tmp, q, y);
+    vb_op<OP, true>(x, y, z, acc, sh);
+    if (!z.present) {
+      wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, nullptr);
+      continue;
+    }
+    if (z.src >= 0) {  // an operand's container unchanged
+      const bool a = z.src == 0;
+      wg_passthrough(t, CDesc{a ? tk.slot_a : tk.slot_b, a ? tk.card_a : tk.card_b, tk.key, a ? tk.kind_a : tk.kind_b, 0},
+                     a ? pa : pb, oc, nullptr);
+      continue;
+    }
+    if (z.kind == DK_R) {
+      const int nr = count_runs(z.r, acc, sh);
+      if (nr > 2047) {
+        place_big_runs(t, tk.key, z.r, z.card, nr, oc, big, acc, sh, &sh64);
+        continue;
+      }
+    }
+    const uint32_t len = stage_container(z.kind, z.r, z.card, acc, tmp, sh);
+    wg_place(t, true, nullptr, true, tmp, len, (uint32_t)z.card, tk.key, z.kind, oc, nullptr);
+  }
+}
+
+void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
+                     const uint8_t* pb, OutCtx oc, BigRuns big) {
+  const void* k = op == OPR_AND ? (const void*)&k_pair_buf<OPR_AND> : (const void*)&k_pair_buf<OPR_ANDNOT>;
+  const int g = std::max(1, std::min(grid, resident_grid(k)));
+  if (op == OPR_AND) hipLaunchKernelGGL(k_pair_buf<OPR_AND>, dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, big);
+  else hipLaunchKernelGGL(k_pair_buf<OPR_ANDNOT>, dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, big);
+}
+
 void launch_plan_bsi(hipStream_t s, const uint32_t* key_off, const uint32_t* bm, uint32_t need, Task* by_key,
                      uint8_t* flag, uint32_t* wg_count, uint64_t* zlb, uint64_t* ztile, unsigned long long* zsums,
                      uint32_t* zdefer) {

@@ -885,8 +885,61 @@ static int pipe_ranges() {
   const char* e = getenv("RBG_SER_PIPE");  // read per call (tests vary it)
   return e ? std::max(1, atoi(e)) : 1;  // measured: 2-16 ranges are slower than the two calls
 }
+// ImmutableRoaringBitmap.and / andNot and MutableRoaringBitmap's static and / andNot
+// (RB/buffer/ImmutableRoaringBitmap.java:299-325, 441-471; RB/buffer/MutableRoaringBitmap.java:235-301):
+// the pairwise plan, then k_pair_buf (the buffer package's container types).  A run result above
+// 2047 runs goes to the big-run arena; the arena is checked after the op and the op rerun once with
+// the size the first pass reserved (as the buffer naive_and chain, ctx_wide).
+static int ctx_pairwise_buffer(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, int key_lo, int key_hi) {
+  key_lo = std::max(0, key_lo);
+  key_hi = std::min(kMaxKeys, key_hi);
+  Batch *A, *B;
+  CHK(get_batch(c, ia, &A));
+  CHK(get_batch(c, ib, &B));
+  const uint16_t *ka, *kb;
+  const CDesc *da, *db;
+  int na, nb;
+  CHK(operand(A, ma, &ka, &da, &na));
+  CHK(operand(B, mb, &kb, &db, &nb));
+  hipStream_t s = c->stream;
+  const size_t ub = std::max<size_t>(1, op == OP_AND ? (size_t)std::min(na, nb) : (size_t)na);
+  if (!c->big_ctl.p) CHK(c->big_ctl.ensure(16));
+  if (!c->big.p) CHK(c->big.ensure(16ull << 20));
+  for (int attempt = 0;; attempt++) {
+    OutCtx oc;
+    CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub + c->big.cap, &oc, false));
+    c->pending_src = {ia, ib};
+    c->mark(0);
+    launch_plan_pairwise(s, op, key_lo, key_hi, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(),
+                         B->key_off.as<uint32_t>(), db, B->payload.as<uint8_t>(), c->wg_epoch.as<uint64_t>(),
+                         next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), c->zlb, c->ztile, oc.err);
+    HIPCHK(hipMemsetAsync(c->big_ctl.p, 0, 16, s));
+    c->mark(1);
+    launch_pair_buf(s, op, grid_for(ub, 65536), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(),
+                    A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), oc,
+                    BigRuns{c->big.as<uint8_t>(), c->big_ctl.as<unsigned long long>(), c->big.cap});
+    c->mark(2);
+    defer_place(c);
+    c->mark(3);
+    HIPCHK(hipGetLastError());
+    unsigned long long used[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(used, c->big_ctl.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (!used[1]) return RBG_OK;
+    if (attempt) {
+      set_err("buffer and / andNot: the run-container arena overflowed twice");
+      return RBG_ERR_DEVICE;
+    }
+    CHK(c->big.ensure(used[0] + (used[0] >> 3) + 4096));
+  }
+}
+
 static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only, int key_lo = 0,
                         int key_hi = kMaxKeys, int pipe_k = 0) {
+  if (op == RBG_AND_BUFFER || op == RBG_ANDNOT_BUFFER) {
+    if (card_only) return RBG_ERR_ILLEGAL_ARGUMENT;
+    return ctx_pairwise_buffer(c, op == RBG_AND_BUFFER ? OP_AND : OP_ANDNOT, ia, ma, ib, mb, key_lo, key_hi);
+  }
   if (op == RBG_OR_INPLACE && !card_only) {
     CHK(ctx_pairwise(c, OP_OR, ia, ma, ib, mb, false, key_lo, key_hi));
     if (!c->ones.p) {
@@ -2004,7 +2057,7 @@ int rbg_set_devices(uint64_t mask) {
 }
 
 int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, rbg_buffer* out) {
-  if (!out || op < 0 || op > RBG_OR_INPLACE) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!out || op < 0 || op > RBG_ANDNOT_BUFFER) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
@@ -2013,7 +2066,7 @@ int rbg_pairwise(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_
   int32_t ids[2];
   CHK(ctx_load_separate(c, bufs, lens, 2, ids));  // one upload for both operands
   g.ids = {ids[0], ids[1]};
-  CHK(ctx_pairwise(c, op, ids[0], 0, ids[1], 0, false, 0, kMaxKeys, op == RBG_OR_INPLACE ? 0 : pipe_ranges()));
+  CHK(ctx_pairwise(c, op, ids[0], 0, ids[1], 0, false, 0, kMaxKeys, op <= RBG_ANDNOT ? pipe_ranges() : 0));
   return ctx_fetch(c, out);
 }
 

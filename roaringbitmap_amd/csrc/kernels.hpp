@@ -351,6 +351,10 @@ void launch_bsi(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, 
 // task (p.owen_tb, p.task_keys) for the host's horizontal_or queue replay; k_bsi_buf runs the circuit
 void launch_bsi_owen_pre(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p);
 void launch_bsi_buf(hipStream_t s, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, BsiArgs p, OutCtx oc);
+// ImmutableRoaringBitmap.and / andNot (op OP_AND / OP_ANDNOT) over the pairwise plan's task list, the
+// buffer package's container types (workgroup per task; run results above 2047 runs to `big`)
+void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
+                     const uint8_t* pb, OutCtx oc, BigRuns big);
 
 // batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch: per-pair key
 // alignment (count, scan, emit), then one wave per matched key; pairs of more than 64

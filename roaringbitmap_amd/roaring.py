@@ -645,6 +645,81 @@ class BufferFastAggregation:
     priorityqueue_xor = staticmethod(FastAggregation.priorityqueue_xor)
 
 
+class ImmutableRoaringBitmap(RoaringBitmap):
+    """RB/buffer/ImmutableRoaringBitmap.java: the mapped portable-format buffer (the same bytes a
+    RoaringBitmap here holds).  Its static pairwise ops return MutableRoaringBitmap and type their
+    containers as the buffer package does: and / andNot (:299-325, :441-471) per key c1.and(c2) /
+    c1.andNot(c2), where run AND / ANDNOT run keep the merged run container
+    (RB/buffer/MappeableRunContainer.java:474-536, 600-663: no toEfficientContainer, more than 2047
+    runs possible); or / xor (:927-977, :1087-1134) type like the heap's."""
+    __slots__ = ()
+
+    @staticmethod
+    def _bpair(op, x1, x2):
+        b = _lib.rbg_buffer()
+        check(lib().rbg_pairwise(_lib.OP[op], x1._buf, len(x1._buf), x2._buf, len(x2._buf), ctypes.byref(b)))
+        return MutableRoaringBitmap(take(b))
+
+    @staticmethod
+    def _s_and(x1, x2):
+        """and(x1, x2) :299-325"""
+        return ImmutableRoaringBitmap._bpair("and_buffer", x1, x2)
+
+    @staticmethod
+    def _s_andnot(x1, x2):
+        """andNot(x1, x2) :441-471"""
+        return ImmutableRoaringBitmap._bpair("andnot_buffer", x1, x2)
+
+    @staticmethod
+    def _s_or(x1, x2):
+        """or(x1, x2) :927-977"""
+        return ImmutableRoaringBitmap._bpair("or", x1, x2)
+
+    @staticmethod
+    def _s_xor(x1, x2):
+        """xor(x1, x2) :1087-1134"""
+        return ImmutableRoaringBitmap._bpair("xor", x1, x2)
+
+    and_ = _s_and
+    andNot = _s_andnot
+    or_ = _s_or
+    xor = _s_xor
+    andCardinality = RoaringBitmap.__dict__["andCardinality"]  # :336-359, a set-level count
+    intersects = RoaringBitmap.__dict__["intersects"]
+
+
+class MutableRoaringBitmap(ImmutableRoaringBitmap):
+    """RB/buffer/MutableRoaringBitmap.java: the static and / andNot (:235-301) are ImmutableRoaringBitmap's
+    per-key code; the in-place x1.and(x2) (:886-910) and x1.andNot(x2) (:918-954) run
+    MappeableContainer.iand / iandNot, which type like the static ops (MappeableRunContainer.iand /
+    iandNot = and / andNot, :1106-1123; MappeableArrayContainer.iandNot :703-749 keeps an array,
+    MappeableBitmapContainer.iandNot :680-760 by cardinality).  x1.and(x1) leaves x1, x1.andNot(x1)
+    clears it (:887, :919-922).  The in-place or / xor (Container.ior / ixor of the buffer package) are
+    not on this path."""
+    __slots__ = ()
+
+    and_ = _StaticOrInPlace(ImmutableRoaringBitmap._s_and, "and_buffer")
+    andNot = _StaticOrInPlace(ImmutableRoaringBitmap._s_andnot, "andnot_buffer")
+    or_ = _StaticOrInPlace(ImmutableRoaringBitmap._s_or, "or")
+    xor = _StaticOrInPlace(ImmutableRoaringBitmap._s_xor, "xor")
+
+    def _inplace(self, op, x2):
+        if op not in ("and_buffer", "andnot_buffer"):
+            raise NotImplementedError("MutableRoaringBitmap.or / xor in place")
+        if x2 is self:
+            if op == "andnot_buffer":
+                self._buf = EMPTY
+                self._lcard = 0
+            return
+        self._buf = ImmutableRoaringBitmap._bpair(op, self, x2)._buf
+        self._lcard = None
+
+
+setattr(ImmutableRoaringBitmap, "and", ImmutableRoaringBitmap.__dict__["and_"])
+setattr(ImmutableRoaringBitmap, "or", ImmutableRoaringBitmap.__dict__["or_"])
+setattr(MutableRoaringBitmap, "and", MutableRoaringBitmap.__dict__["and_"])
+setattr(MutableRoaringBitmap, "or", MutableRoaringBitmap.__dict__["or_"])
+
 setattr(BufferFastAggregation, "and", BufferFastAggregation.and_)
 setattr(BufferFastAggregation, "or", BufferFastAggregation.or_)
 setattr(ParallelAggregation, "or", ParallelAggregation.or_)

@@ -203,3 +203,28 @@ def test_work_and_memory_shy_and_buffer_check():
     x = RoaringBitmap.bitmapOf(1, 2, 3)
     with pytest.raises(IllegalArgumentException):
         FastAggregation.workAndMemoryShyAnd(np.zeros(100, dtype=np.int64), x, x)
+
+
+def test_pairwise_op_codes_match_header():
+    """_lib.OP (the Python mirror's rbg_pairwise codes) equals the header's enum, including the buffer
+    package's and / andNot (RBG_AND_BUFFER / RBG_ANDNOT_BUFFER)."""
+    src = open(HEADER).read()
+    names = {"and": "RBG_AND", "or": "RBG_OR", "xor": "RBG_XOR", "andnot": "RBG_ANDNOT", "ior": "RBG_OR_INPLACE",
+             "and_buffer": "RBG_AND_BUFFER", "andnot_buffer": "RBG_ANDNOT_BUFFER"}
+    for k, c in names.items():
+        m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
+        assert m and int(m.group(1)) == L.OP[k], k
+
+
+def test_mutable_same_object_needs_no_device():
+    """MutableRoaringBitmap x1.and(x1) leaves x1, x1.andNot(x1) clears it
+    (RB/buffer/MutableRoaringBitmap.java:887, 919-922): answered on the host."""
+    from roaringbitmap_amd import MutableRoaringBitmap
+    buf = O.from_values(np.arange(0, 100000, 3))
+    x = MutableRoaringBitmap(buf)
+    getattr(x, "and")(x)
+    assert x.serialize() == buf
+    x.andNot(x)
+    assert x.isEmpty() and x.serialize() == bytes.fromhex("3a30000000000000")
+    with pytest.raises(NotImplementedError):
+        x.or_(x)
