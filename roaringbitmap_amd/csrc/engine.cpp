@@ -128,9 +128,14 @@ struct DevBuf {
   }
 };
 
+// runOptimize's device statistics (Batch::ro_stats): from byte 64 the k_runopt workgroups' partial
+// counts (4 u64 each), from ro_flags_off(groups) the per-bitmap run flags, computed only when the host
+// asks (ensure_stats).
+static size_t ro_flags_off(size_t groups) { return (64 + 32 * groups + 255) & ~(size_t)255; }
 struct Batch {
   bool live = false;
   bool key_major = false;  // containers sorted by (key, input); else by (input, key)
+  bool gapped = false;     // slots not back to back (runOptimize result: a hole after a shrunk container)
   bool packed = false;     // array payloads packed at 2 B granularity (C3 uniform synthetic
                            // batches): wide ops and fetches only
   size_t n_bm = 0, n_ctr = 0;
@@ -146,9 +151,10 @@ struct Batch {
   int32_t bsi_min = 0, bsi_max = 0;  // synthetic C5: min / max of the indexed values
   bool pair_cap_known = false;        // batched andCardinality: item capacity computed
   // made by runOptimize: kinds / payload bytes / run flags still in ro_stats (device: 5 u64 totals,
-  // then a u32 run flag per bitmap at +64) until ensure_stats reads them
+  // plan partial counts, run flags: ro_flags_off) until ensure_stats derives them
   bool stats_pending = false;
   DevBuf ro_stats;
+  size_t ro_groups = 0;  // plan workgroups whose partial counts ro_stats holds
   std::vector<uint8_t> h_has_run;
   // BSI compare over this batch (ebM = input 0): the task list (keys of ebM) and the per-key input
   // table, planned by the first query and kept (ctx_bsi)
@@ -193,8 +199,8 @@ struct Ctx {
   DevBuf ones;  // 8192 bytes of 0xFF: the full bitmap container of an in-place OR (k_ior_fix)
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   DevBuf order;                     // horizontal_*: chain order of every key segment
-  DevBuf ro_info, ro_size, ro_part, ro_flags;  // runOptimize scratch (kept: no allocation per call)
-  DevBuf rs_card, rs_keep, rs_bm;              // range selection scratch (with ro_info / ro_size / ro_part)
+  DevBuf ro_info, ro_size, ro_part;  // range selection scratch (kept: no allocation per call)
+  DevBuf rs_card, rs_keep, rs_bm;
   // device buffers of released batches kept for the next batch of a similar size (hipMalloc /
   // hipFree of a 0.36 GB payload cost more than runOptimize's kernels); bounded by kPoolMax
   std::vector<DevBuf> pool;
@@ -355,19 +361,22 @@ static int find_batch(Ctx* c, int32_t id, Batch** out) {
 // per-bitmap run flags) in device memory until something on the host needs them: read them then.
 static int ensure_stats(Ctx* c, Batch* b) {
   if (!b->stats_pending) return RBG_OK;
-  const size_t n = b->n_bm;
-  unsigned long long h[5] = {};
+  const size_t n = b->n_bm, g = b->ro_groups, foff = ro_flags_off(g);
+  uint32_t* flags = reinterpret_cast<uint32_t*>(b->ro_stats.as<uint8_t>() + foff);
+  if (n) {
+    HIPCHK(hipMemsetAsync(flags, 0, 4 * n, c->stream));
+    launch_runopt_flags(c->stream, b->desc.as<CDesc>(), b->bm.as<uint32_t>(), b->n_ctr, flags);
+  }
+  std::vector<unsigned long long> hs(8 + 4 * g);
   std::vector<uint32_t> hf(n);
-  HIPCHK(hipMemcpyAsync(h, b->ro_stats.p, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-  if (n) HIPCHK(hipMemcpyAsync(hf.data(), b->ro_stats.as<uint8_t>() + 64, 4 * n, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipMemcpyAsync(hs.data(), b->ro_stats.p, 8 * hs.size(), hipMemcpyDeviceToHost, c->stream));
+  if (n) HIPCHK(hipMemcpyAsync(hf.data(), flags, 4 * n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   b->stats_pending = false;
-  if (h[4] > b->payload_bytes) {  // payload_bytes holds the input's, a bound (a theorem; else a device error)
-    set_err("runOptimize: converted payload larger than its input");
-    return RBG_ERR_DEVICE;
-  }
+  unsigned long long h[4] = {0, 0, 0, 0};
+  for (size_t w = 0; w < g; w++)
+    for (int k = 0; k < 4; k++) h[k] += hs[8 + 4 * w + k];
   for (int k = 0; k < 3; k++) b->n_kind[k] = (int64_t)h[k];
-  b->payload_bytes = h[4];
   int64_t ser = (int64_t)h[3];
   b->h_has_run.assign(n, 0);
   for (size_t i = 0; i < n; i++) {
@@ -1512,7 +1521,8 @@ static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const in
     wa.payload = B->payload.as<uint8_t>();
     wa.skip = skip.empty() ? nullptr : c->skip.as<uint8_t>();
     wa.start_bm = start_bm;
-    wa.all_array = (B->n_kind[DK_B] == 0 && B->n_kind[DK_R] == 0) ? 1u : 0u;
+    // (the all-array path streams a key's slots as one run of values: they must be back to back)
+    wa.all_array = (B->n_kind[DK_B] == 0 && B->n_kind[DK_R] == 0 && !B->gapped) ? 1u : 0u;
     wa.slot32 = B->payload_bytes < (1ull << 36) ? 1u : 0u;
     wa.order = order;
     wa.chain = chain;
@@ -3178,12 +3188,8 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
   }
   hipStream_t s = c->stream;
   const size_t C = a->n_ctr, n = a->n_bm;
-  CHK(c->ro_info.ensure(4 * C + 16));
-  CHK(c->ro_size.ensure(8 * C + 16));
-  CHK(c->ro_part.ensure(8 * (scan_parts(C) + 1)));
-  // the new batch's buffers before any kernel: a conversion only happens when the new form is
-  // smaller, and its 16 B-rounded slot is no larger either, so the input's payload size bounds
-  // the output's -- plan, scan and write then run back to back with one host sync at the end
+  // one kernel: every container is written at its own slot offset (a conversion never makes a slot
+  // larger), so the new batch has the input's payload size and layout and nothing waits on the host
   const int32_t bid = new_batch(c);
   Batch& b = *c->batches[bid];
   struct Drop {  // an error below frees the half-built batch
@@ -3196,22 +3202,18 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
   } drop{c, bid};
   CHK(pool_take(c, b.desc, sizeof(CDesc) * C + 16));
   CHK(pool_take(c, b.payload, a->payload_bytes + 64));
-  CHK(pool_take(c, b.ro_stats, 64 + 4 * n + 16));
+  b.ro_groups = runopt_groups(C);
+  CHK(pool_take(c, b.ro_stats, ro_flags_off(b.ro_groups) + 4 * n + 16));
   CHK(pool_take(c, b.keys, a->keys.cap));
   CHK(pool_take(c, b.bm, a->bm.cap));
   CHK(pool_take(c, b.key_off, a->key_off.cap));
   CHK(pool_take(c, b.bm_off, a->bm_off.cap));
-  HIPCHK(hipMemsetAsync(b.ro_stats.p, 0, 64 + 4 * n + 16, s));
-  unsigned long long* tot = b.ro_stats.as<unsigned long long>();
-  launch_runopt_plan(s, a->desc.as<CDesc>(), a->bm.as<uint32_t>(), a->payload.as<uint8_t>(), C,
-                     c->ro_info.as<uint32_t>(), c->ro_size.as<uint64_t>(), b.ro_stats.as<uint32_t>() + 16, tot);
-  launch_exclusive_scan(s, c->ro_size.as<uint64_t>(), c->ro_size.as<uint64_t>(), C, c->ro_part.as<uint64_t>(),
-                        reinterpret_cast<uint64_t*>(tot + 4));
   const RoCopy cp{a->keys.as<uint16_t>(), b.keys.as<uint16_t>(), a->bm.as<uint32_t>(), b.bm.as<uint32_t>(),
                   a->key_off.as<uint32_t>(), b.key_off.as<uint32_t>(), a->key_off.cap / 4,
                   a->bm_off.as<uint32_t>(), b.bm_off.as<uint32_t>(), a->bm_off.cap / 4};
-  launch_runopt_write(s, a->desc.as<CDesc>(), a->payload.as<uint8_t>(), C, c->ro_info.as<uint32_t>(),
-                      c->ro_size.as<uint64_t>(), b.desc.as<CDesc>(), b.payload.as<uint8_t>(), cp);
+  if (C)
+    launch_runopt(s, a->desc.as<CDesc>(), a->payload.as<uint8_t>(), C, b.desc.as<CDesc>(), b.payload.as<uint8_t>(), cp,
+                  b.ro_stats.as<unsigned long long>() + 8);
   HIPCHK(hipGetLastError());
   // no host read-back here: the new batch's statistics stay on the device until needed (ensure_stats)
   b.n_bm = n;
@@ -3223,7 +3225,8 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
   b.long_card = a->long_card;
   b.bsi_min = a->bsi_min;
   b.bsi_max = a->bsi_max;
-  b.payload_bytes = a->payload_bytes;  // a bound until ensure_stats reads the real size
+  b.payload_bytes = a->payload_bytes;  // the input's layout (holes after shrunk containers)
+  b.gapped = a->gapped || a->n_kind[DK_R] > 0;  // only R -> A can leave an all-array batch with holes
   b.max_ser = 0;  // runOptimize leaves no container above 8194 serialized bytes
   b.ser_bytes = a->ser_bytes ? 1 : 0;  // nonzero: computed by ensure_stats
   b.stats_pending = true;

@@ -396,10 +396,6 @@ void launch_synth_c2(hipStream_t s, uint64_t seed, int force, CDesc* desc, uint1
 uint64_t scan_parts(uint64_t n);
 void launch_exclusive_scan(hipStream_t s, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* part,
                            uint64_t* total);
-// info[i] = new kind | changed << 2 | nruns << 3; size[i] = new slot bytes; bm_has_run[bitmap] = 1
-// where an R container results; totals = {#A, #B, #R, serialized payload bytes}
-void launch_runopt_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
-                        uint32_t* info, uint64_t* size, uint32_t* bm_has_run, unsigned long long* totals);
 // the arrays the new batch shares with the input (keys, input index, key CSR, bitmap CSR), copied by
 // the write kernel
 struct RoCopy {
@@ -414,8 +410,14 @@ struct RoCopy {
   uint32_t* out_boff;
   uint64_t n_boff;
 };
-void launch_runopt_write(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, const uint32_t* info,
-                         const uint64_t* off, CDesc* out_desc, uint8_t* out_payload, RoCopy cp);
+// runOptimize of every container, each written at its own slot offset of the new payload (the input's
+// layout; a converted container is never larger); per workgroup g (of runopt_groups(n)) wstat[4 g + k] =
+// {#A, #B, #R, serialized payload bytes} of its containers
+uint64_t runopt_groups(uint64_t n);
+void launch_runopt(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, CDesc* out_desc,
+                   uint8_t* out_payload, RoCopy cp, unsigned long long* wstat);
+// flags[bitmap] = 1 where the (new) batch holds a run container; flags zeroed by the caller
+void launch_runopt_flags(hipStream_t s, const CDesc* desc, const uint32_t* bm, uint64_t n, uint32_t* flags);
 
 // runopt.hip: selectRangeWithoutCopy of every bitmap of a batch (range-restricted aggregations): the
 // range's first / last key and low bits (lbs..lbl kept on those keys)

@@ -2,18 +2,16 @@
 // (RB/RoaringBitmap.java:2764-2774), and the device-wide exclusive scan it (and
 // the header decode) places slots with.
 //
-//   k_runopt_plan  : one wave per container decides the container's new type
-//                    and slot size, without materialising it:
-//                      A -> R iff 2 card > 2 + 4 nruns  (RB/ArrayContainer.java:1085-1099),
-//                           nruns counted on the sorted values themselves;
-//                      B -> R iff 2 + 4 nruns < 8192    (RB/BitmapContainer.java:1218-1237);
-//                      R -> toEfficientContainer        (RB/RunContainer.java:2083-2085, 2326-2335)
-//                           on the stored run count, as the reference does.
-//   scan           : exclusive scan of the new slot sizes -> slot offsets
-//   k_runopt_write : one wave per container: an unchanged container's slot is
-//                    copied verbatim (R kept as R is the reference's `return this`);
-//                    a converted one is materialised in registers and staged
-//                    through the wave's LDS into its new slot.
+//   k_runopt : one wave per container decides the container's new type
+//                A -> R iff 2 card > 2 + 4 nruns  (RB/ArrayContainer.java:1085-1099),
+//                     nruns counted on the sorted values themselves;
+//                B -> R iff 2 + 4 nruns < 8192    (RB/BitmapContainer.java:1218-1237);
+//                R -> toEfficientContainer        (RB/RunContainer.java:2083-2085, 2326-2335)
+//                     on the stored run count, as the reference does;
+//              and writes it at its own slot offset in the new batch: an unchanged
+//              container's slot is copied verbatim (R kept as R is the reference's
+//              `return this`), a converted one is materialised in registers and
+//              staged through the wave's LDS.
 #include <algorithm>
 
 #include "kernels.hpp"
@@ -101,11 +99,47 @@ __global__ __launch_bounds__(256) void k_scan_apply(const uint64_t* in, uint64_t
   }
 }
 
+// k_scan_apply with the tile prefix summed by the tile itself (up to kScanDirect tiles: at most 16 loads
+// per thread), so no k_scan_partials launch; the last tile writes the total
+constexpr uint64_t kScanDirect = 16 * NT;
+__global__ __launch_bounds__(256) void k_scan_apply_direct(const uint64_t* in, uint64_t n,
+                                                           const uint64_t* __restrict__ part, uint64_t* out,
+                                                           uint64_t* __restrict__ total) {
+  __shared__ uint64_t sh4[4];
+  uint64_t pre = 0;
+  for (uint64_t j = threadIdx.x; j < blockIdx.x; j += NT) pre += part[j];
+  uint64_t pre_sum;
+  block_excl_u64(pre, sh4, &pre_sum);  // the sum over the block: the tile's prefix
+  pre = pre_sum;
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+  uint64_t v[kScanPer];
+  uint64_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < kScanPer; j++) {
+    v[j] = base + j < n ? in[base + j] : 0;
+    sum += v[j];
+  }
+  uint64_t tot;
+  uint64_t run = pre + block_excl_u64(sum, sh4, &tot);
+#pragma unroll
+  for (int j = 0; j < kScanPer; j++) {
+    if (base + j < n) out[base + j] = run;
+    run += v[j];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *total = pre + tot;
+}
+
 uint64_t scan_parts(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
 
 void launch_exclusive_scan(hipStream_t s, const uint64_t* in, uint64_t* out, uint64_t n, uint64_t* part,
                            uint64_t* total) {
   const uint64_t np = scan_parts(n);
+  if (np && np <= kScanDirect) {  // two launches: tile totals, then each tile sums its predecessors itself
+    hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)np), dim3(NT), 0, s, in, n, part);
+    hipLaunchKernelGGL(k_scan_apply_direct, dim3((unsigned)np), dim3(NT), 0, s, in, n, (const uint64_t*)part, out,
+                       total);
+    return;
+  }
   if (np) hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)np), dim3(NT), 0, s, in, n, part);
   hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(NT), 0, s, part, np, total);
   if (np) hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)np), dim3(NT), 0, s, in, n, (const uint64_t*)part, out);
@@ -150,64 +184,19 @@ __device__ __forceinline__ int array_runs(const uint8_t* slot, int card) {
   return (int)uni((uint32_t)wave_sum_i(c));
 }
 
-// info word: kind | changed << 2 | nruns << 3
-__global__ __launch_bounds__(256) void k_runopt_plan(const CDesc* __restrict__ desc, const uint32_t* __restrict__ bm,
-                                                     const uint8_t* __restrict__ payload, uint64_t n,
-                                                     uint32_t* __restrict__ info, uint64_t* __restrict__ size,
-                                                     uint32_t* __restrict__ bm_has_run,
-                                                     unsigned long long* __restrict__ totals) {
-  const uint64_t nw = (uint64_t)gridDim.x * 4;
-  uint64_t cnt[3] = {0, 0, 0}, ser = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
-    const CDesc d = desc[i];
-    const uint8_t* slot = payload + d.slot;
-    const int card = (int)d.card;
-    int nruns, kind;
-    if (d.kind == DK_A) {
-      nruns = array_runs(slot, card);
-      kind = 2 * card > 2 + 4 * nruns ? DK_R : DK_A;
-    } else if (d.kind == DK_B) {
-      WCtr x;
-      w_load_bitmap(slot, x);
-      nruns = w_runs(x);
-      kind = 2 + 4 * nruns < 8192 ? DK_R : DK_B;
-    } else {
-      nruns = *reinterpret_cast<const uint16_t*>(slot + 2);
-      kind = eff(card, nruns);
-    }
-    const uint32_t len = kind == DK_A ? 2u * card : kind == DK_B ? 8192u : 2u + 4u * nruns;
-    if (lane_id() == 0) {
-      info[i] = (uint32_t)kind | ((kind != d.kind) ? 4u : 0u) | ((uint32_t)nruns << 3);
-      size[i] = slot_size_of(kind, len);
-      // one bitmap can own every container: read before writing, so the flag's line
-      // takes a few stores rather than one per run container
-      if (kind == DK_R) {
-        uint32_t* f = bm_has_run + bm[i];
-        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) *f = 1;
-      }
-    }
-    cnt[kind]++;
-    ser += len;
-  }
-  // workgroup totals, one atomic per counter per workgroup
-  __shared__ unsigned long long wsum[4][4];
-  if (lane_id() == 0) {
-    for (int k = 0; k < 3; k++) wsum[threadIdx.x >> 6][k] = cnt[k];
-    wsum[threadIdx.x >> 6][3] = ser;
-  }
-  __syncthreads();
-  if (threadIdx.x < 4) {
-    const unsigned long long v =
-        wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] + wsum[3][threadIdx.x];
-    if (v) atomicAdd(&totals[threadIdx.x], v);
-  }
-}
-
-__global__ __launch_bounds__(256) void k_runopt_write(const CDesc* __restrict__ desc,
-                                                         const uint8_t* __restrict__ payload, uint64_t n,
-                                                         const uint32_t* __restrict__ info,
-                                                         const uint64_t* __restrict__ off, CDesc* __restrict__ out_desc,
-                                                         uint8_t* __restrict__ out_payload, RoCopy cp) {
+// runOptimize in one pass (one wave per container).  Every container keeps its slot offset: a
+// conversion only happens when the new form is smaller, and its 16 B-rounded slot is then no larger
+// than the old one (A -> R iff 2 card > 2 + 4 nruns, so 4 + 4 nruns <= 2 card; B -> R iff
+// 2 + 4 nruns < 8192, so 4 + 4 nruns <= 8192; R -> A / B only where EFF finds them smaller), so the
+// new batch takes the input's layout, with a hole after each shrunk container, and needs no size scan
+// between deciding a type and writing it.  A bitmap is decided from registers and, if it stays a
+// bitmap, stored from them (read once).  Per workgroup g, wstat[4 g + k] = its containers of kind k
+// (k < 3) and their serialized payload bytes (k = 3): plain stores, nothing to zero first; the batch's
+// totals and run flags are derived only when the host asks (k_runopt_flags, ensure_stats).
+__global__ __launch_bounds__(256) void k_runopt(const CDesc* __restrict__ desc, const uint8_t* __restrict__ payload,
+                                                uint64_t n, CDesc* __restrict__ out_desc,
+                                                uint8_t* __restrict__ out_payload, RoCopy cp,
+                                                unsigned long long* __restrict__ wstat) {
   __shared__ __align__(16) uint32_t lds_all[4][2048];
   uint32_t* lds = lds_all[threadIdx.x >> 6];
   const int lane = lane_id();
@@ -223,55 +212,95 @@ __global__ __launch_bounds__(256) void k_runopt_write(const CDesc* __restrict__ 
     for (uint64_t i = g; i < cp.n_koff; i += gs) cp.out_koff[i] = cp.koff[i];
     for (uint64_t i = g; i < cp.n_boff; i += gs) cp.out_boff[i] = cp.boff[i];
   }
+  uint64_t cnt[3] = {0, 0, 0}, ser = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < n; i += nw) {
     const CDesc d = desc[i];
-    const uint32_t inf = info[i];
-    const int kind = (int)(inf & 3);
-    const uint64_t o = off[i];
-    uint8_t* dst = out_payload + o;
-    if (!(inf & 4)) {  // unchanged: the slot as it is (A padding included)
-      const uint32_t nr = inf >> 3;
-      const uint32_t len = kind == DK_A ? 2u * d.card : kind == DK_B ? 8192u : 2u + 4u * nr;
-      const uint32_t nvec = (uint32_t)(slot_size_of(kind, len) >> 4);
-      const uint4* sv = reinterpret_cast<const uint4*>(payload + d.slot);
-      uint4* dv = reinterpret_cast<uint4*>(dst);
-      for (uint32_t j = lane; j < nvec; j += 64) dv[j] = sv[j];
+    const uint8_t* slot = payload + d.slot;
+    uint8_t* dst = out_payload + d.slot;
+    const int card = (int)d.card;
+    int nruns, kind;
+    WCtr x;
+    if (d.kind == DK_A) {
+      nruns = array_runs(slot, card);
+      kind = 2 * card > 2 + 4 * nruns ? DK_R : DK_A;
+    } else if (d.kind == DK_B) {
+      w_load_bitmap(slot, x);
+      nruns = w_runs(x);
+      kind = 2 + 4 * nruns < 8192 ? DK_R : DK_B;
     } else {
-      WCtr x;
-      w_materialize(d, payload, lds, x);
-      if (kind == DK_B) {
-        w_store_bitmap(dst, x);
-      } else {
-        uint32_t copy = w_stage(kind, x, (int)d.card, lds);
-        if (kind == DK_A) {  // pad the slot to 16 B with the last value (batch layout)
-          uint16_t* st = reinterpret_cast<uint16_t*>(lds);
-          const uint32_t c = d.card, padded = (2u * c + 15) & ~15u;
-          const uint16_t last = st[c - 1];
-          for (uint32_t j = c + lane; j < padded / 2; j += 64) st[j] = last;
-          wsync();
-          copy = padded;
-        }
-        copy_lds_to_global<64>(dst + (kind == DK_R ? 2 : 0), lds, copy, lane);
+      nruns = *reinterpret_cast<const uint16_t*>(slot + 2);
+      kind = eff(card, nruns);
+    }
+    const uint32_t len = kind == DK_A ? 2u * card : kind == DK_B ? 8192u : 2u + 4u * nruns;
+    if (kind == DK_B) {  // B kept, or R -> B
+      if (d.kind != DK_B) w_materialize(d, payload, lds, x);
+      w_store_bitmap(dst, x);
+      wsync();
+    } else if (kind == d.kind) {  // A or R kept: the slot as it is (A padding included)
+      const uint32_t nvec = (uint32_t)(slot_size_of(kind, len) >> 4);
+      const uint4* sv = reinterpret_cast<const uint4*>(slot);
+      uint4* dv = reinterpret_cast<uint4*>(dst);
+      uint32_t j = lane;
+      for (; j + 192 < nvec; j += 256) {  // four vectors per lane requested before any is stored
+        const uint4 a0 = sv[j], a1 = sv[j + 64], a2 = sv[j + 128], a3 = sv[j + 192];
+        dv[j] = a0;
+        dv[j + 64] = a1;
+        dv[j + 128] = a2;
+        dv[j + 192] = a3;
       }
+      for (; j < nvec; j += 64) dv[j] = sv[j];
+    } else {  // A -> R, B -> R, R -> A: staged through the wave's LDS
+      if (d.kind != DK_B) w_materialize(d, payload, lds, x);
+      uint32_t copy = w_stage(kind, x, card, lds);
+      if (kind == DK_A) {  // pad the slot to 16 B with the last value (batch layout)
+        uint16_t* st = reinterpret_cast<uint16_t*>(lds);
+        const uint32_t c = d.card, padded = (2u * c + 15) & ~15u;
+        const uint16_t last = st[c - 1];
+        for (uint32_t q = c + lane; q < padded / 2; q += 64) st[q] = last;
+        wsync();
+        copy = padded;
+      }
+      copy_lds_to_global<64>(dst + (kind == DK_R ? 2 : 0), lds, copy, lane);
       wsync();
     }
-    if (lane == 0) out_desc[i] = CDesc{o, d.card, d.key, (uint8_t)kind, d.flags};
+    if (lane == 0) out_desc[i] = CDesc{d.slot, d.card, d.key, (uint8_t)kind, d.flags};
+    cnt[kind]++;
+    ser += len;
+  }
+  __shared__ unsigned long long wsum[4][4];
+  if (lane == 0) {
+    for (int k = 0; k < 3; k++) wsum[threadIdx.x >> 6][k] = cnt[k];
+    wsum[threadIdx.x >> 6][3] = ser;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4)
+    wstat[4 * (uint64_t)blockIdx.x + threadIdx.x] =
+        wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] + wsum[3][threadIdx.x];
+}
+
+// per-bitmap run flags of a runOptimize result (its new descriptors): flag[bm] = 1 if any container
+// of the bitmap is a run container (read before write: one bitmap can own every container)
+__global__ __launch_bounds__(256) void k_runopt_flags(const CDesc* __restrict__ desc, const uint32_t* __restrict__ bm,
+                                                      uint64_t n, uint32_t* __restrict__ flags) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (desc[i].kind != DK_R) continue;
+    uint32_t* f = flags + bm[i];
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) *f = 1;
   }
 }
 
-void launch_runopt_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
-                        uint32_t* info, uint64_t* size, uint32_t* bm_has_run, unsigned long long* totals) {
-  if (!n) return;
-  const uint64_t g = std::min<uint64_t>((n + 3) / 4, 2048);
-  hipLaunchKernelGGL(k_runopt_plan, dim3((unsigned)g), dim3(256), 0, s, desc, bm, payload, n, info, size, bm_has_run,
-                     totals);
+uint64_t runopt_groups(uint64_t n) { return std::max<uint64_t>(1, std::min<uint64_t>((n + 3) / 4, 8192)); }
+
+void launch_runopt(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, CDesc* out_desc,
+                   uint8_t* out_payload, RoCopy cp, unsigned long long* wstat) {
+  hipLaunchKernelGGL(k_runopt, dim3((unsigned)runopt_groups(n)), dim3(256), 0, s, desc, payload, n, out_desc,
+                     out_payload, cp, wstat);
 }
 
-void launch_runopt_write(hipStream_t s, const CDesc* desc, const uint8_t* payload, uint64_t n, const uint32_t* info,
-                         const uint64_t* off, CDesc* out_desc, uint8_t* out_payload, RoCopy cp) {
-  const uint64_t g = std::max<uint64_t>(1, std::min<uint64_t>((n + 3) / 4, 8192));
-  hipLaunchKernelGGL(k_runopt_write, dim3((unsigned)g), dim3(256), 0, s, desc, payload, n, info, off, out_desc,
-                     out_payload, cp);
+void launch_runopt_flags(hipStream_t s, const CDesc* desc, const uint32_t* bm, uint64_t n, uint32_t* flags) {
+  if (!n) return;
+  const uint64_t g = std::min<uint64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(k_runopt_flags, dim3((unsigned)g), dim3(256), 0, s, desc, bm, n, flags);
 }
 
 // ---------------------------------------------------------------------------

@@ -146,3 +146,36 @@ def test_engine_run_optimize_without_readback(gpu):
     assert e.batch_fetch(oc).serialize() == exp_a and ans == [_answer(exp_a)]
     for x in (a, b, oa, ob, oc):
         e.release(x)
+
+
+def test_all_array_result_with_holes(gpu):
+    """runOptimize writes every container at its own slot offset, so an R -> A conversion leaves a hole
+    after the new array.  A batch of arrays and such run containers becomes all-array with holes: the
+    wide OR must not take the back-to-back value stream over it (Batch::gapped), and its bytes equal the
+    oracle's naive_or of the optimized inputs."""
+    from _fmt import A, R, encode
+    from roaringbitmap_amd import Engine
+    rng = np.random.default_rng(31)
+    bufs = []
+    for i in range(6):
+        ctrs = []
+        for k in range(8):
+            if (i + k) % 2:  # one-value runs: R -> A (2 card < 2 + 4 nruns)
+                ctrs.append((k, R, np.arange(3 * i + k, 3 * i + k + 400, 2)))
+            else:
+                ctrs.append((k, A, np.sort(rng.choice(65536, int(rng.integers(1, 3000)), replace=False))))
+        bufs.append(encode(ctrs))
+    e = Engine(0)
+    try:
+        a = e.load(bufs)
+        o, _ = e.run_optimize(a, answers=False)
+        e.wide("or", o)
+        opt = [O.run_optimize(b) for b in bufs]
+        assert all(O.stats(b)["run"] == 0 and O.stats(b)["bitmap"] == 0 for b in opt)
+        assert e.fetch().serialize() == O.wide("or", opt)
+        e.wide("xor", o)
+        assert e.fetch().serialize() == O.wide("xor", opt)
+        got = e.batch_fetch_range(o)
+        assert [g.serialize() for g in got] == opt
+    finally:
+        e.close()
