@@ -1007,6 +1007,10 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   // RBG_PW_BALANCE=0: the direct form, tasks in key order)
   const char* bal_env = getenv("RBG_PW_BALANCE");
   const bool balanced = direct && (!bal_env || atoi(bal_env) != 0);
+  // ... run by one 16-wave workgroup per CU that claims the CU's tasks through LDS (k_pair_cu;
+  // RBG_PW_CU=0: one static walk per wave, k_pair_wave<..., 2>)
+  const char* cu_env = getenv("RBG_PW_CU");
+  const bool cu_pool = balanced && (!cu_env || atoi(cu_env) != 0);
   if (balanced)
     launch_plan_balanced(s, plan_op, card_only ? 1 : 0, key_lo, (uint32_t)nkeys, A->key_off.as<uint32_t>(), da,
                          A->payload.as<uint8_t>(), B->key_off.as<uint32_t>(), db, B->payload.as<uint8_t>(),
@@ -1017,7 +1021,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   const int grid = grid_for(((direct ? nkeys : ub) + 3) / 4, 16384);
   launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(),
                   A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), oc, c->task_card.as<uint32_t>(),
-                  direct ? &pd : nullptr, balanced);
+                  direct ? &pd : nullptr, balanced, cu_pool);
   dbg(s, "pairwise");
   c->mark(2);
   if (card_only) {

@@ -258,9 +258,11 @@ struct PwDirect {
 };
 // direct: null = tasks / nt from launch_plan_pairwise; balanced (with direct): tasks / nt[0..1] from
 // launch_plan_balanced, records at key positions (direct->key_lo)
+// balanced: k_plan_balanced's list (dense ranges); cu_pool: that list run by k_pair_cu (one 16-wave
+// workgroup per CU, tasks claimed from the CU's share) instead of the static per-wave walk
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
                      const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct,
-                     bool balanced = false);
+                     bool balanced = false, bool cu_pool = false);
 // dense key ranges: every key's task resolved and ordered by estimated cost within its 256-key segment
 // (heaviest first, rotated by the segment index) into tasks[]; n_tasks[0] = n_tasks[1] = nkeys (records
 // and list positions, one per key: keys without a task are marked, with an empty record / a zero count)

@@ -221,8 +221,9 @@ __global__ __launch_bounds__(256) void k_plan_balanced(int key_lo, uint32_t nkey
 
 constexpr int kWaves = 4;  // waves per workgroup
 // u32 words of LDS per wave: the 8 KiB bitmap map / staging area, plus room for
-// the run lists of run-domain R AND R (4 waves x 10 KiB x 4 workgroups = 160 KiB)
-constexpr int kWaveLds = 2560;
+// the run lists of run-domain R AND R (4 waves x 10 KiB x 4 workgroups = 160 KiB; two words
+// short of 10 KiB, so that k_pair_cu's 16 waves and its task counter fit one CU's 160 KiB)
+constexpr int kWaveLds = 2558;
 static_assert(kWaveLds >= 2048, "the 8 KiB bitmap map / staging area");
 
 // Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
@@ -234,11 +235,11 @@ static_assert(kWaveLds >= 2048, "the 8 KiB bitmap map / staging area");
 // task, no atomics, so the kernel runs at production speed.
 #if RBG_WAVE_PROBE
 __device__ uint4 g_probe[3 * 16384];
-__device__ __forceinline__ void probe_store(uint64_t r0, uint64_t m0, uint32_t ntask) {
+__device__ __forceinline__ void probe_store(uint64_t r0, uint64_t m0, uint32_t ntask,
+                                            uint32_t wid = blockIdx.x * 4 + (threadIdx.x >> 6)) {
   const uint64_t r1 = __builtin_amdgcn_s_memrealtime(), m1 = __builtin_amdgcn_s_memtime();
   uint32_t xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  const uint32_t wid = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (lane_id() == 0 && wid < 16384) {
     g_probe[3 * wid] = make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32));
     g_probe[3 * wid + 1] = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)(m1 >> 32));
@@ -677,8 +678,22 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
     // at band t0 mod nb (only the last band can be short)
     const uint32_t nb = (nt + stride - 1) / stride;
     const uint32_t b0 = t0 % nb;
+#ifndef RBG_BAL_WALK
+#define RBG_BAL_WALK 0
+#endif
+    // RBG_BAL_WALK (experiment builds): 0 every band in a per-wave rotated order; 1 the heavy half's
+    // bands rotated, then the light half's (longest first between halves); 2 heaviest band first
     auto pos_of = [&](uint32_t k) -> uint32_t {
-      const uint32_t b = b0 + k < nb ? b0 + k : b0 + k - nb;
+      uint32_t b;
+      if (RBG_BAL_WALK == 2) {
+        b = k;
+      } else if (RBG_BAL_WALK == 1) {
+        const uint32_t h = (nb + 1) / 2;
+        if (k < h) b = (b0 + k) % h;
+        else b = h + (b0 + k - h) % (nb - h);
+      } else {
+        b = b0 + k < nb ? b0 + k : b0 + k - nb;
+      }
       return b * stride + t0;
     };
     uint32_t k = 0;
@@ -806,9 +821,87 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 #endif
 }
 
+// ---------------------------------------------------------------------------
+// Balanced list, one workgroup of 16 waves per CU (the CU's whole LDS), the CU's tasks claimed
+// through an LDS counter.  The per-wave probe showed each CU's waves ending 50-60 us apart with
+// equal work: the issue arbiter favours older waves, so the youngest workgroups of a CU form the
+// tail.  Here the 16 waves of a CU drain one pool, so a wave that loses arbitration simply runs
+// fewer tasks and the CU ends with its last task, not with its slowest wave.  CU b owns positions
+// 16 b + w (w < 16) of every band of S = 16 x grid list positions: 16 consecutive cost ranks per
+// band, every rank once over the bands (k_plan_balanced's layout).  Claim k takes
+//   RBG_CU_ORDER 0: band (k mod nb + b) mod nb, slot k / nb  -- the CU's waves on different bands;
+//   RBG_CU_ORDER 1: band (k / 16 + b) mod nb, slot k mod 16 -- the CU's heaviest ranks first.
+// A claim is one LDS atomic; the next task is claimed and its record requested while a task runs.
+// ---------------------------------------------------------------------------
+#ifndef RBG_CU_ORDER
+#define RBG_CU_ORDER 0
+#endif
+constexpr int kCuWaves = 16;
+static_assert(kCuWaves * kWaveLds * 4 + 16 <= 163840, "16 waves and the counter in one CU's LDS");
+template <int OP, int MODE>
+__global__ __launch_bounds__(1024, 1) void k_pair_cu(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                                     const uint8_t* pa, const uint8_t* pb, OutCtx oc,
+                                                     uint32_t* __restrict__ task_card, PwDirect dsrc) {
+  __shared__ __align__(16) uint32_t lds_all[kCuWaves][kWaveLds];
+  __shared__ uint32_t ctr;
+  if (threadIdx.x == 0) ctr = 0;
+  __syncthreads();
+  const uint32_t nt = uni(n_tasks[1]);
+  uint32_t* lds = lds_all[threadIdx.x >> 6];
+  const uint32_t S = gridDim.x * kCuWaves;
+  const uint32_t nb = (nt + S - 1) / S;
+  const uint32_t total = nb * kCuWaves, base = blockIdx.x * kCuWaves;
+  auto pos_of = [&](uint32_t k) -> uint32_t {
+    const uint32_t band = RBG_CU_ORDER == 1 ? (k / kCuWaves + blockIdx.x) % nb : (k % nb + blockIdx.x) % nb;
+    const uint32_t w = RBG_CU_ORDER == 1 ? k % kCuWaves : k / nb;
+    return band * S + base + w;
+  };
+  auto claim = [&]() -> uint32_t {  // the next claim whose position holds a list entry
+    uint32_t k;
+    do {
+      uint32_t v = 0;
+      if (lane_id() == 0) v = atomicAdd(&ctr, 1u);
+      k = uni(v);
+    } while (k < total && pos_of(k) >= nt);
+    return k;
+  };
+  uint32_t k = claim();
+  if (k >= total) return;
+#if RBG_STAMPS
+  StampAcc sacc = {};
+#endif
+#if RBG_WAVE_PROBE
+  const uint64_t pr0 = __builtin_amdgcn_s_memrealtime(), pm0 = __builtin_amdgcn_s_memtime();
+  uint32_t ntask = 0;
+#endif
+  PTask cur = load_task(tasks, pos_of(k));
+  for (;;) {
+    const uint32_t kn = claim();
+    PTask nxt;
+    if (kn < total) nxt = load_task(tasks, pos_of(kn));  // in flight while this task runs
+    if (cur.kind_a != kAbsent || cur.kind_b != kAbsent) {  // marked: no task (the plan wrote its record)
+      any_task<OP, MODE>((uint32_t)cur.key - (uint32_t)dsrc.key_lo, cur, pa, pb, oc, task_card, lds SACC_ARG);
+#if RBG_WAVE_PROBE
+      ntask++;
+#endif
+    }
+    if (kn >= total) break;
+    cur = nxt;
+  }
+#if RBG_WAVE_PROBE
+  probe_store(pr0, pm0, ntask, blockIdx.x * kCuWaves + (threadIdx.x >> 6));
+#endif
+}
+
 template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                      const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced) {
+                      const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced,
+                      bool cu_pool) {
+  if (direct && balanced && cu_pool) {  // one workgroup per CU, all of them resident
+    const int g = std::max(1, resident_grid((const void*)&k_pair_cu<OP, MODE>));
+    hipLaunchKernelGGL((k_pair_cu<OP, MODE>), dim3(g), dim3(1024), 0, s, tasks, nt, pa, pb, oc, task_card, *direct);
+    return;
+  }
   if (direct && balanced) {
     const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, 2>)));
     hipLaunchKernelGGL((k_pair_wave<OP, MODE, 2>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
@@ -903,10 +996,11 @@ void launch_plan_pairwise(hipStream_t s, int op, int key_lo, int key_hi, const u
 }
 
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                     const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced) {
-#define RBG_LPW(O)                                                                             \
-  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced); \
-  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced);
+                     const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced,
+                     bool cu_pool) {
+#define RBG_LPW(O)                                                                                      \
+  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced, cu_pool); \
+  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced, cu_pool);
   switch (op) {
     case OP_AND: RBG_LPW(OP_AND) break;
     case OP_OR: RBG_LPW(OP_OR) break;

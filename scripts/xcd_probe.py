@@ -27,7 +27,7 @@ for rnd in range(3):
     e.profile(0)
     times.append(ph[1] / max(k, 1))
 tag = os.environ.get("RBG_LIB", "default")
-print(f"lib={os.path.basename(tag)} k_pair_wave<AND,0,direct> ms per launch (3 x 20 launches): "
+print(f"lib={os.path.basename(tag)} RBG_PW_CU={os.environ.get('RBG_PW_CU', 'default')} C2 AND compute kernel ms per launch (3 x 20 launches): "
       + " ".join(f"{t:.4f}" for t in times), flush=True)
 if "probe" in tag:
     buf = (ctypes.c_uint64 * 20)()
@@ -55,7 +55,9 @@ if "probe" in tag:
         end_us = (r1 - base).astype(np.float64) / 100.0
         life_us = (r1 - r0).astype(np.float64) / 100.0
         print(f"launch {rep}: {live.sum()} waves, last wave end {end_us.max():.1f} us after the first start, "
-              f"starts spread {float((r0.max() - base)) / 100.0:.1f} us", flush=True)
+              f"starts spread {float((r0.max() - base)) / 100.0:.1f} us; wave end p10 / p50 / p90 / p99 "
+              + " / ".join(f"{np.percentile(end_us, q):.1f}" for q in (10, 50, 90, 99)) + " us; tasks per wave "
+              f"min {int(ntask.min())} max {int(ntask.max())}", flush=True)
         for x in range(8):
             m = xcc == x
             if not m.any():

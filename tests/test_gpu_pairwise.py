@@ -305,15 +305,17 @@ def test_dense_key_range_direct_mode(gpu, seed):
     e.release(bb)
 
 
-@pytest.mark.parametrize("balance", ["0", "1"])
+@pytest.mark.parametrize("balance,cu", [("0", "0"), ("1", "0"), ("1", "1")])
 @pytest.mark.parametrize("seed", range(3))
-def test_dense_range_task_orders(gpu, seed, balance, monkeypatch):
-    """Dense key ranges in both task orders: key order (RBG_PW_BALANCE=0, the direct form) and binned by
+def test_dense_range_task_orders(gpu, seed, balance, cu, monkeypatch):
+    """Dense key ranges in every task order: key order (RBG_PW_BALANCE=0, the direct form), binned by
     estimated cost (k_plan_balanced: the task list out of key order, records still at key positions,
-    empty records / zero counts for keys without a task).  Every op, the key-range form and
-    andCardinality over a range that covers every key, against the oracle."""
+    empty records / zero counts for keys without a task) with one static walk per wave (RBG_PW_CU=0)
+    or claimed per CU (k_pair_cu).  Every op, the key-range form and andCardinality over a range that
+    covers every key, against the oracle."""
     from roaringbitmap_amd import Engine
     monkeypatch.setenv("RBG_PW_BALANCE", balance)
+    monkeypatch.setenv("RBG_PW_CU", cu)
     rng = np.random.default_rng(4100 + seed)
     n = int(rng.integers(300, 1500))
     keys = np.arange(n)
