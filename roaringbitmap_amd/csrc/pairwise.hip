@@ -830,8 +830,11 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 // 16 b + w (w < 16) of every band of S = 16 x grid list positions: 16 consecutive cost ranks per
 // band, every rank once over the bands (k_plan_balanced's layout).  Claim k takes
 //   RBG_CU_ORDER 0: band (k mod nb + b) mod nb, slot k / nb  -- the CU's waves on different bands;
-//   RBG_CU_ORDER 1: band (k / 16 + b) mod nb, slot k mod 16 -- the CU's heaviest ranks first.
+//   RBG_CU_ORDER 1: band (k / 16 + b) mod nb, slot k mod 16 -- the CU's heaviest ranks first;
+//   RBG_CU_ORDER 2: band (b - k) mod nb, slot k / nb -- as 0, each round of nb claims heavy to light.
 // A claim is one LDS atomic; the next task is claimed and its record requested while a task runs.
+// (Shared pools of the last 1 / 2 / 4 bands across CUs, claimed by agent-scope atomics, made the
+// kernel 0.23 -> 0.34 / 0.44 / 0.60 ms: profiles/r05/experiments/c2_cu_tail_pools.txt.)
 // ---------------------------------------------------------------------------
 #ifndef RBG_CU_ORDER
 #define RBG_CU_ORDER 0
@@ -852,21 +855,24 @@ __global__ __launch_bounds__(1024, 1) void k_pair_cu(const PTask* __restrict__ t
   const uint32_t nb = (nt + S - 1) / S;
   const uint32_t total = nb * kCuWaves, base = blockIdx.x * kCuWaves;
   auto pos_of = [&](uint32_t k) -> uint32_t {
-    const uint32_t band = RBG_CU_ORDER == 1 ? (k / kCuWaves + blockIdx.x) % nb : (k % nb + blockIdx.x) % nb;
+    const uint32_t band = RBG_CU_ORDER == 1   ? (k / kCuWaves + blockIdx.x) % nb
+                          : RBG_CU_ORDER == 2 ? (blockIdx.x % nb + nb - k % nb) % nb
+                                              : (k % nb + blockIdx.x) % nb;
     const uint32_t w = RBG_CU_ORDER == 1 ? k % kCuWaves : k / nb;
     return band * S + base + w;
   };
-  auto claim = [&]() -> uint32_t {  // the next claim whose position holds a list entry
-    uint32_t k;
-    do {
+  auto claim = [&]() -> uint32_t {  // the next list position of this wave, ~0u when none is left
+    for (;;) {
       uint32_t v = 0;
       if (lane_id() == 0) v = atomicAdd(&ctr, 1u);
-      k = uni(v);
-    } while (k < total && pos_of(k) >= nt);
-    return k;
+      const uint32_t k = uni(v);
+      if (k >= total) return ~0u;
+      const uint32_t p = pos_of(k);
+      if (p < nt) return p;
+    }
   };
-  uint32_t k = claim();
-  if (k >= total) return;
+  uint32_t p = claim();
+  if (p == ~0u) return;
 #if RBG_STAMPS
   StampAcc sacc = {};
 #endif
@@ -874,18 +880,18 @@ __global__ __launch_bounds__(1024, 1) void k_pair_cu(const PTask* __restrict__ t
   const uint64_t pr0 = __builtin_amdgcn_s_memrealtime(), pm0 = __builtin_amdgcn_s_memtime();
   uint32_t ntask = 0;
 #endif
-  PTask cur = load_task(tasks, pos_of(k));
+  PTask cur = load_task(tasks, p);
   for (;;) {
-    const uint32_t kn = claim();
+    const uint32_t pn = claim();
     PTask nxt;
-    if (kn < total) nxt = load_task(tasks, pos_of(kn));  // in flight while this task runs
+    if (pn != ~0u) nxt = load_task(tasks, pn);  // in flight while this task runs
     if (cur.kind_a != kAbsent || cur.kind_b != kAbsent) {  // marked: no task (the plan wrote its record)
       any_task<OP, MODE>((uint32_t)cur.key - (uint32_t)dsrc.key_lo, cur, pa, pb, oc, task_card, lds SACC_ARG);
 #if RBG_WAVE_PROBE
       ntask++;
 #endif
     }
-    if (kn >= total) break;
+    if (pn == ~0u) break;
     cur = nxt;
   }
 #if RBG_WAVE_PROBE
