@@ -45,6 +45,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 # serialization -- measured faster than 2-16 pipelined key ranges)
 PIPELINED = os.environ.get("RBG_BENCH_PIPE", "0") != "0"
 PIPE_K = int(os.environ.get("RBG_SER_PIPE", "4"))  # key ranges when RBG_BENCH_PIPE=1
+# the dense-range pairwise compute kernel: one 16-wave workgroup per CU (RBG_PW_CU=0: one walk per wave)
+PW_KERNEL = "k_pair_wave" if os.environ.get("RBG_PW_CU", "1") == "0" else "k_pair_cu"
 METRIC = "wide-OR/pairwise-AND input GB/s + % of HBM peak at 1/2/4/8 MI355X"
 
 
@@ -629,8 +631,10 @@ def _relaunch(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # 200 timed steps: the loop's fixed cost (the closing stream sync and barrier, ~0.3 ms) is then 1.5 us of
+    # a 0.32 ms step instead of 15 us at 20 steps
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--cpu-seconds", type=float, default=24.0, help="bounded CPU-baseline budget (all legs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c3-n", type=int, default=10000, help="bitmaps of the C3 wide-OR workloads (0 = skip)")
@@ -713,9 +717,10 @@ def main():
     barrier()
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
-    # the compute kernel's device time over the timed region itself: the engine records HIP events
-    # between its phases on its own stream (the stream the kernel runs on), four per op
-    eng.profile(args.steps)
+    # the compute kernel's device time over the timed region itself: the engine records two HIP events per
+    # op on its own stream (the stream the kernel runs on), around the compute launch -- four per op (every
+    # phase) added 8-9 us to each step (scripts/c2_events.py); the pipelined form keeps the phase events
+    eng.profile(args.steps, compute_only=not PIPELINED)
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
@@ -814,7 +819,7 @@ def main():
     extra["c2_and_cardinality"] = {
         "workload": "RoaringBitmap.andCardinality on the C2 pair (device-resident)",
         "ms_per_step": round(card_wall * 1e3, 4), "input_GBps": round(in_bytes / card_wall / 1e9, 1),
-        "roofline": {"kernel": "k_pair_wave<AND, card>", "kernel_ms": round(card_kern, 4),
+        "roofline": {"kernel": f"{PW_KERNEL}<AND, card>", "kernel_ms": round(card_kern, 4),
                      "achieved_GBps": round(in_bytes / (card_kern / 1e3) / 1e9, 1),
                      "frac": round(in_bytes / (card_kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": _pmc_traffic("k_pair_wave_card")}}
@@ -876,7 +881,7 @@ def main():
                        "parallelism": f"key-range sharding over {world} GPU(s)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic(),
-                         "kernel": "k_pair_wave<AND> (container compute)",
+                         "kernel": f"{PW_KERNEL}<AND> (container compute)",
                          "bytes_per_launch": int((in_bytes + out_bytes) / (PIPE_K if PIPELINED and not strong else 1)),
                          "launches_per_step": PIPE_K if PIPELINED and not strong else 1,
                          "measured": "HIP events on the engine stream around the compute launches of the timed steps",
@@ -889,7 +894,7 @@ def main():
                              "place": round(ph_avg[2], 4), "serialize": round(ser_ms, 4)},
                 "step_form": (f"pipelined: rbg_ctx_pairwise_serialized, {PIPE_K} key ranges" if PIPELINED and not strong
                               else "rbg_ctx_pairwise + rbg_ctx_serialize"),
-                "timed_phase_ms": {"compute_span": round(ph_live[1], 4), "step_events": round(sum(ph_live), 4)},
+                "timed_phase_ms": {"compute_span": round(ph_live[1], 4)},
                 "elements_per_s": round((sa["cardinality"] + sb["cardinality"]) / step_s, 1),
                 "operand_mix": {k: [sa[k], sb[k]] for k in ["array", "bitmap", "run"]},
                 "result": rs,

@@ -226,6 +226,9 @@ int rbg_ctx_sync(rbg_ctx* ctx);
  * ms3[0] = key plan + compaction, ms3[1] = container compute kernel, ms3[2] = result
  * assembly (finalize + emit / reduction), and resets the record. */
 int rbg_ctx_profile(rbg_ctx* ctx, int max_ops);
+/* The same with two events per op, around the container compute kernel only (ms3[1]; ms3[0] and
+ * ms3[2] read 0): the least added to a timed loop of back-to-back ops. */
+int rbg_ctx_profile_compute(rbg_ctx* ctx, int max_ops);
 int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops);
 /* Bytes read by the early-exit wide AND (workShyAnd stops reading a key's inputs once the
  * intersection is empty: payload + 4 B per container it read) over the ops run since

@@ -39,7 +39,7 @@ EXPORTED = [
     "rbg_ctx_load", "rbg_ctx_synth", "rbg_ctx_release", "rbg_ctx_batch_stats", "rbg_ctx_batch_fetch",
     "rbg_ctx_pairwise", "rbg_ctx_pairwise_serialized", "rbg_ctx_pairwise_range", "rbg_ctx_pairwise_card", "rbg_ctx_wide", "rbg_ctx_wide_card",
     "rbg_ctx_batch_and_card", "rbg_ctx_card", "rbg_ctx_cards", "rbg_ctx_result_stats", "rbg_ctx_fetch",
-    "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_read", "rbg_ctx_profile_bytes", "rbg_ctx_serialize", "rbg_ctx_wide_start",
+    "rbg_ctx_fetch_shard", "rbg_ctx_profile", "rbg_ctx_profile_compute", "rbg_ctx_profile_read", "rbg_ctx_profile_bytes", "rbg_ctx_serialize", "rbg_ctx_wide_start",
     "rbg_ctx_batch_counts", "rbg_synth_key_bytes", "rbg_ctx_pair_bytes", "rbg_debug_stamps",
     "rbg_bsi_compare", "rbg_bsi_sum", "rbg_ctx_bsi", "rbg_ctx_bsi_sums", "rbg_ctx_bsi_sums_device", "rbg_ctx_bsi_sums_target", "rbg_ctx_batch_minmax",
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
@@ -121,6 +121,7 @@ def _declare(L):
     L.rbg_ctx_result_stats.argtypes = [vp, P(ctypes.c_int64)]
     L.rbg_ctx_fetch.argtypes = [vp, buf]
     L.rbg_ctx_profile.argtypes = [vp, ctypes.c_int]
+    L.rbg_ctx_profile_compute.argtypes = [vp, ctypes.c_int]
     L.rbg_ctx_profile_read.argtypes = [vp, P(ctypes.c_double), P(ctypes.c_int)]
     L.rbg_ctx_profile_bytes.argtypes = [vp, P(ctypes.c_int64)]
     L.rbg_ctx_fetch_shard_device.argtypes = [vp, ctypes.c_int64, ctypes.c_int, ctypes.c_int64, vp, vp, vp, vp]

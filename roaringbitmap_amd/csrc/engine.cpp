@@ -231,7 +231,12 @@ struct Ctx {
     prof_ev.clear();
     prof_cap = prof_n = 0;
   }
+  bool prof_compute_only = false;  // events around the compute launch only (rbg_ctx_profile_compute)
   void mark(int phase) {
+    if (prof_compute_only && (phase == 0 || phase == 3)) {
+      if (phase == 3 && prof_n < prof_cap) prof_n++;  // the op's record is complete
+      return;
+    }
     if (prof_n < prof_cap) (void)hipEventRecord(prof_ev[4 * prof_n + phase], stream);
     if (phase == 3 && prof_n < prof_cap) prof_n++;
   }
@@ -2361,10 +2366,11 @@ void rbg_ctx_destroy(rbg_ctx* ctx) {
   delete ctx;
 }
 void* rbg_ctx_stream(rbg_ctx* ctx) { return ctx ? (void*)ctx->c.stream : nullptr; }
-int rbg_ctx_profile(rbg_ctx* ctx, int max_ops) {
+static int ctx_profile(rbg_ctx* ctx, int max_ops, bool compute_only) {
   CHK(enter(&ctx->c));
   HIPCHK(hipStreamSynchronize(ctx->c.stream));
   ctx->c.prof_free();
+  ctx->c.prof_compute_only = compute_only;
   if (max_ops <= 0) return RBG_OK;
   ctx->c.prof_ev.resize(4 * (size_t)max_ops);
   for (hipEvent_t& e : ctx->c.prof_ev) HIPCHK(hipEventCreate(&e));
@@ -2374,6 +2380,8 @@ int rbg_ctx_profile(rbg_ctx* ctx, int max_ops) {
   HIPCHK(hipMemsetAsync(ctx->c.rd_ctr.p, 0, 8, ctx->c.stream));
   return RBG_OK;
 }
+int rbg_ctx_profile(rbg_ctx* ctx, int max_ops) { return ctx_profile(ctx, max_ops, false); }
+int rbg_ctx_profile_compute(rbg_ctx* ctx, int max_ops) { return ctx_profile(ctx, max_ops, true); }
 int rbg_ctx_profile_bytes(rbg_ctx* ctx, int64_t* bytes) {
   if (!ctx || !bytes) {
     set_err("profile_bytes: null argument");
@@ -2394,6 +2402,7 @@ int rbg_ctx_profile_read(rbg_ctx* ctx, double* ms3, int* n_ops) {
   ms3[0] = ms3[1] = ms3[2] = 0.0;
   for (size_t i = 0; i < c.prof_n; i++) {
     for (int ph = 0; ph < 3; ph++) {
+      if (c.prof_compute_only && ph != 1) continue;  // only the compute launch was bracketed
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, c.prof_ev[4 * i + ph], c.prof_ev[4 * i + ph + 1]));
       ms3[ph] += ms;

@@ -46,9 +46,11 @@ class Engine:
     def sync(self):
         check(lib().rbg_ctx_sync(self._ctx))
 
-    def profile(self, max_ops):
-        """Enable HIP-event phase timing for the next `max_ops` ops (0 disables)."""
-        check(lib().rbg_ctx_profile(self._ctx, int(max_ops)))
+    def profile(self, max_ops, compute_only=False):
+        """Enable HIP-event phase timing for the next `max_ops` ops (0 disables); compute_only: two events
+        per op around the container compute kernel (only compute_ms is read)."""
+        f = lib().rbg_ctx_profile_compute if compute_only else lib().rbg_ctx_profile
+        check(f(self._ctx, int(max_ops)))
 
     def profile_read(self):
         """-> (n_ops, [plan_ms, compute_ms, assemble_ms]) summed over the recorded ops."""

@@ -14,7 +14,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 RX='k_pair|k_emit|k_plan|k_place|k_serialize|k_wide|k_batch|k_bsi|k_dec|k_runopt|k_scan|k_shard|k_header'
 if [[ " $PASSES " == *" kt "* ]]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_kt.json 2> $OUT/kt.err || { echo "kt failed"; tail $OUT/kt.err; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o run -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline > $OUT/bench_kt.json 2> $OUT/kt.err || { echo "kt failed"; tail $OUT/kt.err; exit 1; }
   echo "kernel trace done"
 fi
 if [[ " $PASSES " == *" ktw "* ]]; then
