@@ -17,6 +17,8 @@
 #include <unordered_map>
 
 #include "kernels.hpp"
+#include <cstdlib>
+
 #include "wave.hpp"
 
 namespace rbg {
@@ -583,16 +585,16 @@ __global__ __launch_bounds__(256) void k_gather(const GatherItem* __restrict__ i
 // host launchers
 // ===========================================================================
 
-int resident_grid(const void* kernel) {
+int resident_grid(const void* kernel, int block) {
   static std::mutex mu;
-  static std::unordered_map<const void*, int> cache;
+  static std::unordered_map<const void*, int> cache;  // kernels launch with one block size each
   std::lock_guard<std::mutex> g(mu);
   auto it = cache.find(kernel);
   if (it != cache.end()) return it->second;
   int dev = 0, cus = 0, per_cu = 0;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, 0);
   const int r = std::max(1, cus) * std::max(1, per_cu);
   cache[kernel] = r;
   return r;

@@ -226,7 +226,7 @@ struct BsiArgs {
 // once: CUs x occupancy.  Task kernels launch at most this many workgroups and
 // stride over their tasks, so no workgroup waits for a dispatch slot and no
 // wave pays a launch per task (cached per kernel).
-int resident_grid(const void* kernel);
+int resident_grid(const void* kernel, int block = 256);  // workgroups of `block` threads resident at once
 
 // plan kernels also zero the op's look-back header (zlb, 32 u64) and tile statuses (ztile, 128 u64)
 void launch_plan_wide(hipStream_t s, int mode, const uint32_t* key_off, uint32_t n_req, int key_lo, int key_hi,

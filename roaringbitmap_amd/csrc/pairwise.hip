@@ -904,7 +904,7 @@ static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_
                       const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced,
                       bool cu_pool) {
   if (direct && balanced && cu_pool) {  // one workgroup per CU, all of them resident
-    const int g = std::max(1, resident_grid((const void*)&k_pair_cu<OP, MODE>));
+    const int g = std::max(1, resident_grid((const void*)&k_pair_cu<OP, MODE>, 1024));
     hipLaunchKernelGGL((k_pair_cu<OP, MODE>), dim3(g), dim3(1024), 0, s, tasks, nt, pa, pb, oc, task_card, *direct);
     return;
   }
