@@ -191,6 +191,7 @@ struct Ctx {
   uint64_t* zlb = nullptr;    // look-back state the next plan kernel zeroes (null: none)
   uint64_t* ztile = nullptr;
   DevBuf bsi_defer, bsi_cnts, bsi_kin, bsi_table;  // scratch of the register-resident BSI kernels
+  DevBuf bsi_claims;  // k_bsi_reg's unit-pool counters (zero between queries)
   DevBuf bsi_sums;  // kBsiMaxInputs + 1 u64: per-slice |bA[x] & found|, found count
   void* bsi_sums_dst = nullptr;  // rbg_ctx_bsi_sums_target: (sum, count) also written here by every sum
   // buffer-package BSI: owenGreatEqual's orInput types / task keys / chain order, and the arena of
@@ -1620,6 +1621,11 @@ static int ctx_bsi(Ctx* c, int32_t id, int op, int nbits, int has_found, int32_t
     CHK(c->bsi_kin.ensure((size_t)16 * 34 * ub));
     CHK(c->bsi_table.ensure((size_t)16 * 34 * ub));
     sc = BsiScratch{c->bsi_defer.as<uint32_t>(), c->bsi_cnts.as<int>(), c->bsi_kin.p, ub, c->bsi_table.p};
+    if (!c->bsi_claims.p) {  // zeroed once here, then by k_bsi_types after every query that claims
+      CHK(c->bsi_claims.ensure(4 * kBsiClaimWords));
+      HIPCHK(hipMemsetAsync(c->bsi_claims.p, 0, 4 * kBsiClaimWords, s));
+    }
+    sc.claims = c->bsi_claims.as<unsigned int>();
   }
   WideArgs wa{};
   wa.desc = B->desc.as<CDesc>();

@@ -341,7 +341,16 @@ struct BsiScratch {
   unsigned long long* zsums;
   const uint32_t* nt_src;
   uint32_t* nt_dst;
+  // k_bsi_reg's unit pools: one counter per group of kBsiGroup workgroups, 64 B apart (kBsiClaimWords
+  // words, zero before every query: k_bsi_types zeroes them after k_bsi_reg)
+  unsigned int* claims;
 };
+#ifndef RBG_BSI_GROUP
+#define RBG_BSI_GROUP 4
+#endif
+constexpr int kBsiGroup = RBG_BSI_GROUP;  // workgroups per k_bsi_reg unit pool
+constexpr int kBsiMaxGroups = 1024;  // groups of a resident k_bsi_reg grid (at most 4 workgroups per CU)
+constexpr int kBsiClaimWords = 16 * kBsiMaxGroups;
 // true: compare `op` over `nbits` slices runs the register-resident kernels (k_bsi_table, k_bsi_reg, ...)
 bool bsi_reg_path(int op, int nbits);
 void launch_bsi_table(hipStream_t s, const Task* tasks, const uint32_t* nt, WideArgs args, void* table, size_t stride);
