@@ -554,11 +554,13 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
 #define RBG_BSI_POOL 1
 #endif
 #if RBG_BSI_POOL
-  // Units claimed from a pool per group of kBsiGroup workgroups (blockIdx mod G, one of each dispatch
-  // tier): the per-workgroup probe showed a CU's four workgroups ending 653 / 695 / 736 / 771 us
-  // (dispatch order wins issue arbitration) with a fixed 59-60 units each.  Group g owns the units
-  // [g U, g U + U); a claim is one agent-scope atomic on the group's counter (zeroed by k_bsi_types
-  // after every query), issued a unit ahead so its latency hides behind a unit's work.
+  // Units claimed from a pool per group of kBsiGroup workgroups (blockIdx mod G): the per-workgroup
+  // probe showed a CU's four workgroups ending 653 / 695 / 736 / 771 us (dispatch order wins issue
+  // arbitration) with a fixed 59-60 units each.  Group g owns the units [g U, g U + U); a claim is one
+  // agent-scope atomic on the group's counter (zeroed by k_bsi_types after every query), issued a unit
+  // ahead so its latency hides behind a unit's work.  Groups of 4 / 8 / 16 / 32 / 64 / 128 / 256
+  // workgroups: C5 step 0.843 / 0.836 / 0.826 / 0.822 / 0.815 / 0.806 / 0.807 ms against 0.864 static
+  // (profiles/r05/experiments/c5_bsi_pool_groups.txt): 128, i.e. 8 counters for a 1,024-workgroup grid.
   const uint32_t G = min((uint32_t)kBsiMaxGroups, max(1u, gridDim.x / kBsiGroup)), grp = blockIdx.x % G;
   const uint64_t U = (nunits + G - 1) / G, g0 = (uint64_t)grp * U;
   const uint64_t gcnt = g0 < nunits ? min(U, nunits - g0) : 0;

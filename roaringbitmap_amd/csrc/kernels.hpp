@@ -346,7 +346,7 @@ struct BsiScratch {
   unsigned int* claims;
 };
 #ifndef RBG_BSI_GROUP
-#define RBG_BSI_GROUP 4
+#define RBG_BSI_GROUP 128
 #endif
 constexpr int kBsiGroup = RBG_BSI_GROUP;  // workgroups per k_bsi_reg unit pool
 constexpr int kBsiMaxGroups = 1024;  // groups of a resident k_bsi_reg grid (at most 4 workgroups per CU)
