@@ -834,7 +834,9 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 //   RBG_CU_ORDER 2: band (b - k) mod nb, slot k / nb -- as 0, each round of nb claims heavy to light.
 // A claim is one LDS atomic; the next task is claimed and its record requested while a task runs.
 // (Shared pools of the last 1 / 2 / 4 bands across CUs, claimed by agent-scope atomics, made the
-// kernel 0.23 -> 0.34 / 0.44 / 0.60 ms: profiles/r05/experiments/c2_cu_tail_pools.txt.)
+// kernel 0.23 -> 0.34 / 0.44 / 0.60 ms: profiles/r05/experiments/c2_cu_tail_pools.txt; every wave
+// claiming chunks of 1 / 2 / 4 tasks from per-XCD pools instead of the LDS pool: 0.221-0.226 ->
+// 0.262-0.265 / 0.244-0.251 / 0.255-0.256 ms, c2_cu_global_chunks.txt.)
 // ---------------------------------------------------------------------------
 #ifndef RBG_CU_ORDER
 #define RBG_CU_ORDER 0
