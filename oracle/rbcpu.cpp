@@ -1517,6 +1517,123 @@ Bitmap op_andnot_range(const Bitmap& x1, const Bitmap& x2, uint64_t start, uint6
   return op_andnot(select_range(x1, start, end), select_range(x2, start, end));
 }
 
+// ---------------------------------------------------------------------------
+// orNot (RB/RoaringBitmap.java:1431-1506 in place, :1521-1603 static)
+// ---------------------------------------------------------------------------
+// Container.not(0, end), end in [1, 65536]:
+//  ArrayContainer.not (RB/ArrayContainer.java:876-925): the new cardinality is card - m + (end - m)
+//    (m values below end); above 4096 it is toBitmapContainer().not, else an array of the complement
+//    in [0, end) followed by the values >= end;
+//  BitmapContainer.not = clone().inot (RB/BitmapContainer.java:994-997, 679-687): the range flipped,
+//    toArrayContainer at <= 4096 values;
+//  RunContainer.not (RB/RunContainer.java:1900-1918): no run starts below 0, so the answer is the run
+//    [0, end) followed by every run through smartAppendExclusive, then toEfficientContainer.
+Ctr c_not_prefix(const Ctr& c, int end) {
+  if (end <= 0) return c;
+  if (c.kind == ARRAY) {
+    const int m = (int)(std::lower_bound(c.vals.begin(), c.vals.end(), end) - c.vals.begin());
+    const int newcard = c.card - m + (end - m);
+    if (newcard > kArrayMax) return c_not_prefix(to_bitmap(c), end);
+    std::vector<uint16_t> v;
+    v.reserve(newcard);
+    int i = 0;
+    for (int x = 0; x < end; x++) {
+      if (i < m && (int)c.vals[i] == x) i++;
+      else v.push_back((uint16_t)x);
+    }
+    for (int j = m; j < c.card; j++) v.push_back(c.vals[j]);
+    return make_array(std::move(v));
+  }
+  if (c.kind == BITMAP) {
+    Ctr b = c;
+    const int prev = card_in_range(b.words, 0, end);
+    flip_range(b.words, 0, end);
+    b.card += (end - prev) - prev;
+    if (b.card <= kArrayMax) return bitmap_to_array(b);
+    return b;
+  }
+  RunBuf ans(c.nruns() + 1);
+  ans.smart_append_excl(0, end - 1);
+  for (int k = 0; k < c.nruns(); k++) ans.smart_append_excl(c.vals[2 * k], c.vals[2 * k + 1]);
+  return to_efficient(ans.build());
+}
+
+// Container.rangeOfOnes(0, last) (RB/Container.java:29-37): an array up to 2 values, else a run
+static Ctr range_of_ones(int last) {
+  if (last <= 2) {
+    std::vector<uint16_t> v;
+    for (int x = 0; x < last; x++) v.push_back((uint16_t)x);
+    return make_array(std::move(v));
+  }
+  return make_run({0, (uint16_t)(last - 1)}, 1);
+}
+
+// Container.orNot / iorNot (RB/Container.java:191-196, 536-541): or / ior with
+// x.not(0, end).iremove(end, 0x10000) (end < 0x10000) or x.not(0, 0x10000)
+static Ctr c_ornot(const Ctr& c1, const Ctr& c2, int end, bool inplace) {
+  Ctr x = c_not_prefix(c2, end);
+  if (end < 0x10000) x = c_remove_range(x, end, 0x10000);
+  return inplace ? c_ior(c1, x) : c_or(c1, x);
+}
+
+Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inplace, bool* neg) {
+  *neg = false;
+  // (int)((rangeEnd - 1) >>> 16): -1 for rangeEnd == 0
+  const int max_key = range_end == 0 ? -1 : (int)((range_end - 1) >> 16);
+  const int last_run = (range_end & 0xFFFF) == 0 ? 0x10000 : (int)(range_end & 0xFFFF);
+  const int n1 = (int)x1.size(), n2 = (int)x2.size();
+  int remainder = 0;
+  for (int i = n1 - 1; i >= 0 && (int)x1.keys[i] > max_key; --i) ++remainder;
+  int correction = 0;
+  for (int i = 0; i < n2 - remainder; ++i) {
+    correction += x2.ctrs[i].full() ? 1 : 0;
+    if ((int)x2.keys[i] >= max_key) break;
+  }
+  // the reference's "conservative overestimate", which bounds the key loop below
+  const int max_size = std::min(max_key + 1 + remainder - correction + n1, 0x10000);
+  if (max_size < 0) {
+    *neg = true;
+    return Bitmap();
+  }
+  if (max_size == 0) return inplace ? x1 : Bitmap();
+  Bitmap ans;
+  int p1 = 0, p2 = 0;
+  int s1 = n1 > 0 ? x1.keys[0] : max_key + 1;
+  int s2 = n2 > 0 ? x2.keys[0] : max_key + 1;
+  int size = 0;
+  for (int key = 0; key <= max_key && size < max_size; ++key) {
+    const int e = key == max_key ? last_run : 0x10000;
+    Ctr v;
+    if (key == s1 && key == s2) {
+      v = c_ornot(x1.ctrs[p1], x2.ctrs[p2], e, inplace);
+      ++p1;
+      ++p2;
+      s1 = p1 < n1 ? x1.keys[p1] : max_key + 1;
+      s2 = p2 < n2 ? x2.keys[p2] : max_key + 1;
+    } else if (key == s1) {  // x1.ior(rangeOfOnes) at maxKey (also in the static form), else full
+      v = key == max_key ? c_ior(x1.ctrs[p1], range_of_ones(last_run)) : run_full();
+      ++p1;
+      s1 = p1 < n1 ? x1.keys[p1] : max_key + 1;
+    } else if (key == s2) {  // the complement, not clipped at rangeEnd
+      v = c_not_prefix(x2.ctrs[p2], e);
+      ++p2;
+      s2 = p2 < n2 ? x2.keys[p2] : max_key + 1;
+    } else {
+      v = key == max_key ? range_of_ones(last_run) : run_full();
+    }
+    if (!v.empty()) {
+      ans.keys.push_back((uint16_t)key);
+      ans.ctrs.push_back(std::move(v));
+      ++size;
+    }
+  }
+  for (int i = n1 - remainder; i < n1; i++) {
+    ans.keys.push_back(x1.keys[i]);
+    ans.ctrs.push_back(x1.ctrs[i]);
+  }
+  return ans;
+}
+
 // key-bitset intersection shared by workShyAnd / workShyAndCardinality
 static std::vector<uint16_t> common_keys(const std::vector<const Bitmap*>& bms) {
   std::vector<uint64_t> words(1024, 0);

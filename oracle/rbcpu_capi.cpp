@@ -138,6 +138,26 @@ int rbo_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t 
   return emit(range_aggregate(op, ptrs, (uint64_t)start, (uint64_t)end), out, out_len);
 }
 
+// RoaringBitmap.orNot(x1, x2, rangeEnd) (inplace 0, RB/RoaringBitmap.java:1521-1603) and
+// x1.orNot(x2, rangeEnd) (inplace 1, :1431-1506).  rangeSanityCheck(0, rangeEnd) -> ERR_ARG; a negative
+// maxSize (the reference's NegativeArraySizeException) -> ERR_ARG with *neg = 1.
+int rbo_ornot(const uint8_t* a, size_t an, const uint8_t* b, size_t bn, int64_t range_end, int inplace,
+              int* neg, uint8_t** out, size_t* out_len) {
+  *neg = 0;
+  if (range_end < 0 || range_end > 0x100000000ll) return ERR_ARG;
+  Bitmap x, y;
+  int st = load(a, an, &x);
+  if (st) return st;
+  if ((st = load(b, bn, &y))) return st;
+  bool ng = false;
+  Bitmap r = op_ornot(x, y, (uint64_t)range_end, inplace != 0, &ng);
+  if (ng) {
+    *neg = 1;
+    return ERR_ARG;
+  }
+  return emit(r, out, out_len);
+}
+
 // RoaringBitmap.getLongSizeInBytes of a serialized bitmap (RB/RoaringBitmap.java:2212-2219)
 int64_t rbo_long_size(const uint8_t* a, size_t an) {
   Bitmap b;

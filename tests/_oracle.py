@@ -73,6 +73,9 @@ def lib():
         L.rbo_range_op.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
                                    ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64,
                                    ctypes.POINTER(ctypes.POINTER(ctypes.c_uint8)), ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_ornot.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64,
+                                ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(u8p),
+                                ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -239,6 +242,24 @@ def range_op(op, bufs, start, end) -> bytes:
     n = ctypes.c_size_t()
     _check(lib().rbo_range_op({"and": 0, "or": 1, "xor": 2, "andnot": 3, "select": 4}[op], arr, lens, len(bufs), start, end,
                               ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
+
+
+class NegativeArraySize(OracleError):
+    """The reference's orNot sizes its key array with a negative maxSize (NegativeArraySizeException)."""
+
+
+def ornot(a, b, range_end, inplace=False) -> bytes:
+    """RoaringBitmap.orNot(x1, x2, rangeEnd) (RB/RoaringBitmap.java:1521-1603) or, inplace, x1.orNot(x2,
+    rangeEnd) (:1431-1506)."""
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    neg = ctypes.c_int()
+    st = lib().rbo_ornot(a, len(a), b, len(b), range_end, int(inplace), ctypes.byref(neg), ctypes.byref(p),
+                         ctypes.byref(n))
+    if neg.value:
+        raise NegativeArraySize(st)
+    _check(st)
     return _take(p, n)
 
 

@@ -13,10 +13,15 @@ Inputs (data files the reference's tests hold; no reference source is copied):
     (ZipRealDataRetriever.fetchBitPositions, real-roaring-dataset/src/main/java/
     org/roaringbitmap/ZipRealDataRetriever.java:40-69), stored as one concatenated
     uint32 `values` array plus `offsets` (len 201).
+  * RoaringBitmap/src/test/resources/testdata/ornot-fuzz-failure.json (the two base64 bitmaps of
+    RBT/TestRoaringBitmapOrNot.java:376-424 testBigOrNot / testBigOrNotStatic)
+    -> tests/golden/testdata/ornot_fuzz_{l,r}.bin.gz, the decoded serialized bytes, gzipped
   * The known-answer constants of jmh/src/test/java/org/roaringbitmap/realdata/
     RealDataBenchmark{Or,And,AndNot,Xor,WideOrNaive,WideAndNaive}Test.java are
     transcribed (as numbers) into known_answers.json.
 """
+import base64
+import gzip
 import json
 import os
 import shutil
@@ -63,6 +68,12 @@ def main():
         f"crashproneinput{i}.bin" for i in range(1, 9)]
     for n in names:
         shutil.copyfile(os.path.join(TESTDATA_SRC, n), os.path.join(td, n))
+
+    with open(os.path.join(TESTDATA_SRC, "ornot-fuzz-failure.json")) as f:
+        bms = json.load(f)["bitmaps"]
+    for tag, b in zip("lr", bms[:2]):
+        with gzip.GzipFile(os.path.join(td, f"ornot_fuzz_{tag}.bin.gz"), "wb", mtime=0) as g:
+            g.write(base64.b64decode(b))
 
     rd = os.path.join(HERE, "realdata")
     os.makedirs(rd, exist_ok=True)
