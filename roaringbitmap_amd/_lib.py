@@ -45,7 +45,7 @@ EXPORTED = [
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
     "rbg_ctx_fetch_shard_device", "rbg_bsi_compare_buffer", "rbg_ctx_bsi_buffer",
     "rbg_ctx_result_layout_device", "rbg_ctx_fetch_shard_device_dyn", "rbg_pairwise_inplace",
-    "rbg_ctx_load_separate",
+    "rbg_ctx_load_separate", "rbg_ornot", "rbg_ctx_ornot",
 ]
 
 _lib = None
@@ -68,6 +68,8 @@ def _declare(L):
     L.rbg_wide.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), P(i32), sz, buf]
     L.rbg_wide_card.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), sz, P(i32)]
     L.rbg_range_op.argtypes = [ctypes.c_int, P(ctypes.c_char_p), P(sz), sz, ctypes.c_int64, ctypes.c_int64, buf]
+    L.rbg_ornot.argtypes = [u8p, sz, u8p, sz, ctypes.c_int64, ctypes.c_int, buf]
+    L.rbg_ctx_ornot.argtypes = [vp, i32, sz, i32, sz, ctypes.c_int64, ctypes.c_int]
     L.rbg_ctx_select_range.argtypes = [vp, i32, ctypes.c_int64, ctypes.c_int64, P(i32)]
     L.rbg_batch_and_card.argtypes = [sz, P(ctypes.c_char_p), P(sz), P(ctypes.c_char_p), P(sz), P(i32)]
     L.rbg_free.argtypes = [buf]

@@ -198,6 +198,7 @@ struct Ctx {
   // result run containers above 2047 runs (BigRuns; big_ctl = {bytes used, overflow})
   DevBuf owen_tb, owen_keys, owen_ord, big, big_ctl;
   DevBuf ones;  // 8192 bytes of 0xFF: the full bitmap container of an in-place OR (k_ior_fix)
+  DevBuf ornot_plan;  // OrNotPlan of the last orNot
   DevBuf gather_items, gather_out;  // batch fetch: slot gather list and download buffer
   DevBuf order;                     // horizontal_*: chain order of every key segment
   DevBuf ro_info, ro_size, ro_part;  // range selection scratch (kept: no allocation per call)
@@ -947,6 +948,54 @@ static int ctx_pairwise_buffer(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib
     }
     CHK(c->big.ensure(used[0] + (used[0] >> 3) + 4096));
   }
+}
+
+// RoaringBitmap.orNot(x1, x2, rangeEnd) (static, RB/RoaringBitmap.java:1521-1603) and x1.orNot(x2,
+// rangeEnd) (in place, :1431-1506), ornot.hip.  rangeSanityCheck(0, rangeEnd) (:204-213).  The
+// reference's maxSize is negative only for rangeEnd == 0 (maxKey = -1) with x1 empty and x2's first
+// container full (new char[-1] throws): only that case reads the plan back before returning.
+static int ctx_ornot(Ctx* c, int32_t ia, size_t ma, int32_t ib, size_t mb, int64_t range_end, bool inplace) {
+  if (range_end < 0 || range_end > (int64_t)0x100000000ll) {
+    set_err("rangeEnd should be in [0, 0xffffffff + 1]");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  Batch *A, *B;
+  CHK(get_batch(c, ia, &A));
+  CHK(get_batch(c, ib, &B));
+  const uint16_t *ka, *kb;
+  const CDesc *da, *db;
+  int na, nb;
+  CHK(operand(A, ma, &ka, &da, &na));
+  CHK(operand(B, mb, &kb, &db, &nb));
+  const int max_key = range_end == 0 ? -1 : (int)((range_end - 1) >> 16);
+  const int last_run = (range_end & 0xFFFF) == 0 ? 0x10000 : (int)(range_end & 0xFFFF);
+  hipStream_t s = c->stream;
+  const size_t ub = std::max<size_t>(1, std::min<size_t>(kMaxKeys, (size_t)(max_key + 1) + (size_t)na));
+  if (!c->ornot_plan.p) CHK(c->ornot_plan.ensure(sizeof(OrNotPlan)));
+  OutCtx oc;
+  CHK(prepare_output(c, ub, A->payload_bytes + B->payload_bytes + (size_t)8194 * ub, &oc, false));
+  c->pending_src = {ia, ib};
+  c->mark(0);
+  c->mark(1);
+  launch_ornot(s, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), na, B->key_off.as<uint32_t>(), db,
+               B->payload.as<uint8_t>(), nb, max_key, last_run, inplace, c->ornot_plan.as<OrNotPlan>(),
+               c->wg_epoch.as<uint64_t>(), next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->zlb,
+               c->ztile, grid_for(ub, 65536));
+  c->mark(2);
+  defer_place(c);
+  c->mark(3);
+  HIPCHK(hipGetLastError());
+  if (max_key < 0 && na == 0 && nb > 0) {
+    OrNotPlan pl;
+    HIPCHK(hipMemcpyAsync(&pl, c->ornot_plan.p, sizeof(pl), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (pl.neg) {
+      c->last = 0;
+      set_err("orNot: negative maxSize (the reference throws NegativeArraySizeException)");
+      return RBG_ERR_ILLEGAL_ARGUMENT;
+    }
+  }
+  return RBG_OK;
 }
 
 static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only, int key_lo = 0,
@@ -2129,6 +2178,27 @@ int rbg_pairwise_inplace(int op, const uint8_t* a, size_t a_len, const uint8_t* 
   // x1.and / xor / andNot(x2) in place type like the static ops (Container.iand / ixor / iandNot
   // end in the same container types); x1.or(x2) is Container.ior's
   return rbg_pairwise(op == RBG_OR ? RBG_OR_INPLACE : op, a, a_len, b, b_len, out);
+}
+
+int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int64_t range_end, int inplace,
+              rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  const uint8_t* bufs[2] = {a, b};
+  const size_t lens[2] = {a_len, b_len};
+  int32_t ids[2];
+  CHK(ctx_load_separate(c, bufs, lens, 2, ids));
+  g.ids = {ids[0], ids[1]};
+  CHK(ctx_ornot(c, ids[0], 0, ids[1], 0, range_end, inplace != 0));
+  return ctx_fetch(c, out);
+}
+
+int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int64_t range_end, int inplace) {
+  if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
+  CHK(enter(&ctx->c));
+  return ctx_ornot(&ctx->c, a, ia, b, ib, range_end, inplace != 0);
 }
 
 int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int32_t* out) {

@@ -367,6 +367,19 @@ void launch_bsi_buf(hipStream_t s, int grid, const Task* tasks, const uint32_t* 
 void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
                      const uint8_t* pb, OutCtx oc, BigRuns big);
 
+// RoaringBitmap.orNot (ornot.hip): the reference's key-loop bound, computed on the device
+struct OrNotPlan {
+  int32_t k_end;       // keys [0, k_end) the loop reaches
+  int32_t neg;         // maxSize < 0 (the reference's NegativeArraySizeException)
+  int32_t max_size;
+  int32_t correction;
+};
+// k_ornot_scan -> k_plan_ornot -> k_ornot<inplace> over single-bitmap batches A (x1) and B (x2)
+void launch_ornot(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint8_t* pa, int na, const uint32_t* kob,
+                  const CDesc* db, const uint8_t* pb, int nb, int max_key, int last_run, bool inplace, OrNotPlan* plan,
+                  uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint64_t* zlb,
+                  uint64_t* ztile, int grid);
+
 // batched andCardinality over pairs (2i, 2i+1) of a bitmap-major batch: per-pair key
 // alignment (count, scan, emit), then one wave per matched key; pairs of more than 64
 // keys take one wave per pair.  Scratch: cnt (n_pairs u64), part (scan_parts(n_pairs)

@@ -20,24 +20,6 @@
 
 namespace rbg {
 
-// Descriptor of key k in a single-bitmap batch through its key CSR (O(1), no search)
-__device__ __forceinline__ void resolve(const uint32_t* key_off, const CDesc* desc, const uint8_t* payload, uint32_t k,
-                                        uint64_t& slot, uint32_t& card, uint8_t& kind, uint16_t& nruns) {
-  const uint32_t p = key_off[k];
-  if (key_off[k + 1] > p) {
-    const CDesc d = desc[p];
-    slot = d.slot;
-    card = d.card;
-    kind = d.kind;
-    nruns = d.kind == DK_R ? *reinterpret_cast<const uint16_t*>(payload + d.slot + 2) : 0;
-  } else {
-    slot = 0;
-    card = 0;
-    kind = kAbsent;
-    nruns = 0;
-  }
-}
-
 // Task class: 1 = filter class (pass-through clones, AND with an array, ANDNOT
 // of an array: results are subsets of one array), 2 = bitmap class.
 __device__ __forceinline__ int pair_class(int op, int ka, int kb) {
@@ -61,8 +43,6 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, int key_lo, int k
                                                        uint64_t* __restrict__ wg_epoch, uint32_t epoch,
                                                        PTask* __restrict__ tasks, uint32_t* __restrict__ n_tasks,
                                                        uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
-  __shared__ int wt[4];
-  __shared__ int wb[4];
   plan_zero(zlb, ztile);
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   PTask t;
@@ -78,37 +58,7 @@ __global__ __launch_bounds__(256) void k_plan_pairwise(int op, int key_lo, int k
     default: f = ia && ib; break;  // AND and andCardinality
   }
   if ((int)k < key_lo || (int)k >= key_hi) f = 0;
-  int tot;
-  const int lane_pre = wave_excl(f, &tot);
-  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = tot;
-  __syncthreads();
-  const int cnt = wt[0] + wt[1] + wt[2] + wt[3];
-  if (threadIdx.x == 0)
-    __hip_atomic_store(wg_epoch + blockIdx.x, ((uint64_t)epoch << 32) | (uint32_t)cnt, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  // counts of the workgroups before this one
-  uint32_t c = 0;
-  if (threadIdx.x < blockIdx.x) {
-    uint64_t v;
-    uint32_t spins = 0;
-    while (((v = __hip_atomic_load(wg_epoch + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
-           epoch) {
-      if (++spins > (1u << 22)) {
-        atomicOr(err, 1u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    c = (uint32_t)v;
-  }
-  const int sw = wave_sum_i((int)c);
-  if ((threadIdx.x & 63) == 0) wb[threadIdx.x >> 6] = sw;
-  __syncthreads();
-  const uint32_t base = (uint32_t)(wb[0] + wb[1] + wb[2] + wb[3]);
-  int wpre = 0;
-  for (int i = 0; i < (int)(threadIdx.x >> 6); i++) wpre += wt[i];
-  if (f) tasks[base + wpre + lane_pre] = t;
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_tasks = base + cnt;
+  plan_emit(f, t, wg_epoch, epoch, tasks, n_tasks, err);
 }
 
 // ---------------------------------------------------------------------------

@@ -453,6 +453,65 @@ __device__ __forceinline__ void plan_zero(uint64_t* lb_header, uint64_t* tile_st
     for (uint32_t i = threadIdx.x; i < (uint32_t)kMaxTiles; i += blockDim.x) tile_status[i] = 0;
 }
 
+// Descriptor of key k in a single-bitmap batch through its key CSR (O(1), no search)
+__device__ __forceinline__ void resolve(const uint32_t* key_off, const CDesc* desc, const uint8_t* payload, uint32_t k,
+                                        uint64_t& slot, uint32_t& card, uint8_t& kind, uint16_t& nruns) {
+  const uint32_t p = key_off[k];
+  if (key_off[k + 1] > p) {
+    const CDesc d = desc[p];
+    slot = d.slot;
+    card = d.card;
+    kind = d.kind;
+    nruns = d.kind == DK_R ? *reinterpret_cast<const uint16_t*>(payload + d.slot + 2) : 0;
+  } else {
+    slot = 0;
+    card = 0;
+    kind = kAbsent;
+    nruns = 0;
+  }
+}
+
+// Plan compaction (one thread per key, 256 workgroups of 256 keys, all resident): each workgroup
+// publishes its task count tagged with the op's epoch, sums the counts of the workgroups before it
+// (one per thread, waiting for the epoch), and writes its flagged tasks straight into the dense task
+// list in key order.  The last workgroup writes the task count.
+__device__ __forceinline__ void plan_emit(int f, const PTask& t, uint64_t* wg_epoch, uint32_t epoch, PTask* tasks,
+                                          uint32_t* n_tasks, uint32_t* err) {
+  __shared__ int wt[4];
+  __shared__ int wb[4];
+  int tot;
+  const int lane_pre = wave_excl(f, &tot);
+  if ((threadIdx.x & 63) == 0) wt[threadIdx.x >> 6] = tot;
+  __syncthreads();
+  const int cnt = wt[0] + wt[1] + wt[2] + wt[3];
+  if (threadIdx.x == 0)
+    __hip_atomic_store(wg_epoch + blockIdx.x, ((uint64_t)epoch << 32) | (uint32_t)cnt, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  // counts of the workgroups before this one
+  uint32_t c = 0;
+  if (threadIdx.x < blockIdx.x) {
+    uint64_t v;
+    uint32_t spins = 0;
+    while (((v = __hip_atomic_load(wg_epoch + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 32) !=
+           epoch) {
+      if (++spins > (1u << 22)) {
+        atomicOr(err, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    c = (uint32_t)v;
+  }
+  const int sw = wave_sum_i((int)c);
+  if ((threadIdx.x & 63) == 0) wb[threadIdx.x >> 6] = sw;
+  __syncthreads();
+  const uint32_t base = (uint32_t)(wb[0] + wb[1] + wb[2] + wb[3]);
+  int wpre = 0;
+  for (int i = 0; i < (int)(threadIdx.x >> 6); i++) wpre += wt[i];
+  if (f) tasks[base + wpre + lane_pre] = t;
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_tasks = base + cnt;
+}
+
 __device__ __forceinline__ void plan_count(int f, uint32_t* wg_count) {
   __shared__ int wc[4];
   const uint64_t m = __ballot(f);

@@ -101,6 +101,42 @@ def _s_andnot(*args):
     return RoaringBitmap._pair("andnot", x1, x2)
 
 
+class _OrNot:
+    """RoaringBitmap.orNot(x1, x2, rangeEnd) (static, RB/RoaringBitmap.java:1521-1603) on the class or with
+    three arguments; x1.orNot(x2, rangeEnd) in place (:1431-1506) on an instance with two."""
+
+    def __get__(self, obj, objtype=None):
+        if obj is None:
+            return _s_ornot
+
+        def call(*args):
+            if len(args) == 3:
+                return _s_ornot(*args)
+            other, range_end = args
+            if other is obj:
+                raise NotImplementedError("orNot between a bitmap and itself?")  # UnsupportedOperationException
+            obj._buf = _ornot(obj, other, range_end, True)
+            obj._lcard = None
+
+        call.__doc__ = _s_ornot.__doc__
+        return call
+
+
+def _ornot(x1, x2, range_end, inplace):
+    b = _lib.rbg_buffer()
+    check(lib().rbg_ornot(x1._buf, len(x1._buf), x2._buf, len(x2._buf), int(range_end), int(inplace), ctypes.byref(b)))
+    return take(b)
+
+
+def _s_ornot(x1, x2, range_end):
+    """static orNot(x1, x2, rangeEnd), RB/RoaringBitmap.java:1521-1603: per key up to (rangeEnd - 1) >>> 16,
+    x1 | ~x2 within the range (Container.orNot, x2's complement alone, full containers where neither
+    holds the key), then x1's keys above; x1.orNot(x2, rangeEnd) in place :1431-1506.  rangeEnd outside
+    [0, 2^32] -> IllegalArgumentException.  x1 is not modified (the reference's static form updates x1's
+    container at maxKey in place)."""
+    return RoaringBitmap(_ornot(x1, x2, range_end, False))
+
+
 class RoaringBitmap:
     __slots__ = ("_buf", "_lcard")
 
@@ -233,6 +269,7 @@ class RoaringBitmap:
     or_ = _StaticOrInPlace(_s_or, "or")
     xor = _StaticOrInPlace(_s_xor, "xor")
     andNot = _StaticOrInPlace(_s_andnot, "andnot")
+    orNot = _OrNot()
 
     def _inplace(self, op, x2):
         """x1.and / or / xor / andNot(x2) in place (rbg_pairwise_inplace); x2 may be x1 itself"""
