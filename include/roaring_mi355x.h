@@ -115,16 +115,20 @@ enum { RBG_WIDE_AND = 0, RBG_WIDE_OR = 1, RBG_WIDE_XOR = 2, RBG_WIDE_AND_ITER = 
 enum { RBG_RANGE_AND = 0, RBG_RANGE_OR = 1, RBG_RANGE_XOR = 2, RBG_RANGE_ANDNOT = 3 };
 int rbg_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int64_t range_start,
                  int64_t range_end, rbg_buffer* out);
-/* orNot: inplace 0 = RoaringBitmap.orNot(x1, x2, rangeEnd) (RB/RoaringBitmap.java:1521-1603), 1 =
- * x1.orNot(x2, rangeEnd) (:1431-1506, the new bytes of x1; the caller rejects x2 == x1 as the reference's
- * UnsupportedOperationException).  Per key <= maxKey = (rangeEnd - 1) >>> 16: x1.orNot(x2) / iorNot
+/* orNot: flags 0 = RoaringBitmap.orNot(x1, x2, rangeEnd) (RB/RoaringBitmap.java:1521-1603);
+ * RBG_ORNOT_INPLACE = x1.orNot(x2, rangeEnd) (:1431-1506, the new bytes of x1; the caller rejects x2 == x1 as
+ * the reference's UnsupportedOperationException); | RBG_ORNOT_BUFFER = the buffer package's
+ * ImmutableRoaringBitmap.orNot (RB/buffer/ImmutableRoaringBitmap.java:484-548) / MutableRoaringBitmap.orNot
+ * (RB/buffer/MutableRoaringBitmap.java:962-1030), whose MappeableBitmapContainer.iremove keeps a
+ * 4096-value bitmap (:1003-1017 of MappeableBitmapContainer.java).  Per key <= maxKey = (rangeEnd - 1) >>> 16: x1.orNot(x2) / iorNot
  * (RB/Container.java:191-196, 536-541), full / x1.ior(rangeOfOnes) at maxKey for x1 alone, x2.not(0, end)
  * for x2 alone (not clipped at rangeEnd), full / rangeOfOnes for neither; the key loop bounded by the
  * reference's maxSize estimate; x1's keys above maxKey appended.  rangeEnd in [0, 2^32] (rangeSanityCheck,
  * :204-213) and a negative maxSize (NegativeArraySizeException) -> RBG_ERR_ILLEGAL_ARGUMENT.  x1 is not
  * modified (the reference's static form updates x1's maxKey container through Container.ior, see
  * DESIGN.md §7). */
-int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int64_t range_end, int inplace,
+enum { RBG_ORNOT_INPLACE = 1, RBG_ORNOT_BUFFER = 2 };
+int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int64_t range_end, int flags,
               rbg_buffer* out);
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
@@ -303,7 +307,7 @@ int rbg_ctx_pairwise_serialized(rbg_ctx* ctx, int op, int32_t a, size_t ia, int3
  * shards of a partition are assembled with rbg_ctx_fetch_shard(_device). */
 int rbg_ctx_pairwise_range(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib, int key_lo, int key_hi);
 /* rbg_ornot over device-resident single-bitmap batches; the result pending like rbg_ctx_pairwise's */
-int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int64_t range_end, int inplace);
+int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int64_t range_end, int flags);
 /* Enqueue a cardinality op; the int32 lands in device memory, read by rbg_ctx_card. */
 int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
 /* Enqueue a wide op over every bitmap of a batch, restricted to keys [key_lo, key_hi)

@@ -1569,14 +1569,25 @@ static Ctr range_of_ones(int last) {
 }
 
 // Container.orNot / iorNot (RB/Container.java:191-196, 536-541): or / ior with
-// x.not(0, end).iremove(end, 0x10000) (end < 0x10000) or x.not(0, 0x10000)
-static Ctr c_ornot(const Ctr& c1, const Ctr& c2, int end, bool inplace) {
+// x.not(0, end).iremove(end, 0x10000) (end < 0x10000) or x.not(0, 0x10000).  buf: the buffer package's
+// MappeableContainer.orNot / iorNot (RB/buffer/MappeableContainer.java:214-236), whose containers type
+// like the heap's except MappeableBitmapContainer.iremove, which becomes an array below 4096 values,
+// not at 4096 (RB/buffer/MappeableBitmapContainer.java:1003-1017)
+static Ctr c_ornot(const Ctr& c1, const Ctr& c2, int end, bool inplace, bool buf) {
   Ctr x = c_not_prefix(c2, end);
-  if (end < 0x10000) x = c_remove_range(x, end, 0x10000);
+  if (end < 0x10000) {
+    if (buf && x.kind == BITMAP) {
+      x.card -= card_in_range(x.words, end, 0x10000);
+      reset_range(x.words, end, 0x10000);
+      if (x.card < kArrayMax) x = bitmap_to_array(x);
+    } else {
+      x = c_remove_range(x, end, 0x10000);
+    }
+  }
   return inplace ? c_ior(c1, x) : c_or(c1, x);
 }
 
-Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inplace, bool* neg) {
+Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inplace, bool* neg, bool buf) {
   *neg = false;
   // (int)((rangeEnd - 1) >>> 16): -1 for rangeEnd == 0
   const int max_key = range_end == 0 ? -1 : (int)((range_end - 1) >> 16);
@@ -1605,7 +1616,7 @@ Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inp
     const int e = key == max_key ? last_run : 0x10000;
     Ctr v;
     if (key == s1 && key == s2) {
-      v = c_ornot(x1.ctrs[p1], x2.ctrs[p2], e, inplace);
+      v = c_ornot(x1.ctrs[p1], x2.ctrs[p2], e, inplace, buf);
       ++p1;
       ++p2;
       s1 = p1 < n1 ? x1.keys[p1] : max_key + 1;

@@ -140,8 +140,10 @@ Bitmap range_aggregate(int op, const std::vector<const Bitmap*>& bms, uint64_t s
 Bitmap op_andnot_range(const Bitmap& x1, const Bitmap& x2, uint64_t start, uint64_t end);  // :1396-1423
 // RoaringBitmap.orNot(x1, x2, rangeEnd) (static, RB/RoaringBitmap.java:1521-1603; inplace = false) and
 // x1.orNot(x2, rangeEnd) (:1431-1506; inplace = true).  *neg = true where the reference's maxSize is
-// negative (new char[maxSize] throws NegativeArraySizeException).
-Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inplace, bool* neg);
+// negative (new char[maxSize] throws NegativeArraySizeException).  buf: ImmutableRoaringBitmap.orNot
+// (RB/buffer/ImmutableRoaringBitmap.java:484-548) / MutableRoaringBitmap.orNot (RB/buffer/
+// MutableRoaringBitmap.java:962-1030), the same loop with the buffer package's container types.
+Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inplace, bool* neg, bool buf = false);
 Ctr c_not_prefix(const Ctr& c, int end);  // Container.not(0, end)
 Bitmap fa_horizontal_or(const std::vector<const Bitmap*>& bms);      // FastAggregation.horizontal_or :124-231
 Bitmap fa_horizontal_xor(const std::vector<const Bitmap*>& bms);     // :243-289

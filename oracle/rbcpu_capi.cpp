@@ -138,10 +138,11 @@ int rbo_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t 
   return emit(range_aggregate(op, ptrs, (uint64_t)start, (uint64_t)end), out, out_len);
 }
 
-// RoaringBitmap.orNot(x1, x2, rangeEnd) (inplace 0, RB/RoaringBitmap.java:1521-1603) and
-// x1.orNot(x2, rangeEnd) (inplace 1, :1431-1506).  rangeSanityCheck(0, rangeEnd) -> ERR_ARG; a negative
-// maxSize (the reference's NegativeArraySizeException) -> ERR_ARG with *neg = 1.
-int rbo_ornot(const uint8_t* a, size_t an, const uint8_t* b, size_t bn, int64_t range_end, int inplace,
+// RoaringBitmap.orNot(x1, x2, rangeEnd) (flags 0, RB/RoaringBitmap.java:1521-1603) and
+// x1.orNot(x2, rangeEnd) (flags 1, :1431-1506); flags | 2: the buffer package's (ImmutableRoaringBitmap /
+// MutableRoaringBitmap.orNot, RB/buffer/ImmutableRoaringBitmap.java:484-548, MutableRoaringBitmap.java:962).
+// rangeSanityCheck(0, rangeEnd) -> ERR_ARG; a negative maxSize (the reference's NegativeArraySizeException) -> ERR_ARG with *neg = 1.
+int rbo_ornot(const uint8_t* a, size_t an, const uint8_t* b, size_t bn, int64_t range_end, int flags,
               int* neg, uint8_t** out, size_t* out_len) {
   *neg = 0;
   if (range_end < 0 || range_end > 0x100000000ll) return ERR_ARG;
@@ -150,7 +151,7 @@ int rbo_ornot(const uint8_t* a, size_t an, const uint8_t* b, size_t bn, int64_t 
   if (st) return st;
   if ((st = load(b, bn, &y))) return st;
   bool ng = false;
-  Bitmap r = op_ornot(x, y, (uint64_t)range_end, inplace != 0, &ng);
+  Bitmap r = op_ornot(x, y, (uint64_t)range_end, (flags & 1) != 0, &ng, (flags & 2) != 0);
   if (ng) {
     *neg = 1;
     return ERR_ARG;

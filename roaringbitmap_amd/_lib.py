@@ -26,6 +26,7 @@ WIDE_OP = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_
            "buffer_and_iter": 15}
 WIDE_CARD_OP = {"and": 0, "or": 1}
 RANGE_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3}
+RBG_ORNOT_INPLACE, RBG_ORNOT_BUFFER = 1, 2
 
 
 class rbg_buffer(ctypes.Structure):

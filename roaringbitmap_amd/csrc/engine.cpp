@@ -954,7 +954,7 @@ static int ctx_pairwise_buffer(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib
 // rangeEnd) (in place, :1431-1506), ornot.hip.  rangeSanityCheck(0, rangeEnd) (:204-213).  The
 // reference's maxSize is negative only for rangeEnd == 0 (maxKey = -1) with x1 empty and x2's first
 // container full (new char[-1] throws): only that case reads the plan back before returning.
-static int ctx_ornot(Ctx* c, int32_t ia, size_t ma, int32_t ib, size_t mb, int64_t range_end, bool inplace) {
+static int ctx_ornot(Ctx* c, int32_t ia, size_t ma, int32_t ib, size_t mb, int64_t range_end, int flags) {
   if (range_end < 0 || range_end > (int64_t)0x100000000ll) {
     set_err("rangeEnd should be in [0, 0xffffffff + 1]");
     return RBG_ERR_ILLEGAL_ARGUMENT;
@@ -978,7 +978,7 @@ static int ctx_ornot(Ctx* c, int32_t ia, size_t ma, int32_t ib, size_t mb, int64
   c->mark(0);
   c->mark(1);
   launch_ornot(s, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), na, B->key_off.as<uint32_t>(), db,
-               B->payload.as<uint8_t>(), nb, max_key, last_run, inplace, c->ornot_plan.as<OrNotPlan>(),
+               B->payload.as<uint8_t>(), nb, max_key, last_run, flags, c->ornot_plan.as<OrNotPlan>(),
                c->wg_epoch.as<uint64_t>(), next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->zlb,
                c->ztile, grid_for(ub, 65536));
   c->mark(2);
@@ -2180,9 +2180,9 @@ int rbg_pairwise_inplace(int op, const uint8_t* a, size_t a_len, const uint8_t* 
   return rbg_pairwise(op == RBG_OR ? RBG_OR_INPLACE : op, a, a_len, b, b_len, out);
 }
 
-int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int64_t range_end, int inplace,
+int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int64_t range_end, int flags,
               rbg_buffer* out) {
-  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!out || flags < 0 || flags > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
@@ -2191,14 +2191,14 @@ int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, in
   int32_t ids[2];
   CHK(ctx_load_separate(c, bufs, lens, 2, ids));
   g.ids = {ids[0], ids[1]};
-  CHK(ctx_ornot(c, ids[0], 0, ids[1], 0, range_end, inplace != 0));
+  CHK(ctx_ornot(c, ids[0], 0, ids[1], 0, range_end, flags));
   return ctx_fetch(c, out);
 }
 
-int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int64_t range_end, int inplace) {
-  if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
+int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int64_t range_end, int flags) {
+  if (!ctx || flags < 0 || flags > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
   CHK(enter(&ctx->c));
-  return ctx_ornot(&ctx->c, a, ia, b, ib, range_end, inplace != 0);
+  return ctx_ornot(&ctx->c, a, ia, b, ib, range_end, flags);
 }
 
 int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int32_t* out) {

@@ -374,9 +374,10 @@ struct OrNotPlan {
   int32_t max_size;
   int32_t correction;
 };
-// k_ornot_scan -> k_plan_ornot -> k_ornot<inplace> over single-bitmap batches A (x1) and B (x2)
+// k_ornot_scan -> k_plan_ornot -> k_ornot over single-bitmap batches A (x1) and B (x2); flags: 1 in place,
+// 2 the buffer package's types (RBG_ORNOT_INPLACE / RBG_ORNOT_BUFFER)
 void launch_ornot(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint8_t* pa, int na, const uint32_t* kob,
-                  const CDesc* db, const uint8_t* pb, int nb, int max_key, int last_run, bool inplace, OrNotPlan* plan,
+                  const CDesc* db, const uint8_t* pb, int nb, int max_key, int last_run, int flags, OrNotPlan* plan,
                   uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint64_t* zlb,
                   uint64_t* ztile, int grid);
 

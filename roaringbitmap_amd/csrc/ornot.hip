@@ -164,14 +164,17 @@ __device__ __forceinline__ void vb_not_prefix(VB& v, int e, uint32_t* lds, int* 
 }
 // v.iremove(e, 0x10000): ArrayContainer.iremove stays an array, BitmapContainer.iremove becomes one at
 // <= 4096 values, RunContainer.iremove stays a run container (RB/ArrayContainer.java:759-780,
-// RB/BitmapContainer.java:788-802, RB/RunContainer.java:1553-...)
+// RB/BitmapContainer.java:788-802, RB/RunContainer.java:1553-...).  BUF: MappeableBitmapContainer.iremove
+// becomes an array only below 4096 values (RB/buffer/MappeableBitmapContainer.java:1003-1017); a bitmap of
+// exactly 4096 values keeps its words as payload.
+template <bool BUF>
 __device__ __forceinline__ void vb_clip(VB& v, int e, int* sh) {
   int w[4];
   owned_words(w);
 #pragma unroll
   for (int i = 0; i < 4; i++) v.r[i] &= prefix_mask(w[i], e);
   const int c = vb_card(v.r, sh);
-  if (v.kind != DK_R) v.kind = by_card(c);
+  if (v.kind == DK_B && (BUF ? c < 4096 : c <= 4096)) v.kind = DK_A;
   v.card = c;
 }
 // Container.rangeOfOnes(0, e) (RB/Container.java:29-37): an array up to 2 values, else a run container
@@ -186,7 +189,10 @@ __device__ __forceinline__ void vb_range_ones(VB& v, int e) {
   v.src = -1;
 }
 
-template <bool INPLACE>
+// INPLACE: x1.orNot (iorNot, ior); BUF: the buffer package's ImmutableRoaringBitmap.orNot /
+// MutableRoaringBitmap.orNot (RB/buffer/ImmutableRoaringBitmap.java:484-548, MutableRoaringBitmap.java
+// :962-1030), whose containers type like the heap's but for vb_clip
+template <bool INPLACE, bool BUF>
 __global__ __launch_bounds__(256) void k_ornot(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                                const uint8_t* pa, const uint8_t* pb, int max_key, int last_run,
                                                OutCtx oc) {
@@ -235,7 +241,7 @@ __global__ __launch_bounds__(256) void k_ornot(const PTask* __restrict__ tasks, 
     if (ib) {
       pb_load(tk.slot_b, tk.card_b, tk.key, tk.kind_b, 1, pb, tmp, q, y);
       vb_not_prefix(y, e, acc, sh);
-      if (ia && e < 65536) vb_clip(y, e, sh);
+      if (ia && e < 65536) vb_clip<BUF>(y, e, sh);
     } else {
       vb_range_ones(y, e);
     }
@@ -259,18 +265,23 @@ __global__ __launch_bounds__(256) void k_ornot(const PTask* __restrict__ tasks, 
 }
 
 void launch_ornot(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint8_t* pa, int na, const uint32_t* kob,
-                  const CDesc* db, const uint8_t* pb, int nb, int max_key, int last_run, bool inplace, OrNotPlan* plan,
+                  const CDesc* db, const uint8_t* pb, int nb, int max_key, int last_run, int flags, OrNotPlan* plan,
                   uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint64_t* zlb,
                   uint64_t* ztile, int grid) {
   hipLaunchKernelGGL(k_ornot_scan, dim3(1), dim3(1024), 0, s, koa, na, kob, db, nb, max_key, plan);
   hipLaunchKernelGGL(k_plan_ornot, dim3(256), dim3(256), 0, s, koa, da, pa, kob, db, pb, max_key, plan, wg_epoch,
                      epoch, tasks, n_tasks, zlb, ztile, oc.err);
-  const void* k = inplace ? (const void*)&k_ornot<true> : (const void*)&k_ornot<false>;
-  const int g = std::max(1, std::min(grid, resident_grid(k)));
-  if (inplace)
-    hipLaunchKernelGGL(k_ornot<true>, dim3(g), dim3(256), 0, s, tasks, n_tasks, pa, pb, max_key, last_run, oc);
-  else
-    hipLaunchKernelGGL(k_ornot<false>, dim3(g), dim3(256), 0, s, tasks, n_tasks, pa, pb, max_key, last_run, oc);
+  const int g0 = std::max(1, grid);
+#define RBG_ORNOT_LAUNCH(I, B)                                                                            \
+  hipLaunchKernelGGL((k_ornot<I, B>), dim3(std::min(g0, resident_grid((const void*)&k_ornot<I, B>))), dim3(256), 0, \
+                     s, tasks, n_tasks, pa, pb, max_key, last_run, oc)
+  switch (flags & 3) {
+    case 0: RBG_ORNOT_LAUNCH(false, false); break;
+    case 1: RBG_ORNOT_LAUNCH(true, false); break;
+    case 2: RBG_ORNOT_LAUNCH(false, true); break;
+    default: RBG_ORNOT_LAUNCH(true, true); break;
+  }
+#undef RBG_ORNOT_LAUNCH
 }
 
 }  // namespace rbg

@@ -119,10 +119,11 @@ class Engine:
             check(lib().rbg_ctx_pairwise_range(self._ctx, _lib.OP[op], int(a), int(ia), int(b), int(ib), int(key_lo),
                                                int(key_hi)))
 
-    def ornot(self, a, b, range_end, inplace=False, ia=0, ib=0):
-        """RoaringBitmap.orNot(x1, x2, rangeEnd) (inplace: x1.orNot(x2, rangeEnd)) of two resident bitmaps;
-        the result pending like pairwise's (rbg_ctx_ornot)."""
-        check(lib().rbg_ctx_ornot(self._ctx, int(a), int(ia), int(b), int(ib), int(range_end), int(bool(inplace))))
+    def ornot(self, a, b, range_end, inplace=False, buffer=False, ia=0, ib=0):
+        """RoaringBitmap.orNot(x1, x2, rangeEnd) (inplace: x1.orNot(x2, rangeEnd); buffer: the buffer
+        package's) of two resident bitmaps; the result pending like pairwise's (rbg_ctx_ornot)."""
+        flags = (_lib.RBG_ORNOT_INPLACE if inplace else 0) | (_lib.RBG_ORNOT_BUFFER if buffer else 0)
+        check(lib().rbg_ctx_ornot(self._ctx, int(a), int(ia), int(b), int(ib), int(range_end), flags))
 
     def pairwise_serialized(self, op, a, b, ia=0, ib=0):
         """pairwise(op) + serialize() as one pipeline (rbg_ctx_pairwise_serialized): the result's

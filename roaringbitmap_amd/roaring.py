@@ -103,28 +103,34 @@ def _s_andnot(*args):
 
 class _OrNot:
     """RoaringBitmap.orNot(x1, x2, rangeEnd) (static, RB/RoaringBitmap.java:1521-1603) on the class or with
-    three arguments; x1.orNot(x2, rangeEnd) in place (:1431-1506) on an instance with two."""
+    three arguments; x1.orNot(x2, rangeEnd) in place (:1431-1506) on an instance with two.  buffer: the
+    buffer package's (MutableRoaringBitmap.orNot, RB/buffer/MutableRoaringBitmap.java:962-1030)."""
+
+    def __init__(self, static, buffer=False):
+        self.static, self.buffer = static, buffer
+        self.__doc__ = static.__doc__
 
     def __get__(self, obj, objtype=None):
         if obj is None:
-            return _s_ornot
+            return self.static
 
         def call(*args):
             if len(args) == 3:
-                return _s_ornot(*args)
+                return self.static(*args)
             other, range_end = args
             if other is obj:
                 raise NotImplementedError("orNot between a bitmap and itself?")  # UnsupportedOperationException
-            obj._buf = _ornot(obj, other, range_end, True)
+            obj._buf = _ornot(obj, other, range_end, True, self.buffer)
             obj._lcard = None
 
-        call.__doc__ = _s_ornot.__doc__
+        call.__doc__ = self.static.__doc__
         return call
 
 
-def _ornot(x1, x2, range_end, inplace):
+def _ornot(x1, x2, range_end, inplace, buffer=False):
     b = _lib.rbg_buffer()
-    check(lib().rbg_ornot(x1._buf, len(x1._buf), x2._buf, len(x2._buf), int(range_end), int(inplace), ctypes.byref(b)))
+    flags = (_lib.RBG_ORNOT_INPLACE if inplace else 0) | (_lib.RBG_ORNOT_BUFFER if buffer else 0)
+    check(lib().rbg_ornot(x1._buf, len(x1._buf), x2._buf, len(x2._buf), int(range_end), flags, ctypes.byref(b)))
     return take(b)
 
 
@@ -269,7 +275,7 @@ class RoaringBitmap:
     or_ = _StaticOrInPlace(_s_or, "or")
     xor = _StaticOrInPlace(_s_xor, "xor")
     andNot = _StaticOrInPlace(_s_andnot, "andnot")
-    orNot = _OrNot()
+    orNot = _OrNot(_s_ornot)
 
     def _inplace(self, op, x2):
         """x1.and / or / xor / andNot(x2) in place (rbg_pairwise_inplace); x2 may be x1 itself"""
@@ -717,6 +723,11 @@ class ImmutableRoaringBitmap(RoaringBitmap):
         """xor(x1, x2) :1087-1134"""
         return ImmutableRoaringBitmap._bpair("xor", x1, x2)
 
+    @staticmethod
+    def orNot(x1, x2, range_end):
+        """orNot(x1, x2, rangeEnd) :484-548 -> MutableRoaringBitmap (the buffer package's container types)"""
+        return MutableRoaringBitmap(_ornot(x1, x2, range_end, False, True))
+
     and_ = _s_and
     andNot = _s_andnot
     or_ = _s_or
@@ -739,6 +750,7 @@ class MutableRoaringBitmap(ImmutableRoaringBitmap):
     andNot = _StaticOrInPlace(ImmutableRoaringBitmap._s_andnot, "andnot_buffer")
     or_ = _StaticOrInPlace(ImmutableRoaringBitmap._s_or, "or")
     xor = _StaticOrInPlace(ImmutableRoaringBitmap._s_xor, "xor")
+    orNot = _OrNot(ImmutableRoaringBitmap.__dict__["orNot"].__func__, buffer=True)  # x1.orNot in place :962-1030
 
     def _inplace(self, op, x2):
         if op not in ("and_buffer", "andnot_buffer"):

@@ -249,13 +249,14 @@ class NegativeArraySize(OracleError):
     """The reference's orNot sizes its key array with a negative maxSize (NegativeArraySizeException)."""
 
 
-def ornot(a, b, range_end, inplace=False) -> bytes:
+def ornot(a, b, range_end, inplace=False, buffer=False) -> bytes:
     """RoaringBitmap.orNot(x1, x2, rangeEnd) (RB/RoaringBitmap.java:1521-1603) or, inplace, x1.orNot(x2,
-    rangeEnd) (:1431-1506)."""
+    rangeEnd) (:1431-1506); buffer: ImmutableRoaringBitmap.orNot / MutableRoaringBitmap.orNot
+    (RB/buffer/ImmutableRoaringBitmap.java:484-548, MutableRoaringBitmap.java:962-1030)."""
     p = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     neg = ctypes.c_int()
-    st = lib().rbo_ornot(a, len(a), b, len(b), range_end, int(inplace), ctypes.byref(neg), ctypes.byref(p),
+    st = lib().rbo_ornot(a, len(a), b, len(b), range_end, int(inplace) | (2 if buffer else 0), ctypes.byref(neg), ctypes.byref(p),
                          ctypes.byref(n))
     if neg.value:
         raise NegativeArraySize(st)

@@ -33,6 +33,13 @@ def _check(a, b, end, tag=""):
     y = rb.RoaringBitmap(a)
     y.orNot(x2, end)
     assert y.serialize() == O.ornot(a, b, end, inplace=True), f"inplace {tag} end={end}"
+    # the buffer package: ImmutableRoaringBitmap.orNot (static) and MutableRoaringBitmap.orNot (in place)
+    got = rb.ImmutableRoaringBitmap.orNot(rb.ImmutableRoaringBitmap(a), rb.ImmutableRoaringBitmap(b), end)
+    assert isinstance(got, rb.MutableRoaringBitmap)
+    assert got.serialize() == O.ornot(a, b, end, buffer=True), f"buffer static {tag} end={end}"
+    m = rb.MutableRoaringBitmap(a)
+    m.orNot(rb.ImmutableRoaringBitmap(b), end)
+    assert m.serialize() == O.ornot(a, b, end, inplace=True, buffer=True), f"buffer inplace {tag} end={end}"
 
 
 
@@ -105,6 +112,12 @@ def test_quirks_and_errors(gpu):
     # BitmapContainer.ior(ArrayContainer) keeps a full bitmap in place; or() gives the full run
     _check(encode([(0, B, np.arange(1, 65536))]), encode([(0, B, np.arange(1, 65536))]), 1 << 16, "ior-full")
     _check(encode([(0, B, np.arange(1, 65536))]), bm(), 1, "ior-full-maxkey")
+    # the buffer package keeps a 4096-value bitmap through iremove (its payload the 1024 words)
+    e = 10000
+    c2 = encode([(0, B, np.concatenate([np.arange(0, e - 4096), np.arange(20000, 30001)]))])
+    c1 = encode([(0, A, np.array([e - 4096, e - 1]))])
+    assert O.ornot(c1, c2, e, buffer=True) != O.ornot(c1, c2, e)
+    _check(c1, c2, e, "buffer-4096")
     # rangeEnd == 0: x1 cloned, or NegativeArraySizeException (x1 empty, x2's first container full)
     full01 = encode([(0, R, np.arange(65536)), (1, R, np.arange(65536))])
     _check(bm(3, 1 << 20), full01, 0, "end0")

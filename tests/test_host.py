@@ -214,6 +214,23 @@ def test_pairwise_op_codes_match_header():
     for k, c in names.items():
         m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
         assert m and int(m.group(1)) == L.OP[k], k
+    for c in ("RBG_ORNOT_INPLACE", "RBG_ORNOT_BUFFER"):  # rbg_ornot's flags
+        m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
+        assert m and int(m.group(1)) == getattr(L, c), c
+
+
+def test_ornot_self_and_arguments_need_no_device():
+    """x1.orNot(x1, end) is the reference's UnsupportedOperationException (RB/RoaringBitmap.java:1432-1434,
+    RB/buffer/MutableRoaringBitmap.java:963-965), raised before any device call; ImmutableRoaringBitmap
+    has the static form only."""
+    from roaringbitmap_amd import ImmutableRoaringBitmap, MutableRoaringBitmap, RoaringBitmap
+    buf = O.from_values(np.arange(10))
+    for cls in (RoaringBitmap, MutableRoaringBitmap):
+        x = cls(buf)
+        with pytest.raises(NotImplementedError):
+            x.orNot(x, 5)
+    with pytest.raises(TypeError):
+        ImmutableRoaringBitmap.orNot(ImmutableRoaringBitmap(buf), 5)
 
 
 def test_mutable_same_object_needs_no_device():

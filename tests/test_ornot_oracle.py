@@ -249,3 +249,30 @@ def test_container_types():
     c2 = encode([(0, B, np.arange(1, 65536))])  # not -> {0}: array
     assert [c[1] for c in decode(O.ornot(c1, c2, 1 << 16))] == [R]
     assert [c[1] for c in decode(O.ornot(c1, c2, 1 << 16, inplace=True))] == [B]
+
+
+def test_buffer_package_types():
+    """ImmutableRoaringBitmap.orNot / MutableRoaringBitmap.orNot (RB/buffer/ImmutableRoaringBitmap.java:484-548,
+    MutableRoaringBitmap.java:962-1030) run the same loop; their containers type like the heap's except
+    MappeableBitmapContainer.iremove, an array only below 4096 values (RB/buffer/MappeableBitmapContainer.java
+    :1003-1017).  x2's complement clipped to exactly 4096 values, or'ed with a subset of it: the heap gives an
+    array, the buffer package a bitmap -- whose 4096-value payload is its 1024 words (a card-4096 container
+    reads back as an array in the portable format, so only the payload bytes tell them apart)."""
+    e = 10000
+    c2 = encode([(0, B, np.concatenate([np.arange(0, e - 4096), np.arange(20000, 30001)]))])
+    c1 = encode([(0, A, np.array([e - 4096, e - 1]))])
+    want = np.arange(e - 4096, e)
+    words = np.zeros(1024, dtype=np.uint64)
+    np.bitwise_or.at(words, want >> 6, np.uint64(1) << (want.astype(np.uint64) & np.uint64(63)))
+    for inplace in (False, True):
+        heap, buf = O.ornot(c1, c2, e, inplace), O.ornot(c1, c2, e, inplace, buffer=True)
+        assert heap[-8192:] == want.astype("<u2").tobytes()
+        assert buf[-8192:] == words.astype("<u8").tobytes()
+    # elsewhere the bytes agree
+    rng = np.random.default_rng(4)
+    for _ in range(6):
+        v1 = np.unique(rng.integers(0, 3 << 16, 200)).astype(np.uint32)
+        v2 = np.unique(rng.integers(0, 3 << 16, 5000)).astype(np.uint32)
+        a, b = O.from_values(v1), O.from_values(v2)
+        for end in (1 << 16, (2 << 16) + 999, 3 << 16):
+            assert O.ornot(a, b, end, buffer=True) == O.ornot(a, b, end)
