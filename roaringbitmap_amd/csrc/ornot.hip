@@ -259,6 +259,12 @@ __global__ __launch_bounds__(256) void k_ornot(const PTask* __restrict__ tasks, 
       wg_place(t, false, nullptr, true, tmp, 0, 0, key, DK_A, oc, nullptr);
       continue;
     }
+    if (z.kind == DK_B) {  // registers straight to the task's slot (no LDS staging)
+      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+      store_bitmap_owned(slot, z.r);
+      wg_place(t, true, slot, false, nullptr, 8192, (uint32_t)z.card, key, DK_B, oc, nullptr);
+      continue;
+    }
     const uint32_t len = stage_container(z.kind, z.r, z.card, acc, tmp, sh);
     wg_place(t, true, nullptr, true, tmp, len, (uint32_t)z.card, key, z.kind, oc, nullptr);
   }

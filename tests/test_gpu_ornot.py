@@ -155,3 +155,23 @@ def test_resident_batches(gpu):
     for end, inplace in ((7 << 16, False), ((12 << 16) + 5, True), (1 << 32, False)):
         eng.ornot(ia, ib, end, inplace)
         assert eng.fetch().serialize() == O.ornot(a, b, end, inplace), (end, inplace)
+
+
+def _realdata(ds):
+    z = np.load(os.path.join(HERE, "golden", "realdata", ds + ".npz"))
+    v, o = z["values"], z["offsets"]
+    return [v[o[i]:o[i + 1]] for i in range(len(o) - 1)]
+
+
+@pytest.mark.parametrize("ds", ["census1881", "wikileaks-noquotes", "uscensus2000"])
+def test_realdata_pairwise_ornot(gpu, ds):
+    """jmh/.../realdata/RealDataBenchmarkOrNot.java:20-27 pairwiseOrNot: for k, b[k].clone().orNot(b[k+1],
+    b[k].last()) in place and RoaringBitmap.orNot(b[k], b[k+1], toUnsignedLong(b[k].last())), every 9th pair
+    (runOptimize'd inputs on odd pairs) against the oracle"""
+    rb = _rb()
+    sets = _realdata(ds)
+    for k in range(0, len(sets) - 1, 9):
+        a = O.from_values(sets[k], k % 2 == 1)
+        b = O.from_values(sets[k + 1], k % 2 == 1)
+        last = int(sets[k].max())
+        _check(a, b, last, f"{ds}[{k}]")
