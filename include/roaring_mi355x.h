@@ -112,7 +112,19 @@ enum { RBG_WIDE_AND = 0, RBG_WIDE_OR = 1, RBG_WIDE_XOR = 2, RBG_WIDE_AND_ITER = 
  *   RBG_RANGE_ANDNOT  andNot(x1, x2, rangeStart, rangeEnd) :1396-1404 (n == 2)
  * rangeSanityCheck (:204-213): rangeStart in [0, 2^32 - 1], rangeEnd in [0, 2^32], else
  * RBG_ERR_ILLEGAL_ARGUMENT; rangeEnd <= rangeStart gives the empty bitmap. */
-enum { RBG_RANGE_AND = 0, RBG_RANGE_OR = 1, RBG_RANGE_XOR = 2, RBG_RANGE_ANDNOT = 3 };
+/* The buffer package's forms, RB/buffer/ImmutableRoaringBitmap.java (MutableRoaringBitmap results):
+ *   RBG_RANGE_BUFFER_AND     and(Iterator, rangeStart, rangeEnd) :261-267 -> BufferFastAggregation.and
+ *                            (Iterator) = workShyAnd for any input count (RB/buffer/BufferFastAggregation.java
+ *                            :66-89, 505-576)
+ *   RBG_RANGE_BUFFER_OR      or(Iterator, rangeStart, rangeEnd) :992-998 -> naive_or
+ *   RBG_RANGE_BUFFER_XOR     xor(Iterator, rangeStart, rangeEnd) :1048-1053 -> naive_xor
+ *   RBG_RANGE_BUFFER_ANDNOT  andNot(x1, x2, rangeStart, rangeEnd) :402-408 -> ImmutableRoaringBitmap.andNot
+ *                            (RBG_ANDNOT_BUFFER's types)
+ * whose selectRangeWithoutCopy (:768-820) cuts through MappeableContainer.remove: a bitmap becomes an
+ * array only below 4096 values (RB/buffer/MappeableBitmapContainer.java:1597-1612).  The buffer xor has
+ * no rangeSanityCheck in the reference; here every form checks the range. */
+enum { RBG_RANGE_AND = 0, RBG_RANGE_OR = 1, RBG_RANGE_XOR = 2, RBG_RANGE_ANDNOT = 3, RBG_RANGE_BUFFER_AND = 4,
+       RBG_RANGE_BUFFER_OR = 5, RBG_RANGE_BUFFER_XOR = 6, RBG_RANGE_BUFFER_ANDNOT = 7 };
 int rbg_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int64_t range_start,
                  int64_t range_end, rbg_buffer* out);
 /* orNot: flags 0 = RoaringBitmap.orNot(x1, x2, rangeEnd) (RB/RoaringBitmap.java:1521-1603);

@@ -1444,8 +1444,10 @@ Bitmap buf_and(const std::vector<const Bitmap*>& bms, const int* ids) {
 // (RB/ArrayContainer.java:1039-1061, 759-780) stay arrays; BitmapContainer.remove / iremove
 // (RB/BitmapContainer.java:1166-1181, 788-802) become arrays at <= 4096 values; RunContainer.remove
 // = clone().iremove (RB/RunContainer.java:2032-2035, 1553-...) stays a run container, its runs clipped.
-// end == begin: unchanged (remove returns a clone, iremove this).
-static Ctr c_remove_range(const Ctr& c, int begin, int end) {
+// end == begin: unchanged (remove returns a clone, iremove this).  buf: the buffer package's
+// MappeableBitmapContainer.remove / iremove, an array only below 4096 values
+// (RB/buffer/MappeableBitmapContainer.java:1597-1612, 1003-1017); its array and run forms cut alike.
+static Ctr c_remove_range(const Ctr& c, int begin, int end, bool buf = false) {
   if (end == begin) return c;
   if (c.kind == ARRAY) {
     std::vector<uint16_t> v;
@@ -1457,7 +1459,7 @@ static Ctr c_remove_range(const Ctr& c, int begin, int end) {
     Ctr b = c;
     b.card -= card_in_range(b.words, begin, end);
     reset_range(b.words, begin, end);
-    if (b.card <= kArrayMax) return bitmap_to_array(b);
+    if (buf ? b.card < kArrayMax : b.card <= kArrayMax) return bitmap_to_array(b);
     return b;
   }
   std::vector<uint16_t> pairs;
@@ -1480,8 +1482,10 @@ static Ctr c_remove_range(const Ctr& c, int begin, int end) {
 
 // selectRangeWithoutCopy(RoaringBitmap, rangeStart, rangeEnd): the containers of the keys inside the
 // range as they are, the first key's container through remove(0, lbStart), the last key's through
-// remove(lbLast + 1, 65536) (one key: both), empty ones dropped
-Bitmap select_range(const Bitmap& b, uint64_t start, uint64_t end) {
+// remove(lbLast + 1, 65536) (one key: both), empty ones dropped.  buf: the buffer package's
+// ImmutableRoaringBitmap.selectRangeWithoutCopy (RB/buffer/ImmutableRoaringBitmap.java:768-820), the
+// same cuts with MappeableContainer.remove
+Bitmap select_range(const Bitmap& b, uint64_t start, uint64_t end, bool buf) {
   Bitmap ans;
   if (end <= start) return ans;
   const int hbs = (int)(start >> 16), lbs = (int)(start & 0xFFFF);
@@ -1490,8 +1494,8 @@ Bitmap select_range(const Bitmap& b, uint64_t start, uint64_t end) {
     const int k = b.keys[i];
     if (k < hbs || k > hbl) continue;
     Ctr c = b.ctrs[i];
-    if (k == hbs) c = c_remove_range(c, 0, lbs);
-    if (k == hbl) c = c_remove_range(c, lbl + 1, 65536);
+    if (k == hbs) c = c_remove_range(c, 0, lbs, buf);
+    if (k == hbl) c = c_remove_range(c, lbl + 1, 65536, buf);
     if (!c.empty()) {
       ans.keys.push_back((uint16_t)k);
       ans.ctrs.push_back(std::move(c));
@@ -1515,6 +1519,23 @@ Bitmap range_aggregate(int op, const std::vector<const Bitmap*>& bms, uint64_t s
 
 Bitmap op_andnot_range(const Bitmap& x1, const Bitmap& x2, uint64_t start, uint64_t end) {
   return op_andnot(select_range(x1, start, end), select_range(x2, start, end));
+}
+
+// The buffer package's range forms, RB/buffer/ImmutableRoaringBitmap.java: every input through its
+// selectRangeWithoutCopy, then and(Iterator, start, end) :261-267 -> BufferFastAggregation.and(Iterator)
+// = workShyAnd for any count (RB/buffer/BufferFastAggregation.java:66-89, 505-576; no input: empty);
+// or :992-998 -> naive_or (:886-888, 791-798); xor :1048-1053 -> naive_xor (:1072-1074, 843-849);
+// andNot(x1, x2, start, end) :402-408 -> ImmutableRoaringBitmap.andNot (the buffer run types)
+Bitmap range_aggregate_buf(int op, const std::vector<const Bitmap*>& bms, uint64_t start, uint64_t end) {
+  std::vector<Bitmap> sel;
+  sel.reserve(bms.size());
+  for (const Bitmap* b : bms) sel.push_back(select_range(*b, start, end, true));
+  std::vector<const Bitmap*> ptrs;
+  for (const Bitmap& b : sel) ptrs.push_back(&b);
+  if (op == 0) return ptrs.empty() ? Bitmap() : fa_workshy_and(ptrs);
+  if (op == 1) return fa_or(ptrs);
+  if (op == 2) return fa_xor(ptrs);
+  return op_andnot_buf(sel[0], sel[1]);
 }
 
 // ---------------------------------------------------------------------------

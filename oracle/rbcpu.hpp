@@ -135,9 +135,11 @@ Bitmap buf_and(const std::vector<const Bitmap*>& bms, const int* ids);        //
 Bitmap buf_naive_and(const std::vector<const Bitmap*>& bms, const int* ids);  // naive_and(Immutable...) :347-369
 Bitmap buf_and_iter(const std::vector<const Bitmap*>& bms);  // naive_and(Iterator) :383-396, (Mutable...) :407-416
 // range-restricted aggregations, RB/RoaringBitmap.java (selectRangeWithoutCopy, then the op)
-Bitmap select_range(const Bitmap& b, uint64_t start, uint64_t end);
+Bitmap select_range(const Bitmap& b, uint64_t start, uint64_t end, bool buf = false);
 Bitmap range_aggregate(int op, const std::vector<const Bitmap*>& bms, uint64_t start, uint64_t end);  // 0 and 1 or 2 xor
 Bitmap op_andnot_range(const Bitmap& x1, const Bitmap& x2, uint64_t start, uint64_t end);  // :1396-1423
+// the buffer package's (ImmutableRoaringBitmap): 0 and (workShyAnd), 1 or, 2 xor, 3 andNot (n == 2)
+Bitmap range_aggregate_buf(int op, const std::vector<const Bitmap*>& bms, uint64_t start, uint64_t end);
 // RoaringBitmap.orNot(x1, x2, rangeEnd) (static, RB/RoaringBitmap.java:1521-1603; inplace = false) and
 // x1.orNot(x2, rangeEnd) (:1431-1506; inplace = true).  *neg = true where the reference's maxSize is
 // negative (new char[maxSize] throws NegativeArraySizeException).  buf: ImmutableRoaringBitmap.orNot

@@ -118,6 +118,8 @@ int rbo_wide(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, c
 
 // RoaringBitmap.and / or / xor(Iterator, rangeStart, rangeEnd) (op 0 / 1 / 2) and andNot(x1, x2,
 // rangeStart, rangeEnd) (op 3, n == 2): RB/RoaringBitmap.java:1308-1336, 2536-2557, 3359-3379, 1396-1423.
+// op 4: selectRangeWithoutCopy alone; ops 5-8: ImmutableRoaringBitmap's and / or / xor / andNot range
+// forms (RB/buffer/ImmutableRoaringBitmap.java:261, 992, 1048, 402); op 9: the buffer selection alone.
 // rangeSanityCheck (:204-213) -> ERR_ARG.
 int rbo_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int64_t start, int64_t end,
                  uint8_t** out, size_t* out_len) {
@@ -130,9 +132,13 @@ int rbo_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t 
     if (n != 2) return ERR_ARG;
     return emit(op_andnot_range(bms[0], bms[1], (uint64_t)start, (uint64_t)end), out, out_len);
   }
-  if (op == 4) {  // selectRangeWithoutCopy alone (n == 1)
+  if (op == 4 || op == 9) {  // selectRangeWithoutCopy alone (n == 1)
     if (n != 1) return ERR_ARG;
-    return emit(select_range(bms[0], (uint64_t)start, (uint64_t)end), out, out_len);
+    return emit(select_range(bms[0], (uint64_t)start, (uint64_t)end, op == 9), out, out_len);
+  }
+  if (op >= 5 && op <= 8) {
+    if (op == 8 && n != 2) return ERR_ARG;
+    return emit(range_aggregate_buf(op - 5, ptrs, (uint64_t)start, (uint64_t)end), out, out_len);
   }
   if (op < 0 || op > 2) return ERR_ARG;
   return emit(range_aggregate(op, ptrs, (uint64_t)start, (uint64_t)end), out, out_len);

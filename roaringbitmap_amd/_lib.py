@@ -25,7 +25,8 @@ WIDE_OP = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_
            "priorityqueue_or": 11, "priorityqueue_xor": 12, "buffer_and": 13, "buffer_naive_and": 14,
            "buffer_and_iter": 15}
 WIDE_CARD_OP = {"and": 0, "or": 1}
-RANGE_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3}
+RANGE_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3,
+            "and_buffer": 4, "or_buffer": 5, "xor_buffer": 6, "andnot_buffer": 7}  # ImmutableRoaringBitmap's
 RBG_ORNOT_INPLACE, RBG_ORNOT_BUFFER = 1, 2
 
 

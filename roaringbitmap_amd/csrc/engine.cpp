@@ -2241,33 +2241,61 @@ int rbg_wide(int op, const uint8_t* const* bufs, const size_t* lens, const int32
   return ctx_fetch(c, out);
 }
 
-static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int32_t* out_id);
+static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int32_t* out_id, bool buf = false);
+// rangeSanityCheck (RB/RoaringBitmap.java:204-213)
+static int check_range(int64_t start, int64_t end) {
+  if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll) {
+    set_err("rangeStart=" + std::to_string(start) + " should be in [0, 0xffffffff], rangeEnd=" + std::to_string(end) +
+            " in [0, 0xffffffff + 1]");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  return RBG_OK;
+}
 
 int rbg_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t n, int64_t range_start,
                  int64_t range_end, rbg_buffer* out) {
-  if (!out || op < RBG_RANGE_AND || op > RBG_RANGE_ANDNOT || (op == RBG_RANGE_ANDNOT && n != 2))
+  if (!out || op < RBG_RANGE_AND || op > RBG_RANGE_BUFFER_ANDNOT ||
+      ((op == RBG_RANGE_ANDNOT || op == RBG_RANGE_BUFFER_ANDNOT) && n != 2))
     return RBG_ERR_ILLEGAL_ARGUMENT;
+  const bool buf = op >= RBG_RANGE_BUFFER_AND;
+  const int base = buf ? op - RBG_RANGE_BUFFER_AND : op;
+  if (buf && base == RBG_RANGE_AND && n == 0) {
+    // BufferFastAggregation.and(long[], Iterator) with no input: an empty bitmap (:81-88)
+    CHK(check_range(range_start, range_end));
+    static const uint8_t kEmpty[8] = {0x3A, 0x30, 0, 0, 0, 0, 0, 0};
+    uint8_t* p = (uint8_t*)std::malloc(8);
+    if (!p) return RBG_ERR_OUT_OF_MEMORY;
+    std::memcpy(p, kEmpty, 8);
+    out->data = p;
+    out->len = 8;
+    return RBG_OK;
+  }
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
-  if (op == RBG_RANGE_ANDNOT) {  // andNot(x1, x2, start, end): both operands selected, then andNot
+  if (base == RBG_RANGE_ANDNOT) {  // andNot(x1, x2, start, end): both operands selected, then andNot
     int32_t ids[2], sel[2];
     CHK(ctx_load_separate(c, bufs, lens, 2, ids));
     g.ids = {ids[0], ids[1]};
     for (int i = 0; i < 2; i++) {
-      CHK(ctx_select_range(c, ids[i], range_start, range_end, &sel[i]));
+      CHK(ctx_select_range(c, ids[i], range_start, range_end, &sel[i], buf));
       g.ids.push_back(sel[i]);
     }
-    CHK(ctx_pairwise(c, OP_ANDNOT, sel[0], 0, sel[1], 0, false));
+    // the buffer package's andNot keeps R \ R's merged run container (ImmutableRoaringBitmap.andNot)
+    CHK(ctx_pairwise(c, buf ? RBG_ANDNOT_BUFFER : OP_ANDNOT, sel[0], 0, sel[1], 0, false));
     return ctx_fetch(c, out);
   }
   int32_t id, sel;
   CHK(ctx_load(c, bufs, lens, n, &id));
   g.ids.push_back(id);
-  CHK(ctx_select_range(c, id, range_start, range_end, &sel));
+  CHK(ctx_select_range(c, id, range_start, range_end, &sel, buf));
   g.ids.push_back(sel);
-  // and -> FastAggregation.and(Iterator) = naive_and(Iterator); or / xor -> naive_or / naive_xor
-  const int wop = op == RBG_RANGE_AND ? RBG_WIDE_AND_ITER : op == RBG_RANGE_OR ? RBG_WIDE_OR : RBG_WIDE_XOR;
+  // heap: and -> FastAggregation.and(Iterator) = naive_and(Iterator); or / xor -> naive_or / naive_xor.
+  // buffer: and -> BufferFastAggregation.and(Iterator) = workShyAnd for any count (no input: empty);
+  // or / xor -> naive_or / naive_xor, typed like the heap's
+  const int wop = base == RBG_RANGE_AND ? (buf ? RBG_WIDE_WORKSHY_AND : RBG_WIDE_AND_ITER)
+                  : base == RBG_RANGE_OR ? RBG_WIDE_OR
+                                         : RBG_WIDE_XOR;
   int hc;
   bool hv;
   CHK(ctx_wide(c, wop, sel, 0, 65536, nullptr, false, &hc, &hv));
@@ -3332,12 +3360,8 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
 // selectRangeWithoutCopy (RB/RoaringBitmap.java:3160-3214) of every bitmap of a key-major batch into a
 // new batch, on the device (runopt.hip: k_rsel_plan, two scans, k_rsel_write, the key CSR); one host
 // read-back for the new batch's container counts.  rangeSanityCheck (:204-213) first.
-static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int32_t* out_id) {
-  if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll) {
-    set_err("rangeStart=" + std::to_string(start) + " should be in [0, 0xffffffff], rangeEnd=" + std::to_string(end) +
-            " in [0, 0xffffffff + 1]");
-    return RBG_ERR_ILLEGAL_ARGUMENT;
-  }
+static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int32_t* out_id, bool buf) {
+  CHK(check_range(start, end));
   Batch* a;
   CHK(get_batch(c, id, &a));
   if (!a->key_major || a->packed) {
@@ -3346,7 +3370,7 @@ static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int3
   }
   hipStream_t s = c->stream;
   const size_t C = a->n_ctr, n = a->n_bm;
-  RselArgs ra{1, 0, 0, 0};  // end <= start: no key is kept
+  RselArgs ra{1, 0, 0, 0, buf ? 1 : 0};  // end <= start: no key is kept
   if (end > start) {
     ra.hbs = (int)(start >> 16);
     ra.lbs = (int)(start & 0xFFFF);

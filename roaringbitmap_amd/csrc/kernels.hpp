@@ -448,6 +448,7 @@ void launch_runopt_flags(hipStream_t s, const CDesc* desc, const uint32_t* bm, u
 // range's first / last key and low bits (lbs..lbl kept on those keys)
 struct RselArgs {
   int hbs, lbs, hbl, lbl;
+  int buf;  // the buffer package's cut: MappeableBitmapContainer.remove makes an array below 4096 values
 };
 void launch_rsel_plan(hipStream_t s, const CDesc* desc, const uint32_t* bm, const uint8_t* payload, uint64_t n,
                       RselArgs ra, uint32_t* info, uint32_t* card, uint64_t* size, uint64_t* keep,

@@ -393,7 +393,10 @@ __global__ __launch_bounds__(256) void k_rsel_plan(const CDesc* __restrict__ des
 #pragma unroll
       for (int k = 0; k < 16; k++) x.w[k] &= range_mask_word(k >> 1, k & 1, lo, hi);
       card = w_card(x);
-      kind = by_card(card);
+      // BitmapContainer.remove: an array at <= 4096 values (RB/BitmapContainer.java:1166-1181); the
+      // buffer package's MappeableBitmapContainer.remove below 4096 (RB/buffer/MappeableBitmapContainer.java
+      // :1597-1612), so a 4096-value bitmap stays one
+      kind = (ra.buf ? card < 4096 : card <= 4096) ? DK_A : DK_B;
       len = kind == DK_A ? 2u * card : 8192u;
     } else if (cut) {  // R
       int nr;

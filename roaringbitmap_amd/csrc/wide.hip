@@ -219,6 +219,11 @@ __global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, co
         kind = c == 65536 ? DK_R : by_card(c);
       }
     } else if (MODE == WIDE_XOR) {
+      if (n == 1) {  // one input holds the key: the chain's xor clones it, type and all (a 4096-value
+                     // bitmap of the buffer package's range selection included)
+        wg_passthrough(t, A.desc[s], A.payload, oc, &shp);
+        continue;
+      }
       // does a run container take part in this key's chain?
       int has_r = 0;
       for (uint32_t j = threadIdx.x; j < n; j += NT) has_r |= A.desc[s + j].kind == DK_R;

@@ -50,14 +50,15 @@ class _StaticOrInPlace:
         return call
 
 
-def _range_op(op, bitmaps, start, end):
+def _range_op(op, bitmaps, start, end, cls=None):
     """RB/RoaringBitmap.java range-restricted forms: every input through selectRangeWithoutCopy
-    (:3160-3214), then FastAggregation.and / or / xor(Iterator) or andNot (rbg_range_op)."""
+    (:3160-3214), then FastAggregation.and / or / xor(Iterator) or andNot (rbg_range_op); "*_buffer":
+    ImmutableRoaringBitmap's (MutableRoaringBitmap results)."""
     bufs = [b._buf for b in bitmaps]
     arr, lens = _lib.buf_array(bufs)
     b = _lib.rbg_buffer()
     check(lib().rbg_range_op(_lib.RANGE_OP[op], arr, lens, len(bufs), int(start), int(end), ctypes.byref(b)))
-    return RoaringBitmap(take(b))
+    return (cls or RoaringBitmap)(take(b))
 
 
 def _is_range(args):
@@ -704,23 +705,39 @@ class ImmutableRoaringBitmap(RoaringBitmap):
         return MutableRoaringBitmap(take(b))
 
     @staticmethod
-    def _s_and(x1, x2):
-        """and(x1, x2) :299-325"""
+    def _s_and(*args):
+        """and(x1, x2) :299-325; and(Iterator, rangeStart, rangeEnd) :261-267 (selectRangeWithoutCopy, then
+        BufferFastAggregation.and(Iterator) = workShyAnd)"""
+        if _is_range(args):
+            return _range_op("and_buffer", list(args[0]), args[1], args[2], MutableRoaringBitmap)
+        x1, x2 = args
         return ImmutableRoaringBitmap._bpair("and_buffer", x1, x2)
 
     @staticmethod
-    def _s_andnot(x1, x2):
-        """andNot(x1, x2) :441-471"""
+    def _s_andnot(*args):
+        """andNot(x1, x2) :441-471; andNot(x1, x2, rangeStart, rangeEnd) :402-408"""
+        if len(args) == 4:
+            return _range_op("andnot_buffer", [args[0], args[1]], args[2], args[3], MutableRoaringBitmap)
+        x1, x2 = args
         return ImmutableRoaringBitmap._bpair("andnot_buffer", x1, x2)
 
     @staticmethod
-    def _s_or(x1, x2):
-        """or(x1, x2) :927-977"""
-        return ImmutableRoaringBitmap._bpair("or", x1, x2)
+    def _s_or(*args):
+        """or(x1, x2) :927-977; or(Iterator, rangeStart, rangeEnd) :992-998; or(ImmutableRoaringBitmap...)
+        :911 and or(Iterator) :979 = BufferFastAggregation.or = naive_or"""
+        if _is_range(args):
+            return _range_op("or_buffer", list(args[0]), args[1], args[2], MutableRoaringBitmap)
+        if len(args) == 2 and not isinstance(args[0], Iterator):
+            return ImmutableRoaringBitmap._bpair("or", args[0], args[1])
+        bms = list(args[0]) if len(args) == 1 and isinstance(args[0], Iterator) else list(args)
+        return MutableRoaringBitmap(_wide("or", bms)._buf)
 
     @staticmethod
-    def _s_xor(x1, x2):
-        """xor(x1, x2) :1087-1134"""
+    def _s_xor(*args):
+        """xor(x1, x2) :1087-1134; xor(Iterator, rangeStart, rangeEnd) :1048-1053 (naive_xor)"""
+        if _is_range(args):
+            return _range_op("xor_buffer", list(args[0]), args[1], args[2], MutableRoaringBitmap)
+        x1, x2 = args
         return ImmutableRoaringBitmap._bpair("xor", x1, x2)
 
     @staticmethod

@@ -236,11 +236,13 @@ def time_bsi_range_sum_parallel(ebm, slices, lo, hi, threads, reps):
 
 def range_op(op, bufs, start, end) -> bytes:
     """RoaringBitmap.and / or / xor(Iterator, start, end) ("and" / "or" / "xor") and andNot(x1, x2, start,
-    end) ("andnot", two inputs): RB/RoaringBitmap.java:1308-1336, 2536-2557, 3359-3379, 1396-1423."""
+    end) ("andnot", two inputs): RB/RoaringBitmap.java:1308-1336, 2536-2557, 3359-3379, 1396-1423; "*_buf":
+    ImmutableRoaringBitmap's (RB/buffer/ImmutableRoaringBitmap.java:261, 992, 1048, 402)."""
     arr, lens = _bufs(bufs)
     p = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
-    _check(lib().rbo_range_op({"and": 0, "or": 1, "xor": 2, "andnot": 3, "select": 4}[op], arr, lens, len(bufs), start, end,
+    _check(lib().rbo_range_op({"and": 0, "or": 1, "xor": 2, "andnot": 3, "select": 4, "and_buf": 5, "or_buf": 6,
+                               "xor_buf": 7, "andnot_buf": 8, "select_buf": 9}[op], arr, lens, len(bufs), start, end,
                               ctypes.byref(p), ctypes.byref(n)))
     return _take(p, n)
 

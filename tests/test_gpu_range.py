@@ -90,3 +90,45 @@ def test_range_sanity(gpu):
         with pytest.raises(rb.IllegalArgumentException):
             rb.RoaringBitmap.or_(iter([x, x]), st, en)
     assert getattr(rb.RoaringBitmap, "and")(iter([x, x]), 2, 3).toArray().tolist() == [2]
+
+
+def _gpu_buf(op, bufs, start, end):
+    rb = _rb()
+    I = rb.ImmutableRoaringBitmap
+    bms = [I(b) for b in bufs]
+    if op == "andnot":
+        got = I.andNot(bms[0], bms[1], start, end)
+    else:
+        got = getattr(I, op)(iter(bms), start, end)
+    assert isinstance(got, rb.MutableRoaringBitmap)
+    return got.serialize()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_buffer_range_ops(gpu, seed):
+    """ImmutableRoaringBitmap's range forms (RB/buffer/ImmutableRoaringBitmap.java:261 and -> workShyAnd,
+    992 or, 1048 xor, 402 andNot with the buffer run types) against the oracle's range_aggregate_buf"""
+    rng = np.random.default_rng(700 + seed)
+    keys = np.arange(8)
+    bufs = [_gen.bitmap(rng, keys, p_present=0.85) for _ in range(4)]
+    for st, en in _ranges(rng, 8):
+        for op in ("and", "or", "xor"):
+            assert _gpu_buf(op, bufs, st, en) == O.range_op(op + "_buf", bufs, st, en), (op, st, en)
+        assert _gpu_buf("andnot", bufs[:2], st, en) == O.range_op("andnot_buf", bufs[:2], st, en), (st, en)
+    # one input, and no input at all
+    for op in ("and", "or", "xor"):
+        assert _gpu_buf(op, bufs[:1], 1000, 5 << 16) == O.range_op(op + "_buf", bufs[:1], 1000, 5 << 16)
+        assert _gpu_buf(op, [], 0, 1 << 32) == O.range_op(op + "_buf", [], 0, 1 << 32)
+
+
+def test_buffer_range_keeps_4096_value_bitmaps(gpu):
+    """MappeableBitmapContainer.remove keeps a bitmap of exactly 4096 values (RB/buffer/
+    MappeableBitmapContainer.java:1597-1612); the heap's becomes an array"""
+    x = encode([(0, B, np.arange(0, 8192)), (1, A, np.arange(5)), (2, B, np.arange(0, 65536, 2))])
+    y = encode([(3, A, [7])])
+    for st, en in ((0, 4096), (4096, 8192), (0, (2 << 16) + 8192)):
+        for op in ("or", "xor", "and"):
+            assert _gpu_buf(op, [x], st, en) == O.range_op(op + "_buf", [x], st, en), (op, st, en)
+            assert _gpu(op, [x], st, en) == O.range_op(op, [x], st, en), (op, st, en)
+        assert _gpu_buf("andnot", [x, y], st, en) == O.range_op("andnot_buf", [x, y], st, en)
+    assert O.range_op("or_buf", [x], 0, 4096) != O.range_op("or", [x], 0, 4096)

@@ -214,6 +214,11 @@ def test_pairwise_op_codes_match_header():
     for k, c in names.items():
         m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
         assert m and int(m.group(1)) == L.OP[k], k
+    for k, c in {"and_buffer": "RBG_RANGE_BUFFER_AND", "or_buffer": "RBG_RANGE_BUFFER_OR",
+                 "xor_buffer": "RBG_RANGE_BUFFER_XOR", "andnot_buffer": "RBG_RANGE_BUFFER_ANDNOT",
+                 "and": "RBG_RANGE_AND", "andnot": "RBG_RANGE_ANDNOT"}.items():  # rbg_range_op
+        m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
+        assert m and int(m.group(1)) == L.RANGE_OP[k], k
     for c in ("RBG_ORNOT_INPLACE", "RBG_ORNOT_BUFFER"):  # rbg_ornot's flags
         m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
         assert m and int(m.group(1)) == getattr(L, c), c

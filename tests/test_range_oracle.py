@@ -90,3 +90,40 @@ def test_ranged_ops_mixed_containers(seed):
         assert _set(O.range_op("and", bufs, st, en)) == inr(sets[0] & sets[1] & sets[2])
         assert _set(O.range_op("xor", bufs, st, en)) == inr(sets[0] ^ sets[1] ^ sets[2])
         assert _set(O.range_op("andnot", bufs[:2], st, en)) == inr(sets[0] - sets[1])
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_buffer_range_ops_sets(seed):
+    """ImmutableRoaringBitmap's range forms (RB/buffer/ImmutableRoaringBitmap.java:261 and -> workShyAnd,
+    992 or, 1048 xor, 402 andNot): the same sets as the heap's."""
+    rng = np.random.default_rng(90 + seed)
+    keys = np.arange(6)
+    bufs = [bitmap(rng, keys, p_present=0.8) for _ in range(3)]
+    for _ in range(8):
+        st = int(rng.integers(0, 6 << 16))
+        en = st + int(rng.integers(1, 3 << 16))
+        for op in ("and", "or", "xor"):
+            assert _set(O.range_op(op + "_buf", bufs, st, en)) == _set(O.range_op(op, bufs, st, en))
+        assert _set(O.range_op("andnot_buf", bufs[:2], st, en)) == _set(O.range_op("andnot", bufs[:2], st, en))
+
+
+def test_buffer_selection_keeps_4096_value_bitmaps():
+    """MappeableBitmapContainer.remove makes an array only below 4096 values (RB/buffer/
+    MappeableBitmapContainer.java:1597-1612): a bitmap cut to exactly 4096 values stays a bitmap -- its
+    payload the 1024 words -- where the heap's BitmapContainer.remove gives an array.  A single input's
+    container is cloned by or / xor / andNot, so the result keeps it; workShyAnd repairs it to an array."""
+    x = encode([(0, B, np.arange(0, 8192)), (1, A, np.arange(5))])
+    words = np.zeros(1024, dtype=np.uint64)
+    words[:64] = np.uint64(0xFFFFFFFFFFFFFFFF)
+    bits = words.astype("<u8").tobytes()
+    vals = np.arange(4096, dtype="<u2").tobytes()
+    heap = O.range_op("select", [x], 0, 4096)
+    buf = O.range_op("select_buf", [x], 0, 4096)
+    assert heap.endswith(vals) and buf.endswith(bits)
+    for op in ("or", "xor"):
+        assert O.range_op(op, [x], 0, 4096).endswith(vals)
+        assert O.range_op(op + "_buf", [x], 0, 4096).endswith(bits)
+    empty = O.from_values([])
+    assert O.range_op("andnot_buf", [x, empty], 0, 4096).endswith(bits)
+    assert O.range_op("and_buf", [x], 0, 4096).endswith(vals)
+    assert O.range_op("and_buf", [x, x], 0, 4096) == O.range_op("and", [x, x], 0, 4096)
