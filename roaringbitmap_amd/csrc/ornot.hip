@@ -16,7 +16,7 @@
 //                  reaches (an exact walk only when maxSize < maxKey + 1)
 //   k_plan_ornot : one thread per key (the pairwise plan's compaction): the reached keys [0, k_end)
 //                  and x1's keys above maxKey, in key order
-//   k_ornot      : one workgroup per task; the container in registers (vb.hpp), typed as the
+//   k_ornot      : one wave per task; the container in registers (wave.hpp), typed as the
 //                  reference's chain: not() -> iremove -> or / ior.  Full containers (the bulk of a
 //                  dense result) reference one constant run payload; nothing is staged for them.
 #include <algorithm>
@@ -24,7 +24,6 @@
 #include <cstdlib>
 
 #include "kernels.hpp"
-#include "vb.hpp"
 #include "wave.hpp"
 
 namespace rbg {
@@ -126,147 +125,143 @@ __global__ __launch_bounds__(256) void k_plan_ornot(const uint32_t* __restrict__
   plan_emit(f, t, wg_epoch, epoch, tasks, n_tasks, err);
 }
 
-// bits [0, e) of owned word w (device.hpp layout: thread t owns words 2t, 2t+1, 512+2t, 513+2t)
+// bits [0, e) of container word w
 __device__ __forceinline__ uint64_t prefix_mask(int w, int e) {
   const int lo = 64 * w;
   if (e >= lo + 64) return ~0ull;
   if (e <= lo) return 0ull;
   return (1ull << (e - lo)) - 1;
 }
-__device__ __forceinline__ void owned_words(int w[4]) {
-  const int t = threadIdx.x;
-  w[0] = 2 * t;
-  w[1] = 2 * t + 1;
-  w[2] = 512 + 2 * t;
-  w[3] = 513 + 2 * t;
-}
-__device__ __forceinline__ int vb_card(const uint64_t r[4], int* sh) {
-  int c = popc64(r[0]) + popc64(r[1]) + popc64(r[2]) + popc64(r[3]);
-  int u = 0;
-  block_sum2(c, u, sh);
-  return (int)uni((uint32_t)c);
+// ... of register k of the wave layout (WCtr: w[2 i + j] = word 128 i + 2 lane + j)
+__device__ __forceinline__ uint64_t wprefix(int k, int e) {
+  return prefix_mask(128 * (k >> 1) + 2 * lane_id() + (k & 1), e);
 }
 
-// v = v.not(0, e) with Container.not's result type: ArrayContainer.not (RB/ArrayContainer.java:876-925,
-// through toBitmapContainer().not above 4096 values) and BitmapContainer.not = clone().inot
-// (RB/BitmapContainer.java:994-997, 679-687) give an array at <= 4096 values, else a bitmap;
-// RunContainer.not (RB/RunContainer.java:1900-1918) ends in toEfficientContainer.
-__device__ __forceinline__ void vb_not_prefix(VB& v, int e, uint32_t* lds, int* sh) {
-  int w[4];
-  owned_words(w);
+// One task, one wave (20 waves per CU in flight: the per-task chain is a few dependent memory
+// latencies, so the task rate comes from the waves in flight).  Result types:
+//  * c2.not(0, e): ArrayContainer.not (RB/ArrayContainer.java:876-925, through toBitmapContainer().not
+//    above 4096 values) and BitmapContainer.not = clone().inot (RB/BitmapContainer.java:994-997, 679-687)
+//    give an array at <= 4096 values, else a bitmap; RunContainer.not (RB/RunContainer.java:1900-1918)
+//    ends in toEfficientContainer;
+//  * .iremove(e, 0x10000) (both present, e < 65536): an array stays an array, a bitmap becomes one at
+//    <= 4096 values (RB/BitmapContainer.java:788-802), a run container stays one; BUF: the buffer
+//    package's MappeableBitmapContainer.iremove converts only below 4096 values
+//    (RB/buffer/MappeableBitmapContainer.java:1003-1017), so a 4096-value bitmap keeps its words;
+//  * rangeOfOnes(0, e) (RB/Container.java:29-37): an array up to 2 values, else a run container;
+//  * c1.or / c1.ior of that: the pairwise OR rule (device.hpp); Container.ior's one difference,
+//    BitmapContainer.ior(ArrayContainer) keeping a full bitmap (RB/BitmapContainer.java:740-757),
+//    applies to x1-only at maxKey in both forms and to both-present in the in-place form.
+template <bool INPLACE, bool BUF>
+__device__ __forceinline__ void ornot_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
+                                           int max_key, int last_run, const OutCtx& oc, uint32_t* lds) {
+  const int key = tk.key;
+  const bool ia = tk.kind_a != kAbsent, ib = tk.kind_b != kAbsent;
+  if (key > max_key) {  // x1's containers above the range, appended as they are (:1493-1500 / :1588-1596)
+    const uint32_t len = tk.kind_a == DK_A ? 2u * tk.card_a : tk.kind_a == DK_B ? 8192u : 2u + 4u * tk.nruns_a;
+    w_place(t, true, pa + tk.slot_a + (tk.kind_a == DK_R ? 2 : 0), false, lds, len, tk.card_a, (uint32_t)key,
+            tk.kind_a, oc);
+    return;
+  }
+  const int e = key == max_key ? last_run : 65536;
+  if (!ib && e == 65536) {
+    // RunContainer.full(); at maxKey with lastRun = 0x10000, x1's c1.ior(full run) and the full
+    // rangeOfOnes are full run containers as well (RunContainer.or / BitmapContainer.ior(RunContainer) /
+    // RunContainer.ior return full() on a full union)
+    w_place(t, true, reinterpret_cast<const uint8_t*>(g_full_run), false, lds, 6, 65536, (uint32_t)key, DK_R, oc);
+    return;
+  }
+  if (!ia && !ib) {  // rangeOfOnes(0, lastRun) at maxKey, written by lane 0
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+    const bool arr = e <= 2;
+    uint16_t* p = reinterpret_cast<uint16_t*>(arr ? slot : slot + 2);
+    if (lane_id() == 0) {
+      if (arr) {
+        p[0] = 0;
+        p[1] = 1;
+      } else {
+        p[0] = 1;
+        p[1] = 0;
+        p[2] = (uint16_t)(e - 1);
+      }
+    }
+    w_place(t, true, reinterpret_cast<const uint8_t*>(p), false, lds, arr ? 2u * e : 6u, (uint32_t)e, (uint32_t)key,
+            arr ? DK_A : DK_R, oc);
+    return;
+  }
+  WCtr x, y;
+  const int kx = ia ? tk.kind_a : DK_A, cx = ia ? (int)tk.card_a : 0;
+  if (ia) w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0}, pa, lds, x);
+  int ky, cy;
+  if (ib) {
+    w_materialize(CDesc{tk.slot_b, tk.card_b, tk.key, tk.kind_b, 0}, pb, lds, y);
 #pragma unroll
-  for (int i = 0; i < 4; i++) v.r[i] ^= prefix_mask(w[i], e);
-  const int c = vb_card(v.r, sh);
-  v.kind = v.kind == DK_R ? eff(c, count_runs(v.r, lds, sh)) : by_card(c);
-  v.card = c;
-  v.present = 1;
-  v.src = -1;
-}
-// v.iremove(e, 0x10000): ArrayContainer.iremove stays an array, BitmapContainer.iremove becomes one at
-// <= 4096 values, RunContainer.iremove stays a run container (RB/ArrayContainer.java:759-780,
-// RB/BitmapContainer.java:788-802, RB/RunContainer.java:1553-...).  BUF: MappeableBitmapContainer.iremove
-// becomes an array only below 4096 values (RB/buffer/MappeableBitmapContainer.java:1003-1017); a bitmap of
-// exactly 4096 values keeps its words as payload.
-template <bool BUF>
-__device__ __forceinline__ void vb_clip(VB& v, int e, int* sh) {
-  int w[4];
-  owned_words(w);
+    for (int k = 0; k < 16; k++) y.w[k] ^= wprefix(k, e);
+    cy = w_card(y);
+    ky = tk.kind_b == DK_R ? eff(cy, w_runs(y)) : by_card(cy);
+    if (ia && e < 65536) {
 #pragma unroll
-  for (int i = 0; i < 4; i++) v.r[i] &= prefix_mask(w[i], e);
-  const int c = vb_card(v.r, sh);
-  if (v.kind == DK_B && (BUF ? c < 4096 : c <= 4096)) v.kind = DK_A;
-  v.card = c;
-}
-// Container.rangeOfOnes(0, e) (RB/Container.java:29-37): an array up to 2 values, else a run container
-__device__ __forceinline__ void vb_range_ones(VB& v, int e) {
-  int w[4];
-  owned_words(w);
+      for (int k = 0; k < 16; k++) y.w[k] &= wprefix(k, e);
+      cy = w_card(y);
+      if (ky == DK_B && (BUF ? cy < 4096 : cy <= 4096)) ky = DK_A;
+    }
+  } else {  // x1 only, maxKey: c1.ior(rangeOfOnes(0, e))
 #pragma unroll
-  for (int i = 0; i < 4; i++) v.r[i] = prefix_mask(w[i], e);
-  v.kind = e <= 2 ? DK_A : DK_R;
-  v.card = e;
-  v.present = 1;
-  v.src = -1;
+    for (int k = 0; k < 16; k++) y.w[k] = wprefix(k, e);
+    cy = e;
+    ky = e <= 2 ? DK_A : DK_R;
+  }
+  int kz, cz;
+  if (ia) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) x.w[k] |= y.w[k];
+    cz = w_card(x);
+    kz = pairwise_needs_runs(OPR_OR, kx, cx, ky, cy) ? eff(cz, w_runs(x)) : pairwise_kind(OPR_OR, kx, ky, cz);
+    if ((INPLACE || !ib) && kx == DK_B && ky == DK_A) kz = DK_B;
+  } else {  // x2 only: its complement, dropped when empty
+    if (cy == 0) {
+      w_place(t, false, nullptr, true, lds, 0, 0, (uint32_t)key, DK_A, oc);
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; k++) x.w[k] = y.w[k];
+    cz = cy;
+    kz = ky;
+  }
+  if (kz == DK_B) {  // registers straight to the task's slot
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+    w_store_bitmap(slot, x);
+    w_place(t, true, slot, false, lds, 8192, (uint32_t)cz, (uint32_t)key, DK_B, oc);
+    return;
+  }
+  const uint32_t len = w_stage(kz, x, cz, lds);
+  w_place(t, true, nullptr, true, lds, len, (uint32_t)cz, (uint32_t)key, kz, oc);
 }
+
+constexpr int kOrnWaves = 4;
 
 // INPLACE: x1.orNot (iorNot, ior); BUF: the buffer package's ImmutableRoaringBitmap.orNot /
 // MutableRoaringBitmap.orNot (RB/buffer/ImmutableRoaringBitmap.java:484-548, MutableRoaringBitmap.java
-// :962-1030), whose containers type like the heap's but for vb_clip
+// :962-1030).  Static wave stride over the task list; the next record is fetched while a task runs.
 template <bool INPLACE, bool BUF>
 __global__ __launch_bounds__(256) void k_ornot(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                                const uint8_t* pa, const uint8_t* pb, int max_key, int last_run,
                                                OutCtx oc) {
-  __shared__ __align__(16) uint32_t acc[2048];
-  __shared__ __align__(16) uint32_t tmp[2048];
-  __shared__ int q[257];
-  __shared__ int sh[8];
-  const uint32_t nt = *n_tasks;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    const PTask tk = tasks[t];
-    const int key = tk.key;
-    const bool ia = tk.kind_a != kAbsent, ib = tk.kind_b != kAbsent;
-    if (key > max_key) {  // x1's containers above the range, appended as they are (:1493-1500 / :1588-1596)
-      wg_passthrough(t, CDesc{tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0}, pa, oc, nullptr);
-      continue;
-    }
-    const int e = key == max_key ? last_run : 65536;
-    if (!ib && e == 65536) {
-      // RunContainer.full(); at maxKey with lastRun = 0x10000, x1's c1.ior(full run) and the full
-      // rangeOfOnes are full run containers as well (RunContainer.or / BitmapContainer.ior(RunContainer)
-      // / RunContainer.ior return full() on a full union)
-      wg_place(t, true, reinterpret_cast<const uint8_t*>(g_full_run), false, nullptr, 6, 65536, key, DK_R, oc,
-               nullptr);
-      continue;
-    }
-    if (!ia && !ib) {  // rangeOfOnes(0, lastRun) at maxKey, written by one thread
-      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
-      const bool arr = e <= 2;
-      uint16_t* p = reinterpret_cast<uint16_t*>(arr ? slot : slot + 2);
-      if (threadIdx.x == 0) {
-        if (arr) {
-          p[0] = 0;
-          p[1] = 1;
-        } else {
-          p[0] = 1;
-          p[1] = 0;
-          p[2] = (uint16_t)(e - 1);
-        }
-      }
-      wg_place(t, true, reinterpret_cast<const uint8_t*>(p), false, nullptr, arr ? 2u * e : 6u, (uint32_t)e, key,
-               arr ? DK_A : DK_R, oc, nullptr);
-      continue;
-    }
-    VB x, y, z;
-    pb_load(tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0, pa, tmp, q, x);
-    if (ib) {
-      pb_load(tk.slot_b, tk.card_b, tk.key, tk.kind_b, 1, pb, tmp, q, y);
-      vb_not_prefix(y, e, acc, sh);
-      if (ia && e < 65536) vb_clip<BUF>(y, e, sh);
-    } else {
-      vb_range_ones(y, e);
-    }
-    if (ia) {
-      vb_op<OPR_OR>(x, y, z, acc, sh);
-      // Container.ior: BitmapContainer.ior(ArrayContainer) keeps a full bitmap (RB/BitmapContainer.java
-      // :740-757); every other pair types like or.  ior for x1-only at maxKey in both forms, for the
-      // orNot of both in the in-place form
-      if ((INPLACE || !ib) && x.kind == DK_B && y.kind == DK_A) z.kind = DK_B;
-    } else {
-      z = y;
-      if (z.card == 0) z.present = 0;
-    }
-    if (!z.present) {
-      wg_place(t, false, nullptr, true, tmp, 0, 0, key, DK_A, oc, nullptr);
-      continue;
-    }
-    if (z.kind == DK_B) {  // registers straight to the task's slot (no LDS staging)
-      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
-      store_bitmap_owned(slot, z.r);
-      wg_place(t, true, slot, false, nullptr, 8192, (uint32_t)z.card, key, DK_B, oc, nullptr);
-      continue;
-    }
-    const uint32_t len = stage_container(z.kind, z.r, z.card, acc, tmp, sh);
-    wg_place(t, true, nullptr, true, tmp, len, (uint32_t)z.card, key, z.kind, oc, nullptr);
+  __shared__ __align__(16) uint32_t lds_all[kOrnWaves][2048];
+  const int w = threadIdx.x >> 6;
+  uint32_t* lds = lds_all[w];
+  const uint32_t nt = uni(*n_tasks);
+  const uint32_t stride = gridDim.x * kOrnWaves;
+  uint32_t t = uni(blockIdx.x * kOrnWaves + w);
+  if (t >= nt) return;
+  PTask cur = load_task(tasks, t);
+  for (;;) {
+    const uint32_t tn = t + stride;
+    PTask nxt;
+    if (tn < nt) nxt = load_task(tasks, tn);  // in flight while this task runs
+    ornot_task<INPLACE, BUF>(t, cur, pa, pb, max_key, last_run, oc, lds);
+    if (tn >= nt) break;
+    t = tn;
+    cur = nxt;
   }
 }
 
@@ -277,7 +272,7 @@ void launch_ornot(hipStream_t s, const uint32_t* koa, const CDesc* da, const uin
   hipLaunchKernelGGL(k_ornot_scan, dim3(1), dim3(1024), 0, s, koa, na, kob, db, nb, max_key, plan);
   hipLaunchKernelGGL(k_plan_ornot, dim3(256), dim3(256), 0, s, koa, da, pa, kob, db, pb, max_key, plan, wg_epoch,
                      epoch, tasks, n_tasks, zlb, ztile, oc.err);
-  const int g0 = std::max(1, grid);
+  const int g0 = std::max(1, (grid + kOrnWaves - 1) / kOrnWaves);
 #define RBG_ORNOT_LAUNCH(I, B)                                                                            \
   hipLaunchKernelGGL((k_ornot<I, B>), dim3(std::min(g0, resident_grid((const void*)&k_ornot<I, B>))), dim3(256), 0, \
                      s, tasks, n_tasks, pa, pb, max_key, last_run, oc)

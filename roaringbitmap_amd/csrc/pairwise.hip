@@ -560,17 +560,6 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
 }
 
 // 32 B task record through the scalar cache (wave-uniform address)
-__device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
-  typedef const __attribute__((address_space(4))) uint64_t* CU64;
-  const CU64 q = reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(tasks + t));
-  union {
-    uint64_t u[4];
-    PTask p;
-  } r;
-#pragma unroll
-  for (int i = 0; i < 4; i++) r.u[i] = q[i];
-  return r.p;
-}
 
 // ---------------------------------------------------------------------------
 // Direct mode: the compute kernel resolves its tasks itself (no plan launch).  Task t is key

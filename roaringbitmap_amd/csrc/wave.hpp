@@ -471,6 +471,19 @@ __device__ __forceinline__ void resolve(const uint32_t* key_off, const CDesc* de
   }
 }
 
+// a task record through the scalar cache (wave-uniform; loads only)
+__device__ __forceinline__ PTask load_task(const PTask* tasks, uint32_t t) {
+  typedef const __attribute__((address_space(4))) uint64_t* CU64;
+  const CU64 q = reinterpret_cast<CU64>(reinterpret_cast<uintptr_t>(tasks + t));
+  union {
+    uint64_t u[4];
+    PTask p;
+  } r;
+#pragma unroll
+  for (int i = 0; i < 4; i++) r.u[i] = q[i];
+  return r.p;
+}
+
 // Plan compaction (one thread per key, 256 workgroups of 256 keys, all resident): each workgroup
 // publishes its task count tagged with the op's epoch, sums the counts of the workgroups before it
 // (one per thread, waiting for the epoch), and writes its flagged tasks straight into the dense task

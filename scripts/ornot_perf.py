@@ -20,11 +20,18 @@ import roaringbitmap_amd as rb  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-inplace = len(sys.argv) > 3 and sys.argv[3] == "inplace"
+mode = sys.argv[3] if len(sys.argv) > 3 else "mixed"
+inplace = mode == "inplace"
 rng = np.random.default_rng(5)
 keys = np.arange(n)
-a = _gen.bitmap(rng, keys, p_present=0.7)
-b = _gen.bitmap(rng, keys, p_present=0.7)
+if mode == "empty":  # every key x2-free and x1-free: full run containers only (the trivial-task floor)
+    a = b = O.from_values(np.zeros(0, dtype=np.uint32))
+elif mode == "bitmaps":  # every key a bitmap in both operands
+    a = _gen.bitmap(rng, keys, modes=["b_mid"], p_present=1.0)
+    b = _gen.bitmap(rng, keys, modes=["b_mid"], p_present=1.0)
+else:
+    a = _gen.bitmap(rng, keys, p_present=0.7)
+    b = _gen.bitmap(rng, keys, p_present=0.7)
 end = n << 16
 eng = rb.Engine()
 ia, ib = eng.load_pair(a, b)
@@ -39,4 +46,4 @@ for _ in range(reps):
     eng.serialize()
 eng.sync()
 dt = (time.perf_counter() - t0) / reps
-print(f"keys={n} in_bytes={len(a) + len(b)} out_bytes={len(got)} inplace={inplace} host_ms_per_op={dt * 1e3:.3f}")
+print(f"mode={mode} keys={n} in_bytes={len(a) + len(b)} out_bytes={len(got)} inplace={inplace} host_ms_per_op={dt * 1e3:.3f}")
