@@ -405,6 +405,40 @@ def run_optimize_c2(eng, a, sa, steps):
             "types_after": [so["array"], so["bitmap"], so["run"]]}
 
 
+def ornot_c2(eng, a, b, sa, sb, steps):
+    """RoaringBitmap.orNot(x1, x2, 2^32) on the C2 pair (every key holds both operands: c1.or(c2.not(0,
+    65536)) per key) + the device serialization, as the headline step; the orNot launches' own device time
+    from the engine's phase events (k_ornot_scan + k_plan_ornot + k_ornot)."""
+    end = 1 << 32
+    eng.ornot(a, b, end)
+    rs = eng.result_stats()
+    for _ in range(2):
+        eng.ornot(a, b, end)
+        eng.serialize()
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.ornot(a, b, end)
+        eng.serialize()
+    eng.sync()
+    dt = (time.perf_counter() - t0) / steps
+    eng.profile(steps)
+    for _ in range(steps):
+        eng.ornot(a, b, end)
+    n, ph = eng.profile_read()
+    eng.profile(0)
+    k_ms = ph[1] / max(n, 1)
+    in_b = sa["payload_bytes"] + sb["payload_bytes"] + 4 * (sa["containers"] + sb["containers"])
+    out_b = rs["payload_bytes"] + 4 * rs["containers"]
+    return {"workload": "RoaringBitmap.orNot(x1, x2, 2^32) on the C2 pair + serialize (device-resident)",
+            "ms_per_step": round(dt * 1e3, 4), "input_GBps": round(in_b / dt / 1e9, 1),
+            "result_containers": rs["containers"], "result_payload_bytes": rs["payload_bytes"],
+            "roofline": {"kernel": "k_ornot_scan + k_plan_ornot + k_ornot", "kernel_ms": round(k_ms, 4),
+                         "bytes": int(in_b + out_b),
+                         "achieved_GBps": round((in_b + out_b) / (k_ms / 1e3) / 1e9, 1) if k_ms > 0 else None,
+                         "frac": round((in_b + out_b) / (k_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4) if k_ms > 0 else None}}
+
+
 def c5_bsi(eng, rows, rank, world, dist, steps, warmup, cdev):
     """C5: RoaringBitmapSliceIndex.compare(RANGE) + sum over `rows` rows (31 slices),
     rows sharded by key range across the ranks (strong scaling); one step = the fused
@@ -640,7 +674,7 @@ def main():
     ap.add_argument("--c3-n", type=int, default=10000, help="bitmaps of the C3 wide-OR workloads (0 = skip)")
     ap.add_argument("--c4-pairs", type=int, default=1000000, help="pairs of the C4 workload per GPU (0 = skip)")
     ap.add_argument("--c5-rows", type=int, default=1000000000, help="rows of the C5 BSI workload (0 = skip)")
-    ap.add_argument("--only", default="", help="profiling: run one workload alone (c2, c2card, c3u, c3c, c3u_and, c3c_and, c4, c5, runopt)")
+    ap.add_argument("--only", default="", help="profiling: run one workload alone (c2, c2card, c3u, c3c, c3u_and, c3c_and, c4, c5, runopt, ornot)")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL; gloo to rehearse "
                                                        "several ranks on one GPU)")
     args = ap.parse_args()
@@ -846,6 +880,8 @@ def main():
 
     if args.c3_n > 0 or args.c4_pairs > 0 or args.c5_rows > 0:
         run_extra("run_optimize_c2", lambda: run_optimize_c2(eng, a, sa, ks))
+        if not strong:
+            run_extra("ornot_c2", lambda: ornot_c2(eng, a, b, sa, sb, ks))
         run_extra("decode_c2", lambda: decode_c2(eng, a, ks))
         if rank == 0:
             run_extra("c2_and_oneshot", lambda: c2_oneshot(eng, a, b, max(3, ks // 2)))
@@ -935,6 +971,10 @@ def _only(eng, args, rank, world, dist, cdev):
     elif w == "runopt":
         a = eng.synth(0, 0xC2A0 + 0x10000 * rank)
         res = {"only": w, **run_optimize_c2(eng, a, eng.batch_stats(a), steps)}
+    elif w == "ornot":
+        a = eng.synth(0, 0xC2A0 + 0x10000 * rank)
+        b = eng.synth(0, 0xC2B0 + 0x10000 * rank)
+        res = {"only": w, **ornot_c2(eng, a, b, eng.batch_stats(a), eng.batch_stats(b), steps)}
     else:
         raise SystemExit(f"unknown workload {w}")
     if rank == 0:

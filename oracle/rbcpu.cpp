@@ -1579,15 +1579,71 @@ Ctr c_not_prefix(const Ctr& c, int end) {
   return to_efficient(ans.build());
 }
 
-// Container.rangeOfOnes(0, last) (RB/Container.java:29-37): an array up to 2 values, else a run
-static Ctr range_of_ones(int last) {
-  if (last <= 2) {
-    std::vector<uint16_t> v;
-    for (int x = 0; x < last; x++) v.push_back((uint16_t)x);
+// Container.not(start, end) for any range (the static RoaringBitmap.flip's per-key step): as
+// c_not_prefix, with the values below `start` kept -- ArrayContainer.not copies them, RunContainer.not
+// copies the runs that start below `start` and XOR-appends the range and the rest (RB/RunContainer.java
+// :1900-1918)
+static Ctr c_not_range(const Ctr& c, int start, int end) {
+  if (end <= start) return c;
+  if (c.kind == ARRAY) {
+    const int i0 = (int)(std::lower_bound(c.vals.begin(), c.vals.end(), start) - c.vals.begin());
+    const int i1 = (int)(std::lower_bound(c.vals.begin(), c.vals.end(), end) - c.vals.begin());
+    const int m = i1 - i0;
+    const int newcard = c.card - m + (end - start - m);
+    if (newcard > kArrayMax) return c_not_range(to_bitmap(c), start, end);
+    std::vector<uint16_t> v(c.vals.begin(), c.vals.begin() + i0);
+    int i = i0;
+    for (int x = start; x < end; x++) {
+      if (i < i1 && (int)c.vals[i] == x) i++;
+      else v.push_back((uint16_t)x);
+    }
+    v.insert(v.end(), c.vals.begin() + i1, c.vals.end());
     return make_array(std::move(v));
   }
-  return make_run({0, (uint16_t)(last - 1)}, 1);
+  if (c.kind == BITMAP) {
+    Ctr b = c;
+    const int prev = card_in_range(b.words, start, end);
+    flip_range(b.words, start, end);
+    b.card += (end - start - prev) - prev;
+    if (b.card <= kArrayMax) return bitmap_to_array(b);
+    return b;
+  }
+  RunBuf ans(c.nruns() + 1);
+  int k = 0;
+  for (; k < c.nruns() && (int)c.vals[2 * k] < start; k++) ans.push(c.vals[2 * k], c.vals[2 * k + 1]);
+  ans.smart_append_excl(start, end - start - 1);
+  for (; k < c.nruns(); k++) ans.smart_append_excl(c.vals[2 * k], c.vals[2 * k + 1]);
+  return to_efficient(ans.build());
 }
+
+// Container.add(begin, end): ArrayContainer.add (RB/ArrayContainer.java:103-135) an array, or above 4096
+// values toBitmapContainer().iadd, a bitmap; BitmapContainer.add (RB/BitmapContainer.java:131-143) a
+// bitmap, a full one included; RunContainer.add = clone().iadd (RB/RunContainer.java:242-245, 1068-...)
+// a run container whatever its size (its runs merged with the range, adjacent ones joined)
+static Ctr c_add_range(const Ctr& c, int begin, int end) {
+  if (end == begin) return c;
+  Ctr b = to_bitmap(c);
+  set_range(b.words, begin, end);
+  compute_card_inplace(b);
+  if (c.kind == BITMAP) return b;
+  if (c.kind == ARRAY) return b.card > kArrayMax ? b : bitmap_to_array(b);
+  std::vector<uint16_t> v;
+  v.reserve(b.card);
+  for (int w = 0; w < kWords; w++)
+    for (uint64_t x = b.words[w]; x; x &= x - 1) v.push_back((uint16_t)(64 * w + __builtin_ctzll(x)));
+  return runs_from_values(v);
+}
+
+// Container.rangeOfOnes(0, last) (RB/Container.java:29-37): an array up to 2 values, else a run
+static Ctr range_of_ones_at(int start, int last) {
+  if (last - start <= 2) {
+    std::vector<uint16_t> v;
+    for (int x = start; x < last; x++) v.push_back((uint16_t)x);
+    return make_array(std::move(v));
+  }
+  return make_run({(uint16_t)start, (uint16_t)(last - start - 1)}, 1);
+}
+static Ctr range_of_ones(int last) { return range_of_ones_at(0, last); }
 
 // Container.orNot / iorNot (RB/Container.java:191-196, 536-541): or / ior with
 // x.not(0, end).iremove(end, 0x10000) (end < 0x10000) or x.not(0, 0x10000).  buf: the buffer package's
@@ -1663,6 +1719,48 @@ Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inp
     ans.keys.push_back(x1.keys[i]);
     ans.ctrs.push_back(x1.ctrs[i]);
   }
+  return ans;
+}
+
+// The static range mutations, RB/RoaringBitmap.java: add(rb, rangeStart, rangeEnd) :298-345 (first / last
+// key through Container.add, the keys between replaced by full run containers, a missing key by
+// rangeOfOnes), remove(rb, ...) :995-1040 (first / last key through Container.remove unless the cut
+// covers the whole key, the keys between dropped, emptied containers dropped), flip(rb, ...) :626-668
+// (every key of the range through Container.not, a missing key rangeOfOnes, emptied containers dropped);
+// the keys outside the range cloned.  buf: MutableRoaringBitmap's (RB/buffer/MutableRoaringBitmap.java
+// :152-205, 455-505, 649-700), whose MappeableBitmapContainer.remove keeps a 4096-value bitmap.
+// op 0 add, 1 remove, 2 flip.  rangeEnd <= rangeStart: a clone.
+Bitmap op_range_mut(int op, const Bitmap& b, uint64_t start, uint64_t end, bool buf) {
+  if (end <= start) return b;
+  const int hbs = (int)(start >> 16), lbs = (int)(start & 0xFFFF);
+  const int hbl = (int)((end - 1) >> 16), lbl = (int)((end - 1) & 0xFFFF);
+  Bitmap ans;
+  auto put = [&](int k, Ctr c) {
+    if (!c.empty()) {
+      ans.keys.push_back((uint16_t)k);
+      ans.ctrs.push_back(std::move(c));
+    }
+  };
+  const Ctr* cur = nullptr;
+  size_t i = 0;
+  for (; i < b.size() && (int)b.keys[i] < hbs; i++) put(b.keys[i], b.ctrs[i]);
+  for (int k = hbs; k <= hbl; k++) {
+    cur = (i < b.size() && (int)b.keys[i] == k) ? &b.ctrs[i] : nullptr;
+    if (cur) i++;
+    const int lo = k == hbs ? lbs : 0, hi = k == hbl ? lbl : 65535;
+    if (op == 0) {
+      if (k != hbs && k != hbl) put(k, run_full());  // rangeOfOnes(0, 65536)
+      else put(k, cur ? c_add_range(*cur, lo, hi + 1) : range_of_ones_at(lo, hi + 1));
+    } else if (op == 1) {
+      if (!cur) continue;
+      if (hbs == hbl) put(k, c_remove_range(*cur, lo, hi + 1, buf));
+      else if (k == hbs && lbs != 0) put(k, c_remove_range(*cur, lbs, 65536, buf));
+      else if (k == hbl && lbl != 65535) put(k, c_remove_range(*cur, 0, lbl + 1, buf));
+    } else {
+      put(k, cur ? c_not_range(*cur, lo, hi + 1) : range_of_ones_at(lo, hi + 1));
+    }
+  }
+  for (; i < b.size(); i++) put(b.keys[i], b.ctrs[i]);
   return ans;
 }
 

@@ -147,6 +147,9 @@ Bitmap range_aggregate_buf(int op, const std::vector<const Bitmap*>& bms, uint64
 // MutableRoaringBitmap.java:962-1030), the same loop with the buffer package's container types.
 Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inplace, bool* neg, bool buf = false);
 Ctr c_not_prefix(const Ctr& c, int end);  // Container.not(0, end)
+// static add / remove / flip(rb, rangeStart, rangeEnd): op 0 / 1 / 2 (RB/RoaringBitmap.java:298, 995, 626);
+// buf: MutableRoaringBitmap's (RB/buffer/MutableRoaringBitmap.java:152, 649, 455)
+Bitmap op_range_mut(int op, const Bitmap& b, uint64_t start, uint64_t end, bool buf = false);
 Bitmap fa_horizontal_or(const std::vector<const Bitmap*>& bms);      // FastAggregation.horizontal_or :124-231
 Bitmap fa_horizontal_xor(const std::vector<const Bitmap*>& bms);     // :243-289
 Bitmap fa_priorityqueue_or(const std::vector<const Bitmap*>& bms);   // :733-781

@@ -76,6 +76,8 @@ def lib():
         L.rbo_ornot.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64,
                                 ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(u8p),
                                 ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_range_mut.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -263,6 +265,16 @@ def ornot(a, b, range_end, inplace=False, buffer=False) -> bytes:
     if neg.value:
         raise NegativeArraySize(st)
     _check(st)
+    return _take(p, n)
+
+
+def range_mut(op, buf, start, end, buffer=False) -> bytes:
+    """static RoaringBitmap.add / remove / flip(rb, start, end) ("add" / "remove" / "flip",
+    RB/RoaringBitmap.java:298, 995, 626); buffer: MutableRoaringBitmap's."""
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    code = {"add": 0, "remove": 1, "flip": 2}[op] | (4 if buffer else 0)
+    _check(lib().rbo_range_mut(code, buf, len(buf), start, end, ctypes.byref(p), ctypes.byref(n)))
     return _take(p, n)
 
 
