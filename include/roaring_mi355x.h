@@ -142,6 +142,18 @@ int rbg_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t 
 enum { RBG_ORNOT_INPLACE = 1, RBG_ORNOT_BUFFER = 2 };
 int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int64_t range_end, int flags,
               rbg_buffer* out);
+/* static range mutations of one bitmap: RBG_RMUT_ADD = RoaringBitmap.add(rb, rangeStart, rangeEnd)
+ * (RB/RoaringBitmap.java:298-345: Container.add on the first / last key, full run containers between,
+ * rangeOfOnes where a key is missing), RBG_RMUT_REMOVE = remove(rb, ...) (:995-1040: Container.remove on
+ * the first / last key unless the cut covers the whole key, the keys between dropped), RBG_RMUT_FLIP =
+ * flip(rb, ...) (:626-668: Container.not on every key of the range, rangeOfOnes where a key is missing);
+ * empty containers dropped, keys outside the range cloned.  | RBG_RMUT_BUFFER: MutableRoaringBitmap's
+ * (RB/buffer/MutableRoaringBitmap.java:152-205, 649-700, 455-505; ImmutableRoaringBitmap.flip :592),
+ * whose MappeableBitmapContainer.remove keeps a 4096-value bitmap.  rangeSanityCheck (:204-213) ->
+ * RBG_ERR_ILLEGAL_ARGUMENT; rangeEnd <= rangeStart: the input's bytes.  Synchronises the stream (a run
+ * result above 2047 runs, from an input run container that large, is checked for in the run arena). */
+enum { RBG_RMUT_ADD = 0, RBG_RMUT_REMOVE = 1, RBG_RMUT_FLIP = 2, RBG_RMUT_BUFFER = 4 };
+int rbg_range_mut(int op, const uint8_t* a, size_t a_len, int64_t range_start, int64_t range_end, rbg_buffer* out);
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
 
@@ -320,6 +332,8 @@ int rbg_ctx_pairwise_serialized(rbg_ctx* ctx, int op, int32_t a, size_t ia, int3
 int rbg_ctx_pairwise_range(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib, int key_lo, int key_hi);
 /* rbg_ornot over device-resident single-bitmap batches; the result pending like rbg_ctx_pairwise's */
 int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int64_t range_end, int flags);
+/* rbg_range_mut over a device-resident single-bitmap batch; the result pending like rbg_ctx_pairwise's */
+int rbg_ctx_range_mut(rbg_ctx* ctx, int op, int32_t batch, size_t i, int64_t range_start, int64_t range_end);
 /* Enqueue a cardinality op; the int32 lands in device memory, read by rbg_ctx_card. */
 int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
 /* Enqueue a wide op over every bitmap of a batch, restricted to keys [key_lo, key_hi)

@@ -998,6 +998,62 @@ static int ctx_ornot(Ctx* c, int32_t ia, size_t ma, int32_t ib, size_t mb, int64
   return RBG_OK;
 }
 
+// static add / remove / flip(rb, rangeStart, rangeEnd) (RB/RoaringBitmap.java:298-345, 995-1040, 626-668;
+// buf: MutableRoaringBitmap's, RB/buffer/MutableRoaringBitmap.java:152-205, 649-700, 455-505), rangemut.hip.
+// rangeSanityCheck (:204-213); rangeEnd <= rangeStart gives a clone.  A run result above 2047 runs goes
+// to the big-run arena; the arena is checked after the op and the op rerun once with the size the first
+// pass reserved (as ctx_pairwise_buffer).
+static int ctx_range_mut(Ctx* c, int op, int32_t ia, size_t ma, int64_t start, int64_t end, bool buf) {
+  if (op < RMUT_ADD || op > RMUT_FLIP) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll) {
+    set_err("rangeStart=" + std::to_string(start) + " should be in [0, 0xffffffff], rangeEnd=" + std::to_string(end) +
+            " in [0, 0xffffffff + 1]");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  Batch* A;
+  CHK(get_batch(c, ia, &A));
+  const uint16_t* ka;
+  const CDesc* da;
+  int na;
+  CHK(operand(A, ma, &ka, &da, &na));
+  RmutArgs ra{op, 1, 0, 0, 0};  // end <= start: no key in the range, every container cloned
+  if (end > start) {
+    ra.hbs = (int)(start >> 16);
+    ra.lbs = (int)(start & 0xFFFF);
+    ra.hbl = (int)((end - 1) >> 16);
+    ra.lbl = (int)((end - 1) & 0xFFFF);
+  }
+  const size_t in_range = end > start ? (size_t)(ra.hbl - ra.hbs + 1) : 0;
+  const size_t ub = std::max<size_t>(1, std::min<size_t>(kMaxKeys, (size_t)na + in_range));
+  hipStream_t s = c->stream;
+  if (!c->big_ctl.p) CHK(c->big_ctl.ensure(16));
+  if (!c->big.p) CHK(c->big.ensure(16ull << 20));
+  for (int attempt = 0;; attempt++) {
+    OutCtx oc;
+    CHK(prepare_output(c, ub, A->payload_bytes + (size_t)8194 * ub + c->big.cap, &oc, false));
+    c->pending_src = {ia};
+    c->mark(0);
+    HIPCHK(hipMemsetAsync(c->big_ctl.p, 0, 16, s));
+    c->mark(1);
+    launch_rmut(s, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), ra, buf, c->wg_epoch.as<uint64_t>(),
+                next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->zlb, c->ztile,
+                BigRuns{c->big.as<uint8_t>(), c->big_ctl.as<unsigned long long>(), c->big.cap}, grid_for(ub, 65536));
+    c->mark(2);
+    defer_place(c);
+    c->mark(3);
+    HIPCHK(hipGetLastError());
+    unsigned long long used[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(used, c->big_ctl.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (!used[1]) return RBG_OK;
+    if (attempt) {
+      set_err("range add / remove: the run-container arena overflowed twice");
+      return RBG_ERR_DEVICE;
+    }
+    CHK(c->big.ensure(used[0] + (used[0] >> 3) + 4096));
+  }
+}
+
 static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only, int key_lo = 0,
                         int key_hi = kMaxKeys, int pipe_k = 0) {
   if (op == RBG_AND_BUFFER || op == RBG_ANDNOT_BUFFER) {
@@ -2199,6 +2255,26 @@ int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int6
   if (!ctx || flags < 0 || flags > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
   CHK(enter(&ctx->c));
   return ctx_ornot(&ctx->c, a, ia, b, ib, range_end, flags);
+}
+
+int rbg_range_mut(int op, const uint8_t* a, size_t a_len, int64_t range_start, int64_t range_end, rbg_buffer* out) {
+  if (!out || op < 0 || op > (RBG_RMUT_FLIP | RBG_RMUT_BUFFER) || (op & 3) > RBG_RMUT_FLIP)
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(ctx_load_separate(c, &a, &a_len, 1, &id));
+  g.ids = {id};
+  CHK(ctx_range_mut(c, op & 3, id, 0, range_start, range_end, (op & RBG_RMUT_BUFFER) != 0));
+  return ctx_fetch(c, out);
+}
+
+int rbg_ctx_range_mut(rbg_ctx* ctx, int op, int32_t batch, size_t i, int64_t range_start, int64_t range_end) {
+  if (!ctx || op < 0 || (op & 3) > RBG_RMUT_FLIP || op > (RBG_RMUT_FLIP | RBG_RMUT_BUFFER))
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  CHK(enter(&ctx->c));
+  return ctx_range_mut(&ctx->c, op & 3, batch, i, range_start, range_end, (op & RBG_RMUT_BUFFER) != 0);
 }
 
 int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int32_t* out) {

@@ -367,6 +367,15 @@ void launch_bsi_buf(hipStream_t s, int grid, const Task* tasks, const uint32_t* 
 void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
                      const uint8_t* pb, OutCtx oc, BigRuns big);
 
+// static add / remove / flip(rb, rangeStart, rangeEnd) (rangemut.hip); hbs > hbl: no key in the range
+enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2 };
+struct RmutArgs {
+  int op, hbs, lbs, hbl, lbl;
+};
+void launch_rmut(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint8_t* pa, RmutArgs ra, bool buf,
+                 uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint64_t* zlb,
+                 uint64_t* ztile, BigRuns big, int grid);
+
 // RoaringBitmap.orNot (ornot.hip): the reference's key-loop bound, computed on the device
 struct OrNotPlan {
   int32_t k_end;       // keys [0, k_end) the loop reaches

@@ -1,0 +1,182 @@
+// Static range mutations on the MI355X: RoaringBitmap.add(rb, rangeStart, rangeEnd)
+// (RB/RoaringBitmap.java:298-345), remove(rb, ...) (:995-1040), flip(rb, ...) (:626-668), and the
+// buffer package's MutableRoaringBitmap.add / remove / flip (RB/buffer/MutableRoaringBitmap.java
+// :152-205, 649-700, 455-505; ImmutableRoaringBitmap.flip :592-640).
+//
+// Keys outside [hbStart, hbLast] are cloned.  Inside, per key with the cut [lo, hi]:
+//   add    : Container.add(lo, hi + 1) on the first / last key (a missing key: rangeOfOnes), a full run
+//            container on every key between them
+//   remove : Container.remove(lo, hi + 1) on the first / last key unless the cut covers the whole key;
+//            the keys between (and fully covered ones) dropped, emptied containers dropped
+//   flip   : Container.not(lo, hi + 1) on every key (a missing key: rangeOfOnes), emptied dropped
+// Result types (the per-key container methods):
+//   add    : ArrayContainer.add -> an array, or above 4096 values toBitmapContainer().iadd, a bitmap
+//            (RB/ArrayContainer.java:103-135); BitmapContainer.add a bitmap, full included (:131-143);
+//            RunContainer.add = clone().iadd, a run container whatever its size (RB/RunContainer.java:242)
+//   remove : an array stays one; a bitmap becomes an array at <= 4096 values (RB/BitmapContainer.java
+//            :1166-1181), the buffer package's below 4096 (RB/buffer/MappeableBitmapContainer.java
+//            :1597-1612); a run container keeps its clipped runs
+//   flip   : arrays / bitmaps by cardinality (ArrayContainer.not, BitmapContainer.inot), run containers
+//            through toEfficientContainer (RB/RunContainer.java:1900-1918)
+// Run results that stay run containers whatever their size (add / remove of an input with more than
+// 2047 runs) go to the big-run arena, as the buffer package's run AND does (wave.hpp place_big_runs).
+//
+//   k_plan_rmut : one thread per key (the pairwise plan's compaction), the keys that give a container
+//   k_rmut      : one workgroup per task, the container in registers (vb.hpp)
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+#include "kernels.hpp"
+#include "vb.hpp"
+#include "wave.hpp"
+
+namespace rbg {
+
+__device__ uint16_t g_full_run_rm[16] = {1, 0, 0xFFFF};  // RunContainer.full(); slack for the 16 B over-read
+
+__device__ __forceinline__ void rmut_cut(int key, const RmutArgs& ra, int* lo, int* hi) {
+  *lo = key == ra.hbs ? ra.lbs : 0;
+  *hi = key == ra.hbl ? ra.lbl : 65535;
+}
+
+__global__ __launch_bounds__(256) void k_plan_rmut(const uint32_t* __restrict__ koa, const CDesc* __restrict__ da,
+                                                   const uint8_t* __restrict__ pa, RmutArgs ra,
+                                                   uint64_t* __restrict__ wg_epoch, uint32_t epoch,
+                                                   PTask* __restrict__ tasks, uint32_t* __restrict__ n_tasks,
+                                                   uint64_t* zlb, uint64_t* ztile, uint32_t* err) {
+  plan_zero(zlb, ztile);
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  PTask t;
+  resolve(koa, da, pa, k, t.slot_a, t.card_a, t.kind_a, t.nruns_a);
+  t.slot_b = 0;
+  t.card_b = 0;
+  t.kind_b = kAbsent;
+  t.nruns_b = 0;
+  t.key = (uint16_t)k;
+  const bool present = t.kind_a != kAbsent;
+  const bool in = (int)k >= ra.hbs && (int)k <= ra.hbl;
+  int f;
+  if (!in) {
+    f = present;
+  } else if (ra.op == RMUT_REMOVE) {
+    int lo, hi;
+    rmut_cut((int)k, ra, &lo, &hi);
+    f = present && !(lo == 0 && hi == 65535);
+  } else {
+    f = 1;
+  }
+  plan_emit(f, t, wg_epoch, epoch, tasks, n_tasks, err);
+}
+
+// bits [lo, hi] of owned register word i (device.hpp: thread t owns words 2t, 2t+1, 512+2t, 513+2t)
+__device__ __forceinline__ uint64_t owned_range_mask(int i, int lo, int hi) {
+  const int t = threadIdx.x;
+  const int w = (i < 2 ? 2 * t : 512 + 2 * t) + (i & 1);
+  const int b0 = 64 * w, b1 = b0 + 63;
+  if (b1 < lo || b0 > hi) return 0ull;
+  uint64_t m = ~0ull;
+  if (lo > b0) m &= ~0ull << (lo - b0);
+  if (hi < b1) m &= ~0ull >> (b1 - hi);
+  return m;
+}
+
+template <int OP, bool BUF>
+__global__ __launch_bounds__(256) void k_rmut(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+                                              const uint8_t* pa, RmutArgs ra, OutCtx oc, BigRuns big) {
+  __shared__ __align__(16) uint32_t acc[2048];
+  __shared__ __align__(16) uint32_t tmp[2048];
+  __shared__ int q[257];
+  __shared__ int sh[8];
+  __shared__ unsigned long long sh64;
+  const uint32_t nt = *n_tasks;
+  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
+    const PTask tk = tasks[t];
+    const int key = tk.key;
+    const bool present = tk.kind_a != kAbsent;
+    if (key < ra.hbs || key > ra.hbl) {  // outside the range: cloned
+      wg_passthrough(t, CDesc{tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0}, pa, oc, nullptr);
+      continue;
+    }
+    int lo, hi;
+    rmut_cut(key, ra, &lo, &hi);
+    if (OP == RMUT_ADD && key != ra.hbs && key != ra.hbl) {  // rangeOfOnes(0, 65536): a full run container
+      wg_place(t, true, reinterpret_cast<const uint8_t*>(g_full_run_rm), false, nullptr, 6, 65536, key, DK_R, oc,
+               nullptr);
+      continue;
+    }
+    if (!present) {  // rangeOfOnes(lo, hi + 1) (add / flip), written by one thread
+      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+      const int n = hi - lo + 1;
+      const bool arr = n <= 2;
+      uint16_t* p = reinterpret_cast<uint16_t*>(arr ? slot : slot + 2);
+      if (threadIdx.x == 0) {
+        if (arr) {
+          p[0] = (uint16_t)lo;
+          p[1] = (uint16_t)hi;
+        } else {
+          p[0] = 1;
+          p[1] = (uint16_t)lo;
+          p[2] = (uint16_t)(hi - lo);
+        }
+      }
+      wg_place(t, true, reinterpret_cast<const uint8_t*>(p), false, nullptr, arr ? 2u * n : 6u, (uint32_t)n, key,
+               arr ? DK_A : DK_R, oc, nullptr);
+      continue;
+    }
+    VB x;
+    pb_load(tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0, pa, tmp, q, x);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint64_t m = owned_range_mask(i, lo, hi);
+      if (OP == RMUT_ADD) x.r[i] |= m;
+      else if (OP == RMUT_REMOVE) x.r[i] &= ~m;
+      else x.r[i] ^= m;
+    }
+    int c = popc64(x.r[0]) + popc64(x.r[1]) + popc64(x.r[2]) + popc64(x.r[3]);
+    int u = 0;
+    block_sum2(c, u, sh);
+    c = (int)uni((uint32_t)c);
+    if (c == 0) {  // remove / flip emptied the container: dropped
+      wg_place(t, false, nullptr, true, tmp, 0, 0, key, DK_A, oc, nullptr);
+      continue;
+    }
+    int kind;
+    if (OP == RMUT_ADD) kind = x.kind == DK_A ? by_card(c) : x.kind;
+    else if (OP == RMUT_REMOVE) kind = x.kind == DK_B ? ((BUF ? c < 4096 : c <= 4096) ? DK_A : DK_B) : x.kind;
+    else kind = x.kind == DK_R ? eff(c, count_runs(x.r, acc, sh)) : by_card(c);
+    if (kind == DK_B) {  // registers straight to the task's slot
+      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+      store_bitmap_owned(slot, x.r);
+      wg_place(t, true, slot, false, nullptr, 8192, (uint32_t)c, key, DK_B, oc, nullptr);
+      continue;
+    }
+    if (kind == DK_R) {
+      const int nr = count_runs(x.r, acc, sh);
+      if (nr > 2047) {
+        place_big_runs(t, key, x.r, c, nr, oc, big, acc, sh, &sh64);
+        continue;
+      }
+    }
+    const uint32_t len = stage_container(kind, x.r, c, acc, tmp, sh);
+    wg_place(t, true, nullptr, true, tmp, len, (uint32_t)c, key, kind, oc, nullptr);
+  }
+}
+
+void launch_rmut(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint8_t* pa, RmutArgs ra, bool buf,
+                 uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint64_t* zlb,
+                 uint64_t* ztile, BigRuns big, int grid) {
+  hipLaunchKernelGGL(k_plan_rmut, dim3(256), dim3(256), 0, s, koa, da, pa, ra, wg_epoch, epoch, tasks, n_tasks, zlb,
+                     ztile, oc.err);
+  const int g0 = std::max(1, grid);
+#define RBG_RMUT_LAUNCH(O, B)                                                                                    \
+  hipLaunchKernelGGL((k_rmut<O, B>), dim3(std::min(g0, resident_grid((const void*)&k_rmut<O, B>))), dim3(256), 0, s, \
+                     tasks, n_tasks, pa, ra, oc, big)
+  if (ra.op == RMUT_ADD) RBG_RMUT_LAUNCH(RMUT_ADD, false);
+  else if (ra.op == RMUT_FLIP) RBG_RMUT_LAUNCH(RMUT_FLIP, false);
+  else if (buf) RBG_RMUT_LAUNCH(RMUT_REMOVE, true);
+  else RBG_RMUT_LAUNCH(RMUT_REMOVE, false);
+#undef RBG_RMUT_LAUNCH
+}
+
+}  // namespace rbg

@@ -144,6 +144,33 @@ def _s_ornot(x1, x2, range_end):
     return RoaringBitmap(_ornot(x1, x2, range_end, False))
 
 
+class _RangeMut:
+    """The static range mutations RoaringBitmap.add / remove / flip(rb, rangeStart, rangeEnd)
+    (RB/RoaringBitmap.java:298-345, 995-1040, 626-668) on the class or with three arguments; buffer:
+    MutableRoaringBitmap's (RB/buffer/MutableRoaringBitmap.java:152-205, 649-700, 455-505), results of
+    class `cls`.  The instance forms (x.add(start, end) in place) are not on this path."""
+
+    def __init__(self, op, buffer=False, cls=None):
+        self.op, self.buffer, self.cls = op, buffer, cls
+
+    def static(self, rb, range_start, range_end):
+        b = _lib.rbg_buffer()
+        code = _lib.RMUT_OP[self.op] | (_lib.RBG_RMUT_BUFFER if self.buffer else 0)
+        check(lib().rbg_range_mut(code, rb._buf, len(rb._buf), int(range_start), int(range_end), ctypes.byref(b)))
+        return (self.cls or RoaringBitmap)(take(b))
+
+    def __get__(self, obj, objtype=None):
+        if obj is None:
+            return self.static
+
+        def call(*args):
+            if len(args) == 3:
+                return self.static(*args)
+            raise NotImplementedError(f"in-place {self.op}: use the static form {type(obj).__name__}.{self.op}("
+                                      f"rb, rangeStart, rangeEnd)")
+        return call
+
+
 class RoaringBitmap:
     __slots__ = ("_buf", "_lcard")
 
@@ -277,6 +304,9 @@ class RoaringBitmap:
     xor = _StaticOrInPlace(_s_xor, "xor")
     andNot = _StaticOrInPlace(_s_andnot, "andnot")
     orNot = _OrNot(_s_ornot)
+    add = _RangeMut("add")
+    remove = _RangeMut("remove")
+    flip = _RangeMut("flip")
 
     def _inplace(self, op, x2):
         """x1.and / or / xor / andNot(x2) in place (rbg_pairwise_inplace); x2 may be x1 itself"""
@@ -749,6 +779,7 @@ class ImmutableRoaringBitmap(RoaringBitmap):
     andNot = _s_andnot
     or_ = _s_or
     xor = _s_xor
+    add = remove = None  # no static add / remove on ImmutableRoaringBitmap (MutableRoaringBitmap's: below)
     andCardinality = RoaringBitmap.__dict__["andCardinality"]  # :336-359, a set-level count
     intersects = RoaringBitmap.__dict__["intersects"]
 
@@ -785,6 +816,11 @@ setattr(ImmutableRoaringBitmap, "and", ImmutableRoaringBitmap.__dict__["and_"])
 setattr(ImmutableRoaringBitmap, "or", ImmutableRoaringBitmap.__dict__["or_"])
 setattr(MutableRoaringBitmap, "and", MutableRoaringBitmap.__dict__["and_"])
 setattr(MutableRoaringBitmap, "or", MutableRoaringBitmap.__dict__["or_"])
+# the buffer package's static range mutations: ImmutableRoaringBitmap.flip (RB/buffer/ImmutableRoaringBitmap
+# .java:592-640), MutableRoaringBitmap.add / remove / flip (RB/buffer/MutableRoaringBitmap.java:152, 649, 455)
+ImmutableRoaringBitmap.flip = _RangeMut("flip", True, MutableRoaringBitmap)
+for _op in ("add", "remove", "flip"):
+    setattr(MutableRoaringBitmap, _op, _RangeMut(_op, True, MutableRoaringBitmap))
 
 setattr(BufferFastAggregation, "and", BufferFastAggregation.and_)
 setattr(BufferFastAggregation, "or", BufferFastAggregation.or_)

@@ -219,7 +219,10 @@ def test_pairwise_op_codes_match_header():
                  "and": "RBG_RANGE_AND", "andnot": "RBG_RANGE_ANDNOT"}.items():  # rbg_range_op
         m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
         assert m and int(m.group(1)) == L.RANGE_OP[k], k
-    for c in ("RBG_ORNOT_INPLACE", "RBG_ORNOT_BUFFER"):  # rbg_ornot's flags
+    for k, c in {"add": "RBG_RMUT_ADD", "remove": "RBG_RMUT_REMOVE", "flip": "RBG_RMUT_FLIP"}.items():
+        m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
+        assert m and int(m.group(1)) == L.RMUT_OP[k], k
+    for c in ("RBG_ORNOT_INPLACE", "RBG_ORNOT_BUFFER", "RBG_RMUT_BUFFER"):  # rbg_ornot's / rbg_range_mut's flags
         m = re.search(r"\b" + c + r"\s*=\s*(\d+)", src)
         assert m and int(m.group(1)) == getattr(L, c), c
 
