@@ -19,16 +19,15 @@
 //   flip   : arrays / bitmaps by cardinality (ArrayContainer.not, BitmapContainer.inot), run containers
 //            through toEfficientContainer (RB/RunContainer.java:1900-1918)
 // Run results that stay run containers whatever their size (add / remove of an input with more than
-// 2047 runs) go to the big-run arena, as the buffer package's run AND does (wave.hpp place_big_runs).
+// 2047 runs) go to the big-run arena (w_place_big_runs), as the buffer package's run AND results do.
 //
 //   k_plan_rmut : one thread per key (the pairwise plan's compaction), the keys that give a container
-//   k_rmut      : one workgroup per task, the container in registers (vb.hpp)
+//   k_rmut      : one wave per task, the container in registers (wave.hpp)
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
 #include "kernels.hpp"
-#include "vb.hpp"
 #include "wave.hpp"
 
 namespace rbg {
@@ -69,10 +68,9 @@ __global__ __launch_bounds__(256) void k_plan_rmut(const uint32_t* __restrict__ 
   plan_emit(f, t, wg_epoch, epoch, tasks, n_tasks, err);
 }
 
-// bits [lo, hi] of owned register word i (device.hpp: thread t owns words 2t, 2t+1, 512+2t, 513+2t)
-__device__ __forceinline__ uint64_t owned_range_mask(int i, int lo, int hi) {
-  const int t = threadIdx.x;
-  const int w = (i < 2 ? 2 * t : 512 + 2 * t) + (i & 1);
+// bits [lo, hi] of register k of the wave layout (WCtr: w[2 i + j] = word 128 i + 2 lane + j)
+__device__ __forceinline__ uint64_t wrange(int k, int lo, int hi) {
+  const int w = 128 * (k >> 1) + 2 * lane_id() + (k & 1);
   const int b0 = 64 * w, b1 = b0 + 63;
   if (b1 < lo || b0 > hi) return 0ull;
   uint64_t m = ~0ull;
@@ -81,85 +79,128 @@ __device__ __forceinline__ uint64_t owned_range_mask(int i, int lo, int hi) {
   return m;
 }
 
+// A run result of more than 2047 runs (add / remove of an input run container that large, which stay
+// run containers) into the big-run arena: [u16 nruns][(start, length - 1) pairs], straight from the
+// registers (w_stage_runs_chunk without the LDS cap), then the ends turned into lengths.
+__device__ __forceinline__ void w_place_big_runs(uint32_t t, uint32_t key, const WCtr& x, int card, int nr,
+                                                 const OutCtx& oc, const BigRuns& big, uint32_t* lds) {
+  const uint32_t len = 2u + 4u * (uint32_t)nr;
+  unsigned long long off = 0;
+  if (lane_id() == 0) {
+    off = atomicAdd(&big.used[0], (unsigned long long)((len + 15u) & ~15u));
+    if (off + len > big.cap) {
+      atomicOr(&big.used[1], 1ull);  // the host reruns the op with a larger arena
+      off = ~0ull;
+    }
+  }
+  off = __shfl(off, 0);
+  if (off == ~0ull) {
+    w_place(t, false, nullptr, true, lds, 0, 0, key, DK_A, oc);
+    return;
+  }
+  uint16_t* dst = reinterpret_cast<uint16_t*>(big.base + off);
+  w_stage_runs_chunk<0, (1 << 30)>(x, dst, 0, 0);
+  __threadfence_block();
+  wsync();
+  for (int p = lane_id(); p < nr; p += 64) dst[2 + 2 * p] = (uint16_t)(dst[2 + 2 * p] - dst[1 + 2 * p]);
+  if (lane_id() == 0) dst[0] = (uint16_t)nr;
+  w_place(t, true, big.base + off, false, lds, len, (uint32_t)card, key, DK_R, oc);
+}
+
+template <int OP, bool BUF>
+__device__ __forceinline__ void rmut_task(uint32_t t, const PTask& tk, const uint8_t* pa, const RmutArgs& ra,
+                                          const OutCtx& oc, const BigRuns& big, uint32_t* lds) {
+  const int key = tk.key;
+  const bool present = tk.kind_a != kAbsent;
+  if (key < ra.hbs || key > ra.hbl) {  // outside the range: cloned
+    const uint32_t len = tk.kind_a == DK_A ? 2u * tk.card_a : tk.kind_a == DK_B ? 8192u : 2u + 4u * tk.nruns_a;
+    w_place(t, true, pa + tk.slot_a + (tk.kind_a == DK_R ? 2 : 0), false, lds, len, tk.card_a, (uint32_t)key,
+            tk.kind_a, oc);
+    return;
+  }
+  int lo, hi;
+  rmut_cut(key, ra, &lo, &hi);
+  if (OP == RMUT_ADD && key != ra.hbs && key != ra.hbl) {  // rangeOfOnes(0, 65536): a full run container
+    w_place(t, true, reinterpret_cast<const uint8_t*>(g_full_run_rm), false, lds, 6, 65536, (uint32_t)key, DK_R, oc);
+    return;
+  }
+  if (!present) {  // rangeOfOnes(lo, hi + 1) (add / flip), written by lane 0
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+    const int n = hi - lo + 1;
+    const bool arr = n <= 2;
+    uint16_t* p = reinterpret_cast<uint16_t*>(arr ? slot : slot + 2);
+    if (lane_id() == 0) {
+      if (arr) {
+        p[0] = (uint16_t)lo;
+        p[1] = (uint16_t)hi;
+      } else {
+        p[0] = 1;
+        p[1] = (uint16_t)lo;
+        p[2] = (uint16_t)(hi - lo);
+      }
+    }
+    w_place(t, true, reinterpret_cast<const uint8_t*>(p), false, lds, arr ? 2u * n : 6u, (uint32_t)n, (uint32_t)key,
+            arr ? DK_A : DK_R, oc);
+    return;
+  }
+  WCtr x;
+  w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0}, pa, lds, x);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const uint64_t m = wrange(k, lo, hi);
+    if (OP == RMUT_ADD) x.w[k] |= m;
+    else if (OP == RMUT_REMOVE) x.w[k] &= ~m;
+    else x.w[k] ^= m;
+  }
+  const int c = w_card(x);
+  if (c == 0) {  // remove / flip emptied the container: dropped
+    w_place(t, false, nullptr, true, lds, 0, 0, (uint32_t)key, DK_A, oc);
+    return;
+  }
+  const int kx = tk.kind_a;
+  int kind;
+  if (OP == RMUT_ADD) kind = kx == DK_A ? by_card(c) : kx;
+  else if (OP == RMUT_REMOVE) kind = kx == DK_B ? ((BUF ? c < 4096 : c <= 4096) ? DK_A : DK_B) : kx;
+  else kind = kx == DK_R ? eff(c, w_runs(x)) : by_card(c);
+  if (kind == DK_B) {  // registers straight to the task's slot
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+    w_store_bitmap(slot, x);
+    w_place(t, true, slot, false, lds, 8192, (uint32_t)c, (uint32_t)key, DK_B, oc);
+    return;
+  }
+  if (kind == DK_R && OP != RMUT_FLIP) {
+    const int nr = w_runs(x);
+    if (nr > 2047) {
+      w_place_big_runs(t, (uint32_t)key, x, c, nr, oc, big, lds);
+      return;
+    }
+  }
+  const uint32_t len = w_stage(kind, x, c, lds);
+  w_place(t, true, nullptr, true, lds, len, (uint32_t)c, (uint32_t)key, kind, oc);
+}
+
+constexpr int kRmWaves = 4;
+
+// one wave per task over a static stride, the next record fetched while a task runs
 template <int OP, bool BUF>
 __global__ __launch_bounds__(256) void k_rmut(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                               const uint8_t* pa, RmutArgs ra, OutCtx oc, BigRuns big) {
-  __shared__ __align__(16) uint32_t acc[2048];
-  __shared__ __align__(16) uint32_t tmp[2048];
-  __shared__ int q[257];
-  __shared__ int sh[8];
-  __shared__ unsigned long long sh64;
-  const uint32_t nt = *n_tasks;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    const PTask tk = tasks[t];
-    const int key = tk.key;
-    const bool present = tk.kind_a != kAbsent;
-    if (key < ra.hbs || key > ra.hbl) {  // outside the range: cloned
-      wg_passthrough(t, CDesc{tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0}, pa, oc, nullptr);
-      continue;
-    }
-    int lo, hi;
-    rmut_cut(key, ra, &lo, &hi);
-    if (OP == RMUT_ADD && key != ra.hbs && key != ra.hbl) {  // rangeOfOnes(0, 65536): a full run container
-      wg_place(t, true, reinterpret_cast<const uint8_t*>(g_full_run_rm), false, nullptr, 6, 65536, key, DK_R, oc,
-               nullptr);
-      continue;
-    }
-    if (!present) {  // rangeOfOnes(lo, hi + 1) (add / flip), written by one thread
-      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
-      const int n = hi - lo + 1;
-      const bool arr = n <= 2;
-      uint16_t* p = reinterpret_cast<uint16_t*>(arr ? slot : slot + 2);
-      if (threadIdx.x == 0) {
-        if (arr) {
-          p[0] = (uint16_t)lo;
-          p[1] = (uint16_t)hi;
-        } else {
-          p[0] = 1;
-          p[1] = (uint16_t)lo;
-          p[2] = (uint16_t)(hi - lo);
-        }
-      }
-      wg_place(t, true, reinterpret_cast<const uint8_t*>(p), false, nullptr, arr ? 2u * n : 6u, (uint32_t)n, key,
-               arr ? DK_A : DK_R, oc, nullptr);
-      continue;
-    }
-    VB x;
-    pb_load(tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0, pa, tmp, q, x);
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const uint64_t m = owned_range_mask(i, lo, hi);
-      if (OP == RMUT_ADD) x.r[i] |= m;
-      else if (OP == RMUT_REMOVE) x.r[i] &= ~m;
-      else x.r[i] ^= m;
-    }
-    int c = popc64(x.r[0]) + popc64(x.r[1]) + popc64(x.r[2]) + popc64(x.r[3]);
-    int u = 0;
-    block_sum2(c, u, sh);
-    c = (int)uni((uint32_t)c);
-    if (c == 0) {  // remove / flip emptied the container: dropped
-      wg_place(t, false, nullptr, true, tmp, 0, 0, key, DK_A, oc, nullptr);
-      continue;
-    }
-    int kind;
-    if (OP == RMUT_ADD) kind = x.kind == DK_A ? by_card(c) : x.kind;
-    else if (OP == RMUT_REMOVE) kind = x.kind == DK_B ? ((BUF ? c < 4096 : c <= 4096) ? DK_A : DK_B) : x.kind;
-    else kind = x.kind == DK_R ? eff(c, count_runs(x.r, acc, sh)) : by_card(c);
-    if (kind == DK_B) {  // registers straight to the task's slot
-      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
-      store_bitmap_owned(slot, x.r);
-      wg_place(t, true, slot, false, nullptr, 8192, (uint32_t)c, key, DK_B, oc, nullptr);
-      continue;
-    }
-    if (kind == DK_R) {
-      const int nr = count_runs(x.r, acc, sh);
-      if (nr > 2047) {
-        place_big_runs(t, key, x.r, c, nr, oc, big, acc, sh, &sh64);
-        continue;
-      }
-    }
-    const uint32_t len = stage_container(kind, x.r, c, acc, tmp, sh);
-    wg_place(t, true, nullptr, true, tmp, len, (uint32_t)c, key, kind, oc, nullptr);
+  __shared__ __align__(16) uint32_t lds_all[kRmWaves][2048];
+  const int w = threadIdx.x >> 6;
+  uint32_t* lds = lds_all[w];
+  const uint32_t nt = uni(*n_tasks);
+  const uint32_t stride = gridDim.x * kRmWaves;
+  uint32_t t = uni(blockIdx.x * kRmWaves + w);
+  if (t >= nt) return;
+  PTask cur = load_task(tasks, t);
+  for (;;) {
+    const uint32_t tn = t + stride;
+    PTask nxt;
+    if (tn < nt) nxt = load_task(tasks, tn);
+    rmut_task<OP, BUF>(t, cur, pa, ra, oc, big, lds);
+    if (tn >= nt) break;
+    t = tn;
+    cur = nxt;
   }
 }
 
@@ -168,7 +209,7 @@ void launch_rmut(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint
                  uint64_t* ztile, BigRuns big, int grid) {
   hipLaunchKernelGGL(k_plan_rmut, dim3(256), dim3(256), 0, s, koa, da, pa, ra, wg_epoch, epoch, tasks, n_tasks, zlb,
                      ztile, oc.err);
-  const int g0 = std::max(1, grid);
+  const int g0 = std::max(1, (grid + kRmWaves - 1) / kRmWaves);
 #define RBG_RMUT_LAUNCH(O, B)                                                                                    \
   hipLaunchKernelGGL((k_rmut<O, B>), dim3(std::min(g0, resident_grid((const void*)&k_rmut<O, B>))), dim3(256), 0, s, \
                      tasks, n_tasks, pa, ra, oc, big)

@@ -830,7 +830,8 @@ __device__ __forceinline__ int w_probe_pre(const uint32_t* lds, const WPre& p, i
 // (start, len-1) pairs) in LDS when the result has <= 2047 runs (the most a run
 // result can have: EFF keeps R only if 2 + 4 * nruns <= 8192).  Returns the
 // run count.
-template <int I>
+// CAP: runs written at most (2047 for an 8 KiB LDS stage; unbounded for a big-run arena slot)
+template <int I, int CAP = 2047>
 __device__ __forceinline__ int w_stage_runs_chunk(const WCtr& x, uint16_t* st, int base, int base_e) {
   const int l = lane_id();
   uint64_t s0, s1, e0, e1;
@@ -844,28 +845,28 @@ __device__ __forceinline__ int w_stage_runs_chunk(const WCtr& x, uint16_t* st, i
   int pe0 = base_e + (packed >> 16), pe1 = pe0 + ce0;
   while (s0 | s1 | e0 | e1) {
     if (s0) {
-      if (ps0 < 2047) st[1 + 2 * ps0] = (uint16_t)(wb + __builtin_ctzll(s0));
+      if (ps0 < CAP) st[1 + 2 * ps0] = (uint16_t)(wb + __builtin_ctzll(s0));
       ps0++;
       s0 &= s0 - 1;
     }
     if (s1) {
-      if (ps1 < 2047) st[1 + 2 * ps1] = (uint16_t)(wb + 64 + __builtin_ctzll(s1));
+      if (ps1 < CAP) st[1 + 2 * ps1] = (uint16_t)(wb + 64 + __builtin_ctzll(s1));
       ps1++;
       s1 &= s1 - 1;
     }
     if (e0) {
-      if (pe0 < 2047) st[2 + 2 * pe0] = (uint16_t)(wb + __builtin_ctzll(e0));
+      if (pe0 < CAP) st[2 + 2 * pe0] = (uint16_t)(wb + __builtin_ctzll(e0));
       pe0++;
       e0 &= e0 - 1;
     }
     if (e1) {
-      if (pe1 < 2047) st[2 + 2 * pe1] = (uint16_t)(wb + 64 + __builtin_ctzll(e1));
+      if (pe1 < CAP) st[2 + 2 * pe1] = (uint16_t)(wb + 64 + __builtin_ctzll(e1));
       pe1++;
       e1 &= e1 - 1;
     }
   }
   const int nb = base + (tot & 0xFFFF), nbe = base_e + (tot >> 16);
-  if (I < 7) return w_stage_runs_chunk<(I < 7 ? I + 1 : 7)>(x, st, nb, nbe);
+  if (I < 7) return w_stage_runs_chunk<(I < 7 ? I + 1 : 7), CAP>(x, st, nb, nbe);
   return nb;
 }
 

@@ -125,6 +125,12 @@ class Engine:
         flags = (_lib.RBG_ORNOT_INPLACE if inplace else 0) | (_lib.RBG_ORNOT_BUFFER if buffer else 0)
         check(lib().rbg_ctx_ornot(self._ctx, int(a), int(ia), int(b), int(ib), int(range_end), flags))
 
+    def range_mut(self, op, a, range_start, range_end, buffer=False, ia=0):
+        """static RoaringBitmap.add / remove / flip(rb, start, end) ("add" / "remove" / "flip"; buffer:
+        MutableRoaringBitmap's) of a resident bitmap; the result pending like pairwise's (rbg_ctx_range_mut)."""
+        code = _lib.RMUT_OP[op] | (_lib.RBG_RMUT_BUFFER if buffer else 0)
+        check(lib().rbg_ctx_range_mut(self._ctx, code, int(a), int(ia), int(range_start), int(range_end)))
+
     def pairwise_serialized(self, op, a, b, ia=0, ib=0):
         """pairwise(op) + serialize() as one pipeline (rbg_ctx_pairwise_serialized): the result's
         placement and payload copies for one key range overlap the next range's compute."""
