@@ -1195,50 +1195,78 @@ void launch_bsi_buf(hipStream_t s, int grid, const Task* tasks, const uint32_t* 
 // MutableRoaringBitmap's static and / andNot (RB/buffer/MutableRoaringBitmap.java:235-301): per key
 // c1.and(c2) / c1.andNot(c2) with the buffer package's container types -- vb_op<OP, true>, the
 // buffer BSI's step: run AND / ANDNOT run keep the merged run container (more than 2047 runs go to
-// the big-run arena), every other pair types like the heap's.  One workgroup per task of the
+// the big-run arena), every other pair types like the heap's.  Tasks from the
 // pairwise plan (k_plan_pairwise: AND = keys of both, ANDNOT = keys of x1); an x1 container with
 // no x2 counterpart is appended as is (appendCopy, :460-469).
+// one wave per task (20 per CU, the next record in flight): both operands in registers (wave.hpp), the
+// buffer package's type rule (vb_op<OP, true>'s), a run result of more than 2047 runs into the arena
+template <int OP>
+__device__ __forceinline__ void pair_buf_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
+                                              const OutCtx& oc, const BigRuns& big, uint32_t* lds) {
+  const int ka = tk.kind_a, kb = tk.kind_b;
+  if (OP == OPR_ANDNOT && kb == kAbsent) {  // x1's container alone: appendCopy (:460-469)
+    const uint32_t len = ka == DK_A ? 2u * tk.card_a : ka == DK_B ? 8192u : 2u + 4u * tk.nruns_a;
+    w_place(t, true, pa + tk.slot_a + (ka == DK_R ? 2 : 0), false, lds, len, tk.card_a, tk.key, ka, oc);
+    return;
+  }
+  WCtr x;
+  w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, (uint8_t)ka, 0}, pa, lds, x);
+  w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
+  const int c = w_card(x);
+  if (c == 0) {  // empty results are dropped
+    w_place(t, false, nullptr, true, lds, 0, 0, tk.key, DK_A, oc);
+    return;
+  }
+  const bool raw_run = ka == DK_R && kb == DK_R;  // the merged run container, no toEfficientContainer
+  int kind;
+  if (raw_run) kind = DK_R;
+  else if (pairwise_needs_runs(OP, ka, (int)tk.card_a, kb, (int)tk.card_b)) kind = eff(c, w_runs(x));
+  else kind = pairwise_kind(OP, ka, kb, c);
+  if (kind == DK_B) {
+    uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+    w_store_bitmap(slot, x);
+    w_place(t, true, slot, false, lds, 8192, (uint32_t)c, tk.key, DK_B, oc);
+    return;
+  }
+  if (raw_run) {
+    const int nr = w_runs(x);
+    if (nr > 2047) {
+      w_place_big_runs(t, tk.key, x, c, nr, oc, big, lds);
+      return;
+    }
+  }
+  const uint32_t len = w_stage(kind, x, c, lds);
+  w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, oc);
+}
+
+constexpr int kPbWaves = 4;
+
 template <int OP>
 __global__ __launch_bounds__(256) void k_pair_buf(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                                   const uint8_t* pa, const uint8_t* pb, OutCtx oc, BigRuns big) {
-  __shared__ __align__(16) uint32_t acc[2048];
-  __shared__ __align__(16) uint32_t tmp[2048];
-  __shared__ int q[257];
-  __shared__ int sh[8];
-  __shared__ unsigned long long sh64;
-  const uint32_t nt = *n_tasks;
-  for (uint32_t t = blockIdx.x; t < nt; t += gridDim.x) {
-    const PTask tk = tasks[t];
-    VB x, y, z;
-    pb_load(tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0, pa, tmp, q, x);
-    pb_load(tk.slot_b, tk.card_b, tk.key, tk.kind_b, 1, pb, tmp, q, y);
-    vb_op<OP, true>(x, y, z, acc, sh);
-    if (!z.present) {
-      wg_place(t, false, nullptr, true, tmp, 0, 0, tk.key, DK_A, oc, nullptr);
-      continue;
-    }
-    if (z.src >= 0) {  // an operand's container unchanged
-      const bool a = z.src == 0;
-      wg_passthrough(t, CDesc{a ? tk.slot_a : tk.slot_b, a ? tk.card_a : tk.card_b, tk.key, a ? tk.kind_a : tk.kind_b, 0},
-                     a ? pa : pb, oc, nullptr);
-      continue;
-    }
-    if (z.kind == DK_R) {
-      const int nr = count_runs(z.r, acc, sh);
-      if (nr > 2047) {
-        place_big_runs(t, tk.key, z.r, z.card, nr, oc, big, acc, sh, &sh64);
-        continue;
-      }
-    }
-    const uint32_t len = stage_container(z.kind, z.r, z.card, acc, tmp, sh);
-    wg_place(t, true, nullptr, true, tmp, len, (uint32_t)z.card, tk.key, z.kind, oc, nullptr);
+  __shared__ __align__(16) uint32_t lds_all[kPbWaves][2048];
+  const int w = threadIdx.x >> 6;
+  uint32_t* lds = lds_all[w];
+  const uint32_t nt = uni(*n_tasks);
+  const uint32_t stride = gridDim.x * kPbWaves;
+  uint32_t t = uni(blockIdx.x * kPbWaves + w);
+  if (t >= nt) return;
+  PTask cur = load_task(tasks, t);
+  for (;;) {
+    const uint32_t tn = t + stride;
+    PTask nxt;
+    if (tn < nt) nxt = load_task(tasks, tn);
+    pair_buf_task<OP>(t, cur, pa, pb, oc, big, lds);
+    if (tn >= nt) break;
+    t = tn;
+    cur = nxt;
   }
 }
 
 void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
                      const uint8_t* pb, OutCtx oc, BigRuns big) {
   const void* k = op == OPR_AND ? (const void*)&k_pair_buf<OPR_AND> : (const void*)&k_pair_buf<OPR_ANDNOT>;
-  const int g = std::max(1, std::min(grid, resident_grid(k)));
+  const int g = std::max(1, std::min((grid + kPbWaves - 1) / kPbWaves, resident_grid(k)));
   if (op == OPR_AND) hipLaunchKernelGGL(k_pair_buf<OPR_AND>, dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, big);
   else hipLaunchKernelGGL(k_pair_buf<OPR_ANDNOT>, dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, big);
 }

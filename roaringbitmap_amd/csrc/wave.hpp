@@ -1180,6 +1180,34 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
   }
 }
 
+// A run result of more than 2047 runs (results that stay run containers whatever their size: the buffer
+// package's run AND / ANDNOT run, add / remove of an input run container that large) into the big-run arena: [u16 nruns][(start, length - 1) pairs], straight from the
+// registers (w_stage_runs_chunk without the LDS cap), then the ends turned into lengths.
+__device__ __forceinline__ void w_place_big_runs(uint32_t t, uint32_t key, const WCtr& x, int card, int nr,
+                                                 const OutCtx& oc, const BigRuns& big, uint32_t* lds) {
+  const uint32_t len = 2u + 4u * (uint32_t)nr;
+  unsigned long long off = 0;
+  if (lane_id() == 0) {
+    off = atomicAdd(&big.used[0], (unsigned long long)((len + 15u) & ~15u));
+    if (off + len > big.cap) {
+      atomicOr(&big.used[1], 1ull);  // the host reruns the op with a larger arena
+      off = ~0ull;
+    }
+  }
+  off = __shfl(off, 0);
+  if (off == ~0ull) {
+    w_place(t, false, nullptr, true, lds, 0, 0, key, DK_A, oc);
+    return;
+  }
+  uint16_t* dst = reinterpret_cast<uint16_t*>(big.base + off);
+  w_stage_runs_chunk<0, (1 << 30)>(x, dst, 0, 0);
+  __threadfence_block();
+  wsync();
+  for (int p = lane_id(); p < nr; p += 64) dst[2 + 2 * p] = (uint16_t)(dst[2 + 2 * p] - dst[1 + 2 * p]);
+  if (lane_id() == 0) dst[0] = (uint16_t)nr;
+  w_place(t, true, big.base + off, false, lds, len, (uint32_t)card, key, DK_R, oc);
+}
+
 __device__ __forceinline__ void wg_passthrough(uint32_t t, const CDesc& d, const uint8_t* payload, const OutCtx& oc,
                                                Prefix* shp) {
   uint32_t len;
