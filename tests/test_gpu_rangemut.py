@@ -95,3 +95,21 @@ def test_resident_batch(gpu):
     for op in ("add", "remove", "flip"):
         L.check(L.lib().rbg_ctx_range_mut(eng._ctx, L.RMUT_OP[op], ia, 0, 12345, (7 << 16) + 5))
         assert eng.fetch().serialize() == O.range_mut(op, buf, 12345, (7 << 16) + 5), op
+
+
+def test_max_run_count_inputs(gpu):
+    """run containers of 32,768 one-value runs (the most a container can hold): add / remove keep them as
+    run containers of that size (the big-run arena), flip makes them bitmaps; orNot and the buffer
+    package's and / andNot take them as operands"""
+    rb = _rb()
+    alt = np.arange(0, 65536, 2)
+    x = encode([(0, R, alt), (1, R, alt + 1), (2, A, np.arange(0, 4000, 3))])
+    y = encode([(0, R, alt + 1), (1, B, np.arange(0, 65536, 5)), (3, R, alt)])
+    for st, en in ((5, 60000), (0, 3 << 16), (70000, (2 << 16) + 9)):
+        _check(x, st, en, "maxruns")
+    for end in (1 << 16, (1 << 16) + 1001, 4 << 16):
+        got = rb.RoaringBitmap.orNot(rb.RoaringBitmap(x), rb.RoaringBitmap(y), end).serialize()
+        assert got == O.ornot(x, y, end), end
+    I = rb.ImmutableRoaringBitmap
+    assert getattr(I, "and")(I(x), I(y)).serialize() == O.pairwise("and_buf", x, y)
+    assert I.andNot(I(x), I(y)).serialize() == O.pairwise("andnot_buf", x, y)
