@@ -102,6 +102,25 @@ def test_c2_full_pair(eng, c2, variant, op):
 
 
 @pytest.mark.parametrize("variant", ["raw", "runopt"])
+def test_c2_widened_ops(eng, c2, variant):
+    """The round-5 rows at the C2 size, byte-exact against the oracle on the fetched operands:
+    orNot over the whole universe and mid-key (static and in place, heap and buffer), the buffer
+    package's and / andNot, and the static flip / add / remove over ranges that cut keys."""
+    x, y, xa, xb = c2[variant]
+    for end, flags in (((1 << 32), 0), ((40000 << 16) + 123, 0), ((1 << 32), 1), ((40000 << 16) + 123, 3)):
+        eng.ornot(x, y, end, inplace=bool(flags & 1), buffer=bool(flags & 2))
+        _same(eng.fetch().serialize(), O.ornot(xa, xb, end, inplace=bool(flags & 1), buffer=bool(flags & 2)),
+              f"C2 {variant} orNot end={end} flags={flags}")
+    for op in ("and_buffer", "andnot_buffer"):
+        eng.pairwise(op, x, y)
+        _same(eng.fetch().serialize(), O.pairwise(op.replace("_buffer", "_buf"), xa, xb), f"C2 {variant} {op}")
+    for op, st, en in (("flip", 0, 1 << 32), ("flip", (100 << 16) + 5, (60000 << 16) + 7),
+                       ("add", (100 << 16) + 5, (60000 << 16) + 7), ("remove", (100 << 16) + 5, (60000 << 16) + 7)):
+        eng.range_mut(op, x, st, en)
+        _same(eng.fetch().serialize(), O.range_mut(op, xa, st, en), f"C2 {variant} {op} [{st}, {en})")
+
+
+@pytest.mark.parametrize("variant", ["raw", "runopt"])
 def test_c2_full_pair_cardinalities(eng, c2, variant):
     import roaringbitmap_amd as rb
     x, y, xa, xb = c2[variant]
