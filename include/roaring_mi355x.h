@@ -151,8 +151,12 @@ int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, in
  * (RB/buffer/MutableRoaringBitmap.java:152-205, 649-700, 455-505; ImmutableRoaringBitmap.flip :592),
  * whose MappeableBitmapContainer.remove keeps a 4096-value bitmap.  rangeSanityCheck (:204-213) ->
  * RBG_ERR_ILLEGAL_ARGUMENT; rangeEnd <= rangeStart: the input's bytes.  Synchronises the stream (a run
- * result above 2047 runs, from an input run container that large, is checked for in the run arena). */
-enum { RBG_RMUT_ADD = 0, RBG_RMUT_REMOVE = 1, RBG_RMUT_FLIP = 2, RBG_RMUT_BUFFER = 4 };
+ * result above 2047 runs, from an input run container that large, is checked for in the run arena).
+ * RBG_RMUT_ADD_INPLACE = x.add(rangeStart, rangeEnd) (RB/RoaringBitmap.java:1181-1206,
+ * RB/buffer/MutableRoaringBitmap.java:831-858): Container.iadd on every key of the range, so an array
+ * between the first and last key becomes a full bitmap where the static add puts a full run container.
+ * The in-place remove / flip (:2656, :1893) give the static forms' bytes: use RBG_RMUT_REMOVE / FLIP. */
+enum { RBG_RMUT_ADD = 0, RBG_RMUT_REMOVE = 1, RBG_RMUT_FLIP = 2, RBG_RMUT_ADD_INPLACE = 3, RBG_RMUT_BUFFER = 4 };
 int rbg_range_mut(int op, const uint8_t* a, size_t a_len, int64_t range_start, int64_t range_end, rbg_buffer* out);
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };

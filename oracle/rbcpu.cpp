@@ -1729,7 +1729,10 @@ Bitmap op_ornot(const Bitmap& x1, const Bitmap& x2, uint64_t range_end, bool inp
 // (every key of the range through Container.not, a missing key rangeOfOnes, emptied containers dropped);
 // the keys outside the range cloned.  buf: MutableRoaringBitmap's (RB/buffer/MutableRoaringBitmap.java
 // :152-205, 455-505, 649-700), whose MappeableBitmapContainer.remove keeps a 4096-value bitmap.
-// op 0 add, 1 remove, 2 flip.  rangeEnd <= rangeStart: a clone.
+// op 0 add, 1 remove, 2 flip, 3 x.add(rangeStart, rangeEnd) in place (:1181-1206: Container.iadd on every
+// key of the range, the keys between included -- an array there becomes a full bitmap, not a full run
+// container; the in-place remove :2656-2710 and flip :1893-1925 end in the static forms' containers).
+// rangeEnd <= rangeStart: a clone.
 Bitmap op_range_mut(int op, const Bitmap& b, uint64_t start, uint64_t end, bool buf) {
   if (end <= start) return b;
   const int hbs = (int)(start >> 16), lbs = (int)(start & 0xFFFF);
@@ -1748,8 +1751,8 @@ Bitmap op_range_mut(int op, const Bitmap& b, uint64_t start, uint64_t end, bool 
     cur = (i < b.size() && (int)b.keys[i] == k) ? &b.ctrs[i] : nullptr;
     if (cur) i++;
     const int lo = k == hbs ? lbs : 0, hi = k == hbl ? lbl : 65535;
-    if (op == 0) {
-      if (k != hbs && k != hbl) put(k, run_full());  // rangeOfOnes(0, 65536)
+    if (op == 0 || op == 3) {
+      if (op == 0 && k != hbs && k != hbl) put(k, run_full());  // rangeOfOnes(0, 65536)
       else put(k, cur ? c_add_range(*cur, lo, hi + 1) : range_of_ones_at(lo, hi + 1));
     } else if (op == 1) {
       if (!cur) continue;

@@ -166,9 +166,10 @@ int rbo_ornot(const uint8_t* a, size_t an, const uint8_t* b, size_t bn, int64_t 
 }
 
 // static add / remove / flip(rb, rangeStart, rangeEnd) (op 0 / 1 / 2, RB/RoaringBitmap.java:298, 995, 626);
+// op 3: x.add(rangeStart, rangeEnd) in place (:1181);
 // op | 4: MutableRoaringBitmap's (RB/buffer/MutableRoaringBitmap.java:152, 649, 455).  rangeSanityCheck -> ERR_ARG.
 int rbo_range_mut(int op, const uint8_t* a, size_t an, int64_t start, int64_t end, uint8_t** out, size_t* out_len) {
-  if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll || (op & 3) > 2) return ERR_ARG;
+  if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll || op < 0 || op > 7) return ERR_ARG;
   Bitmap x;
   int st = load(a, an, &x);
   if (st) return st;

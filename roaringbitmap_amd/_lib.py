@@ -28,7 +28,7 @@ WIDE_CARD_OP = {"and": 0, "or": 1}
 RANGE_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3,
             "and_buffer": 4, "or_buffer": 5, "xor_buffer": 6, "andnot_buffer": 7}  # ImmutableRoaringBitmap's
 RBG_ORNOT_INPLACE, RBG_ORNOT_BUFFER = 1, 2
-RMUT_OP = {"add": 0, "remove": 1, "flip": 2}  # rbg_range_mut (| RBG_RMUT_BUFFER: MutableRoaringBitmap's)
+RMUT_OP = {"add": 0, "remove": 1, "flip": 2, "add_inplace": 3}  # rbg_range_mut (| RBG_RMUT_BUFFER: MutableRoaringBitmap's)
 RBG_RMUT_BUFFER = 4
 
 

@@ -1004,7 +1004,7 @@ static int ctx_ornot(Ctx* c, int32_t ia, size_t ma, int32_t ib, size_t mb, int64
 // to the big-run arena; the arena is checked after the op and the op rerun once with the size the first
 // pass reserved (as ctx_pairwise_buffer).
 static int ctx_range_mut(Ctx* c, int op, int32_t ia, size_t ma, int64_t start, int64_t end, bool buf) {
-  if (op < RMUT_ADD || op > RMUT_FLIP) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (op < RMUT_ADD || op > RMUT_ADD_INPLACE) return RBG_ERR_ILLEGAL_ARGUMENT;
   if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll) {
     set_err("rangeStart=" + std::to_string(start) + " should be in [0, 0xffffffff], rangeEnd=" + std::to_string(end) +
             " in [0, 0xffffffff + 1]");
@@ -2258,7 +2258,7 @@ int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int6
 }
 
 int rbg_range_mut(int op, const uint8_t* a, size_t a_len, int64_t range_start, int64_t range_end, rbg_buffer* out) {
-  if (!out || op < 0 || op > (RBG_RMUT_FLIP | RBG_RMUT_BUFFER) || (op & 3) > RBG_RMUT_FLIP)
+  if (!out || op < 0 || op > (RBG_RMUT_ADD_INPLACE | RBG_RMUT_BUFFER))
     return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
   CHK(tl_ctx(&c));
@@ -2271,7 +2271,7 @@ int rbg_range_mut(int op, const uint8_t* a, size_t a_len, int64_t range_start, i
 }
 
 int rbg_ctx_range_mut(rbg_ctx* ctx, int op, int32_t batch, size_t i, int64_t range_start, int64_t range_end) {
-  if (!ctx || op < 0 || (op & 3) > RBG_RMUT_FLIP || op > (RBG_RMUT_FLIP | RBG_RMUT_BUFFER))
+  if (!ctx || op < 0 || op > (RBG_RMUT_ADD_INPLACE | RBG_RMUT_BUFFER))
     return RBG_ERR_ILLEGAL_ARGUMENT;
   CHK(enter(&ctx->c));
   return ctx_range_mut(&ctx->c, op & 3, batch, i, range_start, range_end, (op & RBG_RMUT_BUFFER) != 0);

@@ -368,7 +368,8 @@ void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const 
                      const uint8_t* pb, OutCtx oc, BigRuns big);
 
 // static add / remove / flip(rb, rangeStart, rangeEnd) (rangemut.hip); hbs > hbl: no key in the range
-enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2 };
+// RMUT_ADD_INPLACE: x.add(rangeStart, rangeEnd) (RB/RoaringBitmap.java:1181), Container.iadd on every key
+enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2, RMUT_ADD_INPLACE = 3 };
 struct RmutArgs {
   int op, hbs, lbs, hbl, lbl;
 };

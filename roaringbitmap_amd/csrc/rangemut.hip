@@ -18,6 +18,10 @@
 //            :1597-1612); a run container keeps its clipped runs
 //   flip   : arrays / bitmaps by cardinality (ArrayContainer.not, BitmapContainer.inot), run containers
 //            through toEfficientContainer (RB/RunContainer.java:1900-1918)
+//   x.add(rangeStart, rangeEnd) in place (RB/RoaringBitmap.java:1181-1206, RB/buffer/MutableRoaringBitmap.java
+//            :831-858): Container.iadd on every key of the range, the keys between included (an array there
+//            becomes a full bitmap, a bitmap stays one, a run container a full run); the in-place remove and
+//            flip end in the static forms' containers (iremove / inot keep remove / not's thresholds)
 // Run results that stay run containers whatever their size (add / remove of an input with more than
 // 2047 runs) go to the big-run arena (w_place_big_runs), as the buffer package's run AND results do.
 //
@@ -92,6 +96,7 @@ __device__ __forceinline__ void rmut_task(uint32_t t, const PTask& tk, const uin
   }
   int lo, hi;
   rmut_cut(key, ra, &lo, &hi);
+  constexpr bool ADD = OP == RMUT_ADD || OP == RMUT_ADD_INPLACE;
   if (OP == RMUT_ADD && key != ra.hbs && key != ra.hbl) {  // rangeOfOnes(0, 65536): a full run container
     w_place(t, true, reinterpret_cast<const uint8_t*>(g_full_run_rm), false, lds, 6, 65536, (uint32_t)key, DK_R, oc);
     return;
@@ -120,7 +125,7 @@ __device__ __forceinline__ void rmut_task(uint32_t t, const PTask& tk, const uin
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     const uint64_t m = wrange(k, lo, hi);
-    if (OP == RMUT_ADD) x.w[k] |= m;
+    if (ADD) x.w[k] |= m;
     else if (OP == RMUT_REMOVE) x.w[k] &= ~m;
     else x.w[k] ^= m;
   }
@@ -131,7 +136,7 @@ __device__ __forceinline__ void rmut_task(uint32_t t, const PTask& tk, const uin
   }
   const int kx = tk.kind_a;
   int kind;
-  if (OP == RMUT_ADD) kind = kx == DK_A ? by_card(c) : kx;
+  if (ADD) kind = kx == DK_A ? by_card(c) : kx;
   else if (OP == RMUT_REMOVE) kind = kx == DK_B ? ((BUF ? c < 4096 : c <= 4096) ? DK_A : DK_B) : kx;
   else kind = kx == DK_R ? eff(c, w_runs(x)) : by_card(c);
   if (kind == DK_B) {  // registers straight to the task's slot
@@ -186,6 +191,7 @@ void launch_rmut(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint
   hipLaunchKernelGGL((k_rmut<O, B>), dim3(std::min(g0, resident_grid((const void*)&k_rmut<O, B>))), dim3(256), 0, s, \
                      tasks, n_tasks, pa, ra, oc, big)
   if (ra.op == RMUT_ADD) RBG_RMUT_LAUNCH(RMUT_ADD, false);
+  else if (ra.op == RMUT_ADD_INPLACE) RBG_RMUT_LAUNCH(RMUT_ADD_INPLACE, false);
   else if (ra.op == RMUT_FLIP) RBG_RMUT_LAUNCH(RMUT_FLIP, false);
   else if (buf) RBG_RMUT_LAUNCH(RMUT_REMOVE, true);
   else RBG_RMUT_LAUNCH(RMUT_REMOVE, false);

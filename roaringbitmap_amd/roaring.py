@@ -148,16 +148,23 @@ class _RangeMut:
     """The static range mutations RoaringBitmap.add / remove / flip(rb, rangeStart, rangeEnd)
     (RB/RoaringBitmap.java:298-345, 995-1040, 626-668) on the class or with three arguments; buffer:
     MutableRoaringBitmap's (RB/buffer/MutableRoaringBitmap.java:152-205, 649-700, 455-505), results of
-    class `cls`.  The instance forms (x.add(start, end) in place) are not on this path."""
+    class `cls`.  With two arguments on an instance of `cls`: x.add / remove / flip(rangeStart, rangeEnd) in
+    place (RB/RoaringBitmap.java:1181-1206, 2656-2710, 1893-1925; RB/buffer/MutableRoaringBitmap.java
+    :831-858, 1489, 1195): the in-place add runs Container.iadd on every key of the range (its own
+    typing, RBG_RMUT_ADD_INPLACE), the in-place remove / flip end in the static forms' containers.  The
+    single-value forms x.add(int) / remove(int) / flip(int) are not on this path."""
 
     def __init__(self, op, buffer=False, cls=None):
         self.op, self.buffer, self.cls = op, buffer, cls
 
-    def static(self, rb, range_start, range_end):
+    def _run(self, op, rb, range_start, range_end):
         b = _lib.rbg_buffer()
-        code = _lib.RMUT_OP[self.op] | (_lib.RBG_RMUT_BUFFER if self.buffer else 0)
+        code = _lib.RMUT_OP[op] | (_lib.RBG_RMUT_BUFFER if self.buffer else 0)
         check(lib().rbg_range_mut(code, rb._buf, len(rb._buf), int(range_start), int(range_end), ctypes.byref(b)))
-        return (self.cls or RoaringBitmap)(take(b))
+        return take(b)
+
+    def static(self, rb, range_start, range_end):
+        return (self.cls or RoaringBitmap)(self._run(self.op, rb, range_start, range_end))
 
     def __get__(self, obj, objtype=None):
         if obj is None:
@@ -166,8 +173,12 @@ class _RangeMut:
         def call(*args):
             if len(args) == 3:
                 return self.static(*args)
-            raise NotImplementedError(f"in-place {self.op}: use the static form {type(obj).__name__}.{self.op}("
-                                      f"rb, rangeStart, rangeEnd)")
+            if len(args) == 2 and isinstance(obj, self.cls or RoaringBitmap):
+                obj._buf = self._run("add_inplace" if self.op == "add" else self.op, obj, *args)
+                obj._lcard = None
+                return None
+            raise NotImplementedError(f"{type(obj).__name__}.{self.op}{args}: the range forms "
+                                      f"{self.op}(rb, rangeStart, rangeEnd) and x.{self.op}(rangeStart, rangeEnd)")
         return call
 
 

@@ -273,7 +273,7 @@ def range_mut(op, buf, start, end, buffer=False) -> bytes:
     RB/RoaringBitmap.java:298, 995, 626); buffer: MutableRoaringBitmap's."""
     p = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
-    code = {"add": 0, "remove": 1, "flip": 2}[op] | (4 if buffer else 0)
+    code = {"add": 0, "remove": 1, "flip": 2, "add_inplace": 3}[op] | (4 if buffer else 0)
     _check(lib().rbo_range_mut(code, buf, len(buf), start, end, ctypes.byref(p), ctypes.byref(n)))
     return _take(p, n)
 

@@ -10,7 +10,7 @@ import pytest
 
 import _gen
 import _oracle as O
-from _fmt import A, B, R, encode
+from _fmt import A, B, R, container_table, encode
 
 pytestmark = pytest.mark.gpu
 
@@ -31,6 +31,14 @@ def _check(buf, st, en, tag=""):
         assert isinstance(gotb, rb.MutableRoaringBitmap)
         assert gotb.serialize() == O.range_mut(op, buf, st, en, buffer=True), f"{tag} buffer {op} [{st}, {en})"
     assert x.serialize() == buf
+    # in place: x.add / remove / flip(rangeStart, rangeEnd) (RB/RoaringBitmap.java:1181, 2656, 1893)
+    for cls, buffer in ((rb.RoaringBitmap, False), (rb.MutableRoaringBitmap, True)):
+        for op in ("add", "remove", "flip"):
+            y = cls(buf)
+            assert getattr(y, op)(st, en) is None
+            want = O.range_mut("add_inplace" if op == "add" else op, buf, st, en, buffer=buffer)
+            assert y.serialize() == want, f"{tag} in-place {cls.__name__}.{op} [{st}, {en})"
+            assert y.getLongCardinality() == int(container_table(want)[2].sum())
 
 
 def _ranges(rng, nkeys):
@@ -70,6 +78,22 @@ def test_buffer_remove_keeps_4096_value_bitmap(gpu):
     assert O.range_mut("remove", x, (1 << 16) + 12288, 2 << 16, buffer=True) != \
         O.range_mut("remove", x, (1 << 16) + 12288, 2 << 16)
     _check(x, (1 << 16) + 12288, 2 << 16, "b4096")
+
+
+def test_in_place_add_between_keys(gpu):
+    """the in-place add's Container.iadd on the keys between the first and last (an array there becomes a
+    full bitmap) against the static add's full run containers"""
+    rb = _rb()
+    x = encode([(0, A, np.arange(5)), (1, A, np.arange(7)), (2, B, np.arange(0, 65536, 2)), (3, R, np.arange(9)),
+                (5, A, [1])])
+    y = rb.RoaringBitmap(x)
+    y.add(3, (5 << 16) + 2)
+    assert y.serialize() == O.range_mut("add_inplace", x, 3, (5 << 16) + 2)
+    assert y.serialize() != rb.RoaringBitmap.add(rb.RoaringBitmap(x), 3, (5 << 16) + 2).serialize()
+    with pytest.raises(NotImplementedError):
+        rb.ImmutableRoaringBitmap(x).flip(3, 9)
+    with pytest.raises(rb.IllegalArgumentException):
+        y.add(-1, 3)
 
 
 def test_immutable_flip_and_errors(gpu):

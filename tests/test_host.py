@@ -253,3 +253,12 @@ def test_mutable_same_object_needs_no_device():
     assert x.isEmpty() and x.serialize() == bytes.fromhex("3a30000000000000")
     with pytest.raises(NotImplementedError):
         x.or_(x)
+
+
+def test_in_place_range_forms_dispatch():
+    """x.add(start, end) in place maps to RBG_RMUT_ADD_INPLACE; single-value forms are refused"""
+    import roaringbitmap_amd as rb
+    import roaringbitmap_amd._lib as L
+    assert L.RMUT_OP["add_inplace"] == 3
+    with pytest.raises(NotImplementedError):
+        rb.RoaringBitmap().add(5)

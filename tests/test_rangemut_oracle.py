@@ -82,3 +82,19 @@ def test_range_sanity_and_empty_range():
         for st, en in ((-1, 5), (0, (1 << 32) + 1)):
             with pytest.raises(O.OracleError):
                 O.range_mut(op, x, st, en)
+
+
+def test_in_place_add_keeps_container_kinds_between():
+    """x.add(rangeStart, rangeEnd) in place (RB/RoaringBitmap.java:1181-1206) runs Container.iadd on every key
+    of the range: an array between the first and last key becomes a full bitmap (toBitmapContainer().iadd),
+    a bitmap a full bitmap, a run container a full run; the static add puts full run containers there"""
+    x = encode([(0, A, np.arange(5)), (1, A, np.arange(7)), (2, B, np.arange(0, 65536, 2)), (3, R, np.arange(9)),
+                (5, A, [1])])
+    got = decode(O.range_mut("add_inplace", x, 3, (5 << 16) + 2))
+    assert [(c[0], c[1], c[2]) for c in got] == [(0, B, 65536), (1, B, 65536), (2, B, 65536), (3, R, 65536),
+                                                 (4, R, 65536), (5, A, 2)]
+    stat = [(c[0], c[1]) for c in decode(O.range_mut("add", x, 3, (5 << 16) + 2))]
+    assert stat == [(0, B), (1, R), (2, R), (3, R), (4, R), (5, A)]
+    assert _set(O.range_mut("add_inplace", x, 3, (5 << 16) + 2)) == _set(O.range_mut("add", x, 3, (5 << 16) + 2))
+    for buffer in (False, True):
+        assert O.range_mut("add_inplace", x, 9, 7, buffer) == x
