@@ -158,6 +158,13 @@ int rbg_ornot(const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, in
  * The in-place remove / flip (:2656, :1893) give the static forms' bytes: use RBG_RMUT_REMOVE / FLIP. */
 enum { RBG_RMUT_ADD = 0, RBG_RMUT_REMOVE = 1, RBG_RMUT_FLIP = 2, RBG_RMUT_ADD_INPLACE = 3, RBG_RMUT_BUFFER = 4 };
 int rbg_range_mut(int op, const uint8_t* a, size_t a_len, int64_t range_start, int64_t range_end, rbg_buffer* out);
+/* RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288; MutableRoaringBitmap.addOffset,
+ * RB/buffer/MutableRoaringBitmap.java:84-142, gives the same bytes): every value plus offset, values
+ * leaving [0, 2^32) dropped.  The container chain's types (Util.addOffset's parts, Container.ior of a
+ * low part into the previous high part, repairAfterLazy).  A whole-key offset clones the containers;
+ * where the reference's (char) cast would wrap keys out of [0, 65535] into an unsorted key list, those
+ * containers are dropped. */
+int rbg_add_offset(const uint8_t* a, size_t a_len, int64_t offset, rbg_buffer* out);
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
 
@@ -338,6 +345,8 @@ int rbg_ctx_pairwise_range(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b
 int rbg_ctx_ornot(rbg_ctx* ctx, int32_t a, size_t ia, int32_t b, size_t ib, int64_t range_end, int flags);
 /* rbg_range_mut over a device-resident single-bitmap batch; the result pending like rbg_ctx_pairwise's */
 int rbg_ctx_range_mut(rbg_ctx* ctx, int op, int32_t batch, size_t i, int64_t range_start, int64_t range_end);
+/* rbg_add_offset over a device-resident single-bitmap batch; the result pending like rbg_ctx_pairwise's */
+int rbg_ctx_add_offset(rbg_ctx* ctx, int32_t batch, size_t i, int64_t offset);
 /* Enqueue a cardinality op; the int32 lands in device memory, read by rbg_ctx_card. */
 int rbg_ctx_pairwise_card(rbg_ctx* ctx, int op, int32_t a, size_t ia, int32_t b, size_t ib);
 /* Enqueue a wide op over every bitmap of a batch, restricted to keys [key_lo, key_hi)

@@ -1767,6 +1767,96 @@ Bitmap op_range_mut(int op, const Bitmap& b, uint64_t start, uint64_t end, bool 
   return ans;
 }
 
+// Util.addOffset(Container, char offsets) (RB/Util.java:32-126; the buffer package's BufferUtil.addOffset,
+// RB/buffer/BufferUtil.java:33-135, is the same): the container's values plus `off`, split at 65536 into
+// the part that stays in the key (lo) and the part that moves to key + 1 (hi), not converted except a
+// bitmap's, through repairAfterLazy.
+static void add_offset_parts(const Ctr& c, int off, Ctr* lo, Ctr* hi) {
+  if (c.kind == ARRAY) {  // addOffsetArray :43-79
+    std::vector<uint16_t> l, h;
+    for (int k = 0; k < c.card; k++) {
+      const int v = c.vals[k] + off;
+      if (v <= 0xFFFF) l.push_back((uint16_t)v);
+      else h.push_back((uint16_t)v);
+    }
+    *lo = make_array(std::move(l));
+    *hi = make_array(std::move(h));
+  } else if (c.kind == BITMAP) {  // addOffsetBitmap :81-105
+    Ctr l = make_bitmap_zero(), h = make_bitmap_zero();
+    l.card = h.card = -1;
+    const int b = off >> 6, i = off % 64;
+    if (i == 0) {
+      for (int k = 0; k < kWords - b; k++) l.words[b + k] = c.words[k];
+      for (int k = kWords - b; k < kWords; k++) h.words[k - (kWords - b)] = c.words[k];
+    } else {
+      l.words[b] = c.words[0] << i;
+      for (int k = 1; k < kWords - b; k++) l.words[b + k] = (c.words[k] << i) | (c.words[k - 1] >> (64 - i));
+      for (int k = kWords - b; k < kWords; k++)
+        h.words[k - (kWords - b)] = (c.words[k] << i) | (c.words[k - 1] >> (64 - i));
+      h.words[b] = c.words[kWords - 1] >> (64 - i);
+    }
+    *lo = repair_after_lazy(l);
+    *hi = repair_after_lazy(h);
+  } else {  // addOffsetRun :107-126
+    RunBuf l(c.nruns()), h(c.nruns());
+    for (int k = 0; k < c.nruns(); k++) {
+      const int val = c.vals[2 * k] + off, len = c.vals[2 * k + 1];
+      const int finalval = val + len;
+      if (val <= 0xFFFF) {
+        if (finalval <= 0xFFFF) {
+          l.smart_append(val, len);
+        } else {
+          l.smart_append(val, 0xFFFF - val);
+          h.smart_append(0, finalval & 0xFFFF);
+        }
+      } else {
+        h.smart_append(val & 0xFFFF, len);
+      }
+    }
+    *lo = l.build();
+    *hi = h.build();
+  }
+}
+
+// RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288; MutableRoaringBitmap.addOffset,
+// RB/buffer/MutableRoaringBitmap.java:84-142, types alike).  A container offset outside [-65536, 65535]:
+// empty.  A whole-key offset clones the containers under the shifted keys; keys that leave [0, 65535]
+// are dropped here, where the reference's (char) cast wraps them into an unsorted key list (an invalid
+// bitmap).  Otherwise each container's two parts go to key and key + 1; a low part whose
+// key is the last one appended is OR-ed into it with Container.ior; then repairAfterLazy over the bitmap.
+Bitmap op_add_offset(const Bitmap& x, int64_t offset) {
+  const int64_t co_l = offset < 0 ? (offset - (1 << 16) + 1) / (1 << 16) : offset / (1 << 16);
+  Bitmap ans;
+  if (co_l < -(1 << 16) || co_l >= (1 << 16)) return ans;
+  const int co = (int)co_l;
+  const int off = (int)(offset - co_l * (1LL << 16));
+  if (off == 0) {
+    for (size_t p = 0; p < x.size(); p++) {
+      const int key = x.keys[p] + co;
+      if (key < 0 || key > 0xFFFF) continue;
+      ans.keys.push_back((uint16_t)key);
+      ans.ctrs.push_back(x.ctrs[p]);
+    }
+    return ans;
+  }
+  for (size_t p = 0; p < x.size(); p++) {
+    const int key = x.keys[p] + co;
+    if (key + 1 < 0 || key > 0xFFFF) continue;
+    Ctr lo, hi;
+    add_offset_parts(x.ctrs[p], off, &lo, &hi);
+    if (!lo.empty() && key >= 0) {
+      if (!ans.keys.empty() && (int)ans.keys.back() == key) ans.ctrs.back() = c_ior(ans.ctrs.back(), lo);
+      else { ans.keys.push_back((uint16_t)key); ans.ctrs.push_back(std::move(lo)); }
+    }
+    if (!hi.empty() && key + 1 <= 0xFFFF) {
+      ans.keys.push_back((uint16_t)(key + 1));
+      ans.ctrs.push_back(std::move(hi));
+    }
+  }
+  for (auto& c : ans.ctrs) c = repair_after_lazy(c);  // RB/RoaringBitmap.java:2752-2757
+  return ans;
+}
+
 // key-bitset intersection shared by workShyAnd / workShyAndCardinality
 static std::vector<uint16_t> common_keys(const std::vector<const Bitmap*>& bms) {
   std::vector<uint64_t> words(1024, 0);

@@ -150,6 +150,8 @@ Ctr c_not_prefix(const Ctr& c, int end);  // Container.not(0, end)
 // static add / remove / flip(rb, rangeStart, rangeEnd): op 0 / 1 / 2 (RB/RoaringBitmap.java:298, 995, 626);
 // buf: MutableRoaringBitmap's (RB/buffer/MutableRoaringBitmap.java:152, 649, 455)
 Bitmap op_range_mut(int op, const Bitmap& b, uint64_t start, uint64_t end, bool buf = false);
+// RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288; MutableRoaringBitmap's :84-142)
+Bitmap op_add_offset(const Bitmap& x, int64_t offset);
 Bitmap fa_horizontal_or(const std::vector<const Bitmap*>& bms);      // FastAggregation.horizontal_or :124-231
 Bitmap fa_horizontal_xor(const std::vector<const Bitmap*>& bms);     // :243-289
 Bitmap fa_priorityqueue_or(const std::vector<const Bitmap*>& bms);   // :733-781

@@ -176,6 +176,14 @@ int rbo_range_mut(int op, const uint8_t* a, size_t an, int64_t start, int64_t en
   return emit(op_range_mut(op & 3, x, (uint64_t)start, (uint64_t)end, (op & 4) != 0), out, out_len);
 }
 
+// RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288)
+int rbo_add_offset(const uint8_t* a, size_t an, int64_t offset, uint8_t** out, size_t* out_len) {
+  Bitmap x;
+  int st = load(a, an, &x);
+  if (st) return st;
+  return emit(op_add_offset(x, offset), out, out_len);
+}
+
 // RoaringBitmap.getLongSizeInBytes of a serialized bitmap (RB/RoaringBitmap.java:2212-2219)
 int64_t rbo_long_size(const uint8_t* a, size_t an) {
   Bitmap b;

@@ -15,7 +15,7 @@ LIB = os.path.join(LIBDIR, "libroaring_mi355x.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "pairwise.hip", "wide.hip", "pq.hip", "synth.hip", "bsi.hip", "runopt.hip", "ornot.hip", "rangemut.hip", "decode.hip", "engine.cpp", "format.cpp"]
+SOURCES = ["kernels.hip", "pairwise.hip", "wide.hip", "pq.hip", "synth.hip", "bsi.hip", "runopt.hip", "ornot.hip", "rangemut.hip", "addoffset.hip", "decode.hip", "engine.cpp", "format.cpp"]
 HEADERS = ["device.hpp", "kernels.hpp", "format.hpp", "wave.hpp", "vb.hpp"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-result"]

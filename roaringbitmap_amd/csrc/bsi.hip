@@ -1242,7 +1242,7 @@ __device__ __forceinline__ void pair_buf_task(uint32_t t, const PTask& tk, const
 constexpr int kPbWaves = 4;
 
 template <int OP>
-__global__ __launch_bounds__(256) void k_pair_buf(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+__global__ __launch_bounds__(256, 4) void k_pair_buf(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                                   const uint8_t* pa, const uint8_t* pb, OutCtx oc, BigRuns big) {
   __shared__ __align__(16) uint32_t lds_all[kPbWaves][2048];
   const int w = threadIdx.x >> 6;

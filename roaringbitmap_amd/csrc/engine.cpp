@@ -1054,6 +1054,37 @@ static int ctx_range_mut(Ctx* c, int op, int32_t ia, size_t ma, int64_t start, i
   }
 }
 
+// RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288; MutableRoaringBitmap.addOffset,
+// RB/buffer/MutableRoaringBitmap.java:84-142, the same bytes), addoffset.hip.  The container offset is
+// the floor of offset / 65536 (:233-234); outside [-65536, 65535] the result is empty (:235-237).
+static int ctx_add_offset(Ctx* c, int32_t ia, size_t ma, int64_t offset) {
+  Batch* A;
+  CHK(get_batch(c, ia, &A));
+  const uint16_t* ka;
+  const CDesc* da;
+  int na;
+  CHK(operand(A, ma, &ka, &da, &na));
+  const int64_t co = offset < 0 ? (offset - 65535) / 65536 : offset / 65536;
+  AoffArgs aa{0, 0, 1};
+  if (co >= -65536 && co < 65536) aa = AoffArgs{(int)co, (int)(offset - co * 65536), 0};
+  // each input container gives at most two output containers, each staged (<= 8194 B) or a clone
+  const size_t ub = std::max<size_t>(1, std::min<size_t>(kMaxKeys, 2 * (size_t)na));
+  hipStream_t s = c->stream;
+  OutCtx oc;
+  CHK(prepare_output(c, ub, A->payload_bytes + (size_t)8194 * ub, &oc, false));
+  c->pending_src = {ia};
+  c->mark(0);
+  c->mark(1);
+  launch_aoff(s, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), aa, c->wg_epoch.as<uint64_t>(),
+              next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->zlb, c->ztile,
+              grid_for(ub, 65536));
+  c->mark(2);
+  defer_place(c);
+  c->mark(3);
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
+
 static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_t mb, bool card_only, int key_lo = 0,
                         int key_hi = kMaxKeys, int pipe_k = 0) {
   if (op == RBG_AND_BUFFER || op == RBG_ANDNOT_BUFFER) {
@@ -2275,6 +2306,24 @@ int rbg_ctx_range_mut(rbg_ctx* ctx, int op, int32_t batch, size_t i, int64_t ran
     return RBG_ERR_ILLEGAL_ARGUMENT;
   CHK(enter(&ctx->c));
   return ctx_range_mut(&ctx->c, op & 3, batch, i, range_start, range_end, (op & RBG_RMUT_BUFFER) != 0);
+}
+
+int rbg_add_offset(const uint8_t* a, size_t a_len, int64_t offset, rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(ctx_load_separate(c, &a, &a_len, 1, &id));
+  g.ids = {id};
+  CHK(ctx_add_offset(c, id, 0, offset));
+  return ctx_fetch(c, out);
+}
+
+int rbg_ctx_add_offset(rbg_ctx* ctx, int32_t batch, size_t i, int64_t offset) {
+  if (!ctx) return RBG_ERR_ILLEGAL_ARGUMENT;
+  CHK(enter(&ctx->c));
+  return ctx_add_offset(&ctx->c, batch, i, offset);
 }
 
 int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int32_t* out) {

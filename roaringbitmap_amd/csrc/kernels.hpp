@@ -373,6 +373,14 @@ enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2, RMUT_ADD_INPLA
 struct RmutArgs {
   int op, hbs, lbs, hbl, lbl;
 };
+// RoaringBitmap.addOffset (RB/RoaringBitmap.java:230-288), addoffset.hip: offset = 65536 co + off, off in
+// [0, 65535]; none: a container offset outside [-65536, 65535] (an empty result)
+struct AoffArgs {
+  int co, off, none;
+};
+void launch_aoff(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint8_t* pa, AoffArgs aa,
+                 uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint64_t* zlb,
+                 uint64_t* ztile, int grid);
 void launch_rmut(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint8_t* pa, RmutArgs ra, bool buf,
                  uint64_t* wg_epoch, uint32_t epoch, PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint64_t* zlb,
                  uint64_t* ztile, BigRuns big, int grid);

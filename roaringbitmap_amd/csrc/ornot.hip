@@ -243,7 +243,7 @@ constexpr int kOrnWaves = 4;
 // MutableRoaringBitmap.orNot (RB/buffer/ImmutableRoaringBitmap.java:484-548, MutableRoaringBitmap.java
 // :962-1030).  Static wave stride over the task list; the next record is fetched while a task runs.
 template <bool INPLACE, bool BUF>
-__global__ __launch_bounds__(256) void k_ornot(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+__global__ __launch_bounds__(256, 3) void k_ornot(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                                const uint8_t* pa, const uint8_t* pb, int max_key, int last_run,
                                                OutCtx oc) {
   __shared__ __align__(16) uint32_t lds_all[kOrnWaves][2048];

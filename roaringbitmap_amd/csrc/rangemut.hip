@@ -72,17 +72,6 @@ __global__ __launch_bounds__(256) void k_plan_rmut(const uint32_t* __restrict__ 
   plan_emit(f, t, wg_epoch, epoch, tasks, n_tasks, err);
 }
 
-// bits [lo, hi] of register k of the wave layout (WCtr: w[2 i + j] = word 128 i + 2 lane + j)
-__device__ __forceinline__ uint64_t wrange(int k, int lo, int hi) {
-  const int w = 128 * (k >> 1) + 2 * lane_id() + (k & 1);
-  const int b0 = 64 * w, b1 = b0 + 63;
-  if (b1 < lo || b0 > hi) return 0ull;
-  uint64_t m = ~0ull;
-  if (lo > b0) m &= ~0ull << (lo - b0);
-  if (hi < b1) m &= ~0ull >> (b1 - hi);
-  return m;
-}
-
 template <int OP, bool BUF>
 __device__ __forceinline__ void rmut_task(uint32_t t, const PTask& tk, const uint8_t* pa, const RmutArgs& ra,
                                           const OutCtx& oc, const BigRuns& big, uint32_t* lds) {
@@ -160,7 +149,7 @@ constexpr int kRmWaves = 4;
 
 // one wave per task over a static stride, the next record fetched while a task runs
 template <int OP, bool BUF>
-__global__ __launch_bounds__(256) void k_rmut(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+__global__ __launch_bounds__(256, 4) void k_rmut(const PTask* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                               const uint8_t* pa, RmutArgs ra, OutCtx oc, BigRuns big) {
   __shared__ __align__(16) uint32_t lds_all[kRmWaves][2048];
   const int w = threadIdx.x >> 6;

@@ -93,6 +93,17 @@ __device__ __forceinline__ void w_load_bitmap(const uint8_t* p, WCtr& x) {
     x.w[2 * i + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
   }
 }
+// bits [lo, hi] of register k of the wave layout (WCtr: w[2 i + j] = word 128 i + 2 lane + j)
+__device__ __forceinline__ uint64_t wrange(int k, int lo, int hi) {
+  const int w = 128 * (k >> 1) + 2 * lane_id() + (k & 1);
+  const int b0 = 64 * w, b1 = b0 + 63;
+  if (b1 < lo || b0 > hi) return 0ull;
+  uint64_t m = ~0ull;
+  if (lo > b0) m &= ~0ull << (lo - b0);
+  if (hi < b1) m &= ~0ull >> (b1 - hi);
+  return m;
+}
+
 // LDS bitmap (u32[2048]) <-> registers
 __device__ __forceinline__ void w_read_lds(const uint32_t* lds, WCtr& x) {
   const uint4* q = reinterpret_cast<const uint4*>(lds) + lane_id();

@@ -131,6 +131,11 @@ class Engine:
         code = _lib.RMUT_OP[op] | (_lib.RBG_RMUT_BUFFER if buffer else 0)
         check(lib().rbg_ctx_range_mut(self._ctx, code, int(a), int(ia), int(range_start), int(range_end)))
 
+    def add_offset(self, a, offset, ia=0):
+        """RoaringBitmap.addOffset(x, offset) of a resident bitmap; the result pending like pairwise's
+        (rbg_ctx_add_offset)."""
+        check(lib().rbg_ctx_add_offset(self._ctx, int(a), int(ia), int(offset)))
+
     def pairwise_serialized(self, op, a, b, ia=0, ib=0):
         """pairwise(op) + serialize() as one pipeline (rbg_ctx_pairwise_serialized): the result's
         placement and payload copies for one key range overlap the next range's compute."""

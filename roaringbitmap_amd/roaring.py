@@ -319,6 +319,16 @@ class RoaringBitmap:
     remove = _RangeMut("remove")
     flip = _RangeMut("flip")
 
+    @classmethod
+    def addOffset(cls, x, offset):
+        """RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288): every value plus `offset`
+        (a long in [-2^32, 2^32]; values leaving [0, 2^32) dropped).  The buffer package's
+        MutableRoaringBitmap.addOffset(ImmutableRoaringBitmap, long) (RB/buffer/MutableRoaringBitmap.java
+        :84-142) gives the same bytes, as a MutableRoaringBitmap."""
+        b = _lib.rbg_buffer()
+        check(lib().rbg_add_offset(x._buf, len(x._buf), int(offset), ctypes.byref(b)))
+        return cls(take(b))
+
     def _inplace(self, op, x2):
         """x1.and / or / xor / andNot(x2) in place (rbg_pairwise_inplace); x2 may be x1 itself"""
         if x2 is self and op in ("and", "or"):
@@ -791,6 +801,7 @@ class ImmutableRoaringBitmap(RoaringBitmap):
     or_ = _s_or
     xor = _s_xor
     add = remove = None  # no static add / remove on ImmutableRoaringBitmap (MutableRoaringBitmap's: below)
+    addOffset = None  # MutableRoaringBitmap.addOffset(ImmutableRoaringBitmap, long): below
     andCardinality = RoaringBitmap.__dict__["andCardinality"]  # :336-359, a set-level count
     intersects = RoaringBitmap.__dict__["intersects"]
 
@@ -810,6 +821,7 @@ class MutableRoaringBitmap(ImmutableRoaringBitmap):
     or_ = _StaticOrInPlace(ImmutableRoaringBitmap._s_or, "or")
     xor = _StaticOrInPlace(ImmutableRoaringBitmap._s_xor, "xor")
     orNot = _OrNot(ImmutableRoaringBitmap.__dict__["orNot"].__func__, buffer=True)  # x1.orNot in place :962-1030
+    addOffset = RoaringBitmap.__dict__["addOffset"]  # RB/buffer/MutableRoaringBitmap.java:84-142, the same bytes
 
     def _inplace(self, op, x2):
         if op not in ("and_buffer", "andnot_buffer"):

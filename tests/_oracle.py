@@ -78,6 +78,8 @@ def lib():
                                 ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_range_mut.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int64,
                                     ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_add_offset.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.POINTER(u8p),
+                                     ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -275,6 +277,14 @@ def range_mut(op, buf, start, end, buffer=False) -> bytes:
     n = ctypes.c_size_t()
     code = {"add": 0, "remove": 1, "flip": 2, "add_inplace": 3}[op] | (4 if buffer else 0)
     _check(lib().rbo_range_mut(code, buf, len(buf), start, end, ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
+
+
+def add_offset(buf, offset) -> bytes:
+    """RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288; MutableRoaringBitmap's alike)."""
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_add_offset(buf, len(buf), int(offset), ctypes.byref(p), ctypes.byref(n)))
     return _take(p, n)
 
 

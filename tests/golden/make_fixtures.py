@@ -16,6 +16,9 @@ Inputs (data files the reference's tests hold; no reference source is copied):
   * RoaringBitmap/src/test/resources/testdata/ornot-fuzz-failure.json (the two base64 bitmaps of
     RBT/TestRoaringBitmapOrNot.java:376-424 testBigOrNot / testBigOrNotStatic)
     -> tests/golden/testdata/ornot_fuzz_{l,r}.bin.gz, the decoded serialized bytes, gzipped
+  * RoaringBitmap/src/test/resources/testdata/{testIssue260,offset_failure_case_1..3}.txt (the
+    comma-separated value lists of RBT/TestConcatenation.java:32-37, addOffset's cases)
+    -> tests/golden/testdata/addoffset_<name>.u32.gz, the values as little-endian uint32, gzipped
   * The known-answer constants of jmh/src/test/java/org/roaringbitmap/realdata/
     RealDataBenchmark{Or,And,AndNot,Xor,WideOrNaive,WideAndNaive}Test.java are
     transcribed (as numbers) into known_answers.json.
@@ -74,6 +77,12 @@ def main():
     for tag, b in zip("lr", bms[:2]):
         with gzip.GzipFile(os.path.join(td, f"ornot_fuzz_{tag}.bin.gz"), "wb", mtime=0) as g:
             g.write(base64.b64decode(b))
+
+    for n in ("testIssue260", "offset_failure_case_1", "offset_failure_case_2", "offset_failure_case_3"):
+        with open(os.path.join(TESTDATA_SRC, n + ".txt")) as f:
+            vals = np.array([int(x) for x in f.readline().strip().split(",")], dtype="<u4")
+        with gzip.GzipFile(os.path.join(td, f"addoffset_{n}.u32.gz"), "wb", mtime=0) as g:
+            g.write(vals.tobytes())
 
     rd = os.path.join(HERE, "realdata")
     os.makedirs(rd, exist_ok=True)

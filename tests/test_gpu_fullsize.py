@@ -105,7 +105,7 @@ def test_c2_full_pair(eng, c2, variant, op):
 def test_c2_widened_ops(eng, c2, variant):
     """The round-5 rows at the C2 size, byte-exact against the oracle on the fetched operands:
     orNot over the whole universe and mid-key (static and in place, heap and buffer), the buffer
-    package's and / andNot, and the static flip / add / remove over ranges that cut keys."""
+    package's and / andNot, the static flip / add / remove over ranges that cut keys, and addOffset."""
     x, y, xa, xb = c2[variant]
     for end, flags in (((1 << 32), 0), ((40000 << 16) + 123, 0), ((1 << 32), 1), ((40000 << 16) + 123, 3)):
         eng.ornot(x, y, end, inplace=bool(flags & 1), buffer=bool(flags & 2))
@@ -118,6 +118,9 @@ def test_c2_widened_ops(eng, c2, variant):
                        ("add", (100 << 16) + 5, (60000 << 16) + 7), ("remove", (100 << 16) + 5, (60000 << 16) + 7)):
         eng.range_mut(op, x, st, en)
         _same(eng.fetch().serialize(), O.range_mut(op, xa, st, en), f"C2 {variant} {op} [{st}, {en})")
+    for off in (12345, -(7 << 16) - 99, 3 << 16):
+        eng.add_offset(x, off)
+        _same(eng.fetch().serialize(), O.add_offset(xa, off), f"C2 {variant} addOffset {off}")
 
 
 @pytest.mark.parametrize("variant", ["raw", "runopt"])
