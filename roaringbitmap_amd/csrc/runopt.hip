@@ -193,7 +193,7 @@ __device__ __forceinline__ int array_runs(const uint8_t* slot, int card) {
 // bitmap, stored from them (read once).  Per workgroup g, wstat[4 g + k] = its containers of kind k
 // (k < 3) and their serialized payload bytes (k = 3): plain stores, nothing to zero first; the batch's
 // totals and run flags are derived only when the host asks (k_runopt_flags, ensure_stats).
-__global__ __launch_bounds__(256) void k_runopt(const CDesc* __restrict__ desc, const uint8_t* __restrict__ payload,
+__global__ __launch_bounds__(256, 4) void k_runopt(const CDesc* __restrict__ desc, const uint8_t* __restrict__ payload,
                                                 uint64_t n, CDesc* __restrict__ out_desc,
                                                 uint8_t* __restrict__ out_payload, RoCopy cp,
                                                 unsigned long long* __restrict__ wstat) {
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256) void k_rsel_plan(const CDesc* __restrict__ des
 }
 
 // kept container i -> index idx[i], slot at off[i] of the new batch
-__global__ __launch_bounds__(256) void k_rsel_write(const CDesc* __restrict__ desc, const uint32_t* __restrict__ bm,
+__global__ __launch_bounds__(256, 4) void k_rsel_write(const CDesc* __restrict__ desc, const uint32_t* __restrict__ bm,
                                                     const uint8_t* __restrict__ payload, uint64_t n, RselArgs ra,
                                                     const uint32_t* __restrict__ info,
                                                     const uint32_t* __restrict__ ncard,

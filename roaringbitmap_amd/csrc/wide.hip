@@ -144,7 +144,7 @@ __device__ __forceinline__ int block_card(const uint64_t r[4], int* sh) {
 //   naive_xor (:637-644): ixor chain with restart after an empty result
 //             (RB/RoaringBitmap.java:3296-3348)
 template <int MODE>
-__global__ __launch_bounds__(256) void k_wide(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+__global__ __launch_bounds__(256, 4) void k_wide(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                               WideArgs A, OutCtx oc, uint32_t* __restrict__ task_card) {
   __shared__ __align__(16) uint32_t acc[2048];
   __shared__ __align__(16) uint32_t tmp[2048];
@@ -652,7 +652,7 @@ __device__ __forceinline__ CDesc load_desc(const CDesc* desc, uint32_t i) {
 }
 
 template <int MODE>  // WIDE_AND_SHY or WIDE_AND_SHY_CARD
-__global__ __launch_bounds__(256) void k_shy_wave(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
+__global__ __launch_bounds__(256, 4) void k_shy_wave(const Task* __restrict__ tasks, const uint32_t* __restrict__ n_tasks,
                                                   WideArgs A, OutCtx oc, uint32_t* __restrict__ task_card) {
   __shared__ __align__(16) uint32_t lds_all[4][2048];
   const int w = threadIdx.x >> 6, l = lane_id();
