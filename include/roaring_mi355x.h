@@ -65,8 +65,11 @@ typedef struct rbg_buffer {
 enum { RBG_AND = 0, RBG_OR = 1, RBG_XOR = 2, RBG_ANDNOT = 3, RBG_OR_INPLACE = 4, RBG_AND_BUFFER = 5,
        RBG_ANDNOT_BUFFER = 6 };
 /* cardinality ops: andCardinality :413, orCardinality :916, xorCardinality :931,
- * andNotCardinality :944 (all Java int, wrapping mod 2^32), intersects :698 (0/1) */
-enum { RBG_CARD_AND = 0, RBG_CARD_OR = 1, RBG_CARD_XOR = 2, RBG_CARD_ANDNOT = 3, RBG_INTERSECTS = 4 };
+ * andNotCardinality :944 (all Java int, wrapping mod 2^32), intersects :698 (0/1);
+ * RBG_CONTAINS: a.contains(b), b a subset of a (RB/RoaringBitmap.java:2781-2802; ImmutableRoaringBitmap
+ * :1242), 0/1, from the 64-bit and-cardinality (|a AND b| == |b|) */
+enum { RBG_CARD_AND = 0, RBG_CARD_OR = 1, RBG_CARD_XOR = 2, RBG_CARD_ANDNOT = 3, RBG_INTERSECTS = 4,
+       RBG_CONTAINS = 5 };
 /* wide ops, RB/FastAggregation.java:
  *   RBG_WIDE_AND      and(RoaringBitmap...)  :37-42  (N>10 workShyAnd, else naive_and)
  *   RBG_WIDE_OR       or(RoaringBitmap...)   :664-666 (naive_or); also RoaringBitmap.or(...) :844

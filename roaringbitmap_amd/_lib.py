@@ -19,7 +19,7 @@ RBG_ERR_OUT_OF_MEMORY = -5
 
 OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "ior": 4,  # ior: x1.or(x2) in place (Container.ior types)
       "and_buffer": 5, "andnot_buffer": 6}  # the buffer package's and / andNot (ImmutableRoaringBitmap)
-CARD_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4}
+CARD_OP = {"and": 0, "or": 1, "xor": 2, "andnot": 3, "intersects": 4, "contains": 5}
 WIDE_OP = {"and": 0, "or": 1, "xor": 2, "and_iter": 3, "naive_and": 4, "workshy_and": 5, "parallel_or": 6,
            "parallel_xor": 7, "buffer_or_mutable": 8, "horizontal_or": 9, "horizontal_xor": 10,
            "priorityqueue_or": 11, "priorityqueue_xor": 12, "buffer_and": 13, "buffer_naive_and": 14,

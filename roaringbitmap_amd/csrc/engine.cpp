@@ -2327,7 +2327,7 @@ int rbg_ctx_add_offset(rbg_ctx* ctx, int32_t batch, size_t i, int64_t offset) {
 }
 
 int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, size_t b_len, int32_t* out) {
-  if (!out || op < 0 || op > 4) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (!out || op < 0 || op > RBG_CONTAINS) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
@@ -2347,6 +2347,9 @@ int rbg_pairwise_card(int op, const uint8_t* a, size_t a_len, const uint8_t* b, 
     case RBG_CARD_OR: *out = (int32_t)(ca + cb - ac); break;         // RB/RoaringBitmap.java:916-920
     case RBG_CARD_XOR: *out = (int32_t)(ca + cb - 2u * ac); break;   // :931-933
     case RBG_CARD_ANDNOT: *out = (int32_t)(ca - ac); break;          // :944-985 (both branches, mod 2^32)
+    case RBG_CONTAINS:  // b is a subset of a (:2781-2802): every value of b in a AND b, counted in 64 bits
+      *out = ri.long_card == c->batches[ib]->long_card ? 1 : 0;
+      break;
     default: *out = ri.any ? 1 : 0; break;                           // intersects :698-720
   }
   return RBG_OK;

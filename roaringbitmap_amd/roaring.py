@@ -264,7 +264,10 @@ class RoaringBitmap:
         """RoaringBitmap.contains(int) (RB/RoaringBitmap.java:1693-1701): the key's container through
         a binary search of the descriptor table (RoaringArray.getContainer), then the container's own
         contains (ArrayContainer binary search, BitmapContainer bit test, RunContainer binary search
-        of the run starts), read straight from the serialized bytes."""
+        of the run starts), read straight from the serialized bytes.  With a bitmap: contains(subset)
+        (:2781-2802; ImmutableRoaringBitmap.contains :1242), on the GPU (rbg_pairwise_card RBG_CONTAINS)."""
+        if isinstance(x, RoaringBitmap):
+            return RoaringBitmap._card("contains", self, x) != 0
         x = int(x) & 0xFFFFFFFF
         key, low = x >> 16, x & 0xFFFF
         ctr = _find_container(self._buf, key)

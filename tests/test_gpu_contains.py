@@ -1,0 +1,67 @@
+"""RoaringBitmap.contains(RoaringBitmap subset) (RB/RoaringBitmap.java:2781-2802; ImmutableRoaringBitmap
+.contains(ImmutableRoaringBitmap), RB/buffer/ImmutableRoaringBitmap.java:1242) on the MI355X
+(rbg_pairwise_card RBG_CONTAINS: |a AND b| == |b| in 64 bits) against set inclusion of the decoded values
+(the reference walks both key lists and asks Container.contains(Container), a set test; its advanceUntil
+call on the subset's key array only ever advances pos1 by one)."""
+import numpy as np
+import pytest
+
+import _gen
+import _oracle as O
+from _fmt import A, B, R, encode
+
+pytestmark = pytest.mark.gpu
+
+
+def _sub(buf_a, buf_b):
+    a = O.to_values(buf_a)
+    b = O.to_values(buf_b)
+    return bool(np.isin(b, a).all())
+
+
+def _check(buf_a, buf_b, tag=""):
+    import roaringbitmap_amd as rb
+    want = _sub(buf_a, buf_b)
+    assert rb.RoaringBitmap(buf_a).contains(rb.RoaringBitmap(buf_b)) == want, tag
+    assert rb.ImmutableRoaringBitmap(buf_a).contains(rb.ImmutableRoaringBitmap(buf_b)) == want, tag
+    return want
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_subsets(gpu, seed):
+    rng = np.random.default_rng(1300 + seed)
+    a = _gen.bitmap(rng, np.arange(8), p_present=0.9)
+    va = O.to_values(a)
+    seen = set()
+    for frac in (0.0, 0.01, 0.5, 1.0):
+        sub = va[rng.random(va.size) < frac] if frac < 1 else va
+        b = O.from_values(sub)
+        seen.add(_check(a, b, f"subset {frac}"))
+        seen.add(_check(a, O.run_optimize(b), f"subset {frac} runopt"))
+        if sub.size:  # one value not in a: a missing value inside a present key, and one in a new key
+            miss = np.setdiff1d(np.arange(int(sub[0]), int(sub[0]) + 70000, dtype=np.uint32), va)[:1]
+            seen.add(_check(a, O.from_values(np.union1d(sub, miss)), f"subset {frac} + {miss}"))
+            seen.add(_check(a, O.from_values(np.union1d(sub, [0xFFFFFFF0])), f"subset {frac} + new key"))
+    assert seen == {True, False}
+
+
+def test_container_kinds_and_edges(gpu):
+    full = encode([(k, R, np.arange(65536)) for k in (0, 1, 2)])
+    for kind_sub in (A, B, R):
+        vals = np.arange(0, 65536, 3) if kind_sub != A else np.arange(0, 9000, 3)
+        assert _check(full, encode([(1, kind_sub, vals)]))
+        assert not _check(encode([(1, B, np.arange(1, 65536, 3))]), encode([(1, kind_sub, vals)]))
+    empty = O.from_values(np.zeros(0, dtype=np.uint32))
+    assert _check(full, empty) and _check(empty, empty)
+    assert not _check(empty, full)
+
+
+def test_full_universe(gpu):
+    """2^32 values: an int andNot-cardinality would wrap to 0 here; the 64-bit count does not"""
+    import roaringbitmap_amd as rb
+    univ = rb.RoaringBitmap.add(rb.RoaringBitmap(), 0, 1 << 32)
+    empty = rb.RoaringBitmap()
+    assert univ.contains(univ) and univ.contains(empty)
+    assert not empty.contains(univ)
+    holed = rb.RoaringBitmap.remove(univ, 123456, 123457)
+    assert univ.contains(holed) and not holed.contains(univ)

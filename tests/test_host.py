@@ -262,3 +262,8 @@ def test_in_place_range_forms_dispatch():
     assert L.RMUT_OP["add_inplace"] == 3
     with pytest.raises(NotImplementedError):
         rb.RoaringBitmap().add(5)
+
+
+def test_contains_subset_op_code():
+    import roaringbitmap_amd._lib as L
+    assert L.CARD_OP["contains"] == 5
