@@ -283,6 +283,20 @@ class RoaringBitmap:
         i = int(np.searchsorted(starts, low, side="right")) - 1
         return i >= 0 and low <= int(starts[i]) + int(pay[2 * i + 1])
 
+    def isHammingSimilar(self, other, tolerance) -> bool:
+        """RoaringBitmap.isHammingSimilar(other, tolerance) (RB/RoaringBitmap.java:1831-1863): the budget
+        walk ends true iff |self XOR other| <= tolerance (tolerance < 0: false).  The XOR count is
+        |self| + |other| - 2 |self AND other| from the GPU's and-cardinality, in 64 bits (the int
+        and-cardinality wraps only when both bitmaps hold all 2^32 values)."""
+        tolerance = int(tolerance)
+        if tolerance < 0:
+            return False
+        ca, cb = self.getLongCardinality(), other.getLongCardinality()
+        a = RoaringBitmap._card("and", self, other) & 0xFFFFFFFF
+        if a == 0 and ca == cb == 1 << 32:
+            a = 1 << 32
+        return ca + cb - 2 * a <= tolerance
+
     def __contains__(self, x):
         return self.contains(x)
 

@@ -65,3 +65,22 @@ def test_full_universe(gpu):
     assert not empty.contains(univ)
     holed = rb.RoaringBitmap.remove(univ, 123456, 123457)
     assert univ.contains(holed) and not holed.contains(univ)
+
+
+def test_is_hamming_similar(gpu):
+    """RB/RoaringBitmap.java:1831-1863: true iff the XOR cardinality is within the tolerance"""
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(77)
+    a = _gen.bitmap(rng, np.arange(6), p_present=0.9)
+    va = O.to_values(a)
+    flip = va[rng.random(va.size) < 0.001]
+    extra = np.array([0xFFFF0000, 0xFFFF0001, 5], dtype=np.uint32)
+    b = O.from_values(np.setxor1d(np.setdiff1d(va, flip), extra))
+    d = len(np.setxor1d(va, O.to_values(b)))
+    x, y = rb.RoaringBitmap(a), rb.RoaringBitmap(b)
+    assert x.isHammingSimilar(y, d) and y.isHammingSimilar(x, d + 5)
+    assert not x.isHammingSimilar(y, d - 1)
+    assert x.isHammingSimilar(x, 0) and not x.isHammingSimilar(x, -1)
+    univ = rb.RoaringBitmap.add(rb.RoaringBitmap(), 0, 1 << 32)
+    assert univ.isHammingSimilar(univ, 0)
+    assert not univ.isHammingSimilar(rb.RoaringBitmap(), 2 ** 31 - 1)
