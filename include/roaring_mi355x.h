@@ -168,6 +168,14 @@ int rbg_range_mut(int op, const uint8_t* a, size_t a_len, int64_t range_start, i
  * where the reference's (char) cast would wrap keys out of [0, 65535] into an unsorted key list, those
  * containers are dropped. */
 int rbg_add_offset(const uint8_t* a, size_t a_len, int64_t offset, rbg_buffer* out);
+/* x.selectRange(rangeStart, rangeEnd) (RB/RoaringBitmap.java:3095-3147): the values in the range, the
+ * first / last key's container cut by Container.remove (A stays A, B becomes A at <= 4096 values, R stays
+ * R with its runs clipped), the keys between cloned; buffer != 0: ImmutableRoaringBitmap.selectRange
+ * (RB/buffer/ImmutableRoaringBitmap.java:701-757), whose bitmaps become arrays below 4096 values.  The
+ * reference only asserts the range; here rangeSanityCheck's bounds apply (RBG_ERR_ILLEGAL_ARGUMENT).
+ * rangeEnd <= rangeStart: the empty bitmap. */
+int rbg_select_range(const uint8_t* a, size_t a_len, int64_t range_start, int64_t range_end, int buffer,
+                     rbg_buffer* out);
 /* wide cardinalities: andCardinality(RoaringBitmap...) :71-82, orCardinality :90-101 */
 enum { RBG_WIDE_CARD_AND = 0, RBG_WIDE_CARD_OR = 1 };
 

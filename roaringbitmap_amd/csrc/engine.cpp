@@ -2430,6 +2430,20 @@ int rbg_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t 
   return ctx_fetch(c, out);
 }
 
+int rbg_select_range(const uint8_t* a, size_t a_len, int64_t range_start, int64_t range_end, int buffer,
+                     rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id, sel;
+  CHK(ctx_load_separate(c, &a, &a_len, 1, &id));
+  g.ids = {id};
+  CHK(ctx_select_range(c, id, range_start, range_end, &sel, buffer != 0));
+  g.ids.push_back(sel);
+  return ctx_batch_fetch(c, sel, 0, out);
+}
+
 int rbg_ctx_select_range(rbg_ctx* ctx, int32_t batch, int64_t range_start, int64_t range_end, int32_t* out_batch) {
   if (!ctx || !out_batch) return RBG_ERR_ILLEGAL_ARGUMENT;
   CHK(enter(&ctx->c));

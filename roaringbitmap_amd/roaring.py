@@ -283,6 +283,17 @@ class RoaringBitmap:
         i = int(np.searchsorted(starts, low, side="right")) - 1
         return i >= 0 and low <= int(starts[i]) + int(pay[2 * i + 1])
 
+    def selectRange(self, range_start, range_end):
+        """x.selectRange(rangeStart, rangeEnd) (RB/RoaringBitmap.java:3095-3147) on the GPU: the values in
+        [rangeStart, rangeEnd), the cut keys through Container.remove.  ImmutableRoaringBitmap.selectRange
+        (RB/buffer/ImmutableRoaringBitmap.java:701-757) keeps the buffer package's types and returns a
+        MutableRoaringBitmap."""
+        buffer = isinstance(self, ImmutableRoaringBitmap)
+        b = _lib.rbg_buffer()
+        check(lib().rbg_select_range(self._buf, len(self._buf), int(range_start), int(range_end), int(buffer),
+                                     ctypes.byref(b)))
+        return (MutableRoaringBitmap if buffer else RoaringBitmap)(take(b))
+
     def isHammingSimilar(self, other, tolerance) -> bool:
         """RoaringBitmap.isHammingSimilar(other, tolerance) (RB/RoaringBitmap.java:1831-1863): the budget
         walk ends true iff |self XOR other| <= tolerance (tolerance < 0: false).  The XOR count is
