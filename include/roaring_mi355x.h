@@ -168,6 +168,10 @@ int rbg_range_mut(int op, const uint8_t* a, size_t a_len, int64_t range_start, i
  * where the reference's (char) cast would wrap keys out of [0, 65535] into an unsorted key list, those
  * containers are dropped. */
 int rbg_add_offset(const uint8_t* a, size_t a_len, int64_t offset, rbg_buffer* out);
+/* x.removeRunCompression() (RB/RoaringBitmap.java:2738-2749; MutableRoaringBitmap's alike): out = x's
+ * bytes afterwards, every run container as an array (<= 4096 values) or a bitmap
+ * (RunContainer.toBitmapOrArrayContainer, RB/RunContainer.java:2300-2323), the rest unchanged */
+int rbg_remove_run_compression(const uint8_t* a, size_t a_len, rbg_buffer* out);
 /* x.selectRange(rangeStart, rangeEnd) (RB/RoaringBitmap.java:3095-3147): the values in the range, the
  * first / last key's container cut by Container.remove (A stays A, B becomes A at <= 4096 values, R stays
  * R with its runs clipped), the keys between cloned; buffer != 0: ImmutableRoaringBitmap.selectRange

@@ -1857,6 +1857,15 @@ Bitmap op_add_offset(const Bitmap& x, int64_t offset) {
   return ans;
 }
 
+// x.removeRunCompression() (RB/RoaringBitmap.java:2738-2749): every run container through
+// toBitmapOrArrayContainer(getCardinality()) (RB/RunContainer.java:2300-2323)
+Bitmap op_remove_run_compression(const Bitmap& x) {
+  Bitmap ans = x;
+  for (auto& c : ans.ctrs)
+    if (c.kind == RUN) c = to_bitmap_or_array(c, c.cardinality());
+  return ans;
+}
+
 // key-bitset intersection shared by workShyAnd / workShyAndCardinality
 static std::vector<uint16_t> common_keys(const std::vector<const Bitmap*>& bms) {
   std::vector<uint64_t> words(1024, 0);

@@ -184,6 +184,14 @@ int rbo_add_offset(const uint8_t* a, size_t an, int64_t offset, uint8_t** out, s
   return emit(op_add_offset(x, offset), out, out_len);
 }
 
+// x.removeRunCompression() (RB/RoaringBitmap.java:2738-2749)
+int rbo_remove_run_compression(const uint8_t* a, size_t an, uint8_t** out, size_t* out_len) {
+  Bitmap x;
+  int st = load(a, an, &x);
+  if (st) return st;
+  return emit(op_remove_run_compression(x), out, out_len);
+}
+
 // RoaringBitmap.getLongSizeInBytes of a serialized bitmap (RB/RoaringBitmap.java:2212-2219)
 int64_t rbo_long_size(const uint8_t* a, size_t an) {
   Bitmap b;

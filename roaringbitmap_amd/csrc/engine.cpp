@@ -1054,6 +1054,35 @@ static int ctx_range_mut(Ctx* c, int op, int32_t ia, size_t ma, int64_t start, i
   }
 }
 
+// x.removeRunCompression() (RB/RoaringBitmap.java:2738-2749; the buffer package's alike): every run
+// container through toBitmapOrArrayContainer (RB/RunContainer.java:2300-2323), the rest cloned; rangemut.hip
+static int ctx_remove_run_compression(Ctx* c, int32_t ia, size_t ma) {
+  Batch* A;
+  CHK(get_batch(c, ia, &A));
+  const uint16_t* ka;
+  const CDesc* da;
+  int na;
+  CHK(operand(A, ma, &ka, &da, &na));
+  const RmutArgs ra{RMUT_DERUN, 1, 0, 0, 0};
+  const size_t ub = std::max<size_t>(1, (size_t)na);
+  hipStream_t s = c->stream;
+  OutCtx oc;
+  CHK(prepare_output(c, ub, A->payload_bytes + (size_t)8194 * ub, &oc, false));
+  c->pending_src = {ia};
+  c->mark(0);
+  c->mark(1);
+  if (!c->big_ctl.p) CHK(c->big_ctl.ensure(16));
+  if (!c->big.p) CHK(c->big.ensure(16ull << 20));
+  launch_rmut(s, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), ra, false, c->wg_epoch.as<uint64_t>(),
+              next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->zlb, c->ztile,
+              BigRuns{c->big.as<uint8_t>(), c->big_ctl.as<unsigned long long>(), c->big.cap}, grid_for(ub, 65536));
+  c->mark(2);
+  defer_place(c);
+  c->mark(3);
+  HIPCHK(hipGetLastError());
+  return RBG_OK;
+}
+
 // RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288; MutableRoaringBitmap.addOffset,
 // RB/buffer/MutableRoaringBitmap.java:84-142, the same bytes), addoffset.hip.  The container offset is
 // the floor of offset / 65536 (:233-234); outside [-65536, 65535] the result is empty (:235-237).
@@ -2317,6 +2346,18 @@ int rbg_add_offset(const uint8_t* a, size_t a_len, int64_t offset, rbg_buffer* o
   CHK(ctx_load_separate(c, &a, &a_len, 1, &id));
   g.ids = {id};
   CHK(ctx_add_offset(c, id, 0, offset));
+  return ctx_fetch(c, out);
+}
+
+int rbg_remove_run_compression(const uint8_t* a, size_t a_len, rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(ctx_load_separate(c, &a, &a_len, 1, &id));
+  g.ids = {id};
+  CHK(ctx_remove_run_compression(c, id, 0));
   return ctx_fetch(c, out);
 }
 

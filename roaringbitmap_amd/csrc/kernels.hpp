@@ -369,7 +369,8 @@ void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const 
 
 // static add / remove / flip(rb, rangeStart, rangeEnd) (rangemut.hip); hbs > hbl: no key in the range
 // RMUT_ADD_INPLACE: x.add(rangeStart, rangeEnd) (RB/RoaringBitmap.java:1181), Container.iadd on every key
-enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2, RMUT_ADD_INPLACE = 3 };
+// RMUT_DERUN: removeRunCompression (RB/RoaringBitmap.java:2738-2749), every run container by cardinality
+enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2, RMUT_ADD_INPLACE = 3, RMUT_DERUN = 4 };
 struct RmutArgs {
   int op, hbs, lbs, hbl, lbl;
 };

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void k_plan_rmut(const uint32_t* __restrict__ 
   const bool present = t.kind_a != kAbsent;
   const bool in = (int)k >= ra.hbs && (int)k <= ra.hbl;
   int f;
-  if (!in) {
+  if (!in || ra.op == RMUT_DERUN) {
     f = present;
   } else if (ra.op == RMUT_REMOVE) {
     int lo, hi;
@@ -77,7 +77,21 @@ __device__ __forceinline__ void rmut_task(uint32_t t, const PTask& tk, const uin
                                           const OutCtx& oc, const BigRuns& big, uint32_t* lds) {
   const int key = tk.key;
   const bool present = tk.kind_a != kAbsent;
-  if (key < ra.hbs || key > ra.hbl) {  // outside the range: cloned
+  if (OP == RMUT_DERUN && tk.kind_a == DK_R) {  // RunContainer.toBitmapOrArrayContainer (RB/RunContainer.java:2300-2323)
+    WCtr x;
+    w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0}, pa, lds, x);
+    const int c = (int)tk.card_a;
+    if (c > 4096) {
+      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+      w_store_bitmap(slot, x);
+      w_place(t, true, slot, false, lds, 8192, (uint32_t)c, (uint32_t)key, DK_B, oc);
+    } else {
+      const uint32_t len = w_stage(DK_A, x, c, lds);
+      w_place(t, true, nullptr, true, lds, len, (uint32_t)c, (uint32_t)key, DK_A, oc);
+    }
+    return;
+  }
+  if (OP == RMUT_DERUN || key < ra.hbs || key > ra.hbl) {  // outside the range (or not a run container): cloned
     const uint32_t len = tk.kind_a == DK_A ? 2u * tk.card_a : tk.kind_a == DK_B ? 8192u : 2u + 4u * tk.nruns_a;
     w_place(t, true, pa + tk.slot_a + (tk.kind_a == DK_R ? 2 : 0), false, lds, len, tk.card_a, (uint32_t)key,
             tk.kind_a, oc);
@@ -181,6 +195,7 @@ void launch_rmut(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint
                      tasks, n_tasks, pa, ra, oc, big)
   if (ra.op == RMUT_ADD) RBG_RMUT_LAUNCH(RMUT_ADD, false);
   else if (ra.op == RMUT_ADD_INPLACE) RBG_RMUT_LAUNCH(RMUT_ADD_INPLACE, false);
+  else if (ra.op == RMUT_DERUN) RBG_RMUT_LAUNCH(RMUT_DERUN, false);
   else if (ra.op == RMUT_FLIP) RBG_RMUT_LAUNCH(RMUT_FLIP, false);
   else if (buf) RBG_RMUT_LAUNCH(RMUT_REMOVE, true);
   else RBG_RMUT_LAUNCH(RMUT_REMOVE, false);

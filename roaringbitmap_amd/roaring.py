@@ -224,6 +224,15 @@ class RoaringBitmap:
         self._buf = take(b)
         return self.container_stats()[2] > 0
 
+    def removeRunCompression(self) -> bool:
+        """In-place removeRunCompression (RB/RoaringBitmap.java:2738-2749; MutableRoaringBitmap's alike): every
+        run container as an array or bitmap by cardinality, on the GPU; True if there was one."""
+        had = self.container_stats()[2] > 0
+        b = _lib.rbg_buffer()
+        check(lib().rbg_remove_run_compression(self._buf, len(self._buf), ctypes.byref(b)))
+        self._buf = take(b)
+        return had
+
     def clone(self):
         return RoaringBitmap(self._buf)
 

@@ -80,6 +80,8 @@ def lib():
                                     ctypes.POINTER(u8p), ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_add_offset.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int64, ctypes.POINTER(u8p),
                                      ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_remove_run_compression.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(u8p),
+                                                 ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -285,6 +287,14 @@ def add_offset(buf, offset) -> bytes:
     p = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     _check(lib().rbo_add_offset(buf, len(buf), int(offset), ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
+
+
+def remove_run_compression(buf) -> bytes:
+    """x.removeRunCompression() (RB/RoaringBitmap.java:2738-2749), x's bytes afterwards."""
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_remove_run_compression(buf, len(buf), ctypes.byref(p), ctypes.byref(n)))
     return _take(p, n)
 
 

@@ -161,3 +161,14 @@ def test_every_mode_neighbours(mode):
             _check_set(buf, off)
             keys, kinds, cards, _, _ = container_table(O.add_offset(buf, off))
             assert np.all(np.diff(keys.astype(np.int64)) > 0)
+
+
+def test_remove_run_compression():
+    """x.removeRunCompression() (RB/RoaringBitmap.java:2738-2749): run containers by cardinality
+    (RunContainer.toBitmapOrArrayContainer, RB/RunContainer.java:2300-2323), a full one a bitmap"""
+    x = encode([(0, R, np.arange(65536)), (1, R, np.arange(100, 4196)), (2, R, np.arange(100, 4197)),
+                (3, A, [1, 2]), (4, B, np.arange(0, 65536, 2))])
+    got = decode(O.remove_run_compression(x))
+    assert [(c[0], c[1], c[2]) for c in got] == [(0, B, 65536), (1, A, 4096), (2, B, 4097), (3, A, 2),
+                                                 (4, B, 32768)]
+    np.testing.assert_array_equal(O.to_values(O.remove_run_compression(x)), O.to_values(x))

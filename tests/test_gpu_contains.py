@@ -8,7 +8,7 @@ import pytest
 
 import _gen
 import _oracle as O
-from _fmt import A, B, R, encode
+from _fmt import A, B, R, container_table, encode
 
 pytestmark = pytest.mark.gpu
 
@@ -109,3 +109,18 @@ def test_select_range(gpu):
     assert h == O.range_op("select", [x], 1 << 16, (1 << 16) + 12288)
     assert bb == O.range_op("select_buf", [x], 1 << 16, (1 << 16) + 12288)
     assert h != bb and len(h) == len(bb)  # 4,096 values: 8,192 payload bytes either way, different bytes
+
+
+def test_remove_run_compression(gpu):
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(11)
+    for m in _gen.MODES:
+        buf = encode([(k, *_gen.container(rng, m)) for k in (0, 7, 65535)])
+        for cls in (rb.RoaringBitmap, rb.MutableRoaringBitmap):
+            x = cls(buf)
+            had = x.removeRunCompression()
+            assert had == bool((container_table(buf)[1] == R).any())
+            assert x.serialize() == O.remove_run_compression(buf), m
+            assert x.container_stats()[2] == 0
+    y = rb.RoaringBitmap(O.from_values(np.arange(10, dtype=np.uint32), run_optimize=True))
+    assert y.removeRunCompression() is True and y.removeRunCompression() is False
