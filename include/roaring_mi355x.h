@@ -172,6 +172,11 @@ int rbg_add_offset(const uint8_t* a, size_t a_len, int64_t offset, rbg_buffer* o
  * bytes afterwards, every run container as an array (<= 4096 values) or a bitmap
  * (RunContainer.toBitmapOrArrayContainer, RB/RunContainer.java:2300-2323), the rest unchanged */
 int rbg_remove_run_compression(const uint8_t* a, size_t a_len, rbg_buffer* out);
+/* x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476): the first maxcardinality values; whole
+ * containers while they fit, the next one through Container.limit (an array stays an array, a bitmap
+ * becomes an array at <= 4096 values, a run container keeps its runs up to the cut); maxcardinality <= 0:
+ * the empty bitmap */
+int rbg_limit(const uint8_t* a, size_t a_len, int32_t maxcard, rbg_buffer* out);
 /* x.selectRange(rangeStart, rangeEnd) (RB/RoaringBitmap.java:3095-3147): the values in the range, the
  * first / last key's container cut by Container.remove (A stays A, B becomes A at <= 4096 values, R stays
  * R with its runs clipped), the keys between cloned; buffer != 0: ImmutableRoaringBitmap.selectRange

@@ -1857,6 +1857,49 @@ Bitmap op_add_offset(const Bitmap& x, int64_t offset) {
   return ans;
 }
 
+// Container.limit(n), n < card: the first n values -- ArrayContainer.limit an array (RB/ArrayContainer.java
+// :825-831), BitmapContainer.limit an array at <= 4096 values, else a bitmap (RB/BitmapContainer.java
+// :912-938), RunContainer.limit the runs up to the n-th value, a run container (RB/RunContainer.java:1856-1875)
+static Ctr c_limit(const Ctr& c, int n) {
+  if (c.kind == ARRAY) return make_array(std::vector<uint16_t>(c.vals.begin(), c.vals.begin() + n));
+  if (c.kind == BITMAP) {
+    std::vector<uint16_t> v;
+    for (int w = 0; w < kWords && (int)v.size() < n; w++)
+      for (uint64_t x = c.words[w]; x && (int)v.size() < n; x &= x - 1) v.push_back((uint16_t)(64 * w + __builtin_ctzll(x)));
+    Ctr a = make_array(std::move(v));
+    return n <= kArrayMax ? a : to_bitmap(a);
+  }
+  std::vector<uint16_t> p;
+  int card = 0, r = 0;
+  for (; r < c.nruns(); r++) {
+    card += c.vals[2 * r + 1] + 1;
+    if (n <= card) break;
+  }
+  p.assign(c.vals.begin(), c.vals.begin() + 2 * (r + 1));
+  p[2 * r + 1] = (uint16_t)(p[2 * r + 1] - card + n);
+  return make_run(std::move(p), r + 1);
+}
+
+// x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476): whole containers while they fit, the next
+// one through Container.limit(leftover)
+Bitmap op_limit(const Bitmap& x, int32_t maxcard) {
+  Bitmap ans;
+  int32_t cur = 0;
+  for (size_t i = 0; cur < maxcard && i < x.size(); i++) {
+    const int cc = x.ctrs[i].cardinality();
+    if ((int64_t)cc + cur <= maxcard) {
+      ans.keys.push_back(x.keys[i]);
+      ans.ctrs.push_back(x.ctrs[i]);
+      cur += cc;
+    } else {
+      ans.keys.push_back(x.keys[i]);
+      ans.ctrs.push_back(c_limit(x.ctrs[i], maxcard - cur));
+      break;
+    }
+  }
+  return ans;
+}
+
 // x.removeRunCompression() (RB/RoaringBitmap.java:2738-2749): every run container through
 // toBitmapOrArrayContainer(getCardinality()) (RB/RunContainer.java:2300-2323)
 Bitmap op_remove_run_compression(const Bitmap& x) {

@@ -184,6 +184,14 @@ int rbo_add_offset(const uint8_t* a, size_t an, int64_t offset, uint8_t** out, s
   return emit(op_add_offset(x, offset), out, out_len);
 }
 
+// x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476)
+int rbo_limit(const uint8_t* a, size_t an, int32_t maxcard, uint8_t** out, size_t* out_len) {
+  Bitmap x;
+  int st = load(a, an, &x);
+  if (st) return st;
+  return emit(op_limit(x, maxcard), out, out_len);
+}
+
 // x.removeRunCompression() (RB/RoaringBitmap.java:2738-2749)
 int rbo_remove_run_compression(const uint8_t* a, size_t an, uint8_t** out, size_t* out_len) {
   Bitmap x;

@@ -2349,6 +2349,81 @@ int rbg_add_offset(const uint8_t* a, size_t a_len, int64_t offset, rbg_buffer* o
   return ctx_fetch(c, out);
 }
 
+// x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476).  The cut is planned from the serialized
+// header's cardinalities on the host (the reference's own loop walks getCardinality per container):
+// keys before it cloned, its container cut to the leftover by k_rmut<RMUT_LIMIT>, the rest dropped.
+int rbg_limit(const uint8_t* a, size_t a_len, int32_t maxcard, rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  HostBitmap hb;
+  std::string err;
+  const int pst = parse(a, a_len, &hb, &err);
+  if (pst) {
+    set_err(err);
+    return pst;
+  }
+  int cut_key = 65536, leftover = 0;
+  int64_t cur = 0;
+  for (size_t i = 0; cur < maxcard && i < hb.ctrs.size(); i++) {
+    const int64_t cc = hb.ctrs[i].card;
+    if (cc + cur <= maxcard) {
+      cur += cc;
+    } else {
+      cut_key = hb.ctrs[i].key;
+      leftover = (int)(maxcard - cur);
+      break;
+    }
+  }
+  if (leftover == 0) {  // the containers that fit whole: those before the first that does not
+    cut_key = 0;
+    for (size_t i = 0, acc = 0; i < hb.ctrs.size() && (int64_t)(acc + hb.ctrs[i].card) <= (int64_t)maxcard; i++) {
+      acc += hb.ctrs[i].card;
+      cut_key = hb.ctrs[i].key + 1;
+    }
+  }
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(ctx_load_separate(c, &a, &a_len, 1, &id));
+  g.ids = {id};
+  Batch* A;
+  CHK(get_batch(c, id, &A));
+  const uint16_t* ka;
+  const CDesc* da;
+  int na;
+  CHK(operand(A, 0, &ka, &da, &na));
+  const RmutArgs ra{RMUT_LIMIT, cut_key, leftover, 0, 0};
+  const size_t ub = std::max<size_t>(1, (size_t)na);
+  hipStream_t s = c->stream;
+  if (!c->big_ctl.p) CHK(c->big_ctl.ensure(16));
+  if (!c->big.p) CHK(c->big.ensure(16ull << 20));
+  for (int attempt = 0;; attempt++) {
+    OutCtx oc;
+    CHK(prepare_output(c, ub, A->payload_bytes + (size_t)8194 * ub + c->big.cap, &oc, false));
+    c->pending_src = {id};
+    c->mark(0);
+    HIPCHK(hipMemsetAsync(c->big_ctl.p, 0, 16, s));
+    c->mark(1);
+    launch_rmut(s, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), ra, false, c->wg_epoch.as<uint64_t>(),
+                next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->zlb, c->ztile,
+                BigRuns{c->big.as<uint8_t>(), c->big_ctl.as<unsigned long long>(), c->big.cap}, grid_for(ub, 65536));
+    c->mark(2);
+    defer_place(c);
+    c->mark(3);
+    HIPCHK(hipGetLastError());
+    unsigned long long used[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(used, c->big_ctl.p, 16, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (!used[1]) break;
+    if (attempt) {
+      set_err("limit: the run-container arena overflowed twice");
+      return RBG_ERR_DEVICE;
+    }
+    CHK(c->big.ensure(used[0] + (used[0] >> 3) + 4096));
+  }
+  return ctx_fetch(c, out);
+}
+
 int rbg_remove_run_compression(const uint8_t* a, size_t a_len, rbg_buffer* out) {
   if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
   Ctx* c;

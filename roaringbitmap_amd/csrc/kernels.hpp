@@ -370,7 +370,9 @@ void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const 
 // static add / remove / flip(rb, rangeStart, rangeEnd) (rangemut.hip); hbs > hbl: no key in the range
 // RMUT_ADD_INPLACE: x.add(rangeStart, rangeEnd) (RB/RoaringBitmap.java:1181), Container.iadd on every key
 // RMUT_DERUN: removeRunCompression (RB/RoaringBitmap.java:2738-2749), every run container by cardinality
-enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2, RMUT_ADD_INPLACE = 3, RMUT_DERUN = 4 };
+// RMUT_LIMIT: limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476): keys below hbs cloned, key hbs cut to its
+// first lbs values (lbs = 0: none), the rest dropped
+enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2, RMUT_ADD_INPLACE = 3, RMUT_DERUN = 4, RMUT_LIMIT = 5 };
 struct RmutArgs {
   int op, hbs, lbs, hbl, lbl;
 };

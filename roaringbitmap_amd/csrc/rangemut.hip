@@ -60,7 +60,9 @@ __global__ __launch_bounds__(256) void k_plan_rmut(const uint32_t* __restrict__ 
   const bool present = t.kind_a != kAbsent;
   const bool in = (int)k >= ra.hbs && (int)k <= ra.hbl;
   int f;
-  if (!in || ra.op == RMUT_DERUN) {
+  if (ra.op == RMUT_LIMIT) {
+    f = present && ((int)k < ra.hbs || ((int)k == ra.hbs && ra.lbs > 0));
+  } else if (!in || ra.op == RMUT_DERUN) {
     f = present;
   } else if (ra.op == RMUT_REMOVE) {
     int lo, hi;
@@ -91,7 +93,50 @@ __device__ __forceinline__ void rmut_task(uint32_t t, const PTask& tk, const uin
     }
     return;
   }
-  if (OP == RMUT_DERUN || key < ra.hbs || key > ra.hbl) {  // outside the range (or not a run container): cloned
+  if (OP == RMUT_LIMIT && key == ra.hbs) {  // Container.limit(lbs): the first lbs values
+    WCtr x;
+    w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, tk.kind_a, 0}, pa, lds, x);
+    const int n = ra.lbs;
+    int base = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int c0 = __popcll(x.w[2 * i]), c1 = __popcll(x.w[2 * i + 1]);
+      int tot;
+      const int p0 = base + wave_excl(c0 + c1, &tot);
+      base += tot;
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int pre = p0 + (j ? c0 : 0), cw = j ? c1 : c0;
+        uint64_t& w = x.w[2 * i + j];
+        if (pre >= n) {
+          w = 0;
+        } else if (pre + cw > n) {  // keep the word's lowest n - pre set bits
+          uint64_t rest = w;
+          for (int q = 0; q < n - pre; q++) rest &= rest - 1;
+          w ^= rest;
+        }
+      }
+    }
+    const int kind = tk.kind_a == DK_B ? by_card(n) : tk.kind_a;
+    if (kind == DK_B) {
+      uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
+      w_store_bitmap(slot, x);
+      w_place(t, true, slot, false, lds, 8192, (uint32_t)n, (uint32_t)key, DK_B, oc);
+      return;
+    }
+    if (kind == DK_R) {
+      const int nr = w_runs(x);
+      if (nr > 2047) {
+        w_place_big_runs(t, (uint32_t)key, x, n, nr, oc, big, lds);
+        return;
+      }
+    }
+    const uint32_t len = w_stage(kind, x, n, lds);
+    w_place(t, true, nullptr, true, lds, len, (uint32_t)n, (uint32_t)key, kind, oc);
+    return;
+  }
+  if (OP == RMUT_DERUN || OP == RMUT_LIMIT || key < ra.hbs || key > ra.hbl) {  // cloned: outside the range,
+                                                                                // not a run container, or kept whole
     const uint32_t len = tk.kind_a == DK_A ? 2u * tk.card_a : tk.kind_a == DK_B ? 8192u : 2u + 4u * tk.nruns_a;
     w_place(t, true, pa + tk.slot_a + (tk.kind_a == DK_R ? 2 : 0), false, lds, len, tk.card_a, (uint32_t)key,
             tk.kind_a, oc);
@@ -196,6 +241,7 @@ void launch_rmut(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint
   if (ra.op == RMUT_ADD) RBG_RMUT_LAUNCH(RMUT_ADD, false);
   else if (ra.op == RMUT_ADD_INPLACE) RBG_RMUT_LAUNCH(RMUT_ADD_INPLACE, false);
   else if (ra.op == RMUT_DERUN) RBG_RMUT_LAUNCH(RMUT_DERUN, false);
+  else if (ra.op == RMUT_LIMIT) RBG_RMUT_LAUNCH(RMUT_LIMIT, false);
   else if (ra.op == RMUT_FLIP) RBG_RMUT_LAUNCH(RMUT_FLIP, false);
   else if (buf) RBG_RMUT_LAUNCH(RMUT_REMOVE, true);
   else RBG_RMUT_LAUNCH(RMUT_REMOVE, false);

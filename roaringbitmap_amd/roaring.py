@@ -224,6 +224,13 @@ class RoaringBitmap:
         self._buf = take(b)
         return self.container_stats()[2] > 0
 
+    def limit(self, maxcardinality):
+        """x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476) on the GPU: a new bitmap of the first
+        maxcardinality values (the cut container through Container.limit)."""
+        b = _lib.rbg_buffer()
+        check(lib().rbg_limit(self._buf, len(self._buf), _int32(maxcardinality), ctypes.byref(b)))
+        return type(self)(take(b))
+
     def removeRunCompression(self) -> bool:
         """In-place removeRunCompression (RB/RoaringBitmap.java:2738-2749; MutableRoaringBitmap's alike): every
         run container as an array or bitmap by cardinality, on the GPU; True if there was one."""

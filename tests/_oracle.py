@@ -82,6 +82,8 @@ def lib():
                                      ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_remove_run_compression.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(u8p),
                                                  ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_limit.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int32, ctypes.POINTER(u8p),
+                                ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -295,6 +297,14 @@ def remove_run_compression(buf) -> bytes:
     p = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     _check(lib().rbo_remove_run_compression(buf, len(buf), ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
+
+
+def limit(buf, maxcard) -> bytes:
+    """x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476)."""
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_limit(buf, len(buf), int(maxcard), ctypes.byref(p), ctypes.byref(n)))
     return _take(p, n)
 
 

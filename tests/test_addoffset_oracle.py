@@ -172,3 +172,21 @@ def test_remove_run_compression():
     assert [(c[0], c[1], c[2]) for c in got] == [(0, B, 65536), (1, A, 4096), (2, B, 4097), (3, A, 2),
                                                  (4, B, 32768)]
     np.testing.assert_array_equal(O.to_values(O.remove_run_compression(x)), O.to_values(x))
+
+
+def test_limit():
+    """x.limit(n) (RB/RoaringBitmap.java:2457-2476): the first n values; the cut container through
+    Container.limit (an array stays one; a bitmap an array at <= 4096 values; a run container keeps its
+    runs up to the n-th value)"""
+    x = encode([(0, A, np.arange(0, 3000, 3)), (1, B, np.arange(0, 65536, 2)), (2, R, np.arange(10, 60000)),
+                (3, A, [5])])
+    vals = O.to_values(x)
+    for n in (0, -5, 1, 999, 1000, 1001, 1000 + 4096, 1000 + 4097, 1000 + 32768, 1000 + 32768 + 7,
+              len(vals) - 1, len(vals), len(vals) + 10, 2 ** 31 - 1):
+        got = O.limit(x, n)
+        np.testing.assert_array_equal(O.to_values(got), vals[:max(n, 0)])
+    kinds = lambda n: [(c[0], c[1]) for c in decode(O.limit(x, n))]
+    assert kinds(1000 + 4096) == [(0, A), (1, A)]
+    assert kinds(1000 + 4097) == [(0, A), (1, B)]
+    assert kinds(1000 + 32768 + 7) == [(0, A), (1, B), (2, R)]
+    assert kinds(500) == [(0, A)]

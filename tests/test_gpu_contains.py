@@ -124,3 +124,24 @@ def test_remove_run_compression(gpu):
             assert x.container_stats()[2] == 0
     y = rb.RoaringBitmap(O.from_values(np.arange(10, dtype=np.uint32), run_optimize=True))
     assert y.removeRunCompression() is True and y.removeRunCompression() is False
+
+
+def test_limit(gpu):
+    """x.limit(n) (RB/RoaringBitmap.java:2457-2476) against the oracle: every mode as the cut container,
+    cuts inside containers, at container edges, n <= 0 and n past the cardinality"""
+    import roaringbitmap_amd as rb
+    rng = np.random.default_rng(21)
+    for m in _gen.MODES:
+        ctrs = [(k, *_gen.container(rng, m)) for k in (2, 9, 40000)]
+        buf = encode(ctrs)
+        cards = [len(c[2]) for c in ctrs]
+        tot = sum(cards)
+        ns = {0, -3, 1, cards[0] - 1, cards[0], cards[0] + 1, cards[0] + cards[1] // 2, tot - 1, tot, tot + 5,
+              cards[0] + 4096, cards[0] + 4097, int(rng.integers(1, tot + 1))}
+        for n in sorted(ns):
+            got = rb.RoaringBitmap(buf).limit(n)
+            assert type(got) is rb.RoaringBitmap
+            assert got.serialize() == O.limit(buf, n), (m, n)
+    alt = np.arange(0, 65536, 2)  # a run container of 32,768 runs cut after 30,000 of them
+    buf = encode([(0, R, alt), (1, A, [3])])
+    assert rb.RoaringBitmap(buf).limit(30000).serialize() == O.limit(buf, 30000)
