@@ -177,6 +177,10 @@ int rbg_remove_run_compression(const uint8_t* a, size_t a_len, rbg_buffer* out);
  * becomes an array at <= 4096 values, a run container keeps its runs up to the cut); maxcardinality <= 0:
  * the empty bitmap */
 int rbg_limit(const uint8_t* a, size_t a_len, int32_t maxcard, rbg_buffer* out);
+/* RoaringBitmap.bitmapOfRange(min, max) (RB/RoaringBitmap.java:588-615): every container a run container
+ * (RunContainer.rangeOfOnes, even for one or two values; static add over an empty bitmap would write
+ * arrays there).  rangeSanityCheck -> RBG_ERR_ILLEGAL_ARGUMENT; max <= min: the empty bitmap. */
+int rbg_bitmap_of_range(int64_t min, int64_t max, rbg_buffer* out);
 /* x.selectRange(rangeStart, rangeEnd) (RB/RoaringBitmap.java:3095-3147): the values in the range, the
  * first / last key's container cut by Container.remove (A stays A, B becomes A at <= 4096 values, R stays
  * R with its runs clipped), the keys between cloned; buffer != 0: ImmutableRoaringBitmap.selectRange

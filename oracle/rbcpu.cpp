@@ -1880,6 +1880,19 @@ static Ctr c_limit(const Ctr& c, int n) {
   return make_run(std::move(p), r + 1);
 }
 
+// RoaringBitmap.bitmapOfRange(min, max) (RB/RoaringBitmap.java:588-615): RunContainer.rangeOfOnes per key
+Bitmap op_bitmap_of_range(uint64_t min, uint64_t max) {
+  Bitmap ans;
+  if (min >= max) return ans;
+  const int hbs = (int)(min >> 16), hbl = (int)((max - 1) >> 16);
+  for (int k = hbs; k <= hbl; k++) {
+    const int lo = k == hbs ? (int)(min & 0xFFFF) : 0, hi = k == hbl ? (int)((max - 1) & 0xFFFF) : 65535;
+    ans.keys.push_back((uint16_t)k);
+    ans.ctrs.push_back(make_run(std::vector<uint16_t>{(uint16_t)lo, (uint16_t)(hi - lo)}, 1));
+  }
+  return ans;
+}
+
 // x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476): whole containers while they fit, the next
 // one through Container.limit(leftover)
 Bitmap op_limit(const Bitmap& x, int32_t maxcard) {

@@ -154,6 +154,7 @@ Bitmap op_range_mut(int op, const Bitmap& b, uint64_t start, uint64_t end, bool 
 Bitmap op_add_offset(const Bitmap& x, int64_t offset);
 Bitmap op_remove_run_compression(const Bitmap& x);  // RB/RoaringBitmap.java:2738-2749
 Bitmap op_limit(const Bitmap& x, int32_t maxcard);   // RB/RoaringBitmap.java:2457-2476
+Bitmap op_bitmap_of_range(uint64_t min, uint64_t max);  // RB/RoaringBitmap.java:588-615
 Bitmap fa_horizontal_or(const std::vector<const Bitmap*>& bms);      // FastAggregation.horizontal_or :124-231
 Bitmap fa_horizontal_xor(const std::vector<const Bitmap*>& bms);     // :243-289
 Bitmap fa_priorityqueue_or(const std::vector<const Bitmap*>& bms);   // :733-781

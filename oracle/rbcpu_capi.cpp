@@ -184,6 +184,12 @@ int rbo_add_offset(const uint8_t* a, size_t an, int64_t offset, uint8_t** out, s
   return emit(op_add_offset(x, offset), out, out_len);
 }
 
+// RoaringBitmap.bitmapOfRange(min, max) (RB/RoaringBitmap.java:588-615); rangeSanityCheck -> ERR_ARG
+int rbo_bitmap_of_range(int64_t min, int64_t max, uint8_t** out, size_t* out_len) {
+  if (min < 0 || min > 0xFFFFFFFFll || max < 0 || max > 0x100000000ll) return ERR_ARG;
+  return emit(op_bitmap_of_range((uint64_t)min, (uint64_t)max), out, out_len);
+}
+
 // x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476)
 int rbo_limit(const uint8_t* a, size_t an, int32_t maxcard, uint8_t** out, size_t* out_len) {
   Bitmap x;

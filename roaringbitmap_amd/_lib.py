@@ -49,7 +49,7 @@ EXPORTED = [
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
     "rbg_ctx_fetch_shard_device", "rbg_bsi_compare_buffer", "rbg_ctx_bsi_buffer",
     "rbg_ctx_result_layout_device", "rbg_ctx_fetch_shard_device_dyn", "rbg_pairwise_inplace",
-    "rbg_ctx_load_separate", "rbg_ornot", "rbg_ctx_ornot", "rbg_range_mut", "rbg_ctx_range_mut", "rbg_add_offset", "rbg_ctx_add_offset", "rbg_select_range", "rbg_remove_run_compression", "rbg_limit",
+    "rbg_ctx_load_separate", "rbg_ornot", "rbg_ctx_ornot", "rbg_range_mut", "rbg_ctx_range_mut", "rbg_add_offset", "rbg_ctx_add_offset", "rbg_select_range", "rbg_remove_run_compression", "rbg_limit", "rbg_bitmap_of_range",
 ]
 
 _lib = None
@@ -79,6 +79,7 @@ def _declare(L):
     L.rbg_add_offset.argtypes = [u8p, sz, ctypes.c_int64, buf]
     L.rbg_remove_run_compression.argtypes = [u8p, sz, buf]
     L.rbg_limit.argtypes = [u8p, sz, ctypes.c_int32, buf]
+    L.rbg_bitmap_of_range.argtypes = [ctypes.c_int64, ctypes.c_int64, buf]
     L.rbg_select_range.argtypes = [u8p, sz, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, buf]
     L.rbg_ctx_add_offset.argtypes = [vp, i32, sz, ctypes.c_int64]
     L.rbg_ctx_select_range.argtypes = [vp, i32, ctypes.c_int64, ctypes.c_int64, P(i32)]

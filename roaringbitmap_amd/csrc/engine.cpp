@@ -1004,7 +1004,7 @@ static int ctx_ornot(Ctx* c, int32_t ia, size_t ma, int32_t ib, size_t mb, int64
 // to the big-run arena; the arena is checked after the op and the op rerun once with the size the first
 // pass reserved (as ctx_pairwise_buffer).
 static int ctx_range_mut(Ctx* c, int op, int32_t ia, size_t ma, int64_t start, int64_t end, bool buf) {
-  if (op < RMUT_ADD || op > RMUT_ADD_INPLACE) return RBG_ERR_ILLEGAL_ARGUMENT;
+  if (op < RMUT_ADD || (op > RMUT_ADD_INPLACE && op != RMUT_RANGE)) return RBG_ERR_ILLEGAL_ARGUMENT;
   if (start < 0 || start > 0xFFFFFFFFll || end < 0 || end > 0x100000000ll) {
     set_err("rangeStart=" + std::to_string(start) + " should be in [0, 0xffffffff], rangeEnd=" + std::to_string(end) +
             " in [0, 0xffffffff + 1]");
@@ -2421,6 +2421,23 @@ int rbg_limit(const uint8_t* a, size_t a_len, int32_t maxcard, rbg_buffer* out) 
     }
     CHK(c->big.ensure(used[0] + (used[0] >> 3) + 4096));
   }
+  return ctx_fetch(c, out);
+}
+
+// RoaringBitmap.bitmapOfRange(min, max) (RB/RoaringBitmap.java:588-615): k_rmut<RMUT_RANGE> over an empty
+// bitmap (every container written as a run container)
+int rbg_bitmap_of_range(int64_t min, int64_t max, rbg_buffer* out) {
+  if (!out) return RBG_ERR_ILLEGAL_ARGUMENT;
+  static const uint8_t kEmpty[8] = {0x3A, 0x30, 0, 0, 0, 0, 0, 0};
+  const uint8_t* a = kEmpty;
+  size_t a_len = 8;
+  Ctx* c;
+  CHK(tl_ctx(&c));
+  BatchGuard g{c, {}};
+  int32_t id;
+  CHK(ctx_load_separate(c, &a, &a_len, 1, &id));
+  g.ids = {id};
+  CHK(ctx_range_mut(c, RMUT_RANGE, id, 0, min, max, false));
   return ctx_fetch(c, out);
 }
 

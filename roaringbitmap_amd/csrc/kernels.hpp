@@ -372,7 +372,10 @@ void launch_pair_buf(hipStream_t s, int op, int grid, const PTask* tasks, const 
 // RMUT_DERUN: removeRunCompression (RB/RoaringBitmap.java:2738-2749), every run container by cardinality
 // RMUT_LIMIT: limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476): keys below hbs cloned, key hbs cut to its
 // first lbs values (lbs = 0: none), the rest dropped
-enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2, RMUT_ADD_INPLACE = 3, RMUT_DERUN = 4, RMUT_LIMIT = 5 };
+// RMUT_RANGE: bitmapOfRange(min, max) (RB/RoaringBitmap.java:588-615), add over an empty bitmap whose
+// containers are all RunContainer.rangeOfOnes (run containers even for one or two values)
+enum RmutOp : int { RMUT_ADD = 0, RMUT_REMOVE = 1, RMUT_FLIP = 2, RMUT_ADD_INPLACE = 3, RMUT_DERUN = 4, RMUT_LIMIT = 5,
+                    RMUT_RANGE = 6 };
 struct RmutArgs {
   int op, hbs, lbs, hbl, lbl;
 };

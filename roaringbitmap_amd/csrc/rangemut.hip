@@ -144,15 +144,15 @@ __device__ __forceinline__ void rmut_task(uint32_t t, const PTask& tk, const uin
   }
   int lo, hi;
   rmut_cut(key, ra, &lo, &hi);
-  constexpr bool ADD = OP == RMUT_ADD || OP == RMUT_ADD_INPLACE;
-  if (OP == RMUT_ADD && key != ra.hbs && key != ra.hbl) {  // rangeOfOnes(0, 65536): a full run container
+  constexpr bool ADD = OP == RMUT_ADD || OP == RMUT_ADD_INPLACE || OP == RMUT_RANGE;
+  if ((OP == RMUT_ADD || OP == RMUT_RANGE) && key != ra.hbs && key != ra.hbl) {  // rangeOfOnes(0, 65536): a full run container
     w_place(t, true, reinterpret_cast<const uint8_t*>(g_full_run_rm), false, lds, 6, 65536, (uint32_t)key, DK_R, oc);
     return;
   }
   if (!present) {  // rangeOfOnes(lo, hi + 1) (add / flip), written by lane 0
     uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
     const int n = hi - lo + 1;
-    const bool arr = n <= 2;
+    const bool arr = OP != RMUT_RANGE && n <= 2;  // Container.rangeOfOnes; bitmapOfRange: RunContainer's
     uint16_t* p = reinterpret_cast<uint16_t*>(arr ? slot : slot + 2);
     if (lane_id() == 0) {
       if (arr) {
@@ -242,6 +242,7 @@ void launch_rmut(hipStream_t s, const uint32_t* koa, const CDesc* da, const uint
   else if (ra.op == RMUT_ADD_INPLACE) RBG_RMUT_LAUNCH(RMUT_ADD_INPLACE, false);
   else if (ra.op == RMUT_DERUN) RBG_RMUT_LAUNCH(RMUT_DERUN, false);
   else if (ra.op == RMUT_LIMIT) RBG_RMUT_LAUNCH(RMUT_LIMIT, false);
+  else if (ra.op == RMUT_RANGE) RBG_RMUT_LAUNCH(RMUT_RANGE, false);
   else if (ra.op == RMUT_FLIP) RBG_RMUT_LAUNCH(RMUT_FLIP, false);
   else if (buf) RBG_RMUT_LAUNCH(RMUT_REMOVE, true);
   else RBG_RMUT_LAUNCH(RMUT_REMOVE, false);

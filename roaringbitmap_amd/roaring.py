@@ -364,6 +364,14 @@ class RoaringBitmap:
     flip = _RangeMut("flip")
 
     @classmethod
+    def bitmapOfRange(cls, range_min, range_max):
+        """RoaringBitmap.bitmapOfRange(min, max) (RB/RoaringBitmap.java:588-615) on the GPU: [min, max) as
+        run containers (RunContainer.rangeOfOnes, even for one or two values)."""
+        b = _lib.rbg_buffer()
+        check(lib().rbg_bitmap_of_range(int(range_min), int(range_max), ctypes.byref(b)))
+        return cls(take(b))
+
+    @classmethod
     def addOffset(cls, x, offset):
         """RoaringBitmap.addOffset(x, offset) (RB/RoaringBitmap.java:230-288): every value plus `offset`
         (a long in [-2^32, 2^32]; values leaving [0, 2^32) dropped).  The buffer package's

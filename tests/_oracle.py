@@ -84,6 +84,8 @@ def lib():
                                                  ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_limit.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int32, ctypes.POINTER(u8p),
                                 ctypes.POINTER(ctypes.c_size_t)]
+        L.rbo_bitmap_of_range.argtypes = [ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(u8p),
+                                          ctypes.POINTER(ctypes.c_size_t)]
         L.rbo_long_size.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
         L.rbo_long_size.restype = ctypes.c_int64
         _lib = L
@@ -305,6 +307,14 @@ def limit(buf, maxcard) -> bytes:
     p = ctypes.POINTER(ctypes.c_uint8)()
     n = ctypes.c_size_t()
     _check(lib().rbo_limit(buf, len(buf), int(maxcard), ctypes.byref(p), ctypes.byref(n)))
+    return _take(p, n)
+
+
+def bitmap_of_range(lo, hi) -> bytes:
+    """RoaringBitmap.bitmapOfRange(min, max) (RB/RoaringBitmap.java:588-615)."""
+    p = ctypes.POINTER(ctypes.c_uint8)()
+    n = ctypes.c_size_t()
+    _check(lib().rbo_bitmap_of_range(int(lo), int(hi), ctypes.byref(p), ctypes.byref(n)))
     return _take(p, n)
 
 

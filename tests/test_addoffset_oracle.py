@@ -190,3 +190,18 @@ def test_limit():
     assert kinds(1000 + 4097) == [(0, A), (1, B)]
     assert kinds(1000 + 32768 + 7) == [(0, A), (1, B), (2, R)]
     assert kinds(500) == [(0, A)]
+
+
+def test_bitmap_of_range():
+    """RoaringBitmap.bitmapOfRange(min, max) (RB/RoaringBitmap.java:588-615): run containers only, even for
+    one or two values, where the static add over an empty bitmap writes arrays (Container.rangeOfOnes)"""
+    empty = O.from_values(np.zeros(0, dtype=np.uint32))
+    for lo, hi in ((5, 6), (5, 7), (5, 8), (65535, 65537), (70000, 5 << 16), (0, 1 << 32), (9, 9), (9, 3)):
+        got = O.bitmap_of_range(lo, hi)
+        keys, kinds, cards, _, _ = container_table(got)
+        assert int(cards.sum()) == max(hi - lo, 0)
+        assert (kinds == R).all()
+        assert (container_table(O.range_mut("add", empty, lo, hi))[2] == cards).all()
+    assert O.bitmap_of_range(5, 7) != O.range_mut("add", empty, 5, 7)
+    with pytest.raises(O.OracleError):
+        O.bitmap_of_range(-1, 5)

@@ -145,3 +145,13 @@ def test_limit(gpu):
     alt = np.arange(0, 65536, 2)  # a run container of 32,768 runs cut after 30,000 of them
     buf = encode([(0, R, alt), (1, A, [3])])
     assert rb.RoaringBitmap(buf).limit(30000).serialize() == O.limit(buf, 30000)
+
+
+def test_bitmap_of_range(gpu):
+    import roaringbitmap_amd as rb
+    for lo, hi in ((5, 6), (5, 7), (5, 8), (65535, 65537), (70000, 5 << 16), (12345, (40000 << 16) + 7),
+                   (0, 1 << 32), (9, 9), (9, 3)):
+        got = rb.RoaringBitmap.bitmapOfRange(lo, hi)
+        assert got.serialize() == O.bitmap_of_range(lo, hi), (lo, hi)
+    with pytest.raises(rb.IllegalArgumentException):
+        rb.RoaringBitmap.bitmapOfRange(0, (1 << 32) + 1)
