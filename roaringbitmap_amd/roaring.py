@@ -226,10 +226,11 @@ class RoaringBitmap:
 
     def limit(self, maxcardinality):
         """x.limit(maxcardinality) (RB/RoaringBitmap.java:2457-2476) on the GPU: a new bitmap of the first
-        maxcardinality values (the cut container through Container.limit)."""
+        maxcardinality values (the cut container through Container.limit).  ImmutableRoaringBitmap.limit
+        (RB/buffer/ImmutableRoaringBitmap.java:1658-1677, the same types) returns a MutableRoaringBitmap."""
         b = _lib.rbg_buffer()
         check(lib().rbg_limit(self._buf, len(self._buf), _int32(maxcardinality), ctypes.byref(b)))
-        return type(self)(take(b))
+        return (MutableRoaringBitmap if isinstance(self, ImmutableRoaringBitmap) else RoaringBitmap)(take(b))
 
     def removeRunCompression(self) -> bool:
         """In-place removeRunCompression (RB/RoaringBitmap.java:2738-2749; MutableRoaringBitmap's alike): every
@@ -854,6 +855,7 @@ class ImmutableRoaringBitmap(RoaringBitmap):
     xor = _s_xor
     add = remove = None  # no static add / remove on ImmutableRoaringBitmap (MutableRoaringBitmap's: below)
     addOffset = None  # MutableRoaringBitmap.addOffset(ImmutableRoaringBitmap, long): below
+    removeRunCompression = None  # in place: MutableRoaringBitmap's (RB/buffer/MutableRoaringBitmap.java:1568)
     andCardinality = RoaringBitmap.__dict__["andCardinality"]  # :336-359, a set-level count
     intersects = RoaringBitmap.__dict__["intersects"]
 
@@ -874,6 +876,7 @@ class MutableRoaringBitmap(ImmutableRoaringBitmap):
     xor = _StaticOrInPlace(ImmutableRoaringBitmap._s_xor, "xor")
     orNot = _OrNot(ImmutableRoaringBitmap.__dict__["orNot"].__func__, buffer=True)  # x1.orNot in place :962-1030
     addOffset = RoaringBitmap.__dict__["addOffset"]  # RB/buffer/MutableRoaringBitmap.java:84-142, the same bytes
+    removeRunCompression = RoaringBitmap.removeRunCompression
 
     def _inplace(self, op, x2):
         if op not in ("and_buffer", "andnot_buffer"):

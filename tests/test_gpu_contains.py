@@ -142,6 +142,9 @@ def test_limit(gpu):
             got = rb.RoaringBitmap(buf).limit(n)
             assert type(got) is rb.RoaringBitmap
             assert got.serialize() == O.limit(buf, n), (m, n)
+    got = rb.ImmutableRoaringBitmap(buf).limit(1000)  # RB/buffer/ImmutableRoaringBitmap.java:1658
+    assert isinstance(got, rb.MutableRoaringBitmap) and got.serialize() == O.limit(buf, 1000)
+    assert rb.ImmutableRoaringBitmap.removeRunCompression is None
     alt = np.arange(0, 65536, 2)  # a run container of 32,768 runs cut after 30,000 of them
     buf = encode([(0, R, alt), (1, A, [3])])
     assert rb.RoaringBitmap(buf).limit(30000).serialize() == O.limit(buf, 30000)
