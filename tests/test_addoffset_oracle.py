@@ -205,3 +205,16 @@ def test_bitmap_of_range():
     assert O.bitmap_of_range(5, 7) != O.range_mut("add", empty, 5, 7)
     with pytest.raises(O.OracleError):
         O.bitmap_of_range(-1, 5)
+
+
+def test_limit_reference_cases():
+    """RBT/TestRoaringBitmap.java:136-162: limit of alternating 9,943-value blocks, and limitTest's
+    [0, 10^7) at 1 .. 10^6"""
+    i = np.arange(500 * 9943, dtype=np.int64)
+    blocks = O.from_values(i[(i // 9943) % 2 == 0].astype(np.uint32))
+    assert O.to_values(O.limit(blocks, 1000000)).size == 1000000
+    empty = O.from_values(np.zeros(0, dtype=np.uint32))
+    r = O.range_mut("add", empty, 0, 10000000)
+    for n in (1, 10, 100, 1000, 10000, 100000, 1000000):
+        got = O.to_values(O.limit(r, n))
+        assert got.size == n and int(got[-1]) == n - 1

@@ -158,3 +158,16 @@ def test_bitmap_of_range(gpu):
         assert got.serialize() == O.bitmap_of_range(lo, hi), (lo, hi)
     with pytest.raises(rb.IllegalArgumentException):
         rb.RoaringBitmap.bitmapOfRange(0, (1 << 32) + 1)
+
+
+def test_limit_reference_cases(gpu):
+    """RBT/TestRoaringBitmap.java:136-162 through the GPU, byte-exact to the oracle"""
+    import roaringbitmap_amd as rb
+    i = np.arange(500 * 9943, dtype=np.int64)
+    blocks = O.from_values(i[(i // 9943) % 2 == 0].astype(np.uint32))
+    got = rb.RoaringBitmap(blocks).limit(1000000)
+    assert got.getCardinality() == 1000000 and got.serialize() == O.limit(blocks, 1000000)
+    r = rb.RoaringBitmap.add(rb.RoaringBitmap(), 0, 10000000)
+    for n in (1, 10, 100, 1000, 10000, 100000, 1000000):
+        lim = r.limit(n)
+        assert lim.getCardinality() == n and lim.serialize() == O.limit(r.serialize(), n)
