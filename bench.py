@@ -9,13 +9,15 @@ portable serialization (RB/RoaringArray.java:896-940) are all inside the step.
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per
 GPU.  At N > 1 the headline is ONE C2 pair's RoaringBitmap.and split into key ranges over
 the ranks (strong scaling): each rank computes its key range, the shard
-layout is all-gathered on the device (RCCL) and every rank writes its slice at its global
-place in its own HBM -- no host round trip inside the step (shard.DeviceShard).  The gather
-of the slices to GPU 0 is timed separately (extra.c2_strong.gather_ms) and the gathered
-bitmap's sha is checked against the whole-pair result.  At N = 1 the step is the whole
-pair's AND + serialization.  barrier + synchronize bracket the timed loop and the max
-time over ranks is used.  extra.c2_and_weak keeps the weak-scaling form (an independent
-pair per rank).
+layout is all-gathered on the device (RCCL), every rank writes its slice at its global
+place (shard.DeviceShard.place) and rank 0 receives every slice at its place
+(DeviceShard.gather, point-to-point RCCL): the step ends, like N = 1, with the whole
+serialized bitmap on GPU 0, whose sha is checked against the whole-pair result
+(extra.c2_strong; its ms_per_step_without_gather is the step with the slices left in
+each rank's HBM).  barrier + synchronize bracket the timed loop and the max time over
+ranks is used.  extra.c2_and_weak keeps the weak-scaling form (an independent pair per
+rank).  At N = 1, extra.rank_slice_ms times on this GPU what rank r of N = 2 / 4 / 8
+does per step, for C2 and C3 uniform.
 
 Prints ONE JSON line (rank 0).  Extra fields:
   roofline     - dominant kernel (container compute) achieved algorithmic GB/s vs
@@ -45,9 +47,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 # serialization -- measured faster than 2-16 pipelined key ranges)
 PIPELINED = os.environ.get("RBG_BENCH_PIPE", "0") != "0"
 PIPE_K = int(os.environ.get("RBG_SER_PIPE", "4"))  # key ranges when RBG_BENCH_PIPE=1
-# the dense-range pairwise compute kernel: one 16-wave workgroup per CU (RBG_PW_CU=0: one walk per wave)
-PW_KERNEL = "k_pair_wave" if os.environ.get("RBG_PW_CU", "1") == "0" else "k_pair_cu"
+# the dense-range pairwise compute kernel: one 16-wave workgroup per CU
+PW_KERNEL = "k_pair_cu"
 METRIC = "wide-OR/pairwise-AND input GB/s + % of HBM peak at 1/2/4/8 MI355X"
+EXTRA_STEPS, EXTRA_WARMUP = 20, 3  # floor of every extra's timed steps, and its warmups (independent of --steps)
 
 
 def _pmc_traffic(key="k_pair_wave"):
@@ -80,7 +83,7 @@ def _cpu_info():
     return {"nproc": os.cpu_count(), "affinity": avail, "model": model}
 
 
-def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
+def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or", slices=None):
     """C3 wide OR (or AND) of n synthetic bitmaps, key-range sharded over the ranks.
 
     Each rank generates and reduces only its key slice (equal input bytes).  One step is the
@@ -145,6 +148,10 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         t[0] = tm[0]
     wall, tin, tout = float(t[0]), float(t[1]), float(t[2])
+    if slices is not None:  # one GPU: rank r of N's share of this job (rank_slices)
+        kb = synth_key_bytes(kind, seed, n)
+        slices.update(rank_slices(eng, lambda lo_, hi_: eng.wide(op, b, lo_, hi_),
+                                  lambda nr: shard.key_ranges(kb, nr), steps, warmup))
     eng.release(b)
     ms = wall / steps * 1e3
     ach = (in_bytes + out_bytes) / (kern_ms / 1e3) / 1e9
@@ -170,6 +177,55 @@ def c3_wide_or(eng, kind, n, rank, world, dist, steps, warmup, cdev, op="or"):
                                 "bytes_read_per_launch": int(rd_bytes),
                                 "achieved_GBps": round((rd_bytes + out_bytes) / (kern_ms / 1e3) / 1e9, 1),
                                 "frac": round((rd_bytes + out_bytes) / (kern_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)})}
+
+
+def rank_slices(eng, run_range, ranges_of, steps, warmup):
+    """SURVEY §8(e) projected on one GPU: for N = 2, 4, 8 ranks, what rank r of a key-sharded op does per
+    step -- its key range's op (run_range(lo, hi)), the result layout into a device tensor
+    (rbg_ctx_result_layout_device) and its slice written at its global place from the global layout
+    (rbg_ctx_fetch_shard_device_dyn) -- timed rank by rank on this GPU (wall clock, >= `steps` steps after
+    `warmup`), with the compute kernel's own share from the engine's events.  The global layout is the
+    one the all-gather would deliver (every range run once first).  Left out: the layout all-gather
+    (3 int64 per rank) and rank 0's receive of the other slices (xGMI), which one GPU cannot time.
+    -> {N: {"max_rank_ms", "per_rank_ms", "per_rank_compute_ms", "ranges"}}"""
+    import torch
+    from roaringbitmap_amd import shard
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty(shard.MAX_SERIALIZED, dtype=torch.uint8, device=dev)
+    runb = torch.empty(shard.KEYS, dtype=torch.uint8, device=dev)
+    lay_local = torch.zeros(3, dtype=torch.int64, device=dev)
+    rows = {}
+    for n in (2, 4, 8):
+        ranges = ranges_of(n)
+        lay = torch.zeros(3 * n, dtype=torch.int64, device=dev)
+        torch.cuda.synchronize(dev)  # the allocations' fills before any engine-stream write
+        for r, (lo, hi) in enumerate(ranges):
+            run_range(lo, hi)
+            eng.result_layout_device(lay[3 * r: 3 * r + 3])
+        eng.sync()
+        per, comp = [], []
+        for r, (lo, hi) in enumerate(ranges):
+            def step():
+                run_range(lo, hi)
+                eng.result_layout_device(lay_local)
+                eng.fetch_shard_device_dyn(lay, r, n, out, runb)
+            for _ in range(warmup):
+                step()
+            eng.sync()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                step()
+            eng.sync()
+            per.append(round((time.perf_counter() - t0) / steps * 1e3, 4))
+            eng.profile(steps)
+            for _ in range(steps):
+                run_range(lo, hi)
+            k, ph = eng.profile_read()
+            eng.profile(0)
+            comp.append(round(ph[1] / max(k, 1), 4))
+        rows[str(n)] = {"max_rank_ms": max(per), "per_rank_ms": per, "per_rank_compute_ms": comp,
+                        "ranges": [list(x) for x in ranges]}
+    return rows
 
 
 def c2_weak(rank, world, dist, steps, warmup, cdev):
@@ -279,8 +335,8 @@ def decode_c2(eng, a, steps):
     """Upload + device decode of one serialized C2 operand (Engine.load: pinned staging, one H2D
     copy, header parse, key sort, slot placement, payload copy); wall time per load."""
     x = eng.batch_fetch(a).serialize()
-    b = eng.load([x])
-    eng.release(b)
+    for _ in range(EXTRA_WARMUP):
+        eng.release(eng.load([x]))
     t0 = time.perf_counter()
     for _ in range(steps):
         b = eng.load([x])
@@ -313,7 +369,8 @@ def c2_oneshot(eng, a, b, steps):
         return n
 
     n_out = one()  # warm the one-shot context (staging and result buffers)
-    one()
+    for _ in range(EXTRA_WARMUP - 1):
+        one()
     t0 = time.perf_counter()
     for _ in range(steps):
         one()
@@ -362,7 +419,8 @@ def pq_or_queue(eng, rows, steps):
     try:
         st = eng.batch_stats(b)
         n = st["bitmaps"]
-        eng.wide("priorityqueue_or", b)
+        for _ in range(EXTRA_WARMUP):
+            eng.wide("priorityqueue_or", b)
         eng.sync()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -370,7 +428,8 @@ def pq_or_queue(eng, rows, steps):
             eng.sync()
         ms = (time.perf_counter() - t0) / steps * 1e3
         rs = eng.result_stats()
-        eng.wide("or", b)
+        for _ in range(EXTRA_WARMUP):
+            eng.wide("or", b)
         eng.sync()
         t0 = time.perf_counter()
         for _ in range(steps):
@@ -392,6 +451,9 @@ def run_optimize_c2(eng, a, sa, steps):
     o, _ = eng.run_optimize(a)
     so = eng.batch_stats(o)
     eng.release(o)
+    for _ in range(EXTRA_WARMUP - 1):
+        o, _ = eng.run_optimize(a, answers=False)
+        eng.release(o)
     eng.sync()
     t0 = time.perf_counter()
     for _ in range(steps):
@@ -412,7 +474,7 @@ def ornot_c2(eng, a, b, sa, sb, steps):
     end = 1 << 32
     eng.ornot(a, b, end)
     rs = eng.result_stats()
-    for _ in range(2):
+    for _ in range(EXTRA_WARMUP):
         eng.ornot(a, b, end)
         eng.serialize()
     eng.sync()
@@ -728,9 +790,10 @@ def main():
         dshard = shard.DeviceShard(eng, rank, world, torch.device("cuda", local),
                                    torch.device("cuda", local) if cdev == "cuda" else "cpu")
 
-        def c2_step():  # this rank's key range of ONE pair -> its slice at its global place in its HBM
+        def c2_step():  # this rank's key range of ONE pair -> its slice at its global place -> one bitmap on GPU 0
             eng.pairwise("and", a, b, key_lo=key_lo, key_hi=key_hi)
             dshard.place()
+            dshard.gather()  # rank 0 receives every slice at its place: the step ends, like N = 1, with one bitmap
     elif PIPELINED:
         def c2_step():  # RoaringBitmap.and(x1, x2) + serialize as one pipeline (rbg_ctx_pairwise_serialized):
             eng.pairwise_serialized("and", a, b)  # key range r placed and copied while range r + 1 computes
@@ -769,19 +832,23 @@ def main():
     ph_live = [x / max(n_live, 1) for x in ph_live]
 
     strong_info = None
-    if strong:  # the gather of the slices to GPU 0, timed apart; its bytes against the whole pair's
-        ks_g = max(2, args.steps // 4)
+    if strong:  # the step without its gather (slices left in each rank's HBM), and the gathered bitmap's sha
+        ks_g = max(EXTRA_STEPS, args.steps // 4)
         barrier()
         tg = time.perf_counter()
         for _ in range(ks_g):
-            out = dshard.gather()
+            eng.pairwise("and", a, b, key_lo=key_lo, key_hi=key_hi)
+            dshard.place()
+        eng.sync()
         barrier()
-        g_ms = (time.perf_counter() - tg) / ks_g * 1e3
+        ng_ms = (time.perf_counter() - tg) / ks_g * 1e3
+        out = dshard.gather()
         got = hashlib.sha256(bytes(out.cpu().numpy().tobytes())).hexdigest()[:16] if rank == 0 else None
         lay = dshard.layout()
         strong_info = {"workload": f"C2 RoaringBitmap.and of ONE pair, key-range sharded over {world} GPUs; the step "
-                                   f"ends with every slice at its global place in its rank's HBM",
-                       "rank0_keys": [key_lo, key_hi], "gather_to_gpu0_ms": round(g_ms, 4),
+                                   f"ends with the whole serialized bitmap on GPU 0 (slices placed on the device, the "
+                                   f"layout all-gathered, every slice received by rank 0 at its place)",
+                       "rank0_keys": [key_lo, key_hi], "ms_per_step_without_gather": round(ng_ms, 4),
                        "result_serialized_bytes": int(lay.nbytes), "result_sha16": got,
                        "sha_equals_whole_pair_result": (got == rs["sha16"]) if rank == 0 else None,
                        "layout_exchange": "device all-gather (RCCL)" if cdev == "cuda" else "gloo (host)"}
@@ -857,26 +924,40 @@ def main():
                      "achieved_GBps": round(in_bytes / (card_kern / 1e3) / 1e9, 1),
                      "frac": round(in_bytes / (card_kern / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                      "traffic": _pmc_traffic("k_pair_wave_card")}}
-    ks = max(3, args.steps // 4)
+    ks = max(EXTRA_STEPS, args.steps // 4)  # every extra: >= 20 timed steps after EXTRA_WARMUP warmups
     # a stream of independent C2 ANDs issued alternately on two engine contexts (two HIP streams):
     # one op's serialization overlaps the next op's compute (throughput of concurrent calls, as a
     # server would issue them; the headline above is one call after another)
     run_extra("c2_and_two_streams", lambda: c2_two_streams(eng, a, b, in_bytes, args.steps, args.warmup))
     if strong:  # the weak-scaling form beside the key-sharded headline
         extra["c2_strong"] = strong_info
-        run_extra("c2_and_weak", lambda: c2_weak(rank, world, dist, ks, 1, cdev))
+        run_extra("c2_and_weak", lambda: c2_weak(rank, world, dist, ks, EXTRA_WARMUP, cdev))
+    # one GPU: what rank r of N = 2 / 4 / 8 does per step, for C2 (equal key ranges, as the strong headline)
+    # and C3 uniform (equal input bytes): the fixed costs that cap a speed-up before an 8-GPU node exists
+    slices = {"c3_uniform_or": {}} if world == 1 else None
+    if world == 1:
+        run_extra("rank_slice_ms", lambda: {
+            "what": rank_slices.__doc__.split("->")[0].strip(),
+            "c2_and": rank_slices(eng, lambda lo_, hi_: eng.pairwise("and", a, b, key_lo=lo_, key_hi=hi_),
+                                  lambda nr: [((65536 * r) // nr, (65536 * (r + 1)) // nr) for r in range(nr)],
+                                  ks, EXTRA_WARMUP),
+            "c2_and_n1_ms_per_step": round(wall_max / args.steps * 1e3, 4),
+            "c3_uniform_or": slices["c3_uniform_or"]})
     if args.c3_n > 0:
         for kind, name in ((1, "c3_uniform_or"), (2, "c3_clustered_or")):
-            run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, 1, cdev))
+            run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, EXTRA_WARMUP, cdev,
+                                                         slices=slices["c3_uniform_or"] if slices and kind == 1
+                                                         else None))
         # FastAggregation.and (N > 10: workShyAnd): per key the chain stops once the
         # intersection is empty, so it reads far less than the algorithmic input bytes
         for kind, name in ((1, "c3_uniform_and"), (2, "c3_clustered_and")):
-            run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, 1, cdev,
-                                                         op="and"))
+            run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, EXTRA_WARMUP,
+                                                         cdev, op="and"))
     if args.c4_pairs > 0:
-        run_extra("c4_batch_and_card", lambda: c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, ks, 1, cdev))
+        run_extra("c4_batch_and_card", lambda: c4_batch_and_card(eng, args.c4_pairs, rank, world, dist, ks,
+                                                                  EXTRA_WARMUP, cdev))
     if args.c5_rows > 0:
-        run_extra("c5_bsi_range_sum", lambda: c5_bsi(eng, args.c5_rows, rank, world, dist, ks, 1, cdev))
+        run_extra("c5_bsi_range_sum", lambda: c5_bsi(eng, args.c5_rows, rank, world, dist, ks, EXTRA_WARMUP, cdev))
 
     if args.c3_n > 0 or args.c4_pairs > 0 or args.c5_rows > 0:
         run_extra("run_optimize_c2", lambda: run_optimize_c2(eng, a, sa, ks))
@@ -884,8 +965,8 @@ def main():
             run_extra("ornot_c2", lambda: ornot_c2(eng, a, b, sa, sb, ks))
         run_extra("decode_c2", lambda: decode_c2(eng, a, ks))
         if rank == 0:
-            run_extra("c2_and_oneshot", lambda: c2_oneshot(eng, a, b, max(3, ks // 2)))
-            run_extra("pq_or_bsi_slices", lambda: pq_or_queue(eng, 10 ** 8, 3))
+            run_extra("c2_and_oneshot", lambda: c2_oneshot(eng, a, b, ks))
+            run_extra("pq_or_bsi_slices", lambda: pq_or_queue(eng, 10 ** 8, ks))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

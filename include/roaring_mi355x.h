@@ -315,6 +315,15 @@ int rbg_ctx_load_separate(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t
 /* Parse + upload n serialized bitmaps as one batch; returns a batch id >= 0. */
 int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n,
                  int32_t* batch);
+/* The same for a batch that feeds wide ops: when every container is an array, the array payloads
+ * stay packed back to back at 2 B granularity as in the portable format (RB/RoaringArray.java:547-629)
+ * instead of 16 B slots -- the layout FastAggregation.or / xor / workShyAnd (and the queue, horizontal
+ * and parallel forms) read fastest.  Such a batch serves those wide ops, the wide cardinalities and
+ * fetches; pairwise, BSI, runOptimize, naive_and chains and batched andCardinality refuse it
+ * (RBG_ERR_ILLEGAL_ARGUMENT).  A batch holding bitmap or run containers is decoded as rbg_ctx_load does.
+ * Replaces nothing in the reference: its deserializer keeps each container's own array (same bytes). */
+int rbg_ctx_load_packed(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n,
+                        int32_t* batch);
 /* Synthetic batches generated on the device (bench configs).
  *   kind 0: C2 operand: one bitmap, all 65536 keys, per key A/B/R with p=1/3 (seed)
  *   kind 1: C3 uniform: n bitmaps x keys [key_lo,key_hi), ~15.26 values per (bitmap,key)

@@ -49,7 +49,7 @@ EXPORTED = [
     "rbg_ctx_run_optimize", "rbg_run_optimize_many", "rbg_ctx_batch_fetch_range",
     "rbg_ctx_fetch_shard_device", "rbg_bsi_compare_buffer", "rbg_ctx_bsi_buffer",
     "rbg_ctx_result_layout_device", "rbg_ctx_fetch_shard_device_dyn", "rbg_pairwise_inplace",
-    "rbg_ctx_load_separate", "rbg_ornot", "rbg_ctx_ornot", "rbg_range_mut", "rbg_ctx_range_mut", "rbg_add_offset", "rbg_ctx_add_offset", "rbg_select_range", "rbg_remove_run_compression", "rbg_limit", "rbg_bitmap_of_range",
+    "rbg_ctx_load_separate", "rbg_ctx_load_packed", "rbg_ornot", "rbg_ctx_ornot", "rbg_range_mut", "rbg_ctx_range_mut", "rbg_add_offset", "rbg_ctx_add_offset", "rbg_select_range", "rbg_remove_run_compression", "rbg_limit", "rbg_bitmap_of_range",
 ]
 
 _lib = None
@@ -100,6 +100,7 @@ def _declare(L):
     L.rbg_ctx_sync.argtypes = [vp]
     L.rbg_ctx_load.argtypes = [vp, P(ctypes.c_char_p), P(sz), sz, P(i32)]
     L.rbg_ctx_load_separate.argtypes = [vp, P(ctypes.c_char_p), P(sz), sz, P(i32)]
+    L.rbg_ctx_load_packed.argtypes = [vp, P(ctypes.c_char_p), P(sz), sz, P(i32)]
     L.rbg_ctx_synth.argtypes = [vp, ctypes.c_int, ctypes.c_uint64, sz, ctypes.c_int, ctypes.c_int, P(i32)]
     L.rbg_ctx_release.argtypes = [vp, i32]
     L.rbg_ctx_batch_stats.argtypes = [vp, i32, P(ctypes.c_int64)]
@@ -173,6 +174,11 @@ class TruncatedInput(RoaringError, OSError):
 
 class IllegalArgumentException(RoaringError, ValueError):
     pass
+
+
+class ArrayIndexOutOfBoundsException(RoaringError, IndexError):
+    """java.lang.ArrayIndexOutOfBoundsException, where the reference's own control flow throws it on
+    caller-supplied input (FastAggregation.workAndMemoryShyAnd with a dirty buffer, RB/FastAggregation.java:541-548)"""
 
 
 class DeviceError(RoaringError, RuntimeError):

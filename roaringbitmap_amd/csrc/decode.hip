@@ -22,7 +22,10 @@
 //                 within a key), the key CSR, slot sizes, an exclusive scan of
 //                 them, then k_dec_fill: one wave per container writes its
 //                 descriptor and copies its payload into its slot (A slots padded
-//                 with the last value, R slots with the u16 pad in front).
+//                 with the last value, R slots with the u16 pad in front).  A batch of
+//                 arrays alone can be decoded packed instead: array payloads back to back
+//                 at 2 B granularity, exactly as in the portable format (RB/RoaringArray.java
+//                 :547-629), the layout the wide kernels read fastest.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -281,11 +284,11 @@ __device__ __forceinline__ uint64_t dec_slot_bytes(uint32_t kind, uint32_t len) 
 
 __global__ __launch_bounds__(256) void k_dec_sizes(const DecCtr* __restrict__ q, const uint32_t* __restrict__ perm,
                                                    uint64_t C, uint64_t* __restrict__ size,
-                                                   unsigned long long* __restrict__ totals) {
+                                                   unsigned long long* __restrict__ totals, int packed) {
   uint64_t cnt[3] = {0, 0, 0}, big = 0;
   for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < C; p += (uint64_t)gridDim.x * blockDim.x) {
     const DecCtr c = q[perm ? perm[p] : p];
-    size[p] = dec_slot_bytes(c.kind, c.len);
+    size[p] = packed && c.kind == DK_A ? (uint64_t)c.len : dec_slot_bytes(c.kind, c.len);
     cnt[c.kind]++;
     if (c.len > 8194) big += c.len;
   }
@@ -301,7 +304,7 @@ __global__ __launch_bounds__(256) void k_dec_sizes(const DecCtr* __restrict__ q,
     wsum[threadIdx.x >> 6][3] = big;
   }
   __syncthreads();
-  if (threadIdx.x < 4) {
+  if (totals && threadIdx.x < 4) {
     const unsigned long long v =
         wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] + wsum[3][threadIdx.x];
     if (v) atomicAdd(&totals[threadIdx.x], v);
@@ -313,7 +316,7 @@ __global__ __launch_bounds__(256) void k_dec_fill(const uint8_t* __restrict__ ra
                                                   const uint64_t* __restrict__ slot, uint64_t C,
                                                   CDesc* __restrict__ desc, uint16_t* __restrict__ keys,
                                                   uint32_t* __restrict__ bm, uint8_t* __restrict__ payload,
-                                                  uint64_t* __restrict__ bm_card) {
+                                                  uint64_t* __restrict__ bm_card, int packed) {
   const int lane = lane_id();
   const uint64_t nw = (uint64_t)gridDim.x * 4;
   for (uint64_t p = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); p < C; p += nw) {
@@ -323,7 +326,7 @@ __global__ __launch_bounds__(256) void k_dec_fill(const uint8_t* __restrict__ ra
     const uint64_t off = slot[p];
     uint8_t* dst = payload + off + (c.kind == DK_R ? 2 : 0);
     group_copy<64>(dst, raw + c.src, c.len, lane);
-    if (c.kind == DK_A) {  // pad the slot to 16 B with the last value
+    if (c.kind == DK_A && !packed) {  // pad the slot to 16 B with the last value
       const uint16_t last = (uint16_t)rd16b(raw + c.src + c.len - 2);
       uint16_t* d16 = reinterpret_cast<uint16_t*>(payload + off);
       for (uint32_t v = c.len / 2 + lane; v < ((c.len + 15) & ~15u) / 2; v += 64) d16[v] = last;
@@ -397,17 +400,18 @@ void launch_dec_key_off(hipStream_t s, const uint16_t* skey, uint64_t C, uint32_
 }
 
 void launch_dec_sizes(hipStream_t s, const DecCtr* q, const uint32_t* perm, uint64_t C, uint64_t* size,
-                      unsigned long long* totals) {
+                      unsigned long long* totals, bool packed) {
   if (!C) return;
-  hipLaunchKernelGGL(k_dec_sizes, dim3(grid_of(C, 256, 1024)), dim3(256), 0, s, q, perm, C, size, totals);
+  hipLaunchKernelGGL(k_dec_sizes, dim3(grid_of(C, 256, 1024)), dim3(256), 0, s, q, perm, C, size, totals,
+                     packed ? 1 : 0);
 }
 
 void launch_dec_fill(hipStream_t s, const uint8_t* raw, const DecCtr* q, const uint16_t* qkey, const uint32_t* perm,
                      const uint64_t* slot, uint64_t C, CDesc* desc, uint16_t* keys, uint32_t* bm, uint8_t* payload,
-                     uint64_t* bm_card) {
+                     uint64_t* bm_card, bool packed) {
   if (!C) return;
   hipLaunchKernelGGL(k_dec_fill, dim3(grid_of(C, 4, 8192)), dim3(256), 0, s, raw, q, qkey, perm, slot, C, desc, keys,
-                     bm, payload, bm_card);
+                     bm, payload, bm_card, packed ? 1 : 0);
 }
 
 }  // namespace rbg

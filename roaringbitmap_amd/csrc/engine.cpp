@@ -577,7 +577,7 @@ static int ctx_upload_raw(Ctx* c, const uint8_t* const* bufs, const size_t* lens
 // key_major: containers sorted by (key, input) with a key CSR (operands of every op);
 // otherwise input order (bitmap-major, batched andCardinality)
 static int ctx_decode_raw(Ctx* c, const uint64_t* off, const size_t* lens, size_t n, bool key_major,
-                          int32_t* out_id) {
+                          int32_t* out_id, bool pack_arrays = false) {
   DecBufs& d = c->dec;
   hipStream_t s = c->stream;
   std::vector<uint64_t> meta(2 * n + 2, 0);  // in_off[n], in_len[n]
@@ -674,12 +674,24 @@ static int ctx_decode_raw(Ctx* c, const uint64_t* off, const size_t* lens, size_
   if (h[0]) return dec_report(c, n);
   for (int k = 0; k < 3; k++) b.n_kind[k] = (int64_t)h[2 + k];
   b.max_ser = h[5];
+  // a key-major batch of arrays alone, for the wide ops: the array payloads packed as in the portable
+  // format (2 B granularity) instead of 16 B slots -- the wide kernels' fastest layout
+  const bool packed = pack_arrays && key_major && C > 0 && b.n_kind[DK_B] == 0 && b.n_kind[DK_R] == 0;
+  if (packed) {
+    launch_dec_sizes(s, d.q.as<DecCtr>(), perm, C, d.size.as<uint64_t>(), nullptr, true);
+    launch_exclusive_scan(s, d.size.as<uint64_t>(), d.size.as<uint64_t>(), C, d.cpart.as<uint64_t>(),
+                          reinterpret_cast<uint64_t*>(sc + 6));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h, sc, 64, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    b.packed = true;
+  }
   b.payload_bytes = h[6];
   CHK(b.payload.ensure(b.payload_bytes + 64));
   dbg(s, "load: sizes + payload alloc");
   launch_dec_fill(s, c->raw.as<uint8_t>(), d.q.as<DecCtr>(), d.qkey.as<uint16_t>(), perm, d.size.as<uint64_t>(), C,
                   b.desc.as<CDesc>(), b.keys.as<uint16_t>(), b.bm.as<uint32_t>(), b.payload.as<uint8_t>(),
-                  d.card.as<uint64_t>());
+                  d.card.as<uint64_t>(), packed);
   HIPCHK(hipGetLastError());
   std::vector<uint64_t> nctr(n), card(n), cons(n);
   if (n) {
@@ -708,14 +720,16 @@ static int ctx_decode_raw(Ctx* c, const uint64_t* off, const size_t* lens, size_
 }
 
 static int ctx_load_impl(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, bool key_major,
-                         int32_t* out_id) {
+                         int32_t* out_id, bool pack_arrays = false) {
   std::vector<uint64_t> off;
   CHK(ctx_upload_raw(c, bufs, lens, n, &off));
-  return ctx_decode_raw(c, off.data(), lens, n, key_major, out_id);
+  return ctx_decode_raw(c, off.data(), lens, n, key_major, out_id, pack_arrays);
 }
 
-static int ctx_load(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out_id) {
-  return ctx_load_impl(c, bufs, lens, n, true, out_id);
+// pack_arrays: a batch of arrays alone is decoded packed (wide ops and fetches only, see Batch::packed)
+static int ctx_load(Ctx* c, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* out_id,
+                    bool pack_arrays = false) {
+  return ctx_load_impl(c, bufs, lens, n, true, out_id, pack_arrays);
 }
 
 // n serialized bitmaps in ONE upload, each decoded into a batch of its own (the operands of a
@@ -1178,10 +1192,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   // RBG_PW_BALANCE=0: the direct form, tasks in key order)
   const char* bal_env = getenv("RBG_PW_BALANCE");
   const bool balanced = direct && (!bal_env || atoi(bal_env) != 0);
-  // ... run by one 16-wave workgroup per CU that claims the CU's tasks through LDS (k_pair_cu;
-  // RBG_PW_CU=0: one static walk per wave, k_pair_wave<..., 2>)
-  const char* cu_env = getenv("RBG_PW_CU");
-  const bool cu_pool = balanced && (!cu_env || atoi(cu_env) != 0);
+  // ... run by one 16-wave workgroup per CU that claims the CU's tasks through LDS (k_pair_cu)
   if (balanced)
     launch_plan_balanced(s, plan_op, card_only ? 1 : 0, key_lo, (uint32_t)nkeys, A->key_off.as<uint32_t>(), da,
                          A->payload.as<uint8_t>(), B->key_off.as<uint32_t>(), db, B->payload.as<uint8_t>(),
@@ -1192,7 +1203,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
   const int grid = grid_for(((direct ? nkeys : ub) + 3) / 4, 16384);
   launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(),
                   A->payload.as<uint8_t>(), B->payload.as<uint8_t>(), oc, c->task_card.as<uint32_t>(),
-                  direct ? &pd : nullptr, balanced, cu_pool);
+                  direct ? &pd : nullptr, balanced);
   dbg(s, "pairwise");
   c->mark(2);
   if (card_only) {
@@ -1561,12 +1572,37 @@ static int ctx_pq(Ctx* c, int op, Batch* B, int32_t id, int key_lo, int key_hi) 
 // FastAggregation dispatch (RB/FastAggregation.java:26-101,653-666,823-836)
 // start_override >= 0: naive_and starts from that input (key-range shards pass the
 // input with the fewest containers over the WHOLE universe, RB/FastAggregation.java:333-339)
+// Wide ops whose kernels read array payloads at any 2 B alignment (a packed batch): every op that runs
+// the per-key OR / XOR kernels or workShyAnd (k_wide, k_shy_wave, and the queue / horizontal / parallel
+// forms, which reduce to them on a batch without run containers).  naive_and's chains (N <= 10, the
+// Iterator forms, the buffer package's and chains) materialise through the slot-aligned helpers.
+static bool wide_reads_packed(int op, size_t n) {
+  switch (op) {
+    case RBG_WIDE_OR:
+    case RBG_WIDE_XOR:
+    case RBG_WIDE_WORKSHY_AND:
+    case RBG_WIDE_PARALLEL_OR:
+    case RBG_WIDE_PARALLEL_XOR:
+    case RBG_WIDE_BUFFER_OR_MUTABLE:
+    case RBG_WIDE_HORIZONTAL_OR:
+    case RBG_WIDE_HORIZONTAL_XOR:
+    case RBG_WIDE_PQ_OR:
+    case RBG_WIDE_PQ_XOR: return true;
+    case RBG_WIDE_AND: return n > 10;  // FastAggregation.and: workShyAnd above 10 inputs (RB/FastAggregation.java:38)
+    default: return false;
+  }
+}
+
 static int ctx_wide(Ctx* c, int op, int32_t id, int key_lo, int key_hi, const int32_t* ids, bool card_only,
                     int* host_card_out, bool* host_card_valid, int32_t start_override = -1) {
   Batch* B;
   CHK(get_batch(c, id, &B));
   if (!B->key_major) {
     set_err("wide ops need a key-major batch");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  if (B->packed && !card_only && !wide_reads_packed(op, B->n_bm)) {
+    set_err("this wide op needs slot-aligned payloads (load the batch without packing)");
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   key_lo = std::max(0, key_lo);
@@ -2494,7 +2530,7 @@ int rbg_wide(int op, const uint8_t* const* bufs, const size_t* lens, const int32
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
   int32_t id;
-  CHK(ctx_load(c, bufs, lens, n, &id));
+  CHK(ctx_load(c, bufs, lens, n, &id, wide_reads_packed(op, n)));
   g.ids.push_back(id);
   int hc;
   bool hv;
@@ -2804,6 +2840,11 @@ int rbg_ctx_load_separate(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t
 int rbg_ctx_load(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* batch) {
   CHK(enter(&ctx->c));
   return ctx_load(&ctx->c, bufs, lens, n, batch);
+}
+int rbg_ctx_load_packed(rbg_ctx* ctx, const uint8_t* const* bufs, const size_t* lens, size_t n, int32_t* batch) {
+  if (!ctx || !batch) return RBG_ERR_ILLEGAL_ARGUMENT;
+  CHK(enter(&ctx->c));
+  return ctx_load(&ctx->c, bufs, lens, n, batch, true);
 }
 int rbg_ctx_release(rbg_ctx* ctx, int32_t batch) {
   Ctx& c = ctx->c;

@@ -258,11 +258,11 @@ struct PwDirect {
 };
 // direct: null = tasks / nt from launch_plan_pairwise; balanced (with direct): tasks / nt[0..1] from
 // launch_plan_balanced, records at key positions (direct->key_lo)
-// balanced: k_plan_balanced's list (dense ranges); cu_pool: that list run by k_pair_cu (one 16-wave
-// workgroup per CU, tasks claimed from the CU's share) instead of the static per-wave walk
+// balanced: k_plan_balanced's list (dense ranges), run by k_pair_cu (one 16-wave workgroup per CU, tasks
+// claimed from the CU's share)
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt,
                      const uint8_t* pa, const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct,
-                     bool balanced = false, bool cu_pool = false);
+                     bool balanced = false);
 // dense key ranges: every key's task resolved and ordered by estimated cost within its 256-key segment
 // (heaviest first, rotated by the segment index) into tasks[]; n_tasks[0] = n_tasks[1] = nkeys (records
 // and list positions, one per key: keys without a task are marked, with an empty record / a zero count)
@@ -270,7 +270,7 @@ void launch_plan_balanced(hipStream_t s, int op, int mode, int key_lo, uint32_t 
                           const CDesc* da, const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb,
                           PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint32_t* task_card, uint64_t* zlb,
                           uint64_t* ztile);
-// diagnostic build (-DRBG_STAMPS=1): per-phase clock totals of the pairwise kernel
+// retired diagnostic (per-phase clock totals of the pairwise kernel): zeroes
 void debug_stamps(uint64_t* out20, bool reset);
 // diagnostic build (-DRBG_BSI_STAMPS=1): per-phase clock totals of k_bsi_reg
 void debug_bsi_stamps(uint64_t* out20, bool reset);
@@ -523,11 +523,13 @@ size_t dec_sort_temp_bytes(uint64_t C);
 int launch_dec_sort(hipStream_t s, void* temp, size_t temp_bytes, const uint16_t* qkey, uint16_t* skey,
                     uint32_t* iota, uint32_t* perm, uint64_t C);
 void launch_dec_key_off(hipStream_t s, const uint16_t* skey, uint64_t C, uint32_t* key_off);
-// perm null: input order.  totals += {#A, #B, #R, bytes of payloads above 8194 B}
+// perm null: input order.  totals (may be null) += {#A, #B, #R, bytes of payloads above 8194 B}.
+// packed: array payloads at their exact length (2 B granularity, as in the portable format) instead of
+// 16 B slots -- only for batches of arrays alone (every other slot stays 16 B aligned that way)
 void launch_dec_sizes(hipStream_t s, const DecCtr* q, const uint32_t* perm, uint64_t C, uint64_t* size,
-                      unsigned long long* totals);
+                      unsigned long long* totals, bool packed = false);
 void launch_dec_fill(hipStream_t s, const uint8_t* raw, const DecCtr* q, const uint16_t* qkey, const uint32_t* perm,
                      const uint64_t* slot, uint64_t C, CDesc* desc, uint16_t* keys, uint32_t* bm, uint8_t* payload,
-                     uint64_t* bm_card);  // bm_card: run-container cardinalities are re-derived from the runs
+                     uint64_t* bm_card, bool packed = false);  // bm_card: run cardinalities are re-derived from the runs
 
 }  // namespace rbg

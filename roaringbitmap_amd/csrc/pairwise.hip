@@ -176,81 +176,20 @@ constexpr int kWaves = 4;  // waves per workgroup
 constexpr int kWaveLds = 2558;
 static_assert(kWaveLds >= 2048, "the 8 KiB bitmap map / staging area");
 
-// Diagnostic build only (-DRBG_STAMPS=1): per-phase shader-clock totals of the
-// pairwise kernel, read back with rbg_debug_stamps.  The stamps go to a buffer of
-// their own; no result depends on them.
-// Diagnostic build only (-DRBG_WAVE_PROBE=1, scripts/xcd_probe.py): per wave of the direct-mode
-// kernel, its start / end on the constant 100 MHz clock (s_memrealtime) and on the shader clock
-// (s_memtime), its XCC_ID and task count: three plain 16 B stores at the wave's end -- nothing per
-// task, no atomics, so the kernel runs at production speed.
-#if RBG_WAVE_PROBE
-__device__ uint4 g_probe[3 * 16384];
-__device__ __forceinline__ void probe_store(uint64_t r0, uint64_t m0, uint32_t ntask,
-                                            uint32_t wid = blockIdx.x * 4 + (threadIdx.x >> 6)) {
-  const uint64_t r1 = __builtin_amdgcn_s_memrealtime(), m1 = __builtin_amdgcn_s_memtime();
-  uint32_t xcc;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  if (lane_id() == 0 && wid < 16384) {
-    g_probe[3 * wid] = make_uint4((uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32));
-    g_probe[3 * wid + 1] = make_uint4((uint32_t)m0, (uint32_t)(m0 >> 32), (uint32_t)m1, (uint32_t)(m1 >> 32));
-    g_probe[3 * wid + 2] = make_uint4(xcc, ntask, 1u, 0u);
-  }
-}
-#endif
-
-#if RBG_STAMPS
-__device__ unsigned long long g_stamp[20];
-__device__ uint4 g_wave[16384];  // per wave: start, end (realtime), XCC_ID, HW_ID
-// per-wave accumulators (registers); flushed once at the end of the kernel
-struct StampAcc {
-  uint64_t v[12];
-};
-#define STAMP_DECL uint64_t st_prev = __builtin_amdgcn_s_memtime();
-#define STAMP(ph)                                          \
-  do {                                                     \
-    const uint64_t st_now = __builtin_amdgcn_s_memtime();  \
-    sacc.v[ph] += st_now - st_prev;                        \
-    st_prev = st_now;                                      \
-  } while (0)
-#define SACC_PARAM , StampAcc& sacc
-#define SACC_ARG , sacc
-#else
-#define SACC_PARAM
-#define SACC_ARG
-#define STAMP_DECL
-#define STAMP(ph) \
-  do {            \
-  } while (0)
-#endif
 
 // Wave priority: a task runs at priority 3 until its operand loads have been
-// consumed, then drops to 0, so waves that are issuing loads win instruction
+// consumed, then drops, so waves that are issuing loads win instruction
 // arbitration over waves in their compute / output phases and more of the CU's
-// memory requests are in flight (C2 AND -1 %, andCardinality -2.5 %).
-// The per-wave probe shows the workgroups of a CU finishing in dispatch order (mean wave end 154 / 162 /
-// 169 / 178 us for the 1st..4th workgroup of a CU, round 5): the issue arbitration favours the oldest
-// waves at equal priority.  RBG_PRIO_TIER (scripts/gpu_r5d.sh): 0: compute phases at priority 0,
-// 1: at the workgroup's dispatch tier (younger = higher; reverses the order, the spread stays),
-// 2: no priorities, 3 (kept): tier / 2 -- with the balanced task order, the AND kernel 0.244 -> 0.233 ms.
-#ifndef RBG_PRIO_TIER
-#define RBG_PRIO_TIER 3
-#endif
-__device__ __forceinline__ void prio_hi() {
-#if RBG_PRIO_TIER != 2
-  __builtin_amdgcn_s_setprio(3);
-#endif
-}
+// memory requests are in flight (C2 AND -1 %, andCardinality -2.5 %).  The per-wave probe
+// (round 5, profiles/r05/experiments/xcd_probe_*) showed the workgroups of a CU finishing in
+// dispatch order at equal priority (the issue arbitration favours the oldest waves), so the
+// compute / output phases run at half the workgroup's dispatch tier, (blockIdx * 4 / grid) / 2:
+// with the balanced task order the AND kernel 0.244 -> 0.233 ms (profiles/r05/experiments/c2_prio_tiers.txt).
+__device__ __forceinline__ void prio_hi() { __builtin_amdgcn_s_setprio(3); }
 __device__ __forceinline__ void prio_lo() {
-#if RBG_PRIO_TIER == 1 || RBG_PRIO_TIER == 3
-  uint32_t tier = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u) / gridDim.x);
-  if (RBG_PRIO_TIER == 3) tier >>= 1;
+  const uint32_t tier = __builtin_amdgcn_readfirstlane((blockIdx.x * 4u) / gridDim.x) >> 1;
   if (tier == 0) __builtin_amdgcn_s_setprio(0);
-  else if (tier == 1) __builtin_amdgcn_s_setprio(1);
-  else if (tier == 2) __builtin_amdgcn_s_setprio(2);
-  else __builtin_amdgcn_s_setprio(3);
-#elif RBG_PRIO_TIER == 0
-  __builtin_amdgcn_s_setprio(0);
-#endif
+  else __builtin_amdgcn_s_setprio(1);
 }
 
 // Filter path: AND with an array operand and ANDNOT of an array c1 always give an
@@ -262,8 +201,7 @@ __device__ __forceinline__ void prio_lo() {
 template <int OP, int MODE>
 __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard, const uint8_t* pslot, int mkind,
                                             int mcard, const uint8_t* mslot, const OutCtx& oc, uint32_t* task_card,
-                                            uint32_t* lds SACC_PARAM) {
-  STAMP_DECL
+                                            uint32_t* lds) {
   // the array's values are requested first, so their memory latency overlaps the
   // map construction (one round trip per task instead of two)
   const int l = lane_id();
@@ -274,7 +212,6 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
   for (int j = 0; j < 8; j++) v[j] = (64 * j + l < nvec) ? ld_in(pv + 64 * j) : make_uint4(0, 0, 0, 0);
   w_map_lds(mkind, mcard, mslot, lds);
   prio_lo();
-  STAMP(4);
   uint32_t hit[8];
   int cnt = 0;
 #pragma unroll
@@ -287,21 +224,12 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
       // hardware shift reads only the low 5 bits, so no masking); the tail of
       // the array is masked once per vector, not per value
       uint32_t h = 0;
-#if RBG_EXP_PROBE_LIN  // counter attribution only (wrong results): lane-linear, conflict-free probes
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const uint32_t wi = w[i >> 1];
-        const uint32_t word = lds[((i & 1) ? bfe_hi_word(wi) & 64u : bfe_lo_word(wi) & 64u) + l];
-        h |= bit_at(word, (i & 1) ? (wi >> 16) : wi) << i;
-      }
-#else
 #pragma unroll
       for (int i = 0; i < 8; i++) {
         const uint32_t wi = w[i >> 1];
         const uint32_t word = lds[(i & 1) ? bfe_hi_word(wi) : bfe_lo_word(wi)];
         h |= bit_at(word, (i & 1) ? (wi >> 16) : wi) << i;
       }
-#endif
       if (OP == OP_ANDNOT) h = ~h & 0xFFu;
       const int rem = pcard - first;
       hit[j] = rem >= 8 ? h : h & ((1u << max(rem, 0)) - 1u);
@@ -310,7 +238,6 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
   }
   if (MODE == 1) {
     const int c = wave_sum_i(cnt);
-    STAMP(5);
     if (l == 0) task_card[t] = (uint32_t)c;
     return;
   }
@@ -354,16 +281,14 @@ __device__ __forceinline__ void filter_task(uint32_t t, uint32_t key, int pcard,
   const uint4* sv = reinterpret_cast<const uint4*>(lds);
   uint4* dv = reinterpret_cast<uint4*>(slot);
   for (int k = l; k < (2 * c + 15) >> 4; k += 64) dv[k] = sv[k];  // the slot has room for the rounded tail
-  STAMP(5);
   // empty results are dropped (RB/RoaringBitmap.java:389,456)
   w_place(t, c > 0, slot, false, lds, 2u * (uint32_t)c, (uint32_t)c, key, DK_A, oc);
-  STAMP(6);
 }
 
 // Filter-class task (pass-through clone, or a filter), one wave, wave-uniform branches.
 template <int OP, int MODE>
 __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
   const int ka = tk.kind_a, kb = tk.kind_b;
   if (ka == kAbsent || kb == kAbsent) {  // unmatched key: clone (appendCopy), RB/RoaringArray.java:184-205
     if (MODE == 0) {
@@ -382,9 +307,9 @@ __device__ __forceinline__ void filter_class_task(uint32_t t, const PTask& tk, c
   const uint8_t* sb = pb + tk.slot_b;
   // filter the array (A & A: the smaller one; A \ x: c1) through a map of the other operand
   if (ka == DK_A && (OP == OP_ANDNOT || kb != DK_A || ca <= cb))
-    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, oc, task_card, lds SACC_ARG);
+    filter_task<OP, MODE>(t, tk.key, ca, sa, kb, cb, sb, oc, task_card, lds);
   else
-    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, oc, task_card, lds SACC_ARG);
+    filter_task<OP, MODE>(t, tk.key, cb, sb, ka, ca, sa, oc, task_card, lds);
 }
 
 // R AND R in the run domain (RB/RunContainer.java and(RunContainer)): the
@@ -521,16 +446,13 @@ __device__ __forceinline__ bool rr_and_task(uint32_t t, const PTask& tk, const u
 // staged in LDS).  One wave, wave-uniform branches.
 template <int OP, int MODE>
 __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+                                                  const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
   const int ka = tk.kind_a, kb = tk.kind_b;
   const int ca = (int)tk.card_a, cb = (int)tk.card_b;
   if (OP == OP_AND && ka == DK_R && kb == DK_R && rr_and_task<MODE>(t, tk, pa, pb, oc, task_card, lds)) return;
-  STAMP_DECL
   WCtr x;
   w_materialize(CDesc{tk.slot_a, tk.card_a, tk.key, (uint8_t)ka, 0}, pa, lds, x);
-  STAMP(0);
   w_combine<OP>(CDesc{tk.slot_b, tk.card_b, tk.key, (uint8_t)kb, 0}, pb, lds, x);
-  STAMP(1);
   prio_lo();
   const int c = w_card(x);
   if (MODE == 1) {
@@ -543,20 +465,16 @@ __device__ __forceinline__ void bitmap_class_task(uint32_t t, const PTask& tk, c
   }
   const bool use_eff = pairwise_needs_runs(OP, ka, ca, kb, cb);
   const int kind = use_eff ? eff(c, w_runs(x)) : pairwise_kind(OP, ka, kb, c);
-  STAMP(2);
   if (kind == DK_B) {
     uint8_t* slot = oc.scratch + (size_t)t * kSlotBytes;
     w_store_bitmap(slot, x);
     w_place(t, true, slot, false, lds, 8192, (uint32_t)c, tk.key, DK_B, oc);
-    STAMP(3);
     return;
   }
   uint32_t len;
   if (kind == DK_A) len = w_stage(DK_A, x, c, lds);
   else len = 2u + 4u * (uint32_t)w_stage_runs(x, lds);
-  STAMP(7);
   w_place(t, true, nullptr, true, lds, len, (uint32_t)c, tk.key, kind, oc);
-  STAMP(8);
 }
 
 // 32 B task record through the scalar cache (wave-uniform address)
@@ -577,12 +495,12 @@ __device__ __forceinline__ bool has_task(const PTask& t) {
 
 template <int OP, int MODE>
 __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint8_t* pa, const uint8_t* pb,
-                                         const OutCtx& oc, uint32_t* task_card, uint32_t* lds SACC_PARAM) {
+                                         const OutCtx& oc, uint32_t* task_card, uint32_t* lds) {
   prio_hi();
   if (pair_class(OP, tk.kind_a, tk.kind_b) == 1)
-    filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
+    filter_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds);
   else
-    bitmap_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds SACC_ARG);
+    bitmap_class_task<OP, MODE>(t, tk, pa, pb, oc, task_card, lds);
 }
 
 // One wave per task, static stride over a resident grid (a contended ticket
@@ -591,82 +509,27 @@ __device__ __forceinline__ void any_task(uint32_t t, const PTask& tk, const uint
 // and bitmap-class tasks share the launch: separate kernels per class were
 // measured 15 % slower on the C2 mix (tail + an extra dependent index load).
 // MODE 0: materialise results.  MODE 1: andCardinality only (task_card[t]).
-// FORM 0: planned task list (key order); 1: direct (task t = key key_lo + t); 2: balanced (k_plan_balanced's
-// list, the bands walked in a per-wave rotated order, records at key positions)
-template <int OP, int MODE, int FORM>
+// DIRECT false: planned task list (key order, sparse key ranges); true: direct (task t = key key_lo + t; the
+// pipelined op's key ranges, and dense ranges with RBG_PW_BALANCE=0)
+template <int OP, int MODE, bool DIRECT>
 __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ tasks,
                                                       const uint32_t* __restrict__ n_tasks, const uint8_t* pa,
                                                       const uint8_t* pb, OutCtx oc, uint32_t* __restrict__ task_card,
                                                       PwDirect dsrc) {
   __shared__ __align__(16) uint32_t lds_all[kWaves][kWaveLds];
-  constexpr bool DIRECT = FORM == 1;
   if (DIRECT) {
     // the plan kernel's other duties: the task count and the op's zeroed look-back state
     plan_zero(dsrc.zlb, dsrc.ztile);
     if (blockIdx.x == 0 && threadIdx.x == 0) dsrc.n_tasks_out[0] = dsrc.n_tasks_write;
   }
-  const uint32_t nt = DIRECT ? dsrc.nkeys : FORM == 2 ? uni(n_tasks[1]) : uni(*n_tasks);
+  const uint32_t nt = DIRECT ? dsrc.nkeys : uni(*n_tasks);
   const int w = threadIdx.x >> 6;
   uint32_t* lds = lds_all[w];
   const uint32_t stride = gridDim.x * kWaves;
   const uint32_t t0 = uni(blockIdx.x * kWaves + w);
   if (t0 >= nt) return;
   uint32_t t = t0;
-  if (FORM == 2) {
-    // band b holds list positions [b S, (b + 1) S); this wave takes position t0 of each band, starting
-    // at band t0 mod nb (only the last band can be short)
-    const uint32_t nb = (nt + stride - 1) / stride;
-    const uint32_t b0 = t0 % nb;
-#ifndef RBG_BAL_WALK
-#define RBG_BAL_WALK 0
-#endif
-    // RBG_BAL_WALK (experiment builds): 0 every band in a per-wave rotated order; 1 the heavy half's
-    // bands rotated, then the light half's (longest first between halves); 2 heaviest band first
-    auto pos_of = [&](uint32_t k) -> uint32_t {
-      uint32_t b;
-      if (RBG_BAL_WALK == 2) {
-        b = k;
-      } else if (RBG_BAL_WALK == 1) {
-        const uint32_t h = (nb + 1) / 2;
-        if (k < h) b = (b0 + k) % h;
-        else b = h + (b0 + k - h) % (nb - h);
-      } else {
-        b = b0 + k < nb ? b0 + k : b0 + k - nb;
-      }
-      return b * stride + t0;
-    };
-    uint32_t k = 0;
-    while (k < nb && pos_of(k) >= nt) k++;
-    if (k >= nb) return;
-#if RBG_WAVE_PROBE
-    const uint64_t pr0 = __builtin_amdgcn_s_memrealtime(), pm0 = __builtin_amdgcn_s_memtime();
-    uint32_t ntask = 0;
-#endif
-    PTask cur = load_task(tasks, pos_of(k));
-    for (;;) {
-      uint32_t kn = k + 1;
-      while (kn < nb && pos_of(kn) >= nt) kn++;
-      PTask nxt;
-      if (kn < nb) nxt = load_task(tasks, pos_of(kn));  // in flight while this task runs
-      if (cur.kind_a != kAbsent || cur.kind_b != kAbsent) {  // marked: no task (the plan wrote its record)
-        any_task<OP, MODE>((uint32_t)cur.key - (uint32_t)dsrc.key_lo, cur, pa, pb, oc, task_card, lds SACC_ARG);
-#if RBG_WAVE_PROBE
-        ntask++;
-#endif
-      }
-      if (kn >= nb) break;
-      k = kn;
-      cur = nxt;
-    }
-#if RBG_WAVE_PROBE
-    probe_store(pr0, pm0, ntask);
-#endif
-    return;
-  }
   if (DIRECT) {
-#if RBG_STAMPS
-    StampAcc sacc = {};
-#endif
     // The wave first resolves all of its tasks at once (lane k: task t0 + k * stride, vector
     // loads through both key CSRs) into its own region of the task buffer, wave-major, then
     // runs them with the planned form's one scalar record load per task.  (Resolving each
@@ -691,9 +554,6 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
     // the records are read back through the scalar cache (a fresh line per wave region: no
     // other wave writes it, and the scalar cache holds nothing of it yet)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the stores are in the L2 the scalar loads read
-#if RBG_WAVE_PROBE
-    const uint64_t pr0 = __builtin_amdgcn_s_memrealtime(), pm0 = __builtin_amdgcn_s_memtime();
-#endif
     uint32_t k = 0;
     PTask cur = load_task(mine, 0);
     for (;;) {
@@ -701,7 +561,7 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
       PTask nxt;
       if (tn < nt) nxt = load_task(mine, k + 1);  // in flight while this task runs
       if (has_task<OP>(cur)) {
-        any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
+        any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds);
       } else if (MODE == 1) {
         if (l == 0) task_card[t] = 0;
       } else {
@@ -712,52 +572,18 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
       k++;
       cur = nxt;
     }
-#if RBG_WAVE_PROBE
-    probe_store(pr0, pm0, k + 1);
-#endif
     return;
   }
   PTask cur = load_task(tasks, t);
-#if RBG_STAMPS
-  StampAcc sacc = {};
-  const uint64_t t_kernel = __builtin_amdgcn_s_memtime();
-  const uint64_t r_kernel = __builtin_amdgcn_s_memrealtime();
-#endif
   for (;;) {
     const uint32_t tn = t + stride;
     PTask nxt;
     if (tn < nt) nxt = load_task(tasks, tn);  // in flight while this task runs
-#if RBG_STAMPS
-    const uint64_t t_in = __builtin_amdgcn_s_memtime();
-    sacc.v[10] += 1;
-#endif
-    any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds SACC_ARG);
-#if RBG_STAMPS
-    sacc.v[11] += __builtin_amdgcn_s_memtime() - t_in;
-#endif
+    any_task<OP, MODE>(t, cur, pa, pb, oc, task_card, lds);
     if (tn >= nt) break;
     t = tn;
     cur = nxt;
   }
-#if RBG_STAMPS
-  const uint64_t life = __builtin_amdgcn_s_memtime() - t_kernel;
-  sacc.v[9] += life;
-  if (lane_id() == 0) {
-    for (int i = 0; i < 12; i++) atomicAdd(&g_stamp[i], (unsigned long long)sacc.v[i]);
-    atomicMax(&g_stamp[12], (unsigned long long)life);  // longest wave
-    atomicAdd(&g_stamp[13], 1ull);                      // waves
-    const uint64_t r_end = __builtin_amdgcn_s_memrealtime();
-    atomicMax(&g_stamp[14], ~(unsigned long long)r_kernel);  // earliest wave start (complemented)
-    atomicMax(&g_stamp[15], (unsigned long long)r_end);     // latest wave end
-    atomicAdd(&g_stamp[16], (unsigned long long)(r_end - r_kernel));
-    atomicMax(&g_stamp[17], (unsigned long long)r_kernel);  // latest wave start
-    uint32_t xcc, hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    const uint32_t wid = blockIdx.x * kWaves + (threadIdx.x >> 6);
-    if (wid < 16384) g_wave[wid] = make_uint4((uint32_t)r_kernel, (uint32_t)r_end, xcc, hw);
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -767,19 +593,16 @@ __global__ __launch_bounds__(256, 4) void k_pair_wave(const PTask* __restrict__ 
 // tail.  Here the 16 waves of a CU drain one pool, so a wave that loses arbitration simply runs
 // fewer tasks and the CU ends with its last task, not with its slowest wave.  CU b owns positions
 // 16 b + w (w < 16) of every band of S = 16 x grid list positions: 16 consecutive cost ranks per
-// band, every rank once over the bands (k_plan_balanced's layout).  Claim k takes
-//   RBG_CU_ORDER 0: band (k mod nb + b) mod nb, slot k / nb  -- the CU's waves on different bands;
-//   RBG_CU_ORDER 1: band (k / 16 + b) mod nb, slot k mod 16 -- the CU's heaviest ranks first;
-//   RBG_CU_ORDER 2: band (b - k) mod nb, slot k / nb -- as 0, each round of nb claims heavy to light.
-// A claim is one LDS atomic; the next task is claimed and its record requested while a task runs.
-// (Shared pools of the last 1 / 2 / 4 bands across CUs, claimed by agent-scope atomics, made the
-// kernel 0.23 -> 0.34 / 0.44 / 0.60 ms: profiles/r05/experiments/c2_cu_tail_pools.txt; every wave
-// claiming chunks of 1 / 2 / 4 tasks from per-XCD pools instead of the LDS pool: 0.221-0.226 ->
-// 0.262-0.265 / 0.244-0.251 / 0.255-0.256 ms, c2_cu_global_chunks.txt.)
+// band, every rank once over the bands (k_plan_balanced's layout).  Claim k takes band
+// (k mod nb + b) mod nb, slot k / nb: the CU's waves work on different bands at once.  A claim is one LDS atomic; the next task is claimed and its
+// record requested while a task runs.  (Round 5 measured, profiles/r05/experiments/: claim orders
+// putting each CU's heaviest ranks first, or each round of claims heavy to light, the same or
+// slower, c2_cu_claim_order.txt; pools of the last 1 / 2 / 4 bands shared by ALL CUs through one
+// agent-scope counter 0.23 -> 0.34 / 0.44 / 0.60 ms, c2_cu_tail_pools.txt -- one counter saturates
+// at ~88 claims per us (MI355X_MICROARCH.md, dequeue row), i.e. 47 us for one band's 4,096 claims.)
+// (Round 6, profiles/r06/experiments/cu_tail_pools.txt: the lightest two bands left out of the own pools
+// and claimed from 8 shared agent-scope counters once a CU's own pool is dry: +1.6 %, not kept.)
 // ---------------------------------------------------------------------------
-#ifndef RBG_CU_ORDER
-#define RBG_CU_ORDER 0
-#endif
 constexpr int kCuWaves = 16;
 static_assert(kCuWaves * kWaveLds * 4 + 16 <= 163840, "16 waves and the counter in one CU's LDS");
 template <int OP, int MODE>
@@ -795,119 +618,56 @@ __global__ __launch_bounds__(1024, 1) void k_pair_cu(const PTask* __restrict__ t
   const uint32_t S = gridDim.x * kCuWaves;
   const uint32_t nb = (nt + S - 1) / S;
   const uint32_t total = nb * kCuWaves, base = blockIdx.x * kCuWaves;
-  auto pos_of = [&](uint32_t k) -> uint32_t {
-    const uint32_t band = RBG_CU_ORDER == 1   ? (k / kCuWaves + blockIdx.x) % nb
-                          : RBG_CU_ORDER == 2 ? (blockIdx.x % nb + nb - k % nb) % nb
-                                              : (k % nb + blockIdx.x) % nb;
-    const uint32_t w = RBG_CU_ORDER == 1 ? k % kCuWaves : k / nb;
-    return band * S + base + w;
-  };
   auto claim = [&]() -> uint32_t {  // the next list position of this wave, ~0u when none is left
     for (;;) {
       uint32_t v = 0;
       if (lane_id() == 0) v = atomicAdd(&ctr, 1u);
       const uint32_t k = uni(v);
       if (k >= total) return ~0u;
-      const uint32_t p = pos_of(k);
+      const uint32_t p = ((k % nb + blockIdx.x) % nb) * S + base + k / nb;  // band (k mod nb + b) mod nb, slot k / nb
       if (p < nt) return p;
     }
   };
   uint32_t p = claim();
   if (p == ~0u) return;
-#if RBG_STAMPS
-  StampAcc sacc = {};
-#endif
-#if RBG_WAVE_PROBE
-  const uint64_t pr0 = __builtin_amdgcn_s_memrealtime(), pm0 = __builtin_amdgcn_s_memtime();
-  uint32_t ntask = 0;
-#endif
   PTask cur = load_task(tasks, p);
   for (;;) {
     const uint32_t pn = claim();
     PTask nxt;
     if (pn != ~0u) nxt = load_task(tasks, pn);  // in flight while this task runs
-    if (cur.kind_a != kAbsent || cur.kind_b != kAbsent) {  // marked: no task (the plan wrote its record)
-      any_task<OP, MODE>((uint32_t)cur.key - (uint32_t)dsrc.key_lo, cur, pa, pb, oc, task_card, lds SACC_ARG);
-#if RBG_WAVE_PROBE
-      ntask++;
-#endif
-    }
+    if (cur.kind_a != kAbsent || cur.kind_b != kAbsent)  // marked: no task (the plan wrote its record)
+      any_task<OP, MODE>((uint32_t)cur.key - (uint32_t)dsrc.key_lo, cur, pa, pb, oc, task_card, lds);
     if (pn == ~0u) break;
     cur = nxt;
   }
-#if RBG_WAVE_PROBE
-  probe_store(pr0, pm0, ntask, blockIdx.x * kCuWaves + (threadIdx.x >> 6));
-#endif
 }
 
 template <int OP, int MODE>
 static void launch_pw(hipStream_t s, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                      const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced,
-                      bool cu_pool) {
-  if (direct && balanced && cu_pool) {  // one workgroup per CU, all of them resident
+                      const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced) {
+  if (direct && balanced) {  // one workgroup per CU, all of them resident
     const int g = std::max(1, resident_grid((const void*)&k_pair_cu<OP, MODE>, 1024));
     hipLaunchKernelGGL((k_pair_cu<OP, MODE>), dim3(g), dim3(1024), 0, s, tasks, nt, pa, pb, oc, task_card, *direct);
-    return;
-  }
-  if (direct && balanced) {
-    const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, 2>)));
-    hipLaunchKernelGGL((k_pair_wave<OP, MODE, 2>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
-                       *direct);
     return;
   }
   if (direct) {
     // Direct mode lays each wave's tasks out in a region of per = ceil(nt / stride) + 3 (rounded to 4)
     // records, stride = 4 g waves: at most nt + 4 stride records.  The task buffer holds
     // kMaxKeys + 32768 (engine.cpp: ctx_init), so stride <= 8192 waves: g <= 2048 workgroups.
-    const int g = std::max(1, std::min({grid, resident_grid((const void*)&k_pair_wave<OP, MODE, 1>), 2048}));
-    hipLaunchKernelGGL((k_pair_wave<OP, MODE, 1>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
+    const int g = std::max(1, std::min({grid, resident_grid((const void*)&k_pair_wave<OP, MODE, true>), 2048}));
+    hipLaunchKernelGGL((k_pair_wave<OP, MODE, true>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
                        *direct);
     return;
   }
-  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, 0>)));
-  hipLaunchKernelGGL((k_pair_wave<OP, MODE, 0>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
+  const int g = std::max(1, std::min(grid, resident_grid((const void*)&k_pair_wave<OP, MODE, false>)));
+  hipLaunchKernelGGL((k_pair_wave<OP, MODE, false>), dim3(g), dim3(256), 0, s, tasks, nt, pa, pb, oc, task_card,
                      PwDirect{});
 }
 
-#if RBG_WAVE_PROBE
-void debug_stamps(uint64_t* out20, bool reset) {
-  (void)hipDeviceSynchronize();
-  for (int i = 0; i < 20; i++) out20[i] = 0;
-  if (const char* f = getenv("RBG_WAVE_DUMP")) {
-    static uint4 h[3 * 16384];
-    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_probe), sizeof(h), 0, hipMemcpyDeviceToHost);
-    if (FILE* fp = fopen(f, "ab")) {
-      fwrite(h, sizeof(h), 1, fp);
-      fclose(fp);
-    }
-  }
-  if (reset) {
-    static uint4 z[3 * 16384];
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_probe), z, sizeof(z), 0, hipMemcpyHostToDevice);
-  }
-}
-#elif RBG_STAMPS
-void debug_stamps(uint64_t* out20, bool reset) {
-  (void)hipDeviceSynchronize();
-  (void)hipMemcpyFromSymbol(out20, HIP_SYMBOL(g_stamp), 20 * 8, 0, hipMemcpyDeviceToHost);
-  if (const char* f = getenv("RBG_WAVE_DUMP")) {
-    static uint4 h[16384];
-    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_wave), sizeof(h), 0, hipMemcpyDeviceToHost);
-    if (FILE* fp = fopen(f, "ab")) {
-      fwrite(h, sizeof(h), 1, fp);
-      fclose(fp);
-    }
-  }
-  if (reset) {
-    unsigned long long z[20] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z), 0, hipMemcpyHostToDevice);
-  }
-}
-#else
+// the diagnostic per-phase stamps builds were retired in round 6 (their results are in profiles/r02-r05)
 void debug_stamps(uint64_t* out20, bool) {
   for (int i = 0; i < 20; i++) out20[i] = 0;
 }
-#endif
 
 template <int OP, int MODE>
 static void launch_pb(hipStream_t s, int key_lo, uint32_t nkeys, const uint32_t* koa, const CDesc* da,
@@ -920,10 +680,10 @@ void launch_plan_balanced(hipStream_t s, int op, int mode, int key_lo, uint32_t 
                           const CDesc* da, const uint8_t* pa, const uint32_t* kob, const CDesc* db, const uint8_t* pb,
                           PTask* tasks, uint32_t* n_tasks, OutCtx oc, uint32_t* task_card, uint64_t* zlb,
                           uint64_t* ztile) {
-#define RBG_LPB(O)                                                                                               \
-  if (mode == 0)                                                                                                 \
-    launch_pb<O, 0>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, tasks, n_tasks, oc, task_card, zlb, ztile);     \
-  else                                                                                                           \
+#define RBG_LPB(O)                                                                                                  \
+  if (mode == 0)                                                                                                    \
+    launch_pb<O, 0>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, tasks, n_tasks, oc, task_card, zlb, ztile); \
+  else                                                                                                              \
     launch_pb<O, 1>(s, key_lo, nkeys, koa, da, pa, kob, db, pb, tasks, n_tasks, oc, task_card, zlb, ztile);
   switch (op) {
     case OP_AND: RBG_LPB(OP_AND) break;
@@ -943,11 +703,10 @@ void launch_plan_pairwise(hipStream_t s, int op, int key_lo, int key_hi, const u
 }
 
 void launch_pairwise(hipStream_t s, int op, int mode, int grid, const PTask* tasks, const uint32_t* nt, const uint8_t* pa,
-                     const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced,
-                     bool cu_pool) {
-#define RBG_LPW(O)                                                                                      \
-  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced, cu_pool); \
-  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced, cu_pool);
+                     const uint8_t* pb, OutCtx oc, uint32_t* task_card, const PwDirect* direct, bool balanced) {
+#define RBG_LPW(O)                                                                             \
+  if (mode == 0) launch_pw<O, 0>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced); \
+  else launch_pw<O, 1>(s, grid, tasks, nt, pa, pb, oc, task_card, direct, balanced);
   switch (op) {
     case OP_AND: RBG_LPW(OP_AND) break;
     case OP_OR: RBG_LPW(OP_OR) break;

@@ -27,11 +27,13 @@ class Engine:
         self._ctx = ctypes.c_void_p()
         check(lib().rbg_ctx_create(int(device), ctypes.byref(self._ctx)))
         self.device = device
+        self._bsi_target = None  # device tensor the BSI sum kernels write into (bsi_sums_target)
 
     def close(self):
         if self._ctx:
             lib().rbg_ctx_destroy(self._ctx)
             self._ctx = ctypes.c_void_p()
+        self._bsi_target = None  # the BSI sums target is released with the context that wrote it
 
     def __del__(self):
         try:
@@ -66,11 +68,15 @@ class Engine:
         return v.value
 
     # ---- batches ------------------------------------------------------------
-    def load(self, bitmaps) -> int:
+    def load(self, bitmaps, packed=False) -> int:
+        """Upload + device decode of serialized bitmaps as one key-major batch.  packed: for a batch
+        that feeds wide ops -- a batch of arrays alone keeps the portable format's packed array
+        payloads (rbg_ctx_load_packed), the wide kernels' fastest layout."""
         bufs = [b.serialize() if isinstance(b, RoaringBitmap) else bytes(b) for b in bitmaps]
         arr, lens = _lib.buf_array(bufs)
         out = ctypes.c_int32()
-        check(lib().rbg_ctx_load(self._ctx, arr, lens, len(bufs), ctypes.byref(out)))
+        f = lib().rbg_ctx_load_packed if packed else lib().rbg_ctx_load
+        check(f(self._ctx, arr, lens, len(bufs), ctypes.byref(out)))
         return out.value
 
     def load_pair(self, *bitmaps):
@@ -218,8 +224,18 @@ class Engine:
 
     def bsi_sums_target(self, dst):
         """From now on every BSI sum also writes its (sum, count) into the int64 device tensor `dst`
-        (two elements) from the kernel that computes it; None stops it (rbg_ctx_bsi_sums_target)."""
+        (two elements) from the kernel that computes it; None stops it (rbg_ctx_bsi_sums_target).
+
+        The engine keeps a reference to `dst` until it is replaced, cleared with None or the engine is
+        closed, so the kernels never write into memory the caller's allocator has handed on."""
+        if dst is not None:
+            import torch
+            if not isinstance(dst, torch.Tensor) or dst.dtype != torch.int64 or not dst.is_contiguous() \
+                    or dst.numel() < 2 or dst.device.type != "cuda" or dst.device.index != self.device:
+                raise ValueError("bsi_sums_target: a contiguous int64 CUDA tensor of at least 2 elements on "
+                                 f"device {self.device} is required")
         check(lib().rbg_ctx_bsi_sums_target(self._ctx, None if dst is None else ctypes.c_void_p(dst.data_ptr())))
+        self._bsi_target = dst
 
     def batch_counts(self, batch) -> np.ndarray:
         """containers per input bitmap of a batch"""

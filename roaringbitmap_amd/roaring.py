@@ -19,7 +19,7 @@ from collections.abc import Iterator
 import numpy as np
 
 from . import _lib
-from ._lib import IllegalArgumentException, check, lib, take
+from ._lib import ArrayIndexOutOfBoundsException, IllegalArgumentException, check, lib, take
 
 EMPTY = bytes.fromhex("3a30000000000000")
 
@@ -472,6 +472,20 @@ def _find_container(buf, key):
     return 2, np.frombuffer(buf, dtype="<u2", count=2 * nr, offset=pos + 2)
 
 
+def _intersect_array_into_bitmap(words, keys) -> int:
+    """Util.intersectArrayIntoBitmap(long[] bitmap, char[] array, int length) (RB/Util.java:531-555) on a
+    uint64 word array in place, with its edge behaviour: an empty array leaves word 0 untouched and zeroes
+    the rest; the words past the array's last word are zeroed to the buffer's end.  -> the bits left."""
+    keys = np.asarray(keys, dtype=np.int64)
+    if len(keys) == 0:
+        words[1:] = 0
+        return 0
+    mask = np.zeros(len(words), dtype=np.uint64)
+    np.bitwise_or.at(mask, keys >> 6, np.uint64(1) << (keys & 63).astype(np.uint64))
+    words &= mask
+    return int(np.unpackbits(words.view(np.uint8)).sum())
+
+
 def _keys_of(buf) -> np.ndarray:
     """the container keys of a portable serialized bitmap (its descriptor table, RB/RoaringArray.java:547-588)"""
     cookie = int.from_bytes(buf[0:4], "little")
@@ -593,29 +607,69 @@ class FastAggregation:
 
     @staticmethod
     def workAndMemoryShyAnd(buffer, *bitmaps):
-        """workAndMemoryShyAnd(long[] buffer, RoaringBitmap...) (RB/FastAggregation.java:522-576).
+        """workAndMemoryShyAnd(long[] buffer, RoaringBitmap...) (RB/FastAggregation.java:522-576), following
+        the reference's control flow on the caller's buffer, which it uses as the key bitset without
+        clearing it first:
 
-        workShyAnd's algorithm (its results and types) with two observable differences, kept here:
-        the buffer length is checked (IllegalArgumentException below 1024), and the caller's buffer is
-        the key bitset, which it does not clear first -- a nonzero buffer contributes its bits as
-        keys of the first bitmap (:527-532); a key of those the first bitmap lacks is skipped by the
-        per-key getIndex (:561-564), so it behaves as a full container there.  Afterwards the buffer
-        holds what the reference leaves: all ones once any key survived the key intersection
-        (Arrays.fill(words, -1L) per key, :558), else the (all-zero) intersection."""
+        - the first bitmap's keys are OR-ed into the buffer (:527-531) and the count starts at its size
+          (:532): an empty first bitmap returns an empty result and leaves the buffer as it was;
+        - every further bitmap's keys are intersected into it with Util.intersectArrayIntoBitmap over the
+          buffer's whole length while the count is nonzero (:533-536; RB/Util.java:531-555, whose word 0
+          survives an empty key array);
+        - the surviving bits are the keys (:540-548): with a single bitmap the key array is sized by its
+          container count, so a dirty bit outside its keys throws ArrayIndexOutOfBoundsException; with
+          more, a dirty bit that survives is a key the first bitmap lacks, skipped by the per-key
+          getIndex (:561-564), i.e. a full container there;
+        - per key the buffer is filled with ones (its whole length) and becomes a lazy bitmap that each
+          container ANDs in place (:557-569), so afterwards it holds the last key's lazy intersection.
+          The result containers are workShyAnd's (computed on the device).
+
+        A buffer longer than 1,024 words reaches the per-key chain as a bitmap of that length: a bitmap
+        container there throws ArrayIndexOutOfBoundsException in the reference (BitmapContainer.iand's
+        loop runs to the buffer's length, RB/BitmapContainer.java:535-538), and so it does here."""
         if buffer is None or len(buffer) < 1024:
             raise IllegalArgumentException("buffer should have at least 1024 elements.")
         bms = list(bitmaps[0]) if len(bitmaps) == 1 and isinstance(bitmaps[0], (list, tuple)) else list(bitmaps)
-        words = np.asarray(buffer[:1024]).astype(np.uint64)
-        garbage = np.nonzero(np.unpackbits(words.view(np.uint8), bitorder="little"))[0]
-        keys = set(garbage.tolist()) | set(_keys_of(bms[0]._buf).tolist())
-        for b in bms[1:]:
-            keys &= set(_keys_of(b._buf).tolist())
-        extra = sorted(set(garbage.tolist()) - set(_keys_of(bms[0]._buf).tolist()))
+        if not isinstance(buffer, np.ndarray) or buffer.dtype.itemsize != 8 or buffer.ndim != 1:
+            raise IllegalArgumentException("buffer must be a one-dimensional numpy array of 64-bit words")
+        words = buffer.view(np.uint64)  # the caller's memory: the reference writes its long[] in place
+        nw = len(words)
+        fk = _keys_of(bms[0]._buf)
+        np.bitwise_or.at(words, fk >> 6, np.uint64(1) << (fk & 63).astype(np.uint64))  # :527-531
+        num = len(fk)
+        for b in bms[1:]:  # :533-536
+            if num == 0:
+                break
+            num = _intersect_array_into_bitmap(words, _keys_of(b._buf))
+        if num == 0:  # :537-539
+            return RoaringBitmap()
+        bits = np.nonzero(np.unpackbits(words.view(np.uint8), bitorder="little"))[0]
+        if len(bits) > num:  # keys[pos++] past numContainers (:540-548)
+            raise ArrayIndexOutOfBoundsException(f"Index {num} out of bounds for length {num}")
+        keys = (bits & 0xFFFF).astype(np.int64)  # (char)(base + tz)
+        in_first = np.isin(keys, fk)
         first = bms[0]
-        if extra:  # the first bitmap with full containers at the buffer's own keys (an identity for AND)
-            first = RoaringBitmap._pair("or", bms[0], RoaringBitmap(_full_containers(extra)))
+        if not in_first.all():  # the first bitmap lacks these keys: skipped there, a full container for AND
+            first = RoaringBitmap._pair("or", bms[0], RoaringBitmap(_full_containers(sorted(keys[~in_first].tolist()))))
+        chains = [[_find_container(b._buf, int(k)) for b in bms] for k in keys]
+        if nw > 1024 and any(c is not None and c[0] == 1 for ch in chains for c in ch):
+            raise ArrayIndexOutOfBoundsException("Index 1024 out of bounds for length 1024")
         out = _wide("workshy_and", [first] + bms[1:])
-        buffer[:1024] = -1 if keys else 0
+        # the buffer after the last key's chain (:557-569): ones, then each present container ANDed in place
+        words[:] = np.uint64(0xFFFFFFFFFFFFFFFF)
+        for c in chains[-1]:
+            if c is None:
+                continue
+            kind, pay = c
+            if kind == 0:  # BitmapContainer.iand(ArrayContainer), lazy: intersectArrayIntoBitmap (:523-527)
+                _intersect_array_into_bitmap(words, pay.astype(np.int64))
+            elif kind == 1:  # lazy iand(BitmapContainer) (:535-538)
+                words[:1024] &= pay
+            else:  # lazy iand(RunContainer): the ranges between runs reset (:557-590)
+                m = np.zeros(65536, dtype=bool)
+                for s, ln in zip(pay[0::2].astype(np.int64), pay[1::2].astype(np.int64)):
+                    m[s:s + ln + 1] = True
+                words[:1024] &= np.packbits(m, bitorder="little").view(np.uint64)
         return out
 
     @staticmethod

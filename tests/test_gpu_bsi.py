@@ -130,7 +130,13 @@ def test_c5_synthetic_bsi(gpu):
     e.bsi(b, "RANGE", 31, lo, hi, mn, mx, want_sum=True)
     e.sync()
     assert (int(d2[0]), int(d2[1])) == o.sum(exp)
+    assert e._bsi_target is d2  # the engine holds the target while kernels may write it
     e.bsi_sums_target(None)
+    assert e._bsi_target is None
+    for bad in (torch.empty(2, dtype=torch.int32, device="cuda:0"), torch.empty(1, dtype=torch.int64, device="cuda:0"),
+                torch.empty(2, dtype=torch.int64), torch.empty(4, dtype=torch.int64, device="cuda:0")[::2]):
+        with pytest.raises(ValueError):
+            e.bsi_sums_target(bad)
     # a second index on the same engine: each batch keeps its own task list and input table
     b2 = e.synth(4, seed + 1, rows // 3)
     mn2, mx2 = e.batch_minmax(b2)

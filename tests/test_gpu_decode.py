@@ -140,3 +140,40 @@ def test_multi_chunk_inputs(gpu):
     ge = _gpu_error(e, [big[1][: len(big[1]) - 5]])
     assert ge is not None and ge == (_host_error(big[1][: len(big[1]) - 5])[0],
                                      "input 0: " + _host_error(big[1][: len(big[1]) - 5])[1])
+
+
+def test_packed_decode_for_wide_ops(gpu):
+    """rbg_ctx_load_packed: 1,000 C3-uniform bitmaps (2,048 keys) from their serialized bytes keep the
+    portable format's packed array payloads (RB/RoaringArray.java:547-629) and every wide op that reads
+    that layout is byte-exact against the oracle (RB/FastAggregation.java:356-414,586-666,823-836);
+    the padded decode gives the same bytes; a packed batch refuses the slot-aligned paths, and a batch
+    holding a bitmap container is decoded slot-aligned whatever the flag."""
+    from roaringbitmap_amd import Engine
+    from roaringbitmap_amd._lib import IllegalArgumentException
+    from _fmt import A, B, encode
+    e = Engine(0)
+    n = 1000
+    sb = e.synth(1, 0xC3000000, n, 3000, 3000 + 2048)
+    bufs = [x.serialize() for x in e.batch_fetch_range(sb)]
+    e.release(sb)
+    packed, padded = e.load(bufs, packed=True), e.load(bufs)
+    assert e.batch_stats(packed)["payload_bytes"] == e.batch_stats(padded)["payload_bytes"]
+    for op in ("or", "xor", "and", "workshy_and", "priorityqueue_or", "horizontal_xor", "parallel_or"):
+        exp = O.wide(op, bufs)
+        for b in (packed, padded):
+            e.wide(op, b)
+            assert e.fetch().serialize() == exp, op
+    e.wide_card("or", packed)
+    assert e.card() == O.wide_card("or", bufs)
+    assert [x.serialize() for x in e.batch_fetch_range(packed, 0, 5)] == bufs[:5]  # fetches read packed payloads
+    with pytest.raises(IllegalArgumentException):  # naive_and's chain needs slots
+        e.wide("naive_and", packed)
+    one = e.load([bufs[0]], packed=True)
+    with pytest.raises(IllegalArgumentException):  # pairwise operands need slots
+        e.pairwise("and", one, one)
+    mixed = encode([(1, A, np.arange(10, dtype=np.uint16)), (2, B, np.arange(0, 9000, 2, dtype=np.uint16))])
+    m = e.load([mixed, bufs[1]], packed=True)  # a bitmap container: slot-aligned, every op allowed
+    e.wide("naive_and", m)
+    assert e.fetch().serialize() == O.wide("naive_and", [mixed, bufs[1]])
+    for b in (packed, padded, one, m):
+        e.release(b)

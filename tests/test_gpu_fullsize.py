@@ -101,6 +101,27 @@ def test_c2_full_pair(eng, c2, variant, op):
         _same(eng.fetch().serialize(), O.pairwise(op, xb, xa), f"C2 {variant} andNot reversed")
 
 
+@pytest.mark.parametrize("lo,hi", [(1000, 19000), (7, 65530), (40000, 65536)])
+def test_c2_key_ranges(eng, c2, lo, hi):
+    """Key-range shards of the C2 pair (the N > 1 headline's per-rank op) against the oracle on operands
+    restricted to [lo, hi) by whole-key removes (RB/RoaringBitmap.java:382-399: a key's result depends on
+    that key's containers only).  18,000 keys: the balanced list's last band is partial and the two
+    lightest bands are k_pair_cu's shared tail; 65,523 keys: the tail with a one-key-short last band."""
+    x, y, xa, xb = c2["raw"]
+
+    def restrict(buf):
+        if lo > 0:
+            buf = O.range_mut("remove", buf, 0, lo << 16)
+        if hi < 65536:
+            buf = O.range_mut("remove", buf, hi << 16, 1 << 32)
+        return buf
+
+    ra, rb_ = restrict(xa), restrict(xb)
+    for op in ("and", "or", "xor", "andnot"):
+        eng.pairwise(op, x, y, key_lo=lo, key_hi=hi)
+        _same(eng.fetch().serialize(), O.pairwise(op, ra, rb_), f"C2 {op} keys [{lo}, {hi})")
+
+
 @pytest.mark.parametrize("variant", ["raw", "runopt"])
 def test_c2_widened_ops(eng, c2, variant):
     """The round-5 rows at the C2 size, byte-exact against the oracle on the fetched operands:

@@ -316,19 +316,34 @@ def test_workshy_forms(gpu, seed):
 def test_work_and_memory_shy_and(gpu):
     """FastAggregation.workAndMemoryShyAnd (RB/FastAggregation.java:522-576): workShyAnd's result with a
     zeroed buffer; a nonzero buffer adds its bits to the first bitmap's keys (a key the first bitmap
-    lacks is skipped per bitmap, i.e. it acts as a full container); the buffer is left all ones once a
-    key survived the key intersection, else zero."""
+    lacks is skipped per bitmap, i.e. it acts as a full container); afterwards the buffer holds the last
+    key's lazy intersection (the per-key fill with ones, then each container ANDed in place)."""
     from roaringbitmap_amd.roaring import _full_containers
+    from roaringbitmap_amd._lib import ArrayIndexOutOfBoundsException
     rb = _rb()
     rng = np.random.default_rng(21)
     bufs = [_gen.bitmap(rng, np.arange(10), p_present=0.9) for _ in range(4)]
     bms = [rb.RoaringBitmap(b) for b in bufs]
+
+    def last_key_and(keys_alive, inputs):
+        """the buffer the reference leaves: the AND of the last surviving key's containers, as 1,024 words"""
+        k = max(keys_alive)
+        m = np.ones(65536, dtype=bool)
+        for x in inputs:
+            v = O.to_values(x)
+            if (v >> 16 == k).any():
+                bits = np.zeros(65536, dtype=bool)
+                bits[(v[v >> 16 == k] & 0xFFFF).astype(np.int64)] = True
+                m &= bits
+        return np.packbits(m, bitorder="little").view(np.int64)
+
+    keysets = [set((O.to_values(b) >> 16).tolist()) for b in bufs]
     buf = np.zeros(1024, dtype=np.int64)
     assert rb.FastAggregation.workAndMemoryShyAnd(buf, *bms).serialize() == O.wide("workshy_and", bufs)
-    assert (buf == -1).all()
+    assert (buf == last_key_and(set.intersection(*keysets), bufs)).all()
     # a dirty buffer: keys 20 and 3 set; key 20 is in no input, so it cannot survive (n > 1)
-    keys0 = set(O.to_values(bufs[0]) >> 16)
-    common = set.intersection(*[set((O.to_values(b) >> 16).tolist()) for b in bufs[1:]])
+    keys0 = keysets[0]
+    common = set.intersection(*keysets[1:])
     extra = sorted(k for k in common if k not in keys0)
     buf = np.zeros(1024, dtype=np.int64)
     for k in [20] + extra:
@@ -336,12 +351,32 @@ def test_work_and_memory_shy_and(gpu):
     exp_first = O.pairwise("or", bufs[0], _full_containers(extra)) if extra else bufs[0]
     got = rb.FastAggregation.workAndMemoryShyAnd(buf, *bms).serialize()
     assert got == O.wide("workshy_and", [exp_first] + bufs[1:])
-    # one input and a dirty buffer: the buffer's keys become full run containers
+    # one input and a dirty buffer: the key array is sized by the first bitmap's containers (:540-548)
     buf = np.zeros(1024, dtype=np.int64)
-    buf[1] = 1  # key 64
-    got = rb.FastAggregation.workAndMemoryShyAnd(buf, bms[0]).serialize()
-    assert got == O.wide("workshy_and", [O.pairwise("or", bufs[0], _full_containers([64]))])
+    buf[1] = 1  # key 64, not a key of bms[0]
+    with pytest.raises(ArrayIndexOutOfBoundsException):
+        rb.FastAggregation.workAndMemoryShyAnd(buf, bms[0])
+    # one input, a dirty bit on one of its own keys: no extra key
+    buf = np.zeros(1024, dtype=np.int64)
+    k0 = min(keys0)
+    buf[k0 >> 6] |= np.int64(1) << np.int64(k0 & 63)
+    assert rb.FastAggregation.workAndMemoryShyAnd(buf, bms[0]).serialize() == O.wide("workshy_and", [bufs[0]])
+    # an empty first bitmap: an empty result, the buffer untouched (:532, :537-539)
+    buf = np.full(1024, 7, dtype=np.int64)
+    assert rb.FastAggregation.workAndMemoryShyAnd(buf, rb.RoaringBitmap.bitmapOf(), *bms).isEmpty()
+    assert (buf == 7).all()
+    # an empty later bitmap: intersectArrayIntoBitmap with no keys leaves word 0 and zeroes the rest
+    buf = np.zeros(1024, dtype=np.int64)
+    buf[5] = 3
+    a = rb.RoaringBitmap.bitmapOf(1, 2, 3 << 16)
+    assert rb.FastAggregation.workAndMemoryShyAnd(buf, a, rb.RoaringBitmap.bitmapOf()).isEmpty()
+    assert buf[0] == 0b1001 and (buf[1:] == 0).all()
     # disjoint keys: nothing survives, the buffer is left zero
     a, b = rb.RoaringBitmap.bitmapOf(1, 2), rb.RoaringBitmap.bitmapOf(1 << 16)
     buf = np.zeros(1024, dtype=np.int64)
     assert rb.FastAggregation.workAndMemoryShyAnd(buf, a, b).isEmpty() and (buf == 0).all()
+    # a longer buffer: the fills and the key intersection run over its whole length
+    buf = np.zeros(1100, dtype=np.int64)
+    x, y = rb.RoaringBitmap.bitmapOf(1, 5, 9), rb.RoaringBitmap.bitmapOf(5, 9, 12)
+    assert rb.FastAggregation.workAndMemoryShyAnd(buf, x, y).serialize() == rb.RoaringBitmap.bitmapOf(5, 9).serialize()
+    assert buf[0] == (1 << 5) | (1 << 9) and (buf[1:] == 0).all()

@@ -205,6 +205,28 @@ def test_work_and_memory_shy_and_buffer_check():
         FastAggregation.workAndMemoryShyAnd(np.zeros(100, dtype=np.int64), x, x)
 
 
+def test_work_and_memory_shy_and_key_bitset():
+    """workAndMemoryShyAnd's key-bitset steps on the caller's buffer, which end before any container work
+    (RB/FastAggregation.java:527-548; RB/Util.java:531-555): an empty first bitmap returns at once with the
+    buffer untouched; an empty later bitmap leaves word 0 and zeroes the rest; one input with a dirty bit
+    outside its keys overruns the key array (ArrayIndexOutOfBoundsException)."""
+    from roaringbitmap_amd._lib import ArrayIndexOutOfBoundsException
+    x = RoaringBitmap.bitmapOf(1, 2, 3 << 16)
+    buf = np.full(1024, 7, dtype=np.int64)
+    assert FastAggregation.workAndMemoryShyAnd(buf, RoaringBitmap.bitmapOf(), x).isEmpty()
+    assert (buf == 7).all()
+    buf = np.zeros(1024, dtype=np.int64)
+    buf[5] = 3
+    assert FastAggregation.workAndMemoryShyAnd(buf, x, RoaringBitmap.bitmapOf()).isEmpty()
+    assert buf[0] == 0b1001 and (buf[1:] == 0).all()
+    buf = np.zeros(1024, dtype=np.int64)
+    buf[1] = 1
+    with pytest.raises(ArrayIndexOutOfBoundsException):
+        FastAggregation.workAndMemoryShyAnd(buf, x)
+    with pytest.raises(IllegalArgumentException):  # not a long[]
+        FastAggregation.workAndMemoryShyAnd(np.zeros(1024, dtype=np.int32), x, x)
+
+
 def test_pairwise_op_codes_match_header():
     """_lib.OP (the Python mirror's rbg_pairwise codes) equals the header's enum, including the buffer
     package's and / andNot (RBG_AND_BUFFER / RBG_ANDNOT_BUFFER)."""
