@@ -228,6 +228,51 @@ def rank_slices(eng, run_range, ranges_of, steps, warmup):
     return rows
 
 
+def c3_uniform_decoded(eng, n, steps, warmup):
+    """FastAggregation.or over C3 uniform bitmaps that arrive as serialized bytes (what the Java class or an
+    ImmutableRoaringBitmap buffer uploads) against the same bitmaps generated on the device: the wide OR +
+    serialization step, input GB/s per layout -- the synthetic packed batch, the decoded batch with its
+    array payloads packed as in the portable format (rbg_ctx_load_packed, the wide ops' load) and the
+    decoded batch with 16 B slots (rbg_ctx_load).  n bitmaps over all 65,536 keys (host memory bounds n)."""
+    sb = eng.synth(1, 0xC3000000, n)
+    st = eng.batch_stats(sb)
+    in_bytes = st["payload_bytes"] + 4 * st["containers"]
+    bufs = [x.serialize() for x in eng.batch_fetch_range(sb)]
+    t0 = time.perf_counter()
+    pk = eng.load(bufs, packed=True)
+    load_s = time.perf_counter() - t0
+    pd = eng.load(bufs)
+    del bufs
+    out = {"workload": f"FastAggregation.or + serialize of {n} C3 uniform bitmaps (all 65,536 keys), device batch "
+                       f"generated vs decoded from the serialized bytes", "input_bytes": int(in_bytes),
+           "load_packed_s_pcie_included": round(load_s, 3)}
+    sha = None
+    for name, b in (("synthetic", sb), ("decoded_packed", pk), ("decoded_slots", pd)):
+        for _ in range(warmup):
+            eng.wide("or", b)
+            eng.serialize()
+        eng.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            eng.wide("or", b)
+            eng.serialize()
+        eng.sync()
+        dt = (time.perf_counter() - t0) / steps
+        eng.profile(steps)
+        for _ in range(steps):
+            eng.wide("or", b)
+        k, ph = eng.profile_read()
+        eng.profile(0)
+        h = hashlib.sha256(eng.fetch().serialize()).hexdigest()[:16]
+        sha = sha or h
+        out[name] = {"ms_per_step": round(dt * 1e3, 4), "input_GBps": round(in_bytes / dt / 1e9, 1),
+                     "kernel_ms": round(ph[1] / max(k, 1), 4), "result_sha16": h, "same_result": h == sha}
+        eng.release(b)
+    out["decoded_packed_vs_synthetic"] = round(out["decoded_packed"]["input_GBps"] / out["synthetic"]["input_GBps"], 4)
+    out["decoded_slots_vs_synthetic"] = round(out["decoded_slots"]["input_GBps"] / out["synthetic"]["input_GBps"], 4)
+    return out
+
+
 def c2_weak(rank, world, dist, steps, warmup, cdev):
     """The weak-scaling form of the headline: every rank ANDs its own C2 pair (seeds offset by the
     rank) with the serialization, no data-path collective; max time over ranks."""
@@ -948,6 +993,9 @@ def main():
             run_extra(name, lambda kind=kind: c3_wide_or(eng, kind, args.c3_n, rank, world, dist, ks, EXTRA_WARMUP, cdev,
                                                          slices=slices["c3_uniform_or"] if slices and kind == 1
                                                          else None))
+        if world == 1:  # the same op over bitmaps decoded from their serialized bytes (packed vs 16 B slots)
+            run_extra("c3_uniform_or_decoded", lambda: c3_uniform_decoded(eng, min(args.c3_n, 2000), ks,
+                                                                          EXTRA_WARMUP))
         # FastAggregation.and (N > 10: workShyAnd): per key the chain stops once the
         # intersection is empty, so it reads far less than the algorithmic input bytes
         for kind, name in ((1, "c3_uniform_and"), (2, "c3_clustered_and")):

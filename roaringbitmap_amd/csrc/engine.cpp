@@ -910,7 +910,8 @@ static int pairwise_pipelined(Ctx* c, int op, int K, PwDirect pd, Batch* A, Batc
   return RBG_OK;
 }
 
-// key ranges of a pipelined op + serialization (RBG_SER_PIPE, default 4; 1 = op, then serialization)
+// key ranges of a pipelined op + serialization (RBG_SER_PIPE; default 1 = the op, then the serialization: pipelining
+// off, measured slower at every split)
 static int pipe_ranges() {
   const char* e = getenv("RBG_SER_PIPE");  // read per call (tests vary it)
   return e ? std::max(1, atoi(e)) : 1;  // measured: 2-16 ranges are slower than the two calls
@@ -1031,10 +1032,10 @@ static int ctx_range_mut(Ctx* c, int op, int32_t ia, size_t ma, int64_t start, i
   int na;
   CHK(operand(A, ma, &ka, &da, &na));
   RmutArgs ra{op, 1, 0, 0, 0};  // end <= start: no key in the range, every container cloned
-  if (end > start) {
-    ra.hbs = (int)(start >> 16);
+  if (end > start) {  // (char) casts: Util.highbits / lowbits
+    ra.hbs = (int)((uint64_t)start >> 16 & 0xFFFF);
     ra.lbs = (int)(start & 0xFFFF);
-    ra.hbl = (int)((end - 1) >> 16);
+    ra.hbl = (int)((uint64_t)(end - 1) >> 16 & 0xFFFF);
     ra.lbl = (int)((end - 1) & 0xFFFF);
   }
   const size_t in_range = end > start ? (size_t)(ra.hbl - ra.hbs + 1) : 0;
@@ -1085,11 +1086,11 @@ static int ctx_remove_run_compression(Ctx* c, int32_t ia, size_t ma) {
   c->pending_src = {ia};
   c->mark(0);
   c->mark(1);
-  if (!c->big_ctl.p) CHK(c->big_ctl.ensure(16));
-  if (!c->big.p) CHK(c->big.ensure(16ull << 20));
+  // RunContainer.toBitmapOrArrayContainer never makes a run container: no big-run arena (RMUT_DERUN's kernel
+  // has no path to it)
   launch_rmut(s, A->key_off.as<uint32_t>(), da, A->payload.as<uint8_t>(), ra, false, c->wg_epoch.as<uint64_t>(),
               next_epoch(c), c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->zlb, c->ztile,
-              BigRuns{c->big.as<uint8_t>(), c->big_ctl.as<unsigned long long>(), c->big.cap}, grid_for(ub, 65536));
+              BigRuns{nullptr, nullptr, 0}, grid_for(ub, 65536));
   c->mark(2);
   defer_place(c);
   c->mark(3);
@@ -2570,6 +2571,7 @@ int rbg_range_op(int op, const uint8_t* const* bufs, const size_t* lens, size_t 
   Ctx* c;
   CHK(tl_ctx(&c));
   BatchGuard g{c, {}};
+  CHK(check_range(range_start, range_end));  // rangeSanityCheck before the selections (RB/RoaringBitmap.java:204-213)
   if (base == RBG_RANGE_ANDNOT) {  // andNot(x1, x2, start, end): both operands selected, then andNot
     int32_t ids[2], sel[2];
     CHK(ctx_load_separate(c, bufs, lens, 2, ids));
@@ -3676,8 +3678,21 @@ static int ctx_run_optimize(Ctx* c, int32_t id, int32_t* out_id, uint8_t* answer
 // selectRangeWithoutCopy (RB/RoaringBitmap.java:3160-3214) of every bitmap of a key-major batch into a
 // new batch, on the device (runopt.hip: k_rsel_plan, two scans, k_rsel_write, the key CSR); one host
 // read-back for the new batch's container counts.  rangeSanityCheck (:204-213) first.
+// x.selectRange(rangeStart, rangeEnd) (RB/RoaringBitmap.java:3095-3147; buffer RB/buffer/ImmutableRoaringBitmap.java
+// :701-757): no rangeSanityCheck (the range aggregations, which do check, call check_range first); the high and
+// low bits are the reference's char casts of rangeStart and rangeEnd - 1 (Util.highbits / lowbits, RB/Util.java
+// :436-438,481-483), so selectRange(x, Long.MAX_VALUE) keeps [start, 0xFFFFFFFF).  Divergences, raised as
+// IllegalArgumentException: a negative bound (the reference's assert) and casts that put the last key below the
+// first (the reference would append keys out of order).
 static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int32_t* out_id, bool buf) {
-  CHK(check_range(start, end));
+  if (start < 0 || end < 0) {
+    set_err("selectRange: rangeStart and rangeEnd must not be negative");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
+  if (end > start && ((uint64_t)start >> 16 & 0xFFFF) > ((uint64_t)(end - 1) >> 16 & 0xFFFF)) {
+    set_err("selectRange: the range's key casts are out of order (the reference would build an unsorted bitmap)");
+    return RBG_ERR_ILLEGAL_ARGUMENT;
+  }
   Batch* a;
   CHK(get_batch(c, id, &a));
   if (!a->key_major || a->packed) {
@@ -3687,10 +3702,10 @@ static int ctx_select_range(Ctx* c, int32_t id, int64_t start, int64_t end, int3
   hipStream_t s = c->stream;
   const size_t C = a->n_ctr, n = a->n_bm;
   RselArgs ra{1, 0, 0, 0, buf ? 1 : 0};  // end <= start: no key is kept
-  if (end > start) {
-    ra.hbs = (int)(start >> 16);
+  if (end > start) {  // (char) casts: Util.highbits / lowbits
+    ra.hbs = (int)((uint64_t)start >> 16 & 0xFFFF);
     ra.lbs = (int)(start & 0xFFFF);
-    ra.hbl = (int)((end - 1) >> 16);
+    ra.hbl = (int)((uint64_t)(end - 1) >> 16 & 0xFFFF);
     ra.lbl = (int)((end - 1) & 0xFFFF);
   }
   CHK(c->ro_info.ensure(4 * C + 16));

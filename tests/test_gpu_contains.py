@@ -109,6 +109,17 @@ def test_select_range(gpu):
     assert h == O.range_op("select", [x], 1 << 16, (1 << 16) + 12288)
     assert bb == O.range_op("select_buf", [x], 1 << 16, (1 << 16) + 12288)
     assert h != bb and len(h) == len(bb)  # 4,096 values: 8,192 payload bytes either way, different bytes
+    # no rangeSanityCheck: the bounds are cast like Util.highbits / lowbits (RB/Util.java:436-438,481-483)
+    full = encode([(k, R, np.arange(65536)) for k in (0, 1, 65535)])
+    for cls in (rb.RoaringBitmap, rb.ImmutableRoaringBitmap):
+        sel = "select" if cls is rb.RoaringBitmap else "select_buf"
+        # selectRange(x, Long.MAX_VALUE): the last key cut after lowbits(MAX - 1) = 0xFFFE
+        assert cls(full).selectRange(5, (1 << 63) - 1).serialize() == O.range_op(sel, [full], 5, (1 << 32) - 1)
+        # bounds past 2^32 wrap to their low 32 bits' keys
+        assert cls(full).selectRange((1 << 32) + 5, (1 << 32) + 70).serialize() == O.range_op(sel, [full], 5, 70)
+        for st, en in ((-1, 10), ((1 << 32) - 70000, (1 << 32) + 10)):  # negative; key casts out of order
+            with pytest.raises(ValueError):
+                cls(full).selectRange(st, en)
 
 
 def test_remove_run_compression(gpu):
