@@ -414,8 +414,8 @@ int rbg_ctx_bsi_sums_device(rbg_ctx* ctx, void* dst2);
 /* From now on every rbg_ctx_bsi with want_sum also writes its {sum, count} (two int64) to device
  * memory dst2, in the kernel that computes them (no copy launch); null stops it. */
 int rbg_ctx_bsi_sums_target(rbg_ctx* ctx, void* dst2);
-/* Diagnostics: 20 per-phase shader-clock totals of the pairwise kernel (all zero unless the
- * library was built with -DRBG_STAMPS=1); reset != 0 clears them. */
+/* Retired diagnostic (the per-phase clock builds of rounds 2-5 are gone; their results are in
+ * profiles/): writes 20 zeros.  Kept so bindings of earlier rounds still link. */
 int rbg_debug_stamps(uint64_t* out20, int reset);
 /* Containers per input bitmap of a batch (out has n == bitmaps entries). */
 int rbg_ctx_batch_counts(rbg_ctx* ctx, int32_t batch, uint32_t* out, size_t n);

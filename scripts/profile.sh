@@ -33,7 +33,7 @@ if [[ " $PASSES " == *" pmc "* ]]; then
   done
 fi
 if [[ " $PASSES " == *" sq "* ]]; then
-  for W in c2 c3u; do
+  for W in c2 c3u c5; do
     timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE --kernel-include-regex "$RX" --output-format csv -d $OUT/sq_$W -o run -- python3 bench.py --only $W --steps 5 --warmup 1 > /dev/null 2> $OUT/sq_$W.err || { echo "sq $W failed"; tail $OUT/sq_$W.err; exit 1; }
     echo "sq $W done"
   done
