@@ -114,7 +114,23 @@ struct OutCtx {
   // k_place also writes the result's (containers, payload bytes, has_run) here when set: the
   // device layout of a key shard (rbg_ctx_result_layout_device) without a launch of its own
   int64_t* layout_out;
+  // pairwise ops (round 6): per tile of kAggTile records, the kept results' (payload bytes, containers,
+  // run containers, cardinality) summed by the compute kernel as it writes them (agg_pack), so that the
+  // serialization places every tile without a look-back pass (k_serialize_agg); null: not accumulated
+  unsigned long long* tile_agg;
 };
+constexpr int kAggTile = 64;                     // records per aggregate tile
+constexpr int kMaxAggTiles = 65536 / kAggTile;  // a result has at most 65,536 records
+// a kept result as a tile-aggregate increment: payload bytes [0, 20), containers [20, 27), run
+// containers [27, 34), cardinality [34, 57) -- no field of a 64-record tile can overflow
+__host__ __device__ __forceinline__ unsigned long long agg_pack(uint32_t len, uint32_t card, uint32_t kind) {
+  return (unsigned long long)len | (1ull << 20) | ((unsigned long long)(kind == DK_R ? 1u : 0u) << 27) |
+         ((unsigned long long)card << 34);
+}
+__host__ __device__ __forceinline__ uint32_t agg_bytes(unsigned long long a) { return (uint32_t)(a & 0xFFFFF); }
+__host__ __device__ __forceinline__ uint32_t agg_count(unsigned long long a) { return (uint32_t)((a >> 20) & 0x7F); }
+__host__ __device__ __forceinline__ uint32_t agg_runs(unsigned long long a) { return (uint32_t)((a >> 27) & 0x7F); }
+__host__ __device__ __forceinline__ uint32_t agg_card(unsigned long long a) { return (uint32_t)(a >> 34); }
 
 // Run containers of more than 2047 runs (8 KiB of runs) do not fit a result slot.  Only the buffer
 // package's run AND / ANDNOT run make them (no toEfficientContainer); such a result is written to

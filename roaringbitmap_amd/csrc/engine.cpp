@@ -219,6 +219,9 @@ struct Ctx {
   size_t pending_ub = 0;
   bool serialized = false;  // pending result already in the portable layout
   bool place_pending = false;  // the op's k_place not launched yet (serialization then places too)
+  // the pending result's records were summed per tile by its compute kernel (OutCtx::tile_agg): its
+  // serialization places and copies in one launch (k_serialize_agg) instead of k_place + k_serialize
+  bool agg_ok = false;
   size_t n_cards = 0;
   int last = 0;  // 0 none, 1 serialized result, 2 cardinality, 3 batch cardinalities
   void* pinned = nullptr;
@@ -325,7 +328,7 @@ static int ctx_init(Ctx* c, int device) {
   CHK(c->wg_count.ensure(4 * 256));
   CHK(c->wg_epoch.ensure(8 * 256));
   HIPCHK(hipMemset(c->wg_epoch.p, 0, 8 * 256));
-  CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + 2 * kMaxTiles)));
+  CHK(c->lb.ensure(kLbHeader + 8 * (kMaxKeys + 2 * kMaxTiles + kMaxAggTiles)));  // + the pairwise tile aggregates
   CHK(c->recs.ensure(sizeof(ORec) * kMaxKeys));
   CHK(c->kind_by_out.ensure(kMaxKeys));
   CHK(c->scalar.ensure(64));
@@ -774,6 +777,7 @@ static int prepare_output(Ctx* c, size_t max_tasks, size_t max_payload, OutCtx* 
   oc->recs = c->recs.as<ORec>();
   c->serialized = false;
   c->place_pending = false;
+  c->agg_ok = false;
   c->ri_valid = false;
   c->pending_ub = 0;
   c->zlb = c->ztile = nullptr;
@@ -821,6 +825,14 @@ static int ctx_serialize(Ctx* c) {
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   if (c->serialized) return RBG_OK;
+  if (c->place_pending && c->agg_ok && !c->pending.spec) {
+    // placement from the compute kernel's tile sums and the serialization in one launch
+    launch_serialize_agg(c->stream, c->ntasks.as<uint32_t>(), c->pending, c->info.as<ResultInfo>(), c->pending_ub);
+    HIPCHK(hipGetLastError());
+    c->place_pending = false;
+    c->serialized = true;
+    return RBG_OK;
+  }
   CHK(ensure_placed(c));
   if (c->pending.spec) launch_spec_fix(c->stream, c->ntasks.as<uint32_t>(), c->pending);
   launch_serialize(c->stream, c->ntasks.as<uint32_t>(), c->pending);
@@ -1147,6 +1159,7 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
     launch_ior_fix(c->stream, c->ntasks.as<uint32_t>(), c->recs.as<ORec>(), A->key_off.as<uint32_t>(),
                    A->desc.as<CDesc>(), B->key_off.as<uint32_t>(), B->desc.as<CDesc>(), c->ones.as<uint8_t>());
     HIPCHK(hipGetLastError());
+    c->agg_ok = false;  // k_ior_fix changed records after the compute kernel summed them
     return RBG_OK;
   }
   if (op < 0 || op > 3) return RBG_ERR_ILLEGAL_ARGUMENT;
@@ -1200,6 +1213,14 @@ static int ctx_pairwise(Ctx* c, int op, int32_t ia, size_t ma, int32_t ib, size_
                          c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(), oc, c->task_card.as<uint32_t>(), c->zlb,
                          c->ztile);
   c->mark(1);
+  // the compute kernel sums its kept results per tile for the serialization (k_serialize_agg) when a
+  // plan kernel has zeroed the sums first: the balanced (dense) and planned (sparse) forms; the direct
+  // form zeroes inside the compute kernel itself
+  if (!card_only && (balanced || !direct)) {
+    oc.tile_agg = reinterpret_cast<unsigned long long*>(oc.tile_status + 2 * kMaxTiles);
+    c->pending.tile_agg = oc.tile_agg;
+    c->agg_ok = true;
+  }
   // 4 waves (tasks) per workgroup, clamped to the resident grid
   const int grid = grid_for(((direct ? nkeys : ub) + 3) / 4, 16384);
   launch_pairwise(s, op, card_only ? 1 : 0, grid, c->tasks.as<PTask>(), c->ntasks.as<uint32_t>(),

@@ -442,6 +442,175 @@ __global__ __launch_bounds__(256) void k_place(const uint32_t* __restrict__ n_ta
   }
 }
 
+// ===========================================================================
+// placement + serialization of a pairwise result in one launch (round 6).  The compute kernel
+// summed every tile of kAggTile records as it wrote them (OutCtx::tile_agg, agg_pack), so a
+// tile's place in the output is a prefix over <= 1024 tile sums that every workgroup reads at
+// once: no look-back chain between tiles and no k_place launch.  One workgroup per tile:
+//   all threads : exclusive prefix of the tile sums (containers, payload bytes) and the totals;
+//   every wave  : the tile's records -> output index and payload offset (wave scans), then the
+//                 payload copies of records w, w + 8, ... (w_copy);
+//   wave 0      : first the records' placement written back (like k_place), the descriptor and
+//                 offset-table entries, and the run-flag bytes whose first container is in the tile
+//                 (the last byte's tail from the next tiles' records);
+//   workgroup 0 : cookie, ResultInfo, totals word, result cardinality and device layout.
+// ===========================================================================
+constexpr int kAggThreads = 512;  // 8 waves: 8 payload copies each (4 waves of 16: 9 % slower serialization)
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, 64);
+  return v;
+}
+
+// 64 VGPRs (8 waves per SIMD): all 1024 workgroups of a 65,536-record result resident at once (at the
+// compiler's 77 VGPRs, 6 waves per SIMD, a quarter of them ran as a second round: +14 us)
+__global__ __launch_bounds__(kAggThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_serialize_agg(const uint32_t* __restrict__ n_tasks, OutCtx oc,
+                                                       ResultInfo* __restrict__ info) {
+  __shared__ uint8_t tcount[kMaxAggTiles];
+  constexpr int kW = kAggThreads / 64;
+  __shared__ uint32_t red[5][kW];
+  __shared__ unsigned long long red_card[kW];
+  __shared__ unsigned long long s_off[kW][kAggTile], s_src[kW][kAggTile];
+  __shared__ uint32_t s_len[kW][kAggTile];
+  const uint32_t nt = *n_tasks;
+  const uint32_t ntiles = (nt + kAggTile - 1) / kAggTile;
+  const uint32_t T = blockIdx.x;
+  if (T != 0 && T >= ntiles) return;
+  const int lane = threadIdx.x & 63, w = (int)uni(threadIdx.x >> 6);  // (w in an SGPR: scalar copy loop)
+  // prefix (tiles < T) and totals of the tile sums
+  // (payload bytes of a result fit 32 bits: <= 65,536 x 8 KiB; its cardinality does not)
+  uint32_t pc = 0, pb = 0, tc = 0, tb = 0, tr = 0;
+  unsigned long long tcard = 0;
+  for (uint32_t i = threadIdx.x; i < ntiles; i += blockDim.x) {
+    const unsigned long long a = oc.tile_agg[i];
+    const uint32_t c = agg_count(a), b = agg_bytes(a);
+    tcount[i] = (uint8_t)c;
+    if (i < T) {
+      pc += c;
+      pb += b;
+    }
+    tc += c;
+    tb += b;
+    tr += agg_runs(a);
+    tcard += agg_card(a);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    pc += __shfl_xor(pc, o, 64);
+    pb += __shfl_xor(pb, o, 64);
+    tc += __shfl_xor(tc, o, 64);
+    tb += __shfl_xor(tb, o, 64);
+    tr += __shfl_xor(tr, o, 64);
+    tcard += __shfl_xor(tcard, o, 64);
+  }
+  if (lane == 0) {
+    red[0][w] = pc;
+    red[1][w] = pb;
+    red[2][w] = tc;
+    red[3][w] = tb;
+    red[4][w] = tr;
+    red_card[w] = tcard;
+  }
+  __syncthreads();
+  uint32_t sum[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 5; j++)
+#pragma unroll
+    for (int i = 0; i < kW; i++) sum[j] += red[j][i];
+  pc = sum[0];
+  pb = sum[1];
+  const uint32_t size = (uint32_t)sum[2];
+  const uint64_t bytes = sum[3];
+  const uint32_t has_run = sum[4] != 0;
+  const uint64_t H = header_bytes(size, has_run);
+  uint8_t* base = oc.out + oc.payload_base - H;
+  if (T == 0 && threadIdx.x == 0) {
+    write_cookie(base, size, has_run);
+    write_info(info, oc, size, has_run, bytes);
+    if (nt > 0) {
+      // the result's long cardinality and the totals word, where k_place leaves them
+      unsigned long long card = 0;
+      for (int i = 0; i < kW; i++) card += red_card[i];
+      reinterpret_cast<unsigned long long*>(oc.err)[kCardWord] = card;
+      __hip_atomic_store(oc.status + nt - 1, lb_pack(2, has_run, size, bytes), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (oc.layout_out) {
+      oc.layout_out[0] = (int64_t)size;
+      oc.layout_out[1] = (int64_t)bytes;
+      oc.layout_out[2] = (int64_t)has_run;
+    }
+  }
+  if (T >= ntiles) return;
+  // every wave scans the tile's records itself (lane = record; 2 KiB from L2), so no wave waits for another
+  // before its copies
+  const uint32_t t = T * kAggTile + lane;
+  const bool in = t < nt;
+  ORec r{};
+  if (in) r = oc.recs[t];
+  const int keep = in && r.keep;
+  const uint32_t len = keep ? r.ser_len : 0u;
+  int tk, tb_;
+  const int ek = wave_excl(keep, &tk);
+  const int eb = wave_excl((int)len, &tb_);  // <= 64 x 8 KiB
+  const uint64_t off = (uint64_t)pb + (uint64_t)eb;
+  // the copy list through the wave's own LDS rows (held in registers across w_copy they spilled)
+  s_off[w][lane] = off;
+  s_src[w][lane] = r.src;
+  s_len[w][lane] = len;
+  if (w == 0) {
+    const uint32_t idx = pc + (uint32_t)ek;
+    if (in) {
+      oc.recs[t].idx = idx;
+      oc.recs[t].off = off;
+    }
+    if (keep) {
+      const uint64_t desc_base = has_run ? 4 + (size + 7) / 8 : 8;
+      *(g_u32*)(base + desc_base + 4ull * idx) = (uint32_t)r.key | ((r.card - 1) << 16);
+      if (!has_run || size >= 4) *(g_u32*)(base + desc_base + 4ull * size + 4ull * idx) = (uint32_t)(H + off);
+    }
+    if (has_run && tk > 0) {
+      // run flags of this tile's containers [first, e), in output order
+      const uint32_t first = pc, e = first + (uint32_t)tk;
+      const uint64_t runs = wave_or64(keep && r.kind == DK_R ? 1ull << ek : 0ull);
+      const uint32_t b0 = (first + 7) / 8, b1 = (e - 1) / 8;  // the bytes that start in this tile
+      uint64_t ahead = 0;  // run flags of the containers after e that share byte b1
+      if (b1 >= b0 && (e & 7) != 0 && e < size) {
+        const uint32_t need = min(8u - (e & 7), size - e);
+        uint32_t got = 0;
+        for (uint32_t u = T + 1; got < need && u < ntiles; u++) {
+          if (tcount[u] == 0) continue;
+          const uint32_t tu = u * kAggTile + lane;
+          const bool k2 = tu < nt && oc.recs[tu].keep;
+          const bool r2 = k2 && oc.recs[tu].kind == DK_R;
+          int t2;
+          const int e2 = wave_excl(k2 ? 1 : 0, &t2);
+          ahead |= wave_or64(r2 && got + e2 < 8 ? 1ull << (got + e2) : 0ull);
+          got += (uint32_t)t2;
+        }
+      }
+      if (b1 >= b0 && (uint32_t)lane <= b1 - b0) {
+        const uint32_t b = b0 + lane;
+        uint32_t v = 0;
+        for (uint32_t k = 0; k < 8; k++) {
+          const uint32_t o = 8 * b + k;
+          if (o >= size) break;
+          const uint32_t rank = o - first;
+          const uint32_t bit = rank < (uint32_t)tk ? (uint32_t)(runs >> rank) & 1u
+                                                   : (uint32_t)(ahead >> (rank - (uint32_t)tk)) & 1u;
+          v |= bit << k;
+        }
+        base[4 + b] = (uint8_t)v;
+      }
+    }
+  }
+  wsync();
+  uint8_t* pay = oc.out + oc.payload_base;
+  for (int i = w; i < kAggTile; i += kW) {
+    const uint32_t n = uni(s_len[w][i]);
+    if (n == 0) continue;
+    w_copy(pay + uni64(s_off[w][i]), reinterpret_cast<const uint8_t*>(uni64(s_src[w][i])), n);
+  }
+}
+
 // payload copies of the scan placement (key-shard fetch): one wave per task (grid-stride)
 // dst: the payload region (a key shard's place in a global bitmap)
 __global__ __launch_bounds__(256) void k_emit(const uint32_t* __restrict__ n_tasks, OutCtx oc, uint8_t* __restrict__ dst) {
@@ -617,6 +786,10 @@ void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info
 void launch_place_tiles(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info, uint32_t t_lo, uint32_t t_hi) {
   const uint32_t tl = t_lo / kTile, th = (t_hi + kTile - 1) / kTile;
   if (th > tl) hipLaunchKernelGGL(k_place, dim3(th - tl), dim3(256), 0, s, nt, oc, info, tl);
+}
+void launch_serialize_agg(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info, size_t max_tasks) {
+  const size_t tiles = std::min<size_t>((max_tasks + kAggTile - 1) / kAggTile, kMaxAggTiles);
+  hipLaunchKernelGGL(k_serialize_agg, dim3((unsigned)std::max<size_t>(1, tiles)), dim3(kAggThreads), 0, s, nt, oc, info);
 }
 void launch_spec_fix(hipStream_t s, const uint32_t* nt, OutCtx oc) {
   hipLaunchKernelGGL(k_spec_fix, dim3(std::max(1, resident_grid((const void*)&k_spec_fix))), dim3(256), 0, s, nt, oc);

@@ -281,6 +281,10 @@ void launch_wide(hipStream_t s, int mode, int grid, const Task* tasks, const uin
 // portable serialization (payload copies, descriptors, offsets, run flags,
 // cookie) runs only when the result is fetched
 void launch_place(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info);
+// placement + serialization in one launch from the compute kernel's per-tile sums (OutCtx::tile_agg):
+// one workgroup per kAggTile records, no look-back; also writes info, the totals word and the result's
+// cardinality like k_place.  max_tasks: an upper bound of *nt (the grid)
+void launch_serialize_agg(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info, size_t max_tasks);
 // the placement tiles covering tasks [t_lo, t_hi) (t_lo a multiple of the 1,024-record tile), for a
 // pipelined op whose key ranges are placed one launch each, in order
 void launch_place_tiles(hipStream_t s, const uint32_t* nt, OutCtx oc, ResultInfo* info, uint32_t t_lo, uint32_t t_hi);

@@ -453,11 +453,15 @@ __device__ __forceinline__ int lower_bound_u16(const uint16_t* keys, int n, uint
 
 // Zeroes the output look-back state of the op about to run (block 0 of a plan
 // kernel; saves two memset launches per op).  Either pointer may be null.
+// The tile aggregates of a pairwise op (OutCtx::tile_agg) follow the tile statuses and cardinalities in the
+// look-back buffer: tile_status + 2 kMaxTiles (engine.cpp: prepare_output), zeroed here too.
 __device__ __forceinline__ void plan_zero(uint64_t* lb_header, uint64_t* tile_status) {
   if (blockIdx.x != 0) return;
   if (lb_header && threadIdx.x < 32) lb_header[threadIdx.x] = 0;
-  if (tile_status)
+  if (tile_status) {
     for (uint32_t i = threadIdx.x; i < (uint32_t)kMaxTiles; i += blockDim.x) tile_status[i] = 0;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kMaxAggTiles; i += blockDim.x) tile_status[2 * kMaxTiles + i] = 0;
+  }
 }
 
 // Descriptor of key k in a single-bitmap batch through its key CSR (O(1), no search)
@@ -1184,6 +1188,9 @@ __device__ __forceinline__ void w_place(uint32_t t, bool keep, const uint8_t* sr
     r.kind = (uint8_t)kind;
     r.keep = keep ? 1 : 0;
     oc.recs[t] = r;
+    if (oc.tile_agg && keep)  // the tile's totals for k_serialize_agg (a non-returning atomic)
+      __hip_atomic_fetch_add(oc.tile_agg + t / kAggTile, agg_pack(len, card, (uint32_t)kind), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
