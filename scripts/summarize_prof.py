@@ -64,9 +64,9 @@ def counters(path):
 
 # workload (bench.py --only) -> (traffic key in pmc_traffic.json, dominant kernel)
 # (round 5: the dense pairwise ranges run the balanced list on one 16-wave workgroup per CU, k_pair_cu<OP, MODE>;
-# k_serialize<3> is the whole serialization)
+# round 6: k_serialize_agg is the whole placement + serialization of a pairwise result)
 WORKLOADS = {"c2": ("k_pair_wave", "k_pair_cu<0, 0>"), "c2card": ("k_pair_wave_card", "k_pair_cu<0, 1>"),
-             "c2ser": ("k_serialize_c2", "k_serialize<3>"), "c4": ("k_pair_items", "k_pair_items"),
+             "c2ser": ("k_serialize_c2", "k_serialize_agg"), "c4": ("k_pair_items", "k_pair_items"),
              "c3u": ("k_wide<OR>_uniform", "k_wide<0>"), "c3c": ("k_wide<OR>_clustered", "k_wide<0>"),
              "c5": ("k_bsi_reg", "k_bsi_reg")}
 
