@@ -54,6 +54,25 @@ __global__ __launch_bounds__(256) void k_rec(const v4u* __restrict__ a, v4u* __r
   }
 }
 
+// the fused serializer's shape: one workgroup of W waves per chunk of R consecutive 8 KiB records, every chunk's
+// workgroup resident at once (the whole range in flight), wave w copying records w, w + W, ... of its chunk
+template <int W, bool NTS>
+__global__ __launch_bounds__(64 * W) void k_chunk(const v4u* __restrict__ a, v4u* __restrict__ c, size_t nrec, int R) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  for (size_t r = (size_t)blockIdx.x * R + w; r < (size_t)(blockIdx.x + 1) * R && r < nrec; r += W) {
+    const v4u* s = a + r * 512 + l;
+    v4u* d = c + r * 512 + l;
+    v4u v[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) v[u] = __builtin_nontemporal_load(s + 64 * u);
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (NTS) __builtin_nontemporal_store(v[u], d + 64 * u);
+      else d[64 * u] = v[u];
+    }
+  }
+}
+
 template <class F>
 static float timeit(F f, int reps) {
   hipEvent_t e0, e1;
@@ -101,6 +120,17 @@ int main() {
     line(b, timeit([&] { hipLaunchKernelGGL(k_rec<false>, dim3(cus * wpc), dim3(256), 0, 0, a, c, nrec); }, 20));
     snprintf(b, sizeof b, "record per wave (8 KiB), nt store, %d WGs/CU", wpc);
     line(b, timeit([&] { hipLaunchKernelGGL(k_rec<true>, dim3(cus * wpc), dim3(256), 0, 0, a, c, nrec); }, 20));
+  }
+  {
+    // 32,768 records in 1,024 chunks of 32 (the fused serializer: 1,024 tiles of ~32 KiB... here 256 KiB each)
+    line("chunk per WG (8 waves, 1024 x 32 records), nt store",
+         timeit([&] { hipLaunchKernelGGL((k_chunk<8, true>), dim3(1024), dim3(512), 0, 0, a, c, nrec, 32); }, 20));
+    line("chunk per WG (8 waves, 1024 x 32 records), plain store",
+         timeit([&] { hipLaunchKernelGGL((k_chunk<8, false>), dim3(1024), dim3(512), 0, 0, a, c, nrec, 32); }, 20));
+    line("chunk per WG (8 waves, 4096 x 8 records), nt store",
+         timeit([&] { hipLaunchKernelGGL((k_chunk<8, true>), dim3(4096), dim3(512), 0, 0, a, c, nrec, 8); }, 20));
+    line("chunk per WG (4 waves, 2048 x 16 records), nt store",
+         timeit([&] { hipLaunchKernelGGL((k_chunk<4, true>), dim3(2048), dim3(256), 0, 0, a, c, nrec, 16); }, 20));
   }
   return 0;
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6: placement + serialization in one launch from the compute kernel's tile sums (k_serialize_agg) --
+# round 6: k_serialize_agg variants -- pairwise parity first, then the C2 step alternating against the previous library (lib/exp/head.so)
 # pairwise parity first, then the C2 step alternating against the previous library (lib/exp/head.so)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
