@@ -11,7 +11,7 @@
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
-template <int NT_LOAD, int NT_STORE, int WAVES_PER_WG>
+template <int NT_LOAD, int NT_STORE, int WAVES_PER_WG, int STRIDE = 520>
 __global__ __launch_bounds__(64 * WAVES_PER_WG) void k_bb(const v4u* __restrict__ a, const v4u* __restrict__ b,
                                                           v4u* __restrict__ c, uint32_t ntask, uint32_t* __restrict__ cards) {
   const uint32_t w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -32,7 +32,7 @@ __global__ __launch_bounds__(64 * WAVES_PER_WG) void k_bb(const v4u* __restrict_
       cnt += __popc(x[i].x) + __popc(x[i].y) + __popc(x[i].z) + __popc(x[i].w);
     }
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-    v4u* pc = c + (size_t)t * 520 + l;  // slot stride 8320 B, as the engine's scratch slots
+    v4u* pc = c + (size_t)t * STRIDE + l;  // slot stride 8320 B (520 vectors) as the engine's scratch slots, or 8192
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       if (NT_STORE) __builtin_nontemporal_store(x[i], pc + 64 * i);
@@ -77,7 +77,7 @@ int main() {
   uint32_t* cards;
   CK(hipMalloc(&a, bytes));
   CK(hipMalloc(&b, bytes));
-  CK(hipMalloc(&c, (size_t)nt * 8320));
+  CK(hipMalloc(&c, (size_t)nt * 16384));
   CK(hipMalloc(&cards, 4 * nt));
   CK(hipMemset(a, 0x5A, bytes));
   CK(hipMemset(b, 0x3C, bytes));
@@ -95,6 +95,10 @@ int main() {
   bb(k_bb<0, 0, 4>, 4, 4, "bb plain-load plain-store 4x4");
   bb(k_bb<1, 1, 4>, 4, 4, "bb nt-load nt-store 4x4");
   bb(k_bb<1, 1, 4>, 4, 8, "bb nt-load nt-store 8x4");
+  bb(k_bb<1, 0, 16, 512>, 16, 1, "bb nt-load plain-store 16x1, stride 8192");
+  bb(k_bb<1, 0, 4, 512>, 4, 4, "bb nt-load plain-store 4x4, stride 8192");
+  bb(k_bb<1, 1, 4, 512>, 4, 4, "bb nt-load nt-store 4x4, stride 8192");
+  bb(k_bb<1, 0, 4, 1024>, 4, 4, "bb nt-load plain-store 4x4, stride 16384");
   {
     const size_t n = 2 * bytes / 16 / 2;  // 1.07 GB copied: read + write = the bb bytes x 4/3
     const float ms = timeit([&] { hipLaunchKernelGGL(k_copy, dim3(cus * 8), dim3(256), 0, 0, a, c, n); }, 20);
