@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6: array AND / ANDNOT run as a walk over the run list (w_run_walk8) instead of an LDS membership map --
+# round 6: array AND / ANDNOT run variants -- pairwise parity first, then per-family and C2-mix compute time against the previous library (lib/exp/head.so)
 # pairwise parity first, then per-family and C2-mix compute time against the previous library (lib/exp/head.so)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
