@@ -73,6 +73,39 @@ def test_perturbed_pairs(gpu, seed):
     check_all(b, a, f"pert{seed}r")
 
 
+def _sparse_result_pair(keys):
+    """Operands whose AND is empty on most keys, a run container on every 211th and an array on every 97th:
+    the result's run-flag bytes span tiles of 64 records with empty tiles between them."""
+    ra = np.concatenate([np.arange(0, 100), np.arange(200, 300)]).astype(np.uint16)
+    rb = np.arange(50, 150, dtype=np.uint16)
+    a, b = [], []
+    for k in keys:
+        k = int(k)
+        if k % 211 == 0:
+            a.append((k, R, ra))
+            b.append((k, R, rb))
+        elif k % 97 == 0:
+            a.append((k, 0, np.array([1, 2, 3, 10 + k % 1000], dtype=np.uint16)))
+            b.append((k, 0, np.array([2, 3, 4], dtype=np.uint16)))
+        else:
+            a.append((k, 0, np.array([5, 6, 7], dtype=np.uint16)))
+            b.append((k, 0, np.array([8, 9], dtype=np.uint16)))
+    return encode(a), encode(b)
+
+
+@pytest.mark.parametrize("form", ["balanced", "planned"])
+def test_serialize_from_tile_sums_sparse_runs(gpu, form):
+    """k_serialize_agg (placement + serialization from the compute kernel's per-tile sums, round 6): a sparse
+    result with run containers, so a flag byte's tail is read from later tiles across empty ones; dense keys
+    take the balanced form (k_pair_cu), every third key the planned one (k_pair_wave)
+    (RB/RoaringArray.java:896-940)."""
+    keys = np.arange(40000) if form == "balanced" else np.arange(0, 65536, 3)
+    a, b = _sparse_result_pair(keys)
+    check_all(a, b, form)
+    got = decode(gpu_pair("and", a, b))
+    assert sum(1 for c in got if c[1] == R) > 50 and len(got) > 200
+
+
 def test_run_and_above_lds_limit(gpu):
     """R AND R whose run lists do not fit one wave's LDS together (na + nb + 2 > 2558: the bitmap path;
     RB/RunContainer.java:381-456), beside pairs that do: runs that straddle 32768 in one or both operands,
