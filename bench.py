@@ -848,14 +848,17 @@ def main():
             eng.pairwise("and", a, b)
             eng.serialize()
 
-    # Device settle before the warmups: ~0.25 s of the same op, so that the timed steps run at the clocks a
-    # sustained load holds.  With the driver's 5 warmups (1.6 ms) the first timed steps still ran the compute
-    # kernel ~4 % slower (0.2197 against 0.2102 ms, --steps 20 beside the default 200 on one box, round 6).
-    # Setup only: the W warmups and the K timed steps that follow are unchanged.
+    # Device settle before the warmups: ~0.25 s of the whole-pair op on this GPU, so that the timed steps run
+    # at the clocks a sustained load holds.  With the driver's 5 warmups (1.6 ms) the first timed steps still
+    # ran the compute kernel ~4 % slower (0.2205 against 0.2089 ms, --steps 20 on one box, round 6,
+    # profiles/r06/experiments/bench_settle.txt).  Setup only, and local: no collective (each rank's clock
+    # decides how many it runs), so at N > 1 the ranks cannot fall out of step; the W warmups and the K timed
+    # steps that follow are unchanged.
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < SETTLE_S:
         for _ in range(16):
-            c2_step()
+            eng.pairwise("and", a, b)
+            eng.serialize()
         eng.sync()
     for _ in range(args.warmup):
         c2_step()
