@@ -825,7 +825,7 @@ static int ctx_serialize(Ctx* c) {
     return RBG_ERR_ILLEGAL_ARGUMENT;
   }
   if (c->serialized) return RBG_OK;
-  if (c->place_pending && c->agg_ok && !c->pending.spec) {
+  if (c->place_pending && c->agg_ok && !c->pending.spec && c->pending_ub <= (size_t)kMaxAggTiles * kAggTile) {
     // placement from the compute kernel's tile sums and the serialization in one launch
     launch_serialize_agg(c->stream, c->ntasks.as<uint32_t>(), c->pending, c->info.as<ResultInfo>(), c->pending_ub);
     HIPCHK(hipGetLastError());
