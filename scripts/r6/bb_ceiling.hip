@@ -42,6 +42,30 @@ __global__ __launch_bounds__(64 * WAVES_PER_WG) void k_bb(const v4u* __restrict_
   }
 }
 
+// the same bytes as a flat stream: c[i] = a[i] & b[i], U float4 per thread in flight, grid-stride (no task structure)
+template <int U, int NTS>
+__global__ __launch_bounds__(256) void k_and_flat(const v4u* __restrict__ a, const v4u* __restrict__ b, v4u* __restrict__ c,
+                                                  size_t n) {
+  const size_t stride = (size_t)gridDim.x * 256 * U;
+  for (size_t i0 = (size_t)blockIdx.x * 256 * U + threadIdx.x; i0 < n; i0 += stride) {
+    v4u x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = i0 + (size_t)u * 256;
+      x[u] = i < n ? __builtin_nontemporal_load(a + i) : v4u{0, 0, 0, 0};
+      y[u] = i < n ? __builtin_nontemporal_load(b + i) : v4u{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = i0 + (size_t)u * 256;
+      if (i < n) {
+        if (NTS) __builtin_nontemporal_store(x[u] & y[u], c + i);
+        else c[i] = x[u] & y[u];
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_copy(const v4u* __restrict__ a, v4u* __restrict__ c, size_t n) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) c[i] = a[i];
 }
@@ -99,6 +123,16 @@ int main() {
   bb(k_bb<1, 0, 4, 512>, 4, 4, "bb nt-load plain-store 4x4, stride 8192");
   bb(k_bb<1, 1, 4, 512>, 4, 4, "bb nt-load nt-store 4x4, stride 8192");
   bb(k_bb<1, 0, 4, 1024>, 4, 4, "bb nt-load plain-store 4x4, stride 16384");
+  for (int wpc : {8, 16}) {
+    const size_t n = bytes / 16;
+    char nm[64];
+    snprintf(nm, sizeof nm, "flat a&b, unroll 4, plain store, %d WG/CU", wpc);
+    float ms = timeit([&] { hipLaunchKernelGGL((k_and_flat<4, 0>), dim3(cus * wpc), dim3(256), 0, 0, a, b, c, n); }, 20);
+    printf("%-44s %8.4f ms  %6.3f TB/s\n", nm, ms, rw / (ms * 1e-3) / 1e12);
+    snprintf(nm, sizeof nm, "flat a&b, unroll 4, nt store, %d WG/CU", wpc);
+    ms = timeit([&] { hipLaunchKernelGGL((k_and_flat<4, 1>), dim3(cus * wpc), dim3(256), 0, 0, a, b, c, n); }, 20);
+    printf("%-44s %8.4f ms  %6.3f TB/s\n", nm, ms, rw / (ms * 1e-3) / 1e12);
+  }
   {
     const size_t n = 2 * bytes / 16 / 2;  // 1.07 GB copied: read + write = the bb bytes x 4/3
     const float ms = timeit([&] { hipLaunchKernelGGL(k_copy, dim3(cus * 8), dim3(256), 0, 0, a, c, n); }, 20);
