@@ -106,6 +106,41 @@ def test_serialize_from_tile_sums_sparse_runs(gpu, form):
     assert sum(1 for c in got if c[1] == R) > 50 and len(got) > 200
 
 
+def test_fused_serialization_and_placement_users(gpu):
+    """k_serialize_agg places the records as k_place does: after it, the result statistics, the key-shard fetch
+    (which reads the records' placement) and the fetch agree with the oracle; and the same op with the
+    statistics first (k_place, then k_serialize) gives the same bytes (RB/RoaringArray.java:896-940)."""
+    import struct
+    from roaringbitmap_amd import Engine
+    a, b = _sparse_result_pair(np.arange(40000))
+    exp = O.pairwise("and", a, b)
+    n = len(decode(exp))
+    has_run = int((struct.unpack("<I", exp[:4])[0] & 0xFFFF) == 12347)
+    desc_base = 4 + (n + 7) // 8 if has_run else 8
+    offsets = not has_run or n >= 4
+    head = desc_base + 4 * n + (4 * n if offsets else 0)
+    e = Engine(0)
+    try:
+        x, y = e.load_pair(a, b)
+        e.pairwise("and", x, y)
+        e.serialize()
+        st = e.result_stats()
+        assert (st["containers"], st["has_run"]) == (n, has_run)
+        assert st["cardinality"] == O.pairwise_card("and", a, b)
+        assert e.fetch().serialize() == exp
+        d, o, p = e.fetch_shard(n, has_run, 0, 0)
+        assert d == exp[desc_base:desc_base + 4 * n]
+        if offsets:
+            assert o == exp[desc_base + 4 * n:head]
+        assert p == exp[head:]
+        e.pairwise("and", x, y)
+        assert e.result_stats() == st
+        e.serialize()
+        assert e.fetch().serialize() == exp
+    finally:
+        e.close()
+
+
 def test_run_and_above_lds_limit(gpu):
     """R AND R whose run lists do not fit one wave's LDS together (na + nb + 2 > 2558: the bitmap path;
     RB/RunContainer.java:381-456), beside pairs that do: runs that straddle 32768 in one or both operands,
