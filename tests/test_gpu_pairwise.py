@@ -64,6 +64,22 @@ def test_random_bitmaps(gpu, seed):
     check_all(_gen.bitmap(rng, keys), _gen.bitmap(rng, keys), f"seed{seed}")
 
 
+@pytest.mark.parametrize("form", ["planned", "balanced"])
+def test_random_bitmaps_many_tiles(gpu, form):
+    """Random container modes over thousands of keys, so results span many tiles of 64 records (the fused
+    placement + serialization's tile sums, round 6): 2,500 random keys of every mode (planned list), or
+    34,000 dense keys present in both operands (balanced list) of the lighter modes."""
+    rng = np.random.default_rng(31 if form == "planned" else 32)
+    if form == "planned":
+        keys = np.sort(rng.choice(65536, size=2500, replace=False))
+        a, b = _gen.bitmap(rng, keys), _gen.bitmap(rng, keys)
+    else:
+        modes = ["a_tiny", "a_small", "r_tiny", "r_single", "r_tie", "r_few"]
+        keys = np.arange(34000)
+        a, b = _gen.bitmap(rng, keys, modes, p_present=1.0), _gen.bitmap(rng, keys, modes, p_present=1.0)
+    check_all(a, b, form)
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_perturbed_pairs(gpu, seed):
     rng = np.random.default_rng(100 + seed)
